@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: http_events Filter(resp_status>=400) -> Map(latency_ms) -> BlockingAgg by
+(service, req_path) with count / mean / quantiles (BASELINE.json configs[1], "C2"), on HBM-
+resident synthetic data, one process per GPU.
+
+One step = one full pass of the fused hot path over the rank's table: pxg_agg_reset ->
+pxg_agg_consume (filter + map + group-key hash + staging) -> [N>1: export partial states,
+RCCL all-to-all by key hash, import] -> pxg_agg_finalize (group sort, count/mean reductions,
+t-digest quantiles, key extraction) — finalized result columns on device.
+
+Prints ONE JSON line on rank 0 (the driver's contract).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 20250117
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--gen-slice", type=int, default=16_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=3_000_000)
+    ap.add_argument("--cpu-batch-rows", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"))
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+
+    from pixie_amd import plans as P
+    from pixie_amd.device import Ctx, Table, datagen_http_events
+    from pixie_amd.pipeline import LinearQuery
+    from pixie_amd.dist import exchange_partials
+
+    n = args.rows_per_gpu
+    row0 = rank * n
+    ctx = Ctx(local_rank)
+    table = Table(ctx, P.HTTP_TYPES)
+    t0 = time.time()
+    svc_bytes = path_bytes = 0
+    for a in range(0, n, args.gen_slice):
+        m = min(args.gen_slice, n - a)
+        cols = datagen_http_events(SEED, row0 + a, m, n_pair_keys=10_000_000, threads=16)
+        svc_bytes += int(cols[2].offsets[-1])
+        path_bytes += int(cols[3].offsets[-1])
+        table.append(cols)
+        del cols
+    table.flush()
+    log(rank, f"[bench] generated + uploaded {n} rows/rank in {time.time() - t0:.1f}s "
+              f"({table.num_chunks} chunks)")
+    # Algorithmic bytes: every referenced column once in Arrow layout.
+    alg_bytes = 8 * n + 8 * n + (4 * n + svc_bytes) + (4 * n + path_bytes)
+
+    q = LinearQuery(P.c2_plan(with_pluck=True), P.HTTP_TYPES, expected_groups=65536)
+    agg = q.make_agg(ctx)
+
+    def step():
+        agg.reset()
+        agg.consume(table)
+        if world > 1:
+            exchange_partials(agg, world, rank, ctx)
+        return agg.finalize()
+
+    for _ in range(args.warmup):
+        ngroups = step()
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        ngroups = step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    ctx.set_profiling(False)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    launches, cons_ms = ctx.kernel_stats("agg_consume")
+    kernel_ms = {}
+    for name in ["agg_consume", "agg_publish_sizes", "agg_publish_write", "radix_hist", "radix_scatter", "run_heads",
+                 "group_starts", "uda_reduce", "classify_groups", "quant_tiny", "quant_mid", "quant_big_chunk_sort",
+                 "quant_big_merge", "quant_big_digest", "key_extract", "key_string_copy", "scan_reduce", "scan_downsweep"]:
+        l, ms = ctx.kernel_stats(name)
+        if l:
+            kernel_ms[name] = round(ms / args.steps, 4)
+    ms_per_step = elapsed * 1000.0 / args.steps
+    selected = agg.rows_selected()
+    total_rows = n * world
+    value = total_rows * args.steps / elapsed
+    avg_launch_ms = cons_ms / max(launches, 1)
+    achieved = alg_bytes / (avg_launch_ms / 1000.0) / 1e9 if launches else None
+
+    traffic = None
+    if os.path.exists(args.pmc_file):
+        try:
+            pm = json.load(open(args.pmc_file))
+            if pm.get("rows_per_gpu") == n and pm.get("kernel") == "agg_consume":
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": "rows/sec + achieved HBM GB/s, http_events filter+group-by agg, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic http_events (counter-based splitmix64, seed 20250117; SURVEY.md §8d spec), HBM-resident",
+            "config": {
+                "workload": "C2: Filter(resp_status>=400) -> Map(latency_ms=latency/1e6) -> BlockingAgg by (service, req_path): "
+                            "count, mean, quantiles -> pluck p50/p99",
+                "rows_per_gpu": n, "total_rows": total_rows, "groups": ngroups, "selected_rows_per_gpu": selected,
+                "parallelism": f"dp{world} (row shards, partial UDA states exchanged by key hash)" if world > 1 else "single GPU",
+                "algorithmic_bytes_per_row": alg_bytes / n,
+                "kernel_ms_per_step": kernel_ms,
+                "step_rate_gbs_algorithmic": alg_bytes * world / (ms_per_step / 1000.0) / 1e9,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "agg_consume",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "avg_launch_ms": avg_launch_ms,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    agg.close()
+    table.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """The CPU Carnot restatement (oracle/, single thread) on a bounded sample of the same
+    workload: the first cpu_sample_rows rows as RowBatches of cpu_batch_rows rows."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        import oracle_client as oc
+        from pixie_amd import plans as P
+        from pixie_amd.device import datagen_http_events
+        m = args.cpu_sample_rows
+        cols = datagen_http_events(SEED, 0, m, n_pair_keys=10_000_000, threads=16)
+        br = args.cpu_batch_rows
+        batches = [[c.slice(a, min(a + br, m)) for c in cols] for a in range(0, m, br)]
+        tables = {"http_events": {"types": P.HTTP_TYPES, "batches": batches, "names": P.HTTP_NAMES}}
+        secs, _ = oc.time_plan(P.c2_plan(with_pluck=True), tables)
+        return {"value": m / secs, "unit": "rows/s", "cores": 1, "kind": "port",
+                "sample": f"first {m} rows of the same synthetic table as {br}-row RowBatches, C2 plan, "
+                          f"1 thread; {secs:.2f} s (execution window only, as in BASELINE.md)"}
+    except Exception as e:  # the baseline must never break the bench line
+        return {"value": None, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
+
+
+if __name__ == "__main__":
+    main()

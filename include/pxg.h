@@ -1,0 +1,291 @@
+/*
+ * pxg.h — C ABI of the MI355X-native Carnot columnar hot path (libpxg.so).
+ *
+ * This is the drop-in boundary.  The reference has no FFI for this path: its
+ * Filter/Map/Agg nodes call the UDF registry in-process.  These entry points are what the
+ * reference-side GPU exec nodes (GpuFilterNode / GpuMapNode / GpuAggNode, added at the
+ * operator switch in src/carnot/exec/exec_graph.cc:66-80) would bind; INTEGRATION.md shows
+ * that binding.  Plain pointers and sizes only; no torch / C++ types cross the ABI.
+ *
+ * Reference interfaces replaced (file:line under /root/reference):
+ *   pxg_table_*            table_store::Table + RowBatch column buffers
+ *                          (src/table_store/table/table.h:71-199,
+ *                           src/table_store/schema/row_batch.h:40-129) — HBM-resident copy.
+ *   pxg_filter             FilterNode::ConsumeNextImpl (src/carnot/exec/filter_node.cc:132-171)
+ *                          + VectorNativeScalarExpressionEvaluator
+ *                          (src/carnot/exec/expression_evaluator.cc:191-275).
+ *   pxg_map                MapNode::ConsumeNextImpl (src/carnot/exec/map_node.cc:64-71)
+ *                          + ArrowNativeScalarExpressionEvaluator (expression_evaluator.cc:277-342).
+ *   pxg_agg_*              AggNode (src/carnot/exec/agg_node.cc:88-542) with the builtin UDAs
+ *                          count/sum/mean/min/max (src/carnot/funcs/builtins/math_ops.h:583-772)
+ *                          and quantiles (src/carnot/funcs/builtins/math_sketches.h:33-82);
+ *                          pxg_agg_consume with a filter program = the fused
+ *                          MemorySource -> Filter -> Map -> BlockingAgg chain.
+ *   pxg_agg_export_partial /
+ *   pxg_agg_import_partial partial_agg / finalize_results split
+ *                          (src/carnot/planpb/plan.proto:250-257), exchanged between GPUs.
+ *
+ * Error convention: every call returns a px.statuspb.Code value
+ * (src/common/base/statuspb/status.proto:27-52); pxg_last_error() gives the message of the
+ * last failing call on the calling thread.  No C++ exception crosses the ABI.
+ *
+ * Threading: a pxg_ctx owns one HIP stream; all work issued through a ctx is stream-ordered
+ * and asynchronous unless the call says it synchronises.  Handles are not thread-safe; use one
+ * ctx per query thread (exec_graph.cc:177-289 drives one query on one thread).
+ */
+#ifndef PXG_H_
+#define PXG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PXG_ABI_VERSION 1
+
+/* px.types.DataType (src/shared/types/typespb/types.proto:26-34). */
+enum pxg_data_type {
+  PXG_DATA_TYPE_UNKNOWN = 0,
+  PXG_BOOLEAN = 1,
+  PXG_INT64 = 2,
+  PXG_UINT128 = 3,
+  PXG_FLOAT64 = 4,
+  PXG_STRING = 5,
+  PXG_TIME64NS = 6
+};
+
+/* px.statuspb.Code (src/common/base/statuspb/status.proto:27-52). */
+enum pxg_code {
+  PXG_OK = 0,
+  PXG_CANCELLED = 1,
+  PXG_UNKNOWN = 2,
+  PXG_INVALID_ARGUMENT = 3,
+  PXG_DEADLINE_EXCEEDED = 4,
+  PXG_NOT_FOUND = 5,
+  PXG_ALREADY_EXISTS = 6,
+  PXG_PERMISSION_DENIED = 7,
+  PXG_UNAUTHENTICATED = 8,
+  PXG_INTERNAL = 9,
+  PXG_UNIMPLEMENTED = 10,
+  PXG_RESOURCE_UNAVAILABLE = 11,
+  PXG_SYSTEM = 12,
+  PXG_FAILED_PRECONDITION = 13
+};
+
+/* ---------------------------------------------------------------------------------------
+ * Columns.  Arrow layout per column (Pixie never sets validity bitmaps):
+ *   INT64 / TIME64NS / FLOAT64 : 8-byte values
+ *   UINT128                    : 16-byte values {low u64, high u64}
+ *   BOOLEAN                    : one byte per value (0/1); the host node unpacks Arrow bits
+ *   STRING                     : int32 offsets[length+1] + UTF-8 bytes
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t type;           /* pxg_data_type */
+  int32_t reserved;
+  int64_t length;         /* rows */
+  const void* values;     /* fixed-width types */
+  const int32_t* offsets; /* STRING */
+  const uint8_t* data;    /* STRING payload */
+} pxg_column_view;
+
+/* Host-visible output column.  Buffers are allocated by the library; release with
+ * pxg_result_free (which frees every column of one result). */
+typedef struct {
+  int32_t type;
+  int32_t reserved;
+  int64_t length;
+  void* values;
+  int32_t* offsets;
+  uint8_t* data;
+  int64_t data_len;
+} pxg_column_out;
+
+/* ---------------------------------------------------------------------------------------
+ * Expression programs: a typed postfix program compiled by the host node from a
+ * plan::ScalarExpression after resolving each ScalarFunc against the device UDF registry
+ * (udf::Registry::GetScalarUDFDefinition(name, arg types), src/carnot/udf/registry.cc:172-198).
+ * Every stack slot carries a statically known type; mixed-type UDF signatures are compiled
+ * with explicit conversions (the same C++ usual arithmetic conversions the reference's
+ * FixedSizedValueType operators perform, src/shared/types/types.h:72-104).
+ * ------------------------------------------------------------------------------------- */
+enum pxg_opcode {
+  PXG_OP_NOP = 0,
+  PXG_OP_COL = 1,      /* push column[arg] (type = column type)                          */
+  PXG_OP_CONST = 2,    /* push imm (BOOLEAN/INT64/TIME64NS: integer, FLOAT64: bits);
+                          STRING: arg = pool offset, imm = length; UINT128: arg=pool off  */
+  PXG_OP_I2F = 3,      /* int64 -> double                                                */
+  PXG_OP_B2I = 4,      /* bool -> int64                                                  */
+  PXG_OP_I2B = 5,      /* int64 -> bool (x != 0)                                         */
+  PXG_OP_F2I = 6,      /* double -> int64, truncating (static_cast<int64_t>)             */
+  PXG_OP_ADD_I = 10, PXG_OP_SUB_I = 11, PXG_OP_MUL_I = 12, PXG_OP_MOD_I = 13,
+  PXG_OP_BIN_I = 14,   /* a - a % b (BinUDF, math_ops.h:512-527)                         */
+  PXG_OP_NEG_I = 15, PXG_OP_INV_I = 16,
+  PXG_OP_ADD_F = 20, PXG_OP_SUB_F = 21, PXG_OP_MUL_F = 22, PXG_OP_DIV_F = 23,
+  PXG_OP_NEG_F = 24,
+  PXG_OP_EQ_I = 30, PXG_OP_NE_I = 31, PXG_OP_LT_I = 32, PXG_OP_LE_I = 33,
+  PXG_OP_GT_I = 34, PXG_OP_GE_I = 35,
+  PXG_OP_EQ_F = 40, PXG_OP_NE_F = 41, PXG_OP_LT_F = 42, PXG_OP_LE_F = 43,
+  PXG_OP_GT_F = 44, PXG_OP_GE_F = 45,
+  PXG_OP_APPROX_EQ_F = 46, /* |a-b| <  DBL_EPSILON (ApproxEqualUDF)                      */
+  PXG_OP_APPROX_NE_F = 47, /* |a-b| >  DBL_EPSILON (ApproxNotEqualUDF)                   */
+  PXG_OP_EQ_S = 50, PXG_OP_NE_S = 51, PXG_OP_LT_S = 52, PXG_OP_LE_S = 53,
+  PXG_OP_GT_S = 54, PXG_OP_GE_S = 55,
+  PXG_OP_EQ_U = 60, PXG_OP_NE_U = 61,
+  PXG_OP_AND = 70, PXG_OP_OR = 71, PXG_OP_NOT = 72
+};
+
+typedef struct {
+  uint16_t op;   /* pxg_opcode */
+  uint16_t type; /* result type of the instruction */
+  int32_t arg;
+  int64_t imm;
+} pxg_insn;
+
+#define PXG_MAX_PROGRAM 48
+#define PXG_MAX_STACK 8
+
+typedef struct {
+  int32_t n_insns;
+  int32_t result_type;
+  const pxg_insn* insns;
+  int32_t pool_len;     /* constant pool (string / uint128 constants) */
+  int32_t reserved;
+  const uint8_t* pool;
+} pxg_program;
+
+/* ---------------------------------------------------------------------------------------
+ * Contexts and HBM-resident tables.
+ * ------------------------------------------------------------------------------------- */
+typedef struct pxg_ctx pxg_ctx;
+typedef struct pxg_table pxg_table;
+typedef struct pxg_agg pxg_agg;
+
+int32_t pxg_abi_version(void);
+const char* pxg_last_error(void);
+int32_t pxg_device_count(int32_t* count);
+
+/* One context per device per query thread; owns a HIP stream. */
+int32_t pxg_ctx_create(int32_t device, pxg_ctx** out);
+int32_t pxg_ctx_destroy(pxg_ctx* ctx);
+/* Blocks until all work issued through ctx is complete.  Device faults surface here. */
+int32_t pxg_ctx_sync(pxg_ctx* ctx);
+/* The hipStream_t the ctx issues on (for callers that record their own events). */
+void* pxg_ctx_stream(pxg_ctx* ctx);
+/* Kernel timing: when enabled every library kernel launch is bracketed by HIP events on the
+ * ctx stream; pxg_ctx_kernel_stats returns launches and summed device milliseconds of the
+ * named kernel since the last reset. */
+int32_t pxg_ctx_set_profiling(pxg_ctx* ctx, int32_t enabled);
+int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* kernel_name, int64_t* launches,
+                             double* total_ms);
+int32_t pxg_ctx_reset_stats(pxg_ctx* ctx);
+
+/* A table: ncols typed columns, stored as device chunks of <= 2^24 rows (STRING payload
+ * < 2^31 bytes per chunk).  Appends coalesce small RowBatches through a pinned staging buffer
+ * (tiny batches are the norm: src/vizier/services/agent/pem/pem_manager.cc:85-99). */
+int32_t pxg_table_create(pxg_ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out);
+int32_t pxg_table_destroy(pxg_table* t);
+/* Append one RowBatch given as host columns (copied; the caller may free on return). */
+int32_t pxg_table_append(pxg_table* t, const pxg_column_view* cols, int64_t nrows);
+/* Append columns that already live in device memory (copied device-to-device). */
+int32_t pxg_table_append_device(pxg_table* t, const pxg_column_view* cols, int64_t nrows);
+/* Flush staging so every appended row is resident in HBM. */
+int32_t pxg_table_flush(pxg_table* t);
+int64_t pxg_table_num_rows(const pxg_table* t);
+int32_t pxg_table_num_chunks(const pxg_table* t);
+/* Device bytes of the table's column data in Arrow layout (values, offsets, payload). */
+int64_t pxg_table_device_bytes(const pxg_table* t, int32_t col);
+/* Copy rows [begin, end) of column col back to host (test / sink path). */
+int32_t pxg_table_fetch(pxg_table* t, int32_t col, int64_t begin, int64_t end,
+                        pxg_column_out* out);
+
+/* ---------------------------------------------------------------------------------------
+ * Filter and Map over a device table (non-fused operator shapes).
+ * ------------------------------------------------------------------------------------- */
+/* FilterNode: evaluates pred over rows [begin,end) and writes the selected columns (in
+ * `select` order) of the passing rows, order preserved, into a new device table. */
+int32_t pxg_filter(pxg_table* in, const pxg_program* pred, int32_t n_select,
+                   const int32_t* select, int64_t begin, int64_t end, pxg_table** out);
+/* MapNode: one output column per program (fixed-width results; a program that is a single
+ * column reference of any type is passed through). */
+int32_t pxg_map(pxg_table* in, int32_t n_exprs, const pxg_program* exprs, int64_t begin,
+                int64_t end, pxg_table** out);
+
+/* ---------------------------------------------------------------------------------------
+ * Hash group-by aggregation with device UDAs.
+ * ------------------------------------------------------------------------------------- */
+enum pxg_uda_kind {
+  PXG_UDA_COUNT = 1,     /* CountUDA      -> INT64                                         */
+  PXG_UDA_SUM = 2,       /* SumUDA        -> INT64 (INT64/BOOLEAN args) or FLOAT64          */
+  PXG_UDA_MEAN = 3,      /* MeanUDA       -> FLOAT64                                        */
+  PXG_UDA_MIN = 4,       /* MinUDA        -> arg type                                       */
+  PXG_UDA_MAX = 5,       /* MaxUDA        -> arg type (init numeric_limits<T>::min())       */
+  PXG_UDA_QUANTILES = 6, /* QuantilesUDA  -> STRING JSON {p01..p99}; 7 FLOAT64 on device    */
+  PXG_UDA_MINSUM = 100   /* test UDA of agg_node_test.cc:44-72 (sum of min(a,b), init arg)  */
+};
+
+typedef struct {
+  int32_t kind;        /* pxg_uda_kind */
+  int32_t arg_type;    /* type of the update argument */
+  pxg_program arg;     /* value expression over the input columns */
+  pxg_program arg2;    /* second argument (MINSUM) */
+  int32_t has_init;
+  int32_t reserved;
+  int64_t init_i64;    /* init argument (MINSUM: initial sum) */
+} pxg_uda_spec;
+
+typedef struct {
+  int32_t n_keys;
+  int32_t n_udas;
+  const pxg_program* keys;  /* group key expressions: a bare column reference, or a
+                               fixed-width program (e.g. bin(time_, 10s))              */
+  const pxg_uda_spec* udas;
+  const pxg_program* filter; /* optional predicate fused in front of the agg (NULL: none) */
+  int64_t expected_groups;   /* sizing hint; the table grows on demand */
+  int32_t windowed;          /* AggregateOperator.windowed */
+  int32_t reserved;
+} pxg_agg_spec;
+
+int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_agg** out);
+int32_t pxg_agg_destroy(pxg_agg* agg);
+/* Update with rows [begin, end) of table (filter applied first when the spec has one). */
+int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin, int64_t end);
+/* Finalize: resolves deferred inserts, computes quantiles, compacts groups.  Synchronises. */
+int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups);
+/* Result columns (groups then values, AggNode output order, agg_node.cc:336-346).  For
+ * QUANTILES the column is FLOAT64 with 7 values per group (p01,p10,p25,p50,p75,p90,p99,
+ * group-major); the host node renders the JSON string (math_sketches.h:40-54). */
+int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
+void pxg_result_free(pxg_column_out* cols, int32_t n_cols);
+/* ClearAggState (agg_node.cc:173-180): drop all groups (windowed emit). */
+int32_t pxg_agg_reset(pxg_agg* agg);
+/* Number of selected (post-filter) rows consumed since the last reset. */
+int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows);
+
+/* Partial aggregation (plan.proto:250-257).  Export serialises every group's key and UDA
+ * state (quantile inputs as raw values) into n_parts device buffers partitioned by
+ * hash(key) % n_parts; part_bytes[i] receives the size of part i.  Buffers are written into
+ * dst (device memory, capacity dst_capacity bytes, parts laid out back to back; part i
+ * starts at part_offsets[i]).  Call with dst == NULL to size.  Import merges a buffer
+ * produced by export (on any device) into this agg (UDA Merge semantics). */
+int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* dst, int64_t dst_capacity,
+                               int64_t* part_offsets, int64_t* part_bytes);
+int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes);
+
+/* ---------------------------------------------------------------------------------------
+ * Synthetic http_events generator (bench/test data; SURVEY.md §8d spec, counter-based
+ * splitmix64 so every row is a pure function of (seed, row) and shards are independent).
+ * Host-side; writes Arrow-layout host buffers allocated by the library.
+ * Columns: 0 time_ TIME64NS, 1 upid UINT128, 2 service STRING, 3 req_path STRING,
+ *          4 remote_addr STRING, 5 resp_status INT64, 6 latency INT64,
+ *          7 req_body_size INT64, 8 resp_body_size INT64, 9 pod STRING
+ * ------------------------------------------------------------------------------------- */
+#define PXG_HTTP_EVENTS_NCOLS 10
+int32_t pxg_datagen_http_events(uint64_t seed, int64_t row_begin, int64_t nrows,
+                                int64_t n_addr_keys, int32_t n_threads, pxg_column_out* cols);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PXG_H_ */

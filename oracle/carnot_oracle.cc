@@ -1,0 +1,1262 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — CPU restatement of Pixie Carnot's hot path.
+// Never linked into the product.  See carnot_oracle.h for the list of restated files.
+//
+// This is deliberately the reference's *algorithm and cost structure* (batch-at-a-time, one
+// thread, per-row std::function UDF calls, per-row RowTuple with std::string copies, hash map
+// of group -> buffered value columns flushed at 512 rows, per-row UDA Update), so it doubles as
+// the "CPU Carnot (restated)" baseline that bench.py times.
+
+#include "carnot_oracle.h"
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "json.h"
+#include "tdigest.h"
+
+namespace oracle {
+
+// px.types.DataType (src/shared/types/typespb/types.proto:26-34).
+enum DT : int32_t { UNKNOWN = 0, BOOLEAN = 1, INT64 = 2, UINT128 = 3, FLOAT64 = 4, STRING = 5, TIME64NS = 6 };
+
+// px.statuspb.Code (src/common/base/statuspb/status.proto:27-52).
+enum Code : int32_t { OK = 0, INVALID_ARGUMENT = 3, NOT_FOUND = 5, INTERNAL = 9, UNIMPLEMENTED = 10 };
+
+struct Error : std::runtime_error {
+  int32_t code;
+  Error(int32_t c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+static DT ParseDT(const Json& j) {
+  if (j.kind == Json::kString) {
+    static const std::map<std::string, DT> m = {{"BOOLEAN", BOOLEAN}, {"INT64", INT64},     {"UINT128", UINT128},
+                                                {"FLOAT64", FLOAT64}, {"STRING", STRING},   {"TIME64NS", TIME64NS},
+                                                {"DATA_TYPE_UNKNOWN", UNKNOWN}};
+    auto it = m.find(j.str);
+    if (it == m.end()) throw Error(INVALID_ARGUMENT, "unknown data type " + j.str);
+    return it->second;
+  }
+  return static_cast<DT>(j.as_i64());
+}
+
+struct U128 {
+  uint64_t lo = 0, hi = 0;
+  bool operator==(const U128& o) const { return lo == o.lo && hi == o.hi; }
+  bool operator!=(const U128& o) const { return !(*this == o); }
+};
+
+// ColumnWrapper (src/shared/types/column_wrapper.h:108-183): a typed std::vector.
+struct Col {
+  DT type = UNKNOWN;
+  std::vector<uint8_t> b;
+  std::vector<int64_t> i;
+  std::vector<double> f;
+  std::vector<std::string> s;
+  std::vector<U128> u;
+  explicit Col(DT t) : type(t) {}
+  size_t size() const {
+    switch (type) {
+      case BOOLEAN: return b.size();
+      case INT64:
+      case TIME64NS: return i.size();
+      case FLOAT64: return f.size();
+      case STRING: return s.size();
+      case UINT128: return u.size();
+      default: return 0;
+    }
+  }
+  void reserve(size_t n) {
+    switch (type) {
+      case BOOLEAN: b.reserve(n); break;
+      case INT64:
+      case TIME64NS: i.reserve(n); break;
+      case FLOAT64: f.reserve(n); break;
+      case STRING: s.reserve(n); break;
+      case UINT128: u.reserve(n); break;
+      default: break;
+    }
+  }
+  void clear() { b.clear(); i.clear(); f.clear(); s.clear(); u.clear(); }
+  void append_from(const Col& o, size_t r) {
+    switch (type) {
+      case BOOLEAN: b.push_back(o.b[r]); break;
+      case INT64:
+      case TIME64NS: i.push_back(o.i[r]); break;
+      case FLOAT64: f.push_back(o.f[r]); break;
+      case STRING: s.push_back(o.s[r]); break;
+      case UINT128: u.push_back(o.u[r]); break;
+      default: break;
+    }
+  }
+};
+using ColPtr = std::shared_ptr<Col>;
+
+struct RowBatch {
+  std::vector<ColPtr> cols;
+  int64_t num_rows = 0;
+  bool eow = false, eos = false;
+};
+
+// A scalar value (ScalarValue, plan.proto:519-531).
+struct Value {
+  DT type = UNKNOWN;
+  bool b = false;
+  int64_t i = 0;
+  double f = 0;
+  std::string s;
+  U128 u;
+};
+
+static Value ParseValue(const Json& j) {
+  Value v;
+  v.type = ParseDT(j["dataType"]);
+  switch (v.type) {
+    case BOOLEAN: v.b = j["boolValue"].as_bool(); break;
+    case INT64: v.i = j["int64Value"].as_i64(); break;
+    case TIME64NS: v.i = j["time64NsValue"].as_i64(); break;
+    case FLOAT64: v.f = j["float64Value"].as_f64(); break;
+    case STRING: v.s = j["stringValue"].as_str(); break;
+    case UINT128:
+      v.u.lo = j["uint128Value"]["low"].as_u64();
+      v.u.hi = j["uint128Value"]["high"].as_u64();
+      break;
+    default: throw Error(INVALID_ARGUMENT, "bad scalar value type");
+  }
+  return v;
+}
+
+// EvalScalarToColumnWrapper (expression_evaluator.cc:115-134): materialise N copies.
+static ColPtr ConstCol(const Value& v, size_t n) {
+  auto c = std::make_shared<Col>(v.type);
+  switch (v.type) {
+    case BOOLEAN: c->b.assign(n, v.b); break;
+    case INT64:
+    case TIME64NS: c->i.assign(n, v.i); break;
+    case FLOAT64: c->f.assign(n, v.f); break;
+    case STRING: c->s.assign(n, v.s); break;
+    case UINT128: c->u.assign(n, v.u); break;
+    default: break;
+  }
+  return c;
+}
+
+/*********************************************************************************************
+ * Scalar UDF registry (math_ops.cc:52-223, json_ops.cc:32), keyed by (name, arg types).
+ *********************************************************************************************/
+using UDFExec = std::function<void(const std::vector<const Col*>& args, Col* out, size_t n)>;
+struct UDFDef {
+  DT out;
+  UDFExec exec;
+};
+
+template <DT T> struct Native;
+template <> struct Native<BOOLEAN> { using type = bool; static bool get(const Col& c, size_t r) { return c.b[r] != 0; } static void put(Col* c, bool v) { c->b.push_back(v ? 1 : 0); } };
+template <> struct Native<INT64> { using type = int64_t; static int64_t get(const Col& c, size_t r) { return c.i[r]; } static void put(Col* c, int64_t v) { c->i.push_back(v); } };
+template <> struct Native<TIME64NS> { using type = int64_t; static int64_t get(const Col& c, size_t r) { return c.i[r]; } static void put(Col* c, int64_t v) { c->i.push_back(v); } };
+template <> struct Native<FLOAT64> { using type = double; static double get(const Col& c, size_t r) { return c.f[r]; } static void put(Col* c, double v) { c->f.push_back(v); } };
+// GetValueFromArrowArray<STRING> returns a std::string copy per access (arrow_adapter.h:123-131).
+template <> struct Native<STRING> { using type = std::string; static std::string get(const Col& c, size_t r) { return c.s[r]; } static void put(Col* c, std::string v) { c->s.push_back(std::move(v)); } };
+template <> struct Native<UINT128> { using type = U128; static U128 get(const Col& c, size_t r) { return c.u[r]; } static void put(Col* c, U128 v) { c->u.push_back(v); } };
+
+static std::string Key(const std::string& name, const std::vector<DT>& types) {
+  std::string k = name + "(";
+  for (auto t : types) k += std::to_string(static_cast<int>(t)) + ",";
+  return k + ")";
+}
+
+class Registry {
+ public:
+  static Registry& Get() {
+    static Registry r;
+    return r;
+  }
+  const UDFDef* GetUDF(const std::string& name, const std::vector<DT>& types) const {
+    auto it = udfs_.find(Key(name, types));
+    return it == udfs_.end() ? nullptr : &it->second;
+  }
+
+  template <DT A, DT B, DT R, typename F>
+  void Bin(const std::string& name, F fn) {
+    udfs_[Key(name, {A, B})] = UDFDef{R, [fn](const std::vector<const Col*>& a, Col* out, size_t n) {
+                                        out->reserve(n);
+                                        for (size_t r = 0; r < n; ++r)
+                                          Native<R>::put(out, fn(Native<A>::get(*a[0], r), Native<B>::get(*a[1], r)));
+                                      }};
+  }
+  template <DT A, DT R, typename F>
+  void Un(const std::string& name, F fn) {
+    udfs_[Key(name, {A})] = UDFDef{R, [fn](const std::vector<const Col*>& a, Col* out, size_t n) {
+                                     out->reserve(n);
+                                     for (size_t r = 0; r < n; ++r) Native<R>::put(out, fn(Native<A>::get(*a[0], r)));
+                                   }};
+  }
+
+ private:
+  std::map<std::string, UDFDef> udfs_;
+  Registry();
+};
+
+// Two's-complement wrapping int64 arithmetic (the reference's signed overflow is UB; every
+// supported target wraps).
+static inline int64_t WAdd(int64_t a, int64_t b) { return static_cast<int64_t>(static_cast<uint64_t>(a) + static_cast<uint64_t>(b)); }
+static inline int64_t WSub(int64_t a, int64_t b) { return static_cast<int64_t>(static_cast<uint64_t>(a) - static_cast<uint64_t>(b)); }
+static inline int64_t WMul(int64_t a, int64_t b) { return static_cast<int64_t>(static_cast<uint64_t>(a) * static_cast<uint64_t>(b)); }
+static inline int64_t SMod(int64_t a, int64_t b) { return b == 0 ? 0 : (b == -1 ? 0 : a % b); }
+
+Registry::Registry() {
+  // add / subtract / multiply (math_ops.h:33-150; math_ops.cc:57-105).
+  Bin<INT64, INT64, INT64>("add", [](int64_t a, int64_t b) { return WAdd(a, b); });
+  Bin<FLOAT64, FLOAT64, FLOAT64>("add", [](double a, double b) { return a + b; });
+  Bin<STRING, STRING, STRING>("add", [](std::string a, std::string b) { return a + b; });
+  Bin<FLOAT64, INT64, FLOAT64>("add", [](double a, int64_t b) { return a + b; });
+  Bin<INT64, FLOAT64, FLOAT64>("add", [](int64_t a, double b) { return a + b; });
+  Bin<TIME64NS, INT64, TIME64NS>("add", [](int64_t a, int64_t b) { return WAdd(a, b); });
+  Bin<INT64, TIME64NS, TIME64NS>("add", [](int64_t a, int64_t b) { return WAdd(a, b); });
+  Bin<INT64, INT64, INT64>("subtract", [](int64_t a, int64_t b) { return WSub(a, b); });
+  Bin<FLOAT64, FLOAT64, FLOAT64>("subtract", [](double a, double b) { return a - b; });
+  Bin<FLOAT64, INT64, FLOAT64>("subtract", [](double a, int64_t b) { return a - b; });
+  Bin<INT64, FLOAT64, FLOAT64>("subtract", [](int64_t a, double b) { return a - b; });
+  Bin<TIME64NS, INT64, TIME64NS>("subtract", [](int64_t a, int64_t b) { return WSub(a, b); });
+  Bin<TIME64NS, TIME64NS, INT64>("subtract", [](int64_t a, int64_t b) { return WSub(a, b); });
+  Bin<INT64, TIME64NS, INT64>("subtract", [](int64_t a, int64_t b) { return WSub(a, b); });
+  // DivideUDF always returns double(a)/double(b) (math_ops.h:84-89).
+  Bin<INT64, INT64, FLOAT64>("divide", [](int64_t a, int64_t b) { return static_cast<double>(a) / static_cast<double>(b); });
+  Bin<FLOAT64, INT64, FLOAT64>("divide", [](double a, int64_t b) { return a / static_cast<double>(b); });
+  Bin<INT64, FLOAT64, FLOAT64>("divide", [](int64_t a, double b) { return static_cast<double>(a) / b; });
+  Bin<FLOAT64, FLOAT64, FLOAT64>("divide", [](double a, double b) { return a / b; });
+  Bin<INT64, INT64, INT64>("multiply", [](int64_t a, int64_t b) { return WMul(a, b); });
+  Bin<FLOAT64, FLOAT64, FLOAT64>("multiply", [](double a, double b) { return a * b; });
+  Bin<FLOAT64, INT64, FLOAT64>("multiply", [](double a, int64_t b) { return a * b; });
+  Bin<INT64, FLOAT64, FLOAT64>("multiply", [](int64_t a, double b) { return a * b; });
+  // modulo (math_ops.cc:118-125): b1 % b2.
+  Bin<TIME64NS, INT64, INT64>("modulo", SMod);
+  Bin<TIME64NS, TIME64NS, INT64>("modulo", SMod);
+  Bin<INT64, TIME64NS, INT64>("modulo", SMod);
+  Bin<INT64, INT64, INT64>("modulo", SMod);
+  // logical (math_ops.h:265-315).
+  Bin<INT64, INT64, BOOLEAN>("logicalOr", [](int64_t a, int64_t b) { return a || b; });
+  Bin<BOOLEAN, BOOLEAN, BOOLEAN>("logicalOr", [](bool a, bool b) { return a || b; });
+  Bin<INT64, INT64, BOOLEAN>("logicalAnd", [](int64_t a, int64_t b) { return a && b; });
+  Bin<BOOLEAN, BOOLEAN, BOOLEAN>("logicalAnd", [](bool a, bool b) { return a && b; });
+  Un<INT64, BOOLEAN>("logicalNot", [](int64_t a) { return !a; });
+  Un<BOOLEAN, BOOLEAN>("logicalNot", [](bool a) { return !a; });
+  Un<INT64, INT64>("negate", [](int64_t a) { return WSub(0, a); });
+  Un<FLOAT64, FLOAT64>("negate", [](double a) { return -a; });
+  Un<INT64, INT64>("invert", [](int64_t a) { return ~a; });
+  // equal / notEqual (math_ops.cc:145-175; math_ops.h:372-410).  FLOAT64==FLOAT64 is
+  // ApproxEqualUDF (|a-b| < epsilon).
+  Bin<INT64, INT64, BOOLEAN>("equal", [](int64_t a, int64_t b) { return a == b; });
+  Bin<STRING, STRING, BOOLEAN>("equal", [](std::string a, std::string b) { return a == b; });
+  Bin<BOOLEAN, BOOLEAN, BOOLEAN>("equal", [](bool a, bool b) { return a == b; });
+  Bin<TIME64NS, TIME64NS, BOOLEAN>("equal", [](int64_t a, int64_t b) { return a == b; });
+  Bin<UINT128, UINT128, BOOLEAN>("equal", [](U128 a, U128 b) { return a == b; });
+  Bin<BOOLEAN, INT64, BOOLEAN>("equal", [](bool a, int64_t b) { return static_cast<int64_t>(a) == b; });
+  Bin<INT64, BOOLEAN, BOOLEAN>("equal", [](int64_t a, bool b) { return a == static_cast<int64_t>(b); });
+  Bin<INT64, FLOAT64, BOOLEAN>("equal", [](int64_t a, double b) { return static_cast<double>(a) == b; });
+  Bin<FLOAT64, INT64, BOOLEAN>("equal", [](double a, int64_t b) { return a == static_cast<double>(b); });
+  Bin<FLOAT64, FLOAT64, BOOLEAN>("equal", [](double a, double b) { return std::abs(a - b) < std::numeric_limits<double>::epsilon(); });
+  Bin<INT64, INT64, BOOLEAN>("notEqual", [](int64_t a, int64_t b) { return a != b; });
+  Bin<STRING, STRING, BOOLEAN>("notEqual", [](std::string a, std::string b) { return a != b; });
+  Bin<BOOLEAN, BOOLEAN, BOOLEAN>("notEqual", [](bool a, bool b) { return a != b; });
+  Bin<TIME64NS, TIME64NS, BOOLEAN>("notEqual", [](int64_t a, int64_t b) { return a != b; });
+  Bin<UINT128, UINT128, BOOLEAN>("notEqual", [](U128 a, U128 b) { return a != b; });
+  Bin<BOOLEAN, INT64, BOOLEAN>("notEqual", [](bool a, int64_t b) { return static_cast<int64_t>(a) != b; });
+  Bin<INT64, BOOLEAN, BOOLEAN>("notEqual", [](int64_t a, bool b) { return a != static_cast<int64_t>(b); });
+  Bin<INT64, FLOAT64, BOOLEAN>("notEqual", [](int64_t a, double b) { return static_cast<double>(a) != b; });
+  Bin<FLOAT64, INT64, BOOLEAN>("notEqual", [](double a, int64_t b) { return a != static_cast<double>(b); });
+  Bin<FLOAT64, FLOAT64, BOOLEAN>("notEqual", [](double a, double b) { return std::abs(a - b) > std::numeric_limits<double>::epsilon(); });
+  Bin<FLOAT64, FLOAT64, BOOLEAN>("approxEqual", [](double a, double b) { return std::abs(a - b) < std::numeric_limits<double>::epsilon(); });
+  // ordering comparisons (math_ops.h:412-510; math_ops.cc:177-200).
+#define PXO_CMP(NAME, OP)                                                                   \
+  Bin<INT64, INT64, BOOLEAN>(NAME, [](int64_t a, int64_t b) { return a OP b; });          \
+  Bin<TIME64NS, TIME64NS, BOOLEAN>(NAME, [](int64_t a, int64_t b) { return a OP b; });    \
+  Bin<FLOAT64, FLOAT64, BOOLEAN>(NAME, [](double a, double b) { return a OP b; });        \
+  Bin<STRING, STRING, BOOLEAN>(NAME, [](std::string a, std::string b) { return a OP b; });
+  PXO_CMP("greaterThan", >)
+  PXO_CMP("greaterThanEqual", >=)
+  PXO_CMP("lessThan", <)
+  PXO_CMP("lessThanEqual", <=)
+#undef PXO_CMP
+  // bin (math_ops.h:512-527): a - a % b.
+  Bin<INT64, INT64, INT64>("bin", [](int64_t a, int64_t b) { return WSub(a, SMod(a, b)); });
+  Bin<TIME64NS, TIME64NS, TIME64NS>("bin", [](int64_t a, int64_t b) { return WSub(a, SMod(a, b)); });
+  Bin<INT64, TIME64NS, INT64>("bin", [](int64_t a, int64_t b) { return WSub(a, SMod(a, b)); });
+  Bin<TIME64NS, INT64, TIME64NS>("bin", [](int64_t a, int64_t b) { return WSub(a, SMod(a, b)); });
+  Bin<FLOAT64, INT64, INT64>("bin", [](double a, int64_t b) {
+    int64_t ia = static_cast<int64_t>(a);
+    return WSub(ia, SMod(ia, b));
+  });
+  Un<TIME64NS, INT64>("time_to_int64", [](int64_t a) { return a; });
+  Un<INT64, TIME64NS>("int64_to_time", [](int64_t a) { return a; });
+  // Test-registry UDFs of FilterNodeTest (filter_node_test.cc:41-53): "eq" on INT64 / STRING.
+  Bin<INT64, INT64, BOOLEAN>("eq", [](int64_t a, int64_t b) { return a == b; });
+  Bin<STRING, STRING, BOOLEAN>("eq", [](std::string a, std::string b) { return a == b; });
+  // pluck_float64 (json_ops.h:131-153).
+  Bin<STRING, STRING, FLOAT64>("pluck_float64", [](std::string in, std::string key) {
+    return oracle_pluck_float64(in.c_str(), key.c_str());
+  });
+}
+
+/*********************************************************************************************
+ * UDAs (math_ops.h:583-772, math_sketches.h:33-82, agg_node_test.cc:44-72 test UDAs).
+ *********************************************************************************************/
+std::string FormatJsonDouble(double v) {
+  // Shortest round-trip rendering, always with a '.' or exponent so that rapidjson reads it back
+  // as a double (IsDouble) — the property pluck_float64 depends on.
+  if (std::isnan(v) || std::isinf(v)) return "null";
+  char buf[64];
+  for (int prec = 1; prec <= 17; ++prec) {
+    snprintf(buf, sizeof(buf), "%.*g", prec, v);
+    if (std::strtod(buf, nullptr) == v) break;
+  }
+  std::string s(buf);
+  if (s.find_first_of(".eEn") == std::string::npos) s += ".0";
+  return s;
+}
+
+std::string QuantilesJson(TDigest* d) {
+  static const char* kNames[7] = {"p01", "p10", "p25", "p50", "p75", "p90", "p99"};
+  static const double kQ[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
+  std::string s = "{";
+  for (int k = 0; k < 7; ++k) {
+    if (k) s += ",";
+    s += "\"";
+    s += kNames[k];
+    s += "\":";
+    s += FormatJsonDouble(d->quantile(kQ[k]));
+  }
+  return s + "}";
+}
+
+struct UDA {
+  virtual ~UDA() = default;
+  // Per-row Update from the arg columns (UDAWrapper::UpdateWrapper, udf_wrapper.h:287-310).
+  virtual void Update(const std::vector<const Col*>& args, size_t r) = 0;
+  virtual void Merge(const UDA& other) = 0;
+  virtual void Finalize(Col* out) = 0;
+};
+
+template <DT A>
+struct CountUDA : UDA {
+  uint64_t count = 0;
+  void Update(const std::vector<const Col*>&, size_t) override { ++count; }
+  void Merge(const UDA& o) override { count += static_cast<const CountUDA&>(o).count; }
+  void Finalize(Col* out) override { out->i.push_back(static_cast<int64_t>(count)); }
+};
+
+template <DT A>
+struct MeanUDA : UDA {
+  uint64_t size = 0;
+  double sum = 0;  // "count" in the reference's MeanInfo
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    ++size;
+    sum += static_cast<double>(Native<A>::get(*a[0], r));
+  }
+  void Merge(const UDA& o) override {
+    auto& m = static_cast<const MeanUDA&>(o);
+    size += m.size;
+    sum += m.sum;
+  }
+  void Finalize(Col* out) override { out->f.push_back(sum / static_cast<double>(size)); }
+};
+
+template <DT A, DT R>
+struct SumUDA : UDA {
+  typename Native<R>::type sum = 0;
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    if constexpr (R == FLOAT64) {
+      sum = sum + Native<A>::get(*a[0], r);
+    } else {
+      sum = WAdd(sum, static_cast<int64_t>(Native<A>::get(*a[0], r)));
+    }
+  }
+  void Merge(const UDA& o) override {
+    if constexpr (R == FLOAT64) sum = sum + static_cast<const SumUDA&>(o).sum;
+    else sum = WAdd(sum, static_cast<const SumUDA&>(o).sum);
+  }
+  void Finalize(Col* out) override { Native<R>::put(out, sum); }
+};
+
+template <DT A>
+struct MaxUDA : UDA {
+  // MaxUDA initialises to numeric_limits<T>::min() (math_ops.h:699): for FLOAT64 that is the
+  // smallest positive double.
+  typename Native<A>::type v = std::numeric_limits<typename Native<A>::type>::min();
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    auto x = Native<A>::get(*a[0], r);
+    if (v < x) v = x;
+  }
+  void Merge(const UDA& o) override {
+    auto x = static_cast<const MaxUDA&>(o).v;
+    if (x > v) v = x;
+  }
+  void Finalize(Col* out) override { Native<A>::put(out, v); }
+};
+
+template <DT A>
+struct MinUDA : UDA {
+  typename Native<A>::type v = std::numeric_limits<typename Native<A>::type>::max();
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    auto x = Native<A>::get(*a[0], r);
+    if (v > x) v = x;
+  }
+  void Merge(const UDA& o) override {
+    auto x = static_cast<const MinUDA&>(o).v;
+    if (x < v) v = x;
+  }
+  void Finalize(Col* out) override { Native<A>::put(out, v); }
+};
+
+template <DT A>
+struct QuantilesUDA : UDA {
+  TDigest digest{1000};
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    digest.add(static_cast<double>(Native<A>::get(*a[0], r)));
+  }
+  void Merge(const UDA& o) override { digest.merge(&static_cast<const QuantilesUDA&>(o).digest); }
+  void Finalize(Col* out) override { out->s.push_back(QuantilesJson(&digest)); }
+};
+
+// Test UDAs registered by AggNodeTest (agg_node_test.cc:44-72, 282-289).
+struct MinSumUDA : UDA {
+  int64_t sum = 0;
+  void Update(const std::vector<const Col*>& a, size_t r) override {
+    sum = WAdd(sum, std::min(a[0]->i[r], a[1]->i[r]));
+  }
+  void Merge(const UDA& o) override { sum = WAdd(sum, static_cast<const MinSumUDA&>(o).sum); }
+  void Finalize(Col* out) override { out->i.push_back(sum); }
+};
+
+struct UDADef {
+  DT out;
+  size_t n_update_args;
+  std::function<std::unique_ptr<UDA>(const std::vector<Value>& init)> make;
+};
+
+class UDARegistry {
+ public:
+  static UDARegistry& Get() {
+    static UDARegistry r;
+    return r;
+  }
+  const UDADef* Find(const std::string& name, const std::vector<DT>& types) const {
+    auto it = defs_.find(Key(name, types));
+    return it == defs_.end() ? nullptr : &it->second;
+  }
+
+ private:
+  std::map<std::string, UDADef> defs_;
+  template <typename T>
+  void Reg(const std::string& name, std::vector<DT> types, DT out, size_t nargs) {
+    defs_[Key(name, types)] = UDADef{out, nargs, [](const std::vector<Value>&) { return std::make_unique<T>(); }};
+  }
+  UDARegistry() {
+    Reg<MeanUDA<FLOAT64>>("mean", {FLOAT64}, FLOAT64, 1);
+    Reg<MeanUDA<INT64>>("mean", {INT64}, FLOAT64, 1);
+    Reg<MeanUDA<BOOLEAN>>("mean", {BOOLEAN}, FLOAT64, 1);
+    Reg<SumUDA<FLOAT64, FLOAT64>>("sum", {FLOAT64}, FLOAT64, 1);
+    Reg<SumUDA<INT64, INT64>>("sum", {INT64}, INT64, 1);
+    Reg<SumUDA<BOOLEAN, INT64>>("sum", {BOOLEAN}, INT64, 1);
+    Reg<MaxUDA<FLOAT64>>("max", {FLOAT64}, FLOAT64, 1);
+    Reg<MaxUDA<INT64>>("max", {INT64}, INT64, 1);
+    Reg<MaxUDA<TIME64NS>>("max", {TIME64NS}, TIME64NS, 1);
+    Reg<MinUDA<FLOAT64>>("min", {FLOAT64}, FLOAT64, 1);
+    Reg<MinUDA<INT64>>("min", {INT64}, INT64, 1);
+    Reg<MinUDA<TIME64NS>>("min", {TIME64NS}, TIME64NS, 1);
+    for (DT t : {FLOAT64, INT64, TIME64NS, BOOLEAN, STRING, UINT128}) {
+      defs_[Key("count", {t})] = UDADef{INT64, 1, [](const std::vector<Value>&) { return std::make_unique<CountUDA<INT64>>(); }};
+    }
+    Reg<QuantilesUDA<INT64>>("quantiles", {INT64}, STRING, 1);
+    Reg<QuantilesUDA<FLOAT64>>("quantiles", {FLOAT64}, STRING, 1);
+    Reg<MinSumUDA>("minsum", {INT64, INT64}, INT64, 2);
+    defs_[Key("minsum_w_init", {INT64, INT64, INT64})] =
+        UDADef{INT64, 2, [](const std::vector<Value>& init) {
+                 auto u = std::make_unique<MinSumUDA>();
+                 if (!init.empty()) u->sum = init[0].i;  // MinSumWithInitUDA::Init
+                 return u;
+               }};
+  }
+};
+
+/*********************************************************************************************
+ * Plan objects (plan/scalar_expression.cc:232-348, plan/operators.cc:59-395).
+ *********************************************************************************************/
+struct Expr {
+  enum Kind { kConst, kColumn, kFunc, kAgg } kind = kConst;
+  Value value;
+  int64_t col_node = 0, col_index = 0;
+  std::string name;
+  std::vector<Value> init_args;
+  std::vector<Expr> args;
+  std::vector<DT> arg_types;
+};
+
+static Expr ParseColumn(const Json& j) {
+  Expr e;
+  e.kind = Expr::kColumn;
+  e.col_node = j["node"].as_i64();
+  e.col_index = j["index"].as_i64();
+  return e;
+}
+
+static Expr ParseScalarExpr(const Json& j) {
+  Expr e;
+  if (j.has("constant")) {
+    e.kind = Expr::kConst;
+    e.value = ParseValue(j["constant"]);
+  } else if (j.has("column")) {
+    e = ParseColumn(j["column"]);
+  } else if (j.has("func")) {
+    const Json& f = j["func"];
+    e.kind = Expr::kFunc;
+    e.name = f["name"].as_str();
+    for (size_t i = 0; i < f["initArgs"].size(); ++i) e.init_args.push_back(ParseValue(f["initArgs"].at(i)));
+    for (size_t i = 0; i < f["args"].size(); ++i) e.args.push_back(ParseScalarExpr(f["args"].at(i)));
+    for (size_t i = 0; i < f["argsDataTypes"].size(); ++i) e.arg_types.push_back(ParseDT(f["argsDataTypes"].at(i)));
+  } else {
+    throw Error(INVALID_ARGUMENT, "bad scalar expression");
+  }
+  return e;
+}
+
+static Expr ParseAggExpr(const Json& j) {
+  Expr e;
+  e.kind = Expr::kAgg;
+  e.name = j["name"].as_str();
+  for (size_t i = 0; i < j["initArgs"].size(); ++i) e.init_args.push_back(ParseValue(j["initArgs"].at(i)));
+  for (size_t i = 0; i < j["args"].size(); ++i) {
+    const Json& a = j["args"].at(i);
+    Expr c;
+    if (a.has("constant")) {
+      c.kind = Expr::kConst;
+      c.value = ParseValue(a["constant"]);
+    } else {
+      c = ParseColumn(a["column"]);
+    }
+    e.args.push_back(c);
+  }
+  for (size_t i = 0; i < j["argsDataTypes"].size(); ++i) e.arg_types.push_back(ParseDT(j["argsDataTypes"].at(i)));
+  return e;
+}
+
+// Output type of an expression given the input relation (ScalarFunc::OutputDataType,
+// scalar_expression.cc:278-311): computed from the children's types via the registry.
+static DT ExprType(const Expr& e, const std::vector<DT>& in) {
+  switch (e.kind) {
+    case Expr::kConst: return e.value.type;
+    case Expr::kColumn:
+      if (e.col_index < 0 || static_cast<size_t>(e.col_index) >= in.size()) throw Error(INVALID_ARGUMENT, "column index out of range");
+      return in[e.col_index];
+    case Expr::kFunc: {
+      std::vector<DT> types;
+      for (auto& v : e.init_args) types.push_back(v.type);
+      for (auto& a : e.args) types.push_back(ExprType(a, in));
+      const UDFDef* d = Registry::Get().GetUDF(e.name, types);
+      if (!d) throw Error(NOT_FOUND, "no UDF " + Key(e.name, types));
+      return d->out;
+    }
+    case Expr::kAgg: {
+      std::vector<DT> types;
+      for (auto& v : e.init_args) types.push_back(v.type);
+      for (auto& a : e.args) types.push_back(ExprType(a, in));
+      const UDADef* d = UDARegistry::Get().Find(e.name, types);
+      if (!d) throw Error(NOT_FOUND, "no UDA " + Key(e.name, types));
+      return d->out;
+    }
+  }
+  return UNKNOWN;
+}
+
+/*********************************************************************************************
+ * Exec nodes (exec_node.h:133-337 NVI).
+ *********************************************************************************************/
+struct ExecNode {
+  std::vector<ExecNode*> children;
+  std::vector<size_t> child_parent_index;
+  std::vector<DT> out_types;
+  virtual ~ExecNode() = default;
+  virtual void ConsumeNext(const RowBatch& rb, size_t parent_index) = 0;
+  void Send(const RowBatch& rb) {
+    if (rb.eos && !rb.eow) throw Error(INTERNAL, "eos without eow");
+    for (size_t i = 0; i < children.size(); ++i) children[i]->ConsumeNext(rb, child_parent_index[i]);
+  }
+};
+
+// VectorNative evaluation (expression_evaluator.cc:191-275): column leaves are copied into
+// ColumnWrappers (column_wrapper.h:207-233), constants materialised, funcs via ExecBatch.
+static ColPtr EvalVectorNative(const Expr& e, const RowBatch& rb) {
+  switch (e.kind) {
+    case Expr::kConst: return ConstCol(e.value, rb.num_rows);
+    case Expr::kColumn: return std::make_shared<Col>(*rb.cols.at(e.col_index));
+    case Expr::kFunc: {
+      std::vector<ColPtr> kids;
+      std::vector<const Col*> raw;
+      std::vector<DT> types;
+      for (auto& v : e.init_args) types.push_back(v.type);
+      for (auto& a : e.args) {
+        kids.push_back(EvalVectorNative(a, rb));
+        raw.push_back(kids.back().get());
+        types.push_back(kids.back()->type);
+      }
+      const UDFDef* d = Registry::Get().GetUDF(e.name, types);
+      if (!d) throw Error(NOT_FOUND, "no UDF " + Key(e.name, types));
+      auto out = std::make_shared<Col>(d->out);
+      d->exec(raw, out.get(), rb.num_rows);
+      return out;
+    }
+    default: throw Error(INVALID_ARGUMENT, "bad expression in scalar context");
+  }
+}
+
+// ArrowNative evaluation (expression_evaluator.cc:277-342): column refs are shared (no copy).
+static ColPtr EvalArrowNative(const Expr& e, const RowBatch& rb) {
+  if (e.kind == Expr::kColumn) return rb.cols.at(e.col_index);
+  if (e.kind == Expr::kConst) return ConstCol(e.value, rb.num_rows);
+  std::vector<ColPtr> kids;
+  std::vector<const Col*> raw;
+  std::vector<DT> types;
+  for (auto& v : e.init_args) types.push_back(v.type);
+  for (auto& a : e.args) {
+    kids.push_back(EvalArrowNative(a, rb));
+    raw.push_back(kids.back().get());
+    types.push_back(kids.back()->type);
+  }
+  const UDFDef* d = Registry::Get().GetUDF(e.name, types);
+  if (!d) throw Error(NOT_FOUND, "no UDF " + Key(e.name, types));
+  auto out = std::make_shared<Col>(d->out);
+  d->exec(raw, out.get(), rb.num_rows);
+  return out;
+}
+
+// FilterNode::ConsumeNextImpl (filter_node.cc:132-171).
+struct FilterNode : ExecNode {
+  Expr pred;
+  std::vector<int64_t> selected;
+  void ConsumeNext(const RowBatch& rb, size_t) override {
+    ColPtr p = EvalVectorNative(pred, rb);
+    if (p->type != BOOLEAN) throw Error(INVALID_ARGUMENT, "predicate must be boolean");
+    size_t n_out = 0;
+    for (size_t r = 0; r < p->b.size(); ++r) n_out += p->b[r] ? 1 : 0;
+    RowBatch out;
+    out.num_rows = static_cast<int64_t>(n_out);
+    for (int64_t ci : selected) {
+      const Col& in = *rb.cols.at(ci);
+      auto c = std::make_shared<Col>(in.type);
+      c->reserve(n_out);
+      for (size_t r = 0; r < p->b.size(); ++r)
+        if (p->b[r]) c->append_from(in, r);
+      out.cols.push_back(c);
+    }
+    out.eow = rb.eow;
+    out.eos = rb.eos;
+    Send(out);
+  }
+};
+
+// MapNode::ConsumeNextImpl (map_node.cc:64-71).
+struct MapNode : ExecNode {
+  std::vector<Expr> exprs;
+  void ConsumeNext(const RowBatch& rb, size_t) override {
+    RowBatch out;
+    out.num_rows = rb.num_rows;
+    for (auto& e : exprs) out.cols.push_back(EvalArrowNative(e, rb));
+    out.eow = rb.eow;
+    out.eos = rb.eos;
+    Send(out);
+  }
+};
+
+// RowTuple (row_tuple.h:71-188): 16 B fixed slots + strings; exact-equality semantics.
+struct RowTuple {
+  std::vector<DT> types;
+  std::vector<std::array<uint64_t, 2>> fixed;
+  std::vector<std::string> strs;
+  bool operator==(const RowTuple& o) const { return fixed == o.fixed && strs == o.strs; }
+};
+struct RowTupleHash {
+  size_t operator()(const RowTuple* rt) const {
+    // Hash64 over fixed bytes then HashCombine per string (row_tuple.h:140-153); the exact hash
+    // function does not affect results (output order is unspecified).
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (auto& f : rt->fixed) {
+      h = (h ^ f[0]) * 0x100000001b3ULL;
+      h = (h ^ f[1]) * 0x100000001b3ULL;
+    }
+    for (auto& s : rt->strs) h = (h * 31) ^ std::hash<std::string>()(s);
+    return h;
+  }
+};
+struct RowTupleEq {
+  bool operator()(const RowTuple* a, const RowTuple* b) const { return *a == *b; }
+};
+
+static void ExtractIntoRowTuple(RowTuple* rt, const Col& c, size_t slot, size_t r) {
+  // ExtractIntoRowTuple<DT> (row_tuple.h:246-252); strings copied into variable_values.
+  switch (c.type) {
+    case BOOLEAN: rt->fixed[slot] = {static_cast<uint64_t>(c.b[r] ? 1 : 0), 0}; break;
+    case INT64:
+    case TIME64NS: rt->fixed[slot] = {static_cast<uint64_t>(c.i[r]), 0}; break;
+    case FLOAT64: {
+      uint64_t bits;
+      std::memcpy(&bits, &c.f[r], 8);
+      rt->fixed[slot] = {bits, 0};
+      break;
+    }
+    case UINT128: rt->fixed[slot] = {c.u[r].lo, c.u[r].hi}; break;
+    case STRING: rt->strs[slot] = c.s[r]; break;
+    default: break;
+  }
+}
+
+static void AppendTupleValue(Col* out, const RowTuple& rt, size_t slot) {
+  switch (out->type) {
+    case BOOLEAN: out->b.push_back(static_cast<uint8_t>(rt.fixed[slot][0])); break;
+    case INT64:
+    case TIME64NS: out->i.push_back(static_cast<int64_t>(rt.fixed[slot][0])); break;
+    case FLOAT64: {
+      double d;
+      std::memcpy(&d, &rt.fixed[slot][0], 8);
+      out->f.push_back(d);
+      break;
+    }
+    case UINT128: out->u.push_back(U128{rt.fixed[slot][0], rt.fixed[slot][1]}); break;
+    case STRING: out->s.push_back(rt.strs[slot]); break;
+    default: break;
+  }
+}
+
+constexpr size_t kAggCompactionThreshold = 512;  // agg_node.cc:43
+
+// AggNode (agg_node.cc:88-542).
+struct AggNode : ExecNode {
+  std::vector<int64_t> groups;
+  std::vector<DT> group_types;
+  std::vector<Expr> values;
+  bool windowed = false;
+  std::vector<DT> in_types;
+  // CreateColumnMapping (agg_node.cc:483-507)
+  std::map<int64_t, size_t> plan_to_stored;
+  std::vector<int64_t> stored_to_plan;
+
+  struct UDAInfo {
+    std::unique_ptr<UDA> uda;
+    const UDADef* def;
+  };
+  struct AggHashValue {
+    std::vector<UDAInfo> udas;
+    std::vector<ColPtr> agg_cols;
+  };
+  std::unordered_map<RowTuple*, AggHashValue*, RowTupleHash, RowTupleEq> map;
+  std::vector<std::unique_ptr<RowTuple>> tuple_pool;
+  std::vector<std::unique_ptr<AggHashValue>> value_pool;
+  std::vector<UDAInfo> no_group_udas;
+  std::vector<const UDADef*> defs;
+
+  void Init() {
+    for (auto& v : values) {
+      std::vector<DT> types;
+      for (auto& a : v.init_args) types.push_back(a.type);
+      for (auto& a : v.args) types.push_back(ExprType(a, in_types));
+      const UDADef* d = UDARegistry::Get().Find(v.name, types);
+      if (!d) throw Error(NOT_FOUND, "no UDA " + Key(v.name, types));
+      defs.push_back(d);
+      for (auto& a : v.args) {
+        if (a.kind == Expr::kColumn && !plan_to_stored.count(a.col_index)) {
+          plan_to_stored[a.col_index] = stored_to_plan.size();
+          stored_to_plan.push_back(a.col_index);
+        }
+      }
+    }
+    for (auto g : groups) group_types.push_back(in_types.at(g));
+    if (groups.empty()) no_group_udas = MakeUDAs();
+  }
+
+  std::vector<UDAInfo> MakeUDAs() {
+    std::vector<UDAInfo> v;
+    for (size_t i = 0; i < values.size(); ++i) v.push_back(UDAInfo{defs[i]->make(values[i].init_args), defs[i]});
+    return v;
+  }
+
+  // EvaluateAggHashValue (agg_node.cc:434-481): per UDA, ExecBatchUpdate over the buffered rows.
+  void EvaluateAggHashValue(AggHashValue* val) {
+    size_t n = val->agg_cols.empty() ? 0 : val->agg_cols[0]->size();
+    for (size_t i = 0; i < values.size(); ++i) {
+      std::vector<ColPtr> kids;
+      std::vector<const Col*> raw;
+      for (auto& a : values[i].args) {
+        if (a.kind == Expr::kConst) kids.push_back(ConstCol(a.value, n));
+        else kids.push_back(val->agg_cols[plan_to_stored[a.col_index]]);
+        raw.push_back(kids.back().get());
+      }
+      for (size_t r = 0; r < n; ++r) val->udas[i].uda->Update(raw, r);
+    }
+    for (auto& c : val->agg_cols) c->clear();
+  }
+
+  void Emit(const RowBatch& rb) {
+    RowBatch out;
+    out.eow = rb.eow;
+    out.eos = rb.eos;
+    if (groups.empty()) {
+      out.num_rows = 1;
+      for (size_t i = 0; i < values.size(); ++i) {
+        auto c = std::make_shared<Col>(defs[i]->out);
+        no_group_udas[i].uda->Finalize(c.get());
+        out.cols.push_back(c);
+      }
+      Send(out);
+      no_group_udas = MakeUDAs();  // ClearAggState
+      return;
+    }
+    // ConvertAggHashMapToRowBatch (agg_node.cc:303-349): groups then values.
+    out.num_rows = static_cast<int64_t>(map.size());
+    std::vector<ColPtr> gcols, vcols;
+    for (auto t : group_types) gcols.push_back(std::make_shared<Col>(t));
+    for (size_t i = 0; i < values.size(); ++i) vcols.push_back(std::make_shared<Col>(defs[i]->out));
+    for (auto& kv : map) {
+      for (size_t g = 0; g < groups.size(); ++g) AppendTupleValue(gcols[g].get(), *kv.first, g);
+      EvaluateAggHashValue(kv.second);
+      for (size_t i = 0; i < values.size(); ++i) kv.second->udas[i].uda->Finalize(vcols[i].get());
+    }
+    for (auto& c : gcols) out.cols.push_back(c);
+    for (auto& c : vcols) out.cols.push_back(c);
+    Send(out);
+    map.clear();  // ClearAggState
+    tuple_pool.clear();
+    value_pool.clear();
+  }
+
+  void ConsumeNext(const RowBatch& rb, size_t) override {
+    bool ready = rb.eos || (rb.eow && windowed);  // ReadyToEmitBatches (agg_node.cc:169-171)
+    if (groups.empty()) {
+      // AggregateGroupByNone (agg_node.cc:182-207): ExecBatchUpdateArrow directly.
+      for (size_t i = 0; i < values.size(); ++i) {
+        std::vector<ColPtr> kids;
+        std::vector<const Col*> raw;
+        for (auto& a : values[i].args) {
+          kids.push_back(a.kind == Expr::kConst ? ConstCol(a.value, rb.num_rows) : rb.cols.at(a.col_index));
+          raw.push_back(kids.back().get());
+        }
+        for (int64_t r = 0; r < rb.num_rows; ++r) no_group_udas[i].uda->Update(raw, r);
+      }
+      if (ready) Emit(rb);
+      return;
+    }
+    // ExtractRowTupleForBatch + HashRowBatch (agg_node.cc:209-271).
+    std::vector<AggHashValue*> row_vals(rb.num_rows);
+    for (int64_t r = 0; r < rb.num_rows; ++r) {
+      auto rt = std::make_unique<RowTuple>();
+      rt->types = group_types;
+      rt->fixed.assign(groups.size(), {0, 0});
+      rt->strs.assign(groups.size(), std::string());
+      for (size_t g = 0; g < groups.size(); ++g) ExtractIntoRowTuple(rt.get(), *rb.cols.at(groups[g]), g, r);
+      auto it = map.find(rt.get());
+      AggHashValue* val;
+      if (it == map.end()) {
+        auto v = std::make_unique<AggHashValue>();
+        v->udas = MakeUDAs();
+        for (auto pi : stored_to_plan) v->agg_cols.push_back(std::make_shared<Col>(in_types[pi]));
+        val = v.get();
+        map[rt.get()] = val;
+        tuple_pool.push_back(std::move(rt));
+        value_pool.push_back(std::move(v));
+      } else {
+        val = it->second;
+      }
+      row_vals[r] = val;
+    }
+    for (size_t s = 0; s < stored_to_plan.size(); ++s) {
+      const Col& in = *rb.cols.at(stored_to_plan[s]);
+      for (int64_t r = 0; r < rb.num_rows; ++r) row_vals[r]->agg_cols[s]->append_from(in, r);
+    }
+    // EvaluatePartialAggregates (agg_node.cc:273-286).
+    if (!values.empty() && !stored_to_plan.empty()) {
+      for (int64_t r = 0; r < rb.num_rows; ++r) {
+        if (row_vals[r]->agg_cols[0]->size() > kAggCompactionThreshold) EvaluateAggHashValue(row_vals[r]);
+      }
+    }
+    if (ready) Emit(rb);
+  }
+};
+
+struct SinkNode : ExecNode {
+  std::string name;
+  std::vector<RowBatch> batches;
+  void ConsumeNext(const RowBatch& rb, size_t) override { batches.push_back(rb); }
+};
+
+struct SourceNode : ExecNode {
+  std::vector<RowBatch> batches;
+  bool explicit_flags = false;
+  size_t next = 0;
+  std::vector<int64_t> col_idxs;
+  bool HasBatchesRemaining() const { return next <= batches.size() && !done; }
+  bool done = false;
+  void ConsumeNext(const RowBatch&, size_t) override {}
+  // MemorySourceNode::GenerateNextImpl (memory_source_node.cc:92-124).
+  void GenerateNext() {
+    if (next >= batches.size()) {
+      RowBatch z;
+      z.num_rows = 0;
+      for (auto t : out_types) z.cols.push_back(std::make_shared<Col>(t));
+      z.eow = z.eos = true;
+      done = true;
+      Send(z);
+      return;
+    }
+    RowBatch rb;
+    const RowBatch& src = batches[next++];
+    rb.num_rows = src.num_rows;
+    for (auto ci : col_idxs) rb.cols.push_back(src.cols.at(ci));
+    if (explicit_flags) {
+      rb.eow = src.eow;
+      rb.eos = src.eos;
+      // Like ExecNodeTester, every given batch is delivered (even after an eos).
+      if (next == batches.size()) done = true;
+      Send(rb);
+      return;
+    }
+    if (next == batches.size()) {
+      rb.eow = rb.eos = true;
+      done = true;
+    }
+    Send(rb);
+  }
+};
+
+/*********************************************************************************************
+ * Plan driver (exec_graph.cc:52-331).
+ *********************************************************************************************/
+struct TableIn {
+  std::vector<std::string> names;
+  std::vector<DT> types;
+  std::vector<RowBatch> batches;
+  bool explicit_flags = false;
+};
+
+struct Graph {
+  std::map<uint64_t, std::unique_ptr<ExecNode>> nodes;
+  std::vector<SourceNode*> sources;
+  std::vector<SinkNode*> sinks;
+
+  void Build(const Json& plan, const std::map<std::string, TableIn>& tables) {
+    const Json& frags = plan["nodes"];
+    for (size_t fi = 0; fi < frags.size(); ++fi) BuildFragment(frags.at(fi), tables);
+  }
+
+  void BuildFragment(const Json& frag, const std::map<std::string, TableIn>& tables) {
+    // Topological order from the fragment DAG (plan_fragment.cc:108-118).
+    std::map<uint64_t, std::vector<uint64_t>> parents;
+    std::vector<uint64_t> order;
+    const Json& dag_nodes = frag["dag"]["nodes"];
+    std::map<uint64_t, int> indeg;
+    std::map<uint64_t, std::vector<uint64_t>> kids;
+    for (size_t i = 0; i < dag_nodes.size(); ++i) {
+      uint64_t id = dag_nodes.at(i)["id"].as_u64();
+      indeg[id];
+      for (size_t p = 0; p < dag_nodes.at(i)["sortedParents"].size(); ++p) {
+        uint64_t pid = dag_nodes.at(i)["sortedParents"].at(p).as_u64();
+        parents[id].push_back(pid);
+        indeg[id]++;
+        kids[pid].push_back(id);
+      }
+    }
+    std::vector<uint64_t> ready;
+    for (auto& kv : indeg)
+      if (kv.second == 0) ready.push_back(kv.first);
+    while (!ready.empty()) {
+      uint64_t id = ready.front();
+      ready.erase(ready.begin());
+      order.push_back(id);
+      for (auto k : kids[id])
+        if (--indeg[k] == 0) ready.push_back(k);
+    }
+    std::map<uint64_t, const Json*> ops;
+    const Json& pn = frag["nodes"];
+    for (size_t i = 0; i < pn.size(); ++i) ops[pn.at(i)["id"].as_u64()] = &pn.at(i)["op"];
+
+    for (uint64_t id : order) {
+      const Json& op = *ops.at(id);
+      std::vector<DT> in;
+      if (!parents[id].empty()) in = nodes.at(parents[id][0])->out_types;
+      std::unique_ptr<ExecNode> node;
+      if (op.has("memSourceOp")) {
+        const Json& m = op["memSourceOp"];
+        auto s = std::make_unique<SourceNode>();
+        auto it = tables.find(m["name"].as_str());
+        if (it == tables.end()) throw Error(NOT_FOUND, "Table '" + m["name"].as_str() + "' not found");
+        s->batches = it->second.batches;
+        s->explicit_flags = it->second.explicit_flags;
+        for (size_t c = 0; c < m["columnIdxs"].size(); ++c) s->col_idxs.push_back(m["columnIdxs"].at(c).as_i64());
+        if (s->col_idxs.empty())
+          for (size_t c = 0; c < it->second.types.size(); ++c) s->col_idxs.push_back(static_cast<int64_t>(c));
+        for (auto c : s->col_idxs) s->out_types.push_back(it->second.types.at(c));
+        sources.push_back(s.get());
+        node = std::move(s);
+      } else if (op.has("filterOp")) {
+        const Json& f = op["filterOp"];
+        auto n = std::make_unique<FilterNode>();
+        n->pred = ParseScalarExpr(f["expression"]);
+        for (size_t c = 0; c < f["columns"].size(); ++c) {
+          int64_t ci = f["columns"].at(c)["index"].as_i64();
+          n->selected.push_back(ci);
+          n->out_types.push_back(in.at(ci));
+        }
+        if (ExprType(n->pred, in) != BOOLEAN) throw Error(INVALID_ARGUMENT, "filter predicate must be BOOLEAN");
+        node = std::move(n);
+      } else if (op.has("mapOp")) {
+        const Json& m = op["mapOp"];
+        auto n = std::make_unique<MapNode>();
+        for (size_t c = 0; c < m["expressions"].size(); ++c) {
+          n->exprs.push_back(ParseScalarExpr(m["expressions"].at(c)));
+          n->out_types.push_back(ExprType(n->exprs.back(), in));
+        }
+        node = std::move(n);
+      } else if (op.has("aggOp")) {
+        const Json& a = op["aggOp"];
+        auto n = std::make_unique<AggNode>();
+        n->in_types = in;
+        n->windowed = a["windowed"].as_bool();
+        for (size_t g = 0; g < a["groups"].size(); ++g) n->groups.push_back(a["groups"].at(g)["index"].as_i64());
+        for (size_t v = 0; v < a["values"].size(); ++v) n->values.push_back(ParseAggExpr(a["values"].at(v)));
+        n->Init();
+        for (auto g : n->groups) n->out_types.push_back(in.at(g));
+        for (auto* d : n->defs) n->out_types.push_back(d->out);
+        node = std::move(n);
+      } else if (op.has("memSinkOp") || op.has("grpcSinkOp")) {
+        auto n = std::make_unique<SinkNode>();
+        if (op.has("memSinkOp")) n->name = op["memSinkOp"]["name"].as_str();
+        else n->name = op["grpcSinkOp"]["outputTable"]["tableName"].as_str();
+        n->out_types = in;
+        sinks.push_back(n.get());
+        node = std::move(n);
+      } else {
+        throw Error(UNIMPLEMENTED, "operator not supported by the restatement");
+      }
+      for (size_t p = 0; p < parents[id].size(); ++p) {
+        nodes.at(parents[id][p])->children.push_back(node.get());
+        nodes.at(parents[id][p])->child_parent_index.push_back(p);
+      }
+      nodes[id] = std::move(node);
+    }
+  }
+
+  // ExecuteSources (exec_graph.cc:177-289): up to 10 consecutive GenerateNext per source.
+  void Execute() {
+    std::vector<SourceNode*> running = sources;
+    while (!running.empty()) {
+      std::vector<SourceNode*> still;
+      for (auto* s : running) {
+        for (int i = 0; i < 10 && !s->done; ++i) s->GenerateNext();
+        if (!s->done) still.push_back(s);
+      }
+      running = still;
+    }
+  }
+};
+
+static std::map<std::string, TableIn> ImportTables(int32_t ntables, const oracle_table* tables) {
+  std::map<std::string, TableIn> out;
+  for (int32_t t = 0; t < ntables; ++t) {
+    const oracle_table& ot = tables[t];
+    TableIn ti;
+    for (int32_t c = 0; c < ot.ncols; ++c) {
+      ti.names.push_back(ot.col_names ? ot.col_names[c] : std::to_string(c));
+      ti.types.push_back(static_cast<DT>(ot.col_types[c]));
+    }
+    for (int32_t b = 0; b < ot.nbatches; ++b) {
+      RowBatch rb;
+      for (int32_t c = 0; c < ot.ncols; ++c) {
+        const oracle_column& oc = ot.cols[static_cast<size_t>(b) * ot.ncols + c];
+        auto col = std::make_shared<Col>(static_cast<DT>(oc.type));
+        int64_t n = oc.length;
+        rb.num_rows = n;
+        switch (col->type) {
+          case BOOLEAN: col->b.assign(static_cast<const uint8_t*>(oc.values), static_cast<const uint8_t*>(oc.values) + n); break;
+          case INT64:
+          case TIME64NS: col->i.assign(static_cast<const int64_t*>(oc.values), static_cast<const int64_t*>(oc.values) + n); break;
+          case FLOAT64: col->f.assign(static_cast<const double*>(oc.values), static_cast<const double*>(oc.values) + n); break;
+          case UINT128: {
+            const uint64_t* p = static_cast<const uint64_t*>(oc.values);
+            for (int64_t r = 0; r < n; ++r) col->u.push_back(U128{p[2 * r], p[2 * r + 1]});
+            break;
+          }
+          case STRING:
+            col->s.reserve(n);
+            for (int64_t r = 0; r < n; ++r)
+              col->s.emplace_back(reinterpret_cast<const char*>(oc.data) + oc.offsets[r], oc.offsets[r + 1] - oc.offsets[r]);
+            break;
+          default: throw Error(INVALID_ARGUMENT, "bad column type");
+        }
+        rb.cols.push_back(col);
+      }
+      if (ot.batch_flags) {
+        rb.eow = (ot.batch_flags[b] & 1) != 0;
+        rb.eos = (ot.batch_flags[b] & 2) != 0;
+        ti.explicit_flags = true;
+      }
+      ti.batches.push_back(std::move(rb));
+    }
+    out[ot.name] = std::move(ti);
+  }
+  return out;
+}
+
+// PXRB serialization (parsed by tests/pxrb.py).
+struct Writer {
+  std::vector<uint8_t> buf;
+  template <typename T>
+  void put(T v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    buf.insert(buf.end(), p, p + sizeof(T));
+  }
+  void bytes(const void* p, size_t n) { buf.insert(buf.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n); }
+};
+
+static void WriteBatch(Writer* w, const RowBatch& rb) {
+  w->put<int64_t>(rb.num_rows);
+  w->put<uint8_t>(rb.eow);
+  w->put<uint8_t>(rb.eos);
+  w->put<uint16_t>(0);
+  w->put<uint32_t>(static_cast<uint32_t>(rb.cols.size()));
+  for (auto& c : rb.cols) {
+    w->put<int32_t>(c->type);
+    switch (c->type) {
+      case BOOLEAN: w->bytes(c->b.data(), c->b.size()); break;
+      case INT64:
+      case TIME64NS: w->bytes(c->i.data(), c->i.size() * 8); break;
+      case FLOAT64: w->bytes(c->f.data(), c->f.size() * 8); break;
+      case UINT128:
+        for (auto& u : c->u) { w->put(u.lo); w->put(u.hi); }
+        break;
+      case STRING: {
+        int32_t off = 0;
+        w->put<int32_t>(0);
+        for (auto& s : c->s) { off += static_cast<int32_t>(s.size()); w->put<int32_t>(off); }
+        for (auto& s : c->s) w->bytes(s.data(), s.size());
+        break;
+      }
+      default: break;
+    }
+  }
+}
+
+}  // namespace oracle
+
+using namespace oracle;
+
+static void SetErr(char* errbuf, int32_t errlen, const std::string& m) {
+  if (errbuf && errlen > 0) {
+    std::snprintf(errbuf, static_cast<size_t>(errlen), "%s", m.c_str());
+  }
+}
+
+extern "C" int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                       uint8_t** out, int64_t* out_len, char* errbuf, int32_t errlen) {
+  try {
+    Json plan = ParseJson(plan_json);
+    auto tbl = ImportTables(ntables, tables);
+    Graph g;
+    g.Build(plan, tbl);
+    g.Execute();
+    Writer w;
+    w.put<uint32_t>(0x42525850u);  // "PXRB"
+    w.put<uint32_t>(static_cast<uint32_t>(g.sinks.size()));
+    for (auto* s : g.sinks) {
+      w.put<uint32_t>(static_cast<uint32_t>(s->name.size()));
+      w.bytes(s->name.data(), s->name.size());
+      w.put<uint32_t>(static_cast<uint32_t>(s->batches.size()));
+      for (auto& rb : s->batches) WriteBatch(&w, rb);
+    }
+    *out_len = static_cast<int64_t>(w.buf.size());
+    *out = static_cast<uint8_t*>(std::malloc(w.buf.size()));
+    std::memcpy(*out, w.buf.data(), w.buf.size());
+    return OK;
+  } catch (const Error& e) {
+    SetErr(errbuf, errlen, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    SetErr(errbuf, errlen, e.what());
+    return INTERNAL;
+  }
+}
+
+extern "C" int32_t oracle_execute_plan_timed(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                             double* seconds, int64_t* out_rows, char* errbuf, int32_t errlen) {
+  try {
+    Json plan = ParseJson(plan_json);
+    auto tbl = ImportTables(ntables, tables);
+    Graph g;
+    g.Build(plan, tbl);
+    auto t0 = std::chrono::steady_clock::now();
+    g.Execute();
+    auto t1 = std::chrono::steady_clock::now();
+    *seconds = std::chrono::duration<double>(t1 - t0).count();
+    int64_t rows = 0;
+    for (auto* s : g.sinks)
+      for (auto& rb : s->batches) rows += rb.num_rows;
+    *out_rows = rows;
+    return OK;
+  } catch (const Error& e) {
+    SetErr(errbuf, errlen, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    SetErr(errbuf, errlen, e.what());
+    return INTERNAL;
+  }
+}
+
+extern "C" void oracle_free(uint8_t* p) { std::free(p); }
+
+static const double kQs[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
+
+extern "C" void oracle_tdigest_quantiles(const double* vals, int64_t n, double* out7) {
+  TDigest d(1000);
+  for (int64_t i = 0; i < n; ++i) d.add(vals[i]);
+  for (int k = 0; k < 7; ++k) out7[k] = d.quantile(kQs[k]);
+}
+
+extern "C" void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb, double* out7) {
+  TDigest d1(1000), d2(1000);
+  for (int64_t i = 0; i < na; ++i) d1.add(a[i]);
+  for (int64_t i = 0; i < nb; ++i) d2.add(b[i]);
+  d1.merge(&d2);
+  for (int k = 0; k < 7; ++k) out7[k] = d1.quantile(kQs[k]);
+}
+
+extern "C" int32_t oracle_quantiles_json(const double* vals, int64_t n, char* buf, int32_t buflen) {
+  TDigest d(1000);
+  for (int64_t i = 0; i < n; ++i) d.add(vals[i]);
+  std::string s = QuantilesJson(&d);
+  std::snprintf(buf, static_cast<size_t>(buflen), "%s", s.c_str());
+  return static_cast<int32_t>(s.size());
+}
+
+extern "C" double oracle_pluck_float64(const char* json, const char* key) {
+  // PluckAsFloat64UDF::Exec (json_ops.h:131-153): parse failure / non-object / missing key /
+  // null / non-double -> 0.0.  A JSON number is a "double" for rapidjson iff it has a '.' or an
+  // exponent.
+  try {
+    Json d = ParseJson(json);
+    if (d.kind != Json::kObject || !d.has(key)) return 0.0;
+    const Json& v = d[key];
+    if (v.kind != Json::kNumber) return 0.0;
+    if (v.num.find_first_of(".eE") == std::string::npos) return 0.0;
+    return std::strtod(v.num.c_str(), nullptr);
+  } catch (...) {
+    return 0.0;
+  }
+}

@@ -1,0 +1,67 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY.
+//
+// C ABI of the CPU restatement of Pixie Carnot's columnar hot path.  Only
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the product
+// (pixie_amd/, include/pxg.h) never links or calls it.  Restated reference files:
+//   src/carnot/exec/{filter_node.cc:78-171, map_node.cc:47-71, agg_node.cc:43-542,
+//   expression_evaluator.cc:61-342, row_tuple.h:71-252, memory_source_node.cc:92-124,
+//   exec_graph.cc:52-331}, src/carnot/udf/udf_wrapper.h:60-438,
+//   src/carnot/funcs/builtins/{math_ops.h, math_ops.cc:52-250, math_sketches.h:33-82,
+//   json_ops.h:131-153}, src/carnot/plan/{operators.cc:59-395, scalar_expression.cc:232-348}.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// One column of one RowBatch, Arrow-like layout (BOOLEAN: one byte per value; UINT128: 16 B
+// per value as {low u64, high u64}; STRING: int32 offsets[length+1] + bytes).
+typedef struct {
+  int32_t type;  // px.types.DataType
+  int64_t length;
+  const void* values;
+  const int32_t* offsets;
+  const uint8_t* data;
+} oracle_column;
+
+// A table as a sequence of RowBatches (batch-major: cols[b * ncols + c]).
+typedef struct {
+  const char* name;
+  int32_t ncols;
+  const char* const* col_names;
+  const int32_t* col_types;
+  int32_t nbatches;
+  const oracle_column* cols;
+  // Optional per-batch flags (bit0 eow, bit1 eos).  When given, the source emits exactly these
+  // flags (the reference's ExecNodeTester feeds batches with explicit eow/eos,
+  // src/carnot/exec/test_utils.h:319-480); otherwise MemorySourceNode semantics apply.
+  const uint8_t* batch_flags;
+} oracle_table;
+
+// Execute a planpb.Plan given in protobuf-JSON form over the given tables.  Result tables are
+// serialized into *out (PXRB format, see tests/pxrb.py) and released with oracle_free.
+// Returns a px.statuspb.Code; on error a message is written into errbuf.
+int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                            uint8_t** out, int64_t* out_len, char* errbuf, int32_t errlen);
+
+// Same, timing only the execution window (first GenerateNext .. last emit), in seconds.
+int32_t oracle_execute_plan_timed(const char* plan_json, int32_t ntables,
+                                  const oracle_table* tables, double* seconds, int64_t* out_rows,
+                                  char* errbuf, int32_t errlen);
+
+void oracle_free(uint8_t* p);
+
+// QuantilesUDA on a value sequence (math_sketches.h:36-54): out[7] = p01,p10,p25,p50,p75,p90,p99.
+void oracle_tdigest_quantiles(const double* vals, int64_t n, double* out7);
+// Two digests built from a and b, then merged (QuantilesUDA::Merge), then the quantiles.
+void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb,
+                                    double* out7);
+// The JSON string QuantilesUDA::Finalize would produce (rapidjson-compatible %.17g rendering).
+int32_t oracle_quantiles_json(const double* vals, int64_t n, char* buf, int32_t buflen);
+// pluck_float64 (json_ops.h:131-153).
+double oracle_pluck_float64(const char* json, const char* key);
+
+#ifdef __cplusplus
+}
+#endif

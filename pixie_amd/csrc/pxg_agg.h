@@ -1,0 +1,64 @@
+// Hash group-by aggregation (AggNode, src/carnot/exec/agg_node.cc:88-542) on MI355X.
+//
+// Design: the fused consume kernel evaluates the filter, the group-key hash and
+// the UDA argument expressions per row and appends one staging record (slot, values) per
+// selected row; group identity is a slot of a global open-addressing table whose 64-bit slot
+// words are only ever written by CAS and read by agent-scope atomic loads (no cross-workgroup
+// plain-data hand-off inside a launch).  Finalize sorts the staging by slot (stable LSD radix
+// sort), reduces each run (count/sum/mean/min/max) and builds each group's t-digest from its
+// sorted values (QuantilesUDA semantics).
+#pragma once
+
+#include "pxg_internal.h"
+
+namespace pxg {
+
+// Slot word layout: [63:33] tag (31 bits, never 0) | [32] kind | [31:0] ref.
+//   kind 0: ref = (chunk << 24) | local row of the table consumed by the current launch
+//   kind 1: ref = 8-byte word offset of the key record in the agg's key arena
+constexpr uint64_t kKindArena = 1ULL << 32;
+constexpr uint32_t kDeferredSlot = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t SlotTag(uint64_t h) { return static_cast<uint32_t>((h >> 33) | 1u) & 0x7FFFFFFFu; }
+__device__ __forceinline__ uint64_t MakeSlotWord(uint32_t tag, uint64_t kind, uint32_t ref) {
+  return (static_cast<uint64_t>(tag) << 33) | kind | ref;
+}
+
+enum ValKind : int32_t { kValProgram = 0, kValMinOf2 = 1 };
+
+struct AggPlanDev {
+  int32_t n_keys;
+  int32_t n_udas;
+  int32_t n_vals;
+  int32_t has_filter;
+  int32_t key_types[kMaxKeys];
+  int32_t uda_kind[kMaxUdas];
+  int32_t uda_val[kMaxUdas];   // staged stream index (-1: none)
+  int32_t uda_arg_type[kMaxUdas];
+  int64_t uda_init[kMaxUdas];   // init arg (MINSUM) or 0
+  int32_t val_kind[kMaxVals];
+  int32_t val_type[kMaxVals];   // result type of the stream (INT64/TIME64NS/FLOAT64/BOOLEAN)
+  int32_t col_types[kMaxCols];
+  DevProgram filter;
+  DevProgram keys[kMaxKeys];
+  DevProgram vals[kMaxVals];
+  DevProgram vals2[kMaxVals];
+};
+
+struct AggTableDev {
+  unsigned long long* slots;
+  uint32_t mask;
+  uint32_t limit;                 // inserts beyond this are deferred (table kept <= 50% full)
+  unsigned int* counters;         // [0] inserted, [1] new, [2] deferred
+  uint32_t* new_slots;
+  uint32_t* deferred;
+  const uint64_t* arena;
+};
+
+struct StageDev {
+  uint32_t* slot;
+  uint64_t* vals[kMaxVals];
+  unsigned long long* cursor;
+};
+
+}  // namespace pxg

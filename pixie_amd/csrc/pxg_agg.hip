@@ -1,0 +1,572 @@
+// Fused Filter -> Map -> BlockingAgg consume path, key arena publication and table growth.
+//
+// Reference loops replaced: filter predicate (filter_node.cc:135-153),
+// compaction (filter_node.cc:78-130), map UDF row loop (udf_wrapper.h:102-133), group-key
+// extraction + hash probe (agg_node.cc:209-271) and the per-row UDA value buffering
+// (agg_node.cc:258-268).  One launch streams every row of the table once.
+#include <algorithm>
+
+#include "pxg_agg_host.h"
+#include "pxg_keys.h"
+#include "pxg_program.h"
+#include "pxg_scan.h"
+
+namespace pxg {
+
+constexpr int kConsumeBlock = 256;
+constexpr int kConsumeTile = 4096;  // rows per workgroup tile (16 per thread)
+
+struct TileRange {
+  int64_t tile0;  // first tile index of this range
+  int64_t lo;     // local row range within the chunk
+  int64_t hi;
+  int32_t chunk;
+  int32_t pad;
+};
+
+__device__ __forceinline__ uint32_t FindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                                 const KeySet& keys, uint64_t h, uint32_t rowref, const AggTableDev& tab) {
+  const uint32_t tag = SlotTag(h);
+  uint32_t pos = static_cast<uint32_t>(h) & tab.mask;
+  for (uint32_t probe = 0; probe <= tab.mask; ++probe) {
+    unsigned long long w = __hip_atomic_load(&tab.slots[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 0) {
+      unsigned int ins = __hip_atomic_load(&tab.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ins >= tab.limit) return kDeferredSlot;
+      unsigned long long expected = 0;
+      const unsigned long long desired = MakeSlotWord(tag, 0, rowref);
+      if (__hip_atomic_compare_exchange_strong(&tab.slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        atomicAdd(&tab.counters[0], 1u);
+        const unsigned int k = atomicAdd(&tab.counters[1], 1u);
+        tab.new_slots[k] = pos;
+        return pos;
+      }
+      w = expected;
+    }
+    if (static_cast<uint32_t>(w >> 33) == tag) {
+      KeySet rep;
+      const uint32_t ref = static_cast<uint32_t>(w);
+      if (w & kKindArena) {
+        LoadKeysArena(plan, tab.arena + ref, rep);
+      } else {
+        LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), rep);
+      }
+      if (KeysEqual(plan, keys, rep)) return pos;
+    }
+    pos = (pos + 1) & tab.mask;
+  }
+  return kDeferredSlot;
+}
+
+__device__ __forceinline__ void ProcessRow(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                           const DevChunk& ch, uint32_t chunk_idx, int64_t local, const AggTableDev& tab,
+                                           const StageDev& stg, uint64_t pos) {
+  KeySet k;
+  LoadKeysRow(plan, ch, local, k);
+  const uint64_t h = HashKeys(plan, k);
+  const uint32_t rowref = (chunk_idx << kChunkShift) | static_cast<uint32_t>(local);
+  const uint32_t slot = FindOrInsert(plan, chunks, k, h, rowref, tab);
+  if (slot == kDeferredSlot) {
+    const unsigned int d = atomicAdd(&tab.counters[2], 1u);
+    tab.deferred[d] = rowref;
+  }
+  stg.slot[pos] = slot;
+  const int nv = plan->n_vals;
+  for (int v = 0; v < nv; ++v) {
+    uint64_t x;
+    if (plan->val_kind[v] == kValMinOf2) {
+      const int64_t a = static_cast<int64_t>(EvalProgram(&plan->vals[v], ch, local, plan->col_types).a);
+      const int64_t b = static_cast<int64_t>(EvalProgram(&plan->vals2[v], ch, local, plan->col_types).a);
+      x = static_cast<uint64_t>(a < b ? a : b);
+    } else {
+      x = EvalProgram(&plan->vals[v], ch, local, plan->col_types).a;
+    }
+    stg.vals[v][pos] = x;
+  }
+}
+
+// One workgroup per tile of 4096 rows (grid-stride).  Phase 1 evaluates the predicate with
+// coalesced column loads and compacts the passing rows into LDS with a wave ballot + popcount
+// prefix; phase 2 processes the compacted rows densely (all lanes busy regardless of
+// selectivity) and appends one staging record per row.
+__global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanDev* __restrict__ plan,
+                                                                  const DevChunk* __restrict__ chunks,
+                                                                  const TileRange* __restrict__ ranges, int nranges,
+                                                                  int64_t ntiles, AggTableDev tab, StageDev stg) {
+  __shared__ int32_t s_sel[kConsumeTile];
+  __shared__ int32_t s_n;
+  __shared__ unsigned long long s_base;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
+  for (int64_t t = bid; t < ntiles; t += gridDim.x) {
+    int ri = 0;
+    while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
+    const TileRange rg = ranges[ri];
+    const DevChunk& ch = chunks[rg.chunk];
+    const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
+    const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < kConsumeTile / kConsumeBlock; ++k) {
+      const int64_t r = row0 + k * kConsumeBlock + threadIdx.x;
+      bool pass = r < row1;
+      if (pass && plan->has_filter) pass = EvalProgram(&plan->filter, ch, r, plan->col_types).a != 0;
+      const unsigned long long m = __ballot(pass);
+      if (m) {
+        const int leader = __ffsll(static_cast<long long>(m)) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&s_n, __popcll(m));
+        base = __shfl(base, leader);
+        if (pass) s_sel[base + __popcll(m & lanemask_lt)] = static_cast<int32_t>(r - row0);
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    if (threadIdx.x == 0) s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(n));
+    __syncthreads();
+    const uint64_t base = s_base;
+    for (int i = threadIdx.x; i < n; i += kConsumeBlock)
+      ProcessRow(plan, chunks, ch, static_cast<uint32_t>(rg.chunk), row0 + s_sel[i], tab, stg, base + i);
+    __syncthreads();
+  }
+}
+
+// Re-process deferred rows (already past the filter) after the table grew.
+__global__ void __launch_bounds__(kConsumeBlock) AggConsumeListKernel(const AggPlanDev* __restrict__ plan,
+                                                                      const DevChunk* __restrict__ chunks,
+                                                                      const uint32_t* __restrict__ list, uint32_t n,
+                                                                      AggTableDev tab, StageDev stg) {
+  __shared__ unsigned long long s_base;
+  for (uint32_t t0 = blockIdx.x * kConsumeBlock; t0 < n; t0 += gridDim.x * kConsumeBlock) {
+    const uint32_t cnt = min(static_cast<uint32_t>(kConsumeBlock), n - t0);
+    if (threadIdx.x == 0) s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(cnt));
+    __syncthreads();
+    const uint32_t i = t0 + threadIdx.x;
+    if (threadIdx.x < cnt) {
+      const uint32_t ref = list[i];
+      const uint32_t c = ref >> kChunkShift;
+      ProcessRow(plan, chunks, chunks[c], c, static_cast<int64_t>(ref & (kChunkRows - 1)), tab, stg, s_base + threadIdx.x);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void AggPublishSizesKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                      const unsigned long long* __restrict__ slots, const uint32_t* __restrict__ new_slots,
+                                      uint32_t n, uint64_t* __restrict__ sizes) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long w = slots[new_slots[i]];
+  const uint32_t ref = static_cast<uint32_t>(w);
+  KeySet k;
+  LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
+  sizes[i] = KeyRecordWords(plan, k);
+}
+
+__global__ void AggPublishWriteKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                      unsigned long long* __restrict__ slots, const uint32_t* __restrict__ new_slots, uint32_t n,
+                                      const uint64_t* __restrict__ offs, uint64_t base, uint64_t* __restrict__ arena) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t pos = new_slots[i];
+  const unsigned long long w = slots[pos];
+  const uint32_t ref = static_cast<uint32_t>(w);
+  KeySet k;
+  LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
+  const uint64_t at = base + offs[i];
+  WriteKeyRecord(plan, k, arena + at);
+  slots[pos] = MakeSlotWord(static_cast<uint32_t>(w >> 33), kKindArena, static_cast<uint32_t>(at));
+}
+
+__global__ void AggRehashKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ old_slots,
+                                uint32_t old_cap, unsigned long long* __restrict__ new_slots, uint32_t new_mask,
+                                const uint64_t* __restrict__ arena, uint32_t* __restrict__ remap) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap) return;
+  const unsigned long long w = old_slots[i];
+  if (w == 0) return;
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
+  const uint64_t h = HashKeys(plan, k);
+  uint32_t p = static_cast<uint32_t>(h) & new_mask;
+  for (uint32_t probe = 0; probe <= new_mask; ++probe) {
+    unsigned long long expected = 0;
+    if (__hip_atomic_compare_exchange_strong(&new_slots[p], &expected, w, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      remap[i] = p;
+      return;
+    }
+    p = (p + 1) & new_mask;
+  }
+}
+
+__global__ void StageRemapKernel(uint32_t* __restrict__ slot, uint64_t n, const uint32_t* __restrict__ remap) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  if (s != kDeferredSlot) slot[i] = remap[s];
+}
+
+// ---------------------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------------------
+static uint32_t NextPow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return static_cast<uint32_t>(std::min<uint64_t>(p, uint64_t(1) << 31));
+}
+
+static AggTableDev TableDev(Agg* a, int defer_buf) {
+  AggTableDev t;
+  t.slots = a->slots.as<unsigned long long>();
+  t.mask = a->cap - 1;
+  t.limit = a->cap / 2;
+  t.counters = a->counters.as<unsigned int>();
+  t.new_slots = a->new_slots.as<uint32_t>();
+  t.deferred = a->deferred[defer_buf].as<uint32_t>();
+  t.arena = a->arena.as<uint64_t>();
+  return t;
+}
+
+static StageDev StageDevOf(Agg* a) {
+  StageDev s;
+  s.slot = a->st_slot.as<uint32_t>();
+  for (int v = 0; v < kMaxVals; ++v) s.vals[v] = v < a->n_vals ? a->st_val[v].as<uint64_t>() : nullptr;
+  s.cursor = reinterpret_cast<unsigned long long*>(a->counters.as<uint8_t>() + 16);
+  return s;
+}
+
+int32_t Agg::ReadCounters(uint32_t* c3, uint64_t* stage_cursor) {
+  uint8_t tmp[32];
+  PXG_HIP(hipMemcpyAsync(tmp, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  std::memcpy(c3, tmp, 12);
+  std::memcpy(stage_cursor, tmp + 16, 8);
+  return PXG_OK;
+}
+
+int32_t Agg::EnsureTable(uint32_t want) {
+  if (slots.p) return PXG_OK;
+  cap = want;
+  PXG_RETURN_IF_ERROR(slots.Alloc(static_cast<size_t>(cap) * 8));
+  PXG_HIP(hipMemsetAsync(slots.p, 0, static_cast<size_t>(cap) * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(new_slots.Alloc(static_cast<size_t>(cap) * 4));
+  return PXG_OK;
+}
+
+int32_t Agg::EnsureStage(uint64_t need) {
+  // Capacity is whatever the buffers hold now (finalize swaps in exactly-sized sort buffers).
+  st_cap = st_slot.bytes / 4;
+  for (int v = 0; v < n_vals; ++v) st_cap = std::min<uint64_t>(st_cap, st_val[v].bytes / 8);
+  if (need <= st_cap) return PXG_OK;
+  uint64_t c = std::max<uint64_t>(need, st_cap * 2);
+  PXG_RETURN_IF_ERROR(st_slot.Reserve(c * 4, st_n * 4, ctx->stream));
+  for (int v = 0; v < n_vals; ++v) PXG_RETURN_IF_ERROR(st_val[v].Reserve(c * 8, st_n * 8, ctx->stream));
+  st_cap = c;
+  return PXG_OK;
+}
+
+int32_t Agg::Grow(uint32_t new_cap) {
+  if (new_cap <= cap) return PXG_OK;
+  DevBuf ns;
+  PXG_RETURN_IF_ERROR(ns.Alloc(static_cast<size_t>(new_cap) * 8));
+  PXG_HIP(hipMemsetAsync(ns.p, 0, static_cast<size_t>(new_cap) * 8, ctx->stream));
+  DevBuf remap;
+  PXG_RETURN_IF_ERROR(remap.Alloc(static_cast<size_t>(cap) * 4));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_rehash", AggRehashKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), slots.as<const unsigned long long>(), cap,
+                             ns.as<unsigned long long>(), new_cap - 1, arena.as<const uint64_t>(), remap.as<uint32_t>()));
+  if (st_n > 0) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "stage_remap", StageRemapKernel, dim3(GridFor(static_cast<int64_t>(st_n), 256, 1 << 30)), dim3(256), 0,
+                               st_slot.as<uint32_t>(), st_n, remap.as<const uint32_t>()));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  slots = std::move(ns);
+  cap = new_cap;
+  PXG_RETURN_IF_ERROR(new_slots.Alloc(static_cast<size_t>(cap) * 4));
+  return PXG_OK;
+}
+
+int32_t Agg::PublishNew(Table* t, uint32_t n_new) {
+  if (n_new == 0) return PXG_OK;
+  // sizes -> exclusive scan -> reserve arena -> write records + flip slot words to kind 1.
+  const size_t sz_bytes = static_cast<size_t>(n_new + 1) * 8;
+  const size_t need = sz_bytes + 64 + ScanScratchBytes(n_new);
+  if (scratch.bytes < need) PXG_RETURN_IF_ERROR(scratch.Alloc(need));
+  uint64_t* sizes = scratch.as<uint64_t>();
+  uint64_t* total = reinterpret_cast<uint64_t*>(scratch.as<uint8_t>() + sz_bytes);
+  void* sc = scratch.as<uint8_t>() + sz_bytes + 64;
+  const DevChunk* chunks = t->d_chunks.as<const DevChunk>();
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_sizes", AggPublishSizesKernel, dim3(GridFor(n_new, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), chunks, slots.as<const unsigned long long>(),
+                             new_slots.as<const uint32_t>(), n_new, sizes));
+  PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, n_new, total, sc));
+  uint64_t words = 0;
+  PXG_HIP(hipMemcpyAsync(&words, total, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + 64, arena_words * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(n_new, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(),
+                             new_slots.as<const uint32_t>(), n_new, static_cast<const uint64_t*>(sizes), arena_words,
+                             arena.as<uint64_t>()));
+  arena_words += words;
+  if (arena_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  return PXG_OK;
+}
+
+static int32_t CheckTableTypes(const Agg& a, const Table& t) {
+  for (auto& cr : a.col_refs) {
+    if (cr.first >= t.ncols) return SetError(PXG_INVALID_ARGUMENT, "program references column %d; table has %d", cr.first, t.ncols);
+    if (t.types[cr.first] != cr.second)
+      return SetError(PXG_INVALID_ARGUMENT, "column %d has type %d; program expects %d", cr.first, t.types[cr.first], cr.second);
+  }
+  return PXG_OK;
+}
+
+int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
+  PXG_RETURN_IF_ERROR(CheckTableTypes(*this, *t));
+  PXG_RETURN_IF_ERROR(t->EnsureDeviceDescriptors());
+  if (t->chunks.size() > 255) return SetError(PXG_UNIMPLEMENTED, "tables are limited to 255 chunks per agg consume");
+  std::vector<TileRange> ranges;
+  int64_t ntiles = 0;
+  for (size_t c = 0; c < t->chunks.size(); ++c) {
+    const Chunk& ch = *t->chunks[c];
+    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
+    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
+    if (lo >= hi) continue;
+    TileRange r;
+    r.tile0 = ntiles;
+    r.lo = lo;
+    r.hi = hi;
+    r.chunk = static_cast<int32_t>(c);
+    r.pad = 0;
+    ranges.push_back(r);
+    ntiles += (hi - lo + kConsumeTile - 1) / kConsumeTile;
+  }
+  if (ranges.empty()) return PXG_OK;
+  const int64_t rows = end - begin;
+  PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
+  PXG_RETURN_IF_ERROR(deferred[0].Reserve(static_cast<size_t>(rows) * 4 + 16, 0, ctx->stream));
+  DevBuf d_ranges;
+  PXG_RETURN_IF_ERROR(d_ranges.Alloc(ranges.size() * sizeof(TileRange)));
+  PXG_HIP(hipMemcpy(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice));
+  PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 4, 0, 8, ctx->stream));  // new, deferred
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", AggConsumeKernel, dim3(grid), dim3(kConsumeBlock), 0,
+                             d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
+                             static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this)));
+  uint32_t c3[3];
+  PXG_RETURN_IF_ERROR(ReadCounters(c3, &st_n));
+  inserted = c3[0];
+  PXG_RETURN_IF_ERROR(PublishNew(t, c3[1]));
+  uint32_t n_def = c3[2];
+  int buf = 0;
+  while (n_def > 0) {
+    PXG_RETURN_IF_ERROR(Grow(NextPow2(4 * (static_cast<uint64_t>(inserted) + n_def))));
+    PXG_RETURN_IF_ERROR(deferred[1 - buf].Reserve(static_cast<size_t>(n_def) * 4 + 16, 0, ctx->stream));
+    PXG_RETURN_IF_ERROR(EnsureStage(st_n + n_def));
+    PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 4, 0, 8, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume_list", AggConsumeListKernel, dim3(GridFor(n_def, kConsumeBlock, ctx->num_cus * 8)),
+                               dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(),
+                               deferred[buf].as<const uint32_t>(), n_def, TableDev(this, 1 - buf), StageDevOf(this)));
+    PXG_RETURN_IF_ERROR(ReadCounters(c3, &st_n));
+    inserted = c3[0];
+    PXG_RETURN_IF_ERROR(PublishNew(t, c3[1]));
+    n_def = c3[2];
+    buf = 1 - buf;
+  }
+  // Keep the table at most ~37% full for the next consume.
+  if (inserted > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(static_cast<uint64_t>(inserted) * 4)));
+  return PXG_OK;
+}
+
+}  // namespace pxg
+
+using namespace pxg;
+
+// ---------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------
+static void CollectColRefs(const pxg_program& p, std::vector<std::pair<int32_t, int32_t>>* refs) {
+  for (int i = 0; i < p.n_insns; ++i)
+    if (p.insns[i].op == PXG_OP_COL) refs->push_back({p.insns[i].arg, p.insns[i].type});
+}
+
+static bool SameProgram(const pxg_program& a, const pxg_program& b) {
+  if (a.n_insns != b.n_insns || a.result_type != b.result_type || a.pool_len != b.pool_len) return false;
+  for (int i = 0; i < a.n_insns; ++i) {
+    const pxg_insn &x = a.insns[i], &y = b.insns[i];
+    if (x.op != y.op || x.type != y.type || x.arg != y.arg || x.imm != y.imm) return false;
+  }
+  return a.pool_len == 0 || std::memcmp(a.pool, b.pool, a.pool_len) == 0;
+}
+
+static int32_t UdaOutType(int kind, int arg_type) {
+  switch (kind) {
+    case PXG_UDA_COUNT: return PXG_INT64;
+    case PXG_UDA_SUM: return arg_type == PXG_FLOAT64 ? PXG_FLOAT64 : PXG_INT64;
+    case PXG_UDA_MEAN: return PXG_FLOAT64;
+    case PXG_UDA_MIN:
+    case PXG_UDA_MAX: return arg_type;
+    case PXG_UDA_QUANTILES: return PXG_FLOAT64;
+    case PXG_UDA_MINSUM: return PXG_INT64;
+    default: return PXG_DATA_TYPE_UNKNOWN;
+  }
+}
+
+// Device UDA registry: (kind, arg type) signatures supported on the device, mirroring the
+// builtin registrations (math_ops.cc:228-250, math_sketches.cc:25-28).
+static bool UdaSupported(int kind, int arg) {
+  switch (kind) {
+    case PXG_UDA_COUNT: return arg >= PXG_BOOLEAN && arg <= PXG_TIME64NS;
+    case PXG_UDA_SUM: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_BOOLEAN;
+    case PXG_UDA_MEAN: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_BOOLEAN;
+    case PXG_UDA_MIN:
+    case PXG_UDA_MAX: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_TIME64NS;
+    case PXG_UDA_QUANTILES: return arg == PXG_FLOAT64 || arg == PXG_INT64;
+    case PXG_UDA_MINSUM: return arg == PXG_INT64;
+    default: return false;
+  }
+}
+
+extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_agg** out) {
+  if (!ctx || !spec || !out) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  if (spec->n_keys < 0 || spec->n_keys > kMaxKeys) return SetError(PXG_UNIMPLEMENTED, "at most %d group keys", kMaxKeys);
+  if (spec->n_udas < 0 || spec->n_udas > kMaxUdas) return SetError(PXG_UNIMPLEMENTED, "at most %d aggregate expressions", kMaxUdas);
+  auto holder = std::make_unique<pxg_agg>();
+  Agg& a = holder->impl;
+  a.ctx = &ctx->impl;
+  a.n_keys = spec->n_keys;
+  a.n_udas = spec->n_udas;
+  a.windowed = spec->windowed != 0;
+  a.has_filter = spec->filter != nullptr;
+  std::memset(&a.hplan, 0, sizeof(a.hplan));
+  std::vector<uint8_t> pool;
+  std::vector<std::pair<DevProgram*, size_t>> pool_fix;
+  size_t off = 0;
+  a.hplan.n_keys = a.n_keys;
+  a.hplan.n_udas = a.n_udas;
+  a.hplan.has_filter = a.has_filter ? 1 : 0;
+  if (a.has_filter) {
+    if (spec->filter->result_type != PXG_BOOLEAN) return SetError(PXG_INVALID_ARGUMENT, "filter must be BOOLEAN");
+    PXG_RETURN_IF_ERROR(CompileProgram(*spec->filter, nullptr, kMaxCols, &a.hplan.filter, &pool, &off));
+    pool_fix.push_back({&a.hplan.filter, off});
+    CollectColRefs(*spec->filter, &a.col_refs);
+  }
+  for (int k = 0; k < a.n_keys; ++k) {
+    const pxg_program& p = spec->keys[k];
+    if (p.result_type == PXG_STRING && !(p.n_insns == 1 && p.insns && p.insns[0].op == PXG_OP_COL))
+      return SetError(PXG_UNIMPLEMENTED, "computed STRING group keys are not supported on device");
+    PXG_RETURN_IF_ERROR(CompileProgram(p, nullptr, kMaxCols, &a.hplan.keys[k], &pool, &off));
+    pool_fix.push_back({&a.hplan.keys[k], off});
+    a.hplan.key_types[k] = p.result_type;
+    a.key_types.push_back(p.result_type);
+    CollectColRefs(p, &a.col_refs);
+  }
+  std::vector<const pxg_program*> val_progs, val_progs2;
+  std::vector<int> val_kinds;
+  for (int u = 0; u < a.n_udas; ++u) {
+    const pxg_uda_spec& us = spec->udas[u];
+    if (!UdaSupported(us.kind, us.arg_type)) return SetError(PXG_UNIMPLEMENTED, "UDA kind %d with arg type %d has no device implementation", us.kind, us.arg_type);
+    a.uda_kind.push_back(us.kind);
+    a.uda_arg_type.push_back(us.arg_type);
+    a.uda_out_type.push_back(UdaOutType(us.kind, us.arg_type));
+    a.uda_init.push_back(us.init_i64);
+    a.uda_has_init.push_back(us.has_init);
+    int vi = -1;
+    if (us.kind != PXG_UDA_COUNT) {
+      if (us.arg.result_type != us.arg_type) return SetError(PXG_INVALID_ARGUMENT, "UDA %d arg type mismatch", u);
+      const int vk = us.kind == PXG_UDA_MINSUM ? kValMinOf2 : kValProgram;
+      for (size_t j = 0; j < val_progs.size(); ++j) {
+        if (val_kinds[j] == vk && SameProgram(*val_progs[j], us.arg) &&
+            (vk != kValMinOf2 || SameProgram(*val_progs2[j], us.arg2))) {
+          vi = static_cast<int>(j);
+          break;
+        }
+      }
+      if (vi < 0) {
+        if (static_cast<int>(val_progs.size()) >= kMaxVals) return SetError(PXG_UNIMPLEMENTED, "too many distinct UDA arguments");
+        vi = static_cast<int>(val_progs.size());
+        val_progs.push_back(&us.arg);
+        val_progs2.push_back(&us.arg2);
+        val_kinds.push_back(vk);
+        a.val_type.push_back(us.arg_type);
+      }
+    }
+    a.uda_val.push_back(vi);
+    a.hplan.uda_kind[u] = us.kind;
+    a.hplan.uda_val[u] = vi;
+    a.hplan.uda_arg_type[u] = us.arg_type;
+    a.hplan.uda_init[u] = us.has_init ? us.init_i64 : 0;
+  }
+  a.n_vals = static_cast<int32_t>(val_progs.size());
+  a.hplan.n_vals = a.n_vals;
+  for (int v = 0; v < a.n_vals; ++v) {
+    a.hplan.val_kind[v] = val_kinds[v];
+    a.hplan.val_type[v] = a.val_type[v];
+    PXG_RETURN_IF_ERROR(CompileProgram(*val_progs[v], nullptr, kMaxCols, &a.hplan.vals[v], &pool, &off));
+    pool_fix.push_back({&a.hplan.vals[v], off});
+    CollectColRefs(*val_progs[v], &a.col_refs);
+    if (val_kinds[v] == kValMinOf2) {
+      PXG_RETURN_IF_ERROR(CompileProgram(*val_progs2[v], nullptr, kMaxCols, &a.hplan.vals2[v], &pool, &off));
+      pool_fix.push_back({&a.hplan.vals2[v], off});
+      CollectColRefs(*val_progs2[v], &a.col_refs);
+    }
+  }
+  for (auto& cr : a.col_refs) {
+    if (cr.first < 0 || cr.first >= kMaxCols) return SetError(PXG_INVALID_ARGUMENT, "column index %d out of range", cr.first);
+    a.hplan.col_types[cr.first] = cr.second;
+  }
+  PXG_RETURN_IF_ERROR(a.d_pool.Alloc(pool.size() + 16));
+  if (!pool.empty()) PXG_HIP(hipMemcpy(a.d_pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
+  for (auto& pf : pool_fix) pf.first->pool = a.d_pool.as<uint8_t>() + pf.second;
+  PXG_RETURN_IF_ERROR(a.d_plan.Alloc(sizeof(AggPlanDev)));
+  PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));
+  PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
+  PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
+  const int64_t expected = spec->expected_groups > 0 ? spec->expected_groups : 4096;
+  PXG_RETURN_IF_ERROR(a.EnsureTable(NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 4, 1024))));
+  PXG_RETURN_IF_ERROR(a.arena.Alloc(1 << 16));
+  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  *out = holder.release();
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_destroy(pxg_agg* agg) {
+  if (!agg) return PXG_OK;
+  hipStreamSynchronize(agg->impl.ctx->stream);
+  delete agg;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin, int64_t end) {
+  if (!agg || !table) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Table& t = table->impl;
+  PXG_RETURN_IF_ERROR(t.FlushStage());
+  if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "row range [%lld,%lld) outside table of %lld rows", (long long)begin, (long long)end, (long long)t.nrows);
+  if (t.ctx != agg->impl.ctx) return SetError(PXG_INVALID_ARGUMENT, "table and agg belong to different contexts");
+  agg->impl.res.ready = false;
+  return agg->impl.ConsumeRange(&t, begin, end);
+}
+
+extern "C" int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows) {
+  if (!agg || !rows) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  *rows = static_cast<int64_t>(agg->impl.st_n);
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
+  if (!agg) return SetError(PXG_INVALID_ARGUMENT, "agg is null");
+  Agg& a = agg->impl;
+  PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
+  PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
+  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  a.st_n = 0;
+  a.arena_words = 0;
+  a.inserted = 0;
+  a.res = AggResult();
+  return PXG_OK;
+}

@@ -1,0 +1,74 @@
+// Host-side state of one aggregation (pxg_agg).
+#pragma once
+
+#include <vector>
+
+#include "pxg_agg.h"
+
+namespace pxg {
+
+struct AggResult {
+  int64_t n_groups = 0;
+  bool ready = false;
+  // device outputs (dense by group)
+  DevBuf key_fixed[kMaxKeys];   // 8 or 16 B per group
+  DevBuf key_offsets[kMaxKeys]; // STRING: int32 offsets (n+1)
+  DevBuf key_data[kMaxKeys];
+  int64_t key_data_len[kMaxKeys] = {0};
+  DevBuf uda_out[kMaxUdas];     // 8 B per group (QUANTILES: 7 doubles per group)
+};
+
+struct Agg {
+  Ctx* ctx = nullptr;
+  int32_t n_keys = 0, n_udas = 0, n_vals = 0;
+  bool windowed = false;
+  bool has_filter = false;
+  std::vector<int32_t> uda_kind, uda_arg_type, uda_val, uda_out_type;
+  std::vector<int64_t> uda_init;
+  std::vector<int32_t> uda_has_init;
+  std::vector<int32_t> key_types;
+  std::vector<int32_t> val_type;
+  // Programs reference input columns by index/type; checked against each consumed table.
+  std::vector<std::pair<int32_t, int32_t>> col_refs;  // (col, type)
+
+  AggPlanDev hplan;
+  DevBuf d_plan;
+  DevBuf d_pool;
+
+  // Global open-addressing table.
+  DevBuf slots;
+  uint32_t cap = 0;
+  DevBuf counters;  // u32 [0] inserted [1] new [2] deferred [3] pad ; u64 [2] stage cursor [3] arena cursor
+  DevBuf new_slots;
+  DevBuf deferred[2];
+  DevBuf arena;
+  uint64_t arena_words = 0;  // used (host mirror after publish)
+  uint64_t inserted = 0;     // host mirror
+
+  // Staging (one record per selected row).
+  DevBuf st_slot;
+  DevBuf st_val[kMaxVals];
+  uint64_t st_cap = 0;
+  uint64_t st_n = 0;  // host mirror of the cursor
+
+  AggResult res;
+  DevBuf scratch;
+
+  int32_t EnsureTable(uint32_t new_cap);
+  int32_t EnsureStage(uint64_t need);
+  int32_t Grow(uint32_t new_cap);
+  int32_t PublishNew(Table* t, uint32_t n_new);
+  int32_t ConsumeRange(Table* t, int64_t begin, int64_t end);
+  int32_t ConsumeList(Table* t, const uint32_t* list, uint32_t n);
+  int32_t Finalize();
+  int32_t ReadCounters(uint32_t* c3, uint64_t* stage_cursor);
+};
+
+// Finalize stages (pxg_finalize.hip).
+int32_t AggFinalizeImpl(Agg* agg);
+
+}  // namespace pxg
+
+struct pxg_agg {
+  pxg::Agg impl;
+};

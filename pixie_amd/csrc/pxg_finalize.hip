@@ -1,0 +1,810 @@
+// Agg finalize: group the staging records by slot (stable LSD radix sort), reduce each group
+// (ConvertAggHashMapToRowBatch + UDA Finalize, agg_node.cc:303-349), build quantile digests and
+// extract the group keys from the arena.
+#include <algorithm>
+
+#include "pxg_agg_host.h"
+#include "pxg_keys.h"
+#include "pxg_scan.h"
+#include "pxg_tdigest.h"
+
+namespace pxg {
+
+constexpr int kRadixBlock = 256;
+constexpr int kRadixItems = 16;
+constexpr int kRadixTile = kRadixBlock * kRadixItems;
+constexpr int kRadixBits = 8;
+constexpr int kRadixBuckets = 1 << kRadixBits;
+
+struct ValPtrs {
+  uint64_t* p[kMaxVals];
+};
+struct ConstValPtrs {
+  const uint64_t* p[kMaxVals];
+};
+
+__global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t cap,
+                                                               int shift, uint32_t* __restrict__ hist, uint32_t nblocks) {
+  __shared__ uint32_t h[4][kRadixBuckets];
+  uint32_t* hf = &h[0][0];
+  for (int i = threadIdx.x; i < 4 * kRadixBuckets; i += kRadixBlock) hf[i] = 0;
+  __syncthreads();
+  const int wid = threadIdx.x >> 6;
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+#pragma unroll 4
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    if (i < n) {
+      const uint32_t key = min(keys[i], cap);
+      atomicAdd(&h[wid][(key >> shift) & (kRadixBuckets - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  const int d = threadIdx.x;
+  hist[static_cast<uint64_t>(d) * nblocks + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+}
+
+// Stable scatter: items of a tile keep their relative order within each digit.  Ranks within
+// a wave come from an 8-ballot match of the digit bits; waves are ordered through LDS counts.
+__global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
+                                                                  ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n,
+                                                                  uint32_t cap, int shift, const uint32_t* __restrict__ offs,
+                                                                  uint32_t nblocks) {
+  __shared__ uint32_t running[kRadixBuckets];
+  __shared__ uint32_t wcnt[4][kRadixBuckets];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  running[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * nblocks + blockIdx.x];
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  for (int k = 0; k < kRadixItems; ++k) {
+    uint32_t* wf = &wcnt[0][0];
+    for (int i = threadIdx.x; i < 4 * kRadixBuckets; i += kRadixBlock) wf[i] = 0;
+    __syncthreads();
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t key = valid ? kin[i] : 0u;
+    const uint32_t d = (min(key, cap) >> shift) & (kRadixBuckets - 1);
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRadixBits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(valid && bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t rank = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
+    if (valid && rank == 0) wcnt[wid][d] = static_cast<uint32_t>(__popcll(peers));
+    __syncthreads();
+    if (valid) {
+      uint32_t pre = 0;
+      for (int w = 0; w < wid; ++w) pre += wcnt[w][d];
+      const uint32_t pos = running[d] + pre + rank;
+      kout[pos] = key;
+      for (int v = 0; v < nvals; ++v) vout.p[v][pos] = vin.p[v][i];
+    }
+    __syncthreads();
+    running[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+    __syncthreads();
+  }
+}
+
+__global__ void RunHeadsKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t cap, uint32_t* __restrict__ flags,
+                               unsigned long long* __restrict__ n_valid) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = min(keys[i], cap);
+  const uint32_t prev = i ? min(keys[i - 1], cap) : 0xFFFFFFFFu;
+  flags[i] = (k < cap && k != prev) ? 1u : 0u;
+  if (k == cap && prev != cap) *n_valid = i;
+}
+
+__global__ void GroupStartsKernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ flags,
+                                  const uint32_t* __restrict__ gidx, uint64_t n, uint32_t* __restrict__ gstart,
+                                  uint32_t* __restrict__ gslot, const unsigned long long* __restrict__ n_valid, uint32_t ngroups) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i == 0) gstart[ngroups] = static_cast<uint32_t>(*n_valid);
+  if (i >= n) return;
+  if (flags[i]) {
+    const uint32_t g = gidx[i];
+    gstart[g] = static_cast<uint32_t>(i);
+    gslot[g] = keys[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-group UDA reductions (one wave per group).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t WaveSumU64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double WaveSumF64(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int64_t WaveMinI64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t x = __shfl_xor(v, o, 64);
+    v = x < v ? x : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t WaveMaxI64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t x = __shfl_xor(v, o, 64);
+    v = x > v ? x : v;
+  }
+  return v;
+}
+
+struct UdaOut {
+  uint64_t* p[kMaxUdas];
+};
+
+__global__ void __launch_bounds__(256) UdaReduceKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
+                                                       uint32_t ngroups, ConstValPtrs vals, UdaOut out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t g = wave; g < ngroups; g += nwaves) {
+    const uint32_t s = gstart[g], e = gstart[g + 1];
+    const uint64_t cnt = e - s;
+    for (int u = 0; u < plan->n_udas; ++u) {
+      const int kind = plan->uda_kind[u];
+      const int at = plan->uda_arg_type[u];
+      const int vi = plan->uda_val[u];
+      const uint64_t* v = vi >= 0 ? vals.p[vi] : nullptr;
+      uint64_t r = 0;
+      switch (kind) {
+        case PXG_UDA_COUNT: r = cnt; break;
+        case PXG_UDA_SUM:
+        case PXG_UDA_MINSUM:
+          if (at == PXG_FLOAT64) {
+            double acc = 0;
+            for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
+            r = FBits(WaveSumF64(acc));
+          } else {
+            uint64_t acc = 0;
+            for (uint32_t i = s + lane; i < e; i += 64) acc += v[i];
+            r = WaveSumU64(acc) + static_cast<uint64_t>(plan->uda_init[u]);
+          }
+          break;
+        case PXG_UDA_MEAN: {
+          double acc = 0;
+          if (at == PXG_FLOAT64) {
+            for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
+          } else {
+            for (uint32_t i = s + lane; i < e; i += 64) acc += static_cast<double>(static_cast<int64_t>(v[i]));
+          }
+          r = FBits(WaveSumF64(acc) / static_cast<double>(cnt));
+          break;
+        }
+        case PXG_UDA_MAX:
+          if (at == PXG_FLOAT64) {
+            int64_t m = OrderedFromDouble(FBits(kDblMin));  // MaxUDA init numeric_limits<double>::min()
+            for (uint32_t i = s + lane; i < e; i += 64) {
+              const uint64_t x = v[i];
+              if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o > m ? o : m; }
+            }
+            r = DoubleFromOrdered(WaveMaxI64(m));
+          } else {
+            int64_t m = INT64_MIN;
+            for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x > m ? x : m; }
+            r = static_cast<uint64_t>(WaveMaxI64(m));
+          }
+          break;
+        case PXG_UDA_MIN:
+          if (at == PXG_FLOAT64) {
+            int64_t m = OrderedFromDouble(FBits(kDblMax));
+            for (uint32_t i = s + lane; i < e; i += 64) {
+              const uint64_t x = v[i];
+              if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o < m ? o : m; }
+            }
+            r = DoubleFromOrdered(WaveMinI64(m));
+          } else {
+            int64_t m = INT64_MAX;
+            for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x < m ? x : m; }
+            r = static_cast<uint64_t>(WaveMinI64(m));
+          }
+          break;
+        default: continue;  // QUANTILES handled by the digest kernels
+      }
+      if (lane == 0) out.p[u][g] = r;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Quantiles.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t QKey(uint64_t raw, int arg_type) {
+  const uint64_t bits = arg_type == PXG_FLOAT64 ? raw : FBits(static_cast<double>(static_cast<int64_t>(raw)));
+  return SortKeyF(bits);
+}
+__device__ __forceinline__ double QVal(uint64_t key) { return AsF(FromSortKeyF(key)); }
+
+constexpr uint64_t kNegInfKey = 0x000FFFFFFFFFFFFFULL;  // SortKeyF(-inf) = ~0xFFF0... = 0x000F...F
+constexpr uint64_t kPosInfKey = 0xFFF0000000000000ULL;  // SortKeyF(+inf) = 0x7FF0... ^ 0x8000...
+
+__global__ void ClassifyGroupsKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups, uint32_t* __restrict__ lists,
+                                     uint32_t* __restrict__ counts, uint32_t tiny_max, uint32_t mid_max) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const uint32_t n = gstart[g + 1] - gstart[g];
+  const int cls = n <= tiny_max ? 0 : (n <= mid_max ? 1 : 2);
+  const uint32_t k = atomicAdd(&counts[cls], 1u);
+  lists[static_cast<uint64_t>(cls) * ngroups + k] = g;
+}
+
+__device__ __forceinline__ uint64_t BitonicStepWave(uint64_t x, int lane, int k, int j) {
+  const uint64_t y = __shfl_xor(x, j, 64);
+  const bool up = (lane & k) == 0;
+  const bool lower = (lane & j) == 0;
+  const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+  return (lower == up) ? mn : mx;
+}
+
+// One wave per group with n <= 64: register bitonic sort, singleton digest.
+__global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restrict__ list, uint32_t nlist,
+                                                       const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
+                                                       int arg_type, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t li = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (li >= nlist) return;
+  const uint32_t g = list[li];
+  const uint32_t s = gstart[g], n = gstart[g + 1] - s;
+  uint64_t key = lane < static_cast<int>(n) ? QKey(vals[s + lane], arg_type) : ~0ULL;
+  for (int k = 2; k <= 64; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) key = BitonicStepWave(key, lane, k, j);
+  const bool valid = lane < static_cast<int>(n) && key >= kNegInfKey && key <= kPosInfKey;
+  const bool neg_nan = lane < static_cast<int>(n) && key < kNegInfKey;
+  const uint32_t lead = static_cast<uint32_t>(__popcll(__ballot(neg_nan)));
+  const int64_t W = __popcll(__ballot(valid));
+  double q = lane < 7 ? kQuantileQ[lane] : 0.0;
+  // Every lane participates in the shuffles the value accessor performs.
+  double res = 0;
+  if (W == 0) {
+    res = __longlong_as_double(0x7FF8000000000000LL);
+  } else {
+    auto val = [&](int64_t j) -> double { return QVal(__shfl(key, static_cast<int>(lead + j), 64)); };
+    // Uniform-control version of SingletonQuantile: every lane evaluates with its own q.
+    const double Wd = static_cast<double>(W);
+    const double index = q * Wd;
+    const double v0 = val(0);
+    const double vlast = val(W - 1);
+    const double mn = StdMin(kDblMax, v0);
+    const double mx = StdMax(kDblMin, vlast);
+    // lower_bound over cum(j) = j + 0.5 (j < W), cum(W) = W
+    int64_t j = 0;
+    if (index > W - 0.5) j = W;
+    else { j = static_cast<int64_t>(ceil(index - 0.5)); if (j < 0) j = 0; }
+    const int64_t jm1 = j > 0 ? j - 1 : 0;
+    const int64_t jj = j < W ? j : W - 1;
+    const double vjm1 = val(jm1);
+    const double vj = val(jj);
+    if (W == 1) {
+      res = v0;
+    } else if (index <= 0.5) {
+      res = mn + 2.0 * index / 1.0 * (v0 - mn);
+    } else if (j < W) {
+      const double z1 = index - (static_cast<double>(j - 1) + 0.5);
+      const double z2 = (static_cast<double>(j) + 0.5) - index;
+      res = WeightedAverage(vjm1, z2, vj, z1);
+    } else {
+      const double z1 = index - Wd - 1.0 / 2.0;
+      const double z2 = 1.0 / 2 - z1;
+      res = WeightedAverage(vlast, z1, mx, z2);
+    }
+  }
+  if (lane < 7) out[static_cast<uint64_t>(g) * 7 + lane] = res;
+}
+
+constexpr int kMidMax = 4096;
+constexpr int kMidCentroids = 2048;
+
+__device__ __forceinline__ void BitonicSortLds(uint64_t* a, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Lower bound of `key` in sorted a[0, n).
+template <typename Acc>
+__device__ __forceinline__ int64_t LowerBoundKey(Acc a, int64_t n, uint64_t key) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a(mid) < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Digest of a sorted key array accessible through `keyat` (block-cooperative).
+template <typename KeyAt>
+__device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, double* means, int64_t max_c, double* out7,
+                            unsigned int* err, int64_t* s_meta) {
+  // trim NaNs: keys < kNegInfKey (negative NaN) at the front, > kPosInfKey at the back
+  if (threadIdx.x == 0) {
+    const int64_t lead = LowerBoundKey(keyat, n, kNegInfKey);
+    const int64_t tail = LowerBoundKey(keyat, n, kPosInfKey + 1);
+    s_meta[0] = lead;
+    s_meta[1] = tail - lead;
+  }
+  __syncthreads();
+  const int64_t lead = s_meta[0], W = s_meta[1];
+  auto val = [&](int64_t j) -> double { return QVal(keyat(lead + j)); };
+  if (W <= kSingletonMaxW) {
+    if (threadIdx.x < 7) out7[threadIdx.x] = W == 0 ? __longlong_as_double(0x7FF8000000000000LL) : SingletonQuantile(kQuantileQ[threadIdx.x], W, val);
+    __syncthreads();
+    return;
+  }
+  if (threadIdx.x == 0) {
+    const int64_t nc = DigestBoundaries(W, starts, max_c);
+    if (nc < 0) atomicExch(err, 1u);
+    s_meta[2] = nc < 0 ? 0 : nc;
+  }
+  __syncthreads();
+  const int64_t nc = s_meta[2];
+  for (int64_t j = threadIdx.x; j < nc; j += blockDim.x) {
+    const int64_t st = starts[j], en = j + 1 < nc ? starts[j + 1] : W;
+    means[j] = CentroidMean(val, st, en);
+  }
+  __syncthreads();
+  if (threadIdx.x < 7) {
+    out7[threadIdx.x] = DigestQuantile(
+        kQuantileQ[threadIdx.x], nc, W, [&](int64_t j) -> int64_t { return starts[j]; }, [&](int64_t j) -> double { return means[j]; });
+  }
+  __syncthreads();
+}
+
+// One workgroup per group with 64 < n <= 4096: LDS bitonic sort + digest.
+__global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
+                                                      const uint64_t* __restrict__ vals, int arg_type, double* __restrict__ out,
+                                                      unsigned int* __restrict__ err) {
+  __shared__ uint64_t keys[kMidMax];
+  __shared__ uint32_t starts[kMidCentroids];
+  __shared__ double means[kMidCentroids];
+  __shared__ int64_t meta[4];
+  const uint32_t g = list[blockIdx.x];
+  const uint32_t s = gstart[g], n = gstart[g + 1] - s;
+  int P = 64;
+  while (P < static_cast<int>(n)) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) keys[i] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
+  __syncthreads();
+  BitonicSortLds(keys, P);
+  BlockDigest([&](int64_t i) -> uint64_t { return keys[i]; }, n, starts, means, kMidCentroids, out + static_cast<uint64_t>(g) * 7, err,
+              meta);
+}
+
+// Big groups: chunk sort (one workgroup per 4096-element chunk) into sort keys.
+struct BigChunk {
+  uint64_t off;  // absolute staging offset
+  uint32_t len;
+  uint32_t pad;
+};
+
+__global__ void __launch_bounds__(256) BigChunkSortKernel(const BigChunk* __restrict__ chunks, const uint64_t* __restrict__ vals,
+                                                          int arg_type, uint64_t* __restrict__ outk) {
+  __shared__ uint64_t keys[kMidMax];
+  const BigChunk c = chunks[blockIdx.x];
+  for (int i = threadIdx.x; i < kMidMax; i += blockDim.x) keys[i] = i < static_cast<int>(c.len) ? QKey(vals[c.off + i], arg_type) : ~0ULL;
+  __syncthreads();
+  BitonicSortLds(keys, kMidMax);
+  for (int i = threadIdx.x; i < static_cast<int>(c.len); i += blockDim.x) outk[c.off + i] = keys[i];
+}
+
+struct BigGroup {
+  uint64_t off;     // absolute staging offset of the group
+  uint64_t n;
+  uint64_t eoff;    // prefix of element counts (for the flattened launch)
+  uint32_t g;
+  uint32_t pad;
+};
+
+// One merge pass: runs of width w inside every big group are merged pairwise (stable).
+__global__ void BigMergeKernel(const BigGroup* __restrict__ groups, uint32_t ngroups, uint64_t total,
+                               const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t w) {
+  const uint64_t e = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  uint32_t lo = 0, hi = ngroups;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (groups[mid].eoff <= e) lo = mid;
+    else hi = mid;
+  }
+  const BigGroup G = groups[lo];
+  const uint64_t j = e - G.eoff;
+  const uint64_t r = j / w;
+  const uint64_t pr = r ^ 1;
+  const uint64_t base = (r & ~1ULL) * w;
+  const uint64_t key = in[G.off + j];
+  uint64_t pos;
+  if (pr * w >= G.n) {
+    pos = j;
+  } else {
+    const uint64_t ps = pr * w, pe = min(ps + w, G.n);
+    const uint64_t* B = in + G.off + ps;
+    const int64_t nb = static_cast<int64_t>(pe - ps);
+    int64_t cnt;
+    if ((r & 1) == 0) {  // left run: strictly-less elements of the right run precede
+      int64_t a = 0, b = nb;
+      while (a < b) { const int64_t m = (a + b) >> 1; if (B[m] < key) a = m + 1; else b = m; }
+      cnt = a;
+    } else {  // right run: less-or-equal elements of the left run precede (stability)
+      int64_t a = 0, b = nb;
+      while (a < b) { const int64_t m = (a + b) >> 1; if (B[m] <= key) a = m + 1; else b = m; }
+      cnt = a;
+    }
+    pos = base + (j - r * w) + static_cast<uint64_t>(cnt);
+  }
+  out[G.off + pos] = key;
+}
+
+constexpr int kBigCentroids = 8192;
+
+__global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restrict__ groups, const uint64_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ starts_all, double* __restrict__ means_all,
+                                                       double* __restrict__ out, unsigned int* __restrict__ err) {
+  __shared__ int64_t meta[4];
+  const BigGroup G = groups[blockIdx.x];
+  uint32_t* starts = starts_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
+  double* means = means_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
+  const uint64_t* k = keys + G.off;
+  BlockDigest([&](int64_t i) -> uint64_t { return k[i]; }, static_cast<int64_t>(G.n), starts, means, kBigCentroids,
+              out + static_cast<uint64_t>(G.g) * 7, err, meta);
+}
+
+// ---------------------------------------------------------------------------------------
+// Keys out of the arena.
+// ---------------------------------------------------------------------------------------
+struct KeyOutDev {
+  uint64_t* fixed[kMaxKeys];  // 8 B (16 B for UINT128) per group
+  uint32_t* len[kMaxKeys];    // STRING lengths
+};
+
+__global__ void KeyExtractKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gslot, uint32_t ngroups,
+                                 const unsigned long long* __restrict__ slots, const uint64_t* __restrict__ arena, KeyOutDev ko) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const unsigned long long w = slots[gslot[g]];
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
+  for (int i = 0; i < plan->n_keys; ++i) {
+    const int t = plan->key_types[i];
+    if (t == PXG_STRING) {
+      ko.len[i][g] = static_cast<uint32_t>(k.v[i].b);
+    } else if (t == PXG_UINT128) {
+      ko.fixed[i][2 * g] = k.v[i].a;
+      ko.fixed[i][2 * g + 1] = k.v[i].b;
+    } else if (t == PXG_BOOLEAN) {
+      reinterpret_cast<uint8_t*>(ko.fixed[i])[g] = static_cast<uint8_t>(k.v[i].a);
+    } else {
+      ko.fixed[i][g] = k.v[i].a;
+    }
+  }
+}
+
+__global__ void KeyStringCopyKernel(const AggPlanDev* __restrict__ plan, int key, const uint32_t* __restrict__ gslot,
+                                    uint32_t ngroups, const unsigned long long* __restrict__ slots,
+                                    const uint64_t* __restrict__ arena, const uint32_t* __restrict__ offs,
+                                    uint8_t* __restrict__ data) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const unsigned long long w = slots[gslot[g]];
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[key].a);
+  const uint32_t len = static_cast<uint32_t>(k.v[key].b);
+  uint8_t* dst = data + offs[g];
+  for (uint32_t i = 0; i < len; ++i) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// Host orchestration.
+// ---------------------------------------------------------------------------------------
+static int Log2Ceil(uint64_t x) {
+  int b = 0;
+  while ((uint64_t(1) << b) < x) ++b;
+  return b;
+}
+
+int32_t AggFinalizeImpl(Agg* a) {
+  Ctx* ctx = a->ctx;
+  AggResult& R = a->res;
+  R = AggResult();
+  const uint64_t n = a->st_n;
+  if (n == 0) {
+    R.n_groups = 0;
+    R.ready = true;
+    return PXG_OK;
+  }
+  if (n >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
+  // 1. Stable LSD radix sort of (slot, vals...) by slot; deferred (invalid) slots map to cap.
+  const int nbits = Log2Ceil(static_cast<uint64_t>(a->cap) + 1);
+  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
+  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
+  DevBuf alt_slot, hist, tmp;
+  DevBuf alt_val[kMaxVals];
+  PXG_RETURN_IF_ERROR(alt_slot.Alloc(n * 4));
+  for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(alt_val[v].Alloc(n * 8));
+  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
+  PXG_RETURN_IF_ERROR(hist.Alloc(nh * 4 + 64));
+  const size_t scan_bytes = ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(nh, n)));
+  PXG_RETURN_IF_ERROR(tmp.Alloc(scan_bytes + 64));
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * kRadixBits;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, a->st_slot.as<const uint32_t>(), n,
+                               a->cap, shift, hist.as<uint32_t>(), nblocks));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, hist.as<uint32_t>(), hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, tmp.p));
+    ConstValPtrs vin;
+    ValPtrs vout;
+    for (int v = 0; v < kMaxVals; ++v) {
+      vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+      vout.p[v] = v < a->n_vals ? alt_val[v].as<uint64_t>() : nullptr;
+    }
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0,
+                               a->st_slot.as<const uint32_t>(), alt_slot.as<uint32_t>(), vin, vout, a->n_vals, n, a->cap, shift,
+                               hist.as<const uint32_t>(), nblocks));
+    std::swap(a->st_slot, alt_slot);
+    for (int v = 0; v < a->n_vals; ++v) std::swap(a->st_val[v], alt_val[v]);
+  }
+  // 2. Runs -> groups.
+  DevBuf flags, gidx, meta;
+  PXG_RETURN_IF_ERROR(flags.Alloc(n * 4));
+  PXG_RETURN_IF_ERROR(gidx.Alloc(n * 4));
+  PXG_RETURN_IF_ERROR(meta.Alloc(64));
+  unsigned long long* d_nvalid = meta.as<unsigned long long>();
+  uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta.as<uint8_t>() + 8);
+  unsigned int* d_err = reinterpret_cast<unsigned int*>(meta.as<uint8_t>() + 16);
+  uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta.as<uint8_t>() + 32);
+  {
+    uint64_t init[8] = {n, 0, 0, 0, 0, 0, 0, 0};
+    PXG_HIP(hipMemcpy(meta.p, init, 64, hipMemcpyHostToDevice));  // fresh buffer: synchronous copy
+  }
+  PXG_RETURN_IF_ERROR(Launch(ctx, "run_heads", RunHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                             a->st_slot.as<const uint32_t>(), n, a->cap, flags.as<uint32_t>(), d_nvalid));
+  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, flags.as<const uint32_t>(), gidx.as<uint32_t>(), static_cast<int64_t>(n), d_ngroups, tmp.p));
+  uint32_t ngroups = 0;
+  PXG_HIP(hipMemcpyAsync(&ngroups, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  R.n_groups = ngroups;
+  if (ngroups == 0) {
+    R.ready = true;
+    return PXG_OK;
+  }
+  DevBuf gstart, gslot;
+  PXG_RETURN_IF_ERROR(gstart.Alloc((static_cast<size_t>(ngroups) + 1) * 4));
+  PXG_RETURN_IF_ERROR(gslot.Alloc(static_cast<size_t>(ngroups) * 4));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "group_starts", GroupStartsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                             a->st_slot.as<const uint32_t>(), flags.as<const uint32_t>(), gidx.as<const uint32_t>(), n,
+                             gstart.as<uint32_t>(), gslot.as<uint32_t>(), static_cast<const unsigned long long*>(d_nvalid), ngroups));
+  // 3. UDA reductions.
+  ConstValPtrs cv;
+  for (int v = 0; v < kMaxVals; ++v) cv.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+  UdaOut uo;
+  for (int u = 0; u < kMaxUdas; ++u) uo.p[u] = nullptr;
+  for (int u = 0; u < a->n_udas; ++u) {
+    const size_t per = a->uda_kind[u] == PXG_UDA_QUANTILES ? 7 * 8 : 8;
+    PXG_RETURN_IF_ERROR(R.uda_out[u].Alloc(static_cast<size_t>(ngroups) * per));
+    uo.p[u] = R.uda_out[u].as<uint64_t>();
+  }
+  PXG_RETURN_IF_ERROR(Launch(ctx, "uda_reduce", UdaReduceKernel, dim3(GridFor(static_cast<int64_t>(ngroups) * 64, 256, ctx->num_cus * 16)),
+                             dim3(256), 0, a->d_plan.as<const AggPlanDev>(), gstart.as<const uint32_t>(), ngroups, cv, uo));
+  // 4. Quantile digests.
+  bool any_q = false;
+  for (int u = 0; u < a->n_udas; ++u) any_q |= a->uda_kind[u] == PXG_UDA_QUANTILES;
+  if (any_q) {
+    DevBuf lists;
+    PXG_RETURN_IF_ERROR(lists.Alloc(static_cast<size_t>(ngroups) * 3 * 4));
+    PXG_HIP(hipMemsetAsync(d_cls, 0, 12, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                               gstart.as<const uint32_t>(), ngroups, lists.as<uint32_t>(), d_cls, 64u, static_cast<uint32_t>(kMidMax)));
+    uint32_t cls[3];
+    PXG_HIP(hipMemcpyAsync(cls, d_cls, 12, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    // Big-group metadata (host side; few groups).
+    std::vector<BigGroup> big;
+    std::vector<BigChunk> bchunks;
+    uint64_t big_total = 0, big_max = 0;
+    if (cls[2] > 0) {
+      std::vector<uint32_t> bl(cls[2]);
+      PXG_HIP(hipMemcpy(bl.data(), lists.as<uint32_t>() + 2 * static_cast<uint64_t>(ngroups), cls[2] * 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> gs(static_cast<size_t>(ngroups) + 1);
+      PXG_HIP(hipMemcpy(gs.data(), gstart.p, gs.size() * 4, hipMemcpyDeviceToHost));
+      for (uint32_t g : bl) {
+        BigGroup B;
+        B.off = gs[g];
+        B.n = gs[g + 1] - gs[g];
+        B.eoff = big_total;
+        B.g = g;
+        B.pad = 0;
+        big.push_back(B);
+        big_total += B.n;
+        big_max = std::max<uint64_t>(big_max, B.n);
+        for (uint64_t o = 0; o < B.n; o += kMidMax) {
+          BigChunk c;
+          c.off = B.off + o;
+          c.len = static_cast<uint32_t>(std::min<uint64_t>(kMidMax, B.n - o));
+          c.pad = 0;
+          bchunks.push_back(c);
+        }
+      }
+    }
+    DevBuf d_big, d_bchunks, keysA, keysB, bstarts, bmeans;
+    if (!big.empty()) {
+      PXG_RETURN_IF_ERROR(d_big.Alloc(big.size() * sizeof(BigGroup)));
+      PXG_HIP(hipMemcpy(d_big.p, big.data(), big.size() * sizeof(BigGroup), hipMemcpyHostToDevice));
+      PXG_RETURN_IF_ERROR(d_bchunks.Alloc(bchunks.size() * sizeof(BigChunk)));
+      PXG_HIP(hipMemcpy(d_bchunks.p, bchunks.data(), bchunks.size() * sizeof(BigChunk), hipMemcpyHostToDevice));
+      PXG_RETURN_IF_ERROR(keysA.Alloc(n * 8));
+      PXG_RETURN_IF_ERROR(keysB.Alloc(n * 8));
+      PXG_RETURN_IF_ERROR(bstarts.Alloc(big.size() * kBigCentroids * 4));
+      PXG_RETURN_IF_ERROR(bmeans.Alloc(big.size() * kBigCentroids * 8));
+    }
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+      const uint64_t* vals = a->st_val[a->uda_val[u]].as<const uint64_t>();
+      const int at = a->uda_arg_type[u];
+      double* qo = R.uda_out[u].as<double>();
+      if (cls[0] > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((cls[0] + 3) / 4), dim3(256), 0, lists.as<const uint32_t>(),
+                                   cls[0], gstart.as<const uint32_t>(), vals, at, qo));
+      if (cls[1] > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[1]), dim3(256), 0,
+                                   lists.as<const uint32_t>() + static_cast<uint64_t>(ngroups), gstart.as<const uint32_t>(), vals, at, qo,
+                                   d_err));
+      if (!big.empty()) {
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(static_cast<unsigned>(bchunks.size())), dim3(256), 0,
+                                   d_bchunks.as<const BigChunk>(), vals, at, keysA.as<uint64_t>()));
+        DevBuf* src = &keysA;
+        DevBuf* dst = &keysB;
+        for (uint64_t w = kMidMax; w < big_max; w *= 2) {
+          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeKernel, dim3(GridFor(static_cast<int64_t>(big_total), 256, 1 << 30)),
+                                     dim3(256), 0, d_big.as<const BigGroup>(), static_cast<uint32_t>(big.size()), big_total,
+                                     src->as<const uint64_t>(), dst->as<uint64_t>(), w));
+          std::swap(src, dst);
+        }
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(static_cast<unsigned>(big.size())), dim3(256), 0,
+                                   d_big.as<const BigGroup>(), src->as<const uint64_t>(), bstarts.as<uint32_t>(), bmeans.as<double>(), qo,
+                                   d_err));
+      }
+    }
+    unsigned int err = 0;
+    PXG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
+  }
+  // 5. Keys.
+  KeyOutDev ko;
+  for (int k = 0; k < kMaxKeys; ++k) {
+    ko.fixed[k] = nullptr;
+    ko.len[k] = nullptr;
+  }
+  for (int k = 0; k < a->n_keys; ++k) {
+    const int t = a->key_types[k];
+    if (t == PXG_STRING) {
+      PXG_RETURN_IF_ERROR(R.key_offsets[k].Alloc((static_cast<size_t>(ngroups) + 1) * 4));
+      ko.len[k] = R.key_offsets[k].as<uint32_t>();
+    } else {
+      PXG_RETURN_IF_ERROR(R.key_fixed[k].Alloc(static_cast<size_t>(ngroups) * (t == PXG_UINT128 ? 16 : 8)));
+      ko.fixed[k] = R.key_fixed[k].as<uint64_t>();
+    }
+  }
+  if (a->n_keys > 0) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                               a->d_plan.as<const AggPlanDev>(), gslot.as<const uint32_t>(), ngroups,
+                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
+  }
+  for (int k = 0; k < a->n_keys; ++k) {
+    if (a->key_types[k] != PXG_STRING) continue;
+    uint32_t* off = R.key_offsets[k].as<uint32_t>();
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, ngroups, off + ngroups, tmp.p));
+    uint32_t total = 0;
+    PXG_HIP(hipMemcpyAsync(&total, off + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    R.key_data_len[k] = total;
+    PXG_RETURN_IF_ERROR(R.key_data[k].Alloc(static_cast<size_t>(total) + 16));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "key_string_copy", KeyStringCopyKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                               a->d_plan.as<const AggPlanDev>(), k, gslot.as<const uint32_t>(), ngroups,
+                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), static_cast<const uint32_t*>(off),
+                               R.key_data[k].as<uint8_t>()));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  R.ready = true;
+  return PXG_OK;
+}
+
+}  // namespace pxg
+
+using namespace pxg;
+
+extern "C" int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups) {
+  if (!agg) return SetError(PXG_INVALID_ARGUMENT, "agg is null");
+  PXG_RETURN_IF_ERROR(AggFinalizeImpl(&agg->impl));
+  int64_t g = agg->impl.res.n_groups;
+  if (agg->impl.n_keys == 0 && g == 0) g = 1;  // no-groups agg always emits one row
+  if (n_groups) *n_groups = g;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols) {
+  if (!agg || !cols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Agg& a = agg->impl;
+  if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
+  if (n_cols != a.n_keys + a.n_udas) return SetError(PXG_INVALID_ARGUMENT, "expected %d result columns", a.n_keys + a.n_udas);
+  const int64_t G = a.res.n_groups;
+  const bool synth = a.n_keys == 0 && G == 0;  // AggregateGroupByNone over no rows
+  const int64_t rows = synth ? 1 : G;
+  for (int c = 0; c < n_cols; ++c) std::memset(&cols[c], 0, sizeof(cols[c]));
+  for (int k = 0; k < a.n_keys; ++k) {
+    pxg_column_out& o = cols[k];
+    o.type = a.key_types[k];
+    o.length = rows;
+    if (o.type == PXG_STRING) {
+      o.offsets = static_cast<int32_t*>(std::malloc((rows + 1) * 4));
+      o.data = static_cast<uint8_t*>(std::malloc(a.res.key_data_len[k] + 16));
+      o.data_len = a.res.key_data_len[k];
+      if (G > 0) {
+        PXG_HIP(hipMemcpy(o.offsets, a.res.key_offsets[k].p, (G + 1) * 4, hipMemcpyDeviceToHost));
+        PXG_HIP(hipMemcpy(o.data, a.res.key_data[k].p, o.data_len, hipMemcpyDeviceToHost));
+      } else {
+        o.offsets[0] = 0;
+      }
+    } else {
+      const size_t w = TypeWidth(o.type);
+      o.values = std::malloc(std::max<size_t>(rows * w, 1));
+      if (G > 0) {
+        if (o.type == PXG_BOOLEAN) {
+          PXG_HIP(hipMemcpy(o.values, a.res.key_fixed[k].p, G, hipMemcpyDeviceToHost));
+        } else {
+          PXG_HIP(hipMemcpy(o.values, a.res.key_fixed[k].p, G * w, hipMemcpyDeviceToHost));
+        }
+      }
+    }
+  }
+  for (int u = 0; u < a.n_udas; ++u) {
+    pxg_column_out& o = cols[a.n_keys + u];
+    o.type = a.uda_out_type[u];
+    o.length = rows;
+    const bool q = a.uda_kind[u] == PXG_UDA_QUANTILES;
+    const size_t per = q ? 56 : 8;
+    o.values = std::malloc(std::max<size_t>(rows * per, 8));
+    if (!synth) {
+      PXG_HIP(hipMemcpy(o.values, a.res.uda_out[u].p, G * per, hipMemcpyDeviceToHost));
+      continue;
+    }
+    // Initial UDA states finalized (AggNode no-groups emit over zero rows, agg_node.cc:182-207).
+    uint64_t* p = static_cast<uint64_t*>(o.values);
+    const int at = a.uda_arg_type[u];
+    switch (a.uda_kind[u]) {
+      case PXG_UDA_COUNT: p[0] = 0; break;
+      case PXG_UDA_SUM: { double z = 0; p[0] = at == PXG_FLOAT64 ? *reinterpret_cast<uint64_t*>(&z) : 0; break; }
+      case PXG_UDA_MINSUM: p[0] = static_cast<uint64_t>(a.uda_init[u]); break;
+      case PXG_UDA_MEAN: { double nan = std::nan(""); std::memcpy(p, &nan, 8); break; }
+      case PXG_UDA_MAX:
+        if (at == PXG_FLOAT64) { double d = 2.2250738585072014e-308; std::memcpy(p, &d, 8); }
+        else p[0] = static_cast<uint64_t>(INT64_MIN);
+        break;
+      case PXG_UDA_MIN:
+        if (at == PXG_FLOAT64) { double d = 1.7976931348623157e+308; std::memcpy(p, &d, 8); }
+        else p[0] = static_cast<uint64_t>(INT64_MAX);
+        break;
+      case PXG_UDA_QUANTILES: for (int j = 0; j < 7; ++j) { double nan = std::nan(""); std::memcpy(p + j, &nan, 8); } break;
+      default: break;
+    }
+  }
+  return PXG_OK;
+}

@@ -1,0 +1,196 @@
+// Host-side internals of libpxg: context, device buffers, kernel timing, tables.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pxg.h"
+#include "pxg_device.h"
+#include "pxg_errors.h"
+
+#define PXG_HIP(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return ::pxg::SetError(PXG_INTERNAL, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                             __FILE__, __LINE__);                                               \
+  } while (0)
+
+#define PXG_RETURN_IF_ERROR(expr) \
+  do {                            \
+    int32_t s_ = (expr);          \
+    if (s_ != PXG_OK) return s_;  \
+  } while (0)
+
+namespace pxg {
+
+// Device allocation that frees itself; capacity-tracked for growth.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { Free(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+    return *this;
+  }
+  ~DevBuf() { Free(); }
+  void Free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  int32_t Alloc(size_t n) {
+    Free();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return SetError(PXG_RESOURCE_UNAVAILABLE, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    }
+    bytes = n;
+    return PXG_OK;
+  }
+  // Ensure capacity >= n, preserving the first `keep` bytes (stream-ordered copy).
+  int32_t Reserve(size_t n, size_t keep, hipStream_t s) {
+    if (n <= bytes) return PXG_OK;
+    size_t cap = bytes ? bytes : 256;
+    while (cap < n) cap *= 2;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, cap);
+    if (e != hipSuccess) return SetError(PXG_RESOURCE_UNAVAILABLE, "hipMalloc(%zu) failed: %s", cap, hipGetErrorString(e));
+    if (keep && p) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return SetError(PXG_INTERNAL, "hipMemcpyAsync failed: %s", hipGetErrorString(e));
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return SetError(PXG_INTERNAL, "sync failed: %s", hipGetErrorString(e));
+    }
+    Free();
+    p = q;
+    bytes = cap;
+    return PXG_OK;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct KernelStat {
+  int64_t launches = 0;
+  double total_ms = 0;
+};
+
+struct PendingTiming {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool profiling = false;
+  std::map<std::string, KernelStat> stats;
+  std::vector<PendingTiming> pending;
+  std::vector<hipEvent_t> free_events;
+  int num_cus = 256;
+  // small pinned scratch for counters read back by the host
+  void* pinned = nullptr;
+
+  hipEvent_t GetEvent();
+  int32_t ResolveTimings();
+};
+
+// Launch helper: optional event bracketing on the ctx stream (stats resolved lazily).
+template <typename... KArgs, typename... Args>
+inline int32_t Launch(Ctx* ctx, const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t shmem,
+                      Args&&... args) {
+  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return PXG_OK;
+  hipEvent_t s0 = nullptr, s1 = nullptr;
+  if (ctx->profiling) {
+    s0 = ctx->GetEvent();
+    s1 = ctx->GetEvent();
+    hipEventRecord(s0, ctx->stream);
+  }
+  hipLaunchKernelGGL(kernel, grid, block, shmem, ctx->stream, std::forward<Args>(args)...);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return SetError(PXG_INTERNAL, "launch %s failed: %s", name, hipGetErrorString(e));
+  if (ctx->profiling) {
+    hipEventRecord(s1, ctx->stream);
+    ctx->pending.push_back(PendingTiming{name, s0, s1});
+  }
+  return PXG_OK;
+}
+
+inline int GridFor(int64_t items, int per_block, int cap) {
+  int64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+// ---------------------------------------------------------------------------------------
+// Tables.
+// ---------------------------------------------------------------------------------------
+struct ChunkCol {
+  DevBuf values;   // fixed-width
+  DevBuf offsets;  // STRING (int32, nrows_cap + 1)
+  DevBuf data;     // STRING payload
+  int64_t data_len = 0;
+};
+
+struct Chunk {
+  int64_t nrows = 0;
+  int64_t rows_cap = 0;
+  int64_t row_base = 0;
+  std::vector<ChunkCol> cols;
+  bool sealed = false;
+};
+
+int TypeWidth(int type);
+
+struct Table {
+  Ctx* ctx = nullptr;
+  int32_t ncols = 0;
+  std::vector<int32_t> types;
+  std::vector<std::unique_ptr<Chunk>> chunks;
+  int64_t nrows = 0;
+  // Pinned host staging for coalescing small RowBatches.
+  struct Stage {
+    std::vector<std::vector<uint8_t>> fixed;   // per col
+    std::vector<std::vector<int32_t>> offsets; // per col (STRING), starts with 0
+    std::vector<std::vector<uint8_t>> data;    // per col (STRING)
+    int64_t rows = 0;
+    int64_t bytes = 0;
+  } stage;
+  // Device copy of the chunk descriptors (rebuilt when chunks change).
+  DevBuf d_chunks;
+  DevBuf d_types;
+  int64_t d_chunks_version = -1;
+  int64_t version = 0;
+
+  int32_t FlushStage();
+  int32_t AppendRows(const pxg_column_view* cols, int64_t nrows, hipMemcpyKind kind);
+  int32_t EnsureDeviceDescriptors();
+  DevChunk Descriptor(size_t i) const;
+};
+
+}  // namespace pxg
+
+struct pxg_table;
+namespace pxg {
+int32_t NewTable(Ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out);
+}
+
+struct pxg_ctx {
+  pxg::Ctx impl;
+};
+struct pxg_table {
+  pxg::Table impl;
+};

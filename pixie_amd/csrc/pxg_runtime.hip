@@ -1,0 +1,462 @@
+// libpxg runtime: contexts, kernel timing, HBM-resident tables (RowBatch coalescing), fetch.
+//
+// Table ↔ reference: table_store::Table keeps hot/cold RowBatches per table
+// (src/table_store/table/table.h:71-199) and MemorySourceNode hands them to the graph one
+// batch at a time (src/carnot/exec/memory_source_node.cc:92-124).  Here a table is the
+// HBM-resident image of those batches, coalesced into <= 2^24-row chunks so the operators see
+// a few large Arrow-layout arrays instead of thousands of 100-row batches.
+#include <algorithm>
+#include <cstdlib>
+
+#include "pxg_internal.h"
+#include "pxg_scan.h"
+
+namespace pxg {
+
+int TypeWidth(int type) {
+  switch (type) {
+    case PXG_BOOLEAN: return 1;
+    case PXG_UINT128: return 16;
+    case PXG_STRING: return 0;
+    default: return 8;
+  }
+}
+
+hipEvent_t Ctx::GetEvent() {
+  if (!free_events.empty()) {
+    hipEvent_t e = free_events.back();
+    free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+int32_t Ctx::ResolveTimings() {
+  for (auto& p : pending) {
+    hipError_t e = hipEventSynchronize(p.stop);
+    if (e != hipSuccess) return SetError(PXG_INTERNAL, "event sync failed: %s", hipGetErrorString(e));
+    float ms = 0;
+    hipEventElapsedTime(&ms, p.start, p.stop);
+    auto& st = stats[p.name];
+    st.launches += 1;
+    st.total_ms += ms;
+    free_events.push_back(p.start);
+    free_events.push_back(p.stop);
+  }
+  pending.clear();
+  return PXG_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Tables
+// ---------------------------------------------------------------------------------------
+__global__ void RebaseOffsetsKernel(int32_t* __restrict__ dst, const int32_t* __restrict__ src, int64_t n, int32_t sub,
+                                    int32_t add) {
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i] - sub + add;
+}
+
+DevChunk Table::Descriptor(size_t i) const {
+  DevChunk d;
+  std::memset(&d, 0, sizeof(d));
+  const Chunk& c = *chunks[i];
+  d.nrows = c.nrows;
+  d.row_base = c.row_base;
+  for (int k = 0; k < ncols && k < kMaxCols; ++k) {
+    d.cols[k].values = c.cols[k].values.as<uint8_t>();
+    d.cols[k].offsets = c.cols[k].offsets.as<int32_t>();
+    d.cols[k].data = c.cols[k].data.as<uint8_t>();
+  }
+  return d;
+}
+
+int32_t Table::EnsureDeviceDescriptors() {
+  PXG_RETURN_IF_ERROR(FlushStage());
+  if (d_chunks_version == version) return PXG_OK;
+  std::vector<DevChunk> h(std::max<size_t>(chunks.size(), 1));
+  for (size_t i = 0; i < chunks.size(); ++i) h[i] = Descriptor(i);
+  if (d_chunks.bytes < h.size() * sizeof(DevChunk)) PXG_RETURN_IF_ERROR(d_chunks.Alloc(h.size() * sizeof(DevChunk) * 2));
+  PXG_HIP(hipMemcpyAsync(d_chunks.p, h.data(), h.size() * sizeof(DevChunk), hipMemcpyHostToDevice, ctx->stream));
+  if (!d_types.p) {
+    std::vector<int32_t> t(kMaxCols, 0);
+    for (int k = 0; k < ncols; ++k) t[k] = types[k];
+    PXG_RETURN_IF_ERROR(d_types.Alloc(kMaxCols * sizeof(int32_t)));
+    PXG_HIP(hipMemcpyAsync(d_types.p, t.data(), kMaxCols * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  d_chunks_version = version;
+  return PXG_OK;
+}
+
+static constexpr int64_t kStageRows = 1 << 20;
+static constexpr int64_t kStageBytes = 64 << 20;
+static constexpr int64_t kMaxChunkData = (int64_t(1) << 31) - 64;
+
+// Append rows [0, n) of `cols` (host or device pointers per `kind`) into the table's chunks.
+int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind kind) {
+  const bool from_host = (kind == hipMemcpyHostToDevice);
+  int64_t done = 0;
+  while (done < n) {
+    Chunk* ch = chunks.empty() ? nullptr : chunks.back().get();
+    if (!ch || ch->sealed || ch->nrows >= kChunkRows) {
+      auto c = std::make_unique<Chunk>();
+      c->row_base = nrows;
+      c->cols.resize(ncols);
+      chunks.push_back(std::move(c));
+      ch = chunks.back().get();
+    }
+    int64_t take = std::min<int64_t>(n - done, kChunkRows - ch->nrows);
+    // String payload bounds: shrink `take` so every string column stays < 2^31 bytes.
+    for (int k = 0; k < ncols; ++k) {
+      if (types[k] != PXG_STRING) continue;
+      const int32_t* off = cols[k].offsets;
+      int32_t o_first, o_last;
+      if (from_host) {
+        o_first = off[done];
+        o_last = off[done + take];
+      } else {
+        PXG_HIP(hipMemcpy(&o_first, off + done, 4, hipMemcpyDeviceToHost));
+        PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+      }
+      int64_t bytes = static_cast<int64_t>(o_last) - o_first;
+      while (ch->cols[k].data_len + bytes > kMaxChunkData && take > 1) {
+        take /= 2;
+        if (from_host) {
+          o_last = off[done + take];
+        } else {
+          PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+        }
+        bytes = static_cast<int64_t>(o_last) - o_first;
+      }
+      if (ch->cols[k].data_len + bytes > kMaxChunkData) {
+        if (ch->nrows == 0) return SetError(PXG_INVALID_ARGUMENT, "single string value exceeds 2^31 bytes");
+        ch->sealed = true;
+        take = 0;
+        break;
+      }
+    }
+    if (take == 0) continue;  // sealed; next iteration opens a new chunk
+    const int64_t r0 = ch->nrows, r1 = ch->nrows + take;
+    for (int k = 0; k < ncols; ++k) {
+      ChunkCol& cc = ch->cols[k];
+      const int t = types[k];
+      if (t != PXG_STRING) {
+        const size_t w = TypeWidth(t);
+        PXG_RETURN_IF_ERROR(cc.values.Reserve(static_cast<size_t>(r1) * w + 16, static_cast<size_t>(r0) * w, ctx->stream));
+        const uint8_t* src = static_cast<const uint8_t*>(cols[k].values) + static_cast<size_t>(done) * w;
+        PXG_HIP(hipMemcpyAsync(cc.values.as<uint8_t>() + static_cast<size_t>(r0) * w, src, static_cast<size_t>(take) * w, kind,
+                               ctx->stream));
+        continue;
+      }
+      const int32_t* off = cols[k].offsets;
+      int32_t o_first, o_last;
+      if (from_host) {
+        o_first = off[done];
+        o_last = off[done + take];
+      } else {
+        PXG_HIP(hipMemcpy(&o_first, off + done, 4, hipMemcpyDeviceToHost));
+        PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+      }
+      const int64_t bytes = static_cast<int64_t>(o_last) - o_first;
+      PXG_RETURN_IF_ERROR(cc.offsets.Reserve(static_cast<size_t>(r1 + 1) * 4 + 16, static_cast<size_t>(r0 + 1) * 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(cc.data.Reserve(static_cast<size_t>(cc.data_len + bytes) + 16, static_cast<size_t>(cc.data_len), ctx->stream));
+      PXG_HIP(hipMemcpyAsync(cc.data.as<uint8_t>() + cc.data_len, cols[k].data + o_first, static_cast<size_t>(bytes), kind, ctx->stream));
+      const int32_t add = static_cast<int32_t>(cc.data_len);
+      if (from_host) {
+        std::vector<int32_t> tmp(static_cast<size_t>(take) + 1);
+        for (int64_t i = 0; i <= take; ++i) tmp[i] = off[done + i] - o_first + add;
+        PXG_HIP(hipMemcpyAsync(cc.offsets.as<int32_t>() + r0, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        PXG_HIP(hipStreamSynchronize(ctx->stream));  // tmp goes out of scope
+      } else {
+        PXG_RETURN_IF_ERROR(Launch(ctx, "rebase_offsets", RebaseOffsetsKernel, dim3(GridFor(take + 1, 256, 1 << 30)), dim3(256), 0,
+                                   cc.offsets.as<int32_t>() + r0, off + done, take + 1, o_first, add));
+      }
+      cc.data_len += bytes;
+    }
+    ch->nrows = r1;
+    nrows += take;
+    done += take;
+    ++version;
+  }
+  if (!from_host) PXG_HIP(hipStreamSynchronize(ctx->stream));
+  else PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+int32_t Table::FlushStage() {
+  if (stage.rows == 0) return PXG_OK;
+  std::vector<pxg_column_view> v(ncols);
+  for (int k = 0; k < ncols; ++k) {
+    std::memset(&v[k], 0, sizeof(v[k]));
+    v[k].type = types[k];
+    v[k].length = stage.rows;
+    if (types[k] == PXG_STRING) {
+      v[k].offsets = stage.offsets[k].data();
+      v[k].data = stage.data[k].data();
+    } else {
+      v[k].values = stage.fixed[k].data();
+    }
+  }
+  int64_t rows = stage.rows;
+  stage.rows = 0;
+  stage.bytes = 0;
+  int32_t s = AppendRows(v.data(), rows, hipMemcpyHostToDevice);
+  for (int k = 0; k < ncols; ++k) {
+    stage.fixed[k].clear();
+    stage.data[k].clear();
+    stage.offsets[k].assign(1, 0);
+  }
+  return s;
+}
+
+}  // namespace pxg
+
+using namespace pxg;
+
+// ---------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------
+extern "C" int32_t pxg_abi_version(void) { return PXG_ABI_VERSION; }
+extern "C" const char* pxg_last_error(void) { return LastErrorRef().c_str(); }
+
+extern "C" int32_t pxg_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return SetError(PXG_RESOURCE_UNAVAILABLE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = n;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
+  if (!out) return SetError(PXG_INVALID_ARGUMENT, "out is null");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return SetError(PXG_RESOURCE_UNAVAILABLE, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n) return SetError(PXG_INVALID_ARGUMENT, "device %d out of range [0,%d)", device, n);
+  auto* c = new pxg_ctx();
+  c->impl.device = device;
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete c;
+    return SetError(PXG_INTERNAL, "hipSetDevice: %s", hipGetErrorString(e));
+  }
+  e = hipStreamCreateWithFlags(&c->impl.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return SetError(PXG_INTERNAL, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->impl.num_cus = prop.multiProcessorCount;
+  if (hipHostMalloc(&c->impl.pinned, 4096, hipHostMallocDefault) != hipSuccess) c->impl.pinned = nullptr;
+  *out = c;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
+  if (!ctx) return PXG_OK;
+  hipStreamSynchronize(ctx->impl.stream);
+  ctx->impl.ResolveTimings();
+  for (auto e : ctx->impl.free_events) hipEventDestroy(e);
+  if (ctx->impl.pinned) hipHostFree(ctx->impl.pinned);
+  hipStreamDestroy(ctx->impl.stream);
+  delete ctx;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_ctx_sync(pxg_ctx* ctx) {
+  if (!ctx) return SetError(PXG_INVALID_ARGUMENT, "ctx is null");
+  PXG_HIP(hipStreamSynchronize(ctx->impl.stream));
+  return PXG_OK;
+}
+
+extern "C" void* pxg_ctx_stream(pxg_ctx* ctx) { return ctx ? static_cast<void*>(ctx->impl.stream) : nullptr; }
+
+extern "C" int32_t pxg_ctx_set_profiling(pxg_ctx* ctx, int32_t enabled) {
+  if (!ctx) return SetError(PXG_INVALID_ARGUMENT, "ctx is null");
+  ctx->impl.profiling = enabled != 0;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* name, int64_t* launches, double* total_ms) {
+  if (!ctx || !name) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  PXG_RETURN_IF_ERROR(ctx->impl.ResolveTimings());
+  auto it = ctx->impl.stats.find(name);
+  if (launches) *launches = it == ctx->impl.stats.end() ? 0 : it->second.launches;
+  if (total_ms) *total_ms = it == ctx->impl.stats.end() ? 0 : it->second.total_ms;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_ctx_reset_stats(pxg_ctx* ctx) {
+  if (!ctx) return SetError(PXG_INVALID_ARGUMENT, "ctx is null");
+  PXG_RETURN_IF_ERROR(ctx->impl.ResolveTimings());
+  ctx->impl.stats.clear();
+  return PXG_OK;
+}
+
+namespace pxg {
+int32_t NewTable(Ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out) {
+  if (!ctx || !out || ncols < 0 || (ncols > 0 && !types)) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  if (ncols > kMaxCols) return SetError(PXG_UNIMPLEMENTED, "tables are limited to %d columns", kMaxCols);
+  for (int k = 0; k < ncols; ++k)
+    if (types[k] < PXG_BOOLEAN || types[k] > PXG_TIME64NS) return SetError(PXG_INVALID_ARGUMENT, "bad column type %d", types[k]);
+  auto* t = new pxg_table();
+  t->impl.ctx = ctx;
+  t->impl.ncols = ncols;
+  t->impl.types.assign(types, types + ncols);
+  t->impl.stage.fixed.resize(ncols);
+  t->impl.stage.data.resize(ncols);
+  t->impl.stage.offsets.assign(ncols, std::vector<int32_t>(1, 0));
+  *out = t;
+  return PXG_OK;
+}
+}  // namespace pxg
+
+extern "C" int32_t pxg_table_create(pxg_ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out) {
+  if (!ctx) return SetError(PXG_INVALID_ARGUMENT, "ctx is null");
+  return NewTable(&ctx->impl, ncols, types, out);
+}
+
+extern "C" int32_t pxg_table_destroy(pxg_table* t) {
+  if (!t) return PXG_OK;
+  hipStreamSynchronize(t->impl.ctx->stream);
+  delete t;
+  return PXG_OK;
+}
+
+static int32_t CheckViews(const Table& t, const pxg_column_view* cols, int64_t nrows) {
+  if (nrows < 0) return SetError(PXG_INVALID_ARGUMENT, "negative row count");
+  if (nrows > 0 && !cols) return SetError(PXG_INVALID_ARGUMENT, "cols is null");
+  for (int k = 0; k < t.ncols && nrows > 0; ++k) {
+    // RowBatch::AddColumn checks (src/table_store/schema/row_batch.cc:39-52).
+    if (cols[k].type != t.types[k]) return SetError(PXG_INVALID_ARGUMENT, "column %d type %d != schema %d", k, cols[k].type, t.types[k]);
+    if (cols[k].length != nrows) return SetError(PXG_INVALID_ARGUMENT, "column %d length %lld != %lld", k, (long long)cols[k].length, (long long)nrows);
+    if (t.types[k] == PXG_STRING ? (!cols[k].offsets || !cols[k].data) : !cols[k].values)
+      return SetError(PXG_INVALID_ARGUMENT, "column %d missing buffers", k);
+  }
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_table_append(pxg_table* tp, const pxg_column_view* cols, int64_t nrows) {
+  if (!tp) return SetError(PXG_INVALID_ARGUMENT, "table is null");
+  Table& t = tp->impl;
+  PXG_RETURN_IF_ERROR(CheckViews(t, cols, nrows));
+  if (nrows == 0) return PXG_OK;
+  if (nrows >= kStageRows / 4) {
+    PXG_RETURN_IF_ERROR(t.FlushStage());
+    return t.AppendRows(cols, nrows, hipMemcpyHostToDevice);
+  }
+  // Coalesce into the host staging buffer.
+  for (int k = 0; k < t.ncols; ++k) {
+    if (t.types[k] == PXG_STRING) {
+      auto& off = t.stage.offsets[k];
+      auto& dat = t.stage.data[k];
+      int32_t base = static_cast<int32_t>(dat.size());
+      int32_t o0 = cols[k].offsets[0];
+      int64_t bytes = cols[k].offsets[nrows] - o0;
+      dat.insert(dat.end(), cols[k].data + o0, cols[k].data + o0 + bytes);
+      for (int64_t i = 1; i <= nrows; ++i) off.push_back(cols[k].offsets[i] - o0 + base);
+      t.stage.bytes += bytes;
+    } else {
+      size_t w = TypeWidth(t.types[k]);
+      const uint8_t* s = static_cast<const uint8_t*>(cols[k].values);
+      t.stage.fixed[k].insert(t.stage.fixed[k].end(), s, s + nrows * w);
+      t.stage.bytes += nrows * static_cast<int64_t>(w);
+    }
+  }
+  t.stage.rows += nrows;
+  if (t.stage.rows >= kStageRows || t.stage.bytes >= kStageBytes) return t.FlushStage();
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_table_append_device(pxg_table* tp, const pxg_column_view* cols, int64_t nrows) {
+  if (!tp) return SetError(PXG_INVALID_ARGUMENT, "table is null");
+  Table& t = tp->impl;
+  PXG_RETURN_IF_ERROR(CheckViews(t, cols, nrows));
+  if (nrows == 0) return PXG_OK;
+  PXG_RETURN_IF_ERROR(t.FlushStage());
+  return t.AppendRows(cols, nrows, hipMemcpyDeviceToDevice);
+}
+
+extern "C" int32_t pxg_table_flush(pxg_table* t) {
+  if (!t) return SetError(PXG_INVALID_ARGUMENT, "table is null");
+  PXG_RETURN_IF_ERROR(t->impl.FlushStage());
+  PXG_HIP(hipStreamSynchronize(t->impl.ctx->stream));
+  return PXG_OK;
+}
+
+extern "C" int64_t pxg_table_num_rows(const pxg_table* t) { return t ? t->impl.nrows + t->impl.stage.rows : 0; }
+extern "C" int32_t pxg_table_num_chunks(const pxg_table* t) { return t ? static_cast<int32_t>(t->impl.chunks.size()) : 0; }
+
+extern "C" int64_t pxg_table_device_bytes(const pxg_table* tp, int32_t col) {
+  if (!tp || col < 0 || col >= tp->impl.ncols) return -1;
+  const Table& t = tp->impl;
+  int64_t b = 0;
+  for (auto& c : t.chunks) {
+    if (t.types[col] == PXG_STRING) b += 4 * c->nrows + c->cols[col].data_len;
+    else b += TypeWidth(t.types[col]) * c->nrows;
+  }
+  return b;
+}
+
+extern "C" int32_t pxg_table_fetch(pxg_table* tp, int32_t col, int64_t begin, int64_t end, pxg_column_out* out) {
+  if (!tp || !out || col < 0 || col >= tp->impl.ncols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Table& t = tp->impl;
+  PXG_RETURN_IF_ERROR(t.FlushStage());
+  if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
+  std::memset(out, 0, sizeof(*out));
+  const int type = t.types[col];
+  out->type = type;
+  out->length = end - begin;
+  const int64_t n = end - begin;
+  if (type != PXG_STRING) {
+    size_t w = TypeWidth(type);
+    out->values = std::malloc(std::max<size_t>(n * w, 1));
+  } else {
+    out->offsets = static_cast<int32_t*>(std::malloc((n + 1) * 4));
+    out->offsets[0] = 0;
+  }
+  std::vector<uint8_t> data;
+  PXG_HIP(hipStreamSynchronize(t.ctx->stream));
+  for (auto& cp : t.chunks) {
+    Chunk& c = *cp;
+    int64_t lo = std::max(begin, c.row_base), hi = std::min(end, c.row_base + c.nrows);
+    if (lo >= hi) continue;
+    int64_t l0 = lo - c.row_base, l1 = hi - c.row_base;
+    if (type != PXG_STRING) {
+      size_t w = TypeWidth(type);
+      PXG_HIP(hipMemcpy(static_cast<uint8_t*>(out->values) + (lo - begin) * w, c.cols[col].values.as<uint8_t>() + l0 * w, (l1 - l0) * w,
+                        hipMemcpyDeviceToHost));
+    } else {
+      std::vector<int32_t> off(l1 - l0 + 1);
+      PXG_HIP(hipMemcpy(off.data(), c.cols[col].offsets.as<int32_t>() + l0, off.size() * 4, hipMemcpyDeviceToHost));
+      size_t base = data.size();
+      data.resize(base + (off.back() - off.front()));
+      PXG_HIP(hipMemcpy(data.data() + base, c.cols[col].data.as<uint8_t>() + off.front(), off.back() - off.front(), hipMemcpyDeviceToHost));
+      for (int64_t i = 1; i < static_cast<int64_t>(off.size()); ++i)
+        out->offsets[lo - begin + i] = static_cast<int32_t>(base + off[i] - off.front());
+    }
+  }
+  if (type == PXG_STRING) {
+    out->data = static_cast<uint8_t*>(std::malloc(data.size() + 16));
+    std::memcpy(out->data, data.data(), data.size());
+    out->data_len = static_cast<int64_t>(data.size());
+  }
+  return PXG_OK;
+}
+
+extern "C" void pxg_result_free(pxg_column_out* cols, int32_t n) {
+  if (!cols) return;
+  for (int32_t i = 0; i < n; ++i) {
+    std::free(cols[i].values);
+    std::free(cols[i].offsets);
+    std::free(cols[i].data);
+    cols[i].values = nullptr;
+    cols[i].offsets = nullptr;
+    cols[i].data = nullptr;
+  }
+}

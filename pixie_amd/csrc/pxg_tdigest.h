@@ -1,0 +1,141 @@
+// Device emulation of QuantilesUDA's t-digest (math_sketches.h:33-82 over third-party
+// pixie-io/tdigest @85e0f700, compression 1000) for one group whose W values are sorted.
+//
+// For W <= 8*ceil(delta) the reference never processes before Finalize, so its digest is ONE
+// process() over the sorted multiset with unit weights.  With unit weights wSoFar before
+// element i is exactly i, so the centroid boundaries depend only on W:
+//   s_0 = 0, wLimit_0 = W * Q(1);  s_{j+1} = max(s_j + 1, floor(wLimit_j)),
+//   wLimit_{j+1} = W * Q(L(s_{j+1} / W) + 1)
+// with L = integratedLocation, Q = integratedQ.  Q(L(x)+1) has the closed form
+//   ((2x-1) cos(pi/d) + sqrt(1-(2x-1)^2) sin(pi/d) + 1) / 2      (d = delta, clamp to 1)
+// which is evaluated first; whenever floor() could be decided differently by rounding (within
+// 1e-9 of an integer, or near the clamp) the reference's own asin/sin expression is used.
+// Each centroid mean is the reference's incremental update m += (v - m) / w in sorted order,
+// and quantile() follows tdigest's cumulative-midpoint interpolation including its min/max
+// tails.  For W >= ~1273 rounding-free singletons end; for W <= 1200 every centroid is a
+// singleton (W * pi / (2 d) < 2) and the chain is skipped.
+// Compile with -ffp-contract=off: the reference host build does not fuse multiply-adds.
+#pragma once
+
+#include "pxg_device.h"
+
+namespace pxg {
+
+constexpr double kDelta = 1000.0;
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kDblMin = 2.2250738585072014e-308;   // numeric_limits<double>::min()
+constexpr double kDblMax = 1.7976931348623157e+308;
+constexpr int kSingletonMaxW = 1200;
+
+__device__ __constant__ const double kQuantileQ[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
+
+__device__ __forceinline__ double StdMin(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double StdMax(double a, double b) { return (a < b) ? b : a; }
+
+__device__ __forceinline__ double WeightedAverageSorted(double x1, double w1, double x2, double w2) {
+  const double x = (x1 * w1 + x2 * w2) / (w1 + w2);
+  return StdMax(x1, StdMin(x, x2));
+}
+__device__ __forceinline__ double WeightedAverage(double x1, double w1, double x2, double w2) {
+  return (x1 <= x2) ? WeightedAverageSorted(x1, w1, x2, w2) : WeightedAverageSorted(x2, w2, x1, w1);
+}
+
+__device__ __forceinline__ double IntegratedQ(double k) {
+  return (sin(StdMin(k, kDelta) * kPi / kDelta - kPi / 2) + 1) / 2;
+}
+__device__ __forceinline__ double IntegratedLocation(double q) { return kDelta * (asin(2.0 * q - 1.0) + kPi / 2) / kPi; }
+
+// wLimit after a boundary at index b (W total unit weights).
+__device__ __forceinline__ double NextLimit(int64_t b, double W) {
+  const double kCos = 0.99999506519785548;   // cos(pi/1000)
+  const double kSin = 0.0031415874858795635; // sin(pi/1000)
+  const double x = static_cast<double>(b) / W;
+  const double t = 2.0 * x - 1.0;
+  bool exact = t >= kCos - 1e-9;
+  double wl = 0;
+  if (!exact) {
+    const double s = sqrt(fmax(0.0, (1.0 - t) * (1.0 + t)));
+    wl = W * ((t * kCos + s * kSin + 1.0) * 0.5);
+    const double r = rint(wl);
+    if (fabs(wl - r) < 1e-9 * fmax(1.0, wl)) exact = true;
+  }
+  if (exact) wl = W * IntegratedQ(IntegratedLocation(static_cast<double>(b) / W) + 1.0);
+  return wl;
+}
+
+// Generic quantile over centroids given accessors start(j) (j in [0,nc), start(0)=0),
+// mean(j); W total weight.
+template <typename StartF, typename MeanF>
+__device__ double DigestQuantile(double q, int64_t nc, int64_t W, StartF start, MeanF mean) {
+  if (nc <= 0) return __longlong_as_double(0x7FF8000000000000LL);
+  if (nc == 1) return mean(0);
+  const double Wd = static_cast<double>(W);
+  const double index = q * Wd;
+  auto weight = [&](int64_t j) -> double {
+    return static_cast<double>((j + 1 < nc ? start(j + 1) : W) - start(j));
+  };
+  auto cum = [&](int64_t j) -> double {
+    return j < nc ? static_cast<double>(start(j)) + weight(j) / 2.0 : Wd;
+  };
+  const double w0 = weight(0);
+  const double mn = StdMin(kDblMax, mean(0));
+  const double mx = StdMax(kDblMin, mean(nc - 1));
+  if (index <= w0 / 2.0) return mn + 2.0 * index / w0 * (mean(0) - mn);
+  int64_t lo = 0, hi = nc;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cum(mid) < index) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < nc) {
+    const double z1 = index - cum(lo - 1);
+    const double z2 = cum(lo) - index;
+    return WeightedAverage(mean(lo - 1), z2, mean(lo), z1);
+  }
+  const double wl = weight(nc - 1);
+  const double z1 = index - Wd - wl / 2.0;
+  const double z2 = wl / 2 - z1;
+  return WeightedAverage(mean(nc - 1), z1, mx, z2);
+}
+
+// Singleton digest (W <= kSingletonMaxW): centroid j = value j.
+template <typename ValF>
+__device__ __forceinline__ double SingletonQuantile(double q, int64_t W, ValF val) {
+  return DigestQuantile(q, W, W, [](int64_t j) { return j; }, val);
+}
+
+// Build the centroid boundaries for W unit weights.  Single thread.  Returns the centroid
+// count, or -1 if more than max_c centroids would be needed.
+__device__ inline int64_t DigestBoundaries(int64_t W, uint32_t* starts, int64_t max_c) {
+  if (W <= 0) return 0;
+  int64_t nc = 0;
+  starts[nc++] = 0;
+  const double Wd = static_cast<double>(W);
+  double wl = Wd * IntegratedQ(1.0);
+  int64_t i = 1;
+  while (true) {
+    const double f = floor(wl);
+    int64_t b = f >= static_cast<double>(W) ? W : static_cast<int64_t>(f);
+    if (b < i) b = i;
+    if (b >= W) break;
+    if (nc >= max_c) return -1;
+    starts[nc++] = static_cast<uint32_t>(b);
+    wl = NextLimit(b, Wd);
+    i = b + 1;
+  }
+  return nc;
+}
+
+// Incremental centroid mean over sorted values [s, e) (Centroid::add with unit weights).
+template <typename ValF>
+__device__ __forceinline__ double CentroidMean(ValF val, int64_t s, int64_t e) {
+  double m = val(s);
+  double w = 1.0;
+  for (int64_t t = s + 1; t < e; ++t) {
+    w += 1.0;
+    m += 1.0 * (val(t) - m) / w;
+  }
+  return m;
+}
+
+}  // namespace pxg

@@ -1,0 +1,193 @@
+"""Builders for planpb plans: expression helpers and the BASELINE.json queries.
+
+The query shapes are what the PxL compiler emits for the north-star scripts
+(src/carnot/planner/compiler/compiler_test.cc:1265-1447 shows the compiled shape:
+MemorySource -> Map/Filter -> Agg -> ... -> sink).  Operator-name mapping of PxL infix
+operators follows src/carnot/planner/ir/func_ir.cc:27-48 (>= -> greaterThanEqual, / -> divide).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+from . import planpb
+from ._lib import BOOLEAN, FLOAT64, INT64, STRING, TIME64NS, UINT128
+from .device import HTTP_EVENTS_SCHEMA
+
+
+def col(index: int, node: int = 0):
+    e = planpb.ScalarExpression()
+    e.column.node = node
+    e.column.index = index
+    return e
+
+
+def const(dtype: int, value):
+    e = planpb.ScalarExpression()
+    c = e.constant
+    c.data_type = dtype
+    if dtype == INT64:
+        c.int64_value = int(value)
+    elif dtype == FLOAT64:
+        c.float64_value = float(value)
+    elif dtype == STRING:
+        c.string_value = value
+    elif dtype == BOOLEAN:
+        c.bool_value = bool(value)
+    elif dtype == TIME64NS:
+        c.time64_ns_value = int(value)
+    elif dtype == UINT128:
+        c.uint128_value.low = int(value) & (2**64 - 1)
+        c.uint128_value.high = int(value) >> 64
+    return e
+
+
+def func(name: str, args: Sequence, arg_types: Sequence[int] = (), fid: int = 0):
+    e = planpb.ScalarExpression()
+    f = e.func
+    f.name = name
+    f.id = fid
+    for a in args:
+        f.args.add().CopyFrom(a)
+    f.args_data_types.extend(arg_types)
+    return e
+
+
+def agg_expr(name: str, args: Sequence, arg_types: Sequence[int] = (), fid: int = 0, init_args: Sequence = ()):
+    op = planpb.AggregateOperator()
+    v = op.values.add()
+    v.name = name
+    v.id = fid
+    for a in args:
+        arg = v.args.add()
+        if a.WhichOneof("value") == "column":
+            arg.column.CopyFrom(a.column)
+        else:
+            arg.constant.CopyFrom(a.constant)
+    v.args_data_types.extend(arg_types)
+    for ia in init_args:
+        v.init_args.add().CopyFrom(ia.constant)
+    return v
+
+
+def filter_op(expr, columns: Sequence[int], node: int = 0):
+    op = planpb.Operator()
+    op.op_type = planpb.Operator.DESCRIPTOR.fields_by_name["op_type"].enum_type.values_by_name["FILTER_OPERATOR"].number
+    op.filter_op.expression.CopyFrom(expr)
+    for c in columns:
+        cc = op.filter_op.columns.add()
+        cc.node = node
+        cc.index = c
+    return op
+
+
+def map_op(exprs: Sequence, names: Sequence[str]):
+    op = planpb.Operator()
+    op.op_type = 2000
+    for e in exprs:
+        op.map_op.expressions.add().CopyFrom(e)
+    op.map_op.column_names.extend(names)
+    return op
+
+
+def agg_op(groups: Sequence[int], values: Sequence, group_names: Sequence[str] = (), value_names: Sequence[str] = (),
+           windowed: bool = False, node: int = 0):
+    op = planpb.Operator()
+    op.op_type = 2100
+    for g in groups:
+        c = op.agg_op.groups.add()
+        c.node = node
+        c.index = g
+    for v in values:
+        op.agg_op.values.add().CopyFrom(v)
+    op.agg_op.group_names.extend(group_names or [f"g{i}" for i in range(len(groups))])
+    op.agg_op.value_names.extend(value_names or [f"v{i}" for i in range(len(values))])
+    op.agg_op.windowed = windowed
+    return op
+
+
+def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Sequence[int]):
+    op = planpb.Operator()
+    op.op_type = 1000
+    m = op.mem_source_op
+    m.name = name
+    m.column_idxs.extend(idxs)
+    m.column_types.extend([types[i] for i in idxs])
+    m.column_names.extend([names[i] for i in idxs])
+    return op
+
+
+def sink_op(name: str, types: Sequence[int] = (), names: Sequence[str] = ()):
+    op = planpb.Operator()
+    op.op_type = 9000
+    op.mem_sink_op.name = name
+    op.mem_sink_op.column_types.extend(types)
+    op.mem_sink_op.column_names.extend(names)
+    return op
+
+
+def linear_plan(ops: List) -> "planpb.Plan":
+    """One fragment, nodes 1..n chained in order (exec_graph.cc topological execution)."""
+    plan = planpb.Plan()
+    frag = plan.nodes.add()
+    frag.id = 1
+    for i, op in enumerate(ops):
+        nid = i + 1
+        dn = frag.dag.nodes.add()
+        dn.id = nid
+        if i > 0:
+            dn.sorted_parents.append(nid - 1)
+        if i + 1 < len(ops):
+            dn.sorted_children.append(nid + 1)
+        pn = frag.nodes.add()
+        pn.id = nid
+        pn.op.CopyFrom(op)
+    pdn = plan.dag.nodes.add()
+    pdn.id = 1
+    return plan
+
+
+HTTP_TYPES = [t for _, t in HTTP_EVENTS_SCHEMA]
+HTTP_NAMES = [n for n, _ in HTTP_EVENTS_SCHEMA]
+HE = {n: i for i, n in enumerate(HTTP_NAMES)}
+
+
+def c1_plan(table: str = "http_events"):
+    """groupby('service').agg(count=('latency', px.count), mean=('latency', px.mean))."""
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES, [HE["service"], HE["latency"]])
+    agg = agg_op([0], [agg_expr("count", [col(1)], [INT64]), agg_expr("mean", [col(1)], [INT64], fid=1)],
+                 ["service"], ["count", "mean"])
+    return linear_plan([src, agg, sink_op("output")])
+
+
+def c2_plan(table: str = "http_events", with_pluck: bool = True):
+    """Filter(resp_status >= 400) -> Map(service, req_path, latency_ms = latency / 1e6)
+    -> Agg by (service, req_path): count, mean, quantiles -> Map(pluck p50, p99)."""
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES,
+                    [HE["service"], HE["req_path"], HE["resp_status"], HE["latency"]])
+    flt = filter_op(func("greaterThanEqual", [col(2), const(INT64, 400)], [INT64, INT64]), [0, 1, 2, 3])
+    mp = map_op([col(0), col(1), func("divide", [col(3), const(FLOAT64, 1e6)], [INT64, FLOAT64], fid=1)],
+                ["service", "req_path", "latency_ms"])
+    agg = agg_op([0, 1], [agg_expr("count", [col(2)], [FLOAT64], fid=2),
+                          agg_expr("mean", [col(2)], [FLOAT64], fid=3),
+                          agg_expr("quantiles", [col(2)], [FLOAT64], fid=4)],
+                 ["service", "req_path"], ["count", "mean", "latency_quantiles"])
+    ops = [src, flt, mp, agg]
+    if with_pluck:
+        pl = map_op([col(0), col(1), col(2), col(3),
+                     func("pluck_float64", [col(4), const(STRING, "p50")], [STRING, STRING], fid=5),
+                     func("pluck_float64", [col(4), const(STRING, "p99")], [STRING, STRING], fid=6)],
+                    ["service", "req_path", "count", "mean", "p50", "p99"])
+        ops.append(pl)
+    ops.append(sink_op("output"))
+    return linear_plan(ops)
+
+
+def c3_plan(table: str = "http_events"):
+    """Same filter, group by (pod, remote_addr): count, mean(latency), sum(resp_body_size)."""
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES,
+                    [HE["pod"], HE["remote_addr"], HE["resp_status"], HE["latency"], HE["resp_body_size"]])
+    flt = filter_op(func("greaterThanEqual", [col(2), const(INT64, 400)], [INT64, INT64]), [0, 1, 3, 4])
+    agg = agg_op([0, 1], [agg_expr("count", [col(2)], [INT64]), agg_expr("mean", [col(2)], [INT64], fid=1),
+                          agg_expr("sum", [col(3)], [INT64], fid=2)],
+                 ["pod", "remote_addr"], ["count", "mean_latency", "sum_resp_body"])
+    return linear_plan([src, flt, agg, sink_op("output")])

@@ -1,0 +1,219 @@
+"""ctypes client of the CPU Carnot restatement (oracle/).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import subprocess
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+BOOLEAN, INT64, UINT128, FLOAT64, STRING, TIME64NS = 1, 2, 3, 4, 5, 6
+
+
+class OColumn(C.Structure):
+    _fields_ = [("type", C.c_int32), ("length", C.c_int64), ("values", C.c_void_p),
+                ("offsets", C.c_void_p), ("data", C.c_void_p)]
+
+
+class OTable(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("ncols", C.c_int32), ("col_names", C.POINTER(C.c_char_p)),
+                ("col_types", C.POINTER(C.c_int32)), ("nbatches", C.c_int32), ("cols", C.POINTER(OColumn)),
+                ("batch_flags", C.c_void_p)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_LIB):
+        subprocess.run(["make", "-C", ORACLE_DIR, "-s"], check=True)
+    lib = C.CDLL(ORACLE_LIB)
+    lib.oracle_execute_plan.restype = C.c_int32
+    lib.oracle_execute_plan.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
+    lib.oracle_execute_plan_timed.restype = C.c_int32
+    lib.oracle_execute_plan_timed.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.POINTER(C.c_double),
+                                              C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
+    lib.oracle_free.argtypes = [C.c_void_p]
+    lib.oracle_tdigest_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
+    lib.oracle_tdigest_merge_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
+                                                   C.POINTER(C.c_double)]
+    lib.oracle_quantiles_json.argtypes = [C.POINTER(C.c_double), C.c_int64, C.c_char_p, C.c_int32]
+    lib.oracle_quantiles_json.restype = C.c_int32
+    lib.oracle_pluck_float64.argtypes = [C.c_char_p, C.c_char_p]
+    lib.oracle_pluck_float64.restype = C.c_double
+    _lib = lib
+    return lib
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"oracle error {code}: {msg}")
+        self.code = code
+
+
+def _col_struct(col) -> OColumn:
+    oc = OColumn()
+    oc.type = col.type
+    oc.length = len(col)
+    if col.type == STRING:
+        oc.offsets = col.offsets.ctypes.data
+        oc.data = col.data.ctypes.data
+    else:
+        oc.values = col.values.ctypes.data
+    return oc
+
+
+class _Tables:
+    """Keeps the ctypes structures (and numpy buffers) alive for one call."""
+
+    def __init__(self, tables: Dict[str, dict]):
+        self.keep = []
+        arr = (OTable * max(1, len(tables)))()
+        for ti, (name, t) in enumerate(tables.items()):
+            types = t["types"]
+            names = t.get("names") or [f"c{i}" for i in range(len(types))]
+            batches = t["batches"]
+            cols = (OColumn * max(1, len(batches) * len(types)))()
+            for b, batch in enumerate(batches):
+                for c, col in enumerate(batch):
+                    cols[b * len(types) + c] = _col_struct(col)
+                    self.keep.append(col)
+            cnames = (C.c_char_p * len(names))(*[n.encode() for n in names])
+            ctypes_ = (C.c_int32 * len(types))(*types)
+            self.keep += [cols, cnames, ctypes_]
+            bname = name.encode()
+            self.keep.append(bname)
+            flags = None
+            if t.get("flags") is not None:
+                fl = np.array([(1 if eow else 0) | (2 if eos else 0) for eow, eos in t["flags"]], dtype=np.uint8)
+                self.keep.append(fl)
+                flags = fl.ctypes.data
+            arr[ti] = OTable(bname, len(types), cnames, ctypes_, len(batches), cols, flags)
+        self.arr = arr
+        self.n = len(tables)
+
+
+def parse_pxrb(buf: bytes):
+    """PXRB -> {sink name: [ {'rows': n, 'eow': b, 'eos': b, 'cols': [Column...]} ]}."""
+    from pixie_amd.device import Column
+    off = 0
+
+    def take(fmt):
+        nonlocal off
+        v = struct.unpack_from(fmt, buf, off)
+        off += struct.calcsize(fmt)
+        return v
+
+    magic, ntables = take("<II")
+    assert magic == 0x42525850
+    out = {}
+    for _ in range(ntables):
+        (nl,) = take("<I")
+        name = buf[off:off + nl].decode()
+        off += nl
+        (nb,) = take("<I")
+        batches = []
+        for _ in range(nb):
+            nrows, eow, eos, _pad, ncols = take("<qBBHI")
+            cols = []
+            for _ in range(ncols):
+                (t,) = take("<i")
+                if t == STRING:
+                    offs = np.frombuffer(buf, dtype=np.int32, count=nrows + 1, offset=off).copy()
+                    off += 4 * (nrows + 1)
+                    nbytes = int(offs[-1])
+                    data = np.frombuffer(buf, dtype=np.uint8, count=nbytes, offset=off).copy()
+                    off += nbytes
+                    cols.append(Column(STRING, offsets=offs, data=np.concatenate([data, np.zeros(16, np.uint8)])))
+                elif t == UINT128:
+                    v = np.frombuffer(buf, dtype=np.uint64, count=2 * nrows, offset=off).copy().reshape(nrows, 2)
+                    off += 16 * nrows
+                    cols.append(Column(UINT128, values=v))
+                elif t == BOOLEAN:
+                    v = np.frombuffer(buf, dtype=np.uint8, count=nrows, offset=off).copy()
+                    off += nrows
+                    cols.append(Column(BOOLEAN, values=v))
+                else:
+                    dt = np.float64 if t == FLOAT64 else np.int64
+                    v = np.frombuffer(buf, dtype=dt, count=nrows, offset=off).copy()
+                    off += 8 * nrows
+                    cols.append(Column(t, values=v))
+            batches.append({"rows": nrows, "eow": bool(eow), "eos": bool(eos), "cols": cols})
+        out[name] = batches
+    return out
+
+
+def execute_plan(plan, tables: Dict[str, dict]):
+    """Run a planpb.Plan (message) on the oracle.  tables: name -> {types, batches, names}."""
+    from google.protobuf import json_format
+    lib = load()
+    js = json_format.MessageToJson(plan).encode()
+    t = _Tables(tables)
+    out = C.c_void_p()
+    n = C.c_int64()
+    err = C.create_string_buffer(1024)
+    code = lib.oracle_execute_plan(js, t.n, t.arr, C.byref(out), C.byref(n), err, 1024)
+    if code != 0:
+        raise OracleError(code, err.value.decode())
+    try:
+        buf = C.string_at(out.value, n.value)
+    finally:
+        lib.oracle_free(out)
+    return parse_pxrb(buf)
+
+
+def time_plan(plan, tables: Dict[str, dict]):
+    from google.protobuf import json_format
+    lib = load()
+    js = json_format.MessageToJson(plan).encode()
+    t = _Tables(tables)
+    secs = C.c_double()
+    rows = C.c_int64()
+    err = C.create_string_buffer(1024)
+    code = lib.oracle_execute_plan_timed(js, t.n, t.arr, C.byref(secs), C.byref(rows), err, 1024)
+    if code != 0:
+        raise OracleError(code, err.value.decode())
+    return secs.value, rows.value
+
+
+def tdigest_quantiles(vals: Sequence[float]) -> List[float]:
+    lib = load()
+    a = np.ascontiguousarray(np.array(vals, dtype=np.float64))
+    out = (C.c_double * 7)()
+    lib.oracle_tdigest_quantiles(a.ctypes.data_as(C.POINTER(C.c_double)), len(a), out)
+    return list(out)
+
+
+def tdigest_merge_quantiles(a_vals, b_vals) -> List[float]:
+    lib = load()
+    a = np.ascontiguousarray(np.array(a_vals, dtype=np.float64))
+    b = np.ascontiguousarray(np.array(b_vals, dtype=np.float64))
+    out = (C.c_double * 7)()
+    lib.oracle_tdigest_merge_quantiles(a.ctypes.data_as(C.POINTER(C.c_double)), len(a),
+                                       b.ctypes.data_as(C.POINTER(C.c_double)), len(b), out)
+    return list(out)
+
+
+def quantiles_json(vals) -> str:
+    lib = load()
+    a = np.ascontiguousarray(np.array(vals, dtype=np.float64))
+    buf = C.create_string_buffer(1024)
+    lib.oracle_quantiles_json(a.ctypes.data_as(C.POINTER(C.c_double)), len(a), buf, 1024)
+    return buf.value.decode()
+
+
+def pluck_float64(js: str, key: str) -> float:
+    return load().oracle_pluck_float64(js.encode(), key.encode())

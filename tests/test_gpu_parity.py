@@ -1,0 +1,262 @@
+"""Device parity: the HIP path (through the libpxg C ABI) against the CPU Carnot restatement
+and the reference's golden vectors.  Bars: keys / counts / filters / integer results
+bit-exact; float sum/mean 1e-6 relative; quantiles bit-exact (<= 4 ULP) for groups of
+<= 8000 values, within the t-digest rank bound above that."""
+import bisect
+import math
+
+import numpy as np
+import pytest
+
+import oracle_client as oc
+from device_runner import run_plan
+from kat import case_plan, case_tables, expected_rows, load_kat, rows, rows_match, ulp_diff
+from pixie_amd import _lib
+from pixie_amd import plans as P
+from pixie_amd.device import Agg, Column, Table, datagen_http_events
+from pixie_amd.pipeline import LinearQuery
+
+pytestmark = pytest.mark.gpu
+KAT = load_kat()
+QS = [0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99]
+
+
+@pytest.mark.parametrize("case", KAT["cases"], ids=[c["name"] for c in KAT["cases"]])
+def test_device_matches_reference_kat(ctx, case):
+    out = run_plan(ctx, case_plan(case), case_tables(case))
+    want = case["output"]["batches"]
+    assert len(out) == len(want)
+    for bi, (g, w) in enumerate(zip(out, want)):
+        assert (g["eow"], g["eos"]) == (w["eow"], w["eos"])
+        assert [c.type for c in g["cols"]] == case["output"]["types"]
+        assert rows_match(rows(g["cols"]), expected_rows(case, bi), case["ordered"], case["tol_ulp"]), \
+            f"{case['name']} batch {bi}: {rows(g['cols'])} != {expected_rows(case, bi)}"
+
+
+@pytest.mark.parametrize("q", KAT["quantiles"], ids=["floats", "ints"])
+def test_device_quantiles_known_answers(ctx, q):
+    plan = P.linear_plan([P.source_op("t", [4], ["v"], [0]),
+                          P.agg_op([], [P.agg_expr("quantiles", [P.col(0)], [4])]), P.sink_op("out")])
+    vals = [float(x) for x in q["input"]]
+    out = run_plan(ctx, plan, {"t": {"types": [4], "batches": [[Column.from_values(4, vals)]]}})
+    import json
+    got = json.loads(out[0]["cols"][0].to_list()[0])
+    for k, v in q["expected"].items():
+        assert ulp_diff(got[k], float(v)) <= 4, (k, got[k], v)
+
+
+def _http_tables(nrows, batch_rows=None, n_pair_keys=10_000_000, seed=20250117):
+    cols = datagen_http_events(seed, 0, nrows, n_pair_keys=n_pair_keys, threads=8)
+    if batch_rows is None:
+        batches = [cols]
+    else:
+        batches = [[c.slice(a, min(a + batch_rows, nrows)) for c in cols] for a in range(0, nrows, batch_rows)]
+    return {"http_events": {"types": P.HTTP_TYPES, "batches": batches, "names": P.HTTP_NAMES}}, cols
+
+
+def _by_key(cols, nkeys):
+    r = rows(cols)
+    return {t[:nkeys]: t[nkeys:] for t in r}
+
+
+def _rank(sorted_vals, v):
+    n = len(sorted_vals)
+    return (bisect.bisect_left(sorted_vals, v) + bisect.bisect_right(sorted_vals, v)) / 2 / n
+
+
+def test_c2_query_parity(ctx):
+    tables, cols = _http_tables(400_000, batch_rows=50_000)
+    plan = P.c2_plan(with_pluck=False)
+    ref = oc.execute_plan(plan, tables)["output"]
+    dev = run_plan(ctx, plan, tables)
+    assert len(ref) == len(dev) == 1
+    R = _by_key(ref[0]["cols"], 2)
+    D = _by_key(dev[0]["cols"], 2)
+    assert set(R) == set(D)
+    import json
+    # group values for the rank checks
+    sel = cols[5].values >= 400
+    svc = np.array(cols[2].to_list(), dtype=object)[sel]
+    path = np.array(cols[3].to_list(), dtype=object)[sel]
+    lat = cols[6].values[sel] / 1e6
+    groups = {}
+    for s, p, v in zip(svc, path, lat):
+        groups.setdefault((s, p), []).append(v)
+    n_exact = 0
+    for k in R:
+        rc, rm, rq = R[k]
+        dc, dm, dq = D[k]
+        assert rc == dc, k
+        assert abs(rm - dm) <= 1e-6 * abs(rm), (k, rm, dm)
+        rq, dq = json.loads(rq), json.loads(dq)
+        n = rc
+        if n <= 8000:
+            for name in rq:
+                assert ulp_diff(rq[name], dq[name]) <= 4, (k, name, rq[name], dq[name])
+            n_exact += 1
+        else:
+            s = sorted(groups[k])
+            for q, name in zip(QS, ["p01", "p10", "p25", "p50", "p75", "p90", "p99"]):
+                bound = 2 * math.pi * math.sqrt(q * (1 - q)) / 1000 + 1 / n
+                assert abs(_rank(s, dq[name]) - _rank(s, rq[name])) <= bound, (k, name)
+    assert n_exact > 100
+
+
+def test_c2_with_pluck_matches(ctx):
+    tables, _ = _http_tables(100_000)
+    plan = P.c2_plan(with_pluck=True)
+    ref = oc.execute_plan(plan, tables)["output"][0]
+    dev = run_plan(ctx, plan, tables)[0]
+    R = _by_key(ref["cols"], 2)
+    D = _by_key(dev["cols"], 2)
+    assert set(R) == set(D)
+    for k in R:
+        assert R[k][0] == D[k][0]
+        for a, b in zip(R[k][2:], D[k][2:]):   # p50, p99 through pluck_float64
+            assert ulp_diff(a, b) <= 4, (k, a, b)
+
+
+def test_c1_groupby_service(ctx):
+    tables, _ = _http_tables(200_000, batch_rows=100)
+    plan = P.c1_plan()
+    ref = oc.execute_plan(plan, tables)["output"][0]
+    dev = run_plan(ctx, plan, tables)[0]
+    R, D = _by_key(ref["cols"], 1), _by_key(dev["cols"], 1)
+    assert set(R) == set(D)
+    for k in R:
+        assert R[k][0] == D[k][0]
+        assert abs(R[k][1] - D[k][1]) <= 1e-6 * abs(R[k][1])
+
+
+def test_c3_high_cardinality_with_table_growth(ctx):
+    tables, _ = _http_tables(600_000, n_pair_keys=200_000)
+    plan = P.c3_plan()
+    ref = oc.execute_plan(plan, tables)["output"][0]
+    dev = run_plan(ctx, plan, tables, expected_groups=16)  # forces deferral + rehash growth
+    R, D = _by_key(ref["cols"], 2), _by_key(dev["cols"], 2)
+    assert len(R) > 40_000
+    assert set(R) == set(D)
+    for k in R:
+        assert R[k][0] == D[k][0] and R[k][2] == D[k][2]
+        assert abs(R[k][1] - D[k][1]) <= 1e-6 * abs(R[k][1])
+
+
+def test_big_group_quantiles_rank_bound_and_exact_small(ctx):
+    rng = np.random.default_rng(5)
+    n_big = 150_000
+    keys = ["big"] * n_big + ["g8000"] * 8000 + ["g1500"] * 1500 + ["g3"] * 3
+    vals = np.concatenate([rng.lognormal(1.6, 1.0, n_big), rng.lognormal(1.0, 0.5, 8000), rng.normal(0, 1, 1500),
+                           np.array([3.0, -0.0, 0.0])])
+    perm = rng.permutation(len(keys))
+    keys = [keys[i] for i in perm]
+    vals = vals[perm]
+    plan = P.linear_plan([P.source_op("t", [5, 4], ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("quantiles", [P.col(1)], [4]), P.agg_expr("count", [P.col(1)], [4], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": [5, 4], "batches": [[Column.from_values(5, keys), Column(4, values=vals)]]}}
+    ref = _by_key(oc.execute_plan(plan, tables)["out"][0]["cols"], 1)
+    dev = _by_key(run_plan(ctx, plan, tables)[0]["cols"], 1)
+    import json
+    for k in ref:
+        rq, dq = json.loads(ref[k][0]), json.loads(dev[k][0])
+        assert ref[k][1] == dev[k][1]
+        if ref[k][1] <= 8000:
+            for name in rq:
+                assert ulp_diff(rq[name], dq[name]) <= 4, (k, name, rq[name], dq[name])
+        else:
+            s = sorted(vals[[i for i, kk in enumerate(keys) if kk == k[0]]])
+            n = len(s)
+            for q, name in zip(QS, ["p01", "p10", "p25", "p50", "p75", "p90", "p99"]):
+                bound = 2 * math.pi * math.sqrt(q * (1 - q)) / 1000 + 1 / n
+                assert abs(_rank(s, dq[name]) - _rank(s, rq[name])) <= bound, (k, name, dq[name], rq[name])
+
+
+def test_nan_and_signed_zero_and_key_types(ctx):
+    nan = float("nan")
+    f = [1.5, nan, -0.0, 0.0, 2.5, nan, 7.0, -3.0]
+    bkey = [True, False, True, False, True, False, True, False]
+    fkey = [0.0, -0.0, 0.0, -0.0, 1.5, 1.5, nan, nan]
+    ukey = [1, 1 << 70, 1, 1 << 70, 5, 5, 5, 1]
+    skey = ["", "", "a" * 70, "a" * 70, "a" * 69 + "b", "x", "", "x"]
+    types = [1, 4, 3, 5, 4]
+    batch = [Column.from_values(1, bkey), Column.from_values(4, fkey), Column.from_values(3, ukey),
+             Column.from_values(5, skey), Column.from_values(4, f)]
+    for gcols in ([0], [1], [2], [3], [0, 3], [1, 2, 3]):
+        plan = P.linear_plan([P.source_op("t", types, [f"c{i}" for i in range(5)], list(range(5))),
+                              P.agg_op(gcols, [P.agg_expr("count", [P.col(4)], [4]), P.agg_expr("sum", [P.col(4)], [4], fid=1),
+                                               P.agg_expr("min", [P.col(4)], [4], fid=2), P.agg_expr("max", [P.col(4)], [4], fid=3),
+                                               P.agg_expr("quantiles", [P.col(4)], [4], fid=4)]),
+                              P.sink_op("out")])
+        tables = {"t": {"types": types, "batches": [batch]}}
+        ref = oc.execute_plan(plan, tables)["out"][0]["cols"]
+        dev = run_plan(ctx, plan, tables)[0]["cols"]
+        assert rows_match(rows(dev), rows(ref), ordered=False, tol_ulp=4), (gcols, rows(dev), rows(ref))
+
+
+def test_int64_sum_wraps_and_minmax_init(ctx):
+    big = 2**62
+    vals = [big, big, big, -5]
+    plan = P.linear_plan([P.source_op("t", [2], ["a"], [0]),
+                          P.agg_op([], [P.agg_expr("sum", [P.col(0)], [2]), P.agg_expr("max", [P.col(0)], [2], fid=1),
+                                        P.agg_expr("min", [P.col(0)], [2], fid=2)]), P.sink_op("out")])
+    tables = {"t": {"types": [2], "batches": [[Column.from_values(2, vals)]]}}
+    ref = rows(oc.execute_plan(plan, tables)["out"][0]["cols"])
+    dev = rows(run_plan(ctx, plan, tables)[0]["cols"])
+    assert ref == dev
+    # MaxUDA<FLOAT64> init is numeric_limits<double>::min() (math_ops.h:699)
+    plan = P.linear_plan([P.source_op("t", [4], ["a"], [0]),
+                          P.agg_op([], [P.agg_expr("max", [P.col(0)], [4])]), P.sink_op("out")])
+    tables = {"t": {"types": [4], "batches": [[Column.from_values(4, [-1.0, -2.0])]]}}
+    assert rows(run_plan(ctx, plan, tables)[0]["cols"]) == rows(oc.execute_plan(plan, tables)["out"][0]["cols"])
+
+
+def test_standalone_filter_map_random(ctx):
+    tables, _ = _http_tables(150_000, batch_rows=40_000)
+    plan = P.linear_plan([P.source_op("http_events", P.HTTP_TYPES, P.HTTP_NAMES, list(range(10))),
+                          P.filter_op(P.func("logicalAnd", [P.func("greaterThanEqual", [P.col(5), P.const(2, 400)], [2, 2]),
+                                                            P.func("notEqual", [P.col(2), P.const(5, "ns01/svc-037")], [5, 5])],
+                                             [1, 1]), [0, 2, 3, 5, 6, 9, 1]),
+                          P.map_op([P.col(1), P.col(2), P.func("divide", [P.col(4), P.const(4, 1e6)], [2, 4]),
+                                    P.func("bin", [P.col(0), P.const(2, 10_000_000)], [6, 2]), P.col(6), P.col(5)],
+                                   ["svc", "path", "lat_ms", "t10", "upid", "pod"]),
+                          P.sink_op("out")])
+    ref = oc.execute_plan(plan, tables)["out"]
+    dev = run_plan(ctx, plan, tables)
+    assert len(ref) == len(dev)
+    for a, b in zip(ref, dev):
+        assert (a["eow"], a["eos"]) == (b["eow"], b["eos"])
+        assert rows(a["cols"]) == rows(b["cols"])   # bit-exact, order preserved
+
+
+def test_multiple_consumes_and_small_batch_coalescing(ctx):
+    cols = datagen_http_events(77, 0, 60_000, threads=4)
+    q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES)
+    t1 = Table(ctx, P.HTTP_TYPES)
+    for a in range(0, 30_000, 100):      # reference-sized 100-row RowBatches
+        t1.append([c.slice(a, a + 100) for c in cols])
+    t1.flush()
+    assert t1.num_rows == 30_000
+    t2 = Table(ctx, P.HTTP_TYPES)
+    t2.append([c.slice(30_000, 60_000) for c in cols])
+    agg = q.make_agg(ctx)
+    agg.consume(t1)
+    agg.consume(t2)
+    agg.finalize()
+    two = _by_key(q.emit(agg.result()), 2)
+    t3 = Table(ctx, P.HTTP_TYPES)
+    t3.append(cols)
+    one = _by_key(q.run(ctx, t3), 2)
+    assert set(one) == set(two)
+    for k in one:
+        assert one[k][0] == two[k][0] and one[k][2] == two[k][2]
+        assert abs(one[k][1] - two[k][1]) <= 1e-9 * abs(one[k][1])
+    for c in range(10):
+        assert t1.fetch(c).to_list() == cols[c].slice(0, 30_000).to_list()
+
+
+def test_unsupported_signature_fails_loudly(ctx):
+    from pixie_amd.compile import UnsupportedError
+    plan = P.linear_plan([P.source_op("t", [5], ["s"], [0]), P.agg_op([], [P.agg_expr("max", [P.col(0)], [5])]),
+                          P.sink_op("out")])
+    with pytest.raises(UnsupportedError):
+        LinearQuery(plan, [5])
