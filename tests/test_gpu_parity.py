@@ -132,7 +132,7 @@ def test_c3_high_cardinality_with_table_growth(ctx):
     tables, _ = _http_tables(600_000, n_pair_keys=200_000)
     plan = P.c3_plan()
     ref = oc.execute_plan(plan, tables)["output"][0]
-    dev = run_plan(ctx, plan, tables, expected_groups=16)  # forces deferral + rehash growth
+    dev = run_plan(ctx, plan, tables, expected_groups=16)[0]  # forces deferral + rehash growth
     R, D = _by_key(ref["cols"], 2), _by_key(dev["cols"], 2)
     assert len(R) > 40_000
     assert set(R) == set(D)
