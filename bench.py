@@ -23,6 +23,10 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20250117
+KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "radix_hist", "radix_scatter",
+           "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
+           "quant_tiny", "quant_small", "quant_mid", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
+           "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep"]
 
 
 def parse():
@@ -113,9 +117,7 @@ def main():
         elapsed = float(tt.item())
     launches, cons_ms = ctx.kernel_stats("agg_consume")
     kernel_ms = {}
-    for name in ["agg_consume", "agg_publish_sizes", "agg_publish_write", "radix_hist", "radix_scatter", "run_heads",
-                 "group_starts", "uda_reduce", "classify_groups", "quant_tiny", "quant_mid", "quant_big_chunk_sort",
-                 "quant_big_merge", "quant_big_digest", "key_extract", "key_string_copy", "scan_reduce", "scan_downsweep"]:
+    for name in KERNELS:
         l, ms = ctx.kernel_stats(name)
         if l:
             kernel_ms[name] = round(ms / args.steps, 4)

@@ -49,8 +49,7 @@ struct AggTableDev {
   unsigned long long* slots;
   uint32_t mask;
   uint32_t limit;                 // inserts beyond this are deferred (table kept <= 50% full)
-  unsigned int* counters;         // [0] inserted, [1] new, [2] deferred
-  uint32_t* new_slots;
+  unsigned int* counters;         // [0] groups in the table (flushed per tile), [2] deferred rows
   uint32_t* deferred;
   const uint64_t* arena;
 };

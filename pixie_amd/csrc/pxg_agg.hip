@@ -24,22 +24,28 @@ struct TileRange {
   int32_t pad;
 };
 
+constexpr uint32_t kMaxProbe = 256;  // longer probe sequences defer the row (table grows)
+
+// Probe for the row's group; insert it (CAS of an empty slot word) when absent.  Inserts are
+// counted in the workgroup's LDS counter (`s_ins`) and flushed once per tile, so no per-row
+// atomic ever targets a shared global address.  The table fill check reads the flushed global
+// count: it is a soft guard that keeps probe sequences short; a full or overlong probe defers.
 __device__ __forceinline__ uint32_t FindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
-                                                 const KeySet& keys, uint64_t h, uint32_t rowref, const AggTableDev& tab) {
+                                                 const KeySet& keys, uint64_t h, uint32_t rowref, const AggTableDev& tab,
+                                                 unsigned int* s_ins) {
   const uint32_t tag = SlotTag(h);
   uint32_t pos = static_cast<uint32_t>(h) & tab.mask;
-  for (uint32_t probe = 0; probe <= tab.mask; ++probe) {
+  const uint32_t max_probe = min(tab.mask + 1, kMaxProbe);
+  for (uint32_t probe = 0; probe < max_probe; ++probe) {
     unsigned long long w = __hip_atomic_load(&tab.slots[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (w == 0) {
-      unsigned int ins = __hip_atomic_load(&tab.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned int ins = __hip_atomic_load(&tab.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + *s_ins;
       if (ins >= tab.limit) return kDeferredSlot;
       unsigned long long expected = 0;
       const unsigned long long desired = MakeSlotWord(tag, 0, rowref);
       if (__hip_atomic_compare_exchange_strong(&tab.slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
-        atomicAdd(&tab.counters[0], 1u);
-        const unsigned int k = atomicAdd(&tab.counters[1], 1u);
-        tab.new_slots[k] = pos;
+        atomicAdd(s_ins, 1u);
         return pos;
       }
       w = expected;
@@ -61,15 +67,21 @@ __device__ __forceinline__ uint32_t FindOrInsert(const AggPlanDev* __restrict__ 
 
 __device__ __forceinline__ void ProcessRow(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                            const DevChunk& ch, uint32_t chunk_idx, int64_t local, const AggTableDev& tab,
-                                           const StageDev& stg, uint64_t pos) {
+                                           const StageDev& stg, uint64_t pos, unsigned int* s_ins) {
   KeySet k;
   LoadKeysRow(plan, ch, local, k);
   const uint64_t h = HashKeys(plan, k);
   const uint32_t rowref = (chunk_idx << kChunkShift) | static_cast<uint32_t>(local);
-  const uint32_t slot = FindOrInsert(plan, chunks, k, h, rowref, tab);
-  if (slot == kDeferredSlot) {
-    const unsigned int d = atomicAdd(&tab.counters[2], 1u);
-    tab.deferred[d] = rowref;
+  const uint32_t slot = FindOrInsert(plan, chunks, k, h, rowref, tab, s_ins);
+  // Deferred rows: one list append per wave (ballot + leader atomic).
+  const unsigned long long dm = __ballot(slot == kDeferredSlot);
+  if (dm) {
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(static_cast<long long>(dm)) - 1;
+    unsigned int base = 0;
+    if (lane == leader) base = atomicAdd(&tab.counters[2], static_cast<unsigned int>(__popcll(dm)));
+    base = __shfl(base, leader, 64);
+    if (slot == kDeferredSlot) tab.deferred[base + __popcll(dm & ((1ULL << lane) - 1))] = rowref;
   }
   stg.slot[pos] = slot;
   const int nv = plan->n_vals;
@@ -86,20 +98,24 @@ __device__ __forceinline__ void ProcessRow(const AggPlanDev* __restrict__ plan, 
   }
 }
 
-// One workgroup per tile of 4096 rows (grid-stride).  Phase 1 evaluates the predicate with
-// coalesced column loads and compacts the passing rows into LDS with a wave ballot + popcount
-// prefix; phase 2 processes the compacted rows densely (all lanes busy regardless of
-// selectivity) and appends one staging record per row.
+// One workgroup per tile of 4096 rows (grid-stride).  Phase 1 evaluates the predicate for all
+// 16 rows of each thread first (16 independent loads in flight), then compacts the passing
+// rows into LDS: per-wave ballots, one LDS prefix over the 4 waves; phase 2 processes the
+// compacted rows densely and appends one staging record per row (one cursor atomic per tile).
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanDev* __restrict__ plan,
                                                                   const DevChunk* __restrict__ chunks,
                                                                   const TileRange* __restrict__ ranges, int nranges,
                                                                   int64_t ntiles, AggTableDev tab, StageDev stg) {
+  constexpr int kPer = kConsumeTile / kConsumeBlock;
+  constexpr int kWaves = kConsumeBlock / 64;
   __shared__ int32_t s_sel[kConsumeTile];
-  __shared__ int32_t s_n;
+  __shared__ uint32_t s_wcnt[kWaves];
+  __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
+  if (threadIdx.x == 0) s_ins = 0;
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
     int ri = 0;
     while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
@@ -107,31 +123,50 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
     const DevChunk& ch = chunks[rg.chunk];
     const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
     const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-#pragma unroll 4
-    for (int k = 0; k < kConsumeTile / kConsumeBlock; ++k) {
+    // Rows of this thread: row0 + k*256 + tid (coalesced per k).
+    bool pass[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
       const int64_t r = row0 + k * kConsumeBlock + threadIdx.x;
-      bool pass = r < row1;
-      if (pass && plan->has_filter) pass = EvalProgram(&plan->filter, ch, r, plan->col_types).a != 0;
-      const unsigned long long m = __ballot(pass);
-      if (m) {
-        const int leader = __ffsll(static_cast<long long>(m)) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&s_n, __popcll(m));
-        base = __shfl(base, leader);
-        if (pass) s_sel[base + __popcll(m & lanemask_lt)] = static_cast<int32_t>(r - row0);
+      pass[k] = r < row1;
+      if (pass[k] && plan->has_filter) pass[k] = EvalProgram(&plan->filter, ch, r, plan->col_types).a != 0;
+    }
+    unsigned long long m[kPer];
+    uint32_t wtot = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      m[k] = __ballot(pass[k]);
+      wtot += static_cast<uint32_t>(__popcll(m[k]));
+    }
+    if (lane == 0) s_wcnt[wid] = wtot;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t c = s_wcnt[w];
+      wbase += w < wid ? c : 0;
+      total += c;
+    }
+    // Flush the previous tile's insert count and reserve this tile's staging range.
+    if (threadIdx.x == 0) {
+      if (s_ins) {
+        atomicAdd(&tab.counters[0], s_ins);
+        s_ins = 0;
       }
+      s_base = total ? atomicAdd(stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = k * kConsumeBlock + threadIdx.x;
+      wbase += static_cast<uint32_t>(__popcll(m[k]));
     }
     __syncthreads();
-    const int n = s_n;
-    if (threadIdx.x == 0) s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(n));
-    __syncthreads();
     const uint64_t base = s_base;
-    for (int i = threadIdx.x; i < n; i += kConsumeBlock)
-      ProcessRow(plan, chunks, ch, static_cast<uint32_t>(rg.chunk), row0 + s_sel[i], tab, stg, base + i);
+    for (uint32_t i = threadIdx.x; i < total; i += kConsumeBlock)
+      ProcessRow(plan, chunks, ch, static_cast<uint32_t>(rg.chunk), row0 + s_sel[i], tab, stg, base + i, &s_ins);
     __syncthreads();
   }
+  if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
 }
 
 // Re-process deferred rows (already past the filter) after the table grew.
@@ -140,45 +175,61 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeListKernel(const AggP
                                                                       const uint32_t* __restrict__ list, uint32_t n,
                                                                       AggTableDev tab, StageDev stg) {
   __shared__ unsigned long long s_base;
+  __shared__ unsigned int s_ins;
+  if (threadIdx.x == 0) s_ins = 0;
   for (uint32_t t0 = blockIdx.x * kConsumeBlock; t0 < n; t0 += gridDim.x * kConsumeBlock) {
     const uint32_t cnt = min(static_cast<uint32_t>(kConsumeBlock), n - t0);
-    if (threadIdx.x == 0) s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(cnt));
+    if (threadIdx.x == 0) {
+      if (s_ins) {
+        atomicAdd(&tab.counters[0], s_ins);
+        s_ins = 0;
+      }
+      s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(cnt));
+    }
     __syncthreads();
     const uint32_t i = t0 + threadIdx.x;
     if (threadIdx.x < cnt) {
       const uint32_t ref = list[i];
       const uint32_t c = ref >> kChunkShift;
-      ProcessRow(plan, chunks, chunks[c], c, static_cast<int64_t>(ref & (kChunkRows - 1)), tab, stg, s_base + threadIdx.x);
+      ProcessRow(plan, chunks, chunks[c], c, static_cast<int64_t>(ref & (kChunkRows - 1)), tab, stg, s_base + threadIdx.x, &s_ins);
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
 }
 
+// Publication: every slot still holding a row reference (kind 0) gets its key copied into the
+// arena.  sizes[i] = (1 << 40) | words, so one exclusive scan yields both the record offsets
+// and (total >> 40) the number of published groups.
+constexpr int kPublishCountShift = 40;
 __global__ void AggPublishSizesKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
-                                      const unsigned long long* __restrict__ slots, const uint32_t* __restrict__ new_slots,
-                                      uint32_t n, uint64_t* __restrict__ sizes) {
+                                      const unsigned long long* __restrict__ slots, uint32_t cap, uint64_t* __restrict__ sizes) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const unsigned long long w = slots[new_slots[i]];
-  const uint32_t ref = static_cast<uint32_t>(w);
-  KeySet k;
-  LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
-  sizes[i] = KeyRecordWords(plan, k);
+  if (i >= cap) return;
+  const unsigned long long w = slots[i];
+  uint64_t s = 0;
+  if (w != 0 && !(w & kKindArena)) {
+    const uint32_t ref = static_cast<uint32_t>(w);
+    KeySet k;
+    LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
+    s = (uint64_t(1) << kPublishCountShift) | KeyRecordWords(plan, k);
+  }
+  sizes[i] = s;
 }
 
 __global__ void AggPublishWriteKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
-                                      unsigned long long* __restrict__ slots, const uint32_t* __restrict__ new_slots, uint32_t n,
-                                      const uint64_t* __restrict__ offs, uint64_t base, uint64_t* __restrict__ arena) {
+                                      unsigned long long* __restrict__ slots, uint32_t cap, const uint64_t* __restrict__ offs,
+                                      uint64_t base, uint64_t* __restrict__ arena) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t pos = new_slots[i];
-  const unsigned long long w = slots[pos];
+  if (i >= cap) return;
+  const unsigned long long w = slots[i];
+  if (w == 0 || (w & kKindArena)) return;
   const uint32_t ref = static_cast<uint32_t>(w);
   KeySet k;
   LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
-  const uint64_t at = base + offs[i];
+  const uint64_t at = base + (offs[i] & ((uint64_t(1) << kPublishCountShift) - 1));
   WriteKeyRecord(plan, k, arena + at);
-  slots[pos] = MakeSlotWord(static_cast<uint32_t>(w >> 33), kKindArena, static_cast<uint32_t>(at));
+  slots[i] = MakeSlotWord(static_cast<uint32_t>(w >> 33), kKindArena, static_cast<uint32_t>(at));
 }
 
 __global__ void AggRehashKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ old_slots,
@@ -225,7 +276,6 @@ static AggTableDev TableDev(Agg* a, int defer_buf) {
   t.mask = a->cap - 1;
   t.limit = a->cap / 2;
   t.counters = a->counters.as<unsigned int>();
-  t.new_slots = a->new_slots.as<uint32_t>();
   t.deferred = a->deferred[defer_buf].as<uint32_t>();
   t.arena = a->arena.as<uint64_t>();
   return t;
@@ -239,26 +289,16 @@ static StageDev StageDevOf(Agg* a) {
   return s;
 }
 
-int32_t Agg::ReadCounters(uint32_t* c3, uint64_t* stage_cursor) {
-  uint8_t tmp[32];
-  PXG_HIP(hipMemcpyAsync(tmp, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
-  std::memcpy(c3, tmp, 12);
-  std::memcpy(stage_cursor, tmp + 16, 8);
-  return PXG_OK;
-}
-
 int32_t Agg::EnsureTable(uint32_t want) {
   if (slots.p) return PXG_OK;
   cap = want;
   PXG_RETURN_IF_ERROR(slots.Alloc(static_cast<size_t>(cap) * 8));
   PXG_HIP(hipMemsetAsync(slots.p, 0, static_cast<size_t>(cap) * 8, ctx->stream));
-  PXG_RETURN_IF_ERROR(new_slots.Alloc(static_cast<size_t>(cap) * 4));
   return PXG_OK;
 }
 
 int32_t Agg::EnsureStage(uint64_t need) {
-  // Capacity is whatever the buffers hold now (finalize swaps in exactly-sized sort buffers).
+  // Capacity is whatever the buffers hold now (finalize swaps staging with same-size buffers).
   st_cap = st_slot.bytes / 4;
   for (int v = 0; v < n_vals; ++v) st_cap = std::min<uint64_t>(st_cap, st_val[v].bytes / 8);
   if (need <= st_cap) return PXG_OK;
@@ -286,34 +326,42 @@ int32_t Agg::Grow(uint32_t new_cap) {
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   slots = std::move(ns);
   cap = new_cap;
-  PXG_RETURN_IF_ERROR(new_slots.Alloc(static_cast<size_t>(cap) * 4));
   return PXG_OK;
 }
 
-int32_t Agg::PublishNew(Table* t, uint32_t n_new) {
-  if (n_new == 0) return PXG_OK;
-  // sizes -> exclusive scan -> reserve arena -> write records + flip slot words to kind 1.
-  const size_t sz_bytes = static_cast<size_t>(n_new + 1) * 8;
-  const size_t need = sz_bytes + 64 + ScanScratchBytes(n_new);
-  if (scratch.bytes < need) PXG_RETURN_IF_ERROR(scratch.Alloc(need));
+// Publish every kind-0 slot into the arena; reads back the group count, the deferred count
+// and the staging cursor with one synchronisation.
+int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
+  const size_t sz_bytes = static_cast<size_t>(cap + 1) * 8;
+  const size_t need = sz_bytes + 64 + ScanScratchBytes(cap);
+  PXG_RETURN_IF_ERROR(scratch.Ensure(need));
   uint64_t* sizes = scratch.as<uint64_t>();
   uint64_t* total = reinterpret_cast<uint64_t*>(scratch.as<uint8_t>() + sz_bytes);
   void* sc = scratch.as<uint8_t>() + sz_bytes + 64;
   const DevChunk* chunks = t->d_chunks.as<const DevChunk>();
-  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_sizes", AggPublishSizesKernel, dim3(GridFor(n_new, 256, 1 << 30)), dim3(256), 0,
-                             d_plan.as<const AggPlanDev>(), chunks, slots.as<const unsigned long long>(),
-                             new_slots.as<const uint32_t>(), n_new, sizes));
-  PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, n_new, total, sc));
-  uint64_t words = 0;
-  PXG_HIP(hipMemcpyAsync(&words, total, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_sizes", AggPublishSizesKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), chunks, slots.as<const unsigned long long>(), cap, sizes));
+  PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, cap, total, sc));
+  uint8_t c[32];
+  uint64_t tot = 0;
+  PXG_HIP(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(c, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + 64, arena_words * 8, ctx->stream));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(n_new, 256, 1 << 30)), dim3(256), 0,
-                             d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(),
-                             new_slots.as<const uint32_t>(), n_new, static_cast<const uint64_t*>(sizes), arena_words,
-                             arena.as<uint64_t>()));
-  arena_words += words;
-  if (arena_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  std::memcpy(n_deferred, c + 8, 4);
+  std::memcpy(&st_n, c + 16, 8);
+  const uint64_t n_new = tot >> kPublishCountShift;
+  const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
+  if (n_new > 0) {
+    PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + 64, arena_words * 8, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                               d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
+                               static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>()));
+    arena_words += words;
+    if (arena_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  }
+  inserted += n_new;
+  // The device-side fill count restarts from the exact number of groups.
+  PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
   return PXG_OK;
 }
 
@@ -349,33 +397,26 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   if (ranges.empty()) return PXG_OK;
   const int64_t rows = end - begin;
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
-  PXG_RETURN_IF_ERROR(deferred[0].Reserve(static_cast<size_t>(rows) * 4 + 16, 0, ctx->stream));
-  DevBuf d_ranges;
-  PXG_RETURN_IF_ERROR(d_ranges.Alloc(ranges.size() * sizeof(TileRange)));
-  PXG_HIP(hipMemcpy(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice));
-  PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 4, 0, 8, ctx->stream));  // new, deferred
+  PXG_RETURN_IF_ERROR(deferred[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
+  PXG_RETURN_IF_ERROR(d_ranges.Ensure(ranges.size() * sizeof(TileRange)));
+  PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice, ctx->stream));
+  PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
   PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", AggConsumeKernel, dim3(grid), dim3(kConsumeBlock), 0,
                              d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
                              static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this)));
-  uint32_t c3[3];
-  PXG_RETURN_IF_ERROR(ReadCounters(c3, &st_n));
-  inserted = c3[0];
-  PXG_RETURN_IF_ERROR(PublishNew(t, c3[1]));
-  uint32_t n_def = c3[2];
+  uint32_t n_def = 0;
+  PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
   int buf = 0;
   while (n_def > 0) {
     PXG_RETURN_IF_ERROR(Grow(NextPow2(4 * (static_cast<uint64_t>(inserted) + n_def))));
-    PXG_RETURN_IF_ERROR(deferred[1 - buf].Reserve(static_cast<size_t>(n_def) * 4 + 16, 0, ctx->stream));
+    PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
     PXG_RETURN_IF_ERROR(EnsureStage(st_n + n_def));
-    PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 4, 0, 8, ctx->stream));
+    PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
     PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume_list", AggConsumeListKernel, dim3(GridFor(n_def, kConsumeBlock, ctx->num_cus * 8)),
                                dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(),
                                deferred[buf].as<const uint32_t>(), n_def, TableDev(this, 1 - buf), StageDevOf(this)));
-    PXG_RETURN_IF_ERROR(ReadCounters(c3, &st_n));
-    inserted = c3[0];
-    PXG_RETURN_IF_ERROR(PublishNew(t, c3[1]));
-    n_def = c3[2];
+    PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
     buf = 1 - buf;
   }
   // Keep the table at most ~37% full for the next consume.
@@ -567,6 +608,6 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   a.st_n = 0;
   a.arena_words = 0;
   a.inserted = 0;
-  a.res = AggResult();
+  a.res.Clear();
   return PXG_OK;
 }

@@ -16,6 +16,12 @@ struct AggResult {
   DevBuf key_data[kMaxKeys];
   int64_t key_data_len[kMaxKeys] = {0};
   DevBuf uda_out[kMaxUdas];     // 8 B per group (QUANTILES: 7 doubles per group)
+  // Forget the result; device buffers stay allocated for the next finalize.
+  void Clear() {
+    n_groups = 0;
+    ready = false;
+    for (auto& l : key_data_len) l = 0;
+  }
 };
 
 struct Agg {
@@ -38,9 +44,9 @@ struct Agg {
   // Global open-addressing table.
   DevBuf slots;
   uint32_t cap = 0;
-  DevBuf counters;  // u32 [0] inserted [1] new [2] deferred [3] pad ; u64 [2] stage cursor [3] arena cursor
-  DevBuf new_slots;
+  DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor
   DevBuf deferred[2];
+  DevBuf d_ranges;
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint64_t inserted = 0;     // host mirror
@@ -54,14 +60,20 @@ struct Agg {
   AggResult res;
   DevBuf scratch;
 
+  // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).
+  struct FinalizeWs {
+    DevBuf alt_slot, alt_val[kMaxVals];
+    DevBuf hist, scan, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
+    DevBuf keysA, keysB, bstarts, big, bchunks;
+  } ws;
+
   int32_t EnsureTable(uint32_t new_cap);
   int32_t EnsureStage(uint64_t need);
   int32_t Grow(uint32_t new_cap);
-  int32_t PublishNew(Table* t, uint32_t n_new);
+  int32_t PublishNew(Table* t, uint32_t* n_deferred);
   int32_t ConsumeRange(Table* t, int64_t begin, int64_t end);
   int32_t ConsumeList(Table* t, const uint32_t* list, uint32_t n);
   int32_t Finalize();
-  int32_t ReadCounters(uint32_t* c3, uint64_t* stage_cursor);
 };
 
 // Finalize stages (pxg_finalize.hip).

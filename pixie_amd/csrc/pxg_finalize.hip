@@ -111,8 +111,12 @@ __global__ void GroupStartsKernel(const uint32_t* __restrict__ keys, const uint3
 }
 
 // ---------------------------------------------------------------------------------------
-// Per-group UDA reductions (one wave per group).
+// Per-group UDA reductions, two levels: one wave per chunk of <= kRedChunk rows of a group
+// writes a partial state; one thread per group combines its chunks in order.  Balanced for
+// any group-size skew (the largest C2 group holds ~6% of all rows).
 // ---------------------------------------------------------------------------------------
+constexpr uint32_t kRedChunk = 2048;
+
 __device__ __forceinline__ uint64_t WaveSumU64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -140,76 +144,126 @@ struct UdaOut {
   uint64_t* p[kMaxUdas];
 };
 
-__global__ void __launch_bounds__(256) UdaReduceKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
-                                                       uint32_t ngroups, ConstValPtrs vals, UdaOut out) {
+__global__ void GroupChunkCountKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups, uint32_t* __restrict__ cbase) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  cbase[g] = (gstart[g + 1] - gstart[g] + kRedChunk - 1) / kRedChunk;
+}
+
+// Partial state per (uda, chunk): SUM/MINSUM/MEAN = sum (int64 bits or double bits),
+// MIN/MAX = order-preserving int64 of the extreme (NaN skipped), COUNT unused.
+__global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
+                                                         const uint32_t* __restrict__ cbase, uint32_t ngroups, ConstValPtrs vals,
+                                                         uint64_t* __restrict__ partial, uint64_t pstride) {
   const int lane = threadIdx.x & 63;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t g = wave; g < ngroups; g += nwaves) {
-    const uint32_t s = gstart[g], e = gstart[g + 1];
-    const uint64_t cnt = e - s;
-    for (int u = 0; u < plan->n_udas; ++u) {
-      const int kind = plan->uda_kind[u];
-      const int at = plan->uda_arg_type[u];
-      const int vi = plan->uda_val[u];
-      const uint64_t* v = vi >= 0 ? vals.p[vi] : nullptr;
-      uint64_t r = 0;
-      switch (kind) {
-        case PXG_UDA_COUNT: r = cnt; break;
-        case PXG_UDA_SUM:
-        case PXG_UDA_MINSUM:
-          if (at == PXG_FLOAT64) {
-            double acc = 0;
-            for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
-            r = FBits(WaveSumF64(acc));
-          } else {
-            uint64_t acc = 0;
-            for (uint32_t i = s + lane; i < e; i += 64) acc += v[i];
-            r = WaveSumU64(acc) + static_cast<uint64_t>(plan->uda_init[u]);
-          }
-          break;
-        case PXG_UDA_MEAN: {
-          double acc = 0;
-          if (at == PXG_FLOAT64) {
-            for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
-          } else {
-            for (uint32_t i = s + lane; i < e; i += 64) acc += static_cast<double>(static_cast<int64_t>(v[i]));
-          }
-          r = FBits(WaveSumF64(acc) / static_cast<double>(cnt));
-          break;
-        }
-        case PXG_UDA_MAX:
-          if (at == PXG_FLOAT64) {
-            int64_t m = OrderedFromDouble(FBits(kDblMin));  // MaxUDA init numeric_limits<double>::min()
-            for (uint32_t i = s + lane; i < e; i += 64) {
-              const uint64_t x = v[i];
-              if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o > m ? o : m; }
-            }
-            r = DoubleFromOrdered(WaveMaxI64(m));
-          } else {
-            int64_t m = INT64_MIN;
-            for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x > m ? x : m; }
-            r = static_cast<uint64_t>(WaveMaxI64(m));
-          }
-          break;
-        case PXG_UDA_MIN:
-          if (at == PXG_FLOAT64) {
-            int64_t m = OrderedFromDouble(FBits(kDblMax));
-            for (uint32_t i = s + lane; i < e; i += 64) {
-              const uint64_t x = v[i];
-              if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o < m ? o : m; }
-            }
-            r = DoubleFromOrdered(WaveMinI64(m));
-          } else {
-            int64_t m = INT64_MAX;
-            for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x < m ? x : m; }
-            r = static_cast<uint64_t>(WaveMinI64(m));
-          }
-          break;
-        default: continue;  // QUANTILES handled by the digest kernels
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nchunks = cbase[ngroups];
+  if (w >= nchunks) return;
+  uint32_t lo = 0, hi = ngroups;  // last g with cbase[g] <= w
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cbase[mid] <= w) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t g = lo;
+  const uint32_t s = gstart[g] + (w - cbase[g]) * kRedChunk;
+  const uint32_t e = min(gstart[g + 1], s + kRedChunk);
+  for (int u = 0; u < plan->n_udas; ++u) {
+    const int kind = plan->uda_kind[u];
+    const int at = plan->uda_arg_type[u];
+    const int vi = plan->uda_val[u];
+    if (kind == PXG_UDA_COUNT || kind == PXG_UDA_QUANTILES) continue;
+    const uint64_t* v = vals.p[vi];
+    uint64_t r = 0;
+    if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
+      if (at == PXG_FLOAT64) {
+        double acc = 0;
+        for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
+        r = FBits(WaveSumF64(acc));
+      } else if (kind == PXG_UDA_MEAN) {
+        double acc = 0;
+        for (uint32_t i = s + lane; i < e; i += 64) acc += static_cast<double>(static_cast<int64_t>(v[i]));
+        r = FBits(WaveSumF64(acc));
+      } else {
+        uint64_t acc = 0;
+        for (uint32_t i = s + lane; i < e; i += 64) acc += v[i];
+        r = WaveSumU64(acc);
       }
-      if (lane == 0) out.p[u][g] = r;
+    } else if (kind == PXG_UDA_MAX) {
+      int64_t m = INT64_MIN;
+      if (at == PXG_FLOAT64) {
+        for (uint32_t i = s + lane; i < e; i += 64) {
+          const uint64_t x = v[i];
+          if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o > m ? o : m; }
+        }
+      } else {
+        for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x > m ? x : m; }
+      }
+      r = static_cast<uint64_t>(WaveMaxI64(m));
+    } else if (kind == PXG_UDA_MIN) {
+      int64_t m = INT64_MAX;
+      if (at == PXG_FLOAT64) {
+        for (uint32_t i = s + lane; i < e; i += 64) {
+          const uint64_t x = v[i];
+          if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o < m ? o : m; }
+        }
+      } else {
+        for (uint32_t i = s + lane; i < e; i += 64) { const int64_t x = static_cast<int64_t>(v[i]); m = x < m ? x : m; }
+      }
+      r = static_cast<uint64_t>(WaveMinI64(m));
     }
+    if (lane == 0) partial[static_cast<uint64_t>(u) * pstride + w] = r;
+  }
+}
+
+// UDA Finalize per group (math_ops.h: CountUDA/SumUDA/MeanUDA/MinUDA/MaxUDA).
+__global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
+                                   const uint32_t* __restrict__ cbase, uint32_t ngroups, const uint64_t* __restrict__ partial,
+                                   uint64_t pstride, UdaOut out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  const uint64_t cnt = gstart[g + 1] - gstart[g];
+  const uint32_t c0 = cbase[g], c1 = cbase[g + 1];
+  for (int u = 0; u < plan->n_udas; ++u) {
+    const int kind = plan->uda_kind[u];
+    const int at = plan->uda_arg_type[u];
+    const uint64_t* p = partial + static_cast<uint64_t>(u) * pstride;
+    uint64_t r = 0;
+    switch (kind) {
+      case PXG_UDA_COUNT: r = cnt; break;
+      case PXG_UDA_SUM:
+      case PXG_UDA_MINSUM:
+        if (at == PXG_FLOAT64) {
+          double acc = 0;
+          for (uint32_t c = c0; c < c1; ++c) acc += AsF(p[c]);
+          r = FBits(acc);
+        } else {
+          uint64_t acc = 0;
+          for (uint32_t c = c0; c < c1; ++c) acc += p[c];
+          r = acc + static_cast<uint64_t>(plan->uda_init[u]);
+        }
+        break;
+      case PXG_UDA_MEAN: {
+        double acc = 0;
+        for (uint32_t c = c0; c < c1; ++c) acc += AsF(p[c]);
+        r = FBits(acc / static_cast<double>(cnt));
+        break;
+      }
+      case PXG_UDA_MAX: {
+        int64_t m = at == PXG_FLOAT64 ? OrderedFromDouble(FBits(kDblMin)) : INT64_MIN;  // MaxUDA init numeric_limits<T>::min()
+        for (uint32_t c = c0; c < c1; ++c) { const int64_t x = static_cast<int64_t>(p[c]); m = x > m ? x : m; }
+        r = at == PXG_FLOAT64 ? DoubleFromOrdered(m) : static_cast<uint64_t>(m);
+        break;
+      }
+      case PXG_UDA_MIN: {
+        int64_t m = at == PXG_FLOAT64 ? OrderedFromDouble(FBits(kDblMax)) : INT64_MAX;
+        for (uint32_t c = c0; c < c1; ++c) { const int64_t x = static_cast<int64_t>(p[c]); m = x < m ? x : m; }
+        r = at == PXG_FLOAT64 ? DoubleFromOrdered(m) : static_cast<uint64_t>(m);
+        break;
+      }
+      default: continue;  // QUANTILES: digest kernels
+    }
+    out.p[u][g] = r;
   }
 }
 
@@ -225,14 +279,34 @@ __device__ __forceinline__ double QVal(uint64_t key) { return AsF(FromSortKeyF(k
 constexpr uint64_t kNegInfKey = 0x000FFFFFFFFFFFFFULL;  // SortKeyF(-inf) = ~0xFFF0... = 0x000F...F
 constexpr uint64_t kPosInfKey = 0xFFF0000000000000ULL;  // SortKeyF(+inf) = 0x7FF0... ^ 0x8000...
 
-__global__ void ClassifyGroupsKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups, uint32_t* __restrict__ lists,
-                                     uint32_t* __restrict__ counts, uint32_t tiny_max, uint32_t mid_max) {
+// Size classes: 0 tiny (<= 64, one wave, registers), 1 small (<= 1024, one wave, LDS),
+// 2 mid (<= 4096, one workgroup, LDS), 3 big (chunk sort + merge in HBM).
+constexpr uint32_t kTinyMax = 64;
+constexpr uint32_t kSmallMax = 1024;
+constexpr int kNumClasses = 4;
+
+__global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups,
+                                                            uint32_t* __restrict__ lists, uint32_t* __restrict__ counts,
+                                                            uint32_t mid_max) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngroups) return;
-  const uint32_t n = gstart[g + 1] - gstart[g];
-  const int cls = n <= tiny_max ? 0 : (n <= mid_max ? 1 : 2);
-  const uint32_t k = atomicAdd(&counts[cls], 1u);
-  lists[static_cast<uint64_t>(cls) * ngroups + k] = g;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  int cls = -1;
+  if (g < ngroups) {
+    const uint32_t n = gstart[g + 1] - gstart[g];
+    cls = n <= kTinyMax ? 0 : (n <= kSmallMax ? 1 : (n <= mid_max ? 2 : 3));
+  }
+  // Wave-aggregated list appends: one atomic per class per wave.
+#pragma unroll
+  for (int c = 0; c < kNumClasses; ++c) {
+    const unsigned long long m = __ballot(cls == c);
+    if (!m) continue;
+    const int leader = __ffsll(static_cast<long long>(m)) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&counts[c], static_cast<uint32_t>(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    if (cls == c) lists[static_cast<uint64_t>(c) * ngroups + base + __popcll(m & lanemask_lt)] = g;
+  }
 }
 
 __device__ __forceinline__ uint64_t BitonicStepWave(uint64_t x, int lane, int k, int j) {
@@ -298,6 +372,64 @@ __global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restric
   if (lane < 7) out[static_cast<uint64_t>(g) * 7 + lane] = res;
 }
 
+// Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per group with 64 < n <= 1024: bitonic sort in the wave's LDS slice, singleton
+// digest (W <= 1024 <= kSingletonMaxW).  Waves of a workgroup work on different groups and
+// never meet at a barrier.
+constexpr int kSmallWaves = 4;
+__global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restrict__ list, uint32_t nlist,
+                                                        const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
+                                                        int arg_type, double* __restrict__ out) {
+  __shared__ uint64_t keys[kSmallWaves][kSmallMax];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t li = blockIdx.x * kSmallWaves + wid;
+  if (li >= nlist) return;
+  uint64_t* a = keys[wid];
+  const uint32_t g = list[li];
+  const uint32_t s = gstart[g];
+  const int n = static_cast<int>(gstart[g + 1] - s);
+  int P = 128;
+  while (P < n) P <<= 1;
+  uint64_t cv = 0, cneg = 0;
+  for (int i = lane; i < P; i += 64) {
+    uint64_t k = ~0ULL;
+    if (i < n) {
+      k = QKey(vals[s + i], arg_type);
+      cv += (k >= kNegInfKey && k <= kPosInfKey) ? 1 : 0;
+      cneg += k < kNegInfKey ? 1 : 0;
+    }
+    a[i] = k;
+  }
+  const int64_t W = static_cast<int64_t>(WaveSumU64(cv));
+  const int64_t lead = static_cast<int64_t>(WaveSumU64(cneg));
+  WaveSync();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = lane; t < (P >> 1); t += 64) {
+        const int lo = 2 * t - (t & (j - 1));
+        const int hi = lo + j;
+        const uint64_t x = a[lo], y = a[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          a[lo] = y;
+          a[hi] = x;
+        }
+      }
+      WaveSync();
+    }
+  }
+  if (lane < 7) {
+    out[static_cast<uint64_t>(g) * 7 + lane] =
+        W == 0 ? __longlong_as_double(0x7FF8000000000000LL)
+               : SingletonQuantile(kQuantileQ[lane], W, [&](int64_t j) -> double { return QVal(a[lead + j]); });
+  }
+}
+
 constexpr int kMidMax = 4096;
 constexpr int kMidCentroids = 2048;
 
@@ -332,52 +464,99 @@ __device__ __forceinline__ int64_t LowerBoundKey(Acc a, int64_t n, uint64_t key)
   return lo;
 }
 
-// Digest of a sorted key array accessible through `keyat` (block-cooperative).
+// Digest of a sorted key array accessible through `keyat` (block-cooperative).  Only the
+// centroid means tdigest::quantile() reads are computed (<= 4 per quantile): a recording pass
+// of DigestQuantile lists them (its control flow depends on positions only, never on means),
+// then each is computed — the reference's incremental mean for centroids of <= kSeqMean
+// values (every centroid while W <= ~10000), sum/count cooperatively for larger ones.
+constexpr int kNeed = 7 * 4;
+constexpr int64_t kSeqMean = 16;
+
+struct DigestShared {
+  int64_t meta[4];
+  int32_t need[kNeed];
+  double mean[kNeed];
+  double red[4];
+};
+
 template <typename KeyAt>
-__device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, double* means, int64_t max_c, double* out7,
-                            unsigned int* err, int64_t* s_meta) {
+__device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, int64_t max_c, double* out7, unsigned int* err,
+                            DigestShared& sh) {
+  const int t = threadIdx.x;
   // trim NaNs: keys < kNegInfKey (negative NaN) at the front, > kPosInfKey at the back
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     const int64_t lead = LowerBoundKey(keyat, n, kNegInfKey);
     const int64_t tail = LowerBoundKey(keyat, n, kPosInfKey + 1);
-    s_meta[0] = lead;
-    s_meta[1] = tail - lead;
+    sh.meta[0] = lead;
+    sh.meta[1] = tail - lead;
   }
   __syncthreads();
-  const int64_t lead = s_meta[0], W = s_meta[1];
+  const int64_t lead = sh.meta[0], W = sh.meta[1];
   auto val = [&](int64_t j) -> double { return QVal(keyat(lead + j)); };
   if (W <= kSingletonMaxW) {
-    if (threadIdx.x < 7) out7[threadIdx.x] = W == 0 ? __longlong_as_double(0x7FF8000000000000LL) : SingletonQuantile(kQuantileQ[threadIdx.x], W, val);
+    if (t < 7) out7[t] = W == 0 ? __longlong_as_double(0x7FF8000000000000LL) : SingletonQuantile(kQuantileQ[t], W, val);
     __syncthreads();
     return;
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     const int64_t nc = DigestBoundaries(W, starts, max_c);
     if (nc < 0) atomicExch(err, 1u);
-    s_meta[2] = nc < 0 ? 0 : nc;
+    sh.meta[2] = nc < 0 ? 0 : nc;
+  }
+  if (t < kNeed) sh.need[t] = -1;
+  __syncthreads();
+  const int64_t nc = sh.meta[2];
+  auto start = [&](int64_t j) -> int64_t { return starts[j]; };
+  auto cend = [&](int64_t j) -> int64_t { return j + 1 < nc ? starts[j + 1] : W; };
+  if (t < 7) {
+    int k = 0;
+    (void)DigestQuantile(kQuantileQ[t], nc, W, start, [&](int64_t j) -> double {
+      if (k < 4) sh.need[t * 4 + k] = static_cast<int32_t>(j);
+      ++k;
+      return 0.0;
+    });
   }
   __syncthreads();
-  const int64_t nc = s_meta[2];
-  for (int64_t j = threadIdx.x; j < nc; j += blockDim.x) {
-    const int64_t st = starts[j], en = j + 1 < nc ? starts[j + 1] : W;
-    means[j] = CentroidMean(val, st, en);
+  if (t < kNeed && sh.need[t] >= 0) {
+    const int64_t j = sh.need[t], s = start(j), e = cend(j);
+    if (e - s <= kSeqMean) sh.mean[t] = CentroidMean(val, s, e);
+  }
+  for (int i = 0; i < kNeed; ++i) {  // uniform loop: large centroids, block sum
+    const int64_t j = sh.need[i];
+    if (j < 0) continue;
+    const int64_t s = start(j), e = cend(j);
+    if (e - s <= kSeqMean) continue;
+    double acc = 0;
+    for (int64_t x = s + t; x < e; x += blockDim.x) acc += val(x);
+    acc = WaveSumF64(acc);
+    if ((t & 63) == 0) sh.red[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0;
+      for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) tot += sh.red[w];
+      sh.mean[i] = tot / static_cast<double>(e - s);
+    }
+    __syncthreads();
   }
   __syncthreads();
-  if (threadIdx.x < 7) {
-    out7[threadIdx.x] = DigestQuantile(
-        kQuantileQ[threadIdx.x], nc, W, [&](int64_t j) -> int64_t { return starts[j]; }, [&](int64_t j) -> double { return means[j]; });
+  if (t < 7) {
+    int k = 0;
+    out7[t] = DigestQuantile(kQuantileQ[t], nc, W, start, [&](int64_t) -> double {
+      const double m = sh.mean[t * 4 + (k < 4 ? k : 3)];
+      ++k;
+      return m;
+    });
   }
   __syncthreads();
 }
 
-// One workgroup per group with 64 < n <= 4096: LDS bitonic sort + digest.
+// One workgroup per group with 1024 < n <= 4096: LDS bitonic sort + digest.
 __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
                                                       const uint64_t* __restrict__ vals, int arg_type, double* __restrict__ out,
                                                       unsigned int* __restrict__ err) {
   __shared__ uint64_t keys[kMidMax];
   __shared__ uint32_t starts[kMidCentroids];
-  __shared__ double means[kMidCentroids];
-  __shared__ int64_t meta[4];
+  __shared__ DigestShared sh;
   const uint32_t g = list[blockIdx.x];
   const uint32_t s = gstart[g], n = gstart[g + 1] - s;
   int P = 64;
@@ -385,8 +564,7 @@ __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict
   for (int i = threadIdx.x; i < P; i += blockDim.x) keys[i] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
   __syncthreads();
   BitonicSortLds(keys, P);
-  BlockDigest([&](int64_t i) -> uint64_t { return keys[i]; }, n, starts, means, kMidCentroids, out + static_cast<uint64_t>(g) * 7, err,
-              meta);
+  BlockDigest([&](int64_t i) -> uint64_t { return keys[i]; }, n, starts, kMidCentroids, out + static_cast<uint64_t>(g) * 7, err, sh);
 }
 
 // Big groups: chunk sort (one workgroup per 4096-element chunk) into sort keys.
@@ -456,15 +634,14 @@ __global__ void BigMergeKernel(const BigGroup* __restrict__ groups, uint32_t ngr
 constexpr int kBigCentroids = 8192;
 
 __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restrict__ groups, const uint64_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ starts_all, double* __restrict__ means_all,
-                                                       double* __restrict__ out, unsigned int* __restrict__ err) {
-  __shared__ int64_t meta[4];
+                                                       uint32_t* __restrict__ starts_all, double* __restrict__ out,
+                                                       unsigned int* __restrict__ err) {
+  __shared__ DigestShared sh;
   const BigGroup G = groups[blockIdx.x];
   uint32_t* starts = starts_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
-  double* means = means_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
   const uint64_t* k = keys + G.off;
-  BlockDigest([&](int64_t i) -> uint64_t { return k[i]; }, static_cast<int64_t>(G.n), starts, means, kBigCentroids,
-              out + static_cast<uint64_t>(G.g) * 7, err, meta);
+  BlockDigest([&](int64_t i) -> uint64_t { return k[i]; }, static_cast<int64_t>(G.n), starts, kBigCentroids,
+              out + static_cast<uint64_t>(G.g) * 7, err, sh);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -521,62 +698,70 @@ static int Log2Ceil(uint64_t x) {
   return b;
 }
 
+// meta: u64 [0] rows with a valid slot | u32 @8 groups | u32 @16 digest error | u32 @32.. class counts
+__global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<unsigned long long*>(meta) = n;
+    *reinterpret_cast<uint32_t*>(meta + 8) = 0;
+    *reinterpret_cast<uint32_t*>(meta + 16) = 0;
+    for (int c = 0; c < kNumClasses; ++c) reinterpret_cast<uint32_t*>(meta + 32)[c] = 0;
+  }
+}
+
 int32_t AggFinalizeImpl(Agg* a) {
   Ctx* ctx = a->ctx;
   AggResult& R = a->res;
-  R = AggResult();
+  Agg::FinalizeWs& ws = a->ws;
+  R.Clear();
   const uint64_t n = a->st_n;
   if (n == 0) {
-    R.n_groups = 0;
     R.ready = true;
     return PXG_OK;
   }
   if (n >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
+  PXG_RETURN_IF_ERROR(ws.meta.Ensure(64));
+  uint8_t* meta = ws.meta.as<uint8_t>();
+  unsigned long long* d_nvalid = reinterpret_cast<unsigned long long*>(meta);
+  uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta + 8);
+  unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 16);
+  uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta + 32);
+  PXG_RETURN_IF_ERROR(Launch(ctx, "finalize_init", FinalizeInitKernel, dim3(1), dim3(64), 0, meta, n));
+
   // 1. Stable LSD radix sort of (slot, vals...) by slot; deferred (invalid) slots map to cap.
+  //    The alternate buffers match the staging capacity so the swap keeps both usable.
   const int nbits = Log2Ceil(static_cast<uint64_t>(a->cap) + 1);
   const int passes = (nbits + kRadixBits - 1) / kRadixBits;
   const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
-  DevBuf alt_slot, hist, tmp;
-  DevBuf alt_val[kMaxVals];
-  PXG_RETURN_IF_ERROR(alt_slot.Alloc(n * 4));
-  for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(alt_val[v].Alloc(n * 8));
+  const uint64_t cap_rows = std::max<uint64_t>(a->st_cap, n);
+  PXG_RETURN_IF_ERROR(ws.alt_slot.Ensure(cap_rows * 4));
+  for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(ws.alt_val[v].Ensure(cap_rows * 8));
   const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
-  PXG_RETURN_IF_ERROR(hist.Alloc(nh * 4 + 64));
-  const size_t scan_bytes = ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(nh, n)));
-  PXG_RETURN_IF_ERROR(tmp.Alloc(scan_bytes + 64));
+  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
+  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(nh, n))) + 64));
+  void* scan_tmp = ws.scan.p;
   for (int p = 0; p < passes; ++p) {
     const int shift = p * kRadixBits;
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, a->st_slot.as<const uint32_t>(), n,
-                               a->cap, shift, hist.as<uint32_t>(), nblocks));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, hist.as<uint32_t>(), hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, tmp.p));
+                               a->cap, shift, ws.hist.as<uint32_t>(), nblocks));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, scan_tmp));
     ConstValPtrs vin;
     ValPtrs vout;
     for (int v = 0; v < kMaxVals; ++v) {
       vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
-      vout.p[v] = v < a->n_vals ? alt_val[v].as<uint64_t>() : nullptr;
+      vout.p[v] = v < a->n_vals ? ws.alt_val[v].as<uint64_t>() : nullptr;
     }
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0,
-                               a->st_slot.as<const uint32_t>(), alt_slot.as<uint32_t>(), vin, vout, a->n_vals, n, a->cap, shift,
-                               hist.as<const uint32_t>(), nblocks));
-    std::swap(a->st_slot, alt_slot);
-    for (int v = 0; v < a->n_vals; ++v) std::swap(a->st_val[v], alt_val[v]);
+                               a->st_slot.as<const uint32_t>(), ws.alt_slot.as<uint32_t>(), vin, vout, a->n_vals, n, a->cap, shift,
+                               ws.hist.as<const uint32_t>(), nblocks));
+    std::swap(a->st_slot, ws.alt_slot);
+    for (int v = 0; v < a->n_vals; ++v) std::swap(a->st_val[v], ws.alt_val[v]);
   }
   // 2. Runs -> groups.
-  DevBuf flags, gidx, meta;
-  PXG_RETURN_IF_ERROR(flags.Alloc(n * 4));
-  PXG_RETURN_IF_ERROR(gidx.Alloc(n * 4));
-  PXG_RETURN_IF_ERROR(meta.Alloc(64));
-  unsigned long long* d_nvalid = meta.as<unsigned long long>();
-  uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta.as<uint8_t>() + 8);
-  unsigned int* d_err = reinterpret_cast<unsigned int*>(meta.as<uint8_t>() + 16);
-  uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta.as<uint8_t>() + 32);
-  {
-    uint64_t init[8] = {n, 0, 0, 0, 0, 0, 0, 0};
-    PXG_HIP(hipMemcpy(meta.p, init, 64, hipMemcpyHostToDevice));  // fresh buffer: synchronous copy
-  }
+  PXG_RETURN_IF_ERROR(ws.flags.Ensure(n * 4));
+  PXG_RETURN_IF_ERROR(ws.gidx.Ensure(n * 4));
   PXG_RETURN_IF_ERROR(Launch(ctx, "run_heads", RunHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             a->st_slot.as<const uint32_t>(), n, a->cap, flags.as<uint32_t>(), d_nvalid));
-  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, flags.as<const uint32_t>(), gidx.as<uint32_t>(), static_cast<int64_t>(n), d_ngroups, tmp.p));
+                             a->st_slot.as<const uint32_t>(), n, a->cap, ws.flags.as<uint32_t>(), d_nvalid));
+  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.flags.as<const uint32_t>(), ws.gidx.as<uint32_t>(), static_cast<int64_t>(n), d_ngroups, scan_tmp));
   uint32_t ngroups = 0;
   PXG_HIP(hipMemcpyAsync(&ngroups, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
@@ -585,45 +770,59 @@ int32_t AggFinalizeImpl(Agg* a) {
     R.ready = true;
     return PXG_OK;
   }
-  DevBuf gstart, gslot;
-  PXG_RETURN_IF_ERROR(gstart.Alloc((static_cast<size_t>(ngroups) + 1) * 4));
-  PXG_RETURN_IF_ERROR(gslot.Alloc(static_cast<size_t>(ngroups) * 4));
+  PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
+  PXG_RETURN_IF_ERROR(ws.gslot.Ensure(static_cast<size_t>(ngroups) * 4));
+  const uint32_t* gstart = ws.gstart.as<const uint32_t>();
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_starts", GroupStartsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             a->st_slot.as<const uint32_t>(), flags.as<const uint32_t>(), gidx.as<const uint32_t>(), n,
-                             gstart.as<uint32_t>(), gslot.as<uint32_t>(), static_cast<const unsigned long long*>(d_nvalid), ngroups));
-  // 3. UDA reductions.
+                             a->st_slot.as<const uint32_t>(), ws.flags.as<const uint32_t>(), ws.gidx.as<const uint32_t>(), n,
+                             ws.gstart.as<uint32_t>(), ws.gslot.as<uint32_t>(), static_cast<const unsigned long long*>(d_nvalid), ngroups));
+  // 3. UDA reductions (chunk partials, then per-group combine).
   ConstValPtrs cv;
   for (int v = 0; v < kMaxVals; ++v) cv.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
   UdaOut uo;
   for (int u = 0; u < kMaxUdas; ++u) uo.p[u] = nullptr;
+  bool any_q = false, any_red = false;
   for (int u = 0; u < a->n_udas; ++u) {
-    const size_t per = a->uda_kind[u] == PXG_UDA_QUANTILES ? 7 * 8 : 8;
-    PXG_RETURN_IF_ERROR(R.uda_out[u].Alloc(static_cast<size_t>(ngroups) * per));
+    const bool q = a->uda_kind[u] == PXG_UDA_QUANTILES;
+    any_q |= q;
+    any_red |= !q && a->uda_kind[u] != PXG_UDA_COUNT;
+    PXG_RETURN_IF_ERROR(R.uda_out[u].Ensure(static_cast<size_t>(ngroups) * (q ? 7 * 8 : 8)));
     uo.p[u] = R.uda_out[u].as<uint64_t>();
   }
-  PXG_RETURN_IF_ERROR(Launch(ctx, "uda_reduce", UdaReduceKernel, dim3(GridFor(static_cast<int64_t>(ngroups) * 64, 256, ctx->num_cus * 16)),
-                             dim3(256), 0, a->d_plan.as<const AggPlanDev>(), gstart.as<const uint32_t>(), ngroups, cv, uo));
+  PXG_RETURN_IF_ERROR(ws.cbase.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
+  uint32_t* cbase = ws.cbase.as<uint32_t>();
+  const uint64_t max_chunks = static_cast<uint64_t>(ngroups) + n / kRedChunk + 1;
+  if (any_red) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "group_chunk_count", GroupChunkCountKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
+                               ngroups, cbase));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
+    PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 8));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceKernel, dim3(static_cast<unsigned>((max_chunks * 64 + 255) / 256)), dim3(256), 0,
+                               a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups, cv,
+                               ws.partial.as<uint64_t>(), max_chunks));
+  }
+  PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                             a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups,
+                             ws.partial.as<const uint64_t>(), max_chunks, uo));
   // 4. Quantile digests.
-  bool any_q = false;
-  for (int u = 0; u < a->n_udas; ++u) any_q |= a->uda_kind[u] == PXG_UDA_QUANTILES;
   if (any_q) {
-    DevBuf lists;
-    PXG_RETURN_IF_ERROR(lists.Alloc(static_cast<size_t>(ngroups) * 3 * 4));
-    PXG_HIP(hipMemsetAsync(d_cls, 0, 12, ctx->stream));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               gstart.as<const uint32_t>(), ngroups, lists.as<uint32_t>(), d_cls, 64u, static_cast<uint32_t>(kMidMax)));
-    uint32_t cls[3];
-    PXG_HIP(hipMemcpyAsync(cls, d_cls, 12, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
+                               ngroups, ws.lists.as<uint32_t>(), d_cls, static_cast<uint32_t>(kMidMax)));
+    uint32_t cls[kNumClasses];
+    PXG_HIP(hipMemcpyAsync(cls, d_cls, sizeof(cls), hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));
+    const uint32_t* lists = ws.lists.as<const uint32_t>();
     // Big-group metadata (host side; few groups).
     std::vector<BigGroup> big;
     std::vector<BigChunk> bchunks;
     uint64_t big_total = 0, big_max = 0;
-    if (cls[2] > 0) {
-      std::vector<uint32_t> bl(cls[2]);
-      PXG_HIP(hipMemcpy(bl.data(), lists.as<uint32_t>() + 2 * static_cast<uint64_t>(ngroups), cls[2] * 4, hipMemcpyDeviceToHost));
+    if (cls[3] > 0) {
+      std::vector<uint32_t> bl(cls[3]);
+      PXG_HIP(hipMemcpy(bl.data(), lists + 3 * static_cast<uint64_t>(ngroups), cls[3] * 4, hipMemcpyDeviceToHost));
       std::vector<uint32_t> gs(static_cast<size_t>(ngroups) + 1);
-      PXG_HIP(hipMemcpy(gs.data(), gstart.p, gs.size() * 4, hipMemcpyDeviceToHost));
+      PXG_HIP(hipMemcpy(gs.data(), gstart, gs.size() * 4, hipMemcpyDeviceToHost));
+      std::sort(bl.begin(), bl.end());
       for (uint32_t g : bl) {
         BigGroup B;
         B.off = gs[g];
@@ -642,17 +841,13 @@ int32_t AggFinalizeImpl(Agg* a) {
           bchunks.push_back(c);
         }
       }
-    }
-    DevBuf d_big, d_bchunks, keysA, keysB, bstarts, bmeans;
-    if (!big.empty()) {
-      PXG_RETURN_IF_ERROR(d_big.Alloc(big.size() * sizeof(BigGroup)));
-      PXG_HIP(hipMemcpy(d_big.p, big.data(), big.size() * sizeof(BigGroup), hipMemcpyHostToDevice));
-      PXG_RETURN_IF_ERROR(d_bchunks.Alloc(bchunks.size() * sizeof(BigChunk)));
-      PXG_HIP(hipMemcpy(d_bchunks.p, bchunks.data(), bchunks.size() * sizeof(BigChunk), hipMemcpyHostToDevice));
-      PXG_RETURN_IF_ERROR(keysA.Alloc(n * 8));
-      PXG_RETURN_IF_ERROR(keysB.Alloc(n * 8));
-      PXG_RETURN_IF_ERROR(bstarts.Alloc(big.size() * kBigCentroids * 4));
-      PXG_RETURN_IF_ERROR(bmeans.Alloc(big.size() * kBigCentroids * 8));
+      PXG_RETURN_IF_ERROR(ws.big.Ensure(big.size() * sizeof(BigGroup)));
+      PXG_HIP(hipMemcpy(ws.big.p, big.data(), big.size() * sizeof(BigGroup), hipMemcpyHostToDevice));
+      PXG_RETURN_IF_ERROR(ws.bchunks.Ensure(bchunks.size() * sizeof(BigChunk)));
+      PXG_HIP(hipMemcpy(ws.bchunks.p, bchunks.data(), bchunks.size() * sizeof(BigChunk), hipMemcpyHostToDevice));
+      PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
+      PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
+      PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(big.size() * kBigCentroids * 4));
     }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
@@ -660,32 +855,28 @@ int32_t AggFinalizeImpl(Agg* a) {
       const int at = a->uda_arg_type[u];
       double* qo = R.uda_out[u].as<double>();
       if (cls[0] > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((cls[0] + 3) / 4), dim3(256), 0, lists.as<const uint32_t>(),
-                                   cls[0], gstart.as<const uint32_t>(), vals, at, qo));
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((cls[0] + 3) / 4), dim3(256), 0, lists, cls[0], gstart, vals, at, qo));
       if (cls[1] > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[1]), dim3(256), 0,
-                                   lists.as<const uint32_t>() + static_cast<uint64_t>(ngroups), gstart.as<const uint32_t>(), vals, at, qo,
-                                   d_err));
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_small", QuantSmallKernel, dim3((cls[1] + kSmallWaves - 1) / kSmallWaves), dim3(256), 0,
+                                   lists + static_cast<uint64_t>(ngroups), cls[1], gstart, vals, at, qo));
+      if (cls[2] > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
+                                   gstart, vals, at, qo, d_err));
       if (!big.empty()) {
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(static_cast<unsigned>(bchunks.size())), dim3(256), 0,
-                                   d_bchunks.as<const BigChunk>(), vals, at, keysA.as<uint64_t>()));
-        DevBuf* src = &keysA;
-        DevBuf* dst = &keysB;
+                                   ws.bchunks.as<const BigChunk>(), vals, at, ws.keysA.as<uint64_t>()));
+        DevBuf* src = &ws.keysA;
+        DevBuf* dst = &ws.keysB;
         for (uint64_t w = kMidMax; w < big_max; w *= 2) {
           PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeKernel, dim3(GridFor(static_cast<int64_t>(big_total), 256, 1 << 30)),
-                                     dim3(256), 0, d_big.as<const BigGroup>(), static_cast<uint32_t>(big.size()), big_total,
+                                     dim3(256), 0, ws.big.as<const BigGroup>(), static_cast<uint32_t>(big.size()), big_total,
                                      src->as<const uint64_t>(), dst->as<uint64_t>(), w));
           std::swap(src, dst);
         }
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(static_cast<unsigned>(big.size())), dim3(256), 0,
-                                   d_big.as<const BigGroup>(), src->as<const uint64_t>(), bstarts.as<uint32_t>(), bmeans.as<double>(), qo,
-                                   d_err));
+                                   ws.big.as<const BigGroup>(), src->as<const uint64_t>(), ws.bstarts.as<uint32_t>(), qo, d_err));
       }
     }
-    unsigned int err = 0;
-    PXG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
-    if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
   }
   // 5. Keys.
   KeyOutDev ko;
@@ -696,31 +887,42 @@ int32_t AggFinalizeImpl(Agg* a) {
   for (int k = 0; k < a->n_keys; ++k) {
     const int t = a->key_types[k];
     if (t == PXG_STRING) {
-      PXG_RETURN_IF_ERROR(R.key_offsets[k].Alloc((static_cast<size_t>(ngroups) + 1) * 4));
+      PXG_RETURN_IF_ERROR(R.key_offsets[k].Ensure((static_cast<size_t>(ngroups) + 1) * 4));
       ko.len[k] = R.key_offsets[k].as<uint32_t>();
     } else {
-      PXG_RETURN_IF_ERROR(R.key_fixed[k].Alloc(static_cast<size_t>(ngroups) * (t == PXG_UINT128 ? 16 : 8)));
+      PXG_RETURN_IF_ERROR(R.key_fixed[k].Ensure(static_cast<size_t>(ngroups) * (t == PXG_UINT128 ? 16 : 8)));
       ko.fixed[k] = R.key_fixed[k].as<uint64_t>();
     }
   }
   if (a->n_keys > 0) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), gslot.as<const uint32_t>(), ngroups,
+                               a->d_plan.as<const AggPlanDev>(), static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
                                a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
   }
+  int n_str = 0;
   for (int k = 0; k < a->n_keys; ++k) {
     if (a->key_types[k] != PXG_STRING) continue;
     uint32_t* off = R.key_offsets[k].as<uint32_t>();
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, ngroups, off + ngroups, tmp.p));
-    uint32_t total = 0;
-    PXG_HIP(hipMemcpyAsync(&total, off + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
-    R.key_data_len[k] = total;
-    PXG_RETURN_IF_ERROR(R.key_data[k].Alloc(static_cast<size_t>(total) + 16));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, ngroups, off + ngroups, scan_tmp));
+    ++n_str;
+  }
+  // One sync for the digest error flag and every string-key total.
+  std::vector<uint32_t> totals(kMaxKeys, 0);
+  unsigned int err = 0;
+  for (int k = 0; k < a->n_keys; ++k)
+    if (a->key_types[k] == PXG_STRING)
+      PXG_HIP(hipMemcpyAsync(&totals[k], R.key_offsets[k].as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
+  for (int k = 0; k < a->n_keys && n_str > 0; ++k) {
+    if (a->key_types[k] != PXG_STRING) continue;
+    R.key_data_len[k] = totals[k];
+    PXG_RETURN_IF_ERROR(R.key_data[k].Ensure(static_cast<size_t>(totals[k]) + 16));
     PXG_RETURN_IF_ERROR(Launch(ctx, "key_string_copy", KeyStringCopyKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), k, gslot.as<const uint32_t>(), ngroups,
-                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), static_cast<const uint32_t*>(off),
-                               R.key_data[k].as<uint8_t>()));
+                               a->d_plan.as<const AggPlanDev>(), k, static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
+                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(),
+                               static_cast<const uint32_t*>(R.key_offsets[k].as<uint32_t>()), R.key_data[k].as<uint8_t>()));
   }
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   R.ready = true;

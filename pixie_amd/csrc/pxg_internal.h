@@ -78,6 +78,8 @@ struct DevBuf {
     bytes = cap;
     return PXG_OK;
   }
+  // Grow-only scratch: capacity >= n, contents not preserved.
+  int32_t Ensure(size_t n) { return Reserve(n, 0, nullptr); }
   template <typename T>
   T* as() const { return static_cast<T*>(p); }
 };
