@@ -26,7 +26,9 @@ SEED = 20250117
 KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "radix_hist", "radix_scatter",
            "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
            "quant_tiny", "quant_small", "quant_mid", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
-           "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep"]
+           "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",
+           "export_slot_part", "export_group_rank", "export_row_digit", "export_write_groups", "export_write_rows",
+           "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows"]
 
 
 def parse():
@@ -34,11 +36,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--rows-per-gpu", type=int, default=None,
+                    help="default: 100M at N=1 (configs[1], C2); 125M per GPU at N>1 (configs[3], C4: 1B rows at N=8)")
     ap.add_argument("--gen-slice", type=int, default=16_000_000)
-    ap.add_argument("--cpu-sample-rows", type=int, default=3_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=160_000_000)
     ap.add_argument("--cpu-batch-rows", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--share-gpu0", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (with --backend gloo on a 1-GPU box)")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"))
     return ap.parse_args()
 
@@ -55,16 +61,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    if args.share_gpu0:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(args.backend, init_method="env://")
 
     from pixie_amd import plans as P
     from pixie_amd.device import Ctx, Table, datagen_http_events
     from pixie_amd.pipeline import LinearQuery
     from pixie_amd.dist import exchange_partials
 
-    n = args.rows_per_gpu
+    n = args.rows_per_gpu or (100_000_000 if world == 1 else 125_000_000)
     row0 = rank * n
     ctx = Ctx(local_rank)
     table = Table(ctx, P.HTTP_TYPES)
@@ -90,7 +98,7 @@ def main():
         agg.reset()
         agg.consume(table)
         if world > 1:
-            exchange_partials(agg, world, rank, ctx)
+            exchange_partials(agg)
         return agg.finalize()
 
     for _ in range(args.warmup):
@@ -112,7 +120,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     ctx.set_profiling(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     launches, cons_ms = ctx.kernel_stats("agg_consume")
@@ -187,21 +195,35 @@ def main():
 
 def cpu_baseline(args):
     """The CPU Carnot restatement (oracle/, single thread) on a bounded sample of the same
-    workload: the first cpu_sample_rows rows as RowBatches of cpu_batch_rows rows."""
+    workload: the first cpu_sample_rows rows of the same synthetic table, as RowBatches of
+    cpu_batch_rows rows, C2 plan.  Columns the plan does not read are not materialised."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     try:
         import oracle_client as oc
         from pixie_amd import plans as P
         from pixie_amd.device import datagen_http_events
         m = args.cpu_sample_rows
-        cols = datagen_http_events(SEED, 0, m, n_pair_keys=10_000_000, threads=16)
-        br = args.cpu_batch_rows
-        batches = [[c.slice(a, min(a + br, m)) for c in cols] for a in range(0, m, br)]
+        need = {P.HE["service"], P.HE["req_path"], P.HE["resp_status"], P.HE["latency"]}
+        batches = []
+        for a in range(0, m, args.gen_slice):
+            k = min(args.gen_slice, m - a)
+            cols = datagen_http_events(SEED, a, k, n_pair_keys=10_000_000, threads=16)
+            batches.append([c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)])
+            del cols
         tables = {"http_events": {"types": P.HTTP_TYPES, "batches": batches, "names": P.HTTP_NAMES}}
-        secs, _ = oc.time_plan(P.c2_plan(with_pluck=True), tables)
+        secs, _ = oc.time_plan(P.c2_plan(with_pluck=True), tables, batch_rows=args.cpu_batch_rows)
+        cpu_model = ""
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
         return {"value": m / secs, "unit": "rows/s", "cores": 1, "kind": "port",
-                "sample": f"first {m} rows of the same synthetic table as {br}-row RowBatches, C2 plan, "
-                          f"1 thread; {secs:.2f} s (execution window only, as in BASELINE.md)"}
+                "sample": f"first {m} rows of the same synthetic table as {args.cpu_batch_rows}-row RowBatches, C2 plan, "
+                          f"1 thread of {cpu_model or 'host CPU'}; {secs:.2f} s execution window (first GenerateNext .. "
+                          f"last emit, BASELINE.md); CPU Carnot restated in oracle/ (reference unbuildable, SURVEY.md §8c)"}
     except Exception as e:  # the baseline must never break the bench line
         return {"value": None, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
 

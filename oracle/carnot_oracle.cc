@@ -1068,7 +1068,10 @@ struct Graph {
   }
 };
 
-static std::map<std::string, TableIn> ImportTables(int32_t ntables, const oracle_table* tables) {
+// Given batches are re-sliced into RowBatches of batch_rows rows when batch_rows > 0 (the
+// carnot_executable --rowbatch_size knob, carnot_executable.cc:46-47).  A column given with no
+// buffers (values, offsets and data all null) is never read by the plan: it stays empty.
+static std::map<std::string, TableIn> ImportTables(int32_t ntables, const oracle_table* tables, int64_t batch_rows = 0) {
   std::map<std::string, TableIn> out;
   for (int32_t t = 0; t < ntables; ++t) {
     const oracle_table& ot = tables[t];
@@ -1078,37 +1081,50 @@ static std::map<std::string, TableIn> ImportTables(int32_t ntables, const oracle
       ti.types.push_back(static_cast<DT>(ot.col_types[c]));
     }
     for (int32_t b = 0; b < ot.nbatches; ++b) {
-      RowBatch rb;
+      int64_t n = -1;
       for (int32_t c = 0; c < ot.ncols; ++c) {
         const oracle_column& oc = ot.cols[static_cast<size_t>(b) * ot.ncols + c];
-        auto col = std::make_shared<Col>(static_cast<DT>(oc.type));
-        int64_t n = oc.length;
-        rb.num_rows = n;
-        switch (col->type) {
-          case BOOLEAN: col->b.assign(static_cast<const uint8_t*>(oc.values), static_cast<const uint8_t*>(oc.values) + n); break;
-          case INT64:
-          case TIME64NS: col->i.assign(static_cast<const int64_t*>(oc.values), static_cast<const int64_t*>(oc.values) + n); break;
-          case FLOAT64: col->f.assign(static_cast<const double*>(oc.values), static_cast<const double*>(oc.values) + n); break;
-          case UINT128: {
-            const uint64_t* p = static_cast<const uint64_t*>(oc.values);
-            for (int64_t r = 0; r < n; ++r) col->u.push_back(U128{p[2 * r], p[2 * r + 1]});
-            break;
+        if (oc.values || oc.offsets || oc.data) n = oc.length;
+      }
+      if (n < 0) n = 0;
+      const int64_t step = (batch_rows > 0 && !ot.batch_flags) ? batch_rows : std::max<int64_t>(n, 1);
+      for (int64_t r0 = 0; r0 < n || (n == 0 && r0 == 0); r0 += step) {
+        const int64_t r1 = std::min(n, r0 + step);
+        RowBatch rb;
+        rb.num_rows = r1 - r0;
+        for (int32_t c = 0; c < ot.ncols; ++c) {
+          const oracle_column& oc = ot.cols[static_cast<size_t>(b) * ot.ncols + c];
+          auto col = std::make_shared<Col>(static_cast<DT>(oc.type));
+          const bool present = oc.values || oc.offsets || oc.data;
+          if (present) {
+            switch (col->type) {
+              case BOOLEAN: col->b.assign(static_cast<const uint8_t*>(oc.values) + r0, static_cast<const uint8_t*>(oc.values) + r1); break;
+              case INT64:
+              case TIME64NS: col->i.assign(static_cast<const int64_t*>(oc.values) + r0, static_cast<const int64_t*>(oc.values) + r1); break;
+              case FLOAT64: col->f.assign(static_cast<const double*>(oc.values) + r0, static_cast<const double*>(oc.values) + r1); break;
+              case UINT128: {
+                const uint64_t* p = static_cast<const uint64_t*>(oc.values);
+                for (int64_t r = r0; r < r1; ++r) col->u.push_back(U128{p[2 * r], p[2 * r + 1]});
+                break;
+              }
+              case STRING:
+                col->s.reserve(r1 - r0);
+                for (int64_t r = r0; r < r1; ++r)
+                  col->s.emplace_back(reinterpret_cast<const char*>(oc.data) + oc.offsets[r], oc.offsets[r + 1] - oc.offsets[r]);
+                break;
+              default: throw Error(INVALID_ARGUMENT, "bad column type");
+            }
           }
-          case STRING:
-            col->s.reserve(n);
-            for (int64_t r = 0; r < n; ++r)
-              col->s.emplace_back(reinterpret_cast<const char*>(oc.data) + oc.offsets[r], oc.offsets[r + 1] - oc.offsets[r]);
-            break;
-          default: throw Error(INVALID_ARGUMENT, "bad column type");
+          rb.cols.push_back(col);
         }
-        rb.cols.push_back(col);
+        if (ot.batch_flags) {
+          rb.eow = (ot.batch_flags[b] & 1) != 0;
+          rb.eos = (ot.batch_flags[b] & 2) != 0;
+          ti.explicit_flags = true;
+        }
+        ti.batches.push_back(std::move(rb));
+        if (n == 0) break;
       }
-      if (ot.batch_flags) {
-        rb.eow = (ot.batch_flags[b] & 1) != 0;
-        rb.eos = (ot.batch_flags[b] & 2) != 0;
-        ti.explicit_flags = true;
-      }
-      ti.batches.push_back(std::move(rb));
     }
     out[ot.name] = std::move(ti);
   }
@@ -1196,9 +1212,15 @@ extern "C" int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, c
 
 extern "C" int32_t oracle_execute_plan_timed(const char* plan_json, int32_t ntables, const oracle_table* tables,
                                              double* seconds, int64_t* out_rows, char* errbuf, int32_t errlen) {
+  return oracle_execute_plan_timed_rebatched(plan_json, ntables, tables, 0, seconds, out_rows, errbuf, errlen);
+}
+
+extern "C" int32_t oracle_execute_plan_timed_rebatched(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                                       int64_t batch_rows, double* seconds, int64_t* out_rows, char* errbuf,
+                                                       int32_t errlen) {
   try {
     Json plan = ParseJson(plan_json);
-    auto tbl = ImportTables(ntables, tables);
+    auto tbl = ImportTables(ntables, tables, batch_rows);
     Graph g;
     g.Build(plan, tbl);
     auto t0 = std::chrono::steady_clock::now();

@@ -50,6 +50,13 @@ int32_t oracle_execute_plan_timed(const char* plan_json, int32_t ntables,
                                   const oracle_table* tables, double* seconds, int64_t* out_rows,
                                   char* errbuf, int32_t errlen);
 
+// Same, with every given batch re-sliced into RowBatches of batch_rows rows (0: as given);
+// columns passed with no buffers are not materialised (the plan must not read them).
+int32_t oracle_execute_plan_timed_rebatched(const char* plan_json, int32_t ntables,
+                                            const oracle_table* tables, int64_t batch_rows,
+                                            double* seconds, int64_t* out_rows, char* errbuf,
+                                            int32_t errlen);
+
 void oracle_free(uint8_t* p);
 
 // QuantilesUDA on a value sequence (math_sketches.h:36-54): out[7] = p01,p10,p25,p50,p75,p90,p99.

@@ -590,6 +590,7 @@ extern "C" int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin
   if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "row range [%lld,%lld) outside table of %lld rows", (long long)begin, (long long)end, (long long)t.nrows);
   if (t.ctx != agg->impl.ctx) return SetError(PXG_INVALID_ARGUMENT, "table and agg belong to different contexts");
   agg->impl.res.ready = false;
+  agg->impl.state_version++;
   return agg->impl.ConsumeRange(&t, begin, end);
 }
 
@@ -608,6 +609,7 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   a.st_n = 0;
   a.arena_words = 0;
   a.inserted = 0;
+  a.state_version++;
   a.res.Clear();
   return PXG_OK;
 }

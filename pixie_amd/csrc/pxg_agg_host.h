@@ -44,7 +44,8 @@ struct Agg {
   // Global open-addressing table.
   DevBuf slots;
   uint32_t cap = 0;
-  DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor
+  DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor;
+                    // u32 @32 import inserts, @36 import error flags
   DevBuf deferred[2];
   DevBuf d_ranges;
   DevBuf arena;
@@ -59,6 +60,17 @@ struct Agg {
 
   AggResult res;
   DevBuf scratch;
+  // Bumped by every consume / import / reset: export caches its partition per version.
+  uint64_t state_version = 0;
+
+  // Partial export workspace (pxg_partial.hip), valid for (n_parts, state_version).
+  struct ExportCache {
+    bool valid = false;
+    int32_t n_parts = 0;
+    uint64_t version = 0;
+    DevBuf part_of, words, slist, grank, koff, rdigit, rlist, starts, hist, scan, scan2, desc, remap;
+    std::vector<uint64_t> g_start, r_start, k_start;  // per part (+ total): groups, rows, key words
+  } xc;
 
   // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).
   struct FinalizeWs {
@@ -74,6 +86,9 @@ struct Agg {
   int32_t ConsumeRange(Table* t, int64_t begin, int64_t end);
   int32_t ConsumeList(Table* t, const uint32_t* list, uint32_t n);
   int32_t Finalize();
+  int32_t PrepareExport(int32_t n_parts);
+  int32_t ExportPartial(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
+  int32_t ImportPartial(const void* src, int64_t nbytes);
 };
 
 // Finalize stages (pxg_finalize.hip).

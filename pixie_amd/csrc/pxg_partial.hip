@@ -1,16 +1,506 @@
-// Partial aggregation export/import (planpb AggregateOperator.partial_agg / finalize_results,
-// src/carnot/planpb/plan.proto:250-257).  See DESIGN.md §5 for the wire format.
+// Partial aggregation export/import: the PEM-partial / Kelvin-finalize split
+// (planpb AggregateOperator.partial_agg / finalize_results, src/carnot/planpb/plan.proto:250-257;
+// the splitter that creates it: src/carnot/planner/distributed/splitter/partial_op_mgr/
+// partial_op_mgr.cc:69-83) mapped onto the GPUs of one node.
+//
+// An agg's state after consume is (group table + key arena, staging records).  Export
+// partitions it by hash(group key) into n_parts self-describing byte buffers; import merges a
+// buffer into another agg (on any device): its groups are found-or-inserted into the table by
+// exact key equality and its staged records are appended, remapped onto the local slots.
+// Finalize then runs unchanged, so count/sum/mean/min/max and quantiles of the union are the
+// single-node results (UDA Merge semantics, math_ops.h:590-593,633,668-672,710-714,747;
+// math_sketches.h:38).  QuantilesUDA has no Serialize (math_sketches.h:33-82), so the
+// reference could not split it into partial states at all: its inputs travel as values.
+//
+// Part layout (8-byte aligned sections):
+//   PartHeader (64 B)
+//   koff  u64[n_groups]        word offset of each group's key record within `keys`
+//   keys  u64[key_words]       arena-format key records (pxg_keys.h)
+//   gid   u32[n_rows] (+pad)   group index (into koff) of each staged record
+//   vals  u64[n_vals][n_rows]  staged value streams, stream-major
+#include <algorithm>
+
 #include "pxg_agg_host.h"
+#include "pxg_keys.h"
+#include "pxg_scan.h"
+
+namespace pxg {
+
+constexpr uint32_t kPartMagic = 0x50475850u;  // "PXGP"
+constexpr uint32_t kPartVersion = 1;
+constexpr int kMaxParts = 63;                  // digit 63 = "not exported" sentinel
+
+struct PartHeader {
+  uint32_t magic;
+  uint32_t version;
+  uint32_t n_keys;
+  uint32_t n_vals;
+  uint64_t n_groups;
+  uint64_t n_rows;
+  uint64_t key_words;
+  uint64_t plan_sig;
+  uint64_t reserved[2];
+};
+static_assert(sizeof(PartHeader) == 64, "PartHeader is 64 bytes");
+
+static inline uint64_t Align8(uint64_t x) { return (x + 7) & ~uint64_t(7); }
+
+struct PartLayout {
+  uint64_t koff, keys, gid, vals, bytes;
+};
+static PartLayout LayoutOf(uint64_t n_groups, uint64_t n_rows, uint64_t key_words, int n_vals) {
+  PartLayout L;
+  L.koff = sizeof(PartHeader);
+  L.keys = L.koff + n_groups * 8;
+  L.gid = L.keys + key_words * 8;
+  L.vals = L.gid + Align8(n_rows * 4);
+  L.bytes = L.vals + static_cast<uint64_t>(n_vals) * n_rows * 8;
+  return L;
+}
+
+// Signature of what a part carries: key types and staged value-stream types.
+static uint64_t PlanSig(const Agg& a) {
+  uint64_t h = 1469598103934665603ULL;
+  auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ULL; };
+  mix(static_cast<uint64_t>(a.n_keys));
+  for (int t : a.key_types) mix(static_cast<uint64_t>(t));
+  mix(static_cast<uint64_t>(a.n_vals));
+  for (int t : a.val_type) mix(static_cast<uint64_t>(t));
+  return h;
+}
+
+__device__ __forceinline__ uint32_t PartOfHash(uint64_t h, uint32_t n_parts) {
+  return static_cast<uint32_t>(((h >> 32) * static_cast<uint64_t>(n_parts)) >> 32);
+}
+
+// ---------------------------------------------------------------------------------------
+// Stable partition by a small digit (< 64): per-tile histograms, one scan, stable scatter of
+// item indices (ballot-matched ranks within a wave, LDS counts across waves).
+// ---------------------------------------------------------------------------------------
+constexpr int kPartBlock = 256;
+constexpr int kPartItems = 16;
+constexpr int kPartTile = kPartBlock * kPartItems;
+constexpr int kPartBuckets = 64;
+constexpr int kPartBits = 6;
+
+__global__ void __launch_bounds__(kPartBlock) PartHistKernel(const uint8_t* __restrict__ digit, uint64_t n,
+                                                             uint32_t* __restrict__ hist, uint32_t nblocks) {
+  __shared__ uint32_t h[kPartBuckets];
+  if (threadIdx.x < kPartBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kPartTile;
+  for (int k = 0; k < kPartItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kPartBlock + threadIdx.x;
+    if (i < n) atomicAdd(&h[digit[i]], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kPartBuckets) hist[static_cast<uint64_t>(threadIdx.x) * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kPartBlock) PartScatterKernel(const uint8_t* __restrict__ digit, uint64_t n,
+                                                                const uint32_t* __restrict__ offs, uint32_t nblocks,
+                                                                uint32_t* __restrict__ out) {
+  __shared__ uint32_t running[kPartBuckets];
+  __shared__ uint32_t wcnt[kPartBlock / 64][kPartBuckets];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  if (threadIdx.x < kPartBuckets) running[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * nblocks + blockIdx.x];
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kPartTile;
+  for (int k = 0; k < kPartItems; ++k) {
+    for (int i = threadIdx.x; i < (kPartBlock / 64) * kPartBuckets; i += kPartBlock) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t i = base + static_cast<uint64_t>(k) * kPartBlock + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t d = valid ? digit[i] : 0u;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kPartBits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(valid && bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t rank = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
+    if (valid && rank == 0) wcnt[wid][d] = static_cast<uint32_t>(__popcll(peers));
+    __syncthreads();
+    if (valid) {
+      uint32_t pre = 0;
+      for (int w = 0; w < wid; ++w) pre += wcnt[w][d];
+      out[running[d] + pre + rank] = static_cast<uint32_t>(i);
+    }
+    __syncthreads();
+    if (threadIdx.x < kPartBuckets) {
+      uint32_t s = 0;
+      for (int w = 0; w < kPartBlock / 64; ++w) s += wcnt[w][threadIdx.x];
+      running[threadIdx.x] += s;
+    }
+    __syncthreads();
+  }
+}
+
+// starts[b] = first output position of bucket b (b <= kPartBuckets; starts[64] = n).
+__global__ void PartStartsKernel(const uint32_t* __restrict__ scanned, uint32_t nblocks, uint64_t n, uint64_t* __restrict__ starts) {
+  const int b = threadIdx.x;
+  if (b < kPartBuckets) starts[b] = scanned[static_cast<uint64_t>(b) * nblocks];
+  if (b == kPartBuckets) starts[b] = n;
+}
+
+// ---------------------------------------------------------------------------------------
+// Export kernels.
+// ---------------------------------------------------------------------------------------
+__global__ void SlotPartKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ slots, uint32_t cap,
+                               const uint64_t* __restrict__ arena, uint32_t n_parts, uint8_t* __restrict__ part_of,
+                               uint32_t* __restrict__ words) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= cap) return;
+  const unsigned long long w = slots[s];
+  if (w == 0) {
+    part_of[s] = kMaxParts;
+    words[s] = 0;
+    return;
+  }
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
+  part_of[s] = static_cast<uint8_t>(PartOfHash(HashKeys(plan, k), n_parts));
+  words[s] = KeyRecordWords(plan, k);
+}
+
+// Sorted group list -> per-group key-record words (for the offset scan) and each slot's rank
+// within its part.
+__global__ void GroupRankKernel(const uint32_t* __restrict__ slist, uint64_t ng, const uint8_t* __restrict__ part_of,
+                                const uint32_t* __restrict__ words, const uint64_t* __restrict__ gstarts,
+                                uint64_t* __restrict__ kw, uint32_t* __restrict__ grank) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= ng) return;
+  const uint32_t s = slist[j];
+  kw[j] = words[s];
+  grank[s] = static_cast<uint32_t>(j - gstarts[part_of[s]]);
+}
+
+__global__ void RowDigitKernel(const uint32_t* __restrict__ st_slot, uint64_t n, uint32_t cap, const uint8_t* __restrict__ part_of,
+                               uint8_t* __restrict__ digit) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = st_slot[i];
+  digit[i] = s < cap ? part_of[s] : static_cast<uint8_t>(kMaxParts);
+}
+
+struct PartDst {
+  uint8_t* base;           // dst buffer
+  const uint64_t* poff;    // [n_parts] byte offset of each part in dst
+  const uint64_t* layout;  // [n_parts][4] koff, keys, gid, vals section offsets within the part
+  const uint64_t* nrows;   // [n_parts] rows per part (vals stride)
+};
+
+__global__ void WriteGroupsKernel(const uint32_t* __restrict__ slist, uint64_t ng, const uint8_t* __restrict__ part_of,
+                                  const uint64_t* __restrict__ gstarts, const uint64_t* __restrict__ koff_g,
+                                  const unsigned long long* __restrict__ slots, const uint64_t* __restrict__ arena,
+                                  const uint32_t* __restrict__ words, PartDst dst) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= ng) return;
+  const uint32_t s = slist[j];
+  const uint32_t p = part_of[s];
+  const uint64_t local = j - gstarts[p];
+  const uint64_t kbase = koff_g[gstarts[p]];
+  const uint64_t rel = koff_g[j] - kbase;
+  uint8_t* part = dst.base + dst.poff[p];
+  reinterpret_cast<uint64_t*>(part + dst.layout[p * 4 + 0])[local] = rel;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(part + dst.layout[p * 4 + 1]) + rel;
+  const uint64_t* rec = arena + static_cast<uint32_t>(slots[s]);
+  const uint32_t nw = words[s];
+  for (uint32_t w = 0; w < nw; ++w) keys[w] = rec[w];
+}
+
+struct ConstVals {
+  const uint64_t* p[kMaxVals];
+};
+
+__global__ void WriteRowsKernel(const uint32_t* __restrict__ rlist, uint64_t nr, const uint32_t* __restrict__ st_slot,
+                                const uint8_t* __restrict__ part_of, const uint32_t* __restrict__ grank,
+                                const uint64_t* __restrict__ rstarts, ConstVals vals, int n_vals, PartDst dst) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= nr) return;
+  const uint32_t i = rlist[j];
+  const uint32_t s = st_slot[i];
+  const uint32_t p = part_of[s];
+  const uint64_t local = j - rstarts[p];
+  uint8_t* part = dst.base + dst.poff[p];
+  reinterpret_cast<uint32_t*>(part + dst.layout[p * 4 + 2])[local] = grank[s];
+  uint64_t* v0 = reinterpret_cast<uint64_t*>(part + dst.layout[p * 4 + 3]);
+  const uint64_t stride = dst.nrows[p];
+  for (int v = 0; v < n_vals; ++v) v0[static_cast<uint64_t>(v) * stride + local] = vals.p[v][i];
+}
+
+// ---------------------------------------------------------------------------------------
+// Import kernels.
+// ---------------------------------------------------------------------------------------
+// Find-or-insert an arena key record (kind-1 slot word).  The caller sized the table so that
+// it stays <= 25% full: the probe always terminates at an empty or matching slot.
+__global__ void ImportKeysKernel(const AggPlanDev* __restrict__ plan, unsigned long long* __restrict__ slots, uint32_t mask,
+                                 const uint64_t* __restrict__ arena, uint64_t base, const uint64_t* __restrict__ koff, uint64_t ng,
+                                 uint32_t* __restrict__ remap, unsigned int* __restrict__ n_inserted,
+                                 unsigned int* __restrict__ err) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const uint64_t at = base + koff[g];
+  KeySet k;
+  LoadKeysArena(plan, arena + at, k);
+  const uint64_t h = HashKeys(plan, k);
+  const uint32_t tag = SlotTag(h);
+  const unsigned long long desired = MakeSlotWord(tag, kKindArena, static_cast<uint32_t>(at));
+  uint32_t pos = static_cast<uint32_t>(h) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    unsigned long long w = __hip_atomic_load(&slots[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 0) {
+      unsigned long long expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        atomicAdd(n_inserted, 1u);
+        remap[g] = pos;
+        return;
+      }
+      w = expected;
+    }
+    if (static_cast<uint32_t>(w >> 33) == tag) {
+      KeySet rep;
+      LoadKeysArena(plan, arena + static_cast<uint32_t>(w), rep);
+      if (KeysEqual(plan, k, rep)) {
+        remap[g] = pos;
+        return;
+      }
+    }
+    pos = (pos + 1) & mask;
+  }
+  atomicOr(err, 1u);
+  remap[g] = kDeferredSlot;
+}
+
+__global__ void ImportRowsKernel(const uint32_t* __restrict__ gid, uint64_t nr, uint64_t ng, const uint32_t* __restrict__ remap,
+                                 uint32_t* __restrict__ st_slot, unsigned int* __restrict__ err) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nr) return;
+  const uint32_t g = gid[i];
+  if (g >= ng) {
+    atomicOr(err, 2u);
+    st_slot[i] = kDeferredSlot;
+    return;
+  }
+  st_slot[i] = remap[g];
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side.
+// ---------------------------------------------------------------------------------------
+static int32_t Partition(Ctx* ctx, const uint8_t* digit, uint64_t n, uint32_t* out, uint64_t* d_starts, DevBuf* hist, DevBuf* scan) {
+  const uint32_t nblocks = static_cast<uint32_t>(std::max<uint64_t>(1, (n + kPartTile - 1) / kPartTile));
+  const uint64_t nh = static_cast<uint64_t>(kPartBuckets) * nblocks;
+  PXG_RETURN_IF_ERROR(hist->Ensure(nh * 4 + 64));
+  PXG_RETURN_IF_ERROR(scan->Ensure(ScanScratchBytes(static_cast<int64_t>(nh)) + 64));
+  if (n > 0) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "part_hist", PartHistKernel, dim3(nblocks), dim3(kPartBlock), 0, digit, n, hist->as<uint32_t>(), nblocks));
+  } else {
+    PXG_HIP(hipMemsetAsync(hist->p, 0, nh * 4, ctx->stream));
+  }
+  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, hist->as<uint32_t>(), hist->as<uint32_t>(), static_cast<int64_t>(nh), nullptr, scan->p));
+  if (n > 0)
+    PXG_RETURN_IF_ERROR(Launch(ctx, "part_scatter", PartScatterKernel, dim3(nblocks), dim3(kPartBlock), 0, digit, n,
+                               hist->as<const uint32_t>(), nblocks, out));
+  return Launch(ctx, "part_starts", PartStartsKernel, dim3(1), dim3(128), 0, hist->as<const uint32_t>(), nblocks, n, d_starts);
+}
+
+int32_t Agg::PrepareExport(int32_t n_parts) {
+  ExportCache& X = xc;
+  if (X.valid && X.n_parts == n_parts && X.version == state_version) return PXG_OK;
+  X.valid = false;
+  const uint64_t n = st_n;
+  PXG_RETURN_IF_ERROR(X.part_of.Ensure(cap + 16));
+  PXG_RETURN_IF_ERROR(X.words.Ensure(static_cast<size_t>(cap) * 4 + 16));
+  PXG_RETURN_IF_ERROR(X.slist.Ensure(static_cast<size_t>(cap) * 4 + 16));
+  PXG_RETURN_IF_ERROR(X.grank.Ensure(static_cast<size_t>(cap) * 4 + 16));
+  PXG_RETURN_IF_ERROR(X.starts.Ensure(2 * (kPartBuckets + 1) * 8 + 64));
+  uint64_t* gstarts = X.starts.as<uint64_t>();
+  uint64_t* rstarts = gstarts + kPartBuckets + 1;
+  PXG_RETURN_IF_ERROR(Launch(ctx, "export_slot_part", SlotPartKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), slots.as<const unsigned long long>(), cap, arena.as<const uint64_t>(),
+                             static_cast<uint32_t>(n_parts), X.part_of.as<uint8_t>(), X.words.as<uint32_t>()));
+  PXG_RETURN_IF_ERROR(Partition(ctx, X.part_of.as<const uint8_t>(), cap, X.slist.as<uint32_t>(), gstarts, &X.hist, &X.scan));
+  // Occupied slots come first (parts 0..n_parts-1), then the empty-slot sentinel bucket.
+  uint64_t hg[kPartBuckets + 1];
+  PXG_HIP(hipMemcpyAsync(hg, gstarts, sizeof(hg), hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  const uint64_t ng = hg[n_parts];
+  PXG_RETURN_IF_ERROR(X.koff.Ensure((ng + 1) * 8 + 64));
+  PXG_RETURN_IF_ERROR(X.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(ng + 1)) + 64));
+  uint64_t* koff = X.koff.as<uint64_t>();
+  if (ng > 0) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", GroupRankKernel, dim3(GridFor(static_cast<int64_t>(ng), 256, 1 << 30)), dim3(256), 0,
+                               X.slist.as<const uint32_t>(), ng, X.part_of.as<const uint8_t>(), X.words.as<const uint32_t>(), gstarts, koff,
+                               X.grank.as<uint32_t>()));
+  }
+  PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, koff, koff, static_cast<int64_t>(ng), koff + ng, X.scan2.p));
+  // Rows.
+  PXG_RETURN_IF_ERROR(X.rdigit.Ensure(n + 16));
+  PXG_RETURN_IF_ERROR(X.rlist.Ensure(n * 4 + 16));
+  if (n > 0)
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_row_digit", RowDigitKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                               st_slot.as<const uint32_t>(), n, cap, X.part_of.as<const uint8_t>(), X.rdigit.as<uint8_t>()));
+  PXG_RETURN_IF_ERROR(Partition(ctx, X.rdigit.as<const uint8_t>(), n, X.rlist.as<uint32_t>(), rstarts, &X.hist, &X.scan));
+  // Key-word totals at each part boundary.
+  std::vector<uint64_t> kstart(n_parts + 1);
+  uint64_t hr[kPartBuckets + 1];
+  PXG_HIP(hipMemcpyAsync(hr, rstarts, sizeof(hr), hipMemcpyDeviceToHost, ctx->stream));
+  for (int p = 0; p <= n_parts; ++p) PXG_HIP(hipMemcpyAsync(&kstart[p], koff + hg[p], 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  X.g_start.assign(hg, hg + n_parts + 1);
+  X.r_start.assign(hr, hr + n_parts + 1);
+  X.k_start = kstart;
+  X.n_parts = n_parts;
+  X.version = state_version;
+  X.valid = true;
+  return PXG_OK;
+}
+
+int32_t Agg::ExportPartial(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes) {
+  PXG_RETURN_IF_ERROR(PrepareExport(n_parts));
+  ExportCache& X = xc;
+  std::vector<PartHeader> hdr(n_parts);
+  std::vector<uint64_t> poff(n_parts), lay(4 * n_parts), nrows(n_parts);
+  uint64_t off = 0;
+  const uint64_t sig = PlanSig(*this);
+  for (int p = 0; p < n_parts; ++p) {
+    const uint64_t ng = X.g_start[p + 1] - X.g_start[p];
+    const uint64_t nr = X.r_start[p + 1] - X.r_start[p];
+    const uint64_t kw = X.k_start[p + 1] - X.k_start[p];
+    const PartLayout L = LayoutOf(ng, nr, kw, n_vals);
+    PartHeader& H = hdr[p];
+    std::memset(&H, 0, sizeof(H));
+    H.magic = kPartMagic;
+    H.version = kPartVersion;
+    H.n_keys = static_cast<uint32_t>(n_keys);
+    H.n_vals = static_cast<uint32_t>(n_vals);
+    H.n_groups = ng;
+    H.n_rows = nr;
+    H.key_words = kw;
+    H.plan_sig = sig;
+    poff[p] = off;
+    lay[4 * p + 0] = L.koff;
+    lay[4 * p + 1] = L.keys;
+    lay[4 * p + 2] = L.gid;
+    lay[4 * p + 3] = L.vals;
+    nrows[p] = nr;
+    part_offsets[p] = static_cast<int64_t>(off);
+    part_bytes[p] = static_cast<int64_t>(L.bytes);
+    off += Align8(L.bytes);
+  }
+  if (dst == nullptr) return PXG_OK;
+  if (static_cast<uint64_t>(dst_capacity) < off)
+    return SetError(PXG_INVALID_ARGUMENT, "export buffer holds %lld bytes; %llu needed", (long long)dst_capacity, (unsigned long long)off);
+  // Part descriptors -> device (one small staging copy, kept alive until the sync below).
+  std::vector<uint64_t> desc;
+  desc.insert(desc.end(), poff.begin(), poff.end());
+  desc.insert(desc.end(), lay.begin(), lay.end());
+  desc.insert(desc.end(), nrows.begin(), nrows.end());
+  PXG_RETURN_IF_ERROR(X.desc.Ensure(desc.size() * 8 + 64));
+  PXG_HIP(hipMemcpyAsync(X.desc.p, desc.data(), desc.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  uint8_t* base = static_cast<uint8_t*>(dst);
+  for (int p = 0; p < n_parts; ++p)
+    PXG_HIP(hipMemcpyAsync(base + poff[p], &hdr[p], sizeof(PartHeader), hipMemcpyHostToDevice, ctx->stream));
+  PartDst D;
+  D.base = base;
+  D.poff = X.desc.as<const uint64_t>();
+  D.layout = D.poff + n_parts;
+  D.nrows = D.layout + 4 * n_parts;
+  const uint64_t ng = X.g_start[n_parts];
+  const uint64_t nr = X.r_start[n_parts];
+  const uint64_t* gstarts = X.starts.as<const uint64_t>();
+  const uint64_t* rstarts = gstarts + kPartBuckets + 1;
+  if (ng > 0)
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", WriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(ng), 256, 1 << 30)), dim3(256), 0,
+                               X.slist.as<const uint32_t>(), ng, X.part_of.as<const uint8_t>(), gstarts, X.koff.as<const uint64_t>(),
+                               slots.as<const unsigned long long>(), arena.as<const uint64_t>(), X.words.as<const uint32_t>(), D));
+  if (nr > 0) {
+    ConstVals cv;
+    for (int v = 0; v < kMaxVals; ++v) cv.p[v] = v < n_vals ? st_val[v].as<const uint64_t>() : nullptr;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_rows", WriteRowsKernel, dim3(GridFor(static_cast<int64_t>(nr), 256, 1 << 30)), dim3(256), 0,
+                               X.rlist.as<const uint32_t>(), nr, st_slot.as<const uint32_t>(), X.part_of.as<const uint8_t>(),
+                               X.grank.as<const uint32_t>(), rstarts, cv, n_vals, D));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
+  if (nbytes < static_cast<int64_t>(sizeof(PartHeader))) return SetError(PXG_INVALID_ARGUMENT, "partial buffer of %lld bytes has no header", (long long)nbytes);
+  PartHeader H;
+  PXG_HIP(hipMemcpyAsync(&H, src, sizeof(H), hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  if (H.magic != kPartMagic || H.version != kPartVersion) return SetError(PXG_INVALID_ARGUMENT, "not a pxg partial-agg buffer (magic %08x version %u)", H.magic, H.version);
+  if (H.plan_sig != PlanSig(*this) || H.n_keys != static_cast<uint32_t>(n_keys) || H.n_vals != static_cast<uint32_t>(n_vals))
+    return SetError(PXG_INVALID_ARGUMENT, "partial buffer was exported by an aggregation with different key/value types");
+  const PartLayout L = LayoutOf(H.n_groups, H.n_rows, H.key_words, n_vals);
+  if (static_cast<uint64_t>(nbytes) < L.bytes) return SetError(PXG_INVALID_ARGUMENT, "partial buffer truncated: %lld of %llu bytes", (long long)nbytes, (unsigned long long)L.bytes);
+  state_version++;
+  res.ready = false;
+  if (H.n_groups == 0) {
+    if (H.n_rows != 0) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has rows but no groups");
+    return PXG_OK;
+  }
+  const uint8_t* p = static_cast<const uint8_t*>(src);
+  // Keys -> arena, then find-or-insert.  Size the table for <= 25% fill after the import.
+  const uint64_t base = arena_words;
+  if (base + H.key_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  PXG_RETURN_IF_ERROR(arena.Reserve((base + H.key_words) * 8 + 64, base * 8, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(arena.as<uint64_t>() + base, p + L.keys, H.key_words * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  arena_words += H.key_words;
+  uint64_t want = 4 * (inserted + H.n_groups);
+  if (want > cap) {
+    uint64_t c = cap;
+    while (c < want) c <<= 1;
+    if (c > (uint64_t(1) << 31)) return SetError(PXG_RESOURCE_UNAVAILABLE, "group table would exceed 2^31 slots");
+    PXG_RETURN_IF_ERROR(Grow(static_cast<uint32_t>(c)));
+  }
+  PXG_RETURN_IF_ERROR(xc.remap.Ensure(H.n_groups * 4 + 16));
+  uint8_t* meta = counters.as<uint8_t>();
+  unsigned int* d_ins = reinterpret_cast<unsigned int*>(meta + 32);
+  unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 36);
+  PXG_HIP(hipMemsetAsync(meta + 32, 0, 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "import_keys", ImportKeysKernel, dim3(GridFor(static_cast<int64_t>(H.n_groups), 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), slots.as<unsigned long long>(), cap - 1, arena.as<const uint64_t>(), base,
+                             reinterpret_cast<const uint64_t*>(p + L.koff), H.n_groups, xc.remap.as<uint32_t>(), d_ins, d_err));
+  if (H.n_rows > 0) {
+    PXG_RETURN_IF_ERROR(EnsureStage(st_n + H.n_rows));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", ImportRowsKernel, dim3(GridFor(static_cast<int64_t>(H.n_rows), 256, 1 << 30)), dim3(256), 0,
+                               reinterpret_cast<const uint32_t*>(p + L.gid), H.n_rows, H.n_groups, xc.remap.as<const uint32_t>(),
+                               st_slot.as<uint32_t>() + st_n, d_err));
+    for (int v = 0; v < n_vals; ++v)
+      PXG_HIP(hipMemcpyAsync(st_val[v].as<uint64_t>() + st_n, p + L.vals + static_cast<uint64_t>(v) * H.n_rows * 8, H.n_rows * 8,
+                             hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  uint32_t r[2];
+  PXG_HIP(hipMemcpyAsync(r, meta + 32, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  if (r[1] & 1u) return SetError(PXG_INTERNAL, "group table full during partial import");
+  if (r[1] & 2u) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has a row whose group index is out of range");
+  inserted += r[0];
+  st_n += H.n_rows;
+  // Keep the device fill counter exact (the consume kernel's soft fill guard reads it).
+  PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(counters.as<uint8_t>() + 16, &st_n, 8, hipMemcpyHostToDevice, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+}  // namespace pxg
 
 using namespace pxg;
 
 extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets,
                                           int64_t* part_bytes) {
-  (void)agg; (void)n_parts; (void)dst; (void)dst_capacity; (void)part_offsets; (void)part_bytes;
-  return SetError(PXG_UNIMPLEMENTED, "partial export not implemented yet");
+  if (!agg || !part_offsets || !part_bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  if (n_parts < 1 || n_parts > kMaxParts) return SetError(PXG_INVALID_ARGUMENT, "n_parts must be in [1, %d]", kMaxParts);
+  return agg->impl.ExportPartial(n_parts, dst, dst_capacity, part_offsets, part_bytes);
 }
 
 extern "C" int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes) {
-  (void)agg; (void)src; (void)nbytes;
-  return SetError(PXG_UNIMPLEMENTED, "partial import not implemented yet");
+  if (!agg || !src) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  return agg->impl.ImportPartial(src, nbytes);
 }

@@ -101,6 +101,7 @@ def column_from_out(o: ColumnOut, per_row: int = 1) -> Column:
 
 class Ctx:
     def __init__(self, device: int = 0):
+        self.device = device
         lib = load()
         h = C.c_void_p()
         check(lib.pxg_ctx_create(device, C.byref(h)))
@@ -257,6 +258,25 @@ class Agg:
 
     def reset(self) -> None:
         check(self.lib.pxg_agg_reset(self.h))
+
+    # -- partial aggregation (PEM partial -> exchange by key hash -> Kelvin finalize) --------
+    @property
+    def device(self) -> str:
+        return f"cuda:{self.ctx.device}"
+
+    def export_partial(self, n_parts: int, dst=None):
+        """Partition this agg's groups (and their staged values) by hash(key) % n_parts.
+        With dst=None only sizes; otherwise dst is a uint8 device tensor (on this agg's GPU)
+        of at least sum(aligned sizes) bytes.  Returns (part_offsets, part_bytes)."""
+        offs = (C.c_int64 * n_parts)()
+        nb = (C.c_int64 * n_parts)()
+        ptr, cap = (None, 0) if dst is None else (C.c_void_p(dst.data_ptr()), dst.numel())
+        check(self.lib.pxg_agg_export_partial(self.h, n_parts, ptr, cap, offs, nb))
+        return list(offs), list(nb)
+
+    def import_partial(self, src) -> None:
+        """Merge one exported part (a contiguous uint8 device tensor) into this agg."""
+        check(self.lib.pxg_agg_import_partial(self.h, C.c_void_p(src.data_ptr()), src.numel()))
 
     def rows_selected(self) -> int:
         n = C.c_int64()

@@ -46,6 +46,9 @@ def load():
     lib.oracle_execute_plan_timed.restype = C.c_int32
     lib.oracle_execute_plan_timed.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.POINTER(C.c_double),
                                               C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
+    lib.oracle_execute_plan_timed_rebatched.restype = C.c_int32
+    lib.oracle_execute_plan_timed_rebatched.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.c_int64,
+                                                        C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
     lib.oracle_free.argtypes = [C.c_void_p]
     lib.oracle_tdigest_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
     lib.oracle_tdigest_merge_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
@@ -64,10 +67,23 @@ class OracleError(RuntimeError):
         self.code = code
 
 
+class AbsentColumn:
+    """A table column the plan never reads: passed without buffers, never materialised."""
+
+    def __init__(self, type_: int, length: int):
+        self.type = type_
+        self.length = length
+
+    def __len__(self):
+        return self.length
+
+
 def _col_struct(col) -> OColumn:
     oc = OColumn()
     oc.type = col.type
     oc.length = len(col)
+    if isinstance(col, AbsentColumn):
+        return oc
     if col.type == STRING:
         oc.offsets = col.offsets.ctypes.data
         oc.data = col.data.ctypes.data
@@ -175,7 +191,9 @@ def execute_plan(plan, tables: Dict[str, dict]):
     return parse_pxrb(buf)
 
 
-def time_plan(plan, tables: Dict[str, dict]):
+def time_plan(plan, tables: Dict[str, dict], batch_rows: int = 0):
+    """Execution-window seconds of the plan (first GenerateNext .. last emit).  batch_rows > 0
+    re-slices every given batch into RowBatches of that many rows inside the oracle."""
     from google.protobuf import json_format
     lib = load()
     js = json_format.MessageToJson(plan).encode()
@@ -183,7 +201,7 @@ def time_plan(plan, tables: Dict[str, dict]):
     secs = C.c_double()
     rows = C.c_int64()
     err = C.create_string_buffer(1024)
-    code = lib.oracle_execute_plan_timed(js, t.n, t.arr, C.byref(secs), C.byref(rows), err, 1024)
+    code = lib.oracle_execute_plan_timed_rebatched(js, t.n, t.arr, batch_rows, C.byref(secs), C.byref(rows), err, 1024)
     if code != 0:
         raise OracleError(code, err.value.decode())
     return secs.value, rows.value
