@@ -18,6 +18,9 @@ namespace pxg {
 //   kind 1: ref = 8-byte word offset of the key record in the agg's key arena
 constexpr uint64_t kKindArena = 1ULL << 32;
 constexpr uint32_t kDeferredSlot = 0xFFFFFFFFu;
+// Bytes kept allocated past the last key record: the consume fast path loads a whole key
+// record speculatively (at most kMaxKeys * 7 words) before it knows the record's length.
+constexpr uint64_t kArenaSlack = 512;
 
 __device__ __forceinline__ uint32_t SlotTag(uint64_t h) { return static_cast<uint32_t>((h >> 33) | 1u) & 0x7FFFFFFFu; }
 __device__ __forceinline__ uint64_t MakeSlotWord(uint32_t tag, uint64_t kind, uint32_t ref) {

@@ -5,6 +5,7 @@
 // extraction + hash probe (agg_node.cc:209-271) and the per-row UDA value buffering
 // (agg_node.cc:258-268).  One launch streams every row of the table once.
 #include <algorithm>
+#include <cstdlib>
 
 #include "pxg_agg_host.h"
 #include "pxg_keys.h"
@@ -198,6 +199,399 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeListKernel(const AggP
   if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
 }
 
+// ---------------------------------------------------------------------------------------
+// Fast path: every group key is a bare column, the filter and every value stream are one of
+// the two fast shapes.  Keys live in registers as realigned, tail-masked 8-byte words, so a
+// string key costs two memory round trips (offsets, then every payload word at once) instead
+// of one per word, and equality against the group's representative key is word compares of
+// registers.  No interpreter stack, so no scratch and a small register budget.  The hash is
+// bit-identical to HashKeys (rehash, import and the generic kernel share the table).
+// Rows with a string key longer than kFastStrWords words are deferred to the generic kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int kFastStrWords = 6;
+
+template <int NK>
+struct FastKeys {
+  uint64_t w[NK][kFastStrWords];  // STRING: payload words; fixed: w[0] (UINT128: w[0], w[1])
+  uint32_t len[NK];               // STRING byte length (0 for fixed types)
+};
+
+// Payload words of a string of len <= 8 * kFastStrWords bytes at p, realigned and
+// tail-masked.  The bytes are fetched as 16-byte aligned chunks (<= 4 loads instead of 7
+// eight-byte ones: every load of a divergent wave costs address-processing time per lane);
+// payload buffers are 16-byte aligned with a 16-byte pad, so the over-read stays in bounds.
+constexpr int kFast16 = (8 * kFastStrWords + 15 + 15) / 16;
+__device__ __forceinline__ void LoadStrWords(const uint8_t* p, uint32_t len, uint64_t* w) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const ulonglong2* b16 = reinterpret_cast<const ulonglong2*>(a & ~uintptr_t(15));
+  const uint32_t n16 = (static_cast<uint32_t>(a & 15) + len + 15) >> 4;
+  uint64_t W[2 * kFast16 + 2];
+#pragma unroll
+  for (int i = 0; i < kFast16; ++i) {
+    ulonglong2 v = make_ulonglong2(0, 0);
+    if (static_cast<uint32_t>(i) < n16) v = b16[i];
+    W[2 * i] = v.x;
+    W[2 * i + 1] = v.y;
+  }
+  W[2 * kFast16] = W[2 * kFast16 + 1] = 0;
+  const bool odd = (a & 8) != 0;
+  const unsigned sh = static_cast<unsigned>(a & 7) * 8;
+#pragma unroll
+  for (int j = 0; j < kFastStrWords; ++j) {
+    const uint64_t lo = odd ? W[j + 1] : W[j];
+    const uint64_t hi = odd ? W[j + 2] : W[j + 1];
+    const uint64_t x = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+    const int rem = static_cast<int>(len) - 8 * j;
+    w[j] = rem >= 8 ? x : (rem > 0 ? (x & ((1ULL << (rem * 8)) - 1)) : 0);
+  }
+}
+
+// offsets[r] and offsets[r + 1] with one 12-byte load from the 8-byte aligned pair start.
+__device__ __forceinline__ void LoadOffsetPair(const int32_t* __restrict__ offs, int64_t r, int32_t* o0, int32_t* o1) {
+  struct __attribute__((packed, aligned(4))) I3 { int32_t a, b, c; };
+  const I3 v = *reinterpret_cast<const I3*>(offs + (r & ~int64_t(1)));
+  const bool odd = (r & 1) != 0;
+  *o0 = odd ? v.b : v.a;
+  *o1 = odd ? v.c : v.b;
+}
+
+// Keys of row r.  Returns false when a string key is too long for the register path.
+template <int NK>
+__device__ __forceinline__ bool LoadFastKeysRow(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r,
+                                                FastKeys<NK>& k) {
+  const uint8_t* ptr[NK];
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int t = plan->key_types[i];
+    const DevCol& col = ch.cols[plan->keys[i].col];
+    if (t == PXG_STRING) {
+      int32_t o0, o1;
+      LoadOffsetPair(col.offsets, r, &o0, &o1);
+      ptr[i] = col.data + o0;
+      k.len[i] = static_cast<uint32_t>(o1 - o0);
+      ok = ok && k.len[i] <= 8u * kFastStrWords;
+    } else {
+      const Val v = LoadCol(col, t, r);
+      k.w[i][0] = v.a;
+      k.w[i][1] = v.b;
+      k.len[i] = 0;
+    }
+  }
+  if (!ok) return false;
+#pragma unroll
+  for (int i = 0; i < NK; ++i)
+    if (plan->key_types[i] == PXG_STRING) LoadStrWords(ptr[i], k.len[i], k.w[i]);
+  return true;
+}
+
+template <int NK>
+__device__ __forceinline__ uint64_t HashFastKeys(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& k) {
+  uint64_t h = 0x243F6A8885A308D3ULL;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int t = plan->key_types[i];
+    uint64_t hk;
+    if (t == PXG_STRING) {
+      uint64_t s = 0x13198A2E03707344ULL;
+#pragma unroll
+      for (int j = 0; j < kFastStrWords; ++j) {
+        if (8u * j < k.len[i]) {
+          s = (s ^ k.w[i][j]) * 0x9E3779B97F4A7C15ULL;
+          s ^= s >> 29;
+        }
+      }
+      hk = Fmix64(s ^ (static_cast<uint64_t>(k.len[i]) * 0xC2B2AE3D27D4EB4FULL));
+    } else if (t == PXG_UINT128) {
+      hk = Fmix64(k.w[i][0] ^ Fmix64(k.w[i][1] + 0xA4093822299F31D0ULL));
+    } else {
+      hk = Fmix64(k.w[i][0] + 0x082EFA98EC4E6C89ULL);
+    }
+    h = Fmix64(h * 0x9E3779B97F4A7C15ULL + hk);
+  }
+  return h;
+}
+
+template <int NK>
+__device__ __forceinline__ bool FastKeysEqual(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& x, const FastKeys<NK>& y) {
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int t = plan->key_types[i];
+    if (t == PXG_STRING) {
+      eq = eq && x.len[i] == y.len[i];
+#pragma unroll
+      for (int j = 0; j < kFastStrWords; ++j) eq = eq && x.w[i][j] == y.w[i][j];
+    } else {
+      eq = eq && x.w[i][0] == y.w[i][0] && (t != PXG_UINT128 || x.w[i][1] == y.w[i][1]);
+    }
+  }
+  return eq;
+}
+
+// Equality against an arena key record (pxg_keys.h layout).  The record's word offsets are
+// taken from the probing key's own lengths (a record with different lengths is unequal
+// anyway), so every word is requested at once; the over-read stays inside kArenaSlack.
+template <int NK>
+__device__ __forceinline__ bool FastKeysEqualArena(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& x,
+                                                   const uint64_t* __restrict__ rec) {
+  bool eq = true;
+  int w = 0;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int t = plan->key_types[i];
+    if (t == PXG_STRING) {
+      eq = eq && rec[w] == x.len[i];
+      const int nw = static_cast<int>((x.len[i] + 7) >> 3);
+#pragma unroll
+      for (int j = 0; j < kFastStrWords; ++j)
+        if (j < nw) eq = eq && rec[w + 1 + j] == x.w[i][j];
+      w += 1 + nw;
+    } else if (t == PXG_UINT128) {
+      eq = eq && rec[w] == x.w[i][0] && rec[w + 1] == x.w[i][1];
+      w += 2;
+    } else {
+      eq = eq && rec[w] == x.w[i][0];
+      w += 1;
+    }
+  }
+  return eq;
+}
+
+// Equality against the keys of row r (a group's representative row), compared word by word
+// as the row's payload words arrive; nothing of the row's key is kept in registers.
+template <int NK>
+__device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r,
+                                                 const FastKeys<NK>& x) {
+  bool eq = true;
+  const uint8_t* ptr[NK];
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int t = plan->key_types[i];
+    const DevCol& col = ch.cols[plan->keys[i].col];
+    if (t == PXG_STRING) {
+      int32_t o0, o1;
+      LoadOffsetPair(col.offsets, r, &o0, &o1);
+      ptr[i] = col.data + o0;
+      eq = eq && static_cast<uint32_t>(o1 - o0) == x.len[i];
+    } else {
+      const Val v = LoadCol(col, t, r);
+      eq = eq && v.a == x.w[i][0] && (t != PXG_UINT128 || v.b == x.w[i][1]);
+    }
+  }
+  if (!eq) return false;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    if (plan->key_types[i] != PXG_STRING) continue;
+    uint64_t w[kFastStrWords];
+    LoadStrWords(ptr[i], x.len[i], w);
+#pragma unroll
+    for (int j = 0; j < kFastStrWords; ++j) eq = eq && w[j] == x.w[i][j];
+  }
+  return eq;
+}
+
+template <int NK>
+__device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                                     const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
+                                                     const AggTableDev& tab, unsigned int* s_ins) {
+  const uint32_t tag = SlotTag(h);
+  uint32_t pos = static_cast<uint32_t>(h) & tab.mask;
+  const uint32_t max_probe = min(tab.mask + 1, kMaxProbe);
+  for (uint32_t probe = 0; probe < max_probe; ++probe) {
+    // Plain (cacheable) load: a slot word only ever changes 0 -> final value (by CAS) within a
+    // launch, so a non-zero word seen here is final; a stale 0 just costs the CAS below, which
+    // returns the real word.
+    unsigned long long w = tab.slots[pos];
+    if (w == 0) {
+      const unsigned int ins = __hip_atomic_load(&tab.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + *s_ins;
+      if (ins >= tab.limit) return kDeferredSlot;
+      unsigned long long expected = 0;
+      const unsigned long long desired = MakeSlotWord(tag, 0, rowref);
+      if (__hip_atomic_compare_exchange_strong(&tab.slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        atomicAdd(s_ins, 1u);
+        return pos;
+      }
+      w = expected;
+    }
+    if (static_cast<uint32_t>(w >> 33) == tag) {
+      const uint32_t ref = static_cast<uint32_t>(w);
+      bool eq;
+      if (w & kKindArena) {
+        eq = FastKeysEqualArena<NK>(plan, keys, tab.arena + ref);
+      } else {
+        eq = FastKeysEqualRow<NK>(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
+      }
+      if (eq) return pos;
+    }
+    pos = (pos + 1) & tab.mask;
+  }
+  return kDeferredSlot;
+}
+
+// Per-workgroup LDS cache of recently seen groups: (hash tag, table slot, the key's words).
+// A hit is decided by comparing every key word and length against the cached copy, so it is
+// exact; it skips the global slot-word load (a hot group's slot word would otherwise be read
+// by every CU: same-address traffic at the memory side) and the representative-key reload.
+// Lookups and fills are separated by barriers: a round of <= 256 selected rows first looks up
+// (read-only) and claims entries for its misses (LDS atomicMax of a per-round stamp), then the
+// claim winners write their entries; no entry is ever read while it is written.
+template <int NK>
+struct CacheEntry {
+  uint32_t tag;   // (hash >> 32) | 1; 0 = empty
+  uint32_t slot;
+  uint32_t len[NK];
+  uint64_t w[NK][kFastStrWords];
+};
+template <int NK>
+constexpr int CacheEntries() { return NK <= 2 ? 256 : 128; }
+
+// MODE: 0 = production (no cache), 1 = with the LDS group cache; 2 / 3 are timing-only
+// diagnostic builds that stop after the filter (2) or after key load + hash (3) and write
+// garbage slots (tools/consume_diag.py; never followed by finalize).
+template <int NK, int MODE>
+__global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
+                                                                      const DevChunk* __restrict__ chunks,
+                                                                      const TileRange* __restrict__ ranges, int nranges,
+                                                                      int64_t ntiles, AggTableDev tab, StageDev stg) {
+  constexpr int kPer = kConsumeTile / kConsumeBlock;
+  constexpr int kWaves = kConsumeBlock / 64;
+  constexpr int kEntries = CacheEntries<NK>();
+  __shared__ uint16_t s_sel[kConsumeTile];
+  __shared__ uint32_t s_wcnt[kWaves];
+  __shared__ unsigned int s_ins;
+  __shared__ unsigned long long s_base;
+  __shared__ CacheEntry<NK> s_cache[kEntries];
+  __shared__ uint32_t s_claim[kEntries];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
+  const int nv = plan->n_vals;
+  if (threadIdx.x == 0) s_ins = 0;
+  for (int e = threadIdx.x; e < kEntries; e += kConsumeBlock) {
+    s_cache[e].tag = 0;
+    s_claim[e] = 0;
+  }
+  uint32_t round = 0;  // per-workgroup round counter: claim stamps grow monotonically
+  for (int64_t t = bid; t < ntiles; t += gridDim.x) {
+    int ri = 0;
+    while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
+    const TileRange rg = ranges[ri];
+    const DevChunk& ch = chunks[rg.chunk];
+    const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
+    const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
+    bool pass[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int64_t r = row0 + k * kConsumeBlock + threadIdx.x;
+      pass[k] = r < row1;
+      if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
+    }
+    unsigned long long m[kPer];
+    uint32_t wtot = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      m[k] = __ballot(pass[k]);
+      wtot += static_cast<uint32_t>(__popcll(m[k]));
+    }
+    if (lane == 0) s_wcnt[wid] = wtot;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t c = s_wcnt[w];
+      wbase += w < wid ? c : 0;
+      total += c;
+    }
+    if (threadIdx.x == 0) {
+      if (s_ins) {
+        atomicAdd(&tab.counters[0], s_ins);
+        s_ins = 0;
+      }
+      s_base = total ? atomicAdd(stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = static_cast<uint16_t>(k * kConsumeBlock + threadIdx.x);
+      wbase += static_cast<uint32_t>(__popcll(m[k]));
+    }
+    __syncthreads();
+    const uint64_t base = s_base;
+    // Rounds of kConsumeBlock selected rows; every thread runs every round (barriers inside).
+    for (uint32_t r0 = 0; r0 < total; r0 += kConsumeBlock) {
+      ++round;
+      const uint32_t i = r0 + threadIdx.x;
+      const bool active = i < total;
+      FastKeys<NK> k;
+      uint32_t slot = kDeferredSlot;
+      int cidx = -1;
+      uint32_t ctag = 0;
+      const uint32_t stamp = (round << 9) | (threadIdx.x + 1);
+      if (active) {
+        const int64_t local = row0 + s_sel[i];
+        const uint64_t pos = base + i;
+        // Value streams first: independent of the key chain, their loads overlap it.
+        for (int v = 0; v < nv; ++v) stg.vals[v][pos] = EvalShape(&plan->vals[v], ch, local, plan->col_types);
+        const uint32_t rowref = (static_cast<uint32_t>(rg.chunk) << kChunkShift) | static_cast<uint32_t>(local);
+        if (MODE == 2) {
+          slot = 0;
+        } else if (LoadFastKeysRow<NK>(plan, ch, local, k)) {
+          const uint64_t h = HashFastKeys<NK>(plan, k);
+          if (MODE == 3) {
+            stg.slot[pos] = static_cast<uint32_t>(h);
+            continue;
+          }
+          ctag = static_cast<uint32_t>(h >> 32) | 1u;
+          const int e = static_cast<int>((h >> 20) & (kEntries - 1));
+          const CacheEntry<NK>& ce = s_cache[e];
+          bool hit = MODE == 1 && ce.tag == ctag;
+#pragma unroll
+          for (int q = 0; q < NK; ++q) {
+            hit = hit && ce.len[q] == k.len[q];
+#pragma unroll
+            for (int j = 0; j < kFastStrWords; ++j) hit = hit && ce.w[q][j] == k.w[q][j];
+          }
+          if (hit) {
+            slot = ce.slot;
+          } else {
+            slot = FastFindOrInsert<NK>(plan, chunks, k, h, rowref, tab, &s_ins);
+            if (MODE == 1 && slot != kDeferredSlot) {
+              cidx = e;
+              atomicMax(&s_claim[e], stamp);
+            }
+          }
+        }
+        const unsigned long long dm = __ballot(slot == kDeferredSlot);
+        if (dm) {
+          const int leader = __ffsll(static_cast<long long>(dm)) - 1;
+          unsigned int dbase = 0;
+          if (lane == leader) dbase = atomicAdd(&tab.counters[2], static_cast<unsigned int>(__popcll(dm)));
+          dbase = __shfl(dbase, leader, 64);
+          if (slot == kDeferredSlot) tab.deferred[dbase + __popcll(dm & lanemask_lt)] = rowref;
+        }
+        stg.slot[pos] = slot;
+      }
+      if (MODE != 1) continue;
+      __syncthreads();
+      if (cidx >= 0 && s_claim[cidx] == stamp) {
+        CacheEntry<NK>& ce = s_cache[cidx];
+        ce.tag = ctag;
+        ce.slot = slot;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+          ce.len[q] = k.len[q];
+#pragma unroll
+          for (int j = 0; j < kFastStrWords; ++j) ce.w[q][j] = k.w[q][j];
+        }
+      }
+      __syncthreads();
+    }
+    __syncthreads();  // s_wcnt / s_sel / s_base are rewritten by the next tile
+  }
+  if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
+}
+
 // Publication: every slot still holding a row reference (kind 0) gets its key copied into the
 // arena.  sizes[i] = (1 << 40) | words, so one exclusive scan yields both the record offsets
 // and (total >> 40) the number of published groups.
@@ -352,7 +746,7 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   const uint64_t n_new = tot >> kPublishCountShift;
   const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
   if (n_new > 0) {
-    PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + 64, arena_words * 8, ctx->stream));
+    PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + kArenaSlack, arena_words * 8, ctx->stream));
     PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
                                d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
                                static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>()));
@@ -402,14 +796,35 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice, ctx->stream));
   PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", AggConsumeKernel, dim3(grid), dim3(kConsumeBlock), 0,
+  void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev) = AggConsumeKernel;
+  static const int diag = [] {
+    const char* e = std::getenv("PXG_DIAG_CONSUME");
+    return e ? std::atoi(e) : 0;
+  }();
+  switch (fast_nk * 4 + (diag & 3)) {
+#define PXG_FAST_CASE(nk)                                           \
+  case nk * 4 + 0: kern = AggConsumeFastKernel<nk, 0>; break;       \
+  case nk * 4 + 1: kern = AggConsumeFastKernel<nk, 1>; break;       \
+  case nk * 4 + 2: kern = AggConsumeFastKernel<nk, 2>; break;       \
+  case nk * 4 + 3: kern = AggConsumeFastKernel<nk, 3>; break;
+    PXG_FAST_CASE(1)
+    PXG_FAST_CASE(2)
+    PXG_FAST_CASE(3)
+    PXG_FAST_CASE(4)
+#undef PXG_FAST_CASE
+    default: break;
+  }
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", kern, dim3(grid), dim3(kConsumeBlock), 0,
                              d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
                              static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this)));
   uint32_t n_def = 0;
   PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
   int buf = 0;
-  while (n_def > 0) {
-    PXG_RETURN_IF_ERROR(Grow(NextPow2(4 * (static_cast<uint64_t>(inserted) + n_def))));
+  for (int round = 0; n_def > 0; ++round) {
+    // Rows are deferred by a full table / overlong probe, or (fast path) by a long string key.
+    // Grow unless this is the first retry and the table still has room for every deferred row.
+    const uint64_t want = static_cast<uint64_t>(inserted) + n_def;
+    if (round > 0 || fast_nk == 0 || want > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(4 * want)));
     PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
     PXG_RETURN_IF_ERROR(EnsureStage(st_n + n_def));
     PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
@@ -471,6 +886,26 @@ static bool UdaSupported(int kind, int arg) {
     case PXG_UDA_MINSUM: return arg == PXG_INT64;
     default: return false;
   }
+}
+
+// The consume fast path takes bare-column group keys and fast-shape filter / value programs
+// over fixed-width columns (AggConsumeFastKernel); returns its key count, 0 if not eligible.
+static int32_t FastPathKeys(const AggPlanDev& p) {
+  if (p.n_keys < 1 || p.n_keys > kMaxKeys) return 0;
+  for (int k = 0; k < p.n_keys; ++k) {
+    if (p.keys[k].shape != kShapeCol) return 0;
+    const int t = p.key_types[k];
+    if (t < PXG_BOOLEAN || t > PXG_TIME64NS) return 0;
+  }
+  auto fixed_shape = [&](const DevProgram& q) {
+    if (q.shape != kShapeCol && q.shape != kShapeColOpConst) return false;
+    const int ct = p.col_types[q.col];
+    return ct != PXG_STRING && ct != PXG_UINT128 && ct != PXG_DATA_TYPE_UNKNOWN;
+  };
+  if (p.has_filter && !fixed_shape(p.filter)) return 0;
+  for (int v = 0; v < p.n_vals; ++v)
+    if (p.val_kind[v] != kValProgram || !fixed_shape(p.vals[v])) return 0;
+  return p.n_keys;
 }
 
 extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_agg** out) {
@@ -565,6 +1000,7 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   if (!pool.empty()) PXG_HIP(hipMemcpy(a.d_pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
   for (auto& pf : pool_fix) pf.first->pool = a.d_pool.as<uint8_t>() + pf.second;
   PXG_RETURN_IF_ERROR(a.d_plan.Alloc(sizeof(AggPlanDev)));
+  a.fast_nk = FastPathKeys(a.hplan);
   PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));

@@ -29,6 +29,8 @@ struct Agg {
   int32_t n_keys = 0, n_udas = 0, n_vals = 0;
   bool windowed = false;
   bool has_filter = false;
+  // Keys for the consume fast path (AggConsumeFastKernel<fast_nk>); 0 = generic kernel.
+  int32_t fast_nk = 0;
   std::vector<int32_t> uda_kind, uda_arg_type, uda_val, uda_out_type;
   std::vector<int64_t> uda_init;
   std::vector<int32_t> uda_has_init;

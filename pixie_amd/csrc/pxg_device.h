@@ -242,6 +242,16 @@ __device__ __forceinline__ uint64_t StrOp(int op, const Val& x, const Val& y) {
   }
 }
 
+// The two fast shapes alone (no interpreter stack: kernels that only take these shapes keep
+// their register budget small).  Fixed-width columns only.
+__device__ __forceinline__ uint64_t EvalShape(const DevProgram* __restrict__ p, const DevChunk& ch, int64_t r,
+                                              const int32_t* __restrict__ col_types) {
+  const Val v = LoadCol(ch.cols[p->col], col_types[p->col], r);
+  if (p->shape == kShapeCol) return v.a;
+  const uint64_t x = p->conv ? Conv(p->conv, v.a) : v.a;
+  return BinOp(p->binop, x, static_cast<uint64_t>(p->cimm));
+}
+
 // Evaluate a program on row r of chunk ch.  Uniform control flow across the wave (every lane
 // runs the same program); the generic path keeps its stack in private memory.
 __device__ inline Val EvalProgram(const DevProgram* __restrict__ p, const DevChunk& ch, int64_t r,

@@ -448,7 +448,7 @@ int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
   // Keys -> arena, then find-or-insert.  Size the table for <= 25% fill after the import.
   const uint64_t base = arena_words;
   if (base + H.key_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
-  PXG_RETURN_IF_ERROR(arena.Reserve((base + H.key_words) * 8 + 64, base * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(arena.Reserve((base + H.key_words) * 8 + kArenaSlack, base * 8, ctx->stream));
   PXG_HIP(hipMemcpyAsync(arena.as<uint64_t>() + base, p + L.keys, H.key_words * 8, hipMemcpyDeviceToDevice, ctx->stream));
   arena_words += H.key_words;
   uint64_t want = 4 * (inserted + H.n_groups);
