@@ -79,6 +79,7 @@ struct Agg {
     DevBuf alt_slot, alt_val[kMaxVals];
     DevBuf hist, scan, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
     DevBuf keysA, keysB, bstarts, big, bchunks;
+    DevBuf chain_list, chain_nc, chain_starts;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);

@@ -1,6 +1,7 @@
 // Agg finalize: group the staging records by slot (stable LSD radix sort), reduce each group
 // (ConvertAggHashMapToRowBatch + UDA Finalize, agg_node.cc:303-349), build quantile digests and
 // extract the group keys from the arena.
+#include <cstdlib>
 #include <algorithm>
 
 #include "pxg_agg_host.h"
@@ -469,6 +470,10 @@ __device__ __forceinline__ int64_t LowerBoundKey(Acc a, int64_t n, uint64_t key)
 // of DigestQuantile lists them (its control flow depends on positions only, never on means),
 // then each is computed — the reference's incremental mean for centroids of <= kSeqMean
 // values (every centroid while W <= ~10000), sum/count cooperatively for larger ones.
+// Timing-only diagnosis (PXG_DIAG_QUANT): 1 skips the centroid-boundary chain, 2 skips the
+// mid-group LDS sort.  Results are garbage when set; never set outside tools/.
+__device__ int g_diag_quant = 0;
+
 constexpr int kNeed = 7 * 4;
 constexpr int64_t kSeqMean = 16;
 
@@ -479,9 +484,39 @@ struct DigestShared {
   double red[4];
 };
 
+// Centroid boundaries precomputed by DigestChainKernel for a group assumed NaN-free (W = n);
+// `starts` == nullptr: none.
+struct PreChain {
+  const uint32_t* starts;
+  int64_t nc;
+  int64_t W;
+};
+
+// Centroid-boundary chains (DigestBoundaries) of many groups at once, one thread per group:
+// the chain is sequential per group (~1100 steps for any W > kSingletonMaxW), so running it
+// inside each group's digest workgroup serialised the whole workgroup behind one lane.
+constexpr int kChainCap = 2048;
+__global__ void __launch_bounds__(64) DigestChainKernel(const uint32_t* __restrict__ list, uint32_t nlist,
+                                                        const uint32_t* __restrict__ gstart, uint32_t* __restrict__ starts_out,
+                                                        int32_t* __restrict__ nc_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nlist) return;
+  const uint32_t g = list[i];
+  const int64_t W = gstart[g + 1] - gstart[g];
+  nc_out[i] = W <= kSingletonMaxW ? -2 : static_cast<int32_t>(DigestBoundaries(W, starts_out + static_cast<uint64_t>(i) * kChainCap, kChainCap));
+}
+
+__device__ __forceinline__ PreChain PreChainAt(const uint32_t* starts_all, const int32_t* nc_all, uint32_t i, int64_t n) {
+  PreChain p;
+  p.starts = starts_all ? starts_all + static_cast<uint64_t>(i) * kChainCap : nullptr;
+  p.nc = starts_all ? nc_all[i] : -1;
+  p.W = n;
+  return p;
+}
+
 template <typename KeyAt>
-__device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, int64_t max_c, double* out7, unsigned int* err,
-                            DigestShared& sh) {
+__device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_t max_c, PreChain pre, double* out7,
+                            unsigned int* err, DigestShared& sh) {
   const int t = threadIdx.x;
   // trim NaNs: keys < kNegInfKey (negative NaN) at the front, > kPosInfKey at the back
   if (t == 0) {
@@ -498,8 +533,12 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, int64_t ma
     __syncthreads();
     return;
   }
+  const bool use_pre = pre.starts != nullptr && pre.W == W && pre.nc >= 0;
+  const uint32_t* starts = use_pre ? pre.starts : starts_buf;
   if (t == 0) {
-    const int64_t nc = DigestBoundaries(W, starts, max_c);
+    int64_t nc;
+    if (use_pre) nc = pre.nc;
+    else nc = g_diag_quant == 1 ? (starts_buf[0] = 0, 1) : DigestBoundaries(W, starts_buf, max_c);
     if (nc < 0) atomicExch(err, 1u);
     sh.meta[2] = nc < 0 ? 0 : nc;
   }
@@ -552,6 +591,7 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts, int64_t ma
 
 // One workgroup per group with 1024 < n <= 4096: LDS bitonic sort + digest.
 __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
+                                                      const uint32_t* __restrict__ chain_starts, const int32_t* __restrict__ chain_nc,
                                                       const uint64_t* __restrict__ vals, int arg_type, double* __restrict__ out,
                                                       unsigned int* __restrict__ err) {
   __shared__ uint64_t keys[kMidMax];
@@ -563,8 +603,9 @@ __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict
   while (P < static_cast<int>(n)) P <<= 1;
   for (int i = threadIdx.x; i < P; i += blockDim.x) keys[i] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
   __syncthreads();
-  BitonicSortLds(keys, P);
-  BlockDigest([&](int64_t i) -> uint64_t { return keys[i]; }, n, starts, kMidCentroids, out + static_cast<uint64_t>(g) * 7, err, sh);
+  if (g_diag_quant != 2) BitonicSortLds(keys, P);
+  BlockDigest([&](int64_t i) -> uint64_t { return keys[i]; }, n, starts, kMidCentroids,
+              PreChainAt(chain_starts, chain_nc, blockIdx.x, n), out + static_cast<uint64_t>(g) * 7, err, sh);
 }
 
 // Big groups: chunk sort (one workgroup per 4096-element chunk) into sort keys.
@@ -634,14 +675,15 @@ __global__ void BigMergeKernel(const BigGroup* __restrict__ groups, uint32_t ngr
 constexpr int kBigCentroids = 8192;
 
 __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restrict__ groups, const uint64_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ starts_all, double* __restrict__ out,
+                                                       uint32_t* __restrict__ starts_all, const uint32_t* __restrict__ chain_starts,
+                                                       const int32_t* __restrict__ chain_nc, double* __restrict__ out,
                                                        unsigned int* __restrict__ err) {
   __shared__ DigestShared sh;
   const BigGroup G = groups[blockIdx.x];
   uint32_t* starts = starts_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
   const uint64_t* k = keys + G.off;
   BlockDigest([&](int64_t i) -> uint64_t { return k[i]; }, static_cast<int64_t>(G.n), starts, kBigCentroids,
-              out + static_cast<uint64_t>(G.g) * 7, err, sh);
+              PreChainAt(chain_starts, chain_nc, blockIdx.x, static_cast<int64_t>(G.n)), out + static_cast<uint64_t>(G.g) * 7, err, sh);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -725,6 +767,13 @@ int32_t AggFinalizeImpl(Agg* a) {
   uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta + 8);
   unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 16);
   uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta + 32);
+  {
+    static const int diag = [] {
+      const char* e = std::getenv("PXG_DIAG_QUANT");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (diag) PXG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_quant), &diag, sizeof(int)));
+  }
   PXG_RETURN_IF_ERROR(Launch(ctx, "finalize_init", FinalizeInitKernel, dim3(1), dim3(64), 0, meta, n));
 
   // 1. Stable LSD radix sort of (slot, vals...) by slot; deferred (invalid) slots map to cap.
@@ -849,6 +898,33 @@ int32_t AggFinalizeImpl(Agg* a) {
       PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(big.size() * kBigCentroids * 4));
     }
+    // Centroid-boundary chains for every mid and big group, one thread each, in one launch:
+    // chain slots [0, cls[2]) follow the mid list, [cls[2], +big) the BigGroup order.
+    const uint32_t n_chain = cls[2] + static_cast<uint32_t>(big.size());
+    const uint32_t* chain_starts = nullptr;
+    const int32_t* chain_nc = nullptr;
+    if (n_chain > 0) {
+      PXG_RETURN_IF_ERROR(ws.chain_list.Ensure(static_cast<size_t>(n_chain) * 4));
+      PXG_RETURN_IF_ERROR(ws.chain_nc.Ensure(static_cast<size_t>(n_chain) * 4));
+      PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain) * kChainCap * 4));
+      uint32_t* cl = ws.chain_list.as<uint32_t>();
+      if (cls[2] > 0)
+        PXG_HIP(hipMemcpyAsync(cl, lists + 2 * static_cast<uint64_t>(ngroups), cls[2] * 4, hipMemcpyDeviceToDevice, ctx->stream));
+      if (!big.empty()) {
+        std::vector<uint32_t> bg(big.size());
+        for (size_t b = 0; b < big.size(); ++b) bg[b] = big[b].g;
+        PXG_HIP(hipMemcpyAsync(cl + cls[2], bg.data(), bg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        PXG_HIP(hipStreamSynchronize(ctx->stream));  // bg is a host temporary
+      }
+      // The chains are latency-bound (a few waves, ~1100 dependent steps each): run them on
+      // the side stream, overlapped with the tiny/small digests and the big-group sort.
+      PXG_RETURN_IF_ERROR(ForkSide(ctx));
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain + 63) / 64), dim3(64), 0,
+                                   static_cast<const uint32_t*>(cl), n_chain, gstart, ws.chain_starts.as<uint32_t>(),
+                                   ws.chain_nc.as<int32_t>()));
+      chain_starts = ws.chain_starts.as<const uint32_t>();
+      chain_nc = ws.chain_nc.as<const int32_t>();
+    }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = a->st_val[a->uda_val[u]].as<const uint64_t>();
@@ -859,22 +935,27 @@ int32_t AggFinalizeImpl(Agg* a) {
       if (cls[1] > 0)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_small", QuantSmallKernel, dim3((cls[1] + kSmallWaves - 1) / kSmallWaves), dim3(256), 0,
                                    lists + static_cast<uint64_t>(ngroups), cls[1], gstart, vals, at, qo));
-      if (cls[2] > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
-                                   gstart, vals, at, qo, d_err));
+      DevBuf* src = &ws.keysA;
+      DevBuf* dst = &ws.keysB;
       if (!big.empty()) {
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(static_cast<unsigned>(bchunks.size())), dim3(256), 0,
                                    ws.bchunks.as<const BigChunk>(), vals, at, ws.keysA.as<uint64_t>()));
-        DevBuf* src = &ws.keysA;
-        DevBuf* dst = &ws.keysB;
         for (uint64_t w = kMidMax; w < big_max; w *= 2) {
           PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeKernel, dim3(GridFor(static_cast<int64_t>(big_total), 256, 1 << 30)),
                                      dim3(256), 0, ws.big.as<const BigGroup>(), static_cast<uint32_t>(big.size()), big_total,
                                      src->as<const uint64_t>(), dst->as<uint64_t>(), w));
           std::swap(src, dst);
         }
+      }
+      if (n_chain > 0) PXG_RETURN_IF_ERROR(JoinSide(ctx));
+      if (cls[2] > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
+                                   gstart, chain_starts, chain_nc, vals, at, qo, d_err));
+      if (!big.empty()) {
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(static_cast<unsigned>(big.size())), dim3(256), 0,
-                                   ws.big.as<const BigGroup>(), src->as<const uint64_t>(), ws.bstarts.as<uint32_t>(), qo, d_err));
+                                   ws.big.as<const BigGroup>(), src->as<const uint64_t>(), ws.bstarts.as<uint32_t>(),
+                                   chain_starts ? chain_starts + static_cast<uint64_t>(cls[2]) * kChainCap : nullptr,
+                                   chain_nc ? chain_nc + cls[2] : nullptr, qo, d_err));
       }
     }
   }

@@ -97,6 +97,9 @@ struct PendingTiming {
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // Side stream for latency-bound work that overlaps the main stream (fork/join by events).
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool profiling = false;
   std::map<std::string, KernelStat> stats;
   std::vector<PendingTiming> pending;
@@ -109,24 +112,42 @@ struct Ctx {
   int32_t ResolveTimings();
 };
 
-// Launch helper: optional event bracketing on the ctx stream (stats resolved lazily).
+// Launch helper: optional event bracketing on the launch stream (stats resolved lazily).
 template <typename... KArgs, typename... Args>
-inline int32_t Launch(Ctx* ctx, const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t shmem,
-                      Args&&... args) {
+inline int32_t LaunchOn(Ctx* ctx, hipStream_t stream, const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block,
+                        size_t shmem, Args&&... args) {
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return PXG_OK;
   hipEvent_t s0 = nullptr, s1 = nullptr;
   if (ctx->profiling) {
     s0 = ctx->GetEvent();
     s1 = ctx->GetEvent();
-    hipEventRecord(s0, ctx->stream);
+    (void)hipEventRecord(s0, stream);
   }
-  hipLaunchKernelGGL(kernel, grid, block, shmem, ctx->stream, std::forward<Args>(args)...);
+  hipLaunchKernelGGL(kernel, grid, block, shmem, stream, std::forward<Args>(args)...);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return SetError(PXG_INTERNAL, "launch %s failed: %s", name, hipGetErrorString(e));
   if (ctx->profiling) {
-    hipEventRecord(s1, ctx->stream);
+    (void)hipEventRecord(s1, stream);
     ctx->pending.push_back(PendingTiming{name, s0, s1});
   }
+  return PXG_OK;
+}
+
+template <typename... KArgs, typename... Args>
+inline int32_t Launch(Ctx* ctx, const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t shmem,
+                      Args&&... args) {
+  return LaunchOn(ctx, ctx->stream, name, kernel, grid, block, shmem, std::forward<Args>(args)...);
+}
+
+// Fork the side stream off the main stream / join it back.
+inline int32_t ForkSide(Ctx* ctx) {
+  if (hipEventRecord(ctx->ev_fork, ctx->stream) != hipSuccess || hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0) != hipSuccess)
+    return SetError(PXG_INTERNAL, "side stream fork failed");
+  return PXG_OK;
+}
+inline int32_t JoinSide(Ctx* ctx) {
+  if (hipEventRecord(ctx->ev_join, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0) != hipSuccess)
+    return SetError(PXG_INTERNAL, "side stream join failed");
   return PXG_OK;
 }
 

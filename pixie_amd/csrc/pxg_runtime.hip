@@ -250,6 +250,12 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
     delete c;
     return SetError(PXG_INTERNAL, "hipStreamCreate: %s", hipGetErrorString(e));
   }
+  if (hipStreamCreateWithFlags(&c->impl.side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_join, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return SetError(PXG_INTERNAL, "side stream / event creation failed");
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->impl.num_cus = prop.multiProcessorCount;
   if (hipHostMalloc(&c->impl.pinned, 4096, hipHostMallocDefault) != hipSuccess) c->impl.pinned = nullptr;
@@ -263,6 +269,10 @@ extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   ctx->impl.ResolveTimings();
   for (auto e : ctx->impl.free_events) hipEventDestroy(e);
   if (ctx->impl.pinned) hipHostFree(ctx->impl.pinned);
+  hipStreamSynchronize(ctx->impl.side);
+  hipEventDestroy(ctx->impl.ev_fork);
+  hipEventDestroy(ctx->impl.ev_join);
+  hipStreamDestroy(ctx->impl.side);
   hipStreamDestroy(ctx->impl.stream);
   delete ctx;
   return PXG_OK;

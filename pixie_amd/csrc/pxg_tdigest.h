@@ -45,11 +45,13 @@ __device__ __forceinline__ double IntegratedQ(double k) {
 }
 __device__ __forceinline__ double IntegratedLocation(double q) { return kDelta * (asin(2.0 * q - 1.0) + kPi / 2) / kPi; }
 
-// wLimit after a boundary at index b (W total unit weights).
-__device__ __forceinline__ double NextLimit(int64_t b, double W) {
+// wLimit after a boundary at index b (W total unit weights).  x = b / W is formed as
+// b * (1/W) on the fast path: that moves wl by ~W * 1e-16, far inside the 1e-9 margin that
+// sends a near-integer wl to the reference's own expression (which divides exactly).
+__device__ __forceinline__ double NextLimit(int64_t b, double W, double invW) {
   const double kCos = 0.99999506519785548;   // cos(pi/1000)
   const double kSin = 0.0031415874858795635; // sin(pi/1000)
-  const double x = static_cast<double>(b) / W;
+  const double x = static_cast<double>(static_cast<int32_t>(b)) * invW;
   const double t = 2.0 * x - 1.0;
   bool exact = t >= kCos - 1e-9;
   double wl = 0;
@@ -111,16 +113,18 @@ __device__ inline int64_t DigestBoundaries(int64_t W, uint32_t* starts, int64_t 
   int64_t nc = 0;
   starts[nc++] = 0;
   const double Wd = static_cast<double>(W);
+  const double invW = 1.0 / Wd;
   double wl = Wd * IntegratedQ(1.0);
-  int64_t i = 1;
+  int32_t i = 1;
+  const int32_t W32 = static_cast<int32_t>(W);  // W < 2^31 (staged rows are < 2^32 per agg)
   while (true) {
     const double f = floor(wl);
-    int64_t b = f >= static_cast<double>(W) ? W : static_cast<int64_t>(f);
+    int32_t b = f >= Wd ? W32 : static_cast<int32_t>(f);
     if (b < i) b = i;
-    if (b >= W) break;
+    if (b >= W32) break;
     if (nc >= max_c) return -1;
     starts[nc++] = static_cast<uint32_t>(b);
-    wl = NextLimit(b, Wd);
+    wl = NextLimit(b, Wd, invW);
     i = b + 1;
   }
   return nc;
