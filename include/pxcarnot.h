@@ -1,0 +1,68 @@
+/*
+ * pxcarnot.h — C ABI of the C++ host engine above libpxg (libpxcarnot.so).
+ *
+ * This is the host side of the drop-in: it takes an unmodified, PxL-compiled
+ * px.carnot.planpb.Plan in its binary wire format, builds the execution graph the way
+ * ExecutionGraph::Init does (src/carnot/exec/exec_graph.cc:52-104), with the GPU node classes
+ * at the operator switch, and runs it over RowBatches of host tables.  The node classes keep
+ * the reference's ExecNode NVI (Init / Prepare / Open / ConsumeNext / Close,
+ * src/carnot/exec/exec_node.h:145-315) and resolve every ScalarFunc / AggregateExpression by
+ * (name, registry arg types) like udf::Registry (src/carnot/udf/registry.cc:172-198).
+ *
+ * Reference interfaces replaced:
+ *   pxc_execute_plan   Carnot::ExecutePlan for one plan fragment
+ *                      (src/carnot/carnot.cc:221-333) over MemorySource tables
+ *                      (src/carnot/exec/memory_source_node.cc:54-124).
+ *   pxc_explain_plan   the lowering step alone (no device): which nodes the operator switch
+ *                      picks, fused chains, compiled device programs.
+ *
+ * Errors: px.statuspb.Code values (src/common/base/statuspb/status.proto:27-52);
+ * pxc_last_error() has the message.  There is no CPU execution path: a plan whose operators
+ * or UDF/UDA signatures have no device implementation fails with UNIMPLEMENTED / NOT_FOUND.
+ */
+#ifndef PXCARNOT_H_
+#define PXCARNOT_H_
+
+#include <stdint.h>
+
+#include "pxg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A MemorySource table as a sequence of RowBatches (batch-major: cols[b * ncols + c]).
+ * batch_flags (optional): bit0 eow, bit1 eos per batch; when NULL the source behaves like
+ * MemorySourceNode (eow = eos = true on the last batch). */
+typedef struct {
+  const char* name;
+  int32_t ncols;
+  int32_t nbatches;
+  const int32_t* col_types;
+  const pxg_column_view* cols;
+  const uint8_t* batch_flags;
+} pxc_table;
+
+typedef struct pxc_engine pxc_engine;
+
+int32_t pxc_engine_create(int32_t device, pxc_engine** out);
+int32_t pxc_engine_destroy(pxc_engine* engine);
+
+/* Executes the first plan fragment of a binary planpb.Plan.  Every sink's RowBatches are
+ * serialised into *out (PXRB layout: tests/oracle_client.py::parse_pxrb), released with
+ * pxc_free. */
+int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                         const pxc_table* tables, uint8_t** out, int64_t* out_len);
+
+/* Lowering only (no device): a text description of the node graph and device programs. */
+int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables,
+                         char** out);
+
+void pxc_free(void* p);
+const char* pxc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PXCARNOT_H_ */

@@ -1,0 +1,1216 @@
+// C++ host engine: the reference's execution-graph layer with GPU nodes at the operator switch.
+//
+// Reference structure mirrored (names kept):
+//   ExecNode NVI ........................ src/carnot/exec/exec_node.h:145-315
+//   ExecutionGraph::Init / Execute ...... src/carnot/exec/exec_graph.cc:52-289
+//   MemorySourceNode .................... src/carnot/exec/memory_source_node.cc:54-124
+//   FilterNode / MapNode / AggNode ...... filter_node.cc:78-171, map_node.cc:47-71, agg_node.cc:88-542
+//   MemorySinkNode ...................... src/carnot/exec/memory_sink_node.cc
+//   udf::Registry lookup ................ src/carnot/udf/registry.cc:172-198
+//   UDF / UDA signatures ................ src/carnot/funcs/builtins/math_ops.cc:52-250,
+//                                         math_sketches.cc:25-28
+// The GPU nodes call libpxg (include/pxg.h) only; nothing here computes a row on the CPU.
+// Post-aggregation work on the G result rows (QuantilesUDA's JSON rendering,
+// math_sketches.h:40-54, and pluck_float64 of it, json_ops.h:131-153) is host-side output
+// formatting, as in the reference, where UDA Finalize runs on the host.
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <sstream>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/pxcarnot.h"
+#include "../../include/pxg.h"
+#include "planpb_wire.h"
+
+namespace pxc {
+
+// ---------------------------------------------------------------------------------------
+// Status (px::Status with statuspb codes, src/common/base/status.h:150-160).
+// ---------------------------------------------------------------------------------------
+struct Status {
+  int32_t code = PXG_OK;
+  std::string msg;
+  bool ok() const { return code == PXG_OK; }
+  static Status OK() { return Status(); }
+};
+
+static Status Err(int32_t code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  Status s;
+  s.code = code;
+  s.msg = buf;
+  return s;
+}
+
+static Status FromPxg(int32_t code) {
+  if (code == PXG_OK) return Status::OK();
+  const char* m = pxg_last_error();
+  return Err(code, "%s", m ? m : "libpxg error");
+}
+
+#define PXC_RETURN_IF_ERROR(expr) \
+  do {                            \
+    Status s_ = (expr);           \
+    if (!s_.ok()) return s_;      \
+  } while (0)
+#define PXG_CALL(expr) PXC_RETURN_IF_ERROR(FromPxg(expr))
+
+static thread_local std::string g_last_error;
+
+// ---------------------------------------------------------------------------------------
+// RowBatch (src/table_store/schema/row_batch.h:40-129): Arrow-layout host columns, shared and
+// never mutated; eow / eos flags.
+// ---------------------------------------------------------------------------------------
+struct HostColumn {
+  int32_t type = 0;
+  int64_t length = 0;
+  const void* values = nullptr;
+  const int32_t* offsets = nullptr;
+  const uint8_t* data = nullptr;
+  std::shared_ptr<void> owner;  // keeps library-allocated buffers alive
+
+  pxg_column_view View() const {
+    pxg_column_view v{};
+    v.type = type;
+    v.length = length;
+    v.values = values;
+    v.offsets = offsets;
+    v.data = data;
+    return v;
+  }
+};
+
+// Owns one pxg_column_out (released with pxg_result_free).
+struct OutHolder {
+  pxg_column_out c{};
+  ~OutHolder() { pxg_result_free(&c, 1); }
+};
+
+static HostColumn FromOut(const pxg_column_out& c) {
+  auto h = std::make_shared<OutHolder>();
+  h->c = c;
+  HostColumn hc;
+  hc.type = c.type;
+  hc.length = c.length;
+  hc.values = c.values;
+  hc.offsets = c.offsets;
+  hc.data = c.data;
+  hc.owner = h;
+  return hc;
+}
+
+// A column built on the host (string / double vectors), owning its buffers.
+struct OwnedColumn {
+  std::vector<uint8_t> values;
+  std::vector<int32_t> offsets;
+  std::vector<uint8_t> data;
+};
+
+static HostColumn StringColumn(const std::vector<std::string>& vals) {
+  auto o = std::make_shared<OwnedColumn>();
+  o->offsets.push_back(0);
+  for (auto& s : vals) {
+    o->data.insert(o->data.end(), s.begin(), s.end());
+    o->offsets.push_back(static_cast<int32_t>(o->data.size()));
+  }
+  o->data.resize(o->data.size() + 16, 0);
+  HostColumn hc;
+  hc.type = PXG_STRING;
+  hc.length = static_cast<int64_t>(vals.size());
+  hc.offsets = o->offsets.data();
+  hc.data = o->data.data();
+  hc.owner = o;
+  return hc;
+}
+
+static HostColumn DoubleColumn(const std::vector<double>& vals) {
+  auto o = std::make_shared<OwnedColumn>();
+  o->values.resize(vals.size() * 8 + 8);
+  if (!vals.empty()) std::memcpy(o->values.data(), vals.data(), vals.size() * 8);
+  HostColumn hc;
+  hc.type = PXG_FLOAT64;
+  hc.length = static_cast<int64_t>(vals.size());
+  hc.values = o->values.data();
+  hc.owner = o;
+  return hc;
+}
+
+struct RowBatch {
+  std::vector<HostColumn> cols;
+  int64_t num_rows = 0;
+  bool eow = false, eos = false;
+};
+
+using RowDescriptor = std::vector<int32_t>;  // column types (schema::RowDescriptor)
+
+// ---------------------------------------------------------------------------------------
+// Device programs and the device UDF / UDA registry (compile.py is the same table).
+// ---------------------------------------------------------------------------------------
+struct Program {
+  std::vector<pxg_insn> insns;
+  std::vector<uint8_t> pool;
+  int32_t result_type = 0;
+  pxg_program View() const {
+    pxg_program p{};
+    p.n_insns = static_cast<int32_t>(insns.size());
+    p.result_type = result_type;
+    p.insns = insns.data();
+    p.pool_len = static_cast<int32_t>(pool.size());
+    p.pool = pool.empty() ? nullptr : pool.data();
+    return p;
+  }
+  bool IsColumn() const { return insns.size() == 1 && insns[0].op == PXG_OP_COL; }
+};
+
+static pxg_insn Insn(int op, int type, int32_t arg = 0, int64_t imm = 0) {
+  pxg_insn i;
+  i.op = static_cast<uint16_t>(op);
+  i.type = static_cast<uint16_t>(type);
+  i.arg = arg;
+  i.imm = imm;
+  return i;
+}
+
+// Append `src` to `dst`, relocating its constant-pool references.
+static void AppendProgram(const Program& src, Program* dst) {
+  const int32_t base = static_cast<int32_t>(dst->pool.size());
+  dst->pool.insert(dst->pool.end(), src.pool.begin(), src.pool.end());
+  for (pxg_insn i : src.insns) {
+    if (i.op == PXG_OP_CONST && (i.type == PXG_STRING || i.type == PXG_UINT128)) i.arg += base;
+    dst->insns.push_back(i);
+  }
+}
+
+struct UdfDef {
+  int32_t result = 0;
+  int lconv = 0, rconv = 0;  // conversion opcode applied after operand 0 / 1
+  std::vector<int> ops;      // empty: relabel (x + 0)
+};
+
+enum : int32_t { B = PXG_BOOLEAN, I = PXG_INT64, U = PXG_UINT128, F = PXG_FLOAT64, S = PXG_STRING, T = PXG_TIME64NS };
+
+class Registry {
+ public:
+  Registry() {
+    auto reg = [&](const char* n, std::vector<int32_t> a, int32_t res, std::vector<int> ops, int l = 0, int r = 0) {
+      udfs_[{n, a}] = UdfDef{res, l, r, ops};
+    };
+    // arithmetic (math_ops.h:33-150, math_ops.cc:57-105)
+    reg("add", {I, I}, I, {PXG_OP_ADD_I}); reg("add", {F, F}, F, {PXG_OP_ADD_F});
+    reg("add", {F, I}, F, {PXG_OP_ADD_F}, 0, PXG_OP_I2F); reg("add", {I, F}, F, {PXG_OP_ADD_F}, PXG_OP_I2F);
+    reg("add", {T, I}, T, {PXG_OP_ADD_I}); reg("add", {I, T}, T, {PXG_OP_ADD_I});
+    reg("subtract", {I, I}, I, {PXG_OP_SUB_I}); reg("subtract", {F, F}, F, {PXG_OP_SUB_F});
+    reg("subtract", {F, I}, F, {PXG_OP_SUB_F}, 0, PXG_OP_I2F); reg("subtract", {I, F}, F, {PXG_OP_SUB_F}, PXG_OP_I2F);
+    reg("subtract", {T, I}, T, {PXG_OP_SUB_I}); reg("subtract", {T, T}, I, {PXG_OP_SUB_I}); reg("subtract", {I, T}, I, {PXG_OP_SUB_I});
+    for (auto ab : std::vector<std::pair<int32_t, int32_t>>{{I, I}, {F, I}, {I, F}, {F, F}})  // DivideUDF: double(a)/double(b)
+      reg("divide", {ab.first, ab.second}, F, {PXG_OP_DIV_F}, ab.first == I ? PXG_OP_I2F : 0, ab.second == I ? PXG_OP_I2F : 0);
+    reg("multiply", {I, I}, I, {PXG_OP_MUL_I}); reg("multiply", {F, F}, F, {PXG_OP_MUL_F});
+    reg("multiply", {F, I}, F, {PXG_OP_MUL_F}, 0, PXG_OP_I2F); reg("multiply", {I, F}, F, {PXG_OP_MUL_F}, PXG_OP_I2F);
+    for (auto ab : std::vector<std::pair<int32_t, int32_t>>{{T, I}, {T, T}, {I, T}, {I, I}}) reg("modulo", {ab.first, ab.second}, I, {PXG_OP_MOD_I});
+    // logical (math_ops.h:265-315)
+    reg("logicalOr", {I, I}, B, {PXG_OP_OR}); reg("logicalOr", {B, B}, B, {PXG_OP_OR});
+    reg("logicalAnd", {I, I}, B, {PXG_OP_AND}); reg("logicalAnd", {B, B}, B, {PXG_OP_AND});
+    reg("logicalNot", {I}, B, {PXG_OP_NOT}); reg("logicalNot", {B}, B, {PXG_OP_NOT});
+    reg("negate", {I}, I, {PXG_OP_NEG_I}); reg("negate", {F}, F, {PXG_OP_NEG_F}); reg("invert", {I}, I, {PXG_OP_INV_I});
+    // equality (math_ops.cc:145-175); FLOAT64 == FLOAT64 is ApproxEqualUDF
+    for (int32_t t : {I, T, B}) { reg("equal", {t, t}, B, {PXG_OP_EQ_I}); reg("notEqual", {t, t}, B, {PXG_OP_NE_I}); }
+    reg("equal", {S, S}, B, {PXG_OP_EQ_S}); reg("notEqual", {S, S}, B, {PXG_OP_NE_S});
+    reg("equal", {U, U}, B, {PXG_OP_EQ_U}); reg("notEqual", {U, U}, B, {PXG_OP_NE_U});
+    reg("equal", {B, I}, B, {PXG_OP_EQ_I}); reg("equal", {I, B}, B, {PXG_OP_EQ_I});
+    reg("notEqual", {B, I}, B, {PXG_OP_NE_I}); reg("notEqual", {I, B}, B, {PXG_OP_NE_I});
+    reg("equal", {I, F}, B, {PXG_OP_EQ_F}, PXG_OP_I2F); reg("equal", {F, I}, B, {PXG_OP_EQ_F}, 0, PXG_OP_I2F);
+    reg("notEqual", {I, F}, B, {PXG_OP_NE_F}, PXG_OP_I2F); reg("notEqual", {F, I}, B, {PXG_OP_NE_F}, 0, PXG_OP_I2F);
+    reg("equal", {F, F}, B, {PXG_OP_APPROX_EQ_F}); reg("notEqual", {F, F}, B, {PXG_OP_APPROX_NE_F});
+    reg("approxEqual", {F, F}, B, {PXG_OP_APPROX_EQ_F});
+    // ordering (math_ops.h:412-510)
+    const std::vector<std::tuple<const char*, int, int, int>> ord = {
+        {"greaterThan", PXG_OP_GT_I, PXG_OP_GT_F, PXG_OP_GT_S}, {"greaterThanEqual", PXG_OP_GE_I, PXG_OP_GE_F, PXG_OP_GE_S},
+        {"lessThan", PXG_OP_LT_I, PXG_OP_LT_F, PXG_OP_LT_S}, {"lessThanEqual", PXG_OP_LE_I, PXG_OP_LE_F, PXG_OP_LE_S}};
+    for (auto& o : ord) {
+      reg(std::get<0>(o), {I, I}, B, {std::get<1>(o)}); reg(std::get<0>(o), {T, T}, B, {std::get<1>(o)});
+      reg(std::get<0>(o), {F, F}, B, {std::get<2>(o)}); reg(std::get<0>(o), {S, S}, B, {std::get<3>(o)});
+    }
+    // bin (math_ops.h:512-527)
+    reg("bin", {I, I}, I, {PXG_OP_BIN_I}); reg("bin", {T, T}, T, {PXG_OP_BIN_I}); reg("bin", {I, T}, I, {PXG_OP_BIN_I});
+    reg("bin", {T, I}, T, {PXG_OP_BIN_I}); reg("bin", {F, I}, I, {PXG_OP_BIN_I}, PXG_OP_F2I);
+    reg("time_to_int64", {T}, I, {}); reg("int64_to_time", {I}, T, {});
+    // FilterNodeTest's registry-local UDF (filter_node_test.cc:41-53).
+    reg("eq", {I, I}, B, {PXG_OP_EQ_I}); reg("eq", {S, S}, B, {PXG_OP_EQ_S});
+
+    // UDAs: (name, registry types) -> (kind, arg type, output type)
+    auto uda = [&](const char* n, std::vector<int32_t> a, int32_t kind, int32_t at, int32_t out) {
+      udas_[{n, a}] = std::make_tuple(kind, at, out);
+    };
+    for (int32_t t : {F, I, B}) uda("mean", {t}, PXG_UDA_MEAN, t, F);
+    uda("sum", {F}, PXG_UDA_SUM, F, F); uda("sum", {I}, PXG_UDA_SUM, I, I); uda("sum", {B}, PXG_UDA_SUM, B, I);
+    for (int32_t t : {F, I, T}) { uda("max", {t}, PXG_UDA_MAX, t, t); uda("min", {t}, PXG_UDA_MIN, t, t); }
+    for (int32_t t : {F, I, T, B, S, U}) uda("count", {t}, PXG_UDA_COUNT, t, I);
+    uda("quantiles", {I}, PXG_UDA_QUANTILES, I, S); uda("quantiles", {F}, PXG_UDA_QUANTILES, F, S);
+    // AggNodeTest's registry-local test UDAs (agg_node_test.cc:44-72, 282-289).
+    uda("minsum", {I, I}, PXG_UDA_MINSUM, I, I); uda("minsum_w_init", {I, I, I}, PXG_UDA_MINSUM, I, I);
+  }
+  const UdfDef* GetScalarUDF(const std::string& n, const std::vector<int32_t>& t) const {
+    auto it = udfs_.find({n, t});
+    return it == udfs_.end() ? nullptr : &it->second;
+  }
+  const std::tuple<int32_t, int32_t, int32_t>* GetUDA(const std::string& n, const std::vector<int32_t>& t) const {
+    auto it = udas_.find({n, t});
+    return it == udas_.end() ? nullptr : &it->second;
+  }
+
+ private:
+  std::map<std::pair<std::string, std::vector<int32_t>>, UdfDef> udfs_;
+  std::map<std::pair<std::string, std::vector<int32_t>>, std::tuple<int32_t, int32_t, int32_t>> udas_;
+};
+
+static const Registry& GetRegistry() {
+  static const Registry r;
+  return r;
+}
+
+static std::string TypeName(int32_t t) {
+  switch (t) {
+    case B: return "BOOLEAN";
+    case I: return "INT64";
+    case U: return "UINT128";
+    case F: return "FLOAT64";
+    case S: return "STRING";
+    case T: return "TIME64NS";
+    default: return "UNKNOWN";
+  }
+}
+
+static std::string Signature(const std::string& name, const std::vector<int32_t>& types) {
+  std::string s = name + "(";
+  for (size_t i = 0; i < types.size(); ++i) s += (i ? "," : "") + TypeName(types[i]);
+  return s + ")";
+}
+
+// Lowers planpb.ScalarExpression trees (ScalarExpression walker, scalar_expression.h:243-346).
+// env[i] is the program that computes input column i (a bare column reference, or a Map
+// expression substituted into downstream operators when a chain is fused).
+class ExprCompiler {
+ public:
+  explicit ExprCompiler(std::vector<Program> env) : env_(std::move(env)) {}
+  Status Compile(const planpb::ScalarExpression& e, Program* out) const {
+    Program p;
+    PXC_RETURN_IF_ERROR(Emit(e, &p));
+    *out = std::move(p);
+    return Status::OK();
+  }
+  Status Const(const planpb::ScalarValue& v, Program* p) const {
+    const int32_t dt = v.data_type;
+    switch (dt) {
+      case B: p->insns.push_back(Insn(PXG_OP_CONST, dt, 0, v.bool_value ? 1 : 0)); break;
+      case I: p->insns.push_back(Insn(PXG_OP_CONST, dt, 0, v.int64_value)); break;
+      case T: p->insns.push_back(Insn(PXG_OP_CONST, dt, 0, v.time64_ns_value)); break;
+      case F: {
+        int64_t bits;
+        std::memcpy(&bits, &v.float64_value, 8);
+        p->insns.push_back(Insn(PXG_OP_CONST, dt, 0, bits));
+        break;
+      }
+      case S: {
+        const int32_t off = static_cast<int32_t>(p->pool.size());
+        p->pool.insert(p->pool.end(), v.string_value.begin(), v.string_value.end());
+        while (p->pool.size() % 8) p->pool.push_back(0);
+        p->insns.push_back(Insn(PXG_OP_CONST, dt, off, static_cast<int64_t>(v.string_value.size())));
+        break;
+      }
+      case U: {
+        const int32_t off = static_cast<int32_t>(p->pool.size());
+        const uint8_t* lo = reinterpret_cast<const uint8_t*>(&v.u128_low);
+        const uint8_t* hi = reinterpret_cast<const uint8_t*>(&v.u128_high);
+        p->pool.insert(p->pool.end(), lo, lo + 8);
+        p->pool.insert(p->pool.end(), hi, hi + 8);
+        p->insns.push_back(Insn(PXG_OP_CONST, dt, off, 16));
+        break;
+      }
+      default: return Err(PXG_UNIMPLEMENTED, "constant of type %d", dt);
+    }
+    p->result_type = dt;
+    return Status::OK();
+  }
+
+ private:
+  Status Emit(const planpb::ScalarExpression& e, Program* p) const {
+    switch (e.kind) {
+      case planpb::ScalarExpression::kColumn: {
+        const uint64_t idx = e.column.index;
+        if (idx >= env_.size()) return Err(PXG_INVALID_ARGUMENT, "column %llu out of range", (unsigned long long)idx);
+        AppendProgram(env_[idx], p);
+        p->result_type = env_[idx].result_type;
+        return Status::OK();
+      }
+      case planpb::ScalarExpression::kConstant: return Const(e.constant, p);
+      case planpb::ScalarExpression::kFunc: {
+        const planpb::ScalarFunc& f = *e.func;
+        if (!f.init_args.empty()) return Err(PXG_UNIMPLEMENTED, "scalar UDF %s with init args", f.name.c_str());
+        std::vector<Program> parts(f.args.size());
+        std::vector<int32_t> types;
+        for (size_t i = 0; i < f.args.size(); ++i) {
+          PXC_RETURN_IF_ERROR(Emit(f.args[i], &parts[i]));
+          types.push_back(parts[i].result_type);
+        }
+        const UdfDef* d = GetRegistry().GetScalarUDF(f.name, types);
+        if (!d) return Err(PXG_NOT_FOUND, "no device UDF %s", Signature(f.name, types).c_str());
+        for (size_t i = 0; i < parts.size(); ++i) {
+          AppendProgram(parts[i], p);
+          const int conv = i == 0 ? d->lconv : d->rconv;
+          if (conv) p->insns.push_back(Insn(conv, conv == PXG_OP_I2F ? F : I));
+        }
+        for (int op : d->ops) p->insns.push_back(Insn(op, d->result));
+        if (d->ops.empty()) {  // time_to_int64 / int64_to_time: same bits, relabelled (x + 0)
+          p->insns.push_back(Insn(PXG_OP_CONST, I, 0, 0));
+          p->insns.push_back(Insn(PXG_OP_ADD_I, d->result));
+        }
+        p->result_type = d->result;
+        return Status::OK();
+      }
+      default: return Err(PXG_INVALID_ARGUMENT, "empty scalar expression");
+    }
+  }
+  std::vector<Program> env_;
+};
+
+static std::vector<Program> ColumnEnv(const RowDescriptor& types) {
+  std::vector<Program> env(types.size());
+  for (size_t i = 0; i < types.size(); ++i) {
+    env[i].insns.push_back(Insn(PXG_OP_COL, types[i], static_cast<int32_t>(i)));
+    env[i].result_type = types[i];
+  }
+  return env;
+}
+
+// ---------------------------------------------------------------------------------------
+// ExecState: the device context + registry shared by one query's nodes (exec_state.h:52-180).
+// ---------------------------------------------------------------------------------------
+struct ExecState {
+  pxg_ctx* ctx = nullptr;  // null when only lowering (pxc_explain_plan)
+};
+
+// ---------------------------------------------------------------------------------------
+// ExecNode NVI (src/carnot/exec/exec_node.h:145-315).
+// ---------------------------------------------------------------------------------------
+class ExecNode {
+ public:
+  virtual ~ExecNode() = default;
+  Status Init(const planpb::Operator& op, const RowDescriptor& output, const std::vector<RowDescriptor>& inputs) {
+    output_ = output;
+    inputs_ = inputs;
+    return InitImpl(op);
+  }
+  Status Prepare(ExecState* s) { return PrepareImpl(s); }
+  Status Open(ExecState* s) { return OpenImpl(s); }
+  Status Close(ExecState* s) { return CloseImpl(s); }
+  // exec_node.h:213-226: eos implies eow.
+  Status ConsumeNext(ExecState* s, const RowBatch& rb, size_t parent_index) {
+    if (rb.eos && !rb.eow) return Err(PXG_INTERNAL, "RowBatch has eos set without eow");
+    return ConsumeNextImpl(s, rb, parent_index);
+  }
+  void AddChild(ExecNode* child, size_t parent_index) { children_.push_back({child, parent_index}); }
+  const RowDescriptor& output_descriptor() const { return output_; }
+  virtual std::string DebugString() const = 0;
+
+ protected:
+  virtual Status InitImpl(const planpb::Operator& op) = 0;
+  virtual Status PrepareImpl(ExecState*) { return Status::OK(); }
+  virtual Status OpenImpl(ExecState*) { return Status::OK(); }
+  virtual Status CloseImpl(ExecState*) { return Status::OK(); }
+  virtual Status ConsumeNextImpl(ExecState*, const RowBatch&, size_t) { return Err(PXG_INTERNAL, "not a consumer"); }
+  // exec_node.h:285-297: depth-first push to every child.
+  Status SendRowBatchToChildren(ExecState* s, const RowBatch& rb) {
+    for (auto& c : children_) PXC_RETURN_IF_ERROR(c.first->ConsumeNext(s, rb, c.second));
+    return Status::OK();
+  }
+  RowDescriptor output_;
+  std::vector<RowDescriptor> inputs_;
+  std::vector<std::pair<ExecNode*, size_t>> children_;
+};
+
+// MemorySourceNode (memory_source_node.cc:54-124) over a host table's RowBatches.
+class MemorySourceNode : public ExecNode {
+ public:
+  MemorySourceNode(const pxc_table* t) : table_(t) {}
+  std::string DebugString() const override { return "MemorySourceNode(" + std::string(table_->name) + ")"; }
+  // With explicit batch flags every given batch is fed, as the reference's ExecNodeTester does
+  // (src/carnot/exec/test_utils.h:319-480); otherwise the source stops at eos.
+  bool HasBatchesRemaining() const {
+    if (table_->batch_flags && table_->nbatches > 0) return next_ < table_->nbatches;
+    return next_ < std::max<int32_t>(table_->nbatches, 1) && !done_;
+  }
+  // GenerateNext: one RowBatch (column-projected) to the children.
+  Status GenerateNext(ExecState* s) {
+    RowBatch rb;
+    const int32_t nb = table_->nbatches;
+    if (nb == 0) {  // empty table: one zero-row batch with eow/eos (memory_source_node.cc:107-118)
+      for (size_t c = 0; c < idxs_.size(); ++c) {
+        HostColumn hc;
+        hc.type = output_[c];
+        static const int32_t zero_off[2] = {0, 0};
+        static const uint8_t pad[16] = {0};
+        hc.offsets = zero_off;
+        hc.data = pad;
+        hc.values = pad;
+        rb.cols.push_back(hc);
+      }
+      rb.eow = rb.eos = true;
+      done_ = true;
+      return SendRowBatchToChildren(s, rb);
+    }
+    const int32_t b = next_++;
+    for (int64_t c : idxs_) {
+      const pxg_column_view& v = table_->cols[static_cast<int64_t>(b) * table_->ncols + c];
+      HostColumn hc;
+      hc.type = v.type;
+      hc.length = v.length;
+      hc.values = v.values;
+      hc.offsets = v.offsets;
+      hc.data = v.data;
+      rb.cols.push_back(hc);
+      rb.num_rows = v.length;
+    }
+    if (table_->batch_flags) {
+      rb.eow = (table_->batch_flags[b] & 1) != 0;
+      rb.eos = (table_->batch_flags[b] & 2) != 0;
+    } else {
+      rb.eow = rb.eos = (b == nb - 1);
+    }
+    if (rb.eos) done_ = true;
+    return SendRowBatchToChildren(s, rb);
+  }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    idxs_ = op.mem_source.column_idxs;
+    if (idxs_.empty())
+      for (int32_t c = 0; c < table_->ncols; ++c) idxs_.push_back(c);
+    for (int64_t c : idxs_)
+      if (c < 0 || c >= table_->ncols) return Err(PXG_INVALID_ARGUMENT, "source column %lld out of range", (long long)c);
+    return Status::OK();
+  }
+
+ private:
+  const pxc_table* table_;
+  std::vector<int64_t> idxs_;
+  int32_t next_ = 0;
+  bool done_ = false;
+};
+
+// Uploads a RowBatch into a fresh device table.
+static Status UploadBatch(pxg_ctx* ctx, const RowBatch& rb, const RowDescriptor& types, pxg_table** out) {
+  PXG_CALL(pxg_table_create(ctx, static_cast<int32_t>(types.size()), types.data(), out));
+  if (rb.num_rows > 0) {
+    std::vector<pxg_column_view> v;
+    for (auto& c : rb.cols) v.push_back(c.View());
+    PXG_CALL(pxg_table_append(*out, v.data(), rb.num_rows));
+  }
+  PXG_CALL(pxg_table_flush(*out));
+  return Status::OK();
+}
+
+static Status FetchAll(pxg_table* t, int32_t ncols, RowBatch* rb) {
+  const int64_t n = pxg_table_num_rows(t);
+  rb->num_rows = n;
+  for (int32_t c = 0; c < ncols; ++c) {
+    pxg_column_out o{};
+    PXG_CALL(pxg_table_fetch(t, c, 0, n, &o));
+    rb->cols.push_back(FromOut(o));
+  }
+  return Status::OK();
+}
+
+// GpuFilterNode (FilterNode, filter_node.cc:78-171): one output batch per input batch.
+class GpuFilterNode : public ExecNode {
+ public:
+  std::string DebugString() const override { return "GpuFilterNode"; }
+  Program pred;
+  std::vector<int32_t> select;
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    ExprCompiler comp(ColumnEnv(inputs_[0]));
+    PXC_RETURN_IF_ERROR(comp.Compile(op.filter.expression, &pred));
+    if (pred.result_type != B) return Err(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
+    for (auto& c : op.filter.columns) select.push_back(static_cast<int32_t>(c.index));
+    if (select.empty())
+      for (size_t c = 0; c < inputs_[0].size(); ++c) select.push_back(static_cast<int32_t>(c));
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    pxg_table* in = nullptr;
+    PXC_RETURN_IF_ERROR(UploadBatch(s->ctx, rb, inputs_[0], &in));
+    pxg_table* out = nullptr;
+    const pxg_program p = pred.View();
+    int32_t code = pxg_filter(in, &p, static_cast<int32_t>(select.size()), select.data(), 0, rb.num_rows, &out);
+    RowBatch ob;
+    Status st = FromPxg(code);
+    if (st.ok()) st = FetchAll(out, static_cast<int32_t>(select.size()), &ob);
+    if (out) pxg_table_destroy(out);
+    pxg_table_destroy(in);
+    PXC_RETURN_IF_ERROR(st);
+    ob.eow = rb.eow;
+    ob.eos = rb.eos;
+    return SendRowBatchToChildren(s, ob);
+  }
+};
+
+// GpuMapNode (MapNode, map_node.cc:47-71): one output column per expression.
+class GpuMapNode : public ExecNode {
+ public:
+  std::string DebugString() const override { return "GpuMapNode"; }
+  std::vector<Program> exprs;
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    ExprCompiler comp(ColumnEnv(inputs_[0]));
+    for (auto& e : op.map.expressions) {
+      exprs.emplace_back();
+      PXC_RETURN_IF_ERROR(comp.Compile(e, &exprs.back()));
+    }
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    pxg_table* in = nullptr;
+    PXC_RETURN_IF_ERROR(UploadBatch(s->ctx, rb, inputs_[0], &in));
+    std::vector<pxg_program> pv;
+    for (auto& e : exprs) pv.push_back(e.View());
+    pxg_table* out = nullptr;
+    int32_t code = pxg_map(in, static_cast<int32_t>(pv.size()), pv.data(), 0, rb.num_rows, &out);
+    RowBatch ob;
+    Status st = FromPxg(code);
+    if (st.ok()) st = FetchAll(out, static_cast<int32_t>(pv.size()), &ob);
+    if (out) pxg_table_destroy(out);
+    pxg_table_destroy(in);
+    PXC_RETURN_IF_ERROR(st);
+    ob.eow = rb.eow;
+    ob.eos = rb.eos;
+    return SendRowBatchToChildren(s, ob);
+  }
+};
+
+// Shortest round-trip rendering of a double, always with a '.' or an exponent (the form
+// rapidjson's Writer::Double produces for QuantilesUDA::Finalize).
+static std::string JsonDouble(double v) {
+  if (std::isnan(v) || std::isinf(v)) return "null";
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof(buf), v);
+  std::string s(buf, r.ptr);
+  if (s.find_first_of(".e") == std::string::npos) s += ".0";
+  return s;
+}
+
+static const char* const kQuantileKeys[7] = {"p01", "p10", "p25", "p50", "p75", "p90", "p99"};
+
+// GpuAggNode (AggNode, agg_node.cc:88-542).  When the graph builder fused a
+// Filter / Map chain in front of it, `filter` and the substituted key / argument programs
+// evaluate that chain inside the consume kernel.  Blocking: emits one batch at eos; windowed:
+// one batch per eow, then ClearAggState (agg_node.cc:169-180).
+class GpuAggNode : public ExecNode {
+ public:
+  std::string DebugString() const override { return fused_ ? "GpuAggNode(fused filter/map chain)" : "GpuAggNode"; }
+  // Set by the graph builder for a fused chain: the agg's input columns as programs over the
+  // source table, and the conjunction of the chain's predicates.
+  std::vector<Program> env;
+  bool has_filter = false;
+  Program filter;
+  bool fused_ = false;
+  RowDescriptor source_types;
+
+  std::vector<Program> keys;
+  struct Uda {
+    int32_t kind, arg_type, out_type;
+    Program arg, arg2;
+    bool has_arg = false, has_arg2 = false, has_init = false;
+    int64_t init = 0;
+  };
+  std::vector<Uda> udas;
+  bool windowed = false;
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    const planpb::AggregateOperator& a = op.agg;
+    if (env.empty()) env = ColumnEnv(inputs_[0]);
+    if (source_types.empty()) source_types = inputs_[0];
+    windowed = a.windowed;
+    ExprCompiler comp(env);
+    for (auto& g : a.groups) {
+      if (g.index >= env.size()) return Err(PXG_INVALID_ARGUMENT, "group column %llu out of range", (unsigned long long)g.index);
+      keys.push_back(env[g.index]);
+    }
+    for (auto& v : a.values) {  // AggregateExpression -> registry (registry_arg_types = init ++ args)
+      std::vector<Program> args(v.args.size());
+      std::vector<int32_t> types;
+      for (auto& ia : v.init_args) types.push_back(ia.data_type);
+      for (size_t i = 0; i < v.args.size(); ++i) {
+        if (v.args[i].is_column) {
+          planpb::ScalarExpression e;
+          e.kind = planpb::ScalarExpression::kColumn;
+          e.column = v.args[i].column;
+          PXC_RETURN_IF_ERROR(comp.Compile(e, &args[i]));
+        } else {
+          PXC_RETURN_IF_ERROR(comp.Const(v.args[i].constant, &args[i]));
+        }
+        types.push_back(args[i].result_type);
+      }
+      auto* d = GetRegistry().GetUDA(v.name, types);
+      if (!d) return Err(PXG_NOT_FOUND, "no device UDA %s", Signature(v.name, types).c_str());
+      Uda u;
+      u.kind = std::get<0>(*d);
+      u.arg_type = std::get<1>(*d);
+      u.out_type = std::get<2>(*d);
+      if (!args.empty()) { u.arg = args[0]; u.has_arg = true; }
+      if (args.size() > 1 && u.kind != PXG_UDA_COUNT) { u.arg2 = args[1]; u.has_arg2 = true; }
+      if (!v.init_args.empty()) { u.has_init = true; u.init = v.init_args[0].int64_value; }
+      udas.push_back(u);
+    }
+    if (output_.size() != keys.size() + udas.size())  // agg_node.cc:109-112
+      return Err(PXG_INVALID_ARGUMENT, "output relation arity %zu != groups + values %zu", output_.size(), keys.size() + udas.size());
+    return Status::OK();
+  }
+  Status OpenImpl(ExecState* s) override {
+    if (!s->ctx) return Status::OK();
+    PXC_RETURN_IF_ERROR(CreateAgg(s->ctx));
+    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
+    return Status::OK();
+  }
+  Status CloseImpl(ExecState*) override {
+    if (agg_) pxg_agg_destroy(agg_);
+    if (staging_) pxg_table_destroy(staging_);
+    agg_ = nullptr;
+    staging_ = nullptr;
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    // Tiny batches are coalesced by the table's staging before they reach HBM.
+    if (rb.num_rows > 0) {
+      std::vector<pxg_column_view> v;
+      for (auto& c : rb.cols) v.push_back(c.View());
+      PXG_CALL(pxg_table_append(staging_, v.data(), rb.num_rows));
+    }
+    if (!(rb.eos || (windowed && rb.eow))) return Status::OK();  // agg_node.cc:169-171
+    PXG_CALL(pxg_table_flush(staging_));
+    PXG_CALL(pxg_agg_consume(agg_, staging_, 0, pxg_table_num_rows(staging_)));
+    int64_t groups = 0;
+    PXG_CALL(pxg_agg_finalize(agg_, &groups));
+    std::vector<pxg_column_out> out(keys.size() + udas.size());
+    PXG_CALL(pxg_agg_result(agg_, out.data(), static_cast<int32_t>(out.size())));
+    RowBatch ob;
+    ob.num_rows = out.empty() ? 0 : out[0].length;
+    for (size_t c = 0; c < out.size(); ++c) {
+      const bool q = c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
+      HostColumn hc = FromOut(out[c]);
+      if (q) {  // QuantilesUDA::Finalize JSON (math_sketches.h:40-54) from the 7 device doubles
+        const double* d = static_cast<const double*>(hc.values);
+        std::vector<std::string> js(static_cast<size_t>(hc.length));
+        for (int64_t g = 0; g < hc.length; ++g) {
+          std::string j = "{";
+          for (int k = 0; k < 7; ++k) j += std::string(k ? "," : "") + "\"" + kQuantileKeys[k] + "\":" + JsonDouble(d[g * 7 + k]);
+          js[static_cast<size_t>(g)] = j + "}";
+        }
+        quantiles_raw_[c] = hc;
+        ob.cols.push_back(StringColumn(js));
+      } else {
+        ob.cols.push_back(hc);
+      }
+    }
+    ob.eow = rb.eow;
+    ob.eos = rb.eos;
+    // New staging for the next window, ClearAggState (agg_node.cc:173-180).
+    pxg_table_destroy(staging_);
+    staging_ = nullptr;
+    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
+    PXG_CALL(pxg_agg_reset(agg_));
+    return SendRowBatchToChildren(s, ob);
+  }
+
+ public:
+  // Raw 7-double quantile columns of the last emitted batch (post-agg pluck reads them).
+  std::map<size_t, HostColumn> quantiles_raw_;
+
+ private:
+  Status CreateAgg(pxg_ctx* ctx) {
+    std::vector<pxg_program> kp;
+    for (auto& k : keys) kp.push_back(k.View());
+    std::vector<pxg_uda_spec> us(udas.size());
+    for (size_t i = 0; i < udas.size(); ++i) {
+      pxg_uda_spec& x = us[i];
+      std::memset(&x, 0, sizeof(x));
+      x.kind = udas[i].kind;
+      x.arg_type = udas[i].arg_type;
+      if (udas[i].has_arg) x.arg = udas[i].arg.View();
+      if (udas[i].has_arg2) x.arg2 = udas[i].arg2.View();
+      x.has_init = udas[i].has_init ? 1 : 0;
+      x.init_i64 = udas[i].init;
+    }
+    pxg_agg_spec spec{};
+    spec.n_keys = static_cast<int32_t>(kp.size());
+    spec.n_udas = static_cast<int32_t>(us.size());
+    spec.keys = kp.data();
+    spec.udas = us.data();
+    pxg_program fp = filter.View();
+    spec.filter = has_filter ? &fp : nullptr;
+    spec.expected_groups = 0;
+    spec.windowed = windowed ? 1 : 0;
+    PXG_CALL(pxg_agg_create(ctx, &spec, &agg_));
+    return Status::OK();
+  }
+  pxg_agg* agg_ = nullptr;
+  pxg_table* staging_ = nullptr;
+};
+
+// Post-aggregation Map over the G result rows: column references and pluck_float64 of a
+// quantiles column (PluckAsFloat64UDF, json_ops.h:131-153, on the digest's own doubles).
+class PostAggMapNode : public ExecNode {
+ public:
+  explicit PostAggMapNode(GpuAggNode* agg) : agg_(agg) {}
+  std::string DebugString() const override { return "PostAggMapNode(column refs, pluck_float64)"; }
+
+ protected:
+  struct Out {
+    int64_t col = 0;
+    int quantile = -1;  // >= 0: pluck of quantile key index
+  };
+  std::vector<Out> outs_;
+  Status InitImpl(const planpb::Operator& op) override {
+    for (auto& e : op.map.expressions) {
+      Out o;
+      if (e.kind == planpb::ScalarExpression::kColumn) {
+        o.col = static_cast<int64_t>(e.column.index);
+      } else if (e.kind == planpb::ScalarExpression::kFunc && e.func->name == "pluck_float64" && e.func->args.size() == 2 &&
+                 e.func->args[0].kind == planpb::ScalarExpression::kColumn &&
+                 e.func->args[1].kind == planpb::ScalarExpression::kConstant) {
+        o.col = static_cast<int64_t>(e.func->args[0].column.index);
+        const std::string& key = e.func->args[1].constant.string_value;
+        for (int k = 0; k < 7; ++k)
+          if (key == kQuantileKeys[k]) o.quantile = k;
+        if (o.quantile < 0) return Err(PXG_UNIMPLEMENTED, "pluck_float64 key %s is not a quantile key", key.c_str());
+      } else {
+        return Err(PXG_UNIMPLEMENTED, "post-aggregate Map supports column references and pluck_float64 only");
+      }
+      if (o.col < 0 || o.col >= static_cast<int64_t>(inputs_[0].size())) return Err(PXG_INVALID_ARGUMENT, "column out of range");
+      outs_.push_back(o);
+    }
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    RowBatch ob;
+    ob.num_rows = rb.num_rows;
+    for (auto& o : outs_) {
+      if (o.quantile < 0) {
+        ob.cols.push_back(rb.cols[static_cast<size_t>(o.col)]);
+        continue;
+      }
+      auto it = agg_->quantiles_raw_.find(static_cast<size_t>(o.col));
+      if (it == agg_->quantiles_raw_.end()) return Err(PXG_UNIMPLEMENTED, "pluck_float64 of a column that is not a quantiles UDA");
+      const double* d = static_cast<const double*>(it->second.values);
+      std::vector<double> v(static_cast<size_t>(rb.num_rows));
+      for (int64_t g = 0; g < rb.num_rows; ++g) v[static_cast<size_t>(g)] = d[g * 7 + o.quantile];
+      ob.cols.push_back(DoubleColumn(v));
+    }
+    ob.eow = rb.eow;
+    ob.eos = rb.eos;
+    return SendRowBatchToChildren(s, ob);
+  }
+
+ private:
+  GpuAggNode* agg_;
+};
+
+// MemorySinkNode / GRPCSinkNode result table: collects the batches.
+class SinkNode : public ExecNode {
+ public:
+  explicit SinkNode(std::string name) : name(std::move(name)) {}
+  std::string DebugString() const override { return "SinkNode(" + name + ")"; }
+  std::string name;
+  std::vector<RowBatch> batches;
+
+ protected:
+  Status InitImpl(const planpb::Operator&) override { return Status::OK(); }
+  Status ConsumeNextImpl(ExecState*, const RowBatch& rb, size_t) override {
+    batches.push_back(rb);
+    return Status::OK();
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// ExecutionGraph (exec_graph.cc:52-289): nodes in DAG order, the operator switch picks the GPU
+// node classes, and a MemorySource -> (Filter | Map)* -> Agg(blocking) chain whose
+// intermediates have no other consumer is fused into one GpuAggNode (its intermediate batches
+// are unobservable: a blocking agg emits only at eos, agg_node.cc:169-171).
+// ---------------------------------------------------------------------------------------
+class ExecutionGraph {
+ public:
+  Status Init(const planpb::PlanFragment& pf, int32_t ntables, const pxc_table* tables) {
+    // Topological order from the DAG (plan_fragment.cc:108-118); this engine runs linear chains.
+    std::map<uint64_t, const planpb::Operator*> ops;
+    for (auto& n : pf.nodes) ops[n.id] = &n.op;
+    std::vector<uint64_t> order;
+    if (!pf.dag.empty()) {
+      for (auto& d : pf.dag) {
+        if (d.sorted_parents.size() > 1 || d.sorted_children.size() > 1)
+          return Err(PXG_UNIMPLEMENTED, "only linear plan fragments run on the device engine");
+        order.push_back(d.id);
+      }
+    } else {
+      for (auto& n : pf.nodes) order.push_back(n.id);
+    }
+    std::vector<const planpb::Operator*> chain;
+    for (uint64_t id : order) {
+      auto it = ops.find(id);
+      if (it == ops.end()) return Err(PXG_NOT_FOUND, "plan node %llu missing", (unsigned long long)id);
+      chain.push_back(it->second);
+    }
+    if (chain.empty() || chain[0]->which != 2) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource");
+    const planpb::MemorySourceOperator& ms = chain[0]->mem_source;
+    const pxc_table* tab = nullptr;
+    for (int32_t t = 0; t < ntables; ++t)
+      if (ms.name == tables[t].name) tab = &tables[t];
+    if (!tab) return Err(PXG_NOT_FOUND, "table %s not found", ms.name.c_str());
+    auto* src = new MemorySourceNode(tab);
+    pool_.emplace_back(src);
+    RowDescriptor src_types;
+    if (ms.column_idxs.empty())
+      for (int32_t c = 0; c < tab->ncols; ++c) src_types.push_back(tab->col_types[c]);
+    else
+      for (int64_t c : ms.column_idxs) {
+        if (c < 0 || c >= tab->ncols) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
+        src_types.push_back(tab->col_types[c]);
+      }
+    PXC_RETURN_IF_ERROR(src->Init(*chain[0], src_types, {}));
+    source_ = src;
+    ExecNode* parent = src;
+    RowDescriptor cur = src_types;
+
+    // Fusable prefix: Filter / Map operators up to a blocking Agg.
+    size_t i = 1;
+    size_t agg_at = 0;
+    for (size_t j = 1; j < chain.size(); ++j) {
+      const int w = chain[j]->which;
+      if (w == 4) {
+        if (!chain[j]->agg.windowed) agg_at = j;
+        break;
+      }
+      if (w != 3 && w != 6) break;
+    }
+    if (agg_at > 0) {
+      // Substitute the chain into programs over the source columns.
+      std::vector<Program> env = ColumnEnv(src_types);
+      bool has_filter = false;
+      Program filter;
+      for (size_t j = 1; j < agg_at; ++j) {
+        const planpb::Operator& op = *chain[j];
+        ExprCompiler comp(env);
+        if (op.which == 6) {
+          Program p;
+          PXC_RETURN_IF_ERROR(comp.Compile(op.filter.expression, &p));
+          if (p.result_type != B) return Err(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
+          if (!has_filter) {
+            filter = p;
+          } else {
+            AppendProgram(p, &filter);
+            filter.insns.push_back(Insn(PXG_OP_AND, B));
+          }
+          has_filter = true;
+          std::vector<Program> ne;
+          for (auto& c : op.filter.columns) {
+            if (c.index >= env.size()) return Err(PXG_INVALID_ARGUMENT, "filter column out of range");
+            ne.push_back(env[c.index]);
+          }
+          if (!op.filter.columns.empty()) env = ne;
+        } else {
+          std::vector<Program> ne(op.map.expressions.size());
+          for (size_t e = 0; e < ne.size(); ++e) PXC_RETURN_IF_ERROR(comp.Compile(op.map.expressions[e], &ne[e]));
+          env = ne;
+        }
+      }
+      auto* agg = new GpuAggNode();
+      pool_.emplace_back(agg);
+      agg->env = env;
+      agg->has_filter = has_filter;
+      agg->filter = filter;
+      agg->fused_ = agg_at > 1;
+      agg->source_types = src_types;
+      RowDescriptor env_types;
+      for (auto& p : env) env_types.push_back(p.result_type);
+      PXC_RETURN_IF_ERROR(agg->Init(*chain[agg_at], AggOutputTypes(*chain[agg_at], env, &agg_out_ok_), {env_types}));
+      PXC_RETURN_IF_ERROR(agg_out_ok_);
+      parent->AddChild(agg, 0);
+      parent = agg;
+      cur = agg->output_descriptor();
+      last_agg_ = agg;
+      i = agg_at + 1;
+      lowered_.push_back(agg);
+    }
+    for (; i < chain.size(); ++i) {
+      const planpb::Operator& op = *chain[i];
+      ExecNode* node = nullptr;
+      RowDescriptor out;
+      switch (op.which) {
+        case 6: {
+          auto* f = new GpuFilterNode();
+          node = f;
+          for (auto& c : op.filter.columns) out.push_back(cur.at(c.index));
+          if (op.filter.columns.empty()) out = cur;
+          break;
+        }
+        case 3: {
+          if (last_agg_ && parent == last_agg_) {
+            node = new PostAggMapNode(last_agg_);
+            for (auto& e : op.map.expressions) {
+              if (e.kind == planpb::ScalarExpression::kColumn && e.column.index < cur.size()) out.push_back(cur[e.column.index]);
+              else out.push_back(F);
+            }
+          } else {
+            auto* m = new GpuMapNode();
+            node = m;
+            ExprCompiler comp(ColumnEnv(cur));
+            for (auto& e : op.map.expressions) {
+              Program p;
+              PXC_RETURN_IF_ERROR(comp.Compile(e, &p));
+              out.push_back(p.result_type);
+            }
+          }
+          break;
+        }
+        case 4: {
+          auto* a = new GpuAggNode();
+          node = a;
+          Status st;
+          out = AggOutputTypes(op, ColumnEnv(cur), &st);
+          PXC_RETURN_IF_ERROR(st);
+          last_agg_ = a;
+          break;
+        }
+        case 5:
+        case 1000: {
+          auto* s = new SinkNode(op.which == 5 ? op.mem_sink.name : op.grpc_sink_table);
+          node = s;
+          sinks_.push_back(s);
+          out = cur;
+          break;
+        }
+        default: return Err(PXG_UNIMPLEMENTED, "operator (oneof field %d) has no device node", op.which);
+      }
+      pool_.emplace_back(node);
+      PXC_RETURN_IF_ERROR(node->Init(op, out, {cur}));
+      parent->AddChild(node, 0);
+      lowered_.push_back(node);
+      parent = node;
+      cur = out;
+    }
+    if (sinks_.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no sink");
+    return Status::OK();
+  }
+
+  // ExecuteSources (exec_graph.cc:177-289).
+  Status Execute(ExecState* s) {
+    for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Prepare(s));
+    for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Open(s));
+    Status st;
+    while (st.ok() && source_->HasBatchesRemaining()) st = source_->GenerateNext(s);
+    for (auto& n : pool_) {
+      Status c = n->Close(s);
+      if (st.ok()) st = c;
+    }
+    return st;
+  }
+
+  std::string Explain() const {
+    std::ostringstream os;
+    os << source_->DebugString() << "\n";
+    for (auto* n : lowered_) {
+      os << "  -> " << n->DebugString() << " out=[";
+      for (size_t i = 0; i < n->output_descriptor().size(); ++i) os << (i ? "," : "") << TypeName(n->output_descriptor()[i]);
+      os << "]\n";
+      if (auto* a = dynamic_cast<const GpuAggNode*>(n)) {
+        if (a->has_filter) os << "     filter: " << ProgString(a->filter) << "\n";
+        for (auto& k : a->keys) os << "     key: " << ProgString(k) << "\n";
+        for (auto& u : a->udas) os << "     uda kind=" << u.kind << " arg=" << (u.has_arg ? ProgString(u.arg) : "-") << "\n";
+      }
+    }
+    return os.str();
+  }
+
+  std::vector<SinkNode*> sinks_;
+
+ private:
+  static std::string ProgString(const Program& p) {
+    std::ostringstream os;
+    for (size_t i = 0; i < p.insns.size(); ++i)
+      os << (i ? " " : "") << p.insns[i].op << ":" << p.insns[i].type << ":" << p.insns[i].arg << ":" << p.insns[i].imm;
+    return os.str();
+  }
+  // AggregateOperator output relation: groups, then values (agg_node.cc:336-346).
+  static RowDescriptor AggOutputTypes(const planpb::Operator& op, const std::vector<Program>& env, Status* st) {
+    RowDescriptor out;
+    *st = Status::OK();
+    for (auto& g : op.agg.groups) {
+      if (g.index >= env.size()) {
+        *st = Err(PXG_INVALID_ARGUMENT, "group column out of range");
+        return out;
+      }
+      out.push_back(env[g.index].result_type);
+    }
+    for (auto& v : op.agg.values) {
+      std::vector<int32_t> types;
+      for (auto& ia : v.init_args) types.push_back(ia.data_type);
+      for (auto& a : v.args) {
+        if (a.is_column) {
+          if (a.column.index >= env.size()) {
+            *st = Err(PXG_INVALID_ARGUMENT, "aggregate argument column out of range");
+            return out;
+          }
+          types.push_back(env[a.column.index].result_type);
+        } else {
+          types.push_back(a.constant.data_type);
+        }
+      }
+      auto* d = GetRegistry().GetUDA(v.name, types);
+      if (!d) {
+        *st = Err(PXG_NOT_FOUND, "no device UDA %s", Signature(v.name, types).c_str());
+        return out;
+      }
+      out.push_back(std::get<2>(*d));
+    }
+    return out;
+  }
+
+  std::vector<std::unique_ptr<ExecNode>> pool_;
+  std::vector<ExecNode*> lowered_;
+  MemorySourceNode* source_ = nullptr;
+  GpuAggNode* last_agg_ = nullptr;
+  Status agg_out_ok_;
+};
+
+// PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).
+struct Writer {
+  std::vector<uint8_t> buf;
+  template <typename V>
+  void put(V v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    buf.insert(buf.end(), p, p + sizeof(V));
+  }
+  void bytes(const void* p, size_t n) {
+    if (n) buf.insert(buf.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
+  }
+};
+
+static void WriteBatch(Writer* w, const RowBatch& rb) {
+  w->put<int64_t>(rb.num_rows);
+  w->put<uint8_t>(rb.eow);
+  w->put<uint8_t>(rb.eos);
+  w->put<uint16_t>(0);
+  w->put<uint32_t>(static_cast<uint32_t>(rb.cols.size()));
+  const size_t n = static_cast<size_t>(rb.num_rows);
+  for (auto& c : rb.cols) {
+    w->put<int32_t>(c.type);
+    switch (c.type) {
+      case B: w->bytes(c.values, n); break;
+      case U: w->bytes(c.values, n * 16); break;
+      case S: {
+        const int32_t o0 = n ? c.offsets[0] : 0;
+        for (size_t i = 0; i <= n; ++i) w->put<int32_t>(n ? c.offsets[i] - o0 : 0);
+        if (n) w->bytes(c.data + o0, static_cast<size_t>(c.offsets[n] - o0));
+        break;
+      }
+      default: w->bytes(c.values, n * 8); break;
+    }
+  }
+}
+
+}  // namespace pxc
+
+using namespace pxc;
+
+struct pxc_engine {
+  pxg_ctx* ctx = nullptr;
+};
+
+static int32_t Fail(const Status& s) {
+  g_last_error = s.msg;
+  return s.code;
+}
+
+extern "C" const char* pxc_last_error(void) { return g_last_error.c_str(); }
+extern "C" void pxc_free(void* p) { std::free(p); }
+
+extern "C" int32_t pxc_engine_create(int32_t device, pxc_engine** out) {
+  if (!out) return Fail(Err(PXG_INVALID_ARGUMENT, "out is null"));
+  auto* e = new pxc_engine();
+  const int32_t c = pxg_ctx_create(device, &e->ctx);
+  if (c != PXG_OK) {
+    delete e;
+    return Fail(FromPxg(c));
+  }
+  *out = e;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_engine_destroy(pxc_engine* e) {
+  if (!e) return PXG_OK;
+  pxg_ctx_destroy(e->ctx);
+  delete e;
+  return PXG_OK;
+}
+
+static Status Lower(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, ExecutionGraph* g) {
+  if (!plan || plan_len < 0) return Err(PXG_INVALID_ARGUMENT, "no plan");
+  planpb::Plan p;
+  try {
+    p = planpb::DecodePlan(plan, static_cast<size_t>(plan_len));
+  } catch (const planpb::WireError& e) {
+    return Err(PXG_INVALID_ARGUMENT, "%s", e.what());
+  }
+  if (p.fragments.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no fragments");
+  return g->Init(p.fragments[0], ntables, tables);
+}
+
+extern "C" int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, char** out) {
+  ExecutionGraph g;
+  Status s = Lower(plan, plan_len, ntables, tables, &g);
+  if (!s.ok()) return Fail(s);
+  const std::string txt = g.Explain();
+  *out = static_cast<char*>(std::malloc(txt.size() + 1));
+  std::memcpy(*out, txt.c_str(), txt.size() + 1);
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                                    const pxc_table* tables, uint8_t** out, int64_t* out_len) {
+  if (!engine || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  ExecutionGraph g;
+  Status s = Lower(plan, plan_len, ntables, tables, &g);
+  if (!s.ok()) return Fail(s);
+  ExecState st;
+  st.ctx = engine->ctx;
+  s = g.Execute(&st);
+  if (!s.ok()) return Fail(s);
+  Writer w;
+  w.put<uint32_t>(0x42525850u);  // "PXRB"
+  w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
+  for (auto* sk : g.sinks_) {
+    w.put<uint32_t>(static_cast<uint32_t>(sk->name.size()));
+    w.bytes(sk->name.data(), sk->name.size());
+    w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
+    for (auto& rb : sk->batches) WriteBatch(&w, rb);
+  }
+  *out_len = static_cast<int64_t>(w.buf.size());
+  *out = static_cast<uint8_t*>(std::malloc(w.buf.size()));
+  std::memcpy(*out, w.buf.data(), w.buf.size());
+  return PXG_OK;
+}
