@@ -23,7 +23,8 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20250117
-KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "radix_hist", "radix_scatter",
+KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "slot_flags", "slot_gslot", "group_heads",
+           "radix_hist", "radix_scatter",
            "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
            "digest_chain", "quant_tiny", "quant_small", "quant_mid", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
            "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",

@@ -106,7 +106,8 @@ __device__ __forceinline__ void ProcessRow(const AggPlanDev* __restrict__ plan, 
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanDev* __restrict__ plan,
                                                                   const DevChunk* __restrict__ chunks,
                                                                   const TileRange* __restrict__ ranges, int nranges,
-                                                                  int64_t ntiles, AggTableDev tab, StageDev stg) {
+                                                                  int64_t ntiles, AggTableDev tab, StageDev stg,
+                                                                  uint32_t /*nchunks: signature shared with the fast path*/) {
   constexpr int kPer = kConsumeTile / kConsumeBlock;
   constexpr int kWaves = kConsumeBlock / 64;
   __shared__ int32_t s_sel[kConsumeTile];
@@ -358,24 +359,49 @@ __device__ __forceinline__ bool FastKeysEqualArena(const AggPlanDev* __restrict_
   return eq;
 }
 
+// Key-column base pointers of one chunk.  The consume kernel keeps them in LDS for the first
+// kLdsChunks chunks, so comparing against a group's representative row does not first fetch
+// the row's chunk descriptor from global memory (one dependent round trip less per probe).
+constexpr int kLdsChunks = 64;
+template <int NK>
+struct KeyCols {
+  const int32_t* off[NK];  // STRING offsets
+  const uint8_t* dat[NK];  // STRING payload, or the values of a fixed-width key
+};
+
+template <int NK>
+__device__ __forceinline__ KeyCols<NK> KeyColsOf(const AggPlanDev* __restrict__ plan, const DevChunk& ch) {
+  KeyCols<NK> kc;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const DevCol& col = ch.cols[plan->keys[i].col];
+    kc.off[i] = col.offsets;
+    kc.dat[i] = plan->key_types[i] == PXG_STRING ? col.data : col.values;
+  }
+  return kc;
+}
+
 // Equality against the keys of row r (a group's representative row), compared word by word
 // as the row's payload words arrive; nothing of the row's key is kept in registers.
 template <int NK>
-__device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r,
+__device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ plan, const KeyCols<NK>& kc, int64_t r,
                                                  const FastKeys<NK>& x) {
   bool eq = true;
   const uint8_t* ptr[NK];
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
     const int t = plan->key_types[i];
-    const DevCol& col = ch.cols[plan->keys[i].col];
     if (t == PXG_STRING) {
       int32_t o0, o1;
-      LoadOffsetPair(col.offsets, r, &o0, &o1);
-      ptr[i] = col.data + o0;
+      LoadOffsetPair(kc.off[i], r, &o0, &o1);
+      ptr[i] = kc.dat[i] + o0;
       eq = eq && static_cast<uint32_t>(o1 - o0) == x.len[i];
     } else {
-      const Val v = LoadCol(col, t, r);
+      DevCol c;
+      c.values = kc.dat[i];
+      c.offsets = nullptr;
+      c.data = nullptr;
+      const Val v = LoadCol(c, t, r);
       eq = eq && v.a == x.w[i][0] && (t != PXG_UINT128 || v.b == x.w[i][1]);
     }
   }
@@ -393,16 +419,25 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
 
 template <int NK>
 __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                                     const KeyCols<NK>* __restrict__ s_kc, uint32_t n_lds_chunks,
                                                      const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
                                                      const AggTableDev& tab, unsigned int* s_ins) {
   const uint32_t tag = SlotTag(h);
   uint32_t pos = static_cast<uint32_t>(h) & tab.mask;
   const uint32_t max_probe = min(tab.mask + 1, kMaxProbe);
-  for (uint32_t probe = 0; probe < max_probe; ++probe) {
-    // Plain (cacheable) load: a slot word only ever changes 0 -> final value (by CAS) within a
-    // launch, so a non-zero word seen here is final; a stale 0 just costs the CAS below, which
-    // returns the real word.
+  uint32_t probe = 0;
+  while (probe < max_probe) {
+    // Phase A: walk slot words only, to the first empty slot or tag match.  Lanes of a wave
+    // leave this cheap loop at different probe lengths but meet again for phase B, so the
+    // (expensive) key comparison runs once per wave in the common case instead of once per
+    // probe step.  Plain (cacheable) loads: within a launch a slot word only ever changes
+    // 0 -> final value (by CAS), so a non-zero word is final and a stale 0 costs only the CAS.
     unsigned long long w = tab.slots[pos];
+    while (w != 0 && static_cast<uint32_t>(w >> 33) != tag) {
+      if (++probe >= max_probe) return kDeferredSlot;
+      pos = (pos + 1) & tab.mask;
+      w = tab.slots[pos];
+    }
     if (w == 0) {
       const unsigned int ins = __hip_atomic_load(&tab.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + *s_ins;
       if (ins >= tab.limit) return kDeferredSlot;
@@ -413,18 +448,22 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
         atomicAdd(s_ins, 1u);
         return pos;
       }
-      w = expected;
+      w = expected;  // lost the race: the winner's word decides below
     }
+    // Phase B: exact key comparison against the slot's representative.
     if (static_cast<uint32_t>(w >> 33) == tag) {
       const uint32_t ref = static_cast<uint32_t>(w);
       bool eq;
       if (w & kKindArena) {
         eq = FastKeysEqualArena<NK>(plan, keys, tab.arena + ref);
       } else {
-        eq = FastKeysEqualRow<NK>(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
+        const uint32_t c = ref >> kChunkShift;
+        const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK>(plan, chunks[c]);
+        eq = FastKeysEqualRow<NK>(plan, kc, static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
       }
       if (eq) return pos;
     }
+    ++probe;
     pos = (pos + 1) & tab.mask;
   }
   return kDeferredSlot;
@@ -454,7 +493,8 @@ template <int NK, int MODE>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
-                                                                      int64_t ntiles, AggTableDev tab, StageDev stg) {
+                                                                      int64_t ntiles, AggTableDev tab, StageDev stg,
+                                                                      uint32_t nchunks) {
   constexpr int kPer = kConsumeTile / kConsumeBlock;
   constexpr int kWaves = kConsumeBlock / 64;
   constexpr int kEntries = CacheEntries<NK>();
@@ -462,17 +502,23 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   __shared__ uint32_t s_wcnt[kWaves];
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
-  __shared__ CacheEntry<NK> s_cache[kEntries];
-  __shared__ uint32_t s_claim[kEntries];
+  __shared__ CacheEntry<NK> s_cache[MODE == 1 ? kEntries : 1];
+  __shared__ uint32_t s_claim[MODE == 1 ? kEntries : 1];
+  __shared__ KeyCols<NK> s_kc[kLdsChunks];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
   const int nv = plan->n_vals;
   if (threadIdx.x == 0) s_ins = 0;
-  for (int e = threadIdx.x; e < kEntries; e += kConsumeBlock) {
-    s_cache[e].tag = 0;
-    s_claim[e] = 0;
+  if (MODE == 1) {
+    for (int e = threadIdx.x; e < kEntries; e += kConsumeBlock) {
+      s_cache[e].tag = 0;
+      s_claim[e] = 0;
+    }
   }
+  const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
+  for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK>(plan, chunks[c]);
+  __syncthreads();
   uint32_t round = 0;  // per-workgroup round counter: claim stamps grow monotonically
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
     int ri = 0;
@@ -555,7 +601,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
           if (hit) {
             slot = ce.slot;
           } else {
-            slot = FastFindOrInsert<NK>(plan, chunks, k, h, rowref, tab, &s_ins);
+            slot = FastFindOrInsert<NK>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
             if (MODE == 1 && slot != kDeferredSlot) {
               cidx = e;
               atomicMax(&s_claim[e], stamp);
@@ -796,7 +842,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice, ctx->stream));
   PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
-  void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev) = AggConsumeKernel;
+  void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t) = AggConsumeKernel;
   static const int diag = [] {
     const char* e = std::getenv("PXG_DIAG_CONSUME");
     return e ? std::atoi(e) : 0;
@@ -816,7 +862,8 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   }
   PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", kern, dim3(grid), dim3(kConsumeBlock), 0,
                              d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
-                             static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this)));
+                             static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this),
+                             static_cast<uint32_t>(t->chunks.size())));
   uint32_t n_def = 0;
   PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
   int buf = 0;

@@ -24,7 +24,15 @@ struct ConstValPtrs {
   const uint64_t* p[kMaxVals];
 };
 
-__global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t cap,
+// Sort key of a staged record.  Pass 0 reads table slots and maps them through `rank` (slot ->
+// dense group id; kDeferredSlot / empty -> G, which sorts last); later passes read dense ids.
+__device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G) {
+  if (!rank) return k;
+  return k < cap ? rank[k] : G;
+}
+
+__global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                               const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G,
                                                                int shift, uint32_t* __restrict__ hist, uint32_t nblocks) {
   __shared__ uint32_t h[4][kRadixBuckets];
   uint32_t* hf = &h[0][0];
@@ -36,7 +44,7 @@ __global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* _
   for (int k = 0; k < kRadixItems; ++k) {
     const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
     if (i < n) {
-      const uint32_t key = min(keys[i], cap);
+      const uint32_t key = DenseKey(keys[i], rank, cap, G);
       atomicAdd(&h[wid][(key >> shift) & (kRadixBuckets - 1)], 1u);
     }
   }
@@ -45,26 +53,45 @@ __global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* _
   hist[static_cast<uint64_t>(d) * nblocks + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
-// Stable scatter: items of a tile keep their relative order within each digit.  Ranks within
-// a wave come from an 8-ballot match of the digit bits; waves are ordered through LDS counts.
+// Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stable scatter.  Wave w of a block owns the contiguous quarter [w * 1024, (w + 1) * 1024) of
+// the block's 4096-item tile, in (k, lane) order, so a wave's running per-digit counts live in
+// its own LDS slice and need no block barrier inside the item loop: ranks within a wave come
+// from an 8-ballot match of the digit bits.  The tile is then reordered by digit in LDS and
+// written out in digit runs (consecutive threads -> consecutive addresses), instead of one
+// scattered 4- or 8-byte store per item.
 __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
                                                                   ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n,
-                                                                  uint32_t cap, int shift, const uint32_t* __restrict__ offs,
-                                                                  uint32_t nblocks) {
-  __shared__ uint32_t running[kRadixBuckets];
-  __shared__ uint32_t wcnt[4][kRadixBuckets];
+                                                                  const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G,
+                                                                  int shift, const uint32_t* __restrict__ offs, uint32_t nblocks) {
+  constexpr int kWaves = kRadixBlock / 64;
+  constexpr int kPerWave = kRadixTile / kWaves;
+  __shared__ uint32_t whist[kWaves][kRadixBuckets];
+  __shared__ uint32_t base[kWaves][kRadixBuckets];  // tile-local start of (wave, digit)
+  __shared__ uint32_t dstart[kRadixBuckets];         // tile-local start of each digit
+  __shared__ uint32_t gofs[kRadixBuckets];           // global start of this tile's digit run
+  __shared__ uint32_t s_key[kRadixTile];
+  __shared__ uint64_t s_val[kRadixTile];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
-  running[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * nblocks + blockIdx.x];
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
+  WaveSync();
+  const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
+  const int tn = static_cast<int>(min(static_cast<uint64_t>(kRadixTile), n - tile0));
+  uint32_t part[kRadixItems], keys[kRadixItems], dig[kRadixItems];
+#pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
-    uint32_t* wf = &wcnt[0][0];
-    for (int i = threadIdx.x; i < 4 * kRadixBuckets; i += kRadixBlock) wf[i] = 0;
-    __syncthreads();
-    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
     const bool valid = i < n;
-    const uint32_t key = valid ? kin[i] : 0u;
-    const uint32_t d = (min(key, cap) >> shift) & (kRadixBuckets - 1);
+    const uint32_t key = valid ? DenseKey(kin[i], rank, cap, G) : 0u;
+    const uint32_t d = (key >> shift) & (kRadixBuckets - 1);
     unsigned long long peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < kRadixBits; ++b) {
@@ -72,43 +99,91 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
       const unsigned long long m = __ballot(valid && bit);
       peers &= bit ? m : ~m;
     }
-    const uint32_t rank = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
-    if (valid && rank == 0) wcnt[wid][d] = static_cast<uint32_t>(__popcll(peers));
+    const uint32_t r = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
+    const uint32_t pre = valid ? whist[wid][d] : 0u;
+    WaveSync();
+    if (valid && r == 0) whist[wid][d] = pre + static_cast<uint32_t>(__popcll(peers));
+    WaveSync();
+    part[k] = pre + r;
+    keys[k] = key;
+    dig[k] = d;
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x;  // kRadixBlock == kRadixBuckets
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tot += whist[w][d];
+    // exclusive scan of the tile's digit totals (one digit per thread) through LDS
+    dstart[d] = tot;
     __syncthreads();
-    if (valid) {
-      uint32_t pre = 0;
-      for (int w = 0; w < wid; ++w) pre += wcnt[w][d];
-      const uint32_t pos = running[d] + pre + rank;
-      kout[pos] = key;
-      for (int v = 0; v < nvals; ++v) vout.p[v][pos] = vin.p[v][i];
+    for (int o = 1; o < kRadixBuckets; o <<= 1) {
+      const uint32_t x = d >= o ? dstart[d - o] : 0u;
+      __syncthreads();
+      dstart[d] += x;
+      __syncthreads();
+    }
+    const uint32_t start = dstart[d] - tot;
+    __syncthreads();
+    dstart[d] = start;
+    gofs[d] = offs[static_cast<uint64_t>(d) * nblocks + blockIdx.x];
+    uint32_t acc = start;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      base[w][d] = acc;
+      acc += whist[w][d];
+    }
+  }
+  __syncthreads();
+  uint32_t lpos[kRadixItems];
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    lpos[k] = base[wid][dig[k]] + part[k];
+    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) s_key[lpos[k]] = keys[k];
+  }
+  __syncthreads();
+  // Keys out in digit runs.
+  for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
+    const uint32_t key = s_key[j];
+    const uint32_t d = (key >> shift) & (kRadixBuckets - 1);
+    kout[gofs[d] + (j - dstart[d])] = key;
+  }
+  // Each value stream through the same LDS reordering.
+  for (int v = 0; v < nvals; ++v) {
+#pragma unroll
+    for (int k = 0; k < kRadixItems; ++k) {
+      const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
+      if (i < n) s_val[lpos[k]] = vin.p[v][i];
     }
     __syncthreads();
-    running[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+    for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
+      const uint32_t d = (s_key[j] >> shift) & (kRadixBuckets - 1);
+      vout.p[v][gofs[d] + (j - dstart[d])] = s_val[j];
+    }
     __syncthreads();
   }
 }
 
-__global__ void RunHeadsKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t cap, uint32_t* __restrict__ flags,
-                               unsigned long long* __restrict__ n_valid) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = min(keys[i], cap);
-  const uint32_t prev = i ? min(keys[i - 1], cap) : 0xFFFFFFFFu;
-  flags[i] = (k < cap && k != prev) ? 1u : 0u;
-  if (k == cap && prev != cap) *n_valid = i;
+// Dense group ids of the table's occupied slots, in slot order (rank = exclusive scan of the
+// occupancy flags); gslot[rank] = slot.
+__global__ void SlotFlagsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, uint32_t* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cap) flags[i] = slots[i] != 0 ? 1u : 0u;
+}
+__global__ void SlotGslotKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ rank,
+                                uint32_t* __restrict__ gslot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cap && slots[i] != 0) gslot[rank[i]] = i;
 }
 
-__global__ void GroupStartsKernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ flags,
-                                  const uint32_t* __restrict__ gidx, uint64_t n, uint32_t* __restrict__ gstart,
-                                  uint32_t* __restrict__ gslot, const unsigned long long* __restrict__ n_valid, uint32_t ngroups) {
+// Group starts straight from the sorted dense ids: the first index of every id (ids are dense,
+// so no scan is needed); gstart[G] = the number of records with a valid group.
+__global__ void GroupHeadsKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t G, uint32_t* __restrict__ gstart) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i == 0) gstart[ngroups] = static_cast<uint32_t>(*n_valid);
   if (i >= n) return;
-  if (flags[i]) {
-    const uint32_t g = gidx[i];
-    gstart[g] = static_cast<uint32_t>(i);
-    gslot[g] = keys[i];
-  }
+  const uint32_t k = keys[i];
+  if (i == 0 || keys[i - 1] != k) gstart[k < G ? k : G] = static_cast<uint32_t>(i);
+  if (i == n - 1 && k < G) gstart[G] = static_cast<uint32_t>(n);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -373,12 +448,6 @@ __global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restric
   if (lane < 7) out[static_cast<uint64_t>(g) * 7 + lane] = res;
 }
 
-// Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
-__device__ __forceinline__ void WaveSync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // One wave per group with 64 < n <= 1024: bitonic sort in the wave's LDS slice, singleton
 // digest (W <= 1024 <= kSingletonMaxW).  Waves of a workgroup work on different groups and
@@ -879,7 +948,6 @@ int32_t AggFinalizeImpl(Agg* a) {
   if (n >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
   PXG_RETURN_IF_ERROR(ws.meta.Ensure(64));
   uint8_t* meta = ws.meta.as<uint8_t>();
-  unsigned long long* d_nvalid = reinterpret_cast<unsigned long long*>(meta);
   uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta + 8);
   unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 16);
   uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta + 32);
@@ -892,58 +960,64 @@ int32_t AggFinalizeImpl(Agg* a) {
   }
   PXG_RETURN_IF_ERROR(Launch(ctx, "finalize_init", FinalizeInitKernel, dim3(1), dim3(64), 0, meta, n));
 
-  // 1. Stable LSD radix sort of (slot, vals...) by slot; deferred (invalid) slots map to cap.
-  //    The alternate buffers match the staging capacity so the swap keeps both usable.
-  const int nbits = Log2Ceil(static_cast<uint64_t>(a->cap) + 1);
-  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
-  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
-  const uint64_t cap_rows = std::max<uint64_t>(a->st_cap, n);
-  PXG_RETURN_IF_ERROR(ws.alt_slot.Ensure(cap_rows * 4));
-  for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(ws.alt_val[v].Ensure(cap_rows * 8));
-  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
-  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
-  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(nh, n))) + 64));
-  void* scan_tmp = ws.scan.p;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = p * kRadixBits;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, a->st_slot.as<const uint32_t>(), n,
-                               a->cap, shift, ws.hist.as<uint32_t>(), nblocks));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, scan_tmp));
-    ConstValPtrs vin;
-    ValPtrs vout;
-    for (int v = 0; v < kMaxVals; ++v) {
-      vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
-      vout.p[v] = v < a->n_vals ? ws.alt_val[v].as<uint64_t>() : nullptr;
-    }
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0,
-                               a->st_slot.as<const uint32_t>(), ws.alt_slot.as<uint32_t>(), vin, vout, a->n_vals, n, a->cap, shift,
-                               ws.hist.as<const uint32_t>(), nblocks));
-    std::swap(a->st_slot, ws.alt_slot);
-    for (int v = 0; v < a->n_vals; ++v) std::swap(a->st_val[v], ws.alt_val[v]);
-  }
-  // 2. Runs -> groups.
-  PXG_RETURN_IF_ERROR(ws.flags.Ensure(n * 4));
-  PXG_RETURN_IF_ERROR(ws.gidx.Ensure(n * 4));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "run_heads", RunHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             a->st_slot.as<const uint32_t>(), n, a->cap, ws.flags.as<uint32_t>(), d_nvalid));
-  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.flags.as<const uint32_t>(), ws.gidx.as<uint32_t>(), static_cast<int64_t>(n), d_ngroups, scan_tmp));
-  uint32_t ngroups = 0;
-  PXG_HIP(hipMemcpyAsync(&ngroups, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  // 1. Dense group ids: rank of every occupied table slot (slot order).
+  const uint32_t ngroups = static_cast<uint32_t>(a->inserted);
   R.n_groups = ngroups;
   if (ngroups == 0) {
     R.ready = true;
     return PXG_OK;
   }
-  PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
+  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(n, a->cap) + 1)) + 64));
+  void* scan_tmp = ws.scan.p;
+  PXG_RETURN_IF_ERROR(ws.rank.Ensure(static_cast<size_t>(a->cap) * 4 + 16));
   PXG_RETURN_IF_ERROR(ws.gslot.Ensure(static_cast<size_t>(ngroups) * 4));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "slot_flags", SlotFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                             a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>()));
+  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "slot_gslot", SlotGslotKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                             a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<const uint32_t>(), ws.gslot.as<uint32_t>()));
+
+  // 2. Stable LSD radix sort of (dense id, vals...) by dense id (ceil(log2(G + 1) / 8) passes);
+  //    records without a group (deferred slots) get id G and sort last.  The staging itself is
+  //    left as it is (slots), so finalize can run again and export still works.
+  const int nbits = std::max(1, Log2Ceil(static_cast<uint64_t>(ngroups) + 1));
+  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
+  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
+  for (int b = 0; b < 2; ++b) {
+    PXG_RETURN_IF_ERROR(ws.skey[b].Ensure(n * 4 + 16));
+    for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(ws.sval[b][v].Ensure(n * 8 + 16));
+  }
+  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
+  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
+  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(std::max<uint64_t>(nh, n), a->cap) + 1)) + 64));
+  scan_tmp = ws.scan.p;
+  const uint32_t* kin = a->st_slot.as<const uint32_t>();
+  ConstValPtrs vin;
+  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+  int cur = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * kRadixBits;
+    const uint32_t* rank = p == 0 ? ws.rank.as<const uint32_t>() : nullptr;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, n, rank, a->cap, ngroups,
+                               shift, ws.hist.as<uint32_t>(), nblocks));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, scan_tmp));
+    ValPtrs vout;
+    for (int v = 0; v < kMaxVals; ++v) vout.p[v] = v < a->n_vals ? ws.sval[cur][v].as<uint64_t>() : nullptr;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin,
+                               ws.skey[cur].as<uint32_t>(), vin, vout, a->n_vals, n, rank, a->cap, ngroups, shift,
+                               ws.hist.as<const uint32_t>(), nblocks));
+    kin = ws.skey[cur].as<const uint32_t>();
+    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? ws.sval[cur][v].as<const uint64_t>() : nullptr;
+    cur ^= 1;
+  }
+  const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
+  // 3. Group starts (first index of every id).
+  PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
-  PXG_RETURN_IF_ERROR(Launch(ctx, "group_starts", GroupStartsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             a->st_slot.as<const uint32_t>(), ws.flags.as<const uint32_t>(), ws.gidx.as<const uint32_t>(), n,
-                             ws.gstart.as<uint32_t>(), ws.gslot.as<uint32_t>(), static_cast<const unsigned long long*>(d_nvalid), ngroups));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                             skeys, n, ngroups, ws.gstart.as<uint32_t>()));
   // 3. UDA reductions (chunk partials, then per-group combine).
-  ConstValPtrs cv;
-  for (int v = 0; v < kMaxVals; ++v) cv.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+  const ConstValPtrs cv = vin;
   UdaOut uo;
   for (int u = 0; u < kMaxUdas; ++u) uo.p[u] = nullptr;
   bool any_q = false, any_red = false;
@@ -1047,7 +1121,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
-      const uint64_t* vals = a->st_val[a->uda_val[u]].as<const uint64_t>();
+      const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
       double* qo = R.uda_out[u].as<double>();
       if (cls[0] > 0)
@@ -1114,9 +1188,12 @@ int32_t AggFinalizeImpl(Agg* a) {
   for (int k = 0; k < a->n_keys; ++k)
     if (a->key_types[k] == PXG_STRING)
       PXG_HIP(hipMemcpyAsync(&totals[k], R.key_offsets[k].as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  uint32_t g_dev = 0;
   PXG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(&g_dev, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
+  if (g_dev != ngroups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, ngroups);
   for (int k = 0; k < a->n_keys && n_str > 0; ++k) {
     if (a->key_types[k] != PXG_STRING) continue;
     R.key_data_len[k] = totals[k];
