@@ -217,33 +217,25 @@ struct FastKeys {
   uint32_t len[NK];               // STRING byte length (0 for fixed types)
 };
 
-// Payload words of a string of len <= 8 * kFastStrWords bytes at p, realigned and
-// tail-masked.  The bytes are fetched as 16-byte aligned chunks (<= 4 loads instead of 7
-// eight-byte ones: every load of a divergent wave costs address-processing time per lane);
-// payload buffers are 16-byte aligned with a 16-byte pad, so the over-read stays in bounds.
-constexpr int kFast16 = (8 * kFastStrWords + 15 + 15) / 16;
+// Payload words of a string of len <= 8 * kFastStrWords bytes at p, tail-masked.  The bytes
+// are fetched with 16-byte loads straight from the (unaligned) string start: gfx950 serves
+// unaligned global loads in hardware, so no realignment shifts are needed (<= 3 loads; every
+// load of a divergent wave costs address-processing time per lane).  Payload buffers carry a
+// 16-byte pad, so the over-read of the last load stays in bounds.
+constexpr int kFast16 = kFastStrWords / 2;
 __device__ __forceinline__ void LoadStrWords(const uint8_t* p, uint32_t len, uint64_t* w) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const ulonglong2* b16 = reinterpret_cast<const ulonglong2*>(a & ~uintptr_t(15));
-  const uint32_t n16 = (static_cast<uint32_t>(a & 15) + len + 15) >> 4;
-  uint64_t W[2 * kFast16 + 2];
+  const uint32_t n16 = (len + 15) >> 4;
 #pragma unroll
   for (int i = 0; i < kFast16; ++i) {
     ulonglong2 v = make_ulonglong2(0, 0);
-    if (static_cast<uint32_t>(i) < n16) v = b16[i];
-    W[2 * i] = v.x;
-    W[2 * i + 1] = v.y;
+    if (static_cast<uint32_t>(i) < n16) __builtin_memcpy(&v, p + 16 * i, 16);
+    w[2 * i] = v.x;
+    w[2 * i + 1] = v.y;
   }
-  W[2 * kFast16] = W[2 * kFast16 + 1] = 0;
-  const bool odd = (a & 8) != 0;
-  const unsigned sh = static_cast<unsigned>(a & 7) * 8;
 #pragma unroll
   for (int j = 0; j < kFastStrWords; ++j) {
-    const uint64_t lo = odd ? W[j + 1] : W[j];
-    const uint64_t hi = odd ? W[j + 2] : W[j + 1];
-    const uint64_t x = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
     const int rem = static_cast<int>(len) - 8 * j;
-    w[j] = rem >= 8 ? x : (rem > 0 ? (x & ((1ULL << (rem * 8)) - 1)) : 0);
+    w[j] = rem >= 8 ? w[j] : (rem > 0 ? (w[j] & ((1ULL << (rem * 8)) - 1)) : 0);
   }
 }
 
