@@ -14,6 +14,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 
 def counter_avg(d, kernel, counter):
@@ -21,7 +22,7 @@ def counter_avg(d, kernel, counter):
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path, newline="") as f:
             for row in csv.DictReader(f):
-                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if re.search(kernel, row.get("Kernel_Name", "")) and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} under {d}")
@@ -30,7 +31,7 @@ def counter_avg(d, kernel, counter):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="AggConsumeKernel")
+    ap.add_argument("--kernel", default=r"AggConsume(Fast)?Kernel", help="regex on the kernel name")
     ap.add_argument("--name", default="agg_consume")
     ap.add_argument("--rows", type=int, required=True)
     ap.add_argument("--fetch", required=True)
