@@ -26,7 +26,7 @@ SEED = 20250117
 KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "slot_flags", "slot_gslot", "group_heads",
            "radix_hist", "radix_scatter",
            "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
-           "digest_chain", "quant_tiny", "quant_small", "quant_mid", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
+           "digest_chain", "quant_tiny", "quant_small", "quant_mid", "big_setup", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
            "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",
            "export_slot_part", "export_group_rank", "export_row_digit", "export_write_groups", "export_write_rows",
            "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows"]

@@ -1079,8 +1079,7 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   if (!agg) return SetError(PXG_INVALID_ARGUMENT, "agg is null");
   Agg& a = agg->impl;
   PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
-  PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
-  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));  // stream-ordered before the next consume
   a.st_n = 0;
   a.arena_words = 0;
   a.inserted = 0;

@@ -394,12 +394,12 @@ __device__ __forceinline__ uint64_t BitonicStepWave(uint64_t x, int lane, int k,
 }
 
 // One wave per group with n <= 64: register bitonic sort, singleton digest.
-__global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restrict__ list, uint32_t nlist,
+__global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nlist_p,
                                                        const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
                                                        int arg_type, double* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const uint32_t li = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (li >= nlist) return;
+  if (li >= *nlist_p) return;
   const uint32_t g = list[li];
   const uint32_t s = gstart[g], n = gstart[g + 1] - s;
   uint64_t key = lane < static_cast<int>(n) ? QKey(vals[s + lane], arg_type) : ~0ULL;
@@ -453,13 +453,13 @@ __global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restric
 // digest (W <= 1024 <= kSingletonMaxW).  Waves of a workgroup work on different groups and
 // never meet at a barrier.
 constexpr int kSmallWaves = 4;
-__global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restrict__ list, uint32_t nlist,
+__global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nlist_p,
                                                         const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
                                                         int arg_type, double* __restrict__ out) {
   __shared__ uint64_t keys[kSmallWaves][kSmallMax];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t li = blockIdx.x * kSmallWaves + wid;
-  if (li >= nlist) return;
+  if (li >= *nlist_p) return;
   uint64_t* a = keys[wid];
   const uint32_t g = list[li];
   const uint32_t s = gstart[g];
@@ -632,12 +632,15 @@ struct PreChain {
 // the chain is sequential per group (~1100 steps for any W > kSingletonMaxW), so running it
 // inside each group's digest workgroup serialised the whole workgroup behind one lane.
 constexpr int kChainCap = 2048;
-__global__ void __launch_bounds__(64) DigestChainKernel(const uint32_t* __restrict__ list, uint32_t nlist,
-                                                        const uint32_t* __restrict__ gstart, uint32_t* __restrict__ starts_out,
-                                                        int32_t* __restrict__ nc_out) {
+// Chain slots: list a (mid groups) at [0, a_cap), list b (big groups) at [a_cap, ...).
+__global__ void __launch_bounds__(64) DigestChainKernel(const uint32_t* __restrict__ list_a, const uint32_t* __restrict__ na_p,
+                                                        uint32_t a_cap, const uint32_t* __restrict__ list_b,
+                                                        const uint32_t* __restrict__ nb_p, const uint32_t* __restrict__ gstart,
+                                                        uint32_t* __restrict__ starts_out, int32_t* __restrict__ nc_out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nlist) return;
-  const uint32_t g = list[i];
+  const uint32_t na = *na_p, nb = *nb_p;
+  if (i < a_cap ? i >= na : i - a_cap >= nb) return;
+  const uint32_t g = i < a_cap ? list_a[i] : list_b[i - a_cap];
   const int64_t W = gstart[g + 1] - gstart[g];
   nc_out[i] = W <= kSingletonMaxW ? -2 : static_cast<int32_t>(DigestBoundaries(W, starts_out + static_cast<uint64_t>(i) * kChainCap, kChainCap));
 }
@@ -728,11 +731,12 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_
 // One workgroup per group with 1024 < n <= 4096: LDS bitonic sort + digest.
 __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
                                                       const uint32_t* __restrict__ chain_starts, const int32_t* __restrict__ chain_nc,
-                                                      const uint64_t* __restrict__ vals, int arg_type, double* __restrict__ out,
-                                                      unsigned int* __restrict__ err) {
+                                                      const uint32_t* __restrict__ nlist_p, const uint64_t* __restrict__ vals,
+                                                      int arg_type, double* __restrict__ out, unsigned int* __restrict__ err) {
   __shared__ uint64_t keys[PaddedLen(kMidMax)];
   __shared__ uint32_t starts[kMidCentroids];
   __shared__ DigestShared sh;
+  if (blockIdx.x >= *nlist_p) return;
   const uint32_t g = list[blockIdx.x];
   const uint32_t s = gstart[g], n = gstart[g + 1] - s;
   int P = 64;
@@ -754,8 +758,9 @@ struct BigChunk {
   uint32_t pad;
 };
 
-__global__ void __launch_bounds__(256) BigChunkSortKernel(const BigChunk* __restrict__ chunks, const uint64_t* __restrict__ vals,
-                                                          int arg_type, uint64_t* __restrict__ outk) {
+__global__ void __launch_bounds__(256) BigChunkSortKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
+                                                          const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ outk) {
+  if (blockIdx.x >= *nchunks_p) return;
   __shared__ uint64_t keys[PaddedLen(kMidMax)];
   const BigChunk c = chunks[blockIdx.x];
   for (int i = threadIdx.x; i < kMidMax; i += blockDim.x) keys[PadIdx(i)] = i < static_cast<int>(c.len) ? QKey(vals[c.off + i], arg_type) : ~0ULL;
@@ -771,6 +776,69 @@ struct BigGroup {
   uint32_t g;
   uint32_t passes;  // merge passes it needs: its sorted keys end in keysA (even) / keysB (odd)
 };
+
+// Big-group metadata on the device (one block): per big group its offset, size and merge-pass
+// count, and its 4096-key chunks; meta gets the chunk total and the largest group.
+constexpr int kSetupBlock = 1024;
+__global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                              const uint32_t* __restrict__ gstart, BigGroup* __restrict__ groups,
+                                                              BigChunk* __restrict__ chunks, uint32_t* __restrict__ meta_out) {
+  __shared__ uint32_t scan[kSetupBlock];
+  __shared__ uint32_t s_max;
+  const uint32_t nbig = *count;
+  const int t = threadIdx.x;
+  if (t == 0) s_max = 0;
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nbig; b0 += kSetupBlock) {
+    const uint32_t i = b0 + t;
+    uint32_t g = 0, off = 0, n = 0, nch = 0;
+    if (i < nbig) {
+      g = list[i];
+      off = gstart[g];
+      n = gstart[g + 1] - off;
+      nch = (n + kMidMax - 1) / kMidMax;
+      atomicMax(&s_max, n);
+    }
+    scan[t] = nch;
+    __syncthreads();
+    for (int o = 1; o < kSetupBlock; o <<= 1) {
+      const uint32_t x = t >= o ? scan[t - o] : 0u;
+      __syncthreads();
+      scan[t] += x;
+      __syncthreads();
+    }
+    const uint32_t cbase = carry + scan[t] - nch;
+    const uint32_t tot = scan[kSetupBlock - 1];
+    __syncthreads();
+    if (i < nbig) {
+      uint32_t passes = 0;
+      for (uint64_t r = kMidMax; r < n; r *= 2) ++passes;
+      BigGroup B;
+      B.off = off;
+      B.n = n;
+      B.eoff = 0;
+      B.g = g;
+      B.passes = passes;
+      groups[i] = B;
+      for (uint32_t c = 0; c < nch; ++c) {
+        BigChunk C;
+        C.off = static_cast<uint64_t>(off) + static_cast<uint64_t>(c) * kMidMax;
+        C.g_off = off;
+        C.len = min(static_cast<uint32_t>(kMidMax), n - c * kMidMax);
+        C.g_n = n;
+        C.passes = passes;
+        C.pad = 0;
+        chunks[cbase + c] = C;
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  if (t == 0) {
+    meta_out[0] = carry;  // total chunks
+    meta_out[1] = s_max;  // largest big group
+  }
+}
 
 // Merge-path split of diagonal d between sorted runs A[0,na) and B[0,nb) (ties: A first), by
 // one wave: 64 probes per round, so ~log64(n) dependent global round trips instead of log2.
@@ -796,8 +864,10 @@ __device__ __forceinline__ int64_t WaveMergePath(const uint64_t* __restrict__ A,
 // one 4096-key output tile: its merge-path splits (wave searches), the two input slices
 // staged into LDS with coalesced loads, then 16 outputs per thread by a serial LDS merge.
 // Groups that are already sorted (passes <= pass) are skipped: their keys stay put.
-__global__ void __launch_bounds__(256) BigMergeTileKernel(const BigChunk* __restrict__ chunks, const uint64_t* __restrict__ in,
-                                                          uint64_t* __restrict__ out, uint64_t w, uint32_t pass) {
+__global__ void __launch_bounds__(256) BigMergeTileKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
+                                                          const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t w,
+                                                          uint32_t pass) {
+  if (blockIdx.x >= *nchunks_p) return;
   __shared__ uint64_t s[kMidMax];
   __shared__ int64_t s_split[2];
   const BigChunk c = chunks[blockIdx.x];
@@ -858,12 +928,14 @@ __global__ void __launch_bounds__(256) BigMergeTileKernel(const BigChunk* __rest
 
 constexpr int kBigCentroids = 8192;
 
-__global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restrict__ groups, const uint64_t* __restrict__ keysA,
+__global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ ngroups_p,
+                                                       const uint64_t* __restrict__ keysA,
                                                        const uint64_t* __restrict__ keysB,
                                                        uint32_t* __restrict__ starts_all, const uint32_t* __restrict__ chain_starts,
                                                        const int32_t* __restrict__ chain_nc, double* __restrict__ out,
                                                        unsigned int* __restrict__ err) {
   __shared__ DigestShared sh;
+  if (blockIdx.x >= *ngroups_p) return;
   const BigGroup G = groups[blockIdx.x];
   uint32_t* starts = starts_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
   const uint64_t* k = ((G.passes & 1) ? keysB : keysA) + G.off;
@@ -1048,109 +1120,82 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
     PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
                                ngroups, ws.lists.as<uint32_t>(), d_cls, static_cast<uint32_t>(kMidMax)));
-    uint32_t cls[kNumClasses];
-    PXG_HIP(hipMemcpyAsync(cls, d_cls, sizeof(cls), hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
     const uint32_t* lists = ws.lists.as<const uint32_t>();
-    // Big-group metadata (host side; few groups).
-    std::vector<BigGroup> big;
-    std::vector<BigChunk> bchunks;
-    uint64_t big_total = 0, big_max = 0;
-    if (cls[3] > 0) {
-      std::vector<uint32_t> bl(cls[3]);
-      PXG_HIP(hipMemcpy(bl.data(), lists + 3 * static_cast<uint64_t>(ngroups), cls[3] * 4, hipMemcpyDeviceToHost));
-      std::vector<uint32_t> gs(static_cast<size_t>(ngroups) + 1);
-      PXG_HIP(hipMemcpy(gs.data(), gstart, gs.size() * 4, hipMemcpyDeviceToHost));
-      std::sort(bl.begin(), bl.end());
-      for (uint32_t g : bl) {
-        BigGroup B;
-        B.off = gs[g];
-        B.n = gs[g + 1] - gs[g];
-        B.eoff = big_total;
-        B.g = g;
-        B.passes = 0;
-        for (uint64_t r = kMidMax; r < B.n; r *= 2) ++B.passes;
-        big.push_back(B);
-        big_total += B.n;
-        big_max = std::max<uint64_t>(big_max, B.n);
-        for (uint64_t o = 0; o < B.n; o += kMidMax) {
-          BigChunk c;
-          c.off = B.off + o;
-          c.g_off = B.off;
-          c.len = static_cast<uint32_t>(std::min<uint64_t>(kMidMax, B.n - o));
-          c.g_n = static_cast<uint32_t>(B.n);
-          c.passes = B.passes;
-          c.pad = 0;
-          bchunks.push_back(c);
-        }
-      }
-      PXG_RETURN_IF_ERROR(ws.big.Ensure(big.size() * sizeof(BigGroup)));
-      PXG_HIP(hipMemcpy(ws.big.p, big.data(), big.size() * sizeof(BigGroup), hipMemcpyHostToDevice));
-      PXG_RETURN_IF_ERROR(ws.bchunks.Ensure(bchunks.size() * sizeof(BigChunk)));
-      PXG_HIP(hipMemcpy(ws.bchunks.p, bchunks.data(), bchunks.size() * sizeof(BigChunk), hipMemcpyHostToDevice));
+    // Big-group metadata on the device; one readback of the class counts, the big-group chunk
+    // total and the largest group (grid sizes and the merge-pass count).
+    const uint64_t big_cap = n / (kMidMax + 1) + 1;  // groups of > kMidMax rows
+    const uint64_t chunk_cap = n / kMidMax + big_cap + 1;
+    PXG_RETURN_IF_ERROR(ws.big.Ensure(big_cap * sizeof(BigGroup)));
+    PXG_RETURN_IF_ERROR(ws.bchunks.Ensure(chunk_cap * sizeof(BigChunk)));
+    uint32_t* d_bigmeta = reinterpret_cast<uint32_t*>(meta + 48);
+    PXG_RETURN_IF_ERROR(Launch(ctx, "big_setup", BigSetupKernel, dim3(1), dim3(kSetupBlock), 0, lists + 3 * static_cast<uint64_t>(ngroups),
+                               static_cast<const uint32_t*>(d_cls + 3), gstart, ws.big.as<BigGroup>(), ws.bchunks.as<BigChunk>(),
+                               d_bigmeta));
+    // Kernels whose work lists are counted on the device launch right away with upper-bound
+    // grids (blocks past the device count exit); the host reads the counts back only after
+    // them, so the tiny / small digests and the boundary chains run while it waits.
+    const uint32_t mid_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kSmallMax + 1) + 1));
+    const uint32_t big_cap32 = static_cast<uint32_t>(std::min<uint64_t>(ngroups, big_cap));
+    const uint32_t n_chain_cap = mid_cap + big_cap32;
+    PXG_RETURN_IF_ERROR(ws.chain_nc.Ensure(static_cast<size_t>(n_chain_cap) * 4));
+    PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain_cap) * kChainCap * 4));
+    const uint32_t* chain_starts = ws.chain_starts.as<const uint32_t>();
+    const int32_t* chain_nc = ws.chain_nc.as<const int32_t>();
+    // Chains: latency-bound (a few waves, ~1100 dependent steps each), on the side stream.
+    PXG_RETURN_IF_ERROR(ForkSide(ctx));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain_cap + 63) / 64), dim3(64), 0,
+                                 lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), mid_cap,
+                                 lists + 3 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 3), gstart,
+                                 ws.chain_starts.as<uint32_t>(), ws.chain_nc.as<int32_t>()));
+    const uint32_t small_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kTinyMax + 1) + 1));
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+      const uint64_t* vals = cv.p[a->uda_val[u]];
+      const int at = a->uda_arg_type[u];
+      double* qo = R.uda_out[u].as<double>();
+      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
+                                 static_cast<const uint32_t*>(d_cls), gstart, vals, at, qo));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_small", QuantSmallKernel, dim3((small_cap + kSmallWaves - 1) / kSmallWaves), dim3(256), 0,
+                                 lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart, vals, at, qo));
+    }
+    uint32_t hm[6];
+    PXG_HIP(hipMemcpyAsync(hm, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
+    const uint32_t n_big = cls[3], n_bchunks = hm[4];
+    const uint64_t big_max = hm[5];
+    if (n_big > 0) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
-      PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(big.size() * kBigCentroids * 4));
-    }
-    // Centroid-boundary chains for every mid and big group, one thread each, in one launch:
-    // chain slots [0, cls[2]) follow the mid list, [cls[2], +big) the BigGroup order.
-    const uint32_t n_chain = cls[2] + static_cast<uint32_t>(big.size());
-    const uint32_t* chain_starts = nullptr;
-    const int32_t* chain_nc = nullptr;
-    if (n_chain > 0) {
-      PXG_RETURN_IF_ERROR(ws.chain_list.Ensure(static_cast<size_t>(n_chain) * 4));
-      PXG_RETURN_IF_ERROR(ws.chain_nc.Ensure(static_cast<size_t>(n_chain) * 4));
-      PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain) * kChainCap * 4));
-      uint32_t* cl = ws.chain_list.as<uint32_t>();
-      if (cls[2] > 0)
-        PXG_HIP(hipMemcpyAsync(cl, lists + 2 * static_cast<uint64_t>(ngroups), cls[2] * 4, hipMemcpyDeviceToDevice, ctx->stream));
-      if (!big.empty()) {
-        std::vector<uint32_t> bg(big.size());
-        for (size_t b = 0; b < big.size(); ++b) bg[b] = big[b].g;
-        PXG_HIP(hipMemcpyAsync(cl + cls[2], bg.data(), bg.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-        PXG_HIP(hipStreamSynchronize(ctx->stream));  // bg is a host temporary
-      }
-      // The chains are latency-bound (a few waves, ~1100 dependent steps each): run them on
-      // the side stream, overlapped with the tiny/small digests and the big-group sort.
-      PXG_RETURN_IF_ERROR(ForkSide(ctx));
-      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain + 63) / 64), dim3(64), 0,
-                                   static_cast<const uint32_t*>(cl), n_chain, gstart, ws.chain_starts.as<uint32_t>(),
-                                   ws.chain_nc.as<int32_t>()));
-      chain_starts = ws.chain_starts.as<const uint32_t>();
-      chain_nc = ws.chain_nc.as<const int32_t>();
+      PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(n_big) * kBigCentroids * 4));
     }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
       double* qo = R.uda_out[u].as<double>();
-      if (cls[0] > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((cls[0] + 3) / 4), dim3(256), 0, lists, cls[0], gstart, vals, at, qo));
-      if (cls[1] > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_small", QuantSmallKernel, dim3((cls[1] + kSmallWaves - 1) / kSmallWaves), dim3(256), 0,
-                                   lists + static_cast<uint64_t>(ngroups), cls[1], gstart, vals, at, qo));
       DevBuf* src = &ws.keysA;
       DevBuf* dst = &ws.keysB;
-      if (!big.empty()) {
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(static_cast<unsigned>(bchunks.size())), dim3(256), 0,
-                                   ws.bchunks.as<const BigChunk>(), vals, at, ws.keysA.as<uint64_t>()));
+      if (n_big > 0) {
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
+                                   ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.keysA.as<uint64_t>()));
         uint32_t pass = 0;
         for (uint64_t w = kMidMax; w < big_max; w *= 2, ++pass) {
-          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeTileKernel, dim3(static_cast<unsigned>(bchunks.size())), dim3(256), 0,
-                                     ws.bchunks.as<const BigChunk>(), src->as<const uint64_t>(), dst->as<uint64_t>(), w, pass));
+          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
+                                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), src->as<const uint64_t>(),
+                                     dst->as<uint64_t>(), w, pass));
           std::swap(src, dst);
         }
       }
-      if (n_chain > 0) PXG_RETURN_IF_ERROR(JoinSide(ctx));
+      PXG_RETURN_IF_ERROR(JoinSide(ctx));
       if (cls[2] > 0)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
-                                   gstart, chain_starts, chain_nc, vals, at, qo, d_err));
-      if (!big.empty()) {
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(static_cast<unsigned>(big.size())), dim3(256), 0,
-                                   ws.big.as<const BigGroup>(), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
-                                   ws.bstarts.as<uint32_t>(),
-                                   chain_starts ? chain_starts + static_cast<uint64_t>(cls[2]) * kChainCap : nullptr,
-                                   chain_nc ? chain_nc + cls[2] : nullptr, qo, d_err));
+                                   gstart, chain_starts, chain_nc, static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
+      if (n_big > 0) {
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(n_big), dim3(256), 0,
+                                   ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(),
+                                   ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(),
+                                   chain_starts + static_cast<uint64_t>(mid_cap) * kChainCap, chain_nc + mid_cap, qo, d_err));
       }
     }
   }
