@@ -15,7 +15,7 @@
 namespace pxg {
 
 constexpr int kConsumeBlock = 256;
-constexpr int kConsumeTile = 4096;  // rows per workgroup tile (16 per thread)
+constexpr int kConsumeTile = 8192;  // rows per workgroup tile (32 per thread)
 
 struct TileRange {
   int64_t tile0;  // first tile index of this range
