@@ -15,7 +15,9 @@
 namespace pxg {
 
 constexpr int kConsumeBlock = 256;
-constexpr int kConsumeTile = 8192;  // rows per workgroup tile (32 per thread)
+constexpr int kGenericTile = 4096;   // rows per workgroup tile of the generic kernel (16 per thread)
+constexpr int kConsumeTile = 16384;  // rows per workgroup tile of the fast kernel
+constexpr int kSubRows = 8192;       // rows per phase-1 sub-batch (32 per thread in flight)
 
 struct TileRange {
   int64_t tile0;  // first tile index of this range
@@ -108,9 +110,9 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
                                                                   const TileRange* __restrict__ ranges, int nranges,
                                                                   int64_t ntiles, AggTableDev tab, StageDev stg,
                                                                   uint32_t /*nchunks: signature shared with the fast path*/) {
-  constexpr int kPer = kConsumeTile / kConsumeBlock;
+  constexpr int kPer = kGenericTile / kConsumeBlock;
   constexpr int kWaves = kConsumeBlock / 64;
-  __shared__ int32_t s_sel[kConsumeTile];
+  __shared__ int32_t s_sel[kGenericTile];
   __shared__ uint32_t s_wcnt[kWaves];
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
@@ -123,8 +125,8 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
     while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
     const TileRange rg = ranges[ri];
     const DevChunk& ch = chunks[rg.chunk];
-    const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
-    const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
+    const int64_t row0 = rg.lo + (t - rg.tile0) * kGenericTile;
+    const int64_t row1 = min(row0 + kGenericTile, rg.hi);
     // Rows of this thread: row0 + k*256 + tid (coalesced per k).
     bool pass[kPer];
 #pragma unroll
@@ -487,11 +489,12 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
                                                                       const TileRange* __restrict__ ranges, int nranges,
                                                                       int64_t ntiles, AggTableDev tab, StageDev stg,
                                                                       uint32_t nchunks) {
-  constexpr int kPer = kConsumeTile / kConsumeBlock;
+  constexpr int kPer = kSubRows / kConsumeBlock;
+  constexpr int kSubBatches = kConsumeTile / kSubRows;
   constexpr int kWaves = kConsumeBlock / 64;
   constexpr int kEntries = CacheEntries<NK>();
   __shared__ uint16_t s_sel[kConsumeTile];
-  __shared__ uint32_t s_wcnt[kWaves];
+  __shared__ uint32_t s_wcnt[2][kWaves];
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
   __shared__ CacheEntry<NK> s_cache[MODE == 1 ? kEntries : 1];
@@ -519,28 +522,42 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
     const DevChunk& ch = chunks[rg.chunk];
     const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
     const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
-    bool pass[kPer];
+    // Phase 1 in sub-batches of kSubRows rows (32 per thread in flight each), so the tile can
+    // be larger than what the per-row predicate registers allow; s_wcnt is double-buffered so
+    // each sub-batch needs one barrier.
+    uint32_t total = 0;
+#pragma unroll 1
+    for (int sb = 0; sb < kSubBatches; ++sb) {
+      const int64_t sb0 = row0 + static_cast<int64_t>(sb) * kSubRows;
+      bool pass[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int64_t r = row0 + k * kConsumeBlock + threadIdx.x;
-      pass[k] = r < row1;
-      if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
-    }
-    unsigned long long m[kPer];
-    uint32_t wtot = 0;
+      for (int k = 0; k < kPer; ++k) {
+        const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
+        pass[k] = r < row1;
+        if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
+      }
+      unsigned long long m[kPer];
+      uint32_t wtot = 0;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      m[k] = __ballot(pass[k]);
-      wtot += static_cast<uint32_t>(__popcll(m[k]));
-    }
-    if (lane == 0) s_wcnt[wid] = wtot;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
+      for (int k = 0; k < kPer; ++k) {
+        m[k] = __ballot(pass[k]);
+        wtot += static_cast<uint32_t>(__popcll(m[k]));
+      }
+      if (lane == 0) s_wcnt[sb & 1][wid] = wtot;
+      __syncthreads();
+      uint32_t wbase = total, sbtot = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      const uint32_t c = s_wcnt[w];
-      wbase += w < wid ? c : 0;
-      total += c;
+      for (int w = 0; w < kWaves; ++w) {
+        const uint32_t c = s_wcnt[sb & 1][w];
+        wbase += w < wid ? c : 0;
+        sbtot += c;
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = static_cast<uint16_t>(sb * kSubRows + k * kConsumeBlock + threadIdx.x);
+        wbase += static_cast<uint32_t>(__popcll(m[k]));
+      }
+      total += sbtot;
     }
     if (threadIdx.x == 0) {
       if (s_ins) {
@@ -548,11 +565,6 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
         s_ins = 0;
       }
       s_base = total ? atomicAdd(stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = static_cast<uint16_t>(k * kConsumeBlock + threadIdx.x);
-      wbase += static_cast<uint32_t>(__popcll(m[k]));
     }
     __syncthreads();
     const uint64_t base = s_base;
@@ -810,6 +822,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_RETURN_IF_ERROR(CheckTableTypes(*this, *t));
   PXG_RETURN_IF_ERROR(t->EnsureDeviceDescriptors());
   if (t->chunks.size() > 255) return SetError(PXG_UNIMPLEMENTED, "tables are limited to 255 chunks per agg consume");
+  const int64_t tile_rows = fast_nk > 0 ? kConsumeTile : kGenericTile;
   std::vector<TileRange> ranges;
   int64_t ntiles = 0;
   for (size_t c = 0; c < t->chunks.size(); ++c) {
@@ -824,7 +837,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     r.chunk = static_cast<int32_t>(c);
     r.pad = 0;
     ranges.push_back(r);
-    ntiles += (hi - lo + kConsumeTile - 1) / kConsumeTile;
+    ntiles += (hi - lo + tile_rows - 1) / tile_rows;
   }
   if (ranges.empty()) return PXG_OK;
   const int64_t rows = end - begin;
