@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timing-only diagnosis of agg_consume on the C2 table: runs reset + consume (no finalize)
-under each PXG_DIAG_CONSUME mode (0 production, 1 LDS group cache, 2 filter only,
+under each PXG_DIAG_CONSUME mode (0 production, 2 filter only,
 3 keys + hash without probe) in a child process per mode and prints kernel ms per launch."""
 import json
 import os
