@@ -260,3 +260,26 @@ def test_unsupported_signature_fails_loudly(ctx):
                           P.sink_op("out")])
     with pytest.raises(UnsupportedError):
         LinearQuery(plan, [5])
+
+
+def test_long_and_empty_string_keys_take_the_deferred_path(ctx):
+    """Group keys longer than the fast path's register budget (48 B) are deferred to the generic
+    kernel; empty strings and keys differing only past byte 48 must stay distinct groups."""
+    rng = np.random.default_rng(11)
+    n = 60_000
+    base = "x" * 48
+    pool = ["", "a", base, base + "1", base + "2", "y" * 100, "y" * 99 + "z", "k" * 47, "k" * 49]
+    keys = [pool[i] for i in rng.integers(0, len(pool), n)]
+    keys2 = [("p" * int(l)) for l in rng.integers(0, 60, n)]
+    vals = rng.integers(0, 1000, n)
+    plan = P.linear_plan([P.source_op("t", [5, 5, 2], ["k", "k2", "v"], [0, 1, 2]),
+                          P.filter_op(P.func("greaterThan", [P.col(2), P.const(2, 100)], [2, 2]), [0, 1, 2]),
+                          P.agg_op([0, 1], [P.agg_expr("count", [P.col(2)], [2]), P.agg_expr("sum", [P.col(2)], [2], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": [5, 5, 2], "batches": [[Column.from_values(5, keys), Column.from_values(5, keys2),
+                                                     Column.from_values(2, vals.tolist())]]}}
+    ref = _by_key(oc.execute_plan(plan, tables)["out"][0]["cols"], 2)
+    dev = _by_key(run_plan(ctx, plan, tables)[0]["cols"], 2)
+    assert len(ref) > 400 and set(ref) == set(dev)
+    for k in ref:
+        assert ref[k] == dev[k], k
