@@ -273,6 +273,35 @@ int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* dst, int64_t
 int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes);
 
 /* ---------------------------------------------------------------------------------------
+ * Equijoin (EquijoinNode, src/carnot/exec/equijoin_node.cc:53-470).  A hash table is built on
+ * the build table's key columns (exact key equality, any duplicates kept), the probe table is
+ * streamed against it, and the output is materialised as a new device table whose columns are
+ * (side, column) pairs: side 0 = probe table, side 1 = build table.  Rows of a side that has no
+ * match get the reference's default values (0 / false / "", AppendColumnDefaultValue).  The
+ * host node maps the plan's left/right parents and JoinType onto build/probe and the two
+ * emit_unmatched flags exactly as EquijoinNode::InitImpl does (equijoin_node.cc:53-116).
+ * Output order is the reference's: probe rows in table order, each followed by its matching
+ * build rows in build-table order (or one row with build defaults when unmatched probe rows
+ * are emitted); then the unmatched build rows, grouped by key (the reference emits these in
+ * hash-map order, which is unspecified).  *probe_rows (may be NULL) receives the number of
+ * rows produced by probe rows, i.e. where the unmatched build rows start: the host node cuts
+ * an output batch there (FlushChunkedRows at probe eos, equijoin_node.cc:388-390).
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t n_keys;
+  int32_t emit_unmatched_probe;  /* LEFT_OUTER with probe = left, FULL_OUTER */
+  int32_t emit_unmatched_build;  /* LEFT_OUTER with build = left, FULL_OUTER */
+  int32_t n_out;
+  const int32_t* build_keys;     /* n_keys column indices of the build table */
+  const int32_t* probe_keys;     /* n_keys column indices of the probe table */
+  const int32_t* out_side;       /* n_out: 0 probe, 1 build */
+  const int32_t* out_col;        /* n_out: column index within that side */
+} pxg_join_spec;
+
+int32_t pxg_join(pxg_table* build, pxg_table* probe, const pxg_join_spec* spec, pxg_table** out,
+                 int64_t* probe_rows);
+
+/* ---------------------------------------------------------------------------------------
  * Synthetic http_events generator (bench/test data; SURVEY.md §8d spec, counter-based
  * splitmix64 so every row is a pure function of (seed, row) and shards are independent).
  * Host-side; writes Arrow-layout host buffers allocated by the library.

@@ -937,6 +937,166 @@ struct SourceNode : ExecNode {
   }
 };
 
+// EquijoinNode (equijoin_node.cc:53-470).  The probe table is the left parent when the output
+// has a "time_" column taken from parent 0 (order_by_time, operators.cc:531-541,639-645 and
+// equijoin_node.cc:63-69), otherwise the right parent.  Build rows are buffered per key in
+// insertion order (build_buffer_), probe batches are buffered until the build side reaches
+// eos, then every probe row emits its matches in build order.  Output batches hold
+// rows_per_batch rows (default 1024); the pending batch is sent when the next one is started,
+// a partial batch is cut when the probe side ends and after the unmatched build rows
+// (FlushChunkedRows / NextOutputBatch), and the last batch carries eow/eos.
+struct EquijoinNode : ExecNode {
+  int type = 0;  // 0 INNER, 1 LEFT_OUTER, 3 FULL_OUTER
+  std::vector<int64_t> left_keys, right_keys, build_keys, probe_keys;
+  std::vector<std::pair<int64_t, int64_t>> outputs;  // (parent, column)
+  std::vector<std::string> column_names;
+  std::vector<DT> left_types, right_types;
+  bool probe_is_left = false;
+  int64_t rows_per_batch = 1024;
+  bool emit_unmatched_build = false, emit_unmatched_probe = false;
+  std::vector<std::string> key_order;                // build keys in first-insertion order
+  std::map<std::string, std::vector<std::pair<RowBatch, size_t>>> build;  // key -> rows
+  std::set<std::string> probed;
+  std::vector<RowBatch> probe_buf;
+  bool build_eos = false, probe_eos = false;
+  // current output batch under construction
+  std::vector<ColPtr> cur;
+  int64_t cur_rows = 0;
+  std::unique_ptr<RowBatch> pending;
+
+  void Init() {
+    for (size_t i = 0; i < column_names.size() && i < outputs.size(); ++i)
+      if (column_names[i] == "time_") {
+        probe_is_left = outputs[i].first == 0;
+        // JoinOperator::Init (operators.cc:593-603)
+        if (type == 3) throw Error(INVALID_ARGUMENT, "For time ordered joins, full outer join is not supported.");
+        if (type == 1 && !probe_is_left)
+          throw Error(INVALID_ARGUMENT, "For time ordered joins, left join is only supported when time_ comes from the left table.");
+        break;
+      }
+    switch (type) {
+      case 0: break;
+      case 1:
+        emit_unmatched_build = !probe_is_left;
+        emit_unmatched_probe = probe_is_left;
+        break;
+      case 3: emit_unmatched_build = emit_unmatched_probe = true; break;
+      default: throw Error(INTERNAL, "EquijoinNode: Unknown Join Type");
+    }
+    build_keys = probe_is_left ? right_keys : left_keys;
+    probe_keys = probe_is_left ? left_keys : right_keys;
+    if (rows_per_batch <= 0) rows_per_batch = 1024;
+    NewBatch();
+  }
+  static std::string Key(const RowBatch& rb, const std::vector<int64_t>& keys, size_t r) {
+    std::string k;
+    for (int64_t c : keys) {
+      const Col& col = *rb.cols.at(c);
+      switch (col.type) {
+        case STRING: {
+          const std::string& s = col.s[r];
+          uint64_t n = s.size();
+          k.append(reinterpret_cast<const char*>(&n), 8);
+          k += s;
+          break;
+        }
+        case UINT128: k.append(reinterpret_cast<const char*>(&col.u[r]), 16); break;
+        case FLOAT64: k.append(reinterpret_cast<const char*>(&col.f[r]), 8); break;
+        case BOOLEAN: k.push_back(static_cast<char>(col.b[r])); break;
+        default: k.append(reinterpret_cast<const char*>(&col.i[r]), 8); break;
+      }
+    }
+    return k;
+  }
+  void NewBatch() {
+    cur.clear();
+    for (auto t : out_types) cur.push_back(std::make_shared<Col>(t));
+    cur_rows = 0;
+  }
+  static void AppendDefault(Col* c) {
+    switch (c->type) {
+      case BOOLEAN: c->b.push_back(0); break;
+      case INT64:
+      case TIME64NS: c->i.push_back(0); break;
+      case FLOAT64: c->f.push_back(0.0); break;
+      case STRING: c->s.emplace_back(); break;
+      case UINT128: c->u.push_back(U128{}); break;
+      default: break;
+    }
+  }
+  // NextOutputBatch: the pending batch goes out, the finished one becomes pending.
+  void CutBatch() {
+    if (cur_rows == 0) return;
+    auto rb = std::make_unique<RowBatch>();
+    rb->cols = cur;
+    rb->num_rows = cur_rows;
+    if (pending) Send(*pending);
+    pending = std::move(rb);
+    NewBatch();
+  }
+  void Emit(const RowBatch* probe_rb, size_t pr, const RowBatch* build_rb, size_t br) {
+    for (size_t o = 0; o < outputs.size(); ++o) {
+      const bool from_build = (outputs[o].first == 0) != probe_is_left;
+      const RowBatch* src = from_build ? build_rb : probe_rb;
+      const size_t row = from_build ? br : pr;
+      if (src) cur[o]->append_from(*src->cols.at(outputs[o].second), row);
+      else AppendDefault(cur[o].get());
+    }
+    if (++cur_rows == rows_per_batch) CutBatch();
+  }
+  void DoProbe(const RowBatch& rb) {
+    if (rb.eos) probe_eos = true;
+    for (size_t r = 0; r < static_cast<size_t>(rb.num_rows); ++r) {
+      auto it = build.find(Key(rb, probe_keys, r));
+      if (it == build.end()) {
+        if (emit_unmatched_probe) Emit(&rb, r, nullptr, 0);
+        continue;
+      }
+      probed.insert(it->first);
+      for (auto& m : it->second) Emit(&rb, r, &m.first, m.second);
+    }
+    if (probe_eos) CutBatch();
+  }
+  void ConsumeNext(const RowBatch& rb, size_t parent_index) override {
+    if ((parent_index == 0) == probe_is_left) {
+      if (!build_eos) probe_buf.push_back(rb);
+      else DoProbe(rb);
+    } else {
+      if (rb.eos) build_eos = true;
+      for (size_t r = 0; r < static_cast<size_t>(rb.num_rows); ++r) {
+        std::string k = Key(rb, build_keys, r);
+        auto it = build.find(k);
+        if (it == build.end()) {
+          key_order.push_back(k);
+          it = build.emplace(k, std::vector<std::pair<RowBatch, size_t>>()).first;
+        }
+        it->second.emplace_back(rb, r);
+      }
+      if (build_eos) {
+        for (auto& b : probe_buf) DoProbe(b);
+        probe_buf.clear();
+      }
+    }
+    if (build_eos && probe_eos) {
+      if (emit_unmatched_build) {
+        for (auto& k : key_order) {
+          if (probed.count(k)) continue;
+          for (auto& m : build[k]) Emit(nullptr, 0, &m.first, m.second);
+        }
+        CutBatch();
+      }
+      if (!pending) {
+        pending = std::make_unique<RowBatch>();
+        pending->num_rows = 0;
+        for (auto t : out_types) pending->cols.push_back(std::make_shared<Col>(t));
+      }
+      pending->eow = pending->eos = true;
+      Send(*pending);
+      pending.reset();
+    }
+  }
+};
+
 /*********************************************************************************************
  * Plan driver (exec_graph.cc:52-331).
  *********************************************************************************************/
@@ -1035,6 +1195,31 @@ struct Graph {
         n->Init();
         for (auto g : n->groups) n->out_types.push_back(in.at(g));
         for (auto* d : n->defs) n->out_types.push_back(d->out);
+        node = std::move(n);
+      } else if (op.has("joinOp")) {
+        const Json& j = op["joinOp"];
+        auto n = std::make_unique<EquijoinNode>();
+        if (parents[id].size() != 2) throw Error(INVALID_ARGUMENT, "Join operator expects a two input relations");
+        n->left_types = nodes.at(parents[id][0])->out_types;
+        n->right_types = nodes.at(parents[id][1])->out_types;
+        const std::string jt = j["type"].kind == Json::kString ? j["type"].as_str() : std::string();
+        n->type = jt.empty() ? static_cast<int>(j["type"].as_i64()) : (jt == "INNER" ? 0 : jt == "LEFT_OUTER" ? 1 : jt == "FULL_OUTER" ? 3 : -1);
+        for (size_t c = 0; c < j["equalityConditions"].size(); ++c) {
+          const Json& e = j["equalityConditions"].at(c);
+          n->left_keys.push_back(e["leftColumnIndex"].as_i64());
+          n->right_keys.push_back(e["rightColumnIndex"].as_i64());
+          if (n->left_types.at(n->left_keys.back()) != n->right_types.at(n->right_keys.back()))
+            throw Error(INVALID_ARGUMENT, "join key types differ");
+        }
+        for (size_t c = 0; c < j["outputColumns"].size(); ++c) {
+          const Json& o = j["outputColumns"].at(c);
+          const int64_t pi = o["parentIndex"].as_i64(), ci = o["columnIndex"].as_i64();
+          n->outputs.push_back({pi, ci});
+          n->out_types.push_back((pi == 0 ? n->left_types : n->right_types).at(ci));
+        }
+        for (size_t c = 0; c < j["columnNames"].size(); ++c) n->column_names.push_back(j["columnNames"].at(c).as_str());
+        n->rows_per_batch = j["rowsPerBatch"].as_i64();
+        n->Init();
         node = std::move(n);
       } else if (op.has("memSinkOp") || op.has("grpcSinkOp")) {
         auto n = std::make_unique<SinkNode>();

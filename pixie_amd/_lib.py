@@ -63,6 +63,12 @@ class AggSpec(C.Structure):
                 ("expected_groups", C.c_int64), ("windowed", C.c_int32), ("reserved", C.c_int32)]
 
 
+class JoinSpec(C.Structure):
+    _fields_ = [("n_keys", C.c_int32), ("emit_unmatched_probe", C.c_int32), ("emit_unmatched_build", C.c_int32),
+                ("n_out", C.c_int32), ("build_keys", C.POINTER(C.c_int32)), ("probe_keys", C.POINTER(C.c_int32)),
+                ("out_side", C.POINTER(C.c_int32)), ("out_col", C.POINTER(C.c_int32))]
+
+
 # Every symbol include/pxg.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pxg_abi_version", "pxg_last_error", "pxg_device_count", "pxg_ctx_create", "pxg_ctx_destroy",
@@ -72,7 +78,7 @@ EXPORTED = [
     "pxg_table_device_bytes", "pxg_table_fetch", "pxg_filter", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_result_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_export_partial", "pxg_agg_import_partial",
-    "pxg_datagen_http_events",
+    "pxg_join", "pxg_datagen_http_events",
 ]
 
 _lib = None
@@ -132,6 +138,7 @@ def load() -> C.CDLL:
         "pxg_agg_rows_selected": (i32, [vp, p(i64)]),
         "pxg_agg_export_partial": (i32, [vp, i32, vp, i64, p(i64), p(i64)]),
         "pxg_agg_import_partial": (i32, [vp, vp, i64]),
+        "pxg_join": (i32, [vp, vp, p(JoinSpec), p(vp), p(i64)]),
         "pxg_datagen_http_events": (i32, [C.c_uint64, i64, i64, i64, i32, p(ColumnOut)]),
     }
     for name, (res, args) in sig.items():

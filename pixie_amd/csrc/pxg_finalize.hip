@@ -7,6 +7,7 @@
 #include "pxg_agg_host.h"
 #include "pxg_keys.h"
 #include "pxg_scan.h"
+#include "pxg_sort.h"
 #include "pxg_tdigest.h"
 
 namespace pxg {
@@ -1005,6 +1006,48 @@ __global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
     *reinterpret_cast<uint32_t*>(meta + 16) = 0;
     for (int c = 0; c < kNumClasses; ++c) reinterpret_cast<uint32_t*>(meta + 32)[c] = 0;
   }
+}
+
+int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* vals,
+                       uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals) {
+  if (n == 0 || n >= (uint64_t(1) << 32)) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %llu records", static_cast<unsigned long long>(n));
+  const int nbits = std::max(1, Log2Ceil(static_cast<uint64_t>(G) + 1));
+  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
+  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
+  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
+  for (int b = 0; b < 2; ++b) {
+    PXG_RETURN_IF_ERROR(ws.key[b].Ensure(n * 4 + 16));
+    PXG_RETURN_IF_ERROR(ws.val[b].Ensure(n * 8 + 16));
+  }
+  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
+  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(nh + 1)) + 64));
+  const uint32_t* kin = keys;
+  ConstValPtrs vin;
+  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = nullptr;
+  vin.p[0] = vals;
+  int cur = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * kRadixBits;
+    const uint32_t* rk = p == 0 ? rank : nullptr;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, n, rk, cap, G, shift,
+                               ws.hist.as<uint32_t>(), nblocks));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, ws.scan.p));
+    ValPtrs vout;
+    for (int v = 0; v < kMaxVals; ++v) vout.p[v] = nullptr;
+    vout.p[0] = ws.val[cur].as<uint64_t>();
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, ws.key[cur].as<uint32_t>(),
+                               vin, vout, 1, n, rk, cap, G, shift, ws.hist.as<const uint32_t>(), nblocks));
+    kin = ws.key[cur].as<const uint32_t>();
+    vin.p[0] = ws.val[cur].as<const uint64_t>();
+    cur ^= 1;
+  }
+  *skeys = kin;
+  *svals = vin.p[0];
+  return PXG_OK;
+}
+
+int32_t GroupStarts(Ctx* ctx, const uint32_t* skeys, uint64_t n, uint32_t G, uint32_t* gstart) {
+  return Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0, skeys, n, G, gstart);
 }
 
 int32_t AggFinalizeImpl(Agg* a) {

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -199,6 +199,22 @@ class Table:
         arr = (_lib.Program * max(1, len(progs)))(*[p.c for p in progs])
         check(self.lib.pxg_map(self.h, len(progs), arr, begin, end, C.byref(h)))
         return Table(self.ctx, [p.result_type for p in progs], handle=h)
+
+    def join(self, probe: "Table", build_keys: Sequence[int], probe_keys: Sequence[int],
+             outputs: Sequence[Tuple[int, int]], emit_unmatched_probe: bool = False,
+             emit_unmatched_build: bool = False) -> Tuple["Table", int]:
+        """pxg_join with this table as the build side.  outputs: (side, col), side 0 = probe,
+        1 = build.  Returns (output table, rows produced by probe rows)."""
+        n = len(build_keys)
+        i32a = lambda xs: (C.c_int32 * max(1, len(xs)))(*xs)  # noqa: E731
+        bk, pk = i32a(build_keys), i32a(probe_keys)
+        side, col = i32a([o[0] for o in outputs]), i32a([o[1] for o in outputs])
+        spec = _lib.JoinSpec(n, int(emit_unmatched_probe), int(emit_unmatched_build), len(outputs), bk, pk, side, col)
+        h = C.c_void_p()
+        nprobe = C.c_int64()
+        check(self.lib.pxg_join(self.h, probe.h, C.byref(spec), C.byref(h), C.byref(nprobe)))
+        types = [probe.types[c] if s == 0 else self.types[c] for s, c in outputs]
+        return Table(self.ctx, types, handle=h), nprobe.value
 
     def close(self) -> None:
         if self.h:

@@ -832,6 +832,157 @@ class PostAggMapNode : public ExecNode {
 };
 
 // MemorySinkNode / GRPCSinkNode result table: collects the batches.
+// A zero-row batch of the given types (RowBatch::WithZeroRows).
+static RowBatch ZeroRowBatch(const RowDescriptor& types, bool eow, bool eos) {
+  static const int32_t zero_off[2] = {0, 0};
+  static const uint8_t pad[16] = {0};
+  RowBatch rb;
+  for (int32_t t : types) {
+    HostColumn hc;
+    hc.type = t;
+    hc.offsets = zero_off;
+    hc.data = pad;
+    hc.values = pad;
+    rb.cols.push_back(hc);
+  }
+  rb.eow = eow;
+  rb.eos = eos;
+  return rb;
+}
+
+// GpuEquijoinNode (EquijoinNode, equijoin_node.cc:53-470).  InitImpl maps left/right onto
+// build/probe exactly as the reference does: the probe table is the left parent when the output
+// has a "time_" column taken from parent 0 (order_by_time, operators.cc:531-541,639-645;
+// equijoin_node.cc:63-69), otherwise the right parent; the JoinType then decides which side's
+// unmatched rows are emitted (equijoin_node.cc:71-88).  Both inputs are staged into device
+// tables; once both sides reached eos the join runs once on the device (pxg_join) and its
+// output goes out in rows_per_batch batches: the probe-produced rows, with a partial batch cut at
+// probe eos (FlushChunkedRows, equijoin_node.cc:388-390), then the unmatched build rows
+// (EmitUnmatchedBuildRows, :398-411).  The last batch carries eow/eos; a zero-row eow/eos batch
+// is sent when there is no output at all (equijoin_node.cc:447-459).
+class GpuEquijoinNode : public ExecNode {
+ public:
+  std::string DebugString() const override {
+    std::ostringstream os;
+    os << "GpuEquijoinNode(type=" << type_ << ", probe=" << (probe_is_left_ ? "left" : "right") << ", rows_per_batch=" << rows_per_batch_
+       << ")";
+    return os.str();
+  }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    if (inputs_.size() != 2) return Err(PXG_INVALID_ARGUMENT, "Join operator expects a two input relations, got %zu", inputs_.size());
+    const planpb::JoinOperator& j = op.join;
+    type_ = j.type;
+    rows_per_batch_ = j.rows_per_batch == 0 ? 1024 : static_cast<int64_t>(j.rows_per_batch);
+    for (size_t i = 0; i < j.column_names.size() && i < j.output_columns.size(); ++i) {
+      if (j.column_names[i] != "time_") continue;
+      probe_is_left_ = j.output_columns[i].first == 0;
+      // JoinOperator::Init (operators.cc:593-603).
+      if (type_ == 3) return Err(PXG_INVALID_ARGUMENT, "For time ordered joins, full outer join is not supported.");
+      if (type_ == 1 && !probe_is_left_)
+        return Err(PXG_INVALID_ARGUMENT, "For time ordered joins, left join is only supported when time_ comes from the left table.");
+      break;
+    }
+    switch (type_) {
+      case 0: break;
+      case 1:
+        emit_build_ = !probe_is_left_;
+        emit_probe_ = probe_is_left_;
+        break;
+      case 3: emit_build_ = emit_probe_ = true; break;
+      default: return Err(PXG_INTERNAL, "EquijoinNode: Unknown Join Type %d", type_);
+    }
+    const size_t probe_parent = probe_is_left_ ? 0 : 1;
+    for (auto& c : j.equality_conditions) {
+      if (c.first >= inputs_[0].size() || c.second >= inputs_[1].size()) return Err(PXG_INVALID_ARGUMENT, "join key column out of range");
+      if (inputs_[0][c.first] != inputs_[1][c.second]) return Err(PXG_INVALID_ARGUMENT, "join key types differ");
+      const int32_t l = static_cast<int32_t>(c.first), r = static_cast<int32_t>(c.second);
+      build_keys_.push_back(probe_is_left_ ? r : l);
+      probe_keys_.push_back(probe_is_left_ ? l : r);
+    }
+    if (build_keys_.empty()) return Err(PXG_INVALID_ARGUMENT, "join without equality conditions");
+    for (auto& o : j.output_columns) {
+      if (o.first > 1 || o.second >= inputs_[o.first].size()) return Err(PXG_INVALID_ARGUMENT, "join output column out of range");
+      out_side_.push_back(o.first == probe_parent ? 0 : 1);
+      out_col_.push_back(static_cast<int32_t>(o.second));
+    }
+    if (out_side_.empty()) return Err(PXG_UNIMPLEMENTED, "join with no output columns");
+    return Status::OK();
+  }
+  Status OpenImpl(ExecState* s) override {
+    if (!s->ctx) return Status::OK();
+    for (int side = 0; side < 2; ++side)
+      PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(inputs_[side].size()), inputs_[side].data(), &staged_[side]));
+    return Status::OK();
+  }
+  Status CloseImpl(ExecState*) override {
+    for (auto& t : staged_) {
+      if (t) pxg_table_destroy(t);
+      t = nullptr;
+    }
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t parent_index) override {
+    if (parent_index > 1) return Err(PXG_INTERNAL, "join parent index %zu", parent_index);
+    if (eos_[parent_index]) return Err(PXG_INTERNAL, "join input %zu after eos", parent_index);
+    if (rb.num_rows > 0) {
+      std::vector<pxg_column_view> v;
+      for (auto& c : rb.cols) v.push_back(c.View());
+      PXG_CALL(pxg_table_append(staged_[parent_index], v.data(), rb.num_rows));
+    }
+    if (rb.eos) eos_[parent_index] = true;
+    if (!(eos_[0] && eos_[1])) return Status::OK();
+    return Run(s);
+  }
+
+ private:
+  Status Run(ExecState* s) {
+    pxg_table* probe = staged_[probe_is_left_ ? 0 : 1];
+    pxg_table* build = staged_[probe_is_left_ ? 1 : 0];
+    PXG_CALL(pxg_table_flush(probe));
+    PXG_CALL(pxg_table_flush(build));
+    pxg_join_spec sp{};
+    sp.n_keys = static_cast<int32_t>(build_keys_.size());
+    sp.emit_unmatched_probe = emit_probe_;
+    sp.emit_unmatched_build = emit_build_;
+    sp.n_out = static_cast<int32_t>(out_side_.size());
+    sp.build_keys = build_keys_.data();
+    sp.probe_keys = probe_keys_.data();
+    sp.out_side = out_side_.data();
+    sp.out_col = out_col_.data();
+    pxg_table* out = nullptr;
+    int64_t nprobe = 0;
+    PXG_CALL(pxg_join(build, probe, &sp, &out, &nprobe));
+    std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(out, pxg_table_destroy);
+    const int64_t n = pxg_table_num_rows(out);
+    std::vector<std::pair<int64_t, int64_t>> ranges;
+    for (int64_t b = 0; b < nprobe; b += rows_per_batch_) ranges.push_back({b, std::min(nprobe, b + rows_per_batch_)});
+    for (int64_t b = nprobe; b < n; b += rows_per_batch_) ranges.push_back({b, std::min(n, b + rows_per_batch_)});
+    if (ranges.empty()) return SendRowBatchToChildren(s, ZeroRowBatch(output_, true, true));
+    for (size_t r = 0; r < ranges.size(); ++r) {
+      RowBatch ob;
+      ob.num_rows = ranges[r].second - ranges[r].first;
+      for (size_t c = 0; c < out_side_.size(); ++c) {
+        pxg_column_out o{};
+        PXG_CALL(pxg_table_fetch(out, static_cast<int32_t>(c), ranges[r].first, ranges[r].second, &o));
+        ob.cols.push_back(FromOut(o));
+      }
+      ob.eow = ob.eos = r + 1 == ranges.size();
+      PXC_RETURN_IF_ERROR(SendRowBatchToChildren(s, ob));
+    }
+    return Status::OK();
+  }
+
+  int32_t type_ = 0;
+  int64_t rows_per_batch_ = 1024;
+  bool probe_is_left_ = false;
+  int32_t emit_build_ = 0, emit_probe_ = 0;
+  std::vector<int32_t> build_keys_, probe_keys_, out_side_, out_col_;
+  pxg_table* staged_[2] = {nullptr, nullptr};
+  bool eos_[2] = {false, false};
+};
+
 class SinkNode : public ExecNode {
  public:
   explicit SinkNode(std::string name) : name(std::move(name)) {}
@@ -856,128 +1007,83 @@ class SinkNode : public ExecNode {
 class ExecutionGraph {
  public:
   Status Init(const planpb::PlanFragment& pf, int32_t ntables, const pxc_table* tables) {
-    // Topological order from the DAG (plan_fragment.cc:108-118); this engine runs linear chains.
     std::map<uint64_t, const planpb::Operator*> ops;
     for (auto& n : pf.nodes) ops[n.id] = &n.op;
-    std::vector<uint64_t> order;
+    // Parents / children from the DAG (plan_fragment.cc:108-118); without a DAG the nodes form
+    // a chain in listed order.
+    std::map<uint64_t, std::vector<uint64_t>> parents, children;
+    std::vector<uint64_t> ids;
     if (!pf.dag.empty()) {
       for (auto& d : pf.dag) {
-        if (d.sorted_parents.size() > 1 || d.sorted_children.size() > 1)
-          return Err(PXG_UNIMPLEMENTED, "only linear plan fragments run on the device engine");
-        order.push_back(d.id);
+        ids.push_back(d.id);
+        parents[d.id] = d.sorted_parents;
+        children[d.id] = d.sorted_children;
       }
     } else {
-      for (auto& n : pf.nodes) order.push_back(n.id);
-    }
-    std::vector<const planpb::Operator*> chain;
-    for (uint64_t id : order) {
-      auto it = ops.find(id);
-      if (it == ops.end()) return Err(PXG_NOT_FOUND, "plan node %llu missing", (unsigned long long)id);
-      chain.push_back(it->second);
-    }
-    if (chain.empty() || chain[0]->which != 2) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource");
-    const planpb::MemorySourceOperator& ms = chain[0]->mem_source;
-    const pxc_table* tab = nullptr;
-    for (int32_t t = 0; t < ntables; ++t)
-      if (ms.name == tables[t].name) tab = &tables[t];
-    if (!tab) return Err(PXG_NOT_FOUND, "table %s not found", ms.name.c_str());
-    auto* src = new MemorySourceNode(tab);
-    pool_.emplace_back(src);
-    RowDescriptor src_types;
-    if (ms.column_idxs.empty())
-      for (int32_t c = 0; c < tab->ncols; ++c) src_types.push_back(tab->col_types[c]);
-    else
-      for (int64_t c : ms.column_idxs) {
-        if (c < 0 || c >= tab->ncols) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
-        src_types.push_back(tab->col_types[c]);
-      }
-    PXC_RETURN_IF_ERROR(src->Init(*chain[0], src_types, {}));
-    source_ = src;
-    ExecNode* parent = src;
-    RowDescriptor cur = src_types;
-
-    // Fusable prefix: Filter / Map operators up to a blocking Agg.
-    size_t i = 1;
-    size_t agg_at = 0;
-    for (size_t j = 1; j < chain.size(); ++j) {
-      const int w = chain[j]->which;
-      if (w == 4) {
-        if (!chain[j]->agg.windowed) agg_at = j;
-        break;
-      }
-      if (w != 3 && w != 6) break;
-    }
-    if (agg_at > 0) {
-      // Substitute the chain into programs over the source columns.
-      std::vector<Program> env = ColumnEnv(src_types);
-      bool has_filter = false;
-      Program filter;
-      for (size_t j = 1; j < agg_at; ++j) {
-        const planpb::Operator& op = *chain[j];
-        ExprCompiler comp(env);
-        if (op.which == 6) {
-          Program p;
-          PXC_RETURN_IF_ERROR(comp.Compile(op.filter.expression, &p));
-          if (p.result_type != B) return Err(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
-          if (!has_filter) {
-            filter = p;
-          } else {
-            AppendProgram(p, &filter);
-            filter.insns.push_back(Insn(PXG_OP_AND, B));
-          }
-          has_filter = true;
-          std::vector<Program> ne;
-          for (auto& c : op.filter.columns) {
-            if (c.index >= env.size()) return Err(PXG_INVALID_ARGUMENT, "filter column out of range");
-            ne.push_back(env[c.index]);
-          }
-          if (!op.filter.columns.empty()) env = ne;
-        } else {
-          std::vector<Program> ne(op.map.expressions.size());
-          for (size_t e = 0; e < ne.size(); ++e) PXC_RETURN_IF_ERROR(comp.Compile(op.map.expressions[e], &ne[e]));
-          env = ne;
+      for (size_t i = 0; i < pf.nodes.size(); ++i) {
+        ids.push_back(pf.nodes[i].id);
+        if (i) {
+          parents[pf.nodes[i].id] = {pf.nodes[i - 1].id};
+          children[pf.nodes[i - 1].id] = {pf.nodes[i].id};
         }
       }
-      auto* agg = new GpuAggNode();
-      pool_.emplace_back(agg);
-      agg->env = env;
-      agg->has_filter = has_filter;
-      agg->filter = filter;
-      agg->fused_ = agg_at > 1;
-      agg->source_types = src_types;
-      RowDescriptor env_types;
-      for (auto& p : env) env_types.push_back(p.result_type);
-      PXC_RETURN_IF_ERROR(agg->Init(*chain[agg_at], AggOutputTypes(*chain[agg_at], env, &agg_out_ok_), {env_types}));
-      PXC_RETURN_IF_ERROR(agg_out_ok_);
-      parent->AddChild(agg, 0);
-      parent = agg;
-      cur = agg->output_descriptor();
-      last_agg_ = agg;
-      i = agg_at + 1;
-      lowered_.push_back(agg);
     }
-    for (; i < chain.size(); ++i) {
-      const planpb::Operator& op = *chain[i];
+    for (uint64_t id : ids)
+      if (!ops.count(id)) return Err(PXG_NOT_FOUND, "plan node %llu missing", (unsigned long long)id);
+    // Topological order (Kahn, ties in listed order).
+    std::vector<uint64_t> order;
+    {
+      std::map<uint64_t, size_t> indeg;
+      for (uint64_t id : ids) indeg[id] = parents[id].size();
+      std::vector<uint64_t> ready;
+      for (uint64_t id : ids)
+        if (indeg[id] == 0) ready.push_back(id);
+      for (size_t k = 0; k < ready.size(); ++k) {
+        order.push_back(ready[k]);
+        for (uint64_t c : children[ready[k]])
+          if (indeg.count(c) && --indeg[c] == 0) ready.push_back(c);
+      }
+      if (order.size() != ids.size()) return Err(PXG_INVALID_ARGUMENT, "plan DAG has a cycle");
+    }
+    std::map<uint64_t, ExecNode*> built;
+    std::set<uint64_t> fused_away;
+    for (uint64_t id : order) {
+      if (fused_away.count(id)) continue;
+      const planpb::Operator& op = *ops[id];
+      if (op.which == 2) {
+        PXC_RETURN_IF_ERROR(BuildSource(id, op, ntables, tables, ops, parents, children, &built, &fused_away));
+        continue;
+      }
+      const std::vector<uint64_t>& ps = parents[id];
+      if (ps.empty()) return Err(PXG_UNIMPLEMENTED, "operator (oneof field %d) without inputs has no device node", op.which);
+      std::vector<RowDescriptor> ins;
+      for (uint64_t p : ps) {
+        if (!built.count(p)) return Err(PXG_INTERNAL, "parent %llu not built", (unsigned long long)p);
+        ins.push_back(built[p]->output_descriptor());
+      }
+      const RowDescriptor& cur = ins[0];
       ExecNode* node = nullptr;
       RowDescriptor out;
       switch (op.which) {
         case 6: {
-          auto* f = new GpuFilterNode();
-          node = f;
-          for (auto& c : op.filter.columns) out.push_back(cur.at(c.index));
+          node = new GpuFilterNode();
+          for (auto& c : op.filter.columns) {
+            if (c.index >= cur.size()) return Err(PXG_INVALID_ARGUMENT, "filter column out of range");
+            out.push_back(cur[c.index]);
+          }
           if (op.filter.columns.empty()) out = cur;
           break;
         }
         case 3: {
-          if (last_agg_ && parent == last_agg_) {
-            node = new PostAggMapNode(last_agg_);
+          auto* agg = dynamic_cast<GpuAggNode*>(built[ps[0]]);
+          if (agg) {
+            node = new PostAggMapNode(agg);
             for (auto& e : op.map.expressions) {
               if (e.kind == planpb::ScalarExpression::kColumn && e.column.index < cur.size()) out.push_back(cur[e.column.index]);
               else out.push_back(F);
             }
           } else {
-            auto* m = new GpuMapNode();
-            node = m;
+            node = new GpuMapNode();
             ExprCompiler comp(ColumnEnv(cur));
             for (auto& e : op.map.expressions) {
               Program p;
@@ -988,31 +1094,38 @@ class ExecutionGraph {
           break;
         }
         case 4: {
-          auto* a = new GpuAggNode();
-          node = a;
+          node = new GpuAggNode();
           Status st;
           out = AggOutputTypes(op, ColumnEnv(cur), &st);
           PXC_RETURN_IF_ERROR(st);
-          last_agg_ = a;
+          break;
+        }
+        case 11: {
+          if (ins.size() != 2) return Err(PXG_INVALID_ARGUMENT, "Join operator expects a two input relations, got %zu", ins.size());
+          node = new GpuEquijoinNode();
+          for (auto& o : op.join.output_columns) {
+            if (o.first > 1 || o.second >= ins[o.first].size()) return Err(PXG_INVALID_ARGUMENT, "join output column out of range");
+            out.push_back(ins[o.first][o.second]);
+          }
           break;
         }
         case 5:
         case 1000: {
-          auto* s = new SinkNode(op.which == 5 ? op.mem_sink.name : op.grpc_sink_table);
-          node = s;
-          sinks_.push_back(s);
+          auto* sk = new SinkNode(op.which == 5 ? op.mem_sink.name : op.grpc_sink_table);
+          node = sk;
+          sinks_.push_back(sk);
           out = cur;
           break;
         }
         default: return Err(PXG_UNIMPLEMENTED, "operator (oneof field %d) has no device node", op.which);
       }
       pool_.emplace_back(node);
-      PXC_RETURN_IF_ERROR(node->Init(op, out, {cur}));
-      parent->AddChild(node, 0);
+      PXC_RETURN_IF_ERROR(node->Init(op, out, ins));
+      for (size_t k = 0; k < ps.size(); ++k) built[ps[k]]->AddChild(node, k);
+      built[id] = node;
       lowered_.push_back(node);
-      parent = node;
-      cur = out;
     }
+    if (sources_.empty()) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource");
     if (sinks_.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no sink");
     return Status::OK();
   }
@@ -1021,8 +1134,16 @@ class ExecutionGraph {
   Status Execute(ExecState* s) {
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Prepare(s));
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Open(s));
+    // Round-robin over the sources until all are exhausted (exec_graph.cc:177-289).
     Status st;
-    while (st.ok() && source_->HasBatchesRemaining()) st = source_->GenerateNext(s);
+    for (bool any = true; st.ok() && any;) {
+      any = false;
+      for (auto* src : sources_) {
+        if (!st.ok() || !src->HasBatchesRemaining()) continue;
+        any = true;
+        st = src->GenerateNext(s);
+      }
+    }
     for (auto& n : pool_) {
       Status c = n->Close(s);
       if (st.ok()) st = c;
@@ -1032,7 +1153,7 @@ class ExecutionGraph {
 
   std::string Explain() const {
     std::ostringstream os;
-    os << source_->DebugString() << "\n";
+    for (auto* src : sources_) os << src->DebugString() << "\n";
     for (auto* n : lowered_) {
       os << "  -> " << n->DebugString() << " out=[";
       for (size_t i = 0; i < n->output_descriptor().size(); ++i) os << (i ? "," : "") << TypeName(n->output_descriptor()[i]);
@@ -1090,11 +1211,105 @@ class ExecutionGraph {
     return out;
   }
 
+  // A MemorySource, and the fused GpuAggNode when a chain of single-consumer Filter / Map
+  // nodes below it ends in a blocking Agg (the chain's intermediate batches are unobservable:
+  // a blocking agg emits only at eos, agg_node.cc:169-171).
+  Status BuildSource(uint64_t id, const planpb::Operator& op, int32_t ntables, const pxc_table* tables,
+                     std::map<uint64_t, const planpb::Operator*>& ops, std::map<uint64_t, std::vector<uint64_t>>& parents,
+                     std::map<uint64_t, std::vector<uint64_t>>& children, std::map<uint64_t, ExecNode*>* built,
+                     std::set<uint64_t>* fused_away) {
+    const planpb::MemorySourceOperator& ms = op.mem_source;
+    const pxc_table* tab = nullptr;
+    for (int32_t t = 0; t < ntables; ++t)
+      if (ms.name == tables[t].name) tab = &tables[t];
+    if (!tab) return Err(PXG_NOT_FOUND, "table %s not found", ms.name.c_str());
+    auto* src = new MemorySourceNode(tab);
+    pool_.emplace_back(src);
+    RowDescriptor src_types;
+    if (ms.column_idxs.empty())
+      for (int32_t c = 0; c < tab->ncols; ++c) src_types.push_back(tab->col_types[c]);
+    else
+      for (int64_t c : ms.column_idxs) {
+        if (c < 0 || c >= tab->ncols) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
+        src_types.push_back(tab->col_types[c]);
+      }
+    PXC_RETURN_IF_ERROR(src->Init(op, src_types, {}));
+    sources_.push_back(src);
+    (*built)[id] = src;
+
+    std::vector<uint64_t> chain;
+    uint64_t agg_id = 0;
+    bool found = false;
+    for (uint64_t cur = id; children[cur].size() == 1;) {
+      const uint64_t c = children[cur][0];
+      if (parents[c].size() != 1) break;
+      const planpb::Operator& cop = *ops[c];
+      if (cop.which == 4) {
+        if (!cop.agg.windowed) {
+          agg_id = c;
+          found = true;
+        }
+        break;
+      }
+      if (cop.which != 3 && cop.which != 6) break;
+      chain.push_back(c);
+      cur = c;
+    }
+    if (!found) return Status::OK();
+    // Substitute the chain into programs over the source columns.
+    std::vector<Program> env = ColumnEnv(src_types);
+    bool has_filter = false;
+    Program filter;
+    for (uint64_t cid : chain) {
+      const planpb::Operator& cop = *ops[cid];
+      ExprCompiler comp(env);
+      if (cop.which == 6) {
+        Program p;
+        PXC_RETURN_IF_ERROR(comp.Compile(cop.filter.expression, &p));
+        if (p.result_type != B) return Err(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
+        if (!has_filter) {
+          filter = p;
+        } else {
+          AppendProgram(p, &filter);
+          filter.insns.push_back(Insn(PXG_OP_AND, B));
+        }
+        has_filter = true;
+        std::vector<Program> ne;
+        for (auto& c : cop.filter.columns) {
+          if (c.index >= env.size()) return Err(PXG_INVALID_ARGUMENT, "filter column out of range");
+          ne.push_back(env[c.index]);
+        }
+        if (!cop.filter.columns.empty()) env = ne;
+      } else {
+        std::vector<Program> ne(cop.map.expressions.size());
+        for (size_t e = 0; e < ne.size(); ++e) PXC_RETURN_IF_ERROR(comp.Compile(cop.map.expressions[e], &ne[e]));
+        env = ne;
+      }
+    }
+    auto* agg = new GpuAggNode();
+    pool_.emplace_back(agg);
+    agg->env = env;
+    agg->has_filter = has_filter;
+    agg->filter = filter;
+    agg->fused_ = !chain.empty();
+    agg->source_types = src_types;
+    RowDescriptor env_types;
+    for (auto& p : env) env_types.push_back(p.result_type);
+    Status out_ok;
+    const RowDescriptor out = AggOutputTypes(*ops[agg_id], env, &out_ok);
+    PXC_RETURN_IF_ERROR(out_ok);
+    PXC_RETURN_IF_ERROR(agg->Init(*ops[agg_id], out, {env_types}));
+    src->AddChild(agg, 0);
+    (*built)[agg_id] = agg;
+    for (uint64_t cid : chain) fused_away->insert(cid);
+    fused_away->insert(agg_id);
+    lowered_.push_back(agg);
+    return Status::OK();
+  }
+
   std::vector<std::unique_ptr<ExecNode>> pool_;
   std::vector<ExecNode*> lowered_;
-  MemorySourceNode* source_ = nullptr;
-  GpuAggNode* last_agg_ = nullptr;
-  Status agg_out_ok_;
+  std::vector<MemorySourceNode*> sources_;
 };
 
 // PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).

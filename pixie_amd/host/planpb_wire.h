@@ -10,6 +10,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace pxc {
@@ -173,6 +174,14 @@ struct FilterOperator {  // plan.proto:261-266
   std::vector<Column> columns;
 };
 
+struct JoinOperator {  // plan.proto:301-336
+  int32_t type = 0;  // INNER 0, LEFT_OUTER 1, FULL_OUTER 3
+  std::vector<std::pair<uint64_t, uint64_t>> equality_conditions;  // (left, right) column index
+  std::vector<std::pair<uint64_t, uint64_t>> output_columns;       // (parent index, column index)
+  std::vector<std::string> column_names;
+  uint64_t rows_per_batch = 0;
+};
+
 // OperatorType (plan.proto:58-80).
 enum OperatorType : int32_t {
   OPERATOR_TYPE_UNKNOWN = 0,
@@ -193,6 +202,7 @@ struct Operator {  // plan.proto:82-110
   AggregateOperator agg;
   MemorySinkOperator mem_sink;
   FilterOperator filter;
+  JoinOperator join;
   std::string grpc_sink_table;  // GRPCSinkOperator.output_table.table_name
 };
 
@@ -374,6 +384,34 @@ inline void Decode(Reader r, Operator* op) {
           if (sf == 1) Decode(s.Sub(), &op->filter.expression);
           else if (sf == 2) { op->filter.columns.emplace_back(); Decode(s.Sub(), &op->filter.columns.back()); }
           else s.Skip(sw);
+        }
+        break;
+      }
+      case 11: {
+        op->which = 11;
+        Reader s = r.Sub();
+        uint32_t sf, sw;
+        JoinOperator& j = op->join;
+        while (s.Next(&sf, &sw)) {
+          switch (sf) {
+            case 1: j.type = static_cast<int32_t>(s.Varint()); break;
+            case 2:
+            case 3: {
+              Reader c = s.Sub();
+              uint32_t cf, cw;
+              std::pair<uint64_t, uint64_t> v{0, 0};
+              while (c.Next(&cf, &cw)) {
+                if (cf == 1) v.first = c.Varint();
+                else if (cf == 2) v.second = c.Varint();
+                else c.Skip(cw);
+              }
+              (sf == 2 ? j.equality_conditions : j.output_columns).push_back(v);
+              break;
+            }
+            case 4: j.column_names.push_back(s.String()); break;
+            case 5: j.rows_per_batch = s.Varint(); break;
+            default: s.Skip(sw);
+          }
         }
         break;
       }

@@ -133,6 +133,22 @@ def _build():
                                ("columns", 2, ".px.carnot.planpb.Column", "rep")])
     _msg(p, "LimitOperator", [("limit", 1, "int64"), ("columns", 2, ".px.carnot.planpb.Column", "rep"),
                               ("abortable_srcs", 3, "uint64", "rep")])
+    jo = _msg(p, "JoinOperator", [("type", 1, "enum:.px.carnot.planpb.JoinOperator.JoinType"),
+                                  ("equality_conditions", 2, ".px.carnot.planpb.JoinOperator.EqualityCondition", "rep"),
+                                  ("output_columns", 3, ".px.carnot.planpb.JoinOperator.ParentColumn", "rep"),
+                                  ("column_names", 4, "string", "rep"), ("rows_per_batch", 5, "uint64")])
+    je = jo.enum_type.add()
+    je.name = "JoinType"
+    for k, v in [("INNER", 0), ("LEFT_OUTER", 1), ("FULL_OUTER", 3)]:
+        ev = je.value.add()
+        ev.name, ev.number = k, v
+    for nm, fields in [("EqualityCondition", [("left_column_index", 1), ("right_column_index", 2)]),
+                       ("ParentColumn", [("parent_index", 1), ("column_index", 2)])]:
+        nt = jo.nested_type.add()
+        nt.name = nm
+        for fname, num in fields:
+            f = nt.field.add()
+            f.name, f.number, f.type, f.label = fname, num, F.TYPE_UINT64, F.LABEL_OPTIONAL
     _msg(p, "Operator", [("op_type", 1, "enum:.px.carnot.planpb.OperatorType"),
                          ("mem_source_op", 2, ".px.carnot.planpb.MemorySourceOperator", "opt", "op"),
                          ("map_op", 3, ".px.carnot.planpb.MapOperator", "opt", "op"),
@@ -140,6 +156,7 @@ def _build():
                          ("mem_sink_op", 5, ".px.carnot.planpb.MemorySinkOperator", "opt", "op"),
                          ("filter_op", 6, ".px.carnot.planpb.FilterOperator", "opt", "op"),
                          ("limit_op", 7, ".px.carnot.planpb.LimitOperator", "opt", "op"),
+                         ("join_op", 11, ".px.carnot.planpb.JoinOperator", "opt", "op"),
                          ("grpc_sink_op", 1000, ".px.carnot.planpb.GRPCSinkOperator", "opt", "op")], oneofs=["op"])
     _msg(p, "PlanNode", [("id", 1, "uint64"), ("op", 2, ".px.carnot.planpb.Operator")])
     dag = _msg(p, "DAG", [("nodes", 1, ".px.carnot.planpb.DAG.DAGNode", "rep")])
@@ -155,7 +172,7 @@ def _build():
     pool.Add(p)
     out = {}
     for name in ["Plan", "PlanFragment", "PlanNode", "DAG", "Operator", "MapOperator", "AggregateOperator",
-                 "FilterOperator", "LimitOperator", "MemorySourceOperator", "MemorySinkOperator", "GRPCSinkOperator",
+                 "FilterOperator", "LimitOperator", "JoinOperator", "MemorySourceOperator", "MemorySinkOperator", "GRPCSinkOperator",
                  "ScalarExpression", "ScalarValue", "ScalarFunc", "AggregateExpression", "Column", "PlanOptions"]:
         out[name] = message_factory.GetMessageClass(pool.FindMessageTypeByName("px.carnot.planpb." + name))
     return out

@@ -125,6 +125,50 @@ def sink_op(name: str, types: Sequence[int] = (), names: Sequence[str] = ()):
     return op
 
 
+JOIN_INNER, JOIN_LEFT_OUTER, JOIN_FULL_OUTER = 0, 1, 3
+
+
+def join_op(join_type: int, conditions: Sequence, outputs: Sequence, names: Sequence[str] = (), rows_per_batch: int = 0):
+    """JoinOperator (plan.proto:301-338): conditions = [(left_col, right_col)], outputs =
+    [(parent_index, column_index)] with parent 0 = left, 1 = right."""
+    op = planpb.Operator()
+    op.op_type = 2500
+    j = op.join_op
+    j.type = join_type
+    for lc, rc in conditions:
+        c = j.equality_conditions.add()
+        c.left_column_index = lc
+        c.right_column_index = rc
+    for pi, ci in outputs:
+        o = j.output_columns.add()
+        o.parent_index = pi
+        o.column_index = ci
+    j.column_names.extend(names or [f"c{i}" for i in range(len(outputs))])
+    j.rows_per_batch = rows_per_batch
+    return op
+
+
+def dag_plan(nodes: Sequence) -> "planpb.Plan":
+    """One fragment from [(id, op, [parent ids])] in topological order."""
+    plan = planpb.Plan()
+    frag = plan.nodes.add()
+    frag.id = 1
+    children = {nid: [] for nid, _, _ in nodes}
+    for nid, _, parents in nodes:
+        for p in parents:
+            children[p].append(nid)
+    for nid, op, parents in nodes:
+        dn = frag.dag.nodes.add()
+        dn.id = nid
+        dn.sorted_parents.extend(parents)
+        dn.sorted_children.extend(children[nid])
+        pn = frag.nodes.add()
+        pn.id = nid
+        pn.op.CopyFrom(op)
+    plan.dag.nodes.add().id = 1
+    return plan
+
+
 def linear_plan(ops: List) -> "planpb.Plan":
     """One fragment, nodes 1..n chained in order (exec_graph.cc topological execution)."""
     plan = planpb.Plan()
@@ -191,3 +235,32 @@ def c3_plan(table: str = "http_events"):
                           agg_expr("sum", [col(3)], [INT64], fid=2)],
                  ["pod", "remote_addr"], ["count", "mean_latency", "sum_resp_body"])
     return linear_plan([src, flt, agg, sink_op("output")])
+
+
+# conn_stats subset and a pod metadata table for C5 ("C5 (next)").
+CONN_STATS_SCHEMA = [("time_", TIME64NS), ("upid", UINT128), ("remote_addr", STRING), ("remote_port", INT64),
+                     ("bytes_sent", INT64), ("bytes_recv", INT64)]
+CONN_TYPES = [t for _, t in CONN_STATS_SCHEMA]
+CONN_NAMES = [n for n, _ in CONN_STATS_SCHEMA]
+POD_META_SCHEMA = [("upid", UINT128), ("pod", STRING), ("namespace", STRING)]
+POD_TYPES = [t for _, t in POD_META_SCHEMA]
+POD_NAMES = [n for n, _ in POD_META_SCHEMA]
+C5_WINDOW_NS = 10 * 1000 * 1000 * 1000
+
+
+def c5_plan(conn: str = "conn_stats", pods: str = "pod_metadata", window_ns: int = C5_WINDOW_NS):
+    """df.time_ = px.bin(df.time_, 10s); groupby(time_, upid, remote_addr).agg(bytes_sent=sum,
+    bytes_recv=sum); merge with pod metadata on upid (inner).  The output's time_ comes from the
+    left (aggregate) side, so the aggregate is the probe table (equijoin_node.cc:63-69)."""
+    c = {n: i for i, n in enumerate(CONN_NAMES)}
+    src = source_op(conn, CONN_TYPES, CONN_NAMES,
+                    [c["time_"], c["upid"], c["remote_addr"], c["bytes_sent"], c["bytes_recv"]])
+    mp = map_op([func("bin", [col(0), const(INT64, window_ns)], [TIME64NS, INT64]), col(1), col(2), col(3), col(4)],
+                ["time_", "upid", "remote_addr", "bytes_sent", "bytes_recv"])
+    agg = agg_op([0, 1, 2], [agg_expr("sum", [col(3)], [INT64], fid=1), agg_expr("sum", [col(4)], [INT64], fid=2)],
+                 ["time_", "upid", "remote_addr"], ["bytes_sent", "bytes_recv"])
+    psrc = source_op(pods, POD_TYPES, POD_NAMES, [0, 1, 2])
+    join = join_op(JOIN_INNER, [(1, 0)], [(0, 0), (1, 1), (1, 2), (0, 2), (0, 3), (0, 4)],
+                   names=["time_", "pod", "namespace", "remote_addr", "bytes_sent", "bytes_recv"])
+    return dag_plan([(1, src, []), (2, mp, [1]), (3, agg, [2]), (4, psrc, []), (5, join, [3, 4]),
+                     (6, sink_op("output"), [5])])

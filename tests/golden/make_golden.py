@@ -169,9 +169,83 @@ uda_case("basic_int64_count", "612-615", "count", I, [[5, 2, 7, 1]], 4, I)
 uda_case("merge_count", "617-626", "count", I, [[3, 6, 10, 5, 2], [1, 4, 5, 2]], 9, I)
 uda_case("partial_count", "631-634", "count", I, [[3, 6, 10, 5, 2]], 5, I)
 
+# EquijoinNode known answers (equijoin_node_test.cc).  Left table "l" is parent 0, right table
+# "r" is parent 1.  The output is independent of how the two inputs interleave (probe batches
+# wait for build eos), so each table is simply a batch list.  "unordered_tail": the last N
+# expected batches are compared as one multiset (ExpectRowBatchesData, emitted from a hash map).
+J = "src/carnot/exec/equijoin_node_test.cc"
+join_cases = []
+
+
+def join_case(name, line, jtype, conds, outs, names, lt, lb, rt, rb, out_types, expected, tail=0):
+    plan = P.dag_plan([
+        (1, P.source_op("l", lt, [f"l{i}" for i in range(len(lt))], list(range(len(lt)))), []),
+        (2, P.source_op("r", rt, [f"r{i}" for i in range(len(rt))], list(range(len(rt)))), []),
+        (3, P.join_op(jtype, conds, outs, names=names, rows_per_batch=5), [1, 2]),
+        (4, P.sink_op("out"), [3]),
+    ])
+    join_cases.append({
+        "name": "join." + name, "source": J + ":" + line, "plan": text_format.MessageToString(plan),
+        "tables": {"l": {"types": lt, "batches": lb}, "r": {"types": rt, "batches": rb}},
+        "output": {"types": out_types, "batches": expected}, "ordered": True, "tol_ulp": 0,
+        "unordered_tail": tail,
+    })
+
+
+join_case("ordered_inner_join", "73-152", P.JOIN_INNER, [(0, 1)], [(0, 1), (1, 1), (1, 0)],
+          ["left_1", "right_1", "time_"],
+          [I, F], [[[1, 2, 2], [1.0, 2.0, 2.1]], [[9, 1, 1], [9.0, 1.1, 1.2]]],
+          [T, I], [[[10, 20, 30, 31], [1, 2, 3, 3]], [[101, 150, 190], [1, 5, 9]]],
+          [F, I, T],
+          [batch([[1.0, 1.1, 1.2, 2.0, 2.1], [1, 1, 1, 2, 2], [10, 10, 10, 20, 20]], False, False),
+           batch([[1.0, 1.1, 1.2, 9.0], [1, 1, 1, 9], [101, 101, 101, 190]], True, True)])
+join_case("ordered_left_join", "154-239", P.JOIN_LEFT_OUTER, [(1, 0)], [(1, 1), (0, 1), (0, 0)],
+          ["right_1", "left_1", "time_"],
+          [T, I], [[[10, 20, 30, 31], [1, 2, 3, 3]], [[101, 150, 190], [1, 5, 9]]],
+          [I, F], [[[1, 2, 2], [1.0, 2.0, 2.1]], [[9, 1, 1, 8], [9.0, 1.1, 1.2, 8.0]]],
+          [F, I, T],
+          [batch([[1.0, 1.1, 1.2, 2.0, 2.1], [1, 1, 1, 2, 2], [10, 10, 10, 20, 20]], False, False),
+           batch([[0.0, 0.0, 1.0, 1.1, 1.2], [3, 3, 1, 1, 1], [30, 31, 101, 101, 101]], False, False),
+           batch([[0.0, 9.0], [5, 9], [150, 190]], True, True)])
+fo_l = [[[101, 200, 101, 200, 101], [1, 2, 3, 4, 5]], [[200, 200, 200, 300, 300], [6, 8, 10, 12, 14]],
+        [[400, 500], [16, 18]]]
+fo_r = [[[-10, -20, -30], [110, 120, 101]]]
+unmatched = [2, 4, 6, 8, 10, 12, 14, 16, 18]
+join_case("unordered_full_outer_join", "241-321", P.JOIN_FULL_OUTER, [(0, 1)], [(0, 1), (1, 1), (1, 0)],
+          ["left_1", "right_1", "right_0"], [T, I], fo_l, [I, T], fo_r, [I, T, I],
+          [batch([[0, 0, 1, 3, 5], [110, 120, 101, 101, 101], [-10, -20, -30, -30, -30]], False, False),
+           batch([unmatched[:5], [0] * 5, [0] * 5], False, False),
+           batch([unmatched[5:], [0] * 4, [0] * 4], True, True)], tail=2)
+join_case("unordered_no_left_columns", "323-395", P.JOIN_FULL_OUTER, [(0, 1)], [(1, 1), (1, 0)],
+          ["right_1", "right_0"], [T, I], fo_l, [I, T], fo_r, [T, I],
+          [batch([[110, 120, 101, 101, 101], [-10, -20, -30, -30, -30]], False, False),
+           batch([[0] * 5, [0] * 5], False, False),
+           batch([[0] * 4, [0] * 4], True, True)], tail=2)
+join_case("unordered_no_right_columns", "397-462", P.JOIN_FULL_OUTER, [(0, 1)], [(0, 1)],
+          ["left_1"], [T, I], fo_l, [I, T], fo_r, [I],
+          [batch([[0, 0, 1, 3, 5]], False, False), batch([unmatched[:5]], False, False),
+           batch([unmatched[5:]], True, True)], tail=2)
+nm_l = [[[101, 102, 101, 103, 101], [1, 2, 3, 4, 5]]]
+join_case("unordered_no_matches", "464-526", P.JOIN_INNER, [(0, 1)], [(0, 1), (1, 1), (1, 0)],
+          ["left_1", "right_1", "right_0"], [T, I], nm_l, [I, T], [[[-10, -20, -30], [200, 300, 400]]],
+          [I, T, I], [batch([[], [], []], True, True)])
+join_case("zero_row_row_batch_right", "528-590", P.JOIN_INNER, [(0, 1)], [(0, 1), (1, 1), (1, 0)],
+          ["left_1", "right_1", "right_0"], [T, I], nm_l, [I, T], [[[], []]],
+          [I, T, I], [batch([[], [], []], True, True)])
+join_case("unordered_many_matches", "592-687", P.JOIN_INNER, [(0, 1)], [(0, 1), (1, 1), (1, 0)],
+          ["left_1", "time_", "right_0"],
+          [T, I], [[[101, 102, 103, 101, 102], [1, 2, 3, 4, 5]], [[103, 101, 104], [6, 7, 8]]],
+          [I, T], [[[10, 20, 30, 40], [101, 101, 102, 102]], [[50, 60, 70, 80, 90], [103, 103, 103, 103, 105]]],
+          [I, T, I],
+          [batch([[1, 4, 7, 1, 4], [101] * 5, [10, 10, 10, 20, 20]], False, False),
+           batch([[7, 2, 5, 2, 5], [101, 102, 102, 102, 102], [20, 30, 30, 40, 40]], False, False),
+           batch([[3, 6, 3, 6, 3], [103] * 5, [50, 50, 60, 60, 70]], False, False),
+           batch([[6, 3, 6], [103] * 3, [70, 80, 80]], True, True)])
+
 doc = {
     "generator": "tests/golden/make_golden.py",
     "cases": cases,
+    "join_cases": join_cases,
     # QuantilesUDA known answers (math_sketches_test.cc:30-70); EXPECT_DOUBLE_EQ = 4 ULP.
     "quantiles": [
         {"source": "src/carnot/funcs/builtins/math_sketches_test.cc:30-48", "input": fv,
@@ -182,4 +256,4 @@ doc = {
 }
 with open(OUT, "w") as f:
     json.dump(doc, f, indent=1)
-print(f"wrote {len(cases)} cases to {OUT}")
+print(f"wrote {len(cases)} cases and {len(join_cases)} join cases to {OUT}")

@@ -27,6 +27,11 @@ def case_plan(case):
 
 
 def case_tables(case):
+    if "tables" in case:
+        return {name: {"types": t["types"], "flags": None,
+                       "batches": [[Column.from_values(ty, vals) for ty, vals in zip(t["types"], b)]
+                                   for b in t["batches"]]}
+                for name, t in case["tables"].items()}
     inp = case["input"]
     batches = [[Column.from_values(t, vals) for t, vals in zip(inp["types"], b)] for b in inp["batches"]]
     return {"t": {"types": inp["types"], "batches": batches, "flags": inp.get("flags")}}
@@ -90,3 +95,23 @@ def rows_match(got: List[tuple], want: List[tuple], ordered: bool, tol_ulp: int 
 def expected_rows(case, bi):
     b = case["output"]["batches"][bi]
     return rows(b["cols"])
+
+
+def check_case_output(out, case):
+    """Compare executed output batches with a KAT case.  The last `unordered_tail` expected batches
+    are one multiset split over that many batches (ExpectRowBatchesData)."""
+    want = case["output"]["batches"]
+    tail = case.get("unordered_tail", 0)
+    assert len(out) == len(want), f"{case['name']}: {len(out)} batches, want {len(want)}"
+    for bi, (g, w) in enumerate(zip(out, want)):
+        assert (g["eow"], g["eos"]) == (w["eow"], w["eos"]), f"{case['name']} batch {bi} flags"
+        assert [c.type for c in g["cols"]] == case["output"]["types"]
+    head = len(want) - tail
+    for bi in range(head):
+        got = rows(out[bi]["cols"])
+        assert rows_match(got, expected_rows(case, bi), case["ordered"], case["tol_ulp"]), \
+            f"{case['name']} batch {bi}: {got} != {expected_rows(case, bi)}"
+    if tail:
+        got = [r for bi in range(head, len(want)) for r in rows(out[bi]["cols"])]
+        exp = [r for bi in range(head, len(want)) for r in expected_rows(case, bi)]
+        assert rows_match(got, exp, False, case["tol_ulp"]), f"{case['name']} tail: {got} != {exp}"

@@ -283,3 +283,42 @@ def test_long_and_empty_string_keys_take_the_deferred_path(ctx):
     assert len(ref) > 400 and set(ref) == set(dev)
     for k in ref:
         assert ref[k] == dev[k], k
+
+
+@pytest.mark.gpu
+def test_device_join_hot_key_and_scale(ctx):
+    """pxg_join at scale against numpy: 2M probe rows x 50K build rows with one hot key holding
+    20K build rows (one probe row fans out to 20K outputs), UINT128 keys, unmatched rows on both
+    sides.  Checks the row count, per-row match counts, the probe-order / build-order layout and
+    an order-independent checksum of the gathered payloads."""
+    import numpy as np
+    from pixie_amd.device import Column, Table
+    rng = np.random.default_rng(5)
+    nb, npb = 50_000, 2_000_000
+    bkey = rng.integers(0, 40_000, nb).astype(np.uint64)
+    bkey[:20_000] = 7                                  # hot key
+    bpay = rng.integers(0, 1 << 40, nb).astype(np.int64)
+    pkey = rng.integers(0, 45_000, npb).astype(np.uint64)
+    pkey[rng.integers(0, npb, 20)] = 7                 # a few probe rows hit the hot key
+    ppay = np.arange(npb, dtype=np.int64)
+    u128 = lambda k: Column(_lib.UINT128, values=np.ascontiguousarray(np.stack([k, k ^ np.uint64(0xABCDEF)], axis=1)))  # noqa: E731
+    B = Table(ctx, [_lib.UINT128, _lib.INT64]); B.append([u128(bkey), Column(_lib.INT64, values=bpay)]); B.flush()
+    Pt = Table(ctx, [_lib.UINT128, _lib.INT64]); Pt.append([u128(pkey), Column(_lib.INT64, values=ppay)]); Pt.flush()
+    out, nprobe = B.join(Pt, [0], [0], [(0, 1), (1, 1)])
+    cnt = np.bincount(bkey.astype(np.int64), minlength=50_000)
+    per = cnt[pkey.astype(np.int64)]
+    assert out.num_rows == nprobe == int(per.sum())
+    pp = out.fetch(0).values
+    bp = out.fetch(1).values
+    # probe rows appear in table order, each repeated per match
+    assert np.array_equal(pp, np.repeat(ppay, per))
+    # within one probe row, build rows follow build-table order
+    order = np.argsort(bkey, kind="stable")
+    starts = np.concatenate([[0], np.cumsum(cnt)])
+    first = np.flatnonzero(pkey == 7)[0]
+    o0 = int(per[:first].sum())
+    assert np.array_equal(bp[o0:o0 + cnt[7]], bpay[order[starts[7]:starts[8]]])
+    # checksum of build payloads over all output rows
+    sums = np.bincount(bkey.astype(np.int64), weights=bpay.astype(np.float64), minlength=50_000)
+    assert abs(float(bp.astype(np.float64).sum()) - float(sums[pkey.astype(np.int64)].sum())) < 1e-3 * float(bp.sum())
+    out.close(); B.close(); Pt.close()

@@ -8,7 +8,7 @@ import math
 import pytest
 
 import oracle_client as oc
-from kat import case_plan, case_tables, expected_rows, load_kat, rows, rows_match, ulp_diff
+from kat import case_plan, case_tables, check_case_output, expected_rows, load_kat, rows, rows_match, ulp_diff
 from pixie_amd import host_engine as H
 from pixie_amd import planpb
 from pixie_amd import plans as P
@@ -68,6 +68,47 @@ def test_windowed_agg_is_not_fused():
     assert "GpuFilterNode" in txt and "GpuAggNode out=" in txt and "fused" not in txt
 
 
+JOIN_KAT = {c["name"]: c for c in KAT["join_cases"]}
+
+
+def test_join_plans_pick_the_reference_probe_side():
+    c = JOIN_KAT["join.ordered_inner_join"]          # time_ from the right parent -> probe = right
+    assert "GpuEquijoinNode(type=0, probe=right, rows_per_batch=5)" in H.explain(case_plan(c), case_tables(c))
+    c = JOIN_KAT["join.ordered_left_join"]           # time_ from the left parent -> probe = left
+    assert "GpuEquijoinNode(type=1, probe=left, rows_per_batch=5)" in H.explain(case_plan(c), case_tables(c))
+    c = JOIN_KAT["join.unordered_full_outer_join"]
+    txt = H.explain(case_plan(c), case_tables(c))
+    assert txt.splitlines()[:2] == ["MemorySourceNode(l)", "MemorySourceNode(r)"]
+    assert "GpuEquijoinNode(type=3, probe=right" in txt
+
+
+def _two_table_join(jtype, names, outs=((0, 1), (1, 1)), rows_per_batch=0):
+    return P.dag_plan([(1, P.source_op("l", [2, 2], ["a", "b"], [0, 1]), []),
+                       (2, P.source_op("r", [2, 2], ["c", "d"], [0, 1]), []),
+                       (3, P.join_op(jtype, [(0, 0)], list(outs), names=names, rows_per_batch=rows_per_batch), [1, 2]),
+                       (4, P.sink_op("out"), [3])])
+
+
+def test_time_ordered_join_restrictions_match_operator_init():
+    # JoinOperator::Init (operators.cc:593-603)
+    tabs = {"l": {"types": [2, 2], "batches": []}, "r": {"types": [2, 2], "batches": []}}
+    with pytest.raises(H.PxcError) as e:
+        H.explain(_two_table_join(P.JOIN_FULL_OUTER, ["time_", "x"]), tabs)
+    assert e.value.code == 3 and "full outer" in str(e.value)
+    with pytest.raises(H.PxcError) as e:
+        H.explain(_two_table_join(P.JOIN_LEFT_OUTER, ["x", "time_"], outs=((0, 1), (1, 1))), tabs)
+    assert e.value.code == 3 and "left join" in str(e.value)
+    assert "rows_per_batch=1024" in H.explain(_two_table_join(P.JOIN_INNER, ["x", "y"]), tabs)
+
+
+def test_c5_plan_fuses_the_binned_agg_and_joins_on_device():
+    from pixie_amd import synth
+    txt = H.explain(P.c5_plan(), synth.c5_tables(3, 1000))
+    assert txt.splitlines()[:2] == ["MemorySourceNode(conn_stats)", "MemorySourceNode(pod_metadata)"]
+    assert "GpuAggNode(fused filter/map chain)" in txt and "GpuMapNode" not in txt
+    assert "GpuEquijoinNode(type=0, probe=left, rows_per_batch=1024)" in txt
+
+
 @pytest.fixture(scope="module")
 def engine():
     e = H.Engine(0)
@@ -120,3 +161,85 @@ def test_engine_quantiles_json_keys_and_values(engine):
     assert list(got) == ["p01", "p10", "p25", "p50", "p75", "p90", "p99"]
     for k, v in q["expected"].items():
         assert ulp_diff(got[k], float(v)) <= 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", KAT["join_cases"], ids=[c["name"] for c in KAT["join_cases"]])
+def test_engine_matches_reference_join_kat(engine, case):
+    check_case_output(engine.execute(case_plan(case), case_tables(case))["out"], case)
+
+
+def _random_join_tables(seed, nl=(700, 650, 0, 333), nr=(512, 500, 37, 400)):
+    """Two tables with a (INT64, STRING) key, duplicates on both sides, keys present on one side
+    only, and an empty batch: l = [k INT64, s STRING, f FLOAT64, t TIME64NS],
+    r = [k INT64, s STRING, name STRING, v INT64]."""
+    import numpy as np
+    from pixie_amd.device import Column
+    rng = np.random.default_rng(seed)
+    words = ["", "a", "pod-1", "pod-2", "kube-system/coredns-7f9c", "x" * 40, "y" * 70, "svc"]
+
+    def table(sizes, krange, extra):
+        batches = []
+        for n in sizes:
+            k = rng.integers(0, krange, n)
+            s = [words[i] for i in rng.integers(0, len(words), n)]
+            cols = [Column.from_values(2, k.tolist()), Column.from_values(5, s)]
+            if extra == "l":
+                cols += [Column.from_values(4, rng.normal(size=n).tolist()),
+                         Column.from_values(6, rng.integers(0, 10**12, n).tolist())]
+            else:
+                cols += [Column.from_values(5, [f"n{i}" * int(i % 5) for i in rng.integers(0, 100, n)]),
+                         Column.from_values(2, rng.integers(-10**9, 10**9, n).tolist())]
+            batches.append(cols)
+        return batches
+    return {"l": {"types": [2, 5, 4, 6], "batches": table(nl, 40, "l")},
+            "r": {"types": [2, 5, 5, 2], "batches": table(nr, 50, "r")}}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jtype,time_side", [(P.JOIN_INNER, None), (P.JOIN_INNER, 0), (P.JOIN_LEFT_OUTER, None),
+                                             (P.JOIN_LEFT_OUTER, 0), (P.JOIN_FULL_OUTER, None)])
+def test_engine_join_matches_oracle(engine, jtype, time_side):
+    """Device join vs the CPU restatement, batch for batch.  Rows produced by probe rows must
+    match in order (probe order, then build order per key); unmatched build rows come from a
+    hash map in the reference (order unspecified) and are compared as a multiset."""
+    tables = _random_join_tables(7 + jtype)
+    outs = [(0, 3), (1, 2), (0, 1), (1, 3), (0, 2), (1, 0)]
+    names = ["time_" if (time_side == 0 and i == 0) else f"c{i}" for i in range(len(outs))]
+    plan = P.dag_plan([(1, P.source_op("l", [2, 5, 4, 6], ["k", "s", "f", "t"], [0, 1, 2, 3]), []),
+                       (2, P.source_op("r", [2, 5, 5, 2], ["k", "s", "name", "v"], [0, 1, 2, 3]), []),
+                       (3, P.join_op(jtype, [(0, 0), (1, 1)], outs, names=names, rows_per_batch=256), [1, 2]),
+                       (4, P.sink_op("out"), [3])])
+    ref = oc.execute_plan(plan, tables)["out"]
+    dev = engine.execute(plan, tables)["out"]
+    assert [(b["rows"] if "rows" in b else len(b["cols"][0]), b["eow"], b["eos"]) for b in dev] == \
+           [(b["rows"] if "rows" in b else len(b["cols"][0]), b["eow"], b["eos"]) for b in ref]
+    R = [r for b in ref for r in rows(b["cols"])]
+    D = [r for b in dev for r in rows(b["cols"])]
+    assert len(R) > 1000
+    # rows from unmatched build keys (the side whose rows the probe table did not match)
+    probe_left = time_side == 0
+    emit_build = jtype == P.JOIN_FULL_OUTER or (jtype == P.JOIN_LEFT_OUTER and not probe_left)
+    ub = 0
+    if emit_build:
+        bt, pt = (tables["r"], tables["l"]) if probe_left else (tables["l"], tables["r"])
+        pkeys = {(k, s) for b in pt["batches"] for k, s in zip(b[0].to_list(), b[1].to_list())}
+        ub = sum(1 for b in bt["batches"] for k, s in zip(b[0].to_list(), b[1].to_list()) if (k, s) not in pkeys)
+    head = len(R) - ub
+    assert D[:head] == R[:head]
+    assert sorted(map(repr, D[head:])) == sorted(map(repr, R[head:]))
+
+
+@pytest.mark.gpu
+def test_engine_c5_matches_oracle(engine):
+    """C5: bin(time_, 10s) x (upid, remote_addr) sums joined to pod metadata.  The probe side is
+    the aggregate, whose group order is unspecified, so rows compare as a multiset; batch sizes
+    and flags must match exactly."""
+    from pixie_amd import synth
+    tables = synth.c5_tables(11, 400_000)
+    ref = oc.execute_plan(P.c5_plan(), tables)["output"]
+    dev = engine.execute(P.c5_plan(), tables)["output"]
+    assert [(b["rows"], b["eow"], b["eos"]) for b in dev] == [(b["rows"], b["eow"], b["eos"]) for b in ref]
+    R = sorted(r for b in ref for r in rows(b["cols"]))
+    D = sorted(r for b in dev for r in rows(b["cols"]))
+    assert len(R) > 100_000 and D == R

@@ -4,7 +4,7 @@ import math
 import pytest
 
 import oracle_client as oc
-from kat import case_plan, case_tables, expected_rows, load_kat, rows, rows_match, ulp_diff
+from kat import case_plan, case_tables, check_case_output, expected_rows, load_kat, rows, rows_match, ulp_diff
 
 KAT = load_kat()
 
@@ -19,6 +19,11 @@ def test_oracle_matches_reference_kat(case):
         assert [c.type for c in g["cols"]] == case["output"]["types"]
         assert rows_match(rows(g["cols"]), expected_rows(case, bi), case["ordered"], case["tol_ulp"]), \
             f"{case['name']} batch {bi}: {rows(g['cols'])} != {expected_rows(case, bi)}"
+
+
+@pytest.mark.parametrize("case", KAT["join_cases"], ids=[c["name"] for c in KAT["join_cases"]])
+def test_oracle_matches_reference_join_kat(case):
+    check_case_output(oc.execute_plan(case_plan(case), case_tables(case))["out"], case)
 
 
 @pytest.mark.parametrize("q", KAT["quantiles"], ids=["floats", "ints"])
