@@ -251,12 +251,18 @@ __device__ __forceinline__ void LoadOffsetPair(const int32_t* __restrict__ offs,
   *o1 = odd ? v.c : v.b;
 }
 
-// Keys of row r.  Returns false when a string key is too long for the register path.
+// First round trip of a row's keys: the offset pair of every STRING key (start, length) and the
+// value of every fixed-width key.  Phase 2 issues it one row ahead, so it overlaps the previous
+// row's probe instead of heading each row's dependent load chain.
 template <int NK>
-__device__ __forceinline__ bool LoadFastKeysRow(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r,
-                                                FastKeys<NK>& k) {
-  const uint8_t* ptr[NK];
-  bool ok = true;
+struct KeyHeads {
+  int32_t o0[NK];
+  uint32_t len[NK];
+  uint64_t a[NK], b[NK];
+};
+
+template <int NK>
+__device__ __forceinline__ void LoadKeyHeads(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r, KeyHeads<NK>& h) {
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
     const int t = plan->key_types[i];
@@ -264,14 +270,35 @@ __device__ __forceinline__ bool LoadFastKeysRow(const AggPlanDev* __restrict__ p
     if (t == PXG_STRING) {
       int32_t o0, o1;
       LoadOffsetPair(col.offsets, r, &o0, &o1);
-      ptr[i] = col.data + o0;
-      k.len[i] = static_cast<uint32_t>(o1 - o0);
-      ok = ok && k.len[i] <= 8u * kFastStrWords;
+      h.o0[i] = o0;
+      h.len[i] = static_cast<uint32_t>(o1 - o0);
+      h.a[i] = h.b[i] = 0;
     } else {
+      h.o0[i] = 0;
       const Val v = LoadCol(col, t, r);
-      k.w[i][0] = v.a;
-      k.w[i][1] = v.b;
-      k.len[i] = 0;
+      h.a[i] = v.a;
+      h.b[i] = v.b;
+      h.len[i] = 0;
+    }
+  }
+}
+
+// Second round trip: the string payload words.  Returns false when a string key is too long for
+// the register path.
+template <int NK>
+__device__ __forceinline__ bool LoadKeyBodies(const AggPlanDev* __restrict__ plan, const DevChunk& ch, const KeyHeads<NK>& h,
+                                              FastKeys<NK>& k) {
+  const uint8_t* ptr[NK];
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    k.len[i] = h.len[i];
+    if (plan->key_types[i] == PXG_STRING) {
+      ptr[i] = ch.cols[plan->keys[i].col].data + h.o0[i];
+      ok = ok && h.len[i] <= 8u * kFastStrWords;
+    } else {
+      k.w[i][0] = h.a[i];
+      k.w[i][1] = h.b[i];
     }
   }
   if (!ok) return false;
@@ -549,6 +576,8 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
       }
       __syncthreads();
       const uint64_t base = s_base;
+      KeyHeads<NK> heads = {};
+      if (MODE != 2 && threadIdx.x < total) LoadKeyHeads<NK>(plan, ch, row0 + s_sel[threadIdx.x], heads);
       for (uint32_t i = threadIdx.x; i < total; i += kConsumeBlock) {
         const int64_t local = row0 + s_sel[i];
         const uint64_t pos = base + i;
@@ -557,9 +586,15 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
         FastKeys<NK> k;
         uint32_t slot = kDeferredSlot;
         const uint32_t rowref = (static_cast<uint32_t>(rg.chunk) << kChunkShift) | static_cast<uint32_t>(local);
+        bool have_keys = false;
+        if (MODE != 2) {
+          have_keys = LoadKeyBodies<NK>(plan, ch, heads, k);
+          // the next row's heads, in flight during this row's hash and probe
+          if (i + kConsumeBlock < total) LoadKeyHeads<NK>(plan, ch, row0 + s_sel[i + kConsumeBlock], heads);
+        }
         if (MODE == 2) {
           slot = 0;
-        } else if (LoadFastKeysRow<NK>(plan, ch, local, k)) {
+        } else if (have_keys) {
           const uint64_t h = HashFastKeys<NK>(plan, k);
           if (MODE == 3) {
             stg.slot[pos] = static_cast<uint32_t>(h);
