@@ -15,6 +15,8 @@
  *                      (src/carnot/exec/memory_source_node.cc:54-124).
  *   pxc_explain_plan   the lowering step alone (no device): which nodes the operator switch
  *                      picks, fused chains, compiled device programs.
+ *   pxc_store_*        table_store::TableStore::AddTable / Table::TransferRecordBatch
+ *                      (src/table_store/table/table.cc:174-200) with the tables in HBM.
  *
  * Errors: px.statuspb.Code values (src/common/base/statuspb/status.proto:27-52);
  * pxc_last_error() has the message.  There is no CPU execution path: a plan whose operators
@@ -57,6 +59,27 @@ int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_l
 /* Lowering only (no device): a text description of the node graph and device programs. */
 int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables,
                          char** out);
+
+/* HBM-resident table store (table_store::TableStore / Table, src/table_store/table/table.h:71-199):
+ * named device tables owned by the engine that persist across queries.  A MemorySource whose
+ * name is not among the call's host tables reads the stored table straight from HBM; a fused
+ * Filter/Map -> blocking Agg chain over it consumes the device table in place (no per-query
+ * upload).  Appends are host Arrow-layout batches, coalesced by the device table's pinned
+ * staging into large chunks (the hot -> cold compaction of table.cc:409-427 happens at append).
+ * When the table has a column named "time_" its rows must arrive in non-decreasing time_
+ * order (the order Stirling pushes), which lets MemorySource start_time / stop_time select
+ * [first row >= start, first row > stop) by a device binary search (table.cc:56-95,310-336). */
+int32_t pxc_store_create_table(pxc_engine* engine, const char* name, int32_t ncols, const int32_t* types,
+                               const char* const* names);
+int32_t pxc_store_append(pxc_engine* engine, const char* name, const pxg_column_view* cols, int64_t nrows);
+int32_t pxc_store_drop_table(pxc_engine* engine, const char* name);
+/* Rows in the table, -1 when there is no such table. */
+int64_t pxc_store_num_rows(pxc_engine* engine, const char* name);
+/* The device table itself (owned by the store), NULL when absent. */
+pxg_table* pxc_store_device_table(pxc_engine* engine, const char* name);
+/* pxc_explain_plan with the engine's stored tables visible. */
+int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                                const pxc_table* tables, char** out);
 
 void pxc_free(void* p);
 const char* pxc_last_error(void);

@@ -198,6 +198,11 @@ int64_t pxg_table_device_bytes(const pxg_table* t, int32_t col);
 /* Copy rows [begin, end) of column col back to host (test / sink path). */
 int32_t pxg_table_fetch(pxg_table* t, int32_t col, int64_t begin, int64_t end,
                         pxg_column_out* out);
+/* Time-range cursor support (Table::FindRowIDFromTimeFirstGreaterThanOrEqual / ...GreaterThan,
+ * src/table_store/table/table.cc:310-336): *row = the first row whose value in the
+ * non-decreasing INT64/TIME64NS column col is >= value (strict = 0) or > value (strict = 1);
+ * num_rows when there is none. */
+int32_t pxg_table_time_bound(pxg_table* t, int32_t col, int64_t value, int32_t strict, int64_t* row);
 
 /* ---------------------------------------------------------------------------------------
  * Filter and Map over a device table (non-fused operator shapes).

@@ -1160,6 +1160,30 @@ struct Graph {
         if (it == tables.end()) throw Error(NOT_FOUND, "Table '" + m["name"].as_str() + "' not found");
         s->batches = it->second.batches;
         s->explicit_flags = it->second.explicit_flags;
+        if (m.has("startTime") || m.has("stopTime")) {
+          // Table::Cursor range (table.cc:56-95, 310-336): [first row with time_ >= start,
+          // first row with time_ > stop) of the time-ordered table.
+          int64_t tc = -1;
+          for (size_t c = 0; c < it->second.names.size(); ++c)
+            if (it->second.names[c] == "time_") tc = static_cast<int64_t>(c);
+          if (tc < 0) throw Error(INVALID_ARGUMENT, "table has no time_ column for a time-bounded source");
+          const bool hs = m.has("startTime"), he = m.has("stopTime");
+          const int64_t t0 = hs ? m["startTime"].as_i64() : 0, t1 = he ? m["stopTime"].as_i64() : 0;
+          std::vector<RowBatch> kept;
+          for (const RowBatch& b : s->batches) {
+            const std::vector<int64_t>& tv = b.cols.at(tc)->i;
+            RowBatch nb;
+            for (auto& c : b.cols) nb.cols.push_back(std::make_shared<Col>(c->type));
+            for (int64_t r = 0; r < b.num_rows; ++r) {
+              if ((hs && tv[r] < t0) || (he && tv[r] > t1)) continue;
+              for (size_t c = 0; c < b.cols.size(); ++c) nb.cols[c]->append_from(*b.cols[c], static_cast<size_t>(r));
+              ++nb.num_rows;
+            }
+            if (nb.num_rows > 0) kept.push_back(std::move(nb));
+          }
+          s->batches = std::move(kept);
+          s->explicit_flags = false;
+        }
         for (size_t c = 0; c < m["columnIdxs"].size(); ++c) s->col_idxs.push_back(m["columnIdxs"].at(c).as_i64());
         if (s->col_idxs.empty())
           for (size_t c = 0; c < it->second.types.size(); ++c) s->col_idxs.push_back(static_cast<int64_t>(c));

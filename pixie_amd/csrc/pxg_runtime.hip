@@ -459,6 +459,46 @@ extern "C" int32_t pxg_table_fetch(pxg_table* tp, int32_t col, int64_t begin, in
   return PXG_OK;
 }
 
+// First row whose value in a non-decreasing INT64 / TIME64NS column is >= value (strict = 0) or
+// > value (strict = 1): one thread, a binary search over the chunks by row_base, then over the
+// rows of the chunk (~log2(rows) dependent loads).
+__global__ void TimeBoundKernel(const DevChunk* __restrict__ chunks, int nchunks, int col, int64_t value, int strict,
+                                int64_t nrows, int64_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int64_t lo = 0, hi = nrows;
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    int cl = 0, ch = nchunks - 1;
+    while (cl < ch) {
+      const int cm = (cl + ch + 1) / 2;
+      if (chunks[cm].row_base <= mid) cl = cm;
+      else ch = cm - 1;
+    }
+    const DevChunk& c = chunks[cl];
+    const int64_t v = reinterpret_cast<const int64_t*>(c.cols[col].values)[mid - c.row_base];
+    if (strict ? v > value : v >= value) hi = mid;
+    else lo = mid + 1;
+  }
+  *out = lo;
+}
+
+extern "C" int32_t pxg_table_time_bound(pxg_table* tp, int32_t col, int64_t value, int32_t strict, int64_t* row) {
+  if (!tp || !row || col < 0 || col >= tp->impl.ncols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Table& t = tp->impl;
+  if (t.types[col] != PXG_INT64 && t.types[col] != PXG_TIME64NS) return SetError(PXG_INVALID_ARGUMENT, "time bound needs an INT64/TIME64NS column");
+  PXG_RETURN_IF_ERROR(t.FlushStage());
+  *row = 0;
+  if (t.nrows == 0) return PXG_OK;
+  PXG_RETURN_IF_ERROR(t.EnsureDeviceDescriptors());
+  DevBuf res;
+  PXG_RETURN_IF_ERROR(res.Alloc(16));
+  PXG_RETURN_IF_ERROR(Launch(t.ctx, "table_time_bound", TimeBoundKernel, dim3(1), dim3(64), 0, t.d_chunks.as<const DevChunk>(),
+                             static_cast<int>(t.chunks.size()), col, value, strict ? 1 : 0, t.nrows, res.as<int64_t>()));
+  PXG_HIP(hipMemcpyAsync(row, res.p, 8, hipMemcpyDeviceToHost, t.ctx->stream));
+  PXG_HIP(hipStreamSynchronize(t.ctx->stream));
+  return PXG_OK;
+}
+
 extern "C" void pxg_result_free(pxg_column_out* cols, int32_t n) {
   if (!cols) return;
   for (int32_t i = 0; i < n; ++i) {

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <set>
@@ -442,19 +443,26 @@ class ExecNode {
   std::vector<std::pair<ExecNode*, size_t>> children_;
 };
 
+// Source nodes (exec_node.h:300-315): the graph pulls them until they have nothing left.
+class SourceNode : public ExecNode {
+ public:
+  virtual bool HasBatchesRemaining() const = 0;
+  virtual Status GenerateNext(ExecState* s) = 0;
+};
+
 // MemorySourceNode (memory_source_node.cc:54-124) over a host table's RowBatches.
-class MemorySourceNode : public ExecNode {
+class MemorySourceNode : public SourceNode {
  public:
   MemorySourceNode(const pxc_table* t) : table_(t) {}
   std::string DebugString() const override { return "MemorySourceNode(" + std::string(table_->name) + ")"; }
   // With explicit batch flags every given batch is fed, as the reference's ExecNodeTester does
   // (src/carnot/exec/test_utils.h:319-480); otherwise the source stops at eos.
-  bool HasBatchesRemaining() const {
+  bool HasBatchesRemaining() const override {
     if (table_->batch_flags && table_->nbatches > 0) return next_ < table_->nbatches;
     return next_ < std::max<int32_t>(table_->nbatches, 1) && !done_;
   }
   // GenerateNext: one RowBatch (column-projected) to the children.
-  Status GenerateNext(ExecState* s) {
+  Status GenerateNext(ExecState* s) override {
     RowBatch rb;
     const int32_t nb = table_->nbatches;
     if (nb == 0) {  // empty table: one zero-row batch with eow/eos (memory_source_node.cc:107-118)
@@ -496,6 +504,8 @@ class MemorySourceNode : public ExecNode {
 
  protected:
   Status InitImpl(const planpb::Operator& op) override {
+    if (op.mem_source.has_start_time || op.mem_source.has_stop_time || op.mem_source.streaming)
+      return Err(PXG_UNIMPLEMENTED, "time-bounded or streaming MemorySource needs a stored table (pxc_store_*)");
     idxs_ = op.mem_source.column_idxs;
     if (idxs_.empty())
       for (int32_t c = 0; c < table_->ncols; ++c) idxs_.push_back(c);
@@ -622,13 +632,16 @@ static const char* const kQuantileKeys[7] = {"p01", "p10", "p25", "p50", "p75", 
 // one batch per eow, then ClearAggState (agg_node.cc:169-180).
 class GpuAggNode : public ExecNode {
  public:
-  std::string DebugString() const override { return fused_ ? "GpuAggNode(fused filter/map chain)" : "GpuAggNode"; }
+  std::string DebugString() const override {
+    return std::string(fused_ ? "GpuAggNode(fused filter/map chain)" : "GpuAggNode") + (device_input ? " <- HBM table" : "");
+  }
   // Set by the graph builder for a fused chain: the agg's input columns as programs over the
   // source table, and the conjunction of the chain's predicates.
   std::vector<Program> env;
   bool has_filter = false;
   Program filter;
   bool fused_ = false;
+  bool device_input = false;  // fed by a stored table through ConsumeTable
   RowDescriptor source_types;
 
   std::vector<Program> keys;
@@ -685,7 +698,8 @@ class GpuAggNode : public ExecNode {
   Status OpenImpl(ExecState* s) override {
     if (!s->ctx) return Status::OK();
     PXC_RETURN_IF_ERROR(CreateAgg(s->ctx));
-    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
+    if (!device_input)
+      PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
     return Status::OK();
   }
   Status CloseImpl(ExecState*) override {
@@ -705,6 +719,24 @@ class GpuAggNode : public ExecNode {
     if (!(rb.eos || (windowed && rb.eow))) return Status::OK();  // agg_node.cc:169-171
     PXG_CALL(pxg_table_flush(staging_));
     PXG_CALL(pxg_agg_consume(agg_, staging_, 0, pxg_table_num_rows(staging_)));
+    // New staging for the next window, ClearAggState (agg_node.cc:173-180).
+    pxg_table_destroy(staging_);
+    staging_ = nullptr;
+    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
+    return Emit(s, rb.eow, rb.eos);
+  }
+
+ public:
+  // Fused chain over a stored device table: rows [lo, hi) consumed in place (no staging), then
+  // the one eos batch.  The programs reference the stored table's columns.
+  Status ConsumeTable(ExecState* s, pxg_table* t, int64_t lo, int64_t hi) {
+    if (hi > lo) PXG_CALL(pxg_agg_consume(agg_, t, lo, hi));
+    return Emit(s, true, true);
+  }
+
+ private:
+  // Finalize, render the result batch, ClearAggState, send.
+  Status Emit(ExecState* s, bool eow, bool eos) {
     int64_t groups = 0;
     PXG_CALL(pxg_agg_finalize(agg_, &groups));
     std::vector<pxg_column_out> out(keys.size() + udas.size());
@@ -728,12 +760,8 @@ class GpuAggNode : public ExecNode {
         ob.cols.push_back(hc);
       }
     }
-    ob.eow = rb.eow;
-    ob.eos = rb.eos;
-    // New staging for the next window, ClearAggState (agg_node.cc:173-180).
-    pxg_table_destroy(staging_);
-    staging_ = nullptr;
-    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
+    ob.eow = eow;
+    ob.eos = eos;
     PXG_CALL(pxg_agg_reset(agg_));
     return SendRowBatchToChildren(s, ob);
   }
@@ -999,6 +1027,92 @@ class SinkNode : public ExecNode {
 };
 
 // ---------------------------------------------------------------------------------------
+// HBM-resident table store (table_store::TableStore / Table, table.h:71-199).
+// ---------------------------------------------------------------------------------------
+struct StoredTable {
+  pxg_table* t = nullptr;
+  RowDescriptor types;
+  std::vector<std::string> names;
+  int32_t time_col = -1;  // the "time_" column, if any
+  int64_t last_time = std::numeric_limits<int64_t>::min();
+};
+using TableStore = std::map<std::string, StoredTable>;
+
+// MemorySourceNode over a stored device table.  The cursor range comes from start_time /
+// stop_time as in Table::Cursor (table.cc:56-95): [first row with time_ >= start, first row
+// with time_ > stop).  A fused agg below consumes the range in place; otherwise the range goes
+// out as RowBatches of kBatchRows rows fetched from HBM, the last one with eow/eos (an empty
+// range gives one zero-row eow/eos batch, memory_source_node.cc:97-106).
+class DeviceSourceNode : public SourceNode {
+ public:
+  static constexpr int64_t kBatchRows = 1 << 16;
+  DeviceSourceNode(std::string name, const StoredTable* st) : name_(std::move(name)), st_(st) {}
+  std::string DebugString() const override { return "MemorySourceNode(" + name_ + ", HBM-resident)"; }
+  bool HasBatchesRemaining() const override { return !done_; }
+  GpuAggNode* fused_agg = nullptr;
+  const std::vector<int64_t>& idxs() const { return idxs_; }
+
+  Status GenerateNext(ExecState* s) override {
+    if (!ranged_) {
+      PXC_RETURN_IF_ERROR(Range());
+      ranged_ = true;
+      cur_ = lo_;
+    }
+    if (fused_agg) {
+      done_ = true;
+      return fused_agg->ConsumeTable(s, st_->t, lo_, hi_);
+    }
+    const int64_t end = std::min(hi_, cur_ + kBatchRows);
+    RowBatch rb;
+    if (end <= cur_) {
+      rb = ZeroRowBatch(output_, true, true);
+    } else {
+      rb.num_rows = end - cur_;
+      for (int64_t c : idxs_) {
+        pxg_column_out o{};
+        PXG_CALL(pxg_table_fetch(st_->t, static_cast<int32_t>(c), cur_, end, &o));
+        rb.cols.push_back(FromOut(o));
+      }
+      rb.eow = rb.eos = end >= hi_;
+    }
+    cur_ = end;
+    done_ = rb.eos;
+    return SendRowBatchToChildren(s, rb);
+  }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    const planpb::MemorySourceOperator& ms = op.mem_source;
+    if (ms.streaming) return Err(PXG_UNIMPLEMENTED, "streaming MemorySource (infinite stream) is not supported");
+    idxs_ = ms.column_idxs;
+    if (idxs_.empty())
+      for (size_t c = 0; c < st_->types.size(); ++c) idxs_.push_back(static_cast<int64_t>(c));
+    for (int64_t c : idxs_)
+      if (c < 0 || c >= static_cast<int64_t>(st_->types.size())) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
+    if ((ms.has_start_time || ms.has_stop_time) && st_->time_col < 0)
+      return Err(PXG_INVALID_ARGUMENT, "table %s has no time_ column for a time-bounded source", name_.c_str());
+    ms_ = ms;
+    return Status::OK();
+  }
+
+ private:
+  Status Range() {
+    lo_ = 0;
+    hi_ = pxg_table_num_rows(st_->t);
+    if (ms_.has_start_time) PXG_CALL(pxg_table_time_bound(st_->t, st_->time_col, ms_.start_time, 0, &lo_));
+    if (ms_.has_stop_time) PXG_CALL(pxg_table_time_bound(st_->t, st_->time_col, ms_.stop_time, 1, &hi_));
+    if (hi_ < lo_) hi_ = lo_;
+    return Status::OK();
+  }
+  std::string name_;
+  const StoredTable* st_;
+  planpb::MemorySourceOperator ms_;
+  std::vector<int64_t> idxs_;
+  int64_t lo_ = 0, hi_ = 0, cur_ = 0;
+  bool ranged_ = false, done_ = false;
+};
+
+// ---------------------------------------------------------------------------------------
 // ExecutionGraph (exec_graph.cc:52-289): nodes in DAG order, the operator switch picks the GPU
 // node classes, and a MemorySource -> (Filter | Map)* -> Agg(blocking) chain whose
 // intermediates have no other consumer is fused into one GpuAggNode (its intermediate batches
@@ -1006,7 +1120,8 @@ class SinkNode : public ExecNode {
 // ---------------------------------------------------------------------------------------
 class ExecutionGraph {
  public:
-  Status Init(const planpb::PlanFragment& pf, int32_t ntables, const pxc_table* tables) {
+  Status Init(const planpb::PlanFragment& pf, int32_t ntables, const pxc_table* tables, const TableStore* store) {
+    store_ = store;
     std::map<uint64_t, const planpb::Operator*> ops;
     for (auto& n : pf.nodes) ops[n.id] = &n.op;
     // Parents / children from the DAG (plan_fragment.cc:108-118); without a DAG the nodes form
@@ -1222,17 +1337,31 @@ class ExecutionGraph {
     const pxc_table* tab = nullptr;
     for (int32_t t = 0; t < ntables; ++t)
       if (ms.name == tables[t].name) tab = &tables[t];
-    if (!tab) return Err(PXG_NOT_FOUND, "table %s not found", ms.name.c_str());
-    auto* src = new MemorySourceNode(tab);
-    pool_.emplace_back(src);
+    const StoredTable* stored = nullptr;
+    if (!tab && store_) {
+      auto it = store_->find(ms.name);
+      if (it != store_->end()) stored = &it->second;
+    }
+    if (!tab && !stored) return Err(PXG_NOT_FOUND, "Table '%s' not found", ms.name.c_str());
+    const int32_t ncols = tab ? tab->ncols : static_cast<int32_t>(stored->types.size());
+    auto type_of = [&](int64_t c) { return tab ? tab->col_types[c] : stored->types[static_cast<size_t>(c)]; };
     RowDescriptor src_types;
-    if (ms.column_idxs.empty())
-      for (int32_t c = 0; c < tab->ncols; ++c) src_types.push_back(tab->col_types[c]);
-    else
-      for (int64_t c : ms.column_idxs) {
-        if (c < 0 || c >= tab->ncols) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
-        src_types.push_back(tab->col_types[c]);
-      }
+    std::vector<int64_t> idxs = ms.column_idxs;
+    if (idxs.empty())
+      for (int32_t c = 0; c < ncols; ++c) idxs.push_back(c);
+    for (int64_t c : idxs) {
+      if (c < 0 || c >= ncols) return Err(PXG_INVALID_ARGUMENT, "source column out of range");
+      src_types.push_back(type_of(c));
+    }
+    SourceNode* src;
+    DeviceSourceNode* dsrc = nullptr;
+    if (tab) {
+      src = new MemorySourceNode(tab);
+    } else {
+      dsrc = new DeviceSourceNode(ms.name, stored);
+      src = dsrc;
+    }
+    pool_.emplace_back(src);
     PXC_RETURN_IF_ERROR(src->Init(op, src_types, {}));
     sources_.push_back(src);
     (*built)[id] = src;
@@ -1256,8 +1385,11 @@ class ExecutionGraph {
       cur = c;
     }
     if (!found) return Status::OK();
-    // Substitute the chain into programs over the source columns.
+    // Substitute the chain into programs over the source columns (for a stored table, over
+    // the table's own columns: the agg then reads the device table in place).
     std::vector<Program> env = ColumnEnv(src_types);
+    if (dsrc)
+      for (size_t j = 0; j < env.size(); ++j) env[j].insns[0].arg = static_cast<int32_t>(idxs[j]);
     bool has_filter = false;
     Program filter;
     for (uint64_t cid : chain) {
@@ -1293,6 +1425,7 @@ class ExecutionGraph {
     agg->filter = filter;
     agg->fused_ = !chain.empty();
     agg->source_types = src_types;
+    agg->device_input = dsrc != nullptr;
     RowDescriptor env_types;
     for (auto& p : env) env_types.push_back(p.result_type);
     Status out_ok;
@@ -1300,6 +1433,7 @@ class ExecutionGraph {
     PXC_RETURN_IF_ERROR(out_ok);
     PXC_RETURN_IF_ERROR(agg->Init(*ops[agg_id], out, {env_types}));
     src->AddChild(agg, 0);
+    if (dsrc) dsrc->fused_agg = agg;
     (*built)[agg_id] = agg;
     for (uint64_t cid : chain) fused_away->insert(cid);
     fused_away->insert(agg_id);
@@ -1309,7 +1443,8 @@ class ExecutionGraph {
 
   std::vector<std::unique_ptr<ExecNode>> pool_;
   std::vector<ExecNode*> lowered_;
-  std::vector<MemorySourceNode*> sources_;
+  std::vector<SourceNode*> sources_;
+  const TableStore* store_ = nullptr;
 };
 
 // PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).
@@ -1354,6 +1489,7 @@ using namespace pxc;
 
 struct pxc_engine {
   pxg_ctx* ctx = nullptr;
+  TableStore store;
 };
 
 static int32_t Fail(const Status& s) {
@@ -1378,12 +1514,15 @@ extern "C" int32_t pxc_engine_create(int32_t device, pxc_engine** out) {
 
 extern "C" int32_t pxc_engine_destroy(pxc_engine* e) {
   if (!e) return PXG_OK;
+  for (auto& kv : e->store) pxg_table_destroy(kv.second.t);
+  e->store.clear();
   pxg_ctx_destroy(e->ctx);
   delete e;
   return PXG_OK;
 }
 
-static Status Lower(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, ExecutionGraph* g) {
+static Status Lower(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, const TableStore* store,
+                    ExecutionGraph* g) {
   if (!plan || plan_len < 0) return Err(PXG_INVALID_ARGUMENT, "no plan");
   planpb::Plan p;
   try {
@@ -1392,12 +1531,14 @@ static Status Lower(const uint8_t* plan, int64_t plan_len, int32_t ntables, cons
     return Err(PXG_INVALID_ARGUMENT, "%s", e.what());
   }
   if (p.fragments.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no fragments");
-  return g->Init(p.fragments[0], ntables, tables);
+  return g->Init(p.fragments[0], ntables, tables, store);
 }
 
-extern "C" int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, char** out) {
+static int32_t Explain(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, const TableStore* store,
+                       char** out) {
+  if (!out) return Fail(Err(PXG_INVALID_ARGUMENT, "out is null"));
   ExecutionGraph g;
-  Status s = Lower(plan, plan_len, ntables, tables, &g);
+  Status s = Lower(plan, plan_len, ntables, tables, store, &g);
   if (!s.ok()) return Fail(s);
   const std::string txt = g.Explain();
   *out = static_cast<char*>(std::malloc(txt.size() + 1));
@@ -1405,11 +1546,88 @@ extern "C" int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32
   return PXG_OK;
 }
 
+extern "C" int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, char** out) {
+  return Explain(plan, plan_len, ntables, tables, nullptr, out);
+}
+
+extern "C" int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                                           const pxc_table* tables, char** out) {
+  if (!engine) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  return Explain(plan, plan_len, ntables, tables, &engine->store, out);
+}
+
+// ---------------------------------------------------------------------------------------
+// Table store ABI (TableStore::AddTable, Table::TransferRecordBatch, table.cc:174-200).
+// ---------------------------------------------------------------------------------------
+extern "C" int32_t pxc_store_create_table(pxc_engine* e, const char* name, int32_t ncols, const int32_t* types,
+                                          const char* const* names) {
+  if (!e || !name || ncols <= 0 || !types) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  if (e->store.count(name)) return Fail(Err(PXG_ALREADY_EXISTS, "table %s already exists", name));
+  StoredTable st;
+  for (int32_t c = 0; c < ncols; ++c) {
+    st.types.push_back(types[c]);
+    st.names.push_back(names && names[c] ? names[c] : "");
+    if (st.names.back() == "time_") {
+      if (types[c] != PXG_TIME64NS && types[c] != PXG_INT64) return Fail(Err(PXG_INVALID_ARGUMENT, "time_ must be TIME64NS"));
+      st.time_col = c;
+    }
+  }
+  const int32_t rc = pxg_table_create(e->ctx, ncols, types, &st.t);
+  if (rc != PXG_OK) return Fail(FromPxg(rc));
+  e->store.emplace(name, std::move(st));
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_store_append(pxc_engine* e, const char* name, const pxg_column_view* cols, int64_t nrows) {
+  if (!e || !name || (!cols && nrows > 0) || nrows < 0) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  auto it = e->store.find(name);
+  if (it == e->store.end()) return Fail(Err(PXG_NOT_FOUND, "Table '%s' not found", name));
+  StoredTable& st = it->second;
+  if (nrows == 0) return PXG_OK;
+  for (size_t c = 0; c < st.types.size(); ++c)
+    if (cols[c].type != st.types[c] || cols[c].length != nrows)
+      return Fail(Err(PXG_INVALID_ARGUMENT, "column %zu does not match the table's relation", c));
+  if (st.time_col >= 0) {  // time order (the hot store's append order, table.cc:174-200)
+    const int64_t* t = static_cast<const int64_t*>(cols[st.time_col].values);
+    int64_t prev = st.last_time;
+    for (int64_t r = 0; r < nrows; ++r) {
+      if (t[r] < prev) return Fail(Err(PXG_INVALID_ARGUMENT, "time_ goes backwards at row %lld of the appended batch", (long long)r));
+      prev = t[r];
+    }
+    st.last_time = prev;
+  }
+  const int32_t rc = pxg_table_append(st.t, cols, nrows);
+  return rc == PXG_OK ? PXG_OK : Fail(FromPxg(rc));
+}
+
+extern "C" int32_t pxc_store_drop_table(pxc_engine* e, const char* name) {
+  if (!e || !name) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  auto it = e->store.find(name);
+  if (it == e->store.end()) return Fail(Err(PXG_NOT_FOUND, "Table '%s' not found", name));
+  pxg_table_destroy(it->second.t);
+  e->store.erase(it);
+  return PXG_OK;
+}
+
+extern "C" int64_t pxc_store_num_rows(pxc_engine* e, const char* name) {
+  if (!e || !name) return -1;
+  auto it = e->store.find(name);
+  if (it == e->store.end()) return -1;
+  if (pxg_table_flush(it->second.t) != PXG_OK) return -1;
+  return pxg_table_num_rows(it->second.t);
+}
+
+extern "C" pxg_table* pxc_store_device_table(pxc_engine* e, const char* name) {
+  if (!e || !name) return nullptr;
+  auto it = e->store.find(name);
+  return it == e->store.end() ? nullptr : it->second.t;
+}
+
 extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                                     const pxc_table* tables, uint8_t** out, int64_t* out_len) {
   if (!engine || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
   ExecutionGraph g;
-  Status s = Lower(plan, plan_len, ntables, tables, &g);
+  Status s = Lower(plan, plan_len, ntables, tables, &engine->store, &g);
   if (!s.ok()) return Fail(s);
   ExecState st;
   st.ctx = engine->ctx;

@@ -145,11 +145,14 @@ struct AggregateExpression {  // plan.proto:553-570
   std::vector<int32_t> args_data_types;
 };
 
-struct MemorySourceOperator {  // plan.proto:195-212
+struct MemorySourceOperator {  // plan.proto:149-167
   std::string name;
   std::vector<int64_t> column_idxs;
   std::vector<std::string> column_names;
   std::vector<int32_t> column_types;
+  bool has_start_time = false, has_stop_time = false;  // google.protobuf.Int64Value wrappers
+  int64_t start_time = 0, stop_time = 0;
+  bool streaming = false;
 };
 struct MemorySinkOperator {  // plan.proto:214-222
   std::string name;
@@ -330,6 +333,17 @@ inline void Decode(Reader r, Operator* op) {
           else if (sf == 2) s.RepeatedVarint(sw, &op->mem_source.column_idxs);
           else if (sf == 3) op->mem_source.column_names.push_back(s.String());
           else if (sf == 4) s.RepeatedVarint(sw, &op->mem_source.column_types);
+          else if (sf == 5 || sf == 6) {
+            Reader v = s.Sub();
+            uint32_t vf, vw;
+            int64_t x = 0;
+            while (v.Next(&vf, &vw)) {
+              if (vf == 1) x = static_cast<int64_t>(v.Varint());
+              else v.Skip(vw);
+            }
+            if (sf == 5) { op->mem_source.has_start_time = true; op->mem_source.start_time = x; }
+            else { op->mem_source.has_stop_time = true; op->mem_source.stop_time = x; }
+          } else if (sf == 8) op->mem_source.streaming = s.Varint() != 0;
           else s.Skip(sw);
         }
         break;

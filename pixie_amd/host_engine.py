@@ -40,6 +40,18 @@ def load() -> C.CDLL:
     lib.pxc_execute_plan.restype = i32
     lib.pxc_explain_plan.argtypes = [C.c_char_p, i64, i32, p(PxcTable), p(vp)]
     lib.pxc_explain_plan.restype = i32
+    lib.pxc_engine_explain_plan.argtypes = [vp, C.c_char_p, i64, i32, p(PxcTable), p(vp)]
+    lib.pxc_engine_explain_plan.restype = i32
+    lib.pxc_store_create_table.argtypes = [vp, C.c_char_p, i32, p(i32), p(C.c_char_p)]
+    lib.pxc_store_create_table.restype = i32
+    lib.pxc_store_append.argtypes = [vp, C.c_char_p, p(ColumnView), i64]
+    lib.pxc_store_append.restype = i32
+    lib.pxc_store_drop_table.argtypes = [vp, C.c_char_p]
+    lib.pxc_store_drop_table.restype = i32
+    lib.pxc_store_num_rows.argtypes = [vp, C.c_char_p]
+    lib.pxc_store_num_rows.restype = i64
+    lib.pxc_store_device_table.argtypes = [vp, C.c_char_p]
+    lib.pxc_store_device_table.restype = vp
     lib.pxc_free.argtypes = [vp]
     lib.pxc_free.restype = None
     lib.pxc_last_error.argtypes = []
@@ -113,10 +125,10 @@ class Engine:
         self.h = C.c_void_p()
         _check(self.lib.pxc_engine_create(device, C.byref(self.h)))
 
-    def execute(self, plan, tables: Dict[str, dict]):
+    def execute(self, plan, tables: Dict[str, dict] = None):
         """Run the plan's first fragment; returns {sink: [{'rows','eow','eos','cols'}]}."""
         pb = plan.SerializeToString()
-        t = _Tables(tables)
+        t = _Tables(tables or {})
         out = C.c_void_p()
         n = C.c_int64()
         _check(self.lib.pxc_execute_plan(self.h, pb, len(pb), t.n, t.arr, C.byref(out), C.byref(n)))
@@ -125,6 +137,37 @@ class Engine:
         finally:
             self.lib.pxc_free(out)
         return parse_pxrb(buf)
+
+    def explain(self, plan, tables: Dict[str, dict] = None) -> str:
+        """Lowering with the engine's stored tables visible (no execution)."""
+        pb = plan.SerializeToString()
+        t = _Tables(tables or {})
+        out = C.c_void_p()
+        _check(self.lib.pxc_engine_explain_plan(self.h, pb, len(pb), t.n, t.arr, C.byref(out)))
+        try:
+            return C.string_at(out.value).decode()
+        finally:
+            self.lib.pxc_free(out)
+
+    # HBM-resident table store (pxc_store_*).
+    def create_table(self, name: str, types, names) -> None:
+        ty = (C.c_int32 * len(types))(*types)
+        nm = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        _check(self.lib.pxc_store_create_table(self.h, name.encode(), len(types), ty, nm))
+
+    def append(self, name: str, cols) -> None:
+        """Append one host RowBatch (a list of pixie_amd.device.Column) to a stored table."""
+        views = (ColumnView * max(1, len(cols)))(*[c.view() for c in cols])
+        _check(self.lib.pxc_store_append(self.h, name.encode(), views, len(cols[0]) if cols else 0))
+
+    def drop_table(self, name: str) -> None:
+        _check(self.lib.pxc_store_drop_table(self.h, name.encode()))
+
+    def num_rows(self, name: str) -> int:
+        return int(self.lib.pxc_store_num_rows(self.h, name.encode()))
+
+    def device_table(self, name: str):
+        return self.lib.pxc_store_device_table(self.h, name.encode())
 
     def close(self) -> None:
         if self.h:

@@ -68,12 +68,17 @@ def _build():
                                   ("ST_HTTP_RESP_STATUS", 1400)])
     _msg(types, "UInt128", [("low", 1, "uint64"), ("high", 2, "uint64")])
     pool.Add(types)
+    from google.protobuf import wrappers_pb2
+    wrappers = descriptor_pb2.FileDescriptorProto()
+    wrappers_pb2.DESCRIPTOR.CopyToProto(wrappers)
+    pool.Add(wrappers)
 
     p = descriptor_pb2.FileDescriptorProto()
     p.name = "src/carnot/planpb/plan.proto"
     p.package = "px.carnot.planpb"
     p.syntax = "proto3"
     p.dependency.append("src/shared/types/typespb/types.proto")
+    p.dependency.append("google/protobuf/wrappers.proto")
     DT = "enum:.px.types.DataType"
     ST = "enum:.px.types.SemanticType"
     _enum(p, "OperatorType", [("OPERATOR_TYPE_UNKNOWN", 0), ("MEMORY_SOURCE_OPERATOR", 1000),
@@ -105,6 +110,8 @@ def _build():
         f.name, f.number, f.label, f.type, f.type_name, f.oneof_index = fname, num, F.LABEL_OPTIONAL, F.TYPE_MESSAGE, tn, 0
     _msg(p, "MemorySourceOperator", [("name", 1, "string"), ("column_idxs", 2, "int64", "rep"),
                                      ("column_names", 3, "string", "rep"), ("column_types", 4, DT, "rep"),
+                                     ("start_time", 5, ".google.protobuf.Int64Value"),
+                                     ("stop_time", 6, ".google.protobuf.Int64Value"),
                                      ("tablet", 7, "string"), ("streaming", 8, "bool")])
     _msg(p, "MemorySinkOperator", [("name", 1, "string"), ("column_types", 2, DT, "rep"),
                                    ("column_names", 3, "string", "rep"), ("column_semantic_types", 4, ST, "rep")])

@@ -105,7 +105,8 @@ def agg_op(groups: Sequence[int], values: Sequence, group_names: Sequence[str] =
     return op
 
 
-def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Sequence[int]):
+def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Sequence[int],
+              start_time: int = None, stop_time: int = None):
     op = planpb.Operator()
     op.op_type = 1000
     m = op.mem_source_op
@@ -113,6 +114,10 @@ def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Seque
     m.column_idxs.extend(idxs)
     m.column_types.extend([types[i] for i in idxs])
     m.column_names.extend([names[i] for i in idxs])
+    if start_time is not None:
+        m.start_time.value = start_time
+    if stop_time is not None:
+        m.stop_time.value = stop_time
     return op
 
 

@@ -243,3 +243,134 @@ def test_engine_c5_matches_oracle(engine):
     R = sorted(r for b in ref for r in rows(b["cols"]))
     D = sorted(r for b in dev for r in rows(b["cols"]))
     assert len(R) > 100_000 and D == R
+
+
+# ---------------------------------------------------------------------------------------
+# HBM-resident table store (pxc_store_*).
+# ---------------------------------------------------------------------------------------
+def _http_rows(n, seed=20250117):
+    from pixie_amd.device import datagen_http_events
+    return datagen_http_events(seed, 0, n, threads=8)
+
+
+def _batches(cols, rows_per_batch):
+    n = len(cols[0])
+    return [[c.slice(a, min(a + rows_per_batch, n)) for c in cols] for a in range(0, n, rows_per_batch)]
+
+
+def test_oracle_time_bounded_source_is_the_cursor_range():
+    # [first row >= start, first row > stop) of a time-ordered table (table.cc:56-95).
+    from pixie_amd.device import Column
+    t = list(range(1000, 1100))
+    tables = {"t": {"types": [6, 2], "names": ["time_", "v"],
+                    "batches": [[Column.from_values(6, t[i:i + 7]), Column.from_values(2, t[i:i + 7])] for i in range(0, 100, 7)]}}
+    plan = P.linear_plan([P.source_op("t", [6, 2], ["time_", "v"], [0, 1], start_time=1013, stop_time=1050),
+                          P.agg_op([], [P.agg_expr("count", [P.col(1)], [2]), P.agg_expr("sum", [P.col(1)], [2], fid=1)]),
+                          P.sink_op("out")])
+    out = oc.execute_plan(plan, tables)["out"]
+    assert rows(out[0]["cols"]) == [(38, sum(range(1013, 1051)))]
+    plan = P.linear_plan([P.source_op("t", [6, 2], ["time_", "v"], [0, 1], start_time=5000), P.sink_op("out")])
+    out = oc.execute_plan(plan, tables)["out"]
+    assert [(b["rows"], b["eow"], b["eos"]) for b in out] == [(0, True, True)]
+
+
+def test_time_bounded_source_over_host_tables_is_unimplemented():
+    plan = P.linear_plan([P.source_op("t", [6, 2], ["time_", "v"], [0, 1], start_time=1), P.sink_op("out")])
+    with pytest.raises(H.PxcError) as e:
+        H.explain(plan, {"t": {"types": [6, 2], "batches": []}})
+    assert e.value.code == 10 and "stored table" in str(e.value)
+
+
+@pytest.fixture
+def store_engine():
+    e = H.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.gpu
+def test_store_c2_consumes_the_hbm_table_in_place(store_engine):
+    cols = _http_rows(300_000)
+    store_engine.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
+    for b in _batches(cols, 1024):              # 1024-row RowBatches, coalesced into HBM chunks
+        store_engine.append("http_events", b)
+    assert store_engine.num_rows("http_events") == 300_000
+    txt = store_engine.explain(P.c2_plan(with_pluck=True))
+    assert "MemorySourceNode(http_events, HBM-resident)" in txt and "<- HBM table" in txt
+    dev = store_engine.execute(P.c2_plan(with_pluck=True))["output"]
+    ref = oc.execute_plan(P.c2_plan(with_pluck=True),
+                          {"http_events": {"types": P.HTTP_TYPES, "names": P.HTTP_NAMES, "batches": _batches(cols, 65536)}})["output"]
+    R = {r[:2]: r[2:] for r in rows(ref[0]["cols"])}
+    D = {r[:2]: r[2:] for r in rows(dev[0]["cols"])}
+    assert set(R) == set(D) and len(R) > 1000 and dev[0]["eos"]
+    for k in R:
+        assert R[k][0] == D[k][0]
+        assert abs(R[k][1] - D[k][1]) <= 1e-6 * abs(R[k][1])
+        if R[k][0] <= 8000:
+            for a, b in zip(R[k][2:], D[k][2:]):
+                assert ulp_diff(a, b) <= 4, (k, a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bounds", [(None, None), (1.7e18 + 1000 * 50_000, None), (None, 1.7e18 + 1000 * 123_456),
+                                    (1.7e18 + 1000 * 7, 1.7e18 + 1000 * 199_999 + 1), (10**19 // 2, None), (None, 5)])
+def test_store_time_range_matches_the_oracle(store_engine, bounds):
+    cols = _http_rows(200_000, seed=3)
+    store_engine.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
+    for b in _batches(cols, 4096):
+        store_engine.append("http_events", b)
+    start, stop = (None if x is None else int(x) for x in bounds)
+    src = P.source_op("http_events", P.HTTP_TYPES, P.HTTP_NAMES, [P.HE["time_"], P.HE["service"], P.HE["latency"]],
+                      start_time=start, stop_time=stop)
+    fused = P.linear_plan([src, P.agg_op([1], [P.agg_expr("count", [P.col(2)], [2]),
+                                               P.agg_expr("sum", [P.col(2)], [2], fid=1),
+                                               P.agg_expr("min", [P.col(0)], [6], fid=2)]), P.sink_op("out")])
+    # an unfused consumer (filter -> sink) sees the range as RowBatches, in table order
+    unfused = P.linear_plan([src, P.filter_op(P.func("greaterThan", [P.col(2), P.const(2, 20_000_000)], [2, 2]), [0, 1, 2]),
+                             P.sink_op("out")])
+    host = {"http_events": {"types": P.HTTP_TYPES, "names": P.HTTP_NAMES, "batches": _batches(cols, 65536)}}
+    ref = oc.execute_plan(fused, host)["out"]
+    dev = store_engine.execute(fused)["out"]
+    assert sorted(r for b in dev for r in rows(b["cols"])) == sorted(r for b in ref for r in rows(b["cols"]))
+    ref = oc.execute_plan(unfused, host)["out"]
+    dev = store_engine.execute(unfused)["out"]
+    assert dev[-1]["eos"] and dev[-1]["eow"]
+    assert [r for b in dev for r in rows(b["cols"])] == [r for b in ref for r in rows(b["cols"])]
+
+
+@pytest.mark.gpu
+def test_store_c5_from_stored_tables_matches_oracle(store_engine):
+    from pixie_amd import synth
+    tables = synth.c5_tables(5, 300_000, rows_per_batch=2048)
+    for name, t in tables.items():
+        store_engine.create_table(name, t["types"], t["names"])
+    # conn_stats arrives time-ordered in the generator's batches
+    for name, t in tables.items():
+        for b in t["batches"]:
+            store_engine.append(name, b)
+    ref = oc.execute_plan(P.c5_plan(), tables)["output"]
+    dev = store_engine.execute(P.c5_plan())["output"]
+    assert [(b["rows"], b["eos"]) for b in dev] == [(b["rows"], b["eos"]) for b in ref]
+    assert sorted(r for b in dev for r in rows(b["cols"])) == sorted(r for b in ref for r in rows(b["cols"]))
+
+
+@pytest.mark.gpu
+def test_store_errors(store_engine):
+    from pixie_amd.device import Column
+    store_engine.create_table("t", [6, 2], ["time_", "v"])
+    with pytest.raises(H.PxcError) as e:
+        store_engine.create_table("t", [6, 2], ["time_", "v"])
+    assert e.value.code == 6
+    store_engine.append("t", [Column.from_values(6, [5, 6, 6]), Column.from_values(2, [1, 2, 3])])
+    with pytest.raises(H.PxcError) as e:                       # time_ must not go backwards
+        store_engine.append("t", [Column.from_values(6, [4]), Column.from_values(2, [1])])
+    assert e.value.code == 3
+    with pytest.raises(H.PxcError) as e:                       # relation mismatch
+        store_engine.append("t", [Column.from_values(2, [7]), Column.from_values(2, [1])])
+    assert e.value.code == 3
+    assert store_engine.num_rows("t") == 3 and store_engine.num_rows("nope") == -1
+    with pytest.raises(H.PxcError) as e:
+        store_engine.execute(P.linear_plan([P.source_op("nope", [2], ["x"], [0]), P.sink_op("o")]))
+    assert e.value.code == 5
+    store_engine.drop_table("t")
+    assert store_engine.num_rows("t") == -1
