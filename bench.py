@@ -70,13 +70,17 @@ def main():
 
     from pixie_amd import plans as P
     from pixie_amd.device import Ctx, Table, datagen_http_events
+    from pixie_amd.host_engine import Engine
     from pixie_amd.pipeline import LinearQuery
     from pixie_amd.dist import exchange_partials
 
     n = args.rows_per_gpu or (100_000_000 if world == 1 else 125_000_000)
     row0 = rank * n
-    ctx = Ctx(local_rank)
-    table = Table(ctx, P.HTTP_TYPES)
+    # The table lives in the C++ engine's HBM-resident table store; the timed step runs the
+    # libpxg ABI on that device table, and the engine leg runs the whole plan over it.
+    engine = Engine(local_rank)
+    ctx = Ctx(local_rank, handle=engine.ctx_handle())
+    engine.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
     t0 = time.time()
     svc_bytes = path_bytes = 0
     for a in range(0, n, args.gen_slice):
@@ -84,9 +88,10 @@ def main():
         cols = datagen_http_events(SEED, row0 + a, m, n_pair_keys=10_000_000, threads=16)
         svc_bytes += int(cols[2].offsets[-1])
         path_bytes += int(cols[3].offsets[-1])
-        table.append(cols)
+        engine.append("http_events", cols)
         del cols
-    table.flush()
+    assert engine.num_rows("http_events") == n
+    table = Table(ctx, P.HTTP_TYPES, handle=engine.device_table("http_events"), owned=False)
     log(rank, f"[bench] generated + uploaded {n} rows/rank in {time.time() - t0:.1f}s "
               f"({table.num_chunks} chunks)")
     # Algorithmic bytes: every referenced column once in Arrow layout.
@@ -146,6 +151,23 @@ def main():
         except Exception:
             traffic = None
 
+    # Engine leg (N=1): the unmodified binary C2 plan through pxc_execute_plan over the stored
+    # table: fused consume + finalize + result D2H + quantile JSON + pluck + PXRB serialisation.
+    engine_query = None
+    if world == 1:
+        pb = P.c2_plan(with_pluck=True).SerializeToString()
+        engine.execute_raw(pb)
+        ctx.sync()
+        reps = max(3, min(args.steps, 10))
+        te = time.perf_counter()
+        for _ in range(reps):
+            res = engine.execute_raw(pb)
+        te = time.perf_counter() - te
+        engine_query = {"ms_per_query": te * 1000.0 / reps, "rows_per_s": n * reps / te, "queries": reps,
+                        "result_bytes": len(res),
+                        "path": "pxc_execute_plan (C++ engine, include/pxcarnot.h) over the HBM-resident stored table: "
+                                "fused consume + finalize + result D2H + quantiles JSON + pluck_float64 + PXRB"}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -185,11 +207,13 @@ def main():
                 "avg_launch_ms": avg_launch_ms,
             },
             "cpu_baseline": cpu,
+            "engine_query": engine_query,
         }
         print(json.dumps(line), flush=True)
     agg.close()
     table.close()
     ctx.close()
+    engine.close()
     if world > 1:
         dist.destroy_process_group()
 

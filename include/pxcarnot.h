@@ -77,6 +77,8 @@ int32_t pxc_store_drop_table(pxc_engine* engine, const char* name);
 int64_t pxc_store_num_rows(pxc_engine* engine, const char* name);
 /* The device table itself (owned by the store), NULL when absent. */
 pxg_table* pxc_store_device_table(pxc_engine* engine, const char* name);
+/* The engine's device context (owned by the engine): libpxg calls on stored tables use it. */
+pxg_ctx* pxc_engine_ctx(pxc_engine* engine);
 /* pxc_explain_plan with the engine's stored tables visible. */
 int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                                 const pxc_table* tables, char** out);

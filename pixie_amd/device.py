@@ -100,11 +100,17 @@ def column_from_out(o: ColumnOut, per_row: int = 1) -> Column:
 
 
 class Ctx:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, handle=None):
+        """A new device context, or (handle given) a non-owning view of an existing pxg_ctx,
+        e.g. the one a pxc_engine owns."""
         self.device = device
         lib = load()
-        h = C.c_void_p()
-        check(lib.pxg_ctx_create(device, C.byref(h)))
+        self.owned = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            check(lib.pxg_ctx_create(device, C.byref(h)))
+        else:
+            h = C.c_void_p(handle)
         self.h = h
         self.lib = lib
 
@@ -124,9 +130,9 @@ class Ctx:
         check(self.lib.pxg_ctx_reset_stats(self.h))
 
     def close(self) -> None:
-        if self.h:
+        if self.h and self.owned:
             self.lib.pxg_ctx_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -138,10 +144,11 @@ class Ctx:
 class Table:
     """HBM-resident table (pxg_table)."""
 
-    def __init__(self, ctx: Ctx, types: Sequence[int], handle=None):
+    def __init__(self, ctx: Ctx, types: Sequence[int], handle=None, owned: bool = True):
         self.ctx = ctx
         self.types = list(types)
         self.lib = ctx.lib
+        self.owned = owned or handle is None
         if handle is None:
             h = C.c_void_p()
             arr = (C.c_int32 * len(types))(*types)
@@ -217,9 +224,9 @@ class Table:
         return Table(self.ctx, types, handle=h), nprobe.value
 
     def close(self) -> None:
-        if self.h:
+        if self.h and self.owned:
             self.lib.pxg_table_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

@@ -15,6 +15,7 @@
 // formatting, as in the reference, where UDA Finalize runs on the host.
 #include <algorithm>
 #include <charconv>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -26,6 +27,7 @@
 #include <set>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -71,6 +73,21 @@ static Status FromPxg(int32_t code) {
 #define PXG_CALL(expr) PXC_RETURN_IF_ERROR(FromPxg(expr))
 
 static thread_local std::string g_last_error;
+
+// Opt-in host-side stage timing (PXC_TIMING=1): one stderr line per stage of a query.
+static bool TimingOn() {
+  static const bool on = std::getenv("PXC_TIMING") != nullptr;
+  return on;
+}
+struct StageClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void Mark(const char* what) {
+    if (!TimingOn()) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[pxc] %-24s %9.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
 
 // ---------------------------------------------------------------------------------------
 // RowBatch (src/table_store/schema/row_batch.h:40-129): Arrow-layout host columns, shared and
@@ -402,6 +419,13 @@ static std::vector<Program> ColumnEnv(const RowDescriptor& types) {
 // ---------------------------------------------------------------------------------------
 struct ExecState {
   pxg_ctx* ctx = nullptr;  // null when only lowering (pxc_explain_plan)
+  // Group counts of earlier runs of the same aggregation (engine-lifetime statistics), used
+  // to size the next run's hash table instead of growing it mid-consume.
+  std::map<std::string, int64_t>* group_hints = nullptr;
+  // Aggregation objects of earlier queries, keyed by their full spec: a query takes one,
+  // resets it and gives it back at Close, so the hash table and finalize workspaces keep their
+  // grown device buffers instead of being freed and reallocated per query.
+  std::multimap<std::string, pxg_agg*>* agg_cache = nullptr;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -424,6 +448,9 @@ class ExecNode {
     return ConsumeNextImpl(s, rb, parent_index);
   }
   void AddChild(ExecNode* child, size_t parent_index) { children_.push_back({child, parent_index}); }
+  // Whether this node can observe the value of input column `col` (conservative default).
+  // Lets a producer skip rendering a column no consumer reads.
+  virtual bool ReadsColumnValue(size_t /*col*/) const { return true; }
   const RowDescriptor& output_descriptor() const { return output_; }
   virtual std::string DebugString() const = 0;
 
@@ -613,18 +640,71 @@ class GpuMapNode : public ExecNode {
   }
 };
 
-// Shortest round-trip rendering of a double, always with a '.' or an exponent (the form
-// rapidjson's Writer::Double produces for QuantilesUDA::Finalize).
-static std::string JsonDouble(double v) {
-  if (std::isnan(v) || std::isinf(v)) return "null";
-  char buf[64];
-  auto r = std::to_chars(buf, buf + sizeof(buf), v);
-  std::string s(buf, r.ptr);
-  if (s.find_first_of(".e") == std::string::npos) s += ".0";
-  return s;
-}
-
 static const char* const kQuantileKeys[7] = {"p01", "p10", "p25", "p50", "p75", "p90", "p99"};
+
+// The QuantilesUDA::Finalize JSON strings (math_sketches.h:40-54) of G groups from their 7
+// doubles each, written straight into one STRING column.  Groups are split over host threads;
+// every thread renders into its own buffer, then the buffers are concatenated.  Values are
+// rendered shortest-round-trip, with ".0" appended to integral values (rapidjson's
+// Writer::Double form, so they parse back as doubles), NaN / inf as null.
+static HostColumn RenderQuantilesJson(const double* d, int64_t G) {
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({16, static_cast<int64_t>(std::thread::hardware_concurrency()), G / 2048 + 1}));
+  std::vector<std::vector<char>> bufs(static_cast<size_t>(nt));
+  std::vector<std::vector<int32_t>> lens(static_cast<size_t>(nt));
+  auto work = [&](int64_t t) {
+    const int64_t g0 = G * t / nt, g1 = G * (t + 1) / nt;
+    std::vector<char>& b = bufs[static_cast<size_t>(t)];
+    std::vector<int32_t>& l = lens[static_cast<size_t>(t)];
+    b.reserve(static_cast<size_t>(g1 - g0) * 160);
+    l.reserve(static_cast<size_t>(g1 - g0));
+    char tmp[64];
+    for (int64_t g = g0; g < g1; ++g) {
+      const size_t start = b.size();
+      b.push_back('{');
+      for (int k = 0; k < 7; ++k) {
+        if (k) b.push_back(',');
+        b.push_back('"');
+        b.insert(b.end(), kQuantileKeys[k], kQuantileKeys[k] + 3);
+        b.push_back('"');
+        b.push_back(':');
+        const double v = d[g * 7 + k];
+        if (std::isnan(v) || std::isinf(v)) {
+          b.insert(b.end(), {'n', 'u', 'l', 'l'});
+          continue;
+        }
+        auto r = std::to_chars(tmp, tmp + sizeof(tmp), v);
+        bool frac = false;
+        for (char* c = tmp; c < r.ptr; ++c) frac = frac || *c == '.' || *c == 'e';
+        b.insert(b.end(), tmp, r.ptr);
+        if (!frac) b.insert(b.end(), {'.', '0'});
+      }
+      b.push_back('}');
+      l.push_back(static_cast<int32_t>(b.size() - start));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int64_t t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  auto o = std::make_shared<OwnedColumn>();
+  o->offsets.reserve(static_cast<size_t>(G) + 1);
+  o->offsets.push_back(0);
+  size_t total = 0;
+  for (auto& b : bufs) total += b.size();
+  o->data.reserve(total + 16);
+  for (int64_t t = 0; t < nt; ++t) {
+    o->data.insert(o->data.end(), bufs[static_cast<size_t>(t)].begin(), bufs[static_cast<size_t>(t)].end());
+    for (int32_t len : lens[static_cast<size_t>(t)]) o->offsets.push_back(o->offsets.back() + len);
+  }
+  o->data.resize(o->data.size() + 16, 0);
+  HostColumn hc;
+  hc.type = PXG_STRING;
+  hc.length = G;
+  hc.offsets = o->offsets.data();
+  hc.data = o->data.data();
+  hc.owner = o;
+  return hc;
+}
 
 // GpuAggNode (AggNode, agg_node.cc:88-542).  When the graph builder fused a
 // Filter / Map chain in front of it, `filter` and the substituted key / argument programs
@@ -697,13 +777,28 @@ class GpuAggNode : public ExecNode {
   }
   Status OpenImpl(ExecState* s) override {
     if (!s->ctx) return Status::OK();
-    PXC_RETURN_IF_ERROR(CreateAgg(s->ctx));
+    hints_ = s->group_hints;
+    if (hints_) {
+      auto it = hints_->find(HintKey());
+      if (it != hints_->end()) expected_groups_ = it->second;
+    }
+    cache_ = s->agg_cache;
+    if (cache_) {
+      auto it = cache_->find(SpecKey());
+      if (it != cache_->end()) {
+        agg_ = it->second;
+        cache_->erase(it);
+        PXG_CALL(pxg_agg_reset(agg_));
+      }
+    }
+    if (!agg_) PXC_RETURN_IF_ERROR(CreateAgg(s->ctx));
     if (!device_input)
       PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(source_types.size()), source_types.data(), &staging_));
     return Status::OK();
   }
   Status CloseImpl(ExecState*) override {
-    if (agg_) pxg_agg_destroy(agg_);
+    if (agg_ && cache_ && cache_->count(SpecKey()) == 0 && cache_->size() < kAggCacheMax) cache_->emplace(SpecKey(), agg_);
+    else if (agg_) pxg_agg_destroy(agg_);
     if (staging_) pxg_table_destroy(staging_);
     agg_ = nullptr;
     staging_ = nullptr;
@@ -730,40 +825,48 @@ class GpuAggNode : public ExecNode {
   // Fused chain over a stored device table: rows [lo, hi) consumed in place (no staging), then
   // the one eos batch.  The programs reference the stored table's columns.
   Status ConsumeTable(ExecState* s, pxg_table* t, int64_t lo, int64_t hi) {
+    StageClock clk;
     if (hi > lo) PXG_CALL(pxg_agg_consume(agg_, t, lo, hi));
+    clk.Mark("agg consume (launch)");
     return Emit(s, true, true);
   }
 
  private:
   // Finalize, render the result batch, ClearAggState, send.
   Status Emit(ExecState* s, bool eow, bool eos) {
+    StageClock clk;
     int64_t groups = 0;
     PXG_CALL(pxg_agg_finalize(agg_, &groups));
+    if (hints_) (*hints_)[HintKey()] = std::max<int64_t>(groups, 1);
+    clk.Mark("agg finalize");
     std::vector<pxg_column_out> out(keys.size() + udas.size());
     PXG_CALL(pxg_agg_result(agg_, out.data(), static_cast<int32_t>(out.size())));
+    clk.Mark("agg result D2H");
     RowBatch ob;
     ob.num_rows = out.empty() ? 0 : out[0].length;
     for (size_t c = 0; c < out.size(); ++c) {
       const bool q = c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
       HostColumn hc = FromOut(out[c]);
       if (q) {  // QuantilesUDA::Finalize JSON (math_sketches.h:40-54) from the 7 device doubles
-        const double* d = static_cast<const double*>(hc.values);
-        std::vector<std::string> js(static_cast<size_t>(hc.length));
-        for (int64_t g = 0; g < hc.length; ++g) {
-          std::string j = "{";
-          for (int k = 0; k < 7; ++k) j += std::string(k ? "," : "") + "\"" + kQuantileKeys[k] + "\":" + JsonDouble(d[g * 7 + k]);
-          js[static_cast<size_t>(g)] = j + "}";
-        }
         quantiles_raw_[c] = hc;
-        ob.cols.push_back(StringColumn(js));
+        bool observed = false;
+        for (auto& ch : children_) observed = observed || ch.first->ReadsColumnValue(c);
+        // A column no consumer reads as a string (the pluck-only C2 shape) stays unrendered:
+        // G empty strings keep the batch's relation.
+        ob.cols.push_back(observed ? RenderQuantilesJson(static_cast<const double*>(hc.values), hc.length)
+                                   : StringColumn(std::vector<std::string>(static_cast<size_t>(hc.length))));
       } else {
         ob.cols.push_back(hc);
       }
     }
     ob.eow = eow;
     ob.eos = eos;
+    clk.Mark("agg render (quantile JSON)");
     PXG_CALL(pxg_agg_reset(agg_));
-    return SendRowBatchToChildren(s, ob);
+    clk.Mark("agg reset");
+    Status st = SendRowBatchToChildren(s, ob);
+    clk.Mark("children (map, sink)");
+    return st;
   }
 
  public:
@@ -792,13 +895,47 @@ class GpuAggNode : public ExecNode {
     spec.udas = us.data();
     pxg_program fp = filter.View();
     spec.filter = has_filter ? &fp : nullptr;
-    spec.expected_groups = 0;
+    spec.expected_groups = expected_groups_;
     spec.windowed = windowed ? 1 : 0;
     PXG_CALL(pxg_agg_create(ctx, &spec, &agg_));
     return Status::OK();
   }
+  // Identity of this aggregation for the group-count statistics: source, keys, filter.
+  std::string HintKey() const {
+    std::string k = hint_source + "|";
+    auto add = [&k](const Program& p) {
+      for (auto& i : p.insns) k += std::to_string(i.op) + ":" + std::to_string(i.type) + ":" + std::to_string(i.arg) + ":" + std::to_string(i.imm) + " ";
+      k += "|";
+    };
+    for (auto& p : keys) add(p);
+    if (has_filter) add(filter);
+    return k;
+  }
+  // Everything pxg_agg_create takes.
+  std::string SpecKey() const {
+    std::string k = HintKey();
+    auto add = [&k](const Program& p) {
+      for (auto& i : p.insns) k += std::to_string(i.op) + ":" + std::to_string(i.type) + ":" + std::to_string(i.arg) + ":" + std::to_string(i.imm) + " ";
+      k.append(reinterpret_cast<const char*>(p.pool.data()), p.pool.size());
+      k += "|";
+    };
+    for (auto& u : udas) {
+      k += "U" + std::to_string(u.kind) + ":" + std::to_string(u.arg_type) + ":" + std::to_string(u.has_init) + ":" + std::to_string(u.init) + ":";
+      if (u.has_arg) add(u.arg);
+      if (u.has_arg2) add(u.arg2);
+    }
+    if (has_filter) add(filter);
+    return k + (windowed ? "W" : "B");
+  }
+  static constexpr size_t kAggCacheMax = 8;
   pxg_agg* agg_ = nullptr;
   pxg_table* staging_ = nullptr;
+  int64_t expected_groups_ = 0;
+  std::map<std::string, int64_t>* hints_ = nullptr;
+  std::multimap<std::string, pxg_agg*>* cache_ = nullptr;
+
+ public:
+  std::string hint_source;  // the source table's name (set by the graph builder)
 };
 
 // Post-aggregation Map over the G result rows: column references and pluck_float64 of a
@@ -806,6 +943,12 @@ class GpuAggNode : public ExecNode {
 class PostAggMapNode : public ExecNode {
  public:
   explicit PostAggMapNode(GpuAggNode* agg) : agg_(agg) {}
+  // pluck_float64 of a quantiles column reads the digest's doubles, not the JSON string.
+  bool ReadsColumnValue(size_t col) const override {
+    for (auto& o : outs_)
+      if (o.quantile < 0 && static_cast<size_t>(o.col) == col) return true;
+    return false;
+  }
   std::string DebugString() const override { return "PostAggMapNode(column refs, pluck_float64)"; }
 
  protected:
@@ -1247,8 +1390,10 @@ class ExecutionGraph {
 
   // ExecuteSources (exec_graph.cc:177-289).
   Status Execute(ExecState* s) {
+    StageClock clk;
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Prepare(s));
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Open(s));
+    clk.Mark("prepare + open");
     // Round-robin over the sources until all are exhausted (exec_graph.cc:177-289).
     Status st;
     for (bool any = true; st.ok() && any;) {
@@ -1259,10 +1404,12 @@ class ExecutionGraph {
         st = src->GenerateNext(s);
       }
     }
+    clk.Mark("sources drained");
     for (auto& n : pool_) {
       Status c = n->Close(s);
       if (st.ok()) st = c;
     }
+    clk.Mark("close");
     return st;
   }
 
@@ -1426,6 +1573,7 @@ class ExecutionGraph {
     agg->fused_ = !chain.empty();
     agg->source_types = src_types;
     agg->device_input = dsrc != nullptr;
+    agg->hint_source = ms.name;
     RowDescriptor env_types;
     for (auto& p : env) env_types.push_back(p.result_type);
     Status out_ok;
@@ -1490,6 +1638,8 @@ using namespace pxc;
 struct pxc_engine {
   pxg_ctx* ctx = nullptr;
   TableStore store;
+  std::map<std::string, int64_t> group_hints;
+  std::multimap<std::string, pxg_agg*> agg_cache;
 };
 
 static int32_t Fail(const Status& s) {
@@ -1514,6 +1664,8 @@ extern "C" int32_t pxc_engine_create(int32_t device, pxc_engine** out) {
 
 extern "C" int32_t pxc_engine_destroy(pxc_engine* e) {
   if (!e) return PXG_OK;
+  for (auto& kv : e->agg_cache) pxg_agg_destroy(kv.second);
+  e->agg_cache.clear();
   for (auto& kv : e->store) pxg_table_destroy(kv.second.t);
   e->store.clear();
   pxg_ctx_destroy(e->ctx);
@@ -1617,6 +1769,8 @@ extern "C" int64_t pxc_store_num_rows(pxc_engine* e, const char* name) {
   return pxg_table_num_rows(it->second.t);
 }
 
+extern "C" pxg_ctx* pxc_engine_ctx(pxc_engine* e) { return e ? e->ctx : nullptr; }
+
 extern "C" pxg_table* pxc_store_device_table(pxc_engine* e, const char* name) {
   if (!e || !name) return nullptr;
   auto it = e->store.find(name);
@@ -1626,13 +1780,18 @@ extern "C" pxg_table* pxc_store_device_table(pxc_engine* e, const char* name) {
 extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                                     const pxc_table* tables, uint8_t** out, int64_t* out_len) {
   if (!engine || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  StageClock clk;
   ExecutionGraph g;
   Status s = Lower(plan, plan_len, ntables, tables, &engine->store, &g);
   if (!s.ok()) return Fail(s);
+  clk.Mark("lower");
   ExecState st;
   st.ctx = engine->ctx;
+  st.group_hints = &engine->group_hints;
+  st.agg_cache = &engine->agg_cache;
   s = g.Execute(&st);
   if (!s.ok()) return Fail(s);
+  clk.Mark("execute (total)");
   Writer w;
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
@@ -1645,5 +1804,6 @@ extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int
   *out_len = static_cast<int64_t>(w.buf.size());
   *out = static_cast<uint8_t*>(std::malloc(w.buf.size()));
   std::memcpy(*out, w.buf.data(), w.buf.size());
+  clk.Mark("PXRB serialise");
   return PXG_OK;
 }

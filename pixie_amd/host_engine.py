@@ -52,6 +52,8 @@ def load() -> C.CDLL:
     lib.pxc_store_num_rows.restype = i64
     lib.pxc_store_device_table.argtypes = [vp, C.c_char_p]
     lib.pxc_store_device_table.restype = vp
+    lib.pxc_engine_ctx.argtypes = [vp]
+    lib.pxc_engine_ctx.restype = vp
     lib.pxc_free.argtypes = [vp]
     lib.pxc_free.restype = None
     lib.pxc_last_error.argtypes = []
@@ -124,6 +126,20 @@ class Engine:
         self.lib = load()
         self.h = C.c_void_p()
         _check(self.lib.pxc_engine_create(device, C.byref(self.h)))
+
+    def ctx_handle(self) -> int:
+        return int(self.lib.pxc_engine_ctx(self.h))
+
+    def execute_raw(self, pb: bytes, tables: Dict[str, dict] = None) -> bytes:
+        """pxc_execute_plan on serialized plan bytes; returns the PXRB result bytes."""
+        t = _Tables(tables or {})
+        out = C.c_void_p()
+        n = C.c_int64()
+        _check(self.lib.pxc_execute_plan(self.h, pb, len(pb), t.n, t.arr, C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out.value, n.value)
+        finally:
+            self.lib.pxc_free(out)
 
     def execute(self, plan, tables: Dict[str, dict] = None):
         """Run the plan's first fragment; returns {sink: [{'rows','eow','eos','cols'}]}."""

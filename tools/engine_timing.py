@@ -1,0 +1,24 @@
+"""Stage timing of the C2 plan through the C++ engine over an HBM-resident stored table
+(PXC_TIMING=1 makes libpxcarnot print one line per stage)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("PXC_TIMING", "1")
+from pixie_amd import plans as P  # noqa: E402
+from pixie_amd.device import datagen_http_events  # noqa: E402
+from pixie_amd.host_engine import Engine  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
+e = Engine(0)
+e.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
+for a in range(0, n, 16_000_000):
+    e.append("http_events", datagen_http_events(20250117, a, min(16_000_000, n - a), n_pair_keys=10_000_000, threads=16))
+print("rows", e.num_rows("http_events"), flush=True)
+pb = P.c2_plan(with_pluck=True).SerializeToString()
+for i in range(4):
+    t = time.perf_counter()
+    r = e.execute_raw(pb)
+    print(f"query {i}: {1000 * (time.perf_counter() - t):.2f} ms, {len(r)} bytes", file=sys.stderr, flush=True)
+e.close()
