@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-sample-rows", type=int, default=160_000_000)
     ap.add_argument("--cpu-batch-rows", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-engine-leg", action="store_true",
+                    help="skip the engine query leg (profiling runs: keeps per-kernel averages to the timed steps)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
     ap.add_argument("--share-gpu0", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (with --backend gloo on a 1-GPU box)")
@@ -154,7 +156,7 @@ def main():
     # Engine leg (N=1): the unmodified binary C2 plan through pxc_execute_plan over the stored
     # table: fused consume + finalize + result D2H + quantile JSON + pluck + PXRB serialisation.
     engine_query = None
-    if world == 1:
+    if world == 1 and not args.no_engine_leg:
         pb = P.c2_plan(with_pluck=True).SerializeToString()
         engine.execute_raw(pb)
         ctx.sync()
