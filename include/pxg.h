@@ -132,7 +132,11 @@ enum pxg_opcode {
   PXG_OP_EQ_S = 50, PXG_OP_NE_S = 51, PXG_OP_LT_S = 52, PXG_OP_LE_S = 53,
   PXG_OP_GT_S = 54, PXG_OP_GE_S = 55,
   PXG_OP_EQ_U = 60, PXG_OP_NE_U = 61,
-  PXG_OP_AND = 70, PXG_OP_OR = 71, PXG_OP_NOT = 72
+  PXG_OP_AND = 70, PXG_OP_OR = 71, PXG_OP_NOT = 72,
+  /* push the little-endian 8-byte word at byte offset imm of STRING column[arg], as `type`
+   * (INT64 / TIME64NS / FLOAT64); 0 when the string is shorter than imm + 8.  Reads a UDA state
+   * out of a serialized_expressions column (UDA::Deserialize, udf.h:98-100).             */
+  PXG_OP_STATE_WORD = 80
 };
 
 typedef struct {
@@ -226,6 +230,9 @@ enum pxg_uda_kind {
   PXG_UDA_MIN = 4,       /* MinUDA        -> arg type                                       */
   PXG_UDA_MAX = 5,       /* MaxUDA        -> arg type (init numeric_limits<T>::min())       */
   PXG_UDA_QUANTILES = 6, /* QuantilesUDA  -> STRING JSON {p01..p99}; 7 FLOAT64 on device    */
+  PXG_UDA_MEAN_MERGE = 7,/* MeanUDA::Merge of deserialized MeanInfo states, then Finalize:
+                            arg = FLOAT64 state sum, arg2 = INT64 state size -> FLOAT64
+                            sum(arg) / double(sum(arg2)) (math_ops.h:586-594)              */
   PXG_UDA_MINSUM = 100   /* test UDA of agg_node_test.cc:44-72 (sum of min(a,b), init arg)  */
 };
 
@@ -248,7 +255,14 @@ typedef struct {
   const pxg_program* filter; /* optional predicate fused in front of the agg (NULL: none) */
   int64_t expected_groups;   /* sizing hint; the table grows on demand */
   int32_t windowed;          /* AggregateOperator.windowed */
-  int32_t reserved;
+  int32_t emit_states;       /* partial_agg && !finalize_results (plan.proto:250-257): the
+                                result is the groups, then one STRING column
+                                "serialized_expressions" (operators.cc:251-257) holding, per
+                                group, every UDA's Serialize() bytes back to back in plan
+                                order: count u64; sum i64|f64; mean {u64 size, f64 sum};
+                                min/max the native value (math_ops.h:583-772).  UDAs without
+                                Serialize (quantiles, minsum) are UNIMPLEMENTED, as they are
+                                not splittable in the reference (udf.h:367).            */
 } pxg_agg_spec;
 
 int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_agg** out);
@@ -257,7 +271,8 @@ int32_t pxg_agg_destroy(pxg_agg* agg);
 int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin, int64_t end);
 /* Finalize: resolves deferred inserts, computes quantiles, compacts groups.  Synchronises. */
 int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups);
-/* Result columns (groups then values, AggNode output order, agg_node.cc:336-346).  For
+/* Result columns (groups then values, AggNode output order, agg_node.cc:336-346; with
+ * spec.emit_states: groups then serialized_expressions, n_cols = n_keys + 1).  For
  * QUANTILES the column is FLOAT64 with 7 values per group (p01,p10,p25,p50,p75,p90,p99,
  * group-major); the host node renders the JSON string (math_sketches.h:40-54). */
 int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);

@@ -347,7 +347,20 @@ struct UDA {
   virtual void Update(const std::vector<const Col*>& args, size_t r) = 0;
   virtual void Merge(const UDA& other) = 0;
   virtual void Finalize(Col* out) = 0;
+  // Serialize / Deserialize (udf.h:98-100): the raw state bytes (math_ops.h:602-757).  UDAs
+  // without them (QuantilesUDA, the test MinSum UDAs) are not splittable (udf.h:367).
+  virtual bool SupportsPartial() const { return false; }
+  virtual std::string Serialize() const { throw Error(UNIMPLEMENTED, "UDA has no Serialize"); }
+  virtual void Deserialize(const char*) { throw Error(UNIMPLEMENTED, "UDA has no Deserialize"); }
 };
+template <typename T>
+static std::string RawBytes(const T& v) { return std::string(reinterpret_cast<const char*>(&v), sizeof(v)); }
+template <typename T>
+static T FromRaw(const char* p) {
+  T v;
+  std::memcpy(&v, p, sizeof(v));
+  return v;
+}
 
 template <DT A>
 struct CountUDA : UDA {
@@ -355,6 +368,9 @@ struct CountUDA : UDA {
   void Update(const std::vector<const Col*>&, size_t) override { ++count; }
   void Merge(const UDA& o) override { count += static_cast<const CountUDA&>(o).count; }
   void Finalize(Col* out) override { out->i.push_back(static_cast<int64_t>(count)); }
+  bool SupportsPartial() const override { return true; }
+  std::string Serialize() const override { return RawBytes(count); }  // math_ops.h:741-748
+  void Deserialize(const char* p) override { count = FromRaw<uint64_t>(p); }
 };
 
 template <DT A>
@@ -371,6 +387,13 @@ struct MeanUDA : UDA {
     sum += m.sum;
   }
   void Finalize(Col* out) override { out->f.push_back(sum / static_cast<double>(size)); }
+  // MeanInfo {uint64 size; double count} (math_ops.h:602-609,621-624).
+  bool SupportsPartial() const override { return true; }
+  std::string Serialize() const override { return RawBytes(size) + RawBytes(sum); }
+  void Deserialize(const char* p) override {
+    size = FromRaw<uint64_t>(p);
+    sum = FromRaw<double>(p + 8);
+  }
 };
 
 template <DT A, DT R>
@@ -388,6 +411,9 @@ struct SumUDA : UDA {
     else sum = WAdd(sum, static_cast<const SumUDA&>(o).sum);
   }
   void Finalize(Col* out) override { Native<R>::put(out, sum); }
+  bool SupportsPartial() const override { return true; }
+  std::string Serialize() const override { return RawBytes(sum); }  // math_ops.h:639-646
+  void Deserialize(const char* p) override { sum = FromRaw<typename Native<R>::type>(p); }
 };
 
 template <DT A>
@@ -404,6 +430,9 @@ struct MaxUDA : UDA {
     if (x > v) v = x;
   }
   void Finalize(Col* out) override { Native<A>::put(out, v); }
+  bool SupportsPartial() const override { return true; }
+  std::string Serialize() const override { return RawBytes(v); }  // math_ops.h:723-730
+  void Deserialize(const char* p) override { v = FromRaw<typename Native<A>::type>(p); }
 };
 
 template <DT A>
@@ -418,6 +447,9 @@ struct MinUDA : UDA {
     if (x < v) v = x;
   }
   void Finalize(Col* out) override { Native<A>::put(out, v); }
+  bool SupportsPartial() const override { return true; }
+  std::string Serialize() const override { return RawBytes(v); }  // math_ops.h:750-757
+  void Deserialize(const char* p) override { v = FromRaw<typename Native<A>::type>(p); }
 };
 
 template <DT A>
@@ -746,6 +778,17 @@ struct AggNode : ExecNode {
   std::vector<DT> group_types;
   std::vector<Expr> values;
   bool windowed = false;
+  // plan.proto:250-257.  partial && !finalize: emit groups + serialized_expressions (STRING,
+  // operators.cc:251-257), every UDA's Serialize() back to back in plan order.  !partial &&
+  // finalize: the input is groups + serialized_expressions; each row's states are
+  // Deserialize()d and Merge()d into the group's UDAs, then finalized.  Anything else: a full
+  // aggregate (the reference's AggNode, which ignores both flags).
+  bool partial_agg = false, finalize_results = false;
+  bool EmitStates() const { return partial_agg && !finalize_results; }
+  bool MergeStates() const { return !partial_agg && finalize_results; }
+  int64_t state_col = -1;
+  std::vector<size_t> state_off;
+  size_t state_rec = 0;
   std::vector<DT> in_types;
   // CreateColumnMapping (agg_node.cc:483-507)
   std::map<int64_t, size_t> plan_to_stored;
@@ -769,10 +812,24 @@ struct AggNode : ExecNode {
     for (auto& v : values) {
       std::vector<DT> types;
       for (auto& a : v.init_args) types.push_back(a.type);
-      for (auto& a : v.args) types.push_back(ExprType(a, in_types));
+      if (MergeStates()) {
+        // The arguments name the pre-split input's columns; the plan's args_data_types give
+        // the registry key (scalar_expression.cc:337-346).
+        if (v.arg_types.size() != v.args.size()) throw Error(INVALID_ARGUMENT, "finalize agg needs args_data_types");
+        for (auto t : v.arg_types) types.push_back(t);
+      } else {
+        for (auto& a : v.args) types.push_back(ExprType(a, in_types));
+      }
       const UDADef* d = UDARegistry::Get().Find(v.name, types);
       if (!d) throw Error(NOT_FOUND, "no UDA " + Key(v.name, types));
       defs.push_back(d);
+      if (EmitStates() || MergeStates()) {
+        auto probe = d->make(v.init_args);
+        if (!probe->SupportsPartial()) throw Error(UNIMPLEMENTED, "UDA " + v.name + " does not support partial aggregation");
+        state_off.push_back(state_rec);
+        state_rec += probe->Serialize().size();
+      }
+      if (MergeStates()) continue;
       for (auto& a : v.args) {
         if (a.kind == Expr::kColumn && !plan_to_stored.count(a.col_index)) {
           plan_to_stored[a.col_index] = stored_to_plan.size();
@@ -781,7 +838,27 @@ struct AggNode : ExecNode {
       }
     }
     for (auto g : groups) group_types.push_back(in_types.at(g));
+    if (MergeStates()) {
+      state_col = static_cast<int64_t>(in_types.size()) - 1;
+      if (state_col < 0 || in_types[state_col] != STRING || std::count(groups.begin(), groups.end(), state_col))
+        throw Error(INVALID_ARGUMENT, "finalize agg input must end in the serialized_expressions STRING column");
+    }
     if (groups.empty()) no_group_udas = MakeUDAs();
+  }
+
+  // Deserialize + Merge one row's states into udas (the finalize half of a split agg).
+  void MergeRow(std::vector<UDAInfo>& udas, const std::string& st) {
+    if (st.size() != state_rec) throw Error(INVALID_ARGUMENT, "serialized_expressions of " + std::to_string(st.size()) + " bytes, expected " + std::to_string(state_rec));
+    for (size_t i = 0; i < values.size(); ++i) {
+      auto tmp = defs[i]->make(values[i].init_args);
+      tmp->Deserialize(st.data() + state_off[i]);
+      udas[i].uda->Merge(*tmp);
+    }
+  }
+  std::string SerializeAll(const std::vector<UDAInfo>& udas) const {
+    std::string s;
+    for (auto& u : udas) s += u.uda->Serialize();
+    return s;
   }
 
   std::vector<UDAInfo> MakeUDAs() {
@@ -812,6 +889,14 @@ struct AggNode : ExecNode {
     out.eos = rb.eos;
     if (groups.empty()) {
       out.num_rows = 1;
+      if (EmitStates()) {
+        auto c = std::make_shared<Col>(STRING);
+        c->s.push_back(SerializeAll(no_group_udas));
+        out.cols.push_back(c);
+        Send(out);
+        no_group_udas = MakeUDAs();
+        return;
+      }
       for (size_t i = 0; i < values.size(); ++i) {
         auto c = std::make_shared<Col>(defs[i]->out);
         no_group_udas[i].uda->Finalize(c.get());
@@ -825,11 +910,15 @@ struct AggNode : ExecNode {
     out.num_rows = static_cast<int64_t>(map.size());
     std::vector<ColPtr> gcols, vcols;
     for (auto t : group_types) gcols.push_back(std::make_shared<Col>(t));
-    for (size_t i = 0; i < values.size(); ++i) vcols.push_back(std::make_shared<Col>(defs[i]->out));
+    if (EmitStates()) vcols.push_back(std::make_shared<Col>(STRING));
+    else
+      for (size_t i = 0; i < values.size(); ++i) vcols.push_back(std::make_shared<Col>(defs[i]->out));
     for (auto& kv : map) {
       for (size_t g = 0; g < groups.size(); ++g) AppendTupleValue(gcols[g].get(), *kv.first, g);
-      EvaluateAggHashValue(kv.second);
-      for (size_t i = 0; i < values.size(); ++i) kv.second->udas[i].uda->Finalize(vcols[i].get());
+      if (!MergeStates()) EvaluateAggHashValue(kv.second);
+      if (EmitStates()) vcols[0]->s.push_back(SerializeAll(kv.second->udas));
+      else
+        for (size_t i = 0; i < values.size(); ++i) kv.second->udas[i].uda->Finalize(vcols[i].get());
     }
     for (auto& c : gcols) out.cols.push_back(c);
     for (auto& c : vcols) out.cols.push_back(c);
@@ -842,6 +931,11 @@ struct AggNode : ExecNode {
   void ConsumeNext(const RowBatch& rb, size_t) override {
     bool ready = rb.eos || (rb.eow && windowed);  // ReadyToEmitBatches (agg_node.cc:169-171)
     if (groups.empty()) {
+      if (MergeStates()) {
+        for (int64_t r = 0; r < rb.num_rows; ++r) MergeRow(no_group_udas, rb.cols.at(state_col)->s[r]);
+        if (ready) Emit(rb);
+        return;
+      }
       // AggregateGroupByNone (agg_node.cc:182-207): ExecBatchUpdateArrow directly.
       for (size_t i = 0; i < values.size(); ++i) {
         std::vector<ColPtr> kids;
@@ -877,6 +971,11 @@ struct AggNode : ExecNode {
         val = it->second;
       }
       row_vals[r] = val;
+    }
+    if (MergeStates()) {
+      for (int64_t r = 0; r < rb.num_rows; ++r) MergeRow(row_vals[r]->udas, rb.cols.at(state_col)->s[r]);
+      if (ready) Emit(rb);
+      return;
     }
     for (size_t s = 0; s < stored_to_plan.size(); ++s) {
       const Col& in = *rb.cols.at(stored_to_plan[s]);
@@ -1214,11 +1313,15 @@ struct Graph {
         auto n = std::make_unique<AggNode>();
         n->in_types = in;
         n->windowed = a["windowed"].as_bool();
+        n->partial_agg = a.has("partialAgg") && a["partialAgg"].as_bool();
+        n->finalize_results = a.has("finalizeResults") && a["finalizeResults"].as_bool();
         for (size_t g = 0; g < a["groups"].size(); ++g) n->groups.push_back(a["groups"].at(g)["index"].as_i64());
         for (size_t v = 0; v < a["values"].size(); ++v) n->values.push_back(ParseAggExpr(a["values"].at(v)));
         n->Init();
         for (auto g : n->groups) n->out_types.push_back(in.at(g));
-        for (auto* d : n->defs) n->out_types.push_back(d->out);
+        if (n->EmitStates()) n->out_types.push_back(STRING);
+        else
+          for (auto* d : n->defs) n->out_types.push_back(d->out);
         node = std::move(n);
       } else if (op.has("joinOp")) {
         const Json& j = op["joinOp"];

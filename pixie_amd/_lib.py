@@ -60,7 +60,7 @@ class UdaSpec(C.Structure):
 class AggSpec(C.Structure):
     _fields_ = [("n_keys", C.c_int32), ("n_udas", C.c_int32), ("keys", C.POINTER(Program)),
                 ("udas", C.POINTER(UdaSpec)), ("filter", C.POINTER(Program)),
-                ("expected_groups", C.c_int64), ("windowed", C.c_int32), ("reserved", C.c_int32)]
+                ("expected_groups", C.c_int64), ("windowed", C.c_int32), ("emit_states", C.c_int32)]
 
 
 class JoinSpec(C.Structure):

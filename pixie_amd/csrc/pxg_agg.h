@@ -39,6 +39,10 @@ struct AggPlanDev {
   int32_t uda_val[kMaxUdas];   // staged stream index (-1: none)
   int32_t uda_arg_type[kMaxUdas];
   int64_t uda_init[kMaxUdas];   // init arg (MINSUM) or 0
+  int32_t uda_val2[kMaxUdas];  // second staged stream (MEAN_MERGE: the state sizes) or -1
+  int32_t state_off[kMaxUdas]; // emit_states: byte offset of the UDA's Serialize() bytes
+  int32_t state_rec;           // emit_states: bytes per group record (0: no states)
+  int32_t emit_states;
   int32_t val_kind[kMaxVals];
   int32_t val_type[kMaxVals];   // result type of the stream (INT64/TIME64NS/FLOAT64/BOOLEAN)
   int32_t col_types[kMaxCols];

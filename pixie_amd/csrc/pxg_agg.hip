@@ -878,6 +878,7 @@ using namespace pxg;
 static void CollectColRefs(const pxg_program& p, std::vector<std::pair<int32_t, int32_t>>* refs) {
   for (int i = 0; i < p.n_insns; ++i)
     if (p.insns[i].op == PXG_OP_COL) refs->push_back({p.insns[i].arg, p.insns[i].type});
+    else if (p.insns[i].op == PXG_OP_STATE_WORD) refs->push_back({p.insns[i].arg, PXG_STRING});
 }
 
 static bool SameProgram(const pxg_program& a, const pxg_program& b) {
@@ -894,6 +895,7 @@ static int32_t UdaOutType(int kind, int arg_type) {
     case PXG_UDA_COUNT: return PXG_INT64;
     case PXG_UDA_SUM: return arg_type == PXG_FLOAT64 ? PXG_FLOAT64 : PXG_INT64;
     case PXG_UDA_MEAN: return PXG_FLOAT64;
+    case PXG_UDA_MEAN_MERGE: return PXG_FLOAT64;
     case PXG_UDA_MIN:
     case PXG_UDA_MAX: return arg_type;
     case PXG_UDA_QUANTILES: return PXG_FLOAT64;
@@ -909,6 +911,7 @@ static bool UdaSupported(int kind, int arg) {
     case PXG_UDA_COUNT: return arg >= PXG_BOOLEAN && arg <= PXG_TIME64NS;
     case PXG_UDA_SUM: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_BOOLEAN;
     case PXG_UDA_MEAN: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_BOOLEAN;
+    case PXG_UDA_MEAN_MERGE: return arg == PXG_FLOAT64;
     case PXG_UDA_MIN:
     case PXG_UDA_MAX: return arg == PXG_FLOAT64 || arg == PXG_INT64 || arg == PXG_TIME64NS;
     case PXG_UDA_QUANTILES: return arg == PXG_FLOAT64 || arg == PXG_INT64;
@@ -948,6 +951,7 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   a.n_udas = spec->n_udas;
   a.windowed = spec->windowed != 0;
   a.has_filter = spec->filter != nullptr;
+  a.emit_states = spec->emit_states != 0;
   std::memset(&a.hplan, 0, sizeof(a.hplan));
   std::vector<uint8_t> pool;
   std::vector<std::pair<DevProgram*, size_t>> pool_fix;
@@ -973,6 +977,23 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   }
   std::vector<const pxg_program*> val_progs, val_progs2;
   std::vector<int> val_kinds;
+  // A plain (kValProgram) stream for p, shared with an earlier identical one.
+  auto plain_stream = [&](const pxg_program& p, int32_t type, int* vi) -> int32_t {
+    for (size_t j = 0; j < val_progs.size(); ++j) {
+      if (val_kinds[j] == kValProgram && SameProgram(*val_progs[j], p)) {
+        *vi = static_cast<int>(j);
+        return PXG_OK;
+      }
+    }
+    if (static_cast<int>(val_progs.size()) >= kMaxVals) return SetError(PXG_UNIMPLEMENTED, "too many distinct UDA arguments");
+    *vi = static_cast<int>(val_progs.size());
+    val_progs.push_back(&p);
+    val_progs2.push_back(&p);
+    val_kinds.push_back(kValProgram);
+    a.val_type.push_back(type);
+    return PXG_OK;
+  };
+  int32_t state_off = 0;
   for (int u = 0; u < a.n_udas; ++u) {
     const pxg_uda_spec& us = spec->udas[u];
     if (!UdaSupported(us.kind, us.arg_type)) return SetError(PXG_UNIMPLEMENTED, "UDA kind %d with arg type %d has no device implementation", us.kind, us.arg_type);
@@ -981,8 +1002,19 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
     a.uda_out_type.push_back(UdaOutType(us.kind, us.arg_type));
     a.uda_init.push_back(us.init_i64);
     a.uda_has_init.push_back(us.has_init);
-    int vi = -1;
-    if (us.kind != PXG_UDA_COUNT) {
+    int vi = -1, vi2 = -1;
+    if (a.emit_states) {  // Serialize() sizes (math_ops.h:583-772)
+      if (us.kind == PXG_UDA_QUANTILES || us.kind == PXG_UDA_MINSUM || us.kind == PXG_UDA_MEAN_MERGE)
+        return SetError(PXG_UNIMPLEMENTED, "UDA kind %d has no Serialize: it cannot be partially aggregated", us.kind);
+      a.hplan.state_off[u] = state_off;
+      state_off += us.kind == PXG_UDA_MEAN ? 16 : 8;
+    }
+    if (us.kind == PXG_UDA_MEAN_MERGE) {
+      if (us.arg.result_type != PXG_FLOAT64 || us.arg2.result_type != PXG_INT64)
+        return SetError(PXG_INVALID_ARGUMENT, "MEAN_MERGE takes a FLOAT64 sum and an INT64 size");
+      PXG_RETURN_IF_ERROR(plain_stream(us.arg, PXG_FLOAT64, &vi));
+      PXG_RETURN_IF_ERROR(plain_stream(us.arg2, PXG_INT64, &vi2));
+    } else if (us.kind != PXG_UDA_COUNT) {
       if (us.arg.result_type != us.arg_type) return SetError(PXG_INVALID_ARGUMENT, "UDA %d arg type mismatch", u);
       const int vk = us.kind == PXG_UDA_MINSUM ? kValMinOf2 : kValProgram;
       for (size_t j = 0; j < val_progs.size(); ++j) {
@@ -1004,11 +1036,15 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
     a.uda_val.push_back(vi);
     a.hplan.uda_kind[u] = us.kind;
     a.hplan.uda_val[u] = vi;
+    a.hplan.uda_val2[u] = vi2;
     a.hplan.uda_arg_type[u] = us.arg_type;
     a.hplan.uda_init[u] = us.has_init ? us.init_i64 : 0;
   }
   a.n_vals = static_cast<int32_t>(val_progs.size());
   a.hplan.n_vals = a.n_vals;
+  a.state_rec = state_off;
+  a.hplan.state_rec = state_off;
+  a.hplan.emit_states = a.emit_states ? 1 : 0;
   for (int v = 0; v < a.n_vals; ++v) {
     a.hplan.val_kind[v] = val_kinds[v];
     a.hplan.val_type[v] = a.val_type[v];

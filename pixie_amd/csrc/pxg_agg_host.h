@@ -16,6 +16,7 @@ struct AggResult {
   DevBuf key_data[kMaxKeys];
   int64_t key_data_len[kMaxKeys] = {0};
   DevBuf uda_out[kMaxUdas];     // 8 B per group (QUANTILES: 7 doubles per group)
+  DevBuf states;                // emit_states: state_rec bytes per group (Serialize layout)
   // Forget the result; device buffers stay allocated for the next finalize.
   void Clear() {
     n_groups = 0;
@@ -29,6 +30,8 @@ struct Agg {
   int32_t n_keys = 0, n_udas = 0, n_vals = 0;
   bool windowed = false;
   bool has_filter = false;
+  bool emit_states = false;  // partial_agg && !finalize_results: result = groups + states
+  int32_t state_rec = 0;
   // Keys for the consume fast path (AggConsumeFastKernel<fast_nk>); 0 = generic kernel.
   int32_t fast_nk = 0;
   std::vector<int32_t> uda_kind, uda_arg_type, uda_val, uda_out_type;

@@ -14,8 +14,8 @@ namespace pxg {
 
 constexpr int kMaxCols = 16;
 constexpr int kMaxKeys = 4;
-constexpr int kMaxUdas = 8;
-constexpr int kMaxVals = 8;  // distinct staged value streams
+constexpr int kMaxUdas = 16;
+constexpr int kMaxVals = 16;  // distinct staged value streams (a split-agg merge of 9 UDAs reads 11)
 constexpr int kChunkShift = 24;
 constexpr int64_t kChunkRows = int64_t(1) << kChunkShift;
 constexpr int kWave = 64;
@@ -297,6 +297,16 @@ __device__ inline Val EvalProgram(const DevProgram* __restrict__ p, const DevChu
       case PXG_OP_INV_I: st[sp - 1].a = ~st[sp - 1].a; break;
       case PXG_OP_NEG_F: st[sp - 1].a = st[sp - 1].a ^ 0x8000000000000000ULL; break;
       case PXG_OP_NOT: st[sp - 1].a = st[sp - 1].a == 0; break;
+      case PXG_OP_STATE_WORD: {  // UDA::Deserialize of one state word (udf.h:98-100)
+        const DevCol& c = ch.cols[in.arg];
+        const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
+        uint64_t w = 0;
+        if (static_cast<int64_t>(o1 - o0) >= in.imm + 8) __builtin_memcpy(&w, c.data + o0 + in.imm, 8);
+        st[sp].a = w;
+        st[sp].b = 0;
+        ++sp;
+        break;
+      }
       case PXG_OP_EQ_U: --sp; st[sp - 1].a = (st[sp - 1].a == st[sp].a) && (st[sp - 1].b == st[sp].b); st[sp - 1].b = 0; break;
       case PXG_OP_NE_U: --sp; st[sp - 1].a = !((st[sp - 1].a == st[sp].a) && (st[sp - 1].b == st[sp].b)); st[sp - 1].b = 0; break;
       default:

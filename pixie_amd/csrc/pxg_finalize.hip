@@ -252,7 +252,18 @@ __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __res
     if (kind == PXG_UDA_COUNT || kind == PXG_UDA_QUANTILES) continue;
     const uint64_t* v = vals.p[vi];
     uint64_t r = 0;
-    if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
+    if (kind == PXG_UDA_MEAN_MERGE) {  // MeanUDA::Merge: sizes into the second partial row
+      const uint64_t* sz = vals.p[plan->uda_val2[u]];
+      double acc = 0;
+      uint64_t n = 0;
+      for (uint32_t i = s + lane; i < e; i += 64) {
+        acc += AsF(v[i]);
+        n += sz[i];
+      }
+      r = FBits(WaveSumF64(acc));
+      n = WaveSumU64(n);
+      if (lane == 0) partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
+    } else if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
       if (at == PXG_FLOAT64) {
         double acc = 0;
         for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
@@ -293,10 +304,11 @@ __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __res
   }
 }
 
-// UDA Finalize per group (math_ops.h: CountUDA/SumUDA/MeanUDA/MinUDA/MaxUDA).
+// UDA Finalize per group (math_ops.h: CountUDA/SumUDA/MeanUDA/MinUDA/MaxUDA).  With
+// plan->emit_states every group's states are also written in Serialize() layout (partial agg).
 __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
                                    const uint32_t* __restrict__ cbase, uint32_t ngroups, const uint64_t* __restrict__ partial,
-                                   uint64_t pstride, UdaOut out) {
+                                   uint64_t pstride, UdaOut out, uint8_t* __restrict__ states) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngroups) return;
   const uint64_t cnt = gstart[g + 1] - gstart[g];
@@ -324,6 +336,22 @@ __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const ui
         double acc = 0;
         for (uint32_t c = c0; c < c1; ++c) acc += AsF(p[c]);
         r = FBits(acc / static_cast<double>(cnt));
+        if (states) {  // MeanInfo {uint64 size; double count} (math_ops.h:621-624)
+          uint64_t* st = reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]);
+          st[0] = cnt;
+          st[1] = FBits(acc);
+        }
+        break;
+      }
+      case PXG_UDA_MEAN_MERGE: {
+        const uint64_t* pn = partial + static_cast<uint64_t>(plan->n_udas + u) * pstride;
+        double acc = 0;
+        uint64_t n = 0;
+        for (uint32_t c = c0; c < c1; ++c) {
+          acc += AsF(p[c]);
+          n += pn[c];
+        }
+        r = FBits(acc / static_cast<double>(n));
         break;
       }
       case PXG_UDA_MAX: {
@@ -341,6 +369,9 @@ __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const ui
       default: continue;  // QUANTILES: digest kernels
     }
     out.p[u][g] = r;
+    // count, sum, min, max: the state is the finalized 8-byte value (math_ops.h:602-757).
+    if (states && kind != PXG_UDA_MEAN)
+      *reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]) = r;
   }
 }
 
@@ -1150,14 +1181,19 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "group_chunk_count", GroupChunkCountKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
                                ngroups, cbase));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
-    PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 8));
+    PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 2 * 8));
     PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceKernel, dim3(static_cast<unsigned>((max_chunks * 64 + 255) / 256)), dim3(256), 0,
                                a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups, cv,
                                ws.partial.as<uint64_t>(), max_chunks));
   }
+  uint8_t* states = nullptr;
+  if (a->emit_states && a->state_rec > 0) {
+    PXG_RETURN_IF_ERROR(R.states.Ensure(static_cast<size_t>(ngroups) * a->state_rec + 16));
+    states = R.states.as<uint8_t>();
+  }
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                              a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups,
-                             ws.partial.as<const uint64_t>(), max_chunks, uo));
+                             ws.partial.as<const uint64_t>(), max_chunks, uo, states));
   // 4. Quantile digests.
   if (any_q) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
@@ -1309,11 +1345,35 @@ extern "C" int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups) {
   return PXG_OK;
 }
 
+// Finalize() of a freshly initialised UDA (math_ops.h:583-772): count 0, sum 0, mean 0/0 = NaN,
+// min numeric_limits<T>::max(), max numeric_limits<T>::min(), minsum its init arg.
+static uint64_t InitialFinalValue(int kind, int at, int64_t init) {
+  double d = 0;
+  uint64_t bits = 0;
+  switch (kind) {
+    case PXG_UDA_MINSUM: return static_cast<uint64_t>(init);
+    case PXG_UDA_MEAN:
+    case PXG_UDA_MEAN_MERGE: d = std::nan(""); std::memcpy(&bits, &d, 8); return bits;
+    case PXG_UDA_MAX:
+      if (at != PXG_FLOAT64) return static_cast<uint64_t>(INT64_MIN);
+      d = 2.2250738585072014e-308;
+      std::memcpy(&bits, &d, 8);
+      return bits;
+    case PXG_UDA_MIN:
+      if (at != PXG_FLOAT64) return static_cast<uint64_t>(INT64_MAX);
+      d = 1.7976931348623157e+308;
+      std::memcpy(&bits, &d, 8);
+      return bits;
+    default: return 0;  // COUNT, SUM (0 and +0.0 share their bits)
+  }
+}
+
 extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols) {
   if (!agg || !cols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   Agg& a = agg->impl;
   if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
-  if (n_cols != a.n_keys + a.n_udas) return SetError(PXG_INVALID_ARGUMENT, "expected %d result columns", a.n_keys + a.n_udas);
+  const int32_t n_val_cols = a.emit_states ? 1 : a.n_udas;
+  if (n_cols != a.n_keys + n_val_cols) return SetError(PXG_INVALID_ARGUMENT, "expected %d result columns", a.n_keys + n_val_cols);
   const int64_t G = a.res.n_groups;
   const bool synth = a.n_keys == 0 && G == 0;  // AggregateGroupByNone over no rows
   const int64_t rows = synth ? 1 : G;
@@ -1344,6 +1404,32 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
       }
     }
   }
+  if (a.emit_states) {  // serialized_expressions: fixed-size records (operators.cc:251-257)
+    pxg_column_out& o = cols[a.n_keys];
+    o.type = PXG_STRING;
+    o.length = rows;
+    const int64_t rec = a.state_rec;
+    o.offsets = static_cast<int32_t*>(std::malloc((rows + 1) * 4));
+    o.data = static_cast<uint8_t*>(std::malloc(rows * rec + 16));
+    o.data_len = rows * rec;
+    for (int64_t g = 0; g <= rows; ++g) o.offsets[g] = static_cast<int32_t>(g * rec);
+    if (!synth) {
+      if (G > 0 && rec > 0) PXG_HIP(hipMemcpy(o.data, a.res.states.p, G * rec, hipMemcpyDeviceToHost));
+    } else {
+      // Initial states serialized (no-groups agg over zero rows): Mean {0, 0.0}, the rest as
+      // their initial value.
+      for (int u = 0; u < a.n_udas; ++u) {
+        uint8_t* st = o.data + a.hplan.state_off[u];
+        if (a.uda_kind[u] == PXG_UDA_MEAN) {
+          std::memset(st, 0, 16);
+        } else {
+          const uint64_t v = InitialFinalValue(a.uda_kind[u], a.uda_arg_type[u], a.uda_init[u]);
+          std::memcpy(st, &v, 8);
+        }
+      }
+    }
+    return PXG_OK;
+  }
   for (int u = 0; u < a.n_udas; ++u) {
     pxg_column_out& o = cols[a.n_keys + u];
     o.type = a.uda_out_type[u];
@@ -1357,22 +1443,10 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
     }
     // Initial UDA states finalized (AggNode no-groups emit over zero rows, agg_node.cc:182-207).
     uint64_t* p = static_cast<uint64_t*>(o.values);
-    const int at = a.uda_arg_type[u];
-    switch (a.uda_kind[u]) {
-      case PXG_UDA_COUNT: p[0] = 0; break;
-      case PXG_UDA_SUM: { double z = 0; p[0] = at == PXG_FLOAT64 ? *reinterpret_cast<uint64_t*>(&z) : 0; break; }
-      case PXG_UDA_MINSUM: p[0] = static_cast<uint64_t>(a.uda_init[u]); break;
-      case PXG_UDA_MEAN: { double nan = std::nan(""); std::memcpy(p, &nan, 8); break; }
-      case PXG_UDA_MAX:
-        if (at == PXG_FLOAT64) { double d = 2.2250738585072014e-308; std::memcpy(p, &d, 8); }
-        else p[0] = static_cast<uint64_t>(INT64_MIN);
-        break;
-      case PXG_UDA_MIN:
-        if (at == PXG_FLOAT64) { double d = 1.7976931348623157e+308; std::memcpy(p, &d, 8); }
-        else p[0] = static_cast<uint64_t>(INT64_MAX);
-        break;
-      case PXG_UDA_QUANTILES: for (int j = 0; j < 7; ++j) { double nan = std::nan(""); std::memcpy(p + j, &nan, 8); } break;
-      default: break;
+    if (q) {
+      for (int j = 0; j < 7; ++j) { double nan = std::nan(""); std::memcpy(p + j, &nan, 8); }
+    } else {
+      p[0] = InitialFinalValue(a.uda_kind[u], a.uda_arg_type[u], a.uda_init[u]);
     }
   }
   return PXG_OK;

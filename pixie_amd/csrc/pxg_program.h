@@ -32,6 +32,14 @@ inline int32_t CompileProgram(const pxg_program& in, const int32_t* col_types, i
           return SetError(PXG_INVALID_ARGUMENT, "column %d has type %d, program expects %d", x.arg, col_types[x.arg], x.type);
         st.push_back(x.type);
         break;
+      case PXG_OP_STATE_WORD:
+        if (x.arg < 0 || x.arg >= ncols) return SetError(PXG_INVALID_ARGUMENT, "column %d out of range", x.arg);
+        if (col_types && col_types[x.arg] != PXG_STRING)
+          return SetError(PXG_INVALID_ARGUMENT, "state word of column %d, which is not STRING", x.arg);
+        if (x.imm < 0 || !(x.type == PXG_INT64 || x.type == PXG_TIME64NS || x.type == PXG_FLOAT64))
+          return SetError(PXG_INVALID_ARGUMENT, "bad state word (offset %lld, type %d)", (long long)x.imm, x.type);
+        st.push_back(x.type);
+        break;
       case PXG_OP_CONST:
         if ((x.type == PXG_STRING || x.type == PXG_UINT128) &&
             (x.arg < 0 || x.arg + (x.type == PXG_UINT128 ? 16 : x.imm) > in.pool_len || x.imm < 0))

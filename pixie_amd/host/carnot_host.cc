@@ -733,6 +733,14 @@ class GpuAggNode : public ExecNode {
   };
   std::vector<Uda> udas;
   bool windowed = false;
+  // Split aggregation (plan.proto:250-257).  emit_states (partial_agg && !finalize_results):
+  // the output is the groups + serialized_expressions (operators.cc:251-257).  merge_states
+  // (!partial_agg && finalize_results): the input's last column is serialized_expressions; the
+  // device reads each UDA state word (PXG_OP_STATE_WORD) and merges: count/sum as SUM, min/max
+  // as MIN/MAX, mean as MEAN_MERGE (UDA::Merge semantics, math_ops.h:583-772).
+  bool emit_states = false, merge_states = false;
+  int64_t state_col = -1;
+  int64_t state_rec = 0;
 
  protected:
   Status InitImpl(const planpb::Operator& op) override {
@@ -740,11 +748,14 @@ class GpuAggNode : public ExecNode {
     if (env.empty()) env = ColumnEnv(inputs_[0]);
     if (source_types.empty()) source_types = inputs_[0];
     windowed = a.windowed;
+    emit_states = a.partial_agg && !a.finalize_results;
+    merge_states = !a.partial_agg && a.finalize_results;
     ExprCompiler comp(env);
     for (auto& g : a.groups) {
       if (g.index >= env.size()) return Err(PXG_INVALID_ARGUMENT, "group column %llu out of range", (unsigned long long)g.index);
       keys.push_back(env[g.index]);
     }
+    if (merge_states) return InitMerge(a);
     for (auto& v : a.values) {  // AggregateExpression -> registry (registry_arg_types = init ++ args)
       std::vector<Program> args(v.args.size());
       std::vector<int32_t> types;
@@ -769,9 +780,72 @@ class GpuAggNode : public ExecNode {
       if (!args.empty()) { u.arg = args[0]; u.has_arg = true; }
       if (args.size() > 1 && u.kind != PXG_UDA_COUNT) { u.arg2 = args[1]; u.has_arg2 = true; }
       if (!v.init_args.empty()) { u.has_init = true; u.init = v.init_args[0].int64_value; }
+      if (emit_states && !(u.kind == PXG_UDA_COUNT || u.kind == PXG_UDA_SUM || u.kind == PXG_UDA_MEAN || u.kind == PXG_UDA_MIN || u.kind == PXG_UDA_MAX))
+        return Err(PXG_UNIMPLEMENTED, "UDA %s has no Serialize: it does not support partial aggregation", v.name.c_str());
       udas.push_back(u);
     }
-    if (output_.size() != keys.size() + udas.size())  // agg_node.cc:109-112
+    const size_t nv = emit_states ? 1 : udas.size();
+    if (output_.size() != keys.size() + nv)  // agg_node.cc:109-112, operators.cc:251-257
+      return Err(PXG_INVALID_ARGUMENT, "output relation arity %zu != groups + values %zu", output_.size(), keys.size() + nv);
+    return Status::OK();
+  }
+  // The finalize half of a split aggregate: UDAs resolved by (name, args_data_types); each
+  // UDA's state is read from its offset in the serialized_expressions records.
+  Status InitMerge(const planpb::AggregateOperator& a) {
+    state_col = static_cast<int64_t>(env.size()) - 1;
+    if (state_col < 0 || env[state_col].result_type != S || !env[state_col].IsColumn())
+      return Err(PXG_INVALID_ARGUMENT, "finalize agg input must end in the serialized_expressions STRING column");
+    for (auto& g : a.groups)
+      if (static_cast<int64_t>(g.index) == state_col) return Err(PXG_INVALID_ARGUMENT, "serialized_expressions cannot be a group");
+    const int32_t col = env[state_col].insns[0].arg;
+    auto word = [col](int32_t type, int64_t off) {
+      Program p;
+      p.insns.push_back(Insn(PXG_OP_STATE_WORD, type, col, off));
+      p.result_type = type;
+      return p;
+    };
+    int64_t off = 0;
+    for (auto& v : a.values) {
+      std::vector<int32_t> types;
+      for (auto& ia : v.init_args) types.push_back(ia.data_type);
+      if (v.args_data_types.size() != v.args.size()) return Err(PXG_INVALID_ARGUMENT, "finalize agg %s needs args_data_types", v.name.c_str());
+      for (auto t : v.args_data_types) types.push_back(t);
+      auto* d = GetRegistry().GetUDA(v.name, types);
+      if (!d) return Err(PXG_NOT_FOUND, "no device UDA %s", Signature(v.name, types).c_str());
+      const int32_t kind = std::get<0>(*d), out = std::get<2>(*d);
+      Uda u;
+      u.out_type = out;
+      u.has_arg = true;
+      switch (kind) {
+        case PXG_UDA_COUNT:  // CountUDA state: uint64 count, merged by addition
+        case PXG_UDA_SUM:    // SumUDA state: the running sum (INT64 for BOOLEAN/INT64 args)
+          u.kind = PXG_UDA_SUM;
+          u.arg_type = out;
+          u.arg = word(out, off);
+          off += 8;
+          break;
+        case PXG_UDA_MIN:
+        case PXG_UDA_MAX:
+          u.kind = kind;
+          u.arg_type = out;
+          u.arg = word(out, off);
+          off += 8;
+          break;
+        case PXG_UDA_MEAN:  // MeanInfo {uint64 size; double count}
+          u.kind = PXG_UDA_MEAN_MERGE;
+          u.arg_type = F;
+          u.arg = word(F, off + 8);
+          u.arg2 = word(I, off);
+          u.has_arg2 = true;
+          off += 16;
+          break;
+        default:
+          return Err(PXG_UNIMPLEMENTED, "UDA %s has no Deserialize: it does not support partial aggregation", v.name.c_str());
+      }
+      udas.push_back(u);
+    }
+    state_rec = off;
+    if (output_.size() != keys.size() + udas.size())
       return Err(PXG_INVALID_ARGUMENT, "output relation arity %zu != groups + values %zu", output_.size(), keys.size() + udas.size());
     return Status::OK();
   }
@@ -807,6 +881,12 @@ class GpuAggNode : public ExecNode {
   Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
     // Tiny batches are coalesced by the table's staging before they reach HBM.
     if (rb.num_rows > 0) {
+      if (merge_states) {  // every record is exactly the UDAs' Serialize() bytes
+        const HostColumn& sc = rb.cols.at(static_cast<size_t>(state_col));
+        for (int64_t r = 0; r < rb.num_rows; ++r)
+          if (sc.offsets[r + 1] - sc.offsets[r] != state_rec)
+            return Err(PXG_INVALID_ARGUMENT, "serialized_expressions of %d bytes, expected %lld", sc.offsets[r + 1] - sc.offsets[r], (long long)state_rec);
+      }
       std::vector<pxg_column_view> v;
       for (auto& c : rb.cols) v.push_back(c.View());
       PXG_CALL(pxg_table_append(staging_, v.data(), rb.num_rows));
@@ -839,13 +919,13 @@ class GpuAggNode : public ExecNode {
     PXG_CALL(pxg_agg_finalize(agg_, &groups));
     if (hints_) (*hints_)[HintKey()] = std::max<int64_t>(groups, 1);
     clk.Mark("agg finalize");
-    std::vector<pxg_column_out> out(keys.size() + udas.size());
+    std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
     PXG_CALL(pxg_agg_result(agg_, out.data(), static_cast<int32_t>(out.size())));
     clk.Mark("agg result D2H");
     RowBatch ob;
     ob.num_rows = out.empty() ? 0 : out[0].length;
     for (size_t c = 0; c < out.size(); ++c) {
-      const bool q = c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
+      const bool q = !emit_states && c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
       HostColumn hc = FromOut(out[c]);
       if (q) {  // QuantilesUDA::Finalize JSON (math_sketches.h:40-54) from the 7 device doubles
         quantiles_raw_[c] = hc;
@@ -897,6 +977,7 @@ class GpuAggNode : public ExecNode {
     spec.filter = has_filter ? &fp : nullptr;
     spec.expected_groups = expected_groups_;
     spec.windowed = windowed ? 1 : 0;
+    spec.emit_states = emit_states ? 1 : 0;
     PXG_CALL(pxg_agg_create(ctx, &spec, &agg_));
     return Status::OK();
   }
@@ -925,7 +1006,7 @@ class GpuAggNode : public ExecNode {
       if (u.has_arg2) add(u.arg2);
     }
     if (has_filter) add(filter);
-    return k + (windowed ? "W" : "B");
+    return k + (windowed ? "W" : "B") + (emit_states ? "S" : "");
   }
   static constexpr size_t kAggCacheMax = 8;
   pxg_agg* agg_ = nullptr;
@@ -1449,10 +1530,17 @@ class ExecutionGraph {
       }
       out.push_back(env[g.index].result_type);
     }
+    if (op.agg.partial_agg && !op.agg.finalize_results) {  // operators.cc:251-257
+      out.push_back(S);
+      return out;
+    }
+    const bool merge = !op.agg.partial_agg && op.agg.finalize_results;
     for (auto& v : op.agg.values) {
       std::vector<int32_t> types;
       for (auto& ia : v.init_args) types.push_back(ia.data_type);
+      if (merge) types.insert(types.end(), v.args_data_types.begin(), v.args_data_types.end());
       for (auto& a : v.args) {
+        if (merge) break;
         if (a.is_column) {
           if (a.column.index >= env.size()) {
             *st = Err(PXG_INVALID_ARGUMENT, "aggregate argument column out of range");

@@ -90,7 +90,7 @@ def map_op(exprs: Sequence, names: Sequence[str]):
 
 
 def agg_op(groups: Sequence[int], values: Sequence, group_names: Sequence[str] = (), value_names: Sequence[str] = (),
-           windowed: bool = False, node: int = 0):
+           windowed: bool = False, node: int = 0, partial_agg: bool = False, finalize_results: bool = False):
     op = planpb.Operator()
     op.op_type = 2100
     for g in groups:
@@ -102,6 +102,8 @@ def agg_op(groups: Sequence[int], values: Sequence, group_names: Sequence[str] =
     op.agg_op.group_names.extend(group_names or [f"g{i}" for i in range(len(groups))])
     op.agg_op.value_names.extend(value_names or [f"v{i}" for i in range(len(values))])
     op.agg_op.windowed = windowed
+    op.agg_op.partial_agg = partial_agg
+    op.agg_op.finalize_results = finalize_results
     return op
 
 
@@ -269,3 +271,49 @@ def c5_plan(conn: str = "conn_stats", pods: str = "pod_metadata", window_ns: int
                    names=["time_", "pod", "namespace", "remote_addr", "bytes_sent", "bytes_recv"])
     return dag_plan([(1, src, []), (2, mp, [1]), (3, agg, [2]), (4, psrc, []), (5, join, [3, 4]),
                      (6, sink_op("output"), [5])])
+
+
+# Split aggregation: the PEM-side partial agg and the Kelvin-side
+# finalize agg the distributed splitter makes of one blocking agg
+# (partial_op_mgr.cc:47-83: CreatePrepareOperator sets partial_agg, CreateMergeOperator keeps
+# the pre-split values and sets finalize_results; the partial output relation is the groups +
+# serialized_expressions, operators.cc:251-257).
+SPLIT_SRC_COLS = ["pod", "remote_addr", "resp_status", "latency", "resp_body_size"]
+
+
+def split_values():
+    """Every splittable UDA signature on the path: count, mean/sum/min/max over INT64 columns and
+    over a FLOAT64 map result.  Input columns (after the map): 0 pod, 1 remote_addr, 2 latency,
+    3 resp_body_size, 4 latency_ms."""
+    return [agg_expr("count", [col(2)], [INT64]), agg_expr("mean", [col(2)], [INT64], fid=1),
+            agg_expr("sum", [col(3)], [INT64], fid=2), agg_expr("min", [col(2)], [INT64], fid=3),
+            agg_expr("max", [col(2)], [INT64], fid=4), agg_expr("mean", [col(4)], [FLOAT64], fid=5),
+            agg_expr("sum", [col(4)], [FLOAT64], fid=6), agg_expr("min", [col(4)], [FLOAT64], fid=7),
+            agg_expr("max", [col(4)], [FLOAT64], fid=8)]
+
+
+def split_source_plan(table: str = "http_events", groups: Sequence[int] = (0, 1), values=None,
+                      partial_agg: bool = True, finalize_results: bool = False, sink: str = "partial"):
+    """Filter(resp_status >= 400) -> Map(+ latency_ms) -> Agg(groups, values) with the given
+    split flags (True/False: the PEM half; False/False or True/True: a full aggregate)."""
+    values = split_values() if values is None else values
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES, [HE[n] for n in SPLIT_SRC_COLS])
+    flt = filter_op(func("greaterThanEqual", [col(2), const(INT64, 400)], [INT64, INT64]), [0, 1, 3, 4])
+    mp = map_op([col(0), col(1), col(2), col(3), func("divide", [col(2), const(FLOAT64, 1e6)], [INT64, FLOAT64])],
+                ["pod", "remote_addr", "latency", "resp_body_size", "latency_ms"])
+    agg = agg_op(list(groups), values, [SPLIT_SRC_COLS[g] for g in groups], [f"v{i}" for i in range(len(values))],
+                 partial_agg=partial_agg, finalize_results=finalize_results)
+    return linear_plan([src, flt, mp, agg, sink_op(sink)])
+
+
+def split_merge_plan(partials: str, group_types: Sequence[int], values=None, sink: str = "output"):
+    """The finalize half: MemorySource over the partial outputs (groups + serialized_expressions)
+    -> Agg(partial_agg=False, finalize_results=True) with the pre-split values."""
+    values = split_values() if values is None else values
+    ng = len(group_types)
+    types = list(group_types) + [STRING]
+    names = [f"g{i}" for i in range(ng)] + ["serialized_expressions"]
+    src = source_op(partials, types, names, list(range(ng + 1)))
+    agg = agg_op(list(range(ng)), values, names[:ng], [f"v{i}" for i in range(len(values))],
+                 partial_agg=False, finalize_results=True)
+    return linear_plan([src, agg, sink_op(sink)])
