@@ -183,6 +183,9 @@ int32_t pxg_ctx_set_profiling(pxg_ctx* ctx, int32_t enabled);
 int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* kernel_name, int64_t* launches,
                              double* total_ms);
 int32_t pxg_ctx_reset_stats(pxg_ctx* ctx);
+/* Restrict profiling to launches of one kernel (NULL: every kernel), so a timed region pays
+ * the event bracketing only where a launch duration is wanted. */
+int32_t pxg_ctx_profile_only(pxg_ctx* ctx, const char* kernel_name);
 
 /* A table: ncols typed columns, stored as device chunks of <= 2^24 rows (STRING payload
  * < 2^31 bytes per chunk).  Appends coalesce small RowBatches through a pinned staging buffer

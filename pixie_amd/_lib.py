@@ -72,7 +72,7 @@ class JoinSpec(C.Structure):
 # Every symbol include/pxg.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pxg_abi_version", "pxg_last_error", "pxg_device_count", "pxg_ctx_create", "pxg_ctx_destroy",
-    "pxg_ctx_sync", "pxg_ctx_stream", "pxg_ctx_set_profiling", "pxg_ctx_kernel_stats",
+    "pxg_ctx_sync", "pxg_ctx_stream", "pxg_ctx_set_profiling", "pxg_ctx_profile_only", "pxg_ctx_kernel_stats",
     "pxg_ctx_reset_stats", "pxg_table_create", "pxg_table_destroy", "pxg_table_append",
     "pxg_table_append_device", "pxg_table_flush", "pxg_table_num_rows", "pxg_table_num_chunks",
     "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_map", "pxg_agg_create",
@@ -115,6 +115,7 @@ def load() -> C.CDLL:
         "pxg_ctx_sync": (i32, [vp]),
         "pxg_ctx_stream": (vp, [vp]),
         "pxg_ctx_set_profiling": (i32, [vp, i32]),
+        "pxg_ctx_profile_only": (i32, [vp, C.c_char_p]),
         "pxg_ctx_kernel_stats": (i32, [vp, C.c_char_p, p(i64), p(C.c_double)]),
         "pxg_ctx_reset_stats": (i32, [vp]),
         "pxg_table_create": (i32, [vp, i32, p(i32), p(vp)]),

@@ -101,6 +101,7 @@ struct Ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool profiling = false;
+  std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
@@ -118,7 +119,8 @@ inline int32_t LaunchOn(Ctx* ctx, hipStream_t stream, const char* name, void (*k
                         size_t shmem, Args&&... args) {
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return PXG_OK;
   hipEvent_t s0 = nullptr, s1 = nullptr;
-  if (ctx->profiling) {
+  const bool timed = ctx->profiling && (ctx->profile_only.empty() || ctx->profile_only == name);
+  if (timed) {
     s0 = ctx->GetEvent();
     s1 = ctx->GetEvent();
     (void)hipEventRecord(s0, stream);
@@ -126,7 +128,7 @@ inline int32_t LaunchOn(Ctx* ctx, hipStream_t stream, const char* name, void (*k
   hipLaunchKernelGGL(kernel, grid, block, shmem, stream, std::forward<Args>(args)...);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return SetError(PXG_INTERNAL, "launch %s failed: %s", name, hipGetErrorString(e));
-  if (ctx->profiling) {
+  if (timed) {
     (void)hipEventRecord(s1, stream);
     ctx->pending.push_back(PendingTiming{name, s0, s1});
   }

@@ -292,6 +292,12 @@ extern "C" int32_t pxg_ctx_set_profiling(pxg_ctx* ctx, int32_t enabled) {
   return PXG_OK;
 }
 
+extern "C" int32_t pxg_ctx_profile_only(pxg_ctx* ctx, const char* kernel_name) {
+  if (!ctx) return SetError(PXG_INVALID_ARGUMENT, "ctx is null");
+  ctx->impl.profile_only = kernel_name ? kernel_name : "";
+  return PXG_OK;
+}
+
 extern "C" int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* name, int64_t* launches, double* total_ms) {
   if (!ctx || !name) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   PXG_RETURN_IF_ERROR(ctx->impl.ResolveTimings());

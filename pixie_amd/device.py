@@ -117,7 +117,9 @@ class Ctx:
     def sync(self) -> None:
         check(self.lib.pxg_ctx_sync(self.h))
 
-    def set_profiling(self, on: bool) -> None:
+    def set_profiling(self, on: bool, only: str = None) -> None:
+        """Time kernel launches with HIP events on the ctx stream (only: one kernel name)."""
+        check(self.lib.pxg_ctx_profile_only(self.h, only.encode() if only else None))
         check(self.lib.pxg_ctx_set_profiling(self.h, 1 if on else 0))
 
     def kernel_stats(self, name: str):
