@@ -56,6 +56,33 @@ int32_t pxc_engine_destroy(pxc_engine* engine);
 int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                          const pxc_table* tables, uint8_t** out, int64_t* out_len);
 
+/* RowBatches for one GRPCSourceOperator node (grpc_source_node.cc:52-87), as the
+ * schemapb.RowBatchData payloads of the TransferResultChunkRequests it received, in order. */
+typedef struct {
+  uint64_t grpc_source_id;  /* the GRPCSource's plan node id (GRPCSinkOperator.grpc_source_id) */
+  int32_t nmessages;
+  int32_t reserved;
+  const uint8_t* const* messages;
+  const int64_t* lengths;
+} pxc_grpc_input;
+
+/* pxc_execute_plan for fragments with GRPC sources / sinks (the PEM -> Kelvin hop,
+ * grpc_sink_node.cc:276-330).  GRPC sources read `inputs`; every GRPCSinkOperator whose
+ * destination is a grpc_source_id serialises its RowBatches (split at the reference's 1 MiB
+ * request limit) as schemapb.RowBatchData into *grpc_out: "PXGS" u32 magic, u32 nsinks, then
+ * per sink u64 destination id, u32 nmessages, (u32 length, bytes)*.  Released with pxc_free.
+ * Sinks to a result table are returned in *out as by pxc_execute_plan. */
+int32_t pxc_execute_plan_grpc(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                              const pxc_table* tables, int32_t ninputs, const pxc_grpc_input* inputs, uint8_t** out,
+                              int64_t* out_len, uint8_t** grpc_out, int64_t* grpc_out_len);
+
+/* RowBatch::ToProto / FromProto (src/table_store/schema/row_batch.cc:161-224): one RowBatch of
+ * host Arrow-layout columns <-> schemapb.RowBatchData wire bytes (the canonical proto3
+ * encoding).  from_proto returns the batch in PXRB layout (one sink "rowbatch", one batch). */
+int32_t pxc_rowbatch_to_proto(int32_t ncols, const pxg_column_view* cols, int64_t nrows, int32_t eow, int32_t eos,
+                              uint8_t** out, int64_t* out_len);
+int32_t pxc_rowbatch_from_proto(const uint8_t* msg, int64_t len, uint8_t** out, int64_t* out_len);
+
 /* Lowering only (no device): a text description of the node graph and device programs. */
 int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables,
                          char** out);

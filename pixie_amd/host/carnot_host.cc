@@ -221,6 +221,243 @@ struct UdfDef {
 
 enum : int32_t { B = PXG_BOOLEAN, I = PXG_INT64, U = PXG_UINT128, F = PXG_FLOAT64, S = PXG_STRING, T = PXG_TIME64NS };
 
+// ---------------------------------------------------------------------------------------
+// schemapb.RowBatchData wire codec: RowBatch::ToProto / FromProto (row_batch.cc:161-224,
+// schema.proto:31-79).  One Column message per column, its data in the typed oneof
+// (1 boolean, 2 int64, 3 uint128, 4 time64ns, 5 float64, 6 string); repeated scalars packed
+// (proto3), UInt128 {low = 1, high = 2}; num_rows = 2, eow = 3, eos = 4.  The encoding is the
+// canonical one protobuf emits (fields in number order, proto3 defaults omitted).
+// ---------------------------------------------------------------------------------------
+struct PbOut {
+  std::string b;
+  void Varint(uint64_t v) {
+    while (v >= 0x80) {
+      b.push_back(static_cast<char>((v & 0x7F) | 0x80));
+      v >>= 7;
+    }
+    b.push_back(static_cast<char>(v));
+  }
+  void Key(uint32_t field, uint32_t wire) { Varint((static_cast<uint64_t>(field) << 3) | wire); }
+  void Len(uint32_t field, const std::string& body) {
+    Key(field, 2);
+    Varint(body.size());
+    b += body;
+  }
+};
+
+static int32_t PbFieldOfType(int32_t t) {
+  switch (t) {
+    case B: return 1;
+    case I: return 2;
+    case U: return 3;
+    case T: return 4;
+    case F: return 5;
+    case S: return 6;
+    default: return 0;
+  }
+}
+
+// Rows [r0, r0 + n) of one column as a schemapb.Column message body.
+static std::string EncodePbColumn(const HostColumn& c, int64_t r0, int64_t n) {
+  PbOut data;  // the XxxColumn message
+  if (n > 0) {
+    PbOut packed;
+    switch (c.type) {
+      case B:
+        for (int64_t r = r0; r < r0 + n; ++r) packed.Varint(static_cast<const uint8_t*>(c.values)[r] ? 1 : 0);
+        data.Len(1, packed.b);
+        break;
+      case I:
+      case T:
+        for (int64_t r = r0; r < r0 + n; ++r) packed.Varint(static_cast<uint64_t>(static_cast<const int64_t*>(c.values)[r]));
+        data.Len(1, packed.b);
+        break;
+      case F:
+        packed.b.assign(reinterpret_cast<const char*>(static_cast<const double*>(c.values) + r0), static_cast<size_t>(n) * 8);
+        data.Len(1, packed.b);
+        break;
+      case U:
+        for (int64_t r = r0; r < r0 + n; ++r) {
+          const uint64_t* v = static_cast<const uint64_t*>(c.values) + 2 * r;
+          PbOut u;
+          if (v[0]) { u.Key(1, 0); u.Varint(v[0]); }
+          if (v[1]) { u.Key(2, 0); u.Varint(v[1]); }
+          data.Len(1, u.b);
+        }
+        break;
+      case S:
+        for (int64_t r = r0; r < r0 + n; ++r) {
+          data.Key(1, 2);
+          const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
+          data.Varint(static_cast<uint64_t>(o1 - o0));
+          data.b.append(reinterpret_cast<const char*>(c.data) + o0, static_cast<size_t>(o1 - o0));
+        }
+        break;
+      default: break;
+    }
+  }
+  PbOut col;
+  col.Len(static_cast<uint32_t>(PbFieldOfType(c.type)), data.b);
+  return col.b;
+}
+
+static std::string EncodeRowBatchData(const RowBatch& rb, int64_t r0, int64_t n, bool eow, bool eos) {
+  PbOut m;
+  for (auto& c : rb.cols) m.Len(1, EncodePbColumn(c, r0, n));
+  if (n) { m.Key(2, 0); m.Varint(static_cast<uint64_t>(n)); }
+  if (eow) { m.Key(3, 0); m.Varint(1); }
+  if (eos) { m.Key(4, 0); m.Varint(1); }
+  return m.b;
+}
+
+static Status DecodeRowBatchData(const uint8_t* p, size_t len, RowBatch* rb) {
+  try {
+    planpb::Reader r(p, len);
+    uint32_t f, w;
+    int64_t num_rows = 0;
+    while (r.Next(&f, &w)) {
+      if (f == 1 && w == 2) {
+        planpb::Reader col = r.Sub();
+        uint32_t cf, cw;
+        int32_t type = 0;
+        auto oc = std::make_shared<OwnedColumn>();
+        int64_t rows = 0;
+        while (col.Next(&cf, &cw)) {
+          if (cw != 2 || cf < 1 || cf > 6) { col.Skip(cw); continue; }
+          static const int32_t kTypeOfField[7] = {0, B, I, U, T, F, S};  // ProtoDataType (row_batch.cc:181-199)
+          type = kTypeOfField[cf];
+          oc->values.clear();
+          oc->offsets.assign(1, 0);
+          oc->data.clear();
+          rows = 0;
+          planpb::Reader d = col.Sub();
+          uint32_t df, dw;
+          while (d.Next(&df, &dw)) {
+            if (df != 1) { d.Skip(dw); continue; }
+            if (type == S) {
+              const std::string v = d.String();
+              oc->data.insert(oc->data.end(), v.begin(), v.end());
+              oc->offsets.push_back(static_cast<int32_t>(oc->data.size()));
+              ++rows;
+            } else if (type == U) {
+              planpb::Reader u = d.Sub();
+              uint64_t lo = 0, hi = 0;
+              uint32_t uf, uw;
+              while (u.Next(&uf, &uw)) {
+                if (uf == 1) lo = u.Varint();
+                else if (uf == 2) hi = u.Varint();
+                else u.Skip(uw);
+              }
+              const size_t at = oc->values.size();
+              oc->values.resize(at + 16);
+              std::memcpy(oc->values.data() + at, &lo, 8);
+              std::memcpy(oc->values.data() + at + 8, &hi, 8);
+              ++rows;
+            } else if (type == F) {
+              auto put = [&](uint64_t bits) {
+                const size_t at = oc->values.size();
+                oc->values.resize(at + 8);
+                std::memcpy(oc->values.data() + at, &bits, 8);
+                ++rows;
+              };
+              if (dw == 2) {
+                planpb::Reader pk = d.Sub();
+                while (!pk.done()) put(pk.Fixed64());
+              } else {
+                put(d.Fixed64());
+              }
+            } else {  // BOOLEAN / INT64 / TIME64NS: varints, packed or not
+              std::vector<uint64_t> vs;
+              d.RepeatedVarint(dw, &vs);
+              for (uint64_t v : vs) {
+                if (type == B) {
+                  oc->values.push_back(v ? 1 : 0);
+                } else {
+                  const size_t at = oc->values.size();
+                  oc->values.resize(at + 8);
+                  std::memcpy(oc->values.data() + at, &v, 8);
+                }
+                ++rows;
+              }
+            }
+          }
+        }
+        if (type == 0) return Err(PXG_INTERNAL, "Received unknown column data type in ProtoDataType");
+        HostColumn hc;
+        hc.type = type;
+        hc.length = rows;
+        oc->values.resize(oc->values.size() + 16);  // keeps every pointer valid for empty columns
+        oc->data.resize(oc->data.size() + 16);
+        hc.values = oc->values.data();
+        hc.offsets = oc->offsets.data();
+        hc.data = oc->data.data();
+        hc.owner = oc;
+        rb->cols.push_back(hc);
+      } else if (f == 2 && w == 0) {
+        num_rows = static_cast<int64_t>(r.Varint());
+      } else if (f == 3 && w == 0) {
+        rb->eow = r.Varint() != 0;
+      } else if (f == 4 && w == 0) {
+        rb->eos = r.Varint() != 0;
+      } else {
+        r.Skip(w);
+      }
+    }
+    rb->num_rows = num_rows;
+    for (auto& c : rb->cols)  // RowBatch::AddColumn (row_batch.cc:39-52)
+      if (c.length != num_rows) return Err(PXG_INVALID_ARGUMENT, "column of %lld rows in a RowBatch of %lld", (long long)c.length, (long long)num_rows);
+  } catch (const planpb::WireError& e) {
+    return Err(PXG_INVALID_ARGUMENT, "RowBatchData: %s", e.what());
+  }
+  return Status::OK();
+}
+
+// Row sizes for the GRPC sink's batch split (GetRowSizes / SplitBatchSizes,
+// grpc_sink_node.cc:216-273): BOOLEAN 1 B, UINT128 16 B, other fixed types 8 B, strings their
+// length; batches above (1 MiB - 16 KiB) * 0.9 are cut (grpc_sink_node.h:43-50).
+static std::vector<int64_t> SplitBatchSizes(const RowBatch& rb) {
+  const float limit = static_cast<float>(static_cast<size_t>(1024 * 1024 - 16 * 1024)) * 0.9f;
+  const int64_t desired = static_cast<int64_t>(limit);
+  int64_t fixed = 0;
+  bool has_str = false;
+  std::vector<int64_t> str(static_cast<size_t>(rb.num_rows), 0);
+  for (auto& c : rb.cols) {
+    if (c.type == S) {
+      has_str = true;
+      for (int64_t r = 0; r < rb.num_rows; ++r) str[r] += c.offsets[r + 1] - c.offsets[r];
+    } else {
+      fixed += c.type == B ? 1 : c.type == U ? 16 : 8;
+    }
+  }
+  int64_t total = fixed * rb.num_rows;
+  for (int64_t v : str) total += v;
+  std::vector<int64_t> out;
+  if (rb.num_rows == 0 || !(static_cast<float>(total) > limit)) {
+    out.push_back(rb.num_rows);
+    return out;
+  }
+  if (has_str) {
+    int64_t bytes = 0, rows = 0;
+    for (int64_t r = 0; r < rb.num_rows; ++r) {
+      const int64_t rowb = str[r] + fixed;
+      if (rows > 0 && bytes + rowb > desired) {
+        out.push_back(rows);
+        bytes = rows = 0;
+      }
+      bytes += rowb;
+      ++rows;
+    }
+    out.push_back(rows);
+  } else {
+    int64_t per = fixed ? desired / fixed : rb.num_rows;
+    if (per == 0) per = 1;
+    const int64_t nb = rb.num_rows / per;
+    out.insert(out.end(), static_cast<size_t>(nb), per);
+    if (rb.num_rows - nb * per > 0) out.push_back(rb.num_rows - nb * per);
+  }
+  return out;
+}
+
 class Registry {
  public:
   Registry() {
@@ -1250,6 +1487,31 @@ class SinkNode : public ExecNode {
   }
 };
 
+// GRPCSinkNode to another Carnot (grpc_sink_node.cc:276-330): every RowBatch, split above the
+// request size limit with the last piece keeping eow / eos, serialised as schemapb.RowBatchData
+// (the TransferResultChunkRequest payload).  The transport is the caller's: the messages are
+// returned per destination GRPC source id (pxc_execute_plan_grpc).
+class GrpcSinkNode : public ExecNode {
+ public:
+  explicit GrpcSinkNode(uint64_t dest) : dest_id(dest) {}
+  std::string DebugString() const override { return "GrpcSinkNode(-> grpc source " + std::to_string(dest_id) + ")"; }
+  uint64_t dest_id;
+  std::vector<std::string> messages;
+
+ protected:
+  Status InitImpl(const planpb::Operator&) override { return Status::OK(); }
+  Status ConsumeNextImpl(ExecState*, const RowBatch& rb, size_t) override {
+    const std::vector<int64_t> sizes = SplitBatchSizes(rb);
+    int64_t r0 = 0;
+    for (size_t i = 0; i < sizes.size(); ++i) {
+      const bool last = i + 1 == sizes.size();
+      messages.push_back(EncodeRowBatchData(rb, r0, sizes[i], last && rb.eow, last && rb.eos));
+      r0 += sizes[i];
+    }
+    return Status::OK();
+  }
+};
+
 // ---------------------------------------------------------------------------------------
 // HBM-resident table store (table_store::TableStore / Table, table.h:71-199).
 // ---------------------------------------------------------------------------------------
@@ -1261,6 +1523,77 @@ struct StoredTable {
   int64_t last_time = std::numeric_limits<int64_t>::min();
 };
 using TableStore = std::map<std::string, StoredTable>;
+
+// UnionNode, unordered (union_node.cc:268-289): every parent's batch is forwarded with its
+// columns picked by the parent's column mapping; eow / eos are set once every parent has sent
+// eos.  A union with a time_ column merges by time in the reference (order_by_time,
+// operators.cc:543): not supported here.
+class UnionNode : public ExecNode {
+ public:
+  std::string DebugString() const override { return "UnionNode(unordered)"; }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    for (auto& n : op.union_names)
+      if (n == "time_") return Err(PXG_UNIMPLEMENTED, "time-ordered Union is not supported");
+    maps_ = op.union_mappings;
+    if (maps_.size() != inputs_.size()) return Err(PXG_INVALID_ARGUMENT, "Union has %zu column mappings for %zu parents", maps_.size(), inputs_.size());
+    for (size_t p = 0; p < maps_.size(); ++p) {
+      if (maps_[p].size() != op.union_names.size()) return Err(PXG_INVALID_ARGUMENT, "Union column mapping %zu has the wrong arity", p);
+      for (size_t c = 0; c < maps_[p].size(); ++c)
+        if (maps_[p][c] < 0 || static_cast<size_t>(maps_[p][c]) >= inputs_[p].size() || inputs_[p][maps_[p][c]] != output_[c])
+          return Err(PXG_INVALID_ARGUMENT, "Union column mapping %zu:%zu is invalid", p, c);
+    }
+    eos_.assign(inputs_.size(), false);
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t parent) override {
+    if (rb.eos) eos_[parent] = true;
+    bool all = true;
+    for (bool e : eos_) all = all && e;
+    RowBatch out;
+    out.num_rows = rb.num_rows;
+    for (int64_t i : maps_[parent]) out.cols.push_back(rb.cols[static_cast<size_t>(i)]);
+    out.eow = out.eos = all;
+    return SendRowBatchToChildren(s, out);
+  }
+
+ private:
+  std::vector<std::vector<int64_t>> maps_;
+  std::vector<bool> eos_;
+};
+
+// GRPCSourceNode (grpc_source_node.cc:52-87): RowBatches received from a remote GRPCSink, in
+// arrival order, as schemapb.RowBatchData messages (RowBatch::FromProto, row_batch.cc:201-224).
+// The source is done once a batch with eos has been sent.
+class GrpcSourceNode : public SourceNode {
+ public:
+  GrpcSourceNode(uint64_t id, const std::vector<std::pair<const uint8_t*, int64_t>>* msgs) : id_(id), msgs_(msgs) {}
+  std::string DebugString() const override { return "GrpcSourceNode(" + std::to_string(id_) + ")"; }
+  bool HasBatchesRemaining() const override { return !sent_eos_; }
+  Status GenerateNext(ExecState* s) override {
+    if (!msgs_ || next_ >= msgs_->size())
+      return Err(PXG_INVALID_ARGUMENT, "GRPC source %llu ran out of row batches before eos", (unsigned long long)id_);
+    RowBatch rb;
+    const auto& m = (*msgs_)[next_++];
+    PXC_RETURN_IF_ERROR(DecodeRowBatchData(m.first, static_cast<size_t>(m.second), &rb));
+    if (rb.cols.size() != output_.size()) return Err(PXG_INVALID_ARGUMENT, "RowBatch of %zu columns for a GRPC source of %zu", rb.cols.size(), output_.size());
+    for (size_t c = 0; c < rb.cols.size(); ++c)
+      if (rb.cols[c].type != output_[c]) return Err(PXG_INVALID_ARGUMENT, "RowBatch column %zu has type %d, the GRPC source declares %d", c, rb.cols[c].type, output_[c]);
+    if (rb.eos && !rb.eow) return Err(PXG_INTERNAL, "Cannot have an eos without an eow");  // exec_node.h:217-220
+    sent_eos_ = rb.eos;
+    return SendRowBatchToChildren(s, rb);
+  }
+
+ protected:
+  Status InitImpl(const planpb::Operator&) override { return Status::OK(); }
+
+ private:
+  uint64_t id_;
+  const std::vector<std::pair<const uint8_t*, int64_t>>* msgs_;
+  size_t next_ = 0;
+  bool sent_eos_ = false;
+};
 
 // MemorySourceNode over a stored device table.  The cursor range comes from start_time /
 // stop_time as in Table::Cursor (table.cc:56-95): [first row with time_ >= start, first row
@@ -1393,6 +1726,21 @@ class ExecutionGraph {
         PXC_RETURN_IF_ERROR(BuildSource(id, op, ntables, tables, ops, parents, children, &built, &fused_away));
         continue;
       }
+      if (op.which == 9) {  // GRPCSourceOperator: batches from the caller's transport
+        const std::vector<std::pair<const uint8_t*, int64_t>>* msgs = nullptr;
+        if (grpc_inputs_) {
+          auto it = grpc_inputs_->find(id);
+          if (it != grpc_inputs_->end()) msgs = &it->second;
+        }
+        auto* src = new GrpcSourceNode(id, msgs);
+        pool_.emplace_back(src);
+        for (int32_t t : op.grpc_source_types)
+          if (t < B || t > T) return Err(PXG_INVALID_ARGUMENT, "GRPC source column type %d", t);
+        PXC_RETURN_IF_ERROR(src->Init(op, op.grpc_source_types, {}));
+        sources_.push_back(src);
+        built[id] = src;
+        continue;
+      }
       const std::vector<uint64_t>& ps = parents[id];
       if (ps.empty()) return Err(PXG_UNIMPLEMENTED, "operator (oneof field %d) without inputs has no device node", op.which);
       std::vector<RowDescriptor> ins;
@@ -1439,6 +1787,15 @@ class ExecutionGraph {
           PXC_RETURN_IF_ERROR(st);
           break;
         }
+        case 8: {
+          if (ins.empty() || op.union_mappings.empty()) return Err(PXG_INVALID_ARGUMENT, "Union needs parents and column mappings");
+          node = new UnionNode();
+          for (int64_t i : op.union_mappings[0]) {
+            if (i < 0 || static_cast<size_t>(i) >= ins[0].size()) return Err(PXG_INVALID_ARGUMENT, "Union column mapping out of range");
+            out.push_back(ins[0][static_cast<size_t>(i)]);
+          }
+          break;
+        }
         case 11: {
           if (ins.size() != 2) return Err(PXG_INVALID_ARGUMENT, "Join operator expects a two input relations, got %zu", ins.size());
           node = new GpuEquijoinNode();
@@ -1448,8 +1805,16 @@ class ExecutionGraph {
           }
           break;
         }
-        case 5:
-        case 1000: {
+        case 1000:
+          if (op.grpc_sink_to_source) {
+            auto* gs = new GrpcSinkNode(op.grpc_source_id);
+            node = gs;
+            grpc_sinks_.push_back(gs);
+            out = cur;
+            break;
+          }
+          [[fallthrough]];  // a result table sink
+        case 5: {
           auto* sk = new SinkNode(op.which == 5 ? op.mem_sink.name : op.grpc_sink_table);
           node = sk;
           sinks_.push_back(sk);
@@ -1464,8 +1829,8 @@ class ExecutionGraph {
       built[id] = node;
       lowered_.push_back(node);
     }
-    if (sources_.empty()) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource");
-    if (sinks_.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no sink");
+    if (sources_.empty()) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource or GRPCSource");
+    if (sinks_.empty() && grpc_sinks_.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no sink");
     return Status::OK();
   }
 
@@ -1511,6 +1876,9 @@ class ExecutionGraph {
   }
 
   std::vector<SinkNode*> sinks_;
+  std::vector<GrpcSinkNode*> grpc_sinks_;
+  // GRPCSource node id -> its RowBatchData messages in arrival order (set before Init).
+  const std::map<uint64_t, std::vector<std::pair<const uint8_t*, int64_t>>>* grpc_inputs_ = nullptr;
 
  private:
   static std::string ProgString(const Program& p) {
@@ -1761,8 +2129,11 @@ extern "C" int32_t pxc_engine_destroy(pxc_engine* e) {
   return PXG_OK;
 }
 
+using GrpcInputs = std::map<uint64_t, std::vector<std::pair<const uint8_t*, int64_t>>>;
+
 static Status Lower(const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables, const TableStore* store,
-                    ExecutionGraph* g) {
+                    ExecutionGraph* g, const GrpcInputs* grpc_inputs = nullptr) {
+  g->grpc_inputs_ = grpc_inputs;
   if (!plan || plan_len < 0) return Err(PXG_INVALID_ARGUMENT, "no plan");
   planpb::Plan p;
   try {
@@ -1865,13 +2236,21 @@ extern "C" pxg_table* pxc_store_device_table(pxc_engine* e, const char* name) {
   return it == e->store.end() ? nullptr : it->second.t;
 }
 
-extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
-                                    const pxc_table* tables, uint8_t** out, int64_t* out_len) {
+static uint8_t* CopyOut(const std::vector<uint8_t>& b) {
+  uint8_t* p = static_cast<uint8_t*>(std::malloc(std::max<size_t>(b.size(), 1)));
+  if (!b.empty()) std::memcpy(p, b.data(), b.size());
+  return p;
+}
+
+static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables, const pxc_table* tables,
+                           const GrpcInputs* grpc_inputs, uint8_t** out, int64_t* out_len, uint8_t** grpc_out,
+                           int64_t* grpc_out_len) {
   if (!engine || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
   StageClock clk;
   ExecutionGraph g;
-  Status s = Lower(plan, plan_len, ntables, tables, &engine->store, &g);
+  Status s = Lower(plan, plan_len, ntables, tables, &engine->store, &g, grpc_inputs);
   if (!s.ok()) return Fail(s);
+  if (!grpc_out && !g.grpc_sinks_.empty()) return Fail(Err(PXG_INVALID_ARGUMENT, "plan has GRPC sinks: use pxc_execute_plan_grpc"));
   clk.Mark("lower");
   ExecState st;
   st.ctx = engine->ctx;
@@ -1890,8 +2269,79 @@ extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int
     for (auto& rb : sk->batches) WriteBatch(&w, rb);
   }
   *out_len = static_cast<int64_t>(w.buf.size());
-  *out = static_cast<uint8_t*>(std::malloc(w.buf.size()));
-  std::memcpy(*out, w.buf.data(), w.buf.size());
+  *out = CopyOut(w.buf);
+  if (grpc_out) {  // "PXGS": per GRPC sink, its destination source id and RowBatchData messages
+    Writer gw;
+    gw.put<uint32_t>(0x53475850u);
+    gw.put<uint32_t>(static_cast<uint32_t>(g.grpc_sinks_.size()));
+    for (auto* gs : g.grpc_sinks_) {
+      gw.put<uint64_t>(gs->dest_id);
+      gw.put<uint32_t>(static_cast<uint32_t>(gs->messages.size()));
+      for (auto& m : gs->messages) {
+        gw.put<uint32_t>(static_cast<uint32_t>(m.size()));
+        gw.bytes(m.data(), m.size());
+      }
+    }
+    *grpc_out_len = static_cast<int64_t>(gw.buf.size());
+    *grpc_out = CopyOut(gw.buf);
+  }
   clk.Mark("PXRB serialise");
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_execute_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                                    const pxc_table* tables, uint8_t** out, int64_t* out_len) {
+  return ExecuteImpl(engine, plan, plan_len, ntables, tables, nullptr, out, out_len, nullptr, nullptr);
+}
+
+extern "C" int32_t pxc_execute_plan_grpc(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
+                                         const pxc_table* tables, int32_t ninputs, const pxc_grpc_input* inputs, uint8_t** out,
+                                         int64_t* out_len, uint8_t** grpc_out, int64_t* grpc_out_len) {
+  if (!grpc_out || !grpc_out_len || (ninputs > 0 && !inputs)) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  GrpcInputs in;
+  for (int32_t i = 0; i < ninputs; ++i) {
+    auto& v = in[inputs[i].grpc_source_id];
+    for (int32_t m = 0; m < inputs[i].nmessages; ++m) v.push_back({inputs[i].messages[m], inputs[i].lengths[m]});
+  }
+  return ExecuteImpl(engine, plan, plan_len, ntables, tables, &in, out, out_len, grpc_out, grpc_out_len);
+}
+
+extern "C" int32_t pxc_rowbatch_to_proto(int32_t ncols, const pxg_column_view* cols, int64_t nrows, int32_t eow, int32_t eos,
+                                         uint8_t** out, int64_t* out_len) {
+  if ((ncols > 0 && !cols) || !out || !out_len || nrows < 0) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  RowBatch rb;
+  rb.num_rows = nrows;
+  for (int32_t c = 0; c < ncols; ++c) {
+    HostColumn hc;
+    hc.type = cols[c].type;
+    hc.length = cols[c].length;
+    hc.values = cols[c].values;
+    hc.offsets = cols[c].offsets;
+    hc.data = cols[c].data;
+    if (PbFieldOfType(hc.type) == 0) return Fail(Err(PXG_INVALID_ARGUMENT, "column %d has type %d", c, hc.type));
+    if (hc.length != nrows) return Fail(Err(PXG_INVALID_ARGUMENT, "column %d has %lld rows, batch %lld", c, (long long)hc.length, (long long)nrows));
+    rb.cols.push_back(hc);
+  }
+  const std::string m = EncodeRowBatchData(rb, 0, nrows, eow != 0, eos != 0);
+  *out_len = static_cast<int64_t>(m.size());
+  *out = CopyOut(std::vector<uint8_t>(m.begin(), m.end()));
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_rowbatch_from_proto(const uint8_t* msg, int64_t len, uint8_t** out, int64_t* out_len) {
+  if ((!msg && len > 0) || len < 0 || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  RowBatch rb;
+  Status s = DecodeRowBatchData(msg, static_cast<size_t>(len), &rb);
+  if (!s.ok()) return Fail(s);
+  Writer w;
+  w.put<uint32_t>(0x42525850u);
+  w.put<uint32_t>(1);
+  const std::string name = "rowbatch";
+  w.put<uint32_t>(static_cast<uint32_t>(name.size()));
+  w.bytes(name.data(), name.size());
+  w.put<uint32_t>(1);
+  WriteBatch(&w, rb);
+  *out_len = static_cast<int64_t>(w.buf.size());
+  *out = CopyOut(w.buf);
   return PXG_OK;
 }

@@ -207,6 +207,12 @@ struct Operator {  // plan.proto:82-110
   FilterOperator filter;
   JoinOperator join;
   std::string grpc_sink_table;  // GRPCSinkOperator.output_table.table_name
+  bool grpc_sink_to_source = false;  // GRPCSinkOperator.grpc_source_id is the destination
+  uint64_t grpc_source_id = 0;
+  std::vector<int32_t> grpc_source_types;        // GRPCSourceOperator.column_types (plan.proto:182-187)
+  std::vector<std::string> grpc_source_names;
+  std::vector<std::string> union_names;              // UnionOperator (plan.proto:283-295)
+  std::vector<std::vector<int64_t>> union_mappings;  // per parent: input column of each output column
 };
 
 struct PlanNode {
@@ -441,9 +447,45 @@ inline void Decode(Reader r, Operator* op) {
               if (tf == 1) op->grpc_sink_table = t.String();
               else t.Skip(tw);
             }
+          } else if (sf == 3) {
+            op->grpc_sink_to_source = true;
+            op->grpc_source_id = s.Varint();
           } else {
             s.Skip(sw);
           }
+        }
+        break;
+      }
+      case 8: {  // UnionOperator
+        op->which = 8;
+        Reader s = r.Sub();
+        uint32_t sf, sw;
+        while (s.Next(&sf, &sw)) {
+          if (sf == 1) {
+            op->union_names.push_back(s.String());
+          } else if (sf == 2) {
+            Reader m = s.Sub();
+            std::vector<int64_t> idx;
+            uint32_t mf, mw;
+            while (m.Next(&mf, &mw)) {
+              if (mf == 1) m.RepeatedVarint(mw, &idx);
+              else m.Skip(mw);
+            }
+            op->union_mappings.push_back(idx);
+          } else {
+            s.Skip(sw);
+          }
+        }
+        break;
+      }
+      case 9: {  // GRPCSourceOperator
+        op->which = 9;
+        Reader s = r.Sub();
+        uint32_t sf, sw;
+        while (s.Next(&sf, &sw)) {
+          if (sf == 1) s.RepeatedVarint(sw, &op->grpc_source_types);
+          else if (sf == 2) op->grpc_source_names.push_back(s.String());
+          else s.Skip(sw);
         }
         break;
       }

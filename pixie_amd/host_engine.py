@@ -15,6 +15,11 @@ from .pxrb import parse_pxrb
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpxcarnot.so")
 
 
+class PxcGrpcInput(C.Structure):
+    _fields_ = [("grpc_source_id", C.c_uint64), ("nmessages", C.c_int32), ("reserved", C.c_int32),
+                ("messages", C.POINTER(C.c_void_p)), ("lengths", C.POINTER(C.c_int64))]
+
+
 class PxcTable(C.Structure):
     _fields_ = [("name", C.c_char_p), ("ncols", C.c_int32), ("nbatches", C.c_int32),
                 ("col_types", C.POINTER(C.c_int32)), ("cols", C.POINTER(ColumnView)), ("batch_flags", C.c_void_p)]
@@ -54,6 +59,13 @@ def load() -> C.CDLL:
     lib.pxc_store_device_table.restype = vp
     lib.pxc_engine_ctx.argtypes = [vp]
     lib.pxc_engine_ctx.restype = vp
+    lib.pxc_execute_plan_grpc.argtypes = [vp, C.c_char_p, i64, i32, p(PxcTable), i32, p(PxcGrpcInput), p(vp), p(i64),
+                                          p(vp), p(i64)]
+    lib.pxc_execute_plan_grpc.restype = i32
+    lib.pxc_rowbatch_to_proto.argtypes = [i32, p(ColumnView), i64, i32, i32, p(vp), p(i64)]
+    lib.pxc_rowbatch_to_proto.restype = i32
+    lib.pxc_rowbatch_from_proto.argtypes = [C.c_char_p, i64, p(vp), p(i64)]
+    lib.pxc_rowbatch_from_proto.restype = i32
     lib.pxc_free.argtypes = [vp]
     lib.pxc_free.restype = None
     lib.pxc_last_error.argtypes = []
@@ -108,6 +120,65 @@ class _Tables:
         self.n = len(tables)
 
 
+def _views(cols):
+    views = (ColumnView * max(1, len(cols)))()
+    for c, col in enumerate(cols):
+        v = ColumnView()
+        v.type = col.type
+        v.length = len(col)
+        if col.type == _lib.STRING:
+            v.offsets = col.offsets.ctypes.data
+            v.data = col.data.ctypes.data
+        else:
+            v.values = col.values.ctypes.data
+        views[c] = v
+    return views
+
+
+def _take(lib, out, n) -> bytes:
+    try:
+        return C.string_at(out.value, n.value)
+    finally:
+        lib.pxc_free(out)
+
+
+def rowbatch_to_proto(cols, eow: bool = False, eos: bool = False) -> bytes:
+    """RowBatch::ToProto (row_batch.cc:161-177): host columns -> schemapb.RowBatchData bytes."""
+    lib = load()
+    views = _views(cols)
+    out, n = C.c_void_p(), C.c_int64()
+    nrows = len(cols[0]) if cols else 0
+    _check(lib.pxc_rowbatch_to_proto(len(cols), views, nrows, int(eow), int(eos), C.byref(out), C.byref(n)))
+    return _take(lib, out, n)
+
+
+def rowbatch_from_proto(msg: bytes) -> dict:
+    """RowBatch::FromProto (row_batch.cc:201-224): {'rows','eow','eos','cols'}."""
+    lib = load()
+    out, n = C.c_void_p(), C.c_int64()
+    _check(lib.pxc_rowbatch_from_proto(msg, len(msg), C.byref(out), C.byref(n)))
+    return parse_pxrb(_take(lib, out, n))["rowbatch"][0]
+
+
+def parse_pxgs(buf: bytes) -> Dict[int, list]:
+    """PXGS -> {destination grpc_source_id: [RowBatchData bytes, ...]}."""
+    import struct
+    magic, nsinks = struct.unpack_from("<II", buf, 0)
+    assert magic == 0x53475850
+    off, out = 8, {}
+    for _ in range(nsinks):
+        dest, nm = struct.unpack_from("<QI", buf, off)
+        off += 12
+        msgs = []
+        for _ in range(nm):
+            (ln,) = struct.unpack_from("<I", buf, off)
+            off += 4
+            msgs.append(bytes(buf[off:off + ln]))
+            off += ln
+        out.setdefault(dest, []).extend(msgs)
+    return out
+
+
 def explain(plan, tables: Dict[str, dict]) -> str:
     """Lowering only (no device): the node graph the operator switch builds."""
     lib = load()
@@ -153,6 +224,26 @@ class Engine:
         finally:
             self.lib.pxc_free(out)
         return parse_pxrb(buf)
+
+    def execute_grpc(self, plan, tables: Dict[str, dict] = None, grpc_inputs: Dict[int, list] = None):
+        """pxc_execute_plan_grpc: grpc_inputs = {GRPCSource node id: [RowBatchData bytes]}.
+        Returns (result sinks as execute() does, {destination source id: [RowBatchData bytes]})."""
+        pb = plan.SerializeToString()
+        t = _Tables(tables or {})
+        keep = []
+        gi = grpc_inputs or {}
+        arr = (PxcGrpcInput * max(1, len(gi)))()
+        for i, (sid, msgs) in enumerate(gi.items()):
+            bufs = [C.create_string_buffer(m, len(m)) for m in msgs]
+            ptrs = (C.c_void_p * max(1, len(msgs)))(*[C.addressof(b) for b in bufs])
+            lens = (C.c_int64 * max(1, len(msgs)))(*[len(m) for m in msgs])
+            keep += [bufs, ptrs, lens]
+            arr[i] = PxcGrpcInput(sid, len(msgs), 0, ptrs, lens)
+        out, n, gout, gn = C.c_void_p(), C.c_int64(), C.c_void_p(), C.c_int64()
+        _check(self.lib.pxc_execute_plan_grpc(self.h, pb, len(pb), t.n, t.arr, len(gi), arr, C.byref(out), C.byref(n),
+                                              C.byref(gout), C.byref(gn)))
+        res = parse_pxrb(_take(self.lib, out, n))
+        return res, parse_pxgs(_take(self.lib, gout, gn))
 
     def explain(self, plan, tables: Dict[str, dict] = None) -> str:
         """Lowering with the engine's stored tables visible (no execution)."""

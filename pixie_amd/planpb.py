@@ -130,6 +130,14 @@ def _build():
             f.type_name = ".px.types.DataType"
         if num == 4:
             f.type_name = ".px.types.SemanticType"
+    un = _msg(p, "UnionOperator", [("column_names", 1, "string", "rep"),
+                                   ("column_mappings", 2, ".px.carnot.planpb.UnionOperator.ColumnMapping", "rep"),
+                                   ("rows_per_batch", 3, "uint64")])
+    cm = un.nested_type.add()
+    cm.name = "ColumnMapping"
+    f = cm.field.add()
+    f.name, f.number, f.label, f.type = "column_indexes", 1, F.LABEL_REPEATED, F.TYPE_INT64
+    _msg(p, "GRPCSourceOperator", [("column_types", 1, DT, "rep"), ("column_names", 2, "string", "rep")])
     _msg(p, "MapOperator", [("expressions", 1, ".px.carnot.planpb.ScalarExpression", "rep"),
                             ("column_names", 2, "string", "rep")])
     _msg(p, "AggregateOperator", [("values", 1, ".px.carnot.planpb.AggregateExpression", "rep"),
@@ -163,6 +171,8 @@ def _build():
                          ("mem_sink_op", 5, ".px.carnot.planpb.MemorySinkOperator", "opt", "op"),
                          ("filter_op", 6, ".px.carnot.planpb.FilterOperator", "opt", "op"),
                          ("limit_op", 7, ".px.carnot.planpb.LimitOperator", "opt", "op"),
+                         ("union_op", 8, ".px.carnot.planpb.UnionOperator", "opt", "op"),
+                         ("grpc_source_op", 9, ".px.carnot.planpb.GRPCSourceOperator", "opt", "op"),
                          ("join_op", 11, ".px.carnot.planpb.JoinOperator", "opt", "op"),
                          ("grpc_sink_op", 1000, ".px.carnot.planpb.GRPCSinkOperator", "opt", "op")], oneofs=["op"])
     _msg(p, "PlanNode", [("id", 1, "uint64"), ("op", 2, ".px.carnot.planpb.Operator")])
@@ -177,11 +187,35 @@ def _build():
     _msg(p, "Plan", [("dag", 1, ".px.carnot.planpb.DAG"), ("nodes", 2, ".px.carnot.planpb.PlanFragment", "rep"),
                      ("plan_options", 4, ".px.carnot.planpb.PlanOptions")])
     pool.Add(p)
+    # src/table_store/schemapb/schema.proto:31-79 (RowBatchData, the GRPC transfer payload).
+    sc = descriptor_pb2.FileDescriptorProto()
+    sc.name = "src/table_store/schemapb/schema.proto"
+    sc.package = "px.table_store.schemapb"
+    sc.syntax = "proto3"
+    sc.dependency.append("src/shared/types/typespb/types.proto")
+    for nm, ty in [("BooleanColumn", "bool"), ("Int64Column", "int64"), ("UInt128Column", ".px.types.UInt128"),
+                   ("Float64Column", "double"), ("Time64NSColumn", "int64")]:
+        _msg(sc, nm, [("data", 1, ty, "rep")])
+    sm = sc.message_type.add()
+    sm.name = "StringColumn"
+    f = sm.field.add()
+    f.name, f.number, f.label, f.type = "data", 1, F.LABEL_REPEATED, F.TYPE_BYTES
+    S_ = ".px.table_store.schemapb."
+    _msg(sc, "Column", [("boolean_data", 1, S_ + "BooleanColumn", "opt", "col_data"),
+                        ("int64_data", 2, S_ + "Int64Column", "opt", "col_data"),
+                        ("uint128_data", 3, S_ + "UInt128Column", "opt", "col_data"),
+                        ("time64ns_data", 4, S_ + "Time64NSColumn", "opt", "col_data"),
+                        ("float64_data", 5, S_ + "Float64Column", "opt", "col_data"),
+                        ("string_data", 6, S_ + "StringColumn", "opt", "col_data")], oneofs=["col_data"])
+    _msg(sc, "RowBatchData", [("cols", 1, S_ + "Column", "rep"), ("num_rows", 2, "int64"), ("eow", 3, "bool"),
+                              ("eos", 4, "bool")])
+    pool.Add(sc)
     out = {}
     for name in ["Plan", "PlanFragment", "PlanNode", "DAG", "Operator", "MapOperator", "AggregateOperator",
                  "FilterOperator", "LimitOperator", "JoinOperator", "MemorySourceOperator", "MemorySinkOperator", "GRPCSinkOperator",
                  "ScalarExpression", "ScalarValue", "ScalarFunc", "AggregateExpression", "Column", "PlanOptions"]:
         out[name] = message_factory.GetMessageClass(pool.FindMessageTypeByName("px.carnot.planpb." + name))
+    out["RowBatchData"] = message_factory.GetMessageClass(pool.FindMessageTypeByName("px.table_store.schemapb.RowBatchData"))
     return out
 
 
@@ -194,6 +228,7 @@ ScalarValue = _CLASSES["ScalarValue"]
 AggregateOperator = _CLASSES["AggregateOperator"]
 FilterOperator = _CLASSES["FilterOperator"]
 MapOperator = _CLASSES["MapOperator"]
+RowBatchData = _CLASSES["RowBatchData"]
 
 
 def parse_text(cls, text: str):

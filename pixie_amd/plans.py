@@ -317,3 +317,55 @@ def split_merge_plan(partials: str, group_types: Sequence[int], values=None, sin
     agg = agg_op(list(range(ng)), values, names[:ng], [f"v{i}" for i in range(len(values))],
                  partial_agg=False, finalize_results=True)
     return linear_plan([src, agg, sink_op(sink)])
+
+
+def grpc_sink_op(grpc_source_id: int, address: str = "kelvin:59300"):
+    """GRPCSinkOperator to another Carnot's GRPCSource (plan.proto:190-216)."""
+    op = planpb.Operator()
+    op.op_type = 9100
+    op.grpc_sink_op.address = address
+    op.grpc_sink_op.grpc_source_id = grpc_source_id
+    return op
+
+
+def grpc_source_op(types: Sequence[int], names: Sequence[str]):
+    """GRPCSourceOperator (plan.proto:182-187)."""
+    op = planpb.Operator()
+    op.op_type = 1100
+    op.grpc_source_op.column_types.extend(types)
+    op.grpc_source_op.column_names.extend(names)
+    return op
+
+
+def union_op(names: Sequence[str], mappings: Sequence[Sequence[int]]):
+    """UnionOperator (plan.proto:283-295)."""
+    op = planpb.Operator()
+    op.op_type = 2400
+    op.union_op.column_names.extend(names)
+    for m in mappings:
+        op.union_op.column_mappings.add().column_indexes.extend(m)
+    return op
+
+
+def split_pem_fragment(dest_id: int, table: str = "http_events", groups: Sequence[int] = (0, 1), values=None):
+    """The PEM fragment of a split C3-style aggregate: ... -> Agg(partial) -> GRPCSink(dest)."""
+    plan = split_source_plan(table, groups, values)
+    frag = plan.nodes[0]
+    sink = [n for n in frag.nodes if n.op.WhichOneof("op") == "mem_sink_op"][0]
+    sink.op.CopyFrom(grpc_sink_op(dest_id))
+    return plan
+
+
+def split_kelvin_fragment(source_ids: Sequence[int], group_types: Sequence[int], values=None, sink: str = "output"):
+    """The Kelvin fragment: one GRPCSource per PEM -> Union -> Agg(finalize) -> sink."""
+    values = split_values() if values is None else values
+    ng = len(group_types)
+    types = list(group_types) + [STRING]
+    names = [f"g{i}" for i in range(ng)] + ["serialized_expressions"]
+    nodes = [(sid, grpc_source_op(types, names), []) for sid in source_ids]
+    un = union_op(names, [list(range(ng + 1))] * len(source_ids))
+    agg = agg_op(list(range(ng)), values, names[:ng], [f"v{i}" for i in range(len(values))],
+                 partial_agg=False, finalize_results=True)
+    base = max(source_ids) + 1
+    nodes += [(base, un, list(source_ids)), (base + 1, agg, [base]), (base + 2, sink_op(sink), [base + 1])]
+    return dag_plan(nodes)

@@ -1,0 +1,219 @@
+"""RowBatch protobuf codec and the GRPC sink / source hop.
+
+- RowBatch::ToProto / FromProto (row_batch.cc:161-224) against schemapb.RowBatchData as the
+  protobuf library encodes it (descriptors built field by field from schema.proto:31-79): the
+  C++ encoder must produce the same bytes, and decode what protobuf produces.
+- GRPCSinkNode (grpc_sink_node.cc:216-330): batches above (1 MiB - 16 KiB) * 0.9 bytes are split,
+  the last piece keeping eow / eos.
+- A distributed split aggregate: PEM fragments (-> partial Agg -> GRPCSink) and a Kelvin fragment
+  (GRPCSources -> Union -> finalize Agg) exchanging RowBatchData messages, checked against the
+  CPU Carnot restatement's unsplit aggregate."""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_client as oc
+from pixie_amd import host_engine as H
+from pixie_amd import planpb
+from pixie_amd import plans as P
+from pixie_amd.device import Column
+
+BOOLEAN, INT64, UINT128, FLOAT64, STRING, TIME64NS = 1, 2, 3, 4, 5, 6
+
+
+def sample_columns(n, seed=7):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, 2 ** 63, size=(n, 2), dtype=np.uint64)
+    if n > 2:
+        u[0] = [0, 5]  # zero low word (omitted on the wire)
+        u[1] = [7, 0]
+    strs = [bytes(rng.integers(0, 256, size=int(rng.integers(0, 20)), dtype=np.uint8)) for _ in range(n)]
+    if n > 1:
+        strs[1] = b""
+    return [
+        Column(BOOLEAN, values=(rng.integers(0, 2, n) == 1).astype(np.uint8)),
+        Column(INT64, values=rng.integers(-2 ** 62, 2 ** 62, n, dtype=np.int64)),
+        Column(UINT128, values=u),
+        Column(FLOAT64, values=rng.standard_normal(n)),
+        Column.from_values(STRING, strs),
+        Column(TIME64NS, values=rng.integers(0, 2 ** 62, n, dtype=np.int64)),
+    ]
+
+
+def to_pb(cols, eow, eos):
+    """The protobuf library's RowBatchData for the same columns."""
+    m = planpb.RowBatchData()
+    n = len(cols[0]) if cols else 0
+    for c in cols:
+        pc = m.cols.add()
+        if c.type == BOOLEAN:
+            pc.boolean_data.data.extend([bool(x) for x in c.values])
+        elif c.type == INT64:
+            pc.int64_data.data.extend([int(x) for x in c.values])
+        elif c.type == TIME64NS:
+            pc.time64ns_data.data.extend([int(x) for x in c.values])
+        elif c.type == FLOAT64:
+            pc.float64_data.data.extend([float(x) for x in c.values])
+        elif c.type == UINT128:
+            pc.uint128_data.SetInParent()
+            for lo, hi in c.values:
+                x = pc.uint128_data.data.add()
+                x.low, x.high = int(lo), int(hi)
+        else:
+            pc.string_data.SetInParent()
+            raw, o = c.data.tobytes(), c.offsets
+            pc.string_data.data.extend([raw[o[i]:o[i + 1]] for i in range(n)])
+    m.num_rows = n
+    m.eow, m.eos = eow, eos
+    return m
+
+
+def same_columns(a, b):
+    assert [c.type for c in a] == [c.type for c in b]
+    for x, y in zip(a, b):
+        if x.type == STRING:
+            assert [s.encode(errors="surrogateescape") for s in x.to_list()] == \
+                   [s.encode(errors="surrogateescape") for s in y.to_list()]
+        else:
+            assert np.array_equal(np.asarray(x.values), np.asarray(y.values))
+
+
+@pytest.mark.parametrize("n,eow,eos", [(0, False, False), (1, True, False), (37, True, True), (1000, False, False)])
+def test_encode_matches_protobuf_bytes(n, eow, eos):
+    cols = sample_columns(n)
+    mine = H.rowbatch_to_proto(cols, eow, eos)
+    assert mine == to_pb(cols, eow, eos).SerializeToString()
+    # and protobuf parses it back to the same message
+    back = planpb.RowBatchData()
+    back.ParseFromString(mine)
+    assert back == to_pb(cols, eow, eos)
+
+
+@pytest.mark.parametrize("n", [0, 5, 513])
+def test_decode_protobuf_bytes(n):
+    cols = sample_columns(n, seed=n)
+    rb = H.rowbatch_from_proto(to_pb(cols, True, n == 5).SerializeToString())
+    assert rb["rows"] == n and rb["eow"] and rb["eos"] == (n == 5)
+    same_columns(rb["cols"], cols)
+
+
+def test_decode_accepts_unpacked_scalars_and_rejects_bad_messages():
+    # int64 data as unpacked varints (wire type 0), as a proto2-style writer would send them
+    col = b"\x12" + bytes([4]) + b"\x08\x03\x08\x05"          # Column{int64_data{data: 3, data: 5}}
+    msg = b"\x0a" + bytes([len(col)]) + col + b"\x10\x02\x18\x01"  # cols, num_rows=2, eow
+    rb = H.rowbatch_from_proto(msg)
+    assert rb["rows"] == 2 and rb["eow"] and list(rb["cols"][0].values) == [3, 5]
+    with pytest.raises(H.PxcError) as e:  # a Column without data (ProtoDataType, row_batch.cc:181-199)
+        H.rowbatch_from_proto(b"\x0a\x00\x10\x00")
+    assert e.value.code == 9
+    with pytest.raises(H.PxcError) as e:  # column length != num_rows
+        H.rowbatch_from_proto(b"\x0a" + bytes([len(col)]) + col + b"\x10\x03")
+    assert e.value.code == 3
+    with pytest.raises(H.PxcError) as e:  # truncated
+        H.rowbatch_from_proto(msg[:-3])
+    assert e.value.code == 3
+
+
+def test_kelvin_fragment_lowers_to_grpc_sources_union_and_merge_agg():
+    txt = H.explain(P.split_kelvin_fragment([100, 101], [STRING, STRING]), {})
+    lines = txt.splitlines()
+    assert lines[0] == "GrpcSourceNode(100)" and lines[1] == "GrpcSourceNode(101)"
+    assert "UnionNode(unordered)" in txt and "GpuAggNode" in txt and "SinkNode(output)" in txt
+    pem = H.explain(P.split_pem_fragment(100), {"http_events": {"types": P.HTTP_TYPES, "batches": []}})
+    assert "GrpcSinkNode(-> grpc source 100)" in pem and "fused" in pem
+
+
+def test_time_ordered_union_is_unimplemented():
+    plan = P.dag_plan([(1, P.grpc_source_op([TIME64NS], ["time_"]), []), (2, P.grpc_source_op([TIME64NS], ["time_"]), []),
+                       (3, P.union_op(["time_"], [[0], [0]]), [1, 2]), (4, P.sink_op("out"), [3])])
+    with pytest.raises(H.PxcError) as e:
+        H.explain(plan, {})
+    assert e.value.code == 10
+
+
+# ------------------------------------------------------------------------------------------
+# GPU: whole fragments through the engine.
+# ------------------------------------------------------------------------------------------
+def engine():
+    return H.Engine(0)
+
+
+@pytest.mark.gpu
+def test_grpc_sink_splits_large_batches_like_the_reference():
+    n = 60000
+    rng = np.random.default_rng(3)
+    strs = [b"x" * int(k) for k in rng.integers(0, 40, n)]
+    cols = [Column(INT64, values=np.arange(n, dtype=np.int64)), Column.from_values(STRING, strs)]
+    plan = P.linear_plan([P.source_op("t", [INT64, STRING], ["a", "s"], [0, 1]), P.grpc_sink_op(7)])
+    e = engine()
+    try:
+        res, grpc = e.execute_grpc(plan, {"t": {"types": [INT64, STRING], "batches": [cols]}})
+    finally:
+        e.close()
+    msgs = grpc[7]
+    desired = int(np.float32(1024 * 1024 - 16 * 1024) * np.float32(0.9))
+    rows, got_a, got_s = [], [], []
+    for i, m in enumerate(msgs):
+        pb = planpb.RowBatchData()
+        pb.ParseFromString(m)
+        last = i == len(msgs) - 1
+        assert pb.eow == last and pb.eos == last
+        rows.append(pb.num_rows)
+        got_a += list(pb.cols[0].int64_data.data)
+        got_s += list(pb.cols[1].string_data.data)
+        nbytes = 8 * pb.num_rows + sum(len(s) for s in pb.cols[1].string_data.data)
+        assert nbytes <= desired or pb.num_rows == 1
+    # the reference's greedy cut (grpc_sink_node.cc:240-253)
+    expect, b, r = [], 0, 0
+    for s in strs:
+        rb = 8 + len(s)
+        if r > 0 and b + rb > desired:
+            expect.append(r)
+            b = r = 0
+        b += rb
+        r += 1
+    expect.append(r)
+    assert rows == expect and len(rows) > 1
+    assert got_a == list(range(n)) and got_s == strs
+
+
+@pytest.mark.gpu
+def test_split_aggregate_over_grpc_matches_unsplit_oracle():
+    from test_split_agg import batches_rows, check_final, decode_states, as_bytes, http_shards, http_table
+    shards = http_shards(3, 30000)
+    e = engine()
+    try:
+        inputs = {}
+        for i, s in enumerate(shards):
+            res, grpc = e.execute_grpc(P.split_pem_fragment(100 + i), http_table(s))
+            assert list(grpc) == [100 + i] and res == {}
+            inputs[100 + i] = grpc[100 + i]
+            # the payload is a protobuf RowBatchData holding groups + serialized_expressions
+            pb = planpb.RowBatchData()
+            pb.ParseFromString(inputs[100 + i][-1])
+            assert pb.eos and [c.WhichOneof("col_data") for c in pb.cols] == ["string_data"] * 3
+            decode_states(pb.cols[2].string_data.data[0]) if pb.num_rows else None
+        res, grpc = e.execute_grpc(P.split_kelvin_fragment(sorted(inputs), [STRING, STRING]), {}, inputs)
+    finally:
+        e.close()
+    assert grpc == {}
+    out = res["output"]
+    assert len(out) == 1 and out[0]["eos"]
+    full = oc.execute_plan(P.split_source_plan(partial_agg=False, sink="output"),
+                           http_table([b for s in shards for b in s]))
+    check_final(batches_rows(out, 2), batches_rows(full["output"], 2), "split over GRPC")
+
+
+@pytest.mark.gpu
+def test_grpc_source_without_eos_is_an_error():
+    cols = [Column.from_values(STRING, [b"a"]), Column.from_values(STRING, [b"b"]),
+            Column.from_values(STRING, [b"\0" * 88])]
+    msg = H.rowbatch_to_proto(cols, eow=False, eos=False)
+    e = engine()
+    try:
+        with pytest.raises(H.PxcError) as ex:
+            e.execute_grpc(P.split_kelvin_fragment([100], [STRING, STRING]), {}, {100: [msg]})
+        assert ex.value.code == 3
+    finally:
+        e.close()
