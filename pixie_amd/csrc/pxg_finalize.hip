@@ -13,7 +13,7 @@
 namespace pxg {
 
 constexpr int kRadixBlock = 256;
-constexpr int kRadixItems = 16;
+constexpr int kRadixItems = 12;
 constexpr int kRadixTile = kRadixBlock * kRadixItems;
 constexpr int kRadixBits = 8;
 constexpr int kRadixBuckets = 1 << kRadixBits;
@@ -73,12 +73,15 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
                                                                   int shift, const uint32_t* __restrict__ offs, uint32_t nblocks) {
   constexpr int kWaves = kRadixBlock / 64;
   constexpr int kPerWave = kRadixTile / kWaves;
+  // 42 KB of LDS (3 blocks per CU): per-wave digit counts, turned in place into the tile-local
+  // start of each (wave, digit); one 8-byte-per-item staging buffer that carries the keys,
+  // then each value stream; the digit of every tile position.
   __shared__ uint32_t whist[kWaves][kRadixBuckets];
-  __shared__ uint32_t base[kWaves][kRadixBuckets];  // tile-local start of (wave, digit)
   __shared__ uint32_t dstart[kRadixBuckets];         // tile-local start of each digit
   __shared__ uint32_t gofs[kRadixBuckets];           // global start of this tile's digit run
-  __shared__ uint32_t s_key[kRadixTile];
-  __shared__ uint64_t s_val[kRadixTile];
+  __shared__ uint64_t s_buf[kRadixTile];
+  __shared__ uint8_t s_dig[kRadixTile];
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
@@ -130,38 +133,41 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
     gofs[d] = offs[static_cast<uint64_t>(d) * nblocks + blockIdx.x];
     uint32_t acc = start;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      base[w][d] = acc;
-      acc += whist[w][d];
+    for (int w = 0; w < kWaves; ++w) {  // in place: whist[w][d] becomes the start of (w, d)
+      const uint32_t c = whist[w][d];
+      whist[w][d] = acc;
+      acc += c;
     }
   }
   __syncthreads();
   uint32_t lpos[kRadixItems];
 #pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
-    lpos[k] = base[wid][dig[k]] + part[k];
-    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) s_key[lpos[k]] = keys[k];
+    lpos[k] = whist[wid][dig[k]] + part[k];
+    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) {
+      s_key[lpos[k]] = keys[k];
+      s_dig[lpos[k]] = static_cast<uint8_t>(dig[k]);
+    }
   }
   __syncthreads();
   // Keys out in digit runs.
   for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
-    const uint32_t key = s_key[j];
-    const uint32_t d = (key >> shift) & (kRadixBuckets - 1);
-    kout[gofs[d] + (j - dstart[d])] = key;
+    const uint32_t d = s_dig[j];
+    kout[gofs[d] + (j - dstart[d])] = s_key[j];
   }
-  // Each value stream through the same LDS reordering.
+  // Each value stream through the same LDS reordering (the staging buffer is reused).
   for (int v = 0; v < nvals; ++v) {
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < kRadixItems; ++k) {
       const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-      if (i < n) s_val[lpos[k]] = vin.p[v][i];
+      if (i < n) s_buf[lpos[k]] = vin.p[v][i];
     }
     __syncthreads();
     for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
-      const uint32_t d = (s_key[j] >> shift) & (kRadixBuckets - 1);
-      vout.p[v][gofs[d] + (j - dstart[d])] = s_val[j];
+      const uint32_t d = s_dig[j];
+      vout.p[v][gofs[d] + (j - dstart[d])] = s_buf[j];
     }
-    __syncthreads();
   }
 }
 
