@@ -1200,6 +1200,23 @@ int32_t AggFinalizeImpl(Agg* a) {
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                              a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups,
                              ws.partial.as<const uint64_t>(), max_chunks, uo, states));
+  // Big-group digests, after side stream 2's merges (see below).
+  std::vector<int> big_pending;
+  uint32_t n_big_groups = 0;
+  const uint32_t* chain_starts_big = nullptr;
+  const int32_t* chain_nc_big = nullptr;
+  auto RunBigDigests = [&]() -> int32_t {
+    if (big_pending.empty()) return PXG_OK;
+    PXG_RETURN_IF_ERROR(JoinSide2(ctx));
+    for (int u : big_pending) {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(),
+                                 ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big,
+                                 R.uda_out[u].as<double>(), d_err));
+    }
+    big_pending.clear();
+    return PXG_OK;
+  };
   // 4. Quantile digests.
   if (any_q) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
@@ -1248,39 +1265,49 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_HIP(hipStreamSynchronize(ctx->stream));
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3], n_bchunks = hm[4];
+    n_big_groups = n_big;
+    chain_starts_big = chain_starts + static_cast<uint64_t>(mid_cap) * kChainCap;
+    chain_nc_big = chain_nc + mid_cap;
     const uint64_t big_max = hm[5];
     if (n_big > 0) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(n_big) * kBigCentroids * 4));
     }
+    // Big groups: chunk sort + merge passes on side stream 2 (their late passes hold few
+    // workgroups), overlapping the mid digests and the key output on the main stream; the big
+    // digests join it at the end of finalize.  Each quantile UDA forks again, so its sorts
+    // start after the previous UDA's big digest has read the shared key buffers.
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
-      double* qo = R.uda_out[u].as<double>();
-      DevBuf* src = &ws.keysA;
-      DevBuf* dst = &ws.keysB;
       if (n_big > 0) {
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
-                                   ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.keysA.as<uint64_t>()));
+        PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+        PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
+                                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
+                                     ws.keysA.as<uint64_t>()));
+        DevBuf* src = &ws.keysA;
+        DevBuf* dst = &ws.keysB;
         uint32_t pass = 0;
         for (uint64_t w = kMidMax; w < big_max; w *= 2, ++pass) {
-          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
-                                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), src->as<const uint64_t>(),
-                                     dst->as<uint64_t>(), w, pass));
+          PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
+                                       ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta),
+                                       src->as<const uint64_t>(), dst->as<uint64_t>(), w, pass));
           std::swap(src, dst);
         }
       }
       PXG_RETURN_IF_ERROR(JoinSide(ctx));
+      double* qo = R.uda_out[u].as<double>();
       if (cls[2] > 0)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
                                    gstart, chain_starts, chain_nc, static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
       if (n_big > 0) {
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(n_big), dim3(256), 0,
-                                   ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(),
-                                   ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(),
-                                   chain_starts + static_cast<uint64_t>(mid_cap) * kChainCap, chain_nc + mid_cap, qo, d_err));
+        big_pending.push_back(u);
+        // A later quantile UDA reuses the key buffers: its digest must run before that UDA's sorts.
+        bool more = false;
+        for (int v = u + 1; v < a->n_udas; ++v) more = more || a->uda_kind[v] == PXG_UDA_QUANTILES;
+        if (more) PXG_RETURN_IF_ERROR(RunBigDigests());
       }
     }
   }
@@ -1312,6 +1339,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, ngroups, off + ngroups, scan_tmp));
     ++n_str;
   }
+  PXG_RETURN_IF_ERROR(RunBigDigests());
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;

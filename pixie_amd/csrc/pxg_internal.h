@@ -100,6 +100,9 @@ struct Ctx {
   // Side stream for latency-bound work that overlaps the main stream (fork/join by events).
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // Second side stream: the big-group quantile merges overlap the mid digests and the key output.
+  hipStream_t side2 = nullptr;
+  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool profiling = false;
   std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;
@@ -150,6 +153,17 @@ inline int32_t ForkSide(Ctx* ctx) {
 inline int32_t JoinSide(Ctx* ctx) {
   if (hipEventRecord(ctx->ev_join, ctx->side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0) != hipSuccess)
     return SetError(PXG_INTERNAL, "side stream join failed");
+  return PXG_OK;
+}
+
+inline int32_t ForkSide2(Ctx* ctx) {
+  if (hipEventRecord(ctx->ev_fork2, ctx->stream) != hipSuccess || hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0) != hipSuccess)
+    return SetError(PXG_INTERNAL, "side stream 2 fork failed");
+  return PXG_OK;
+}
+inline int32_t JoinSide2(Ctx* ctx) {
+  if (hipEventRecord(ctx->ev_join2, ctx->side2) != hipSuccess || hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0) != hipSuccess)
+    return SetError(PXG_INTERNAL, "side stream 2 join failed");
   return PXG_OK;
 }
 

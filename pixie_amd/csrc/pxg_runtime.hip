@@ -252,7 +252,10 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
   }
   if (hipStreamCreateWithFlags(&c->impl.side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->impl.ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->impl.ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->impl.side2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_fork2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_join2, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SetError(PXG_INTERNAL, "side stream / event creation failed");
   }
@@ -273,6 +276,10 @@ extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   hipEventDestroy(ctx->impl.ev_fork);
   hipEventDestroy(ctx->impl.ev_join);
   hipStreamDestroy(ctx->impl.side);
+  hipStreamSynchronize(ctx->impl.side2);
+  hipEventDestroy(ctx->impl.ev_fork2);
+  hipEventDestroy(ctx->impl.ev_join2);
+  hipStreamDestroy(ctx->impl.side2);
   hipStreamDestroy(ctx->impl.stream);
   delete ctx;
   return PXG_OK;
