@@ -763,11 +763,14 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_sizes", AggPublishSizesKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
                              d_plan.as<const AggPlanDev>(), chunks, slots.as<const unsigned long long>(), cap, sizes));
   PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, cap, total, sc));
+  uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
+  PXG_HIP(hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
   uint8_t c[32];
   uint64_t tot = 0;
-  PXG_HIP(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(c, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  std::memcpy(&tot, pin, 8);
+  std::memcpy(c, pin + 8, 32);
   std::memcpy(n_deferred, c + 8, 4);
   std::memcpy(&st_n, c + 16, 8);
   const uint64_t n_new = tot >> kPublishCountShift;

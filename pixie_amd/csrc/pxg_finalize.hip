@@ -1183,6 +1183,8 @@ int32_t AggFinalizeImpl(Agg* a) {
   PXG_RETURN_IF_ERROR(ws.cbase.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   uint32_t* cbase = ws.cbase.as<uint32_t>();
   const uint64_t max_chunks = static_cast<uint64_t>(ngroups) + n / kRedChunk + 1;
+  // With quantiles, issued after the boundary chains are forked (they run in their shadow).
+  auto RunReductions = [&]() -> int32_t {
   if (any_red) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "group_chunk_count", GroupChunkCountKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
                                ngroups, cbase));
@@ -1200,6 +1202,9 @@ int32_t AggFinalizeImpl(Agg* a) {
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                              a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups,
                              ws.partial.as<const uint64_t>(), max_chunks, uo, states));
+  return PXG_OK;
+  };
+  if (!any_q) PXG_RETURN_IF_ERROR(RunReductions());
   // Big-group digests, after side stream 2's merges (see below).
   std::vector<int> big_pending;
   uint32_t n_big_groups = 0;
@@ -1233,6 +1238,11 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "big_setup", BigSetupKernel, dim3(1), dim3(kSetupBlock), 0, lists + 3 * static_cast<uint64_t>(ngroups),
                                static_cast<const uint32_t*>(d_cls + 3), gstart, ws.big.as<BigGroup>(), ws.bchunks.as<BigChunk>(),
                                d_bigmeta));
+    // Class counts + big-group metadata to pinned memory right away; the host waits on this
+    // event only, while the digests below keep the GPU busy.
+    uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
+    PXG_HIP(hipMemcpyAsync(pin + 64, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
+    PXG_HIP(hipEventRecord(ctx->ev_meta, ctx->stream));
     // Kernels whose work lists are counted on the device launch right away with upper-bound
     // grids (blocks past the device count exit); the host reads the counts back only after
     // them, so the tiny / small digests and the boundary chains run while it waits.
@@ -1249,6 +1259,7 @@ int32_t AggFinalizeImpl(Agg* a) {
                                  lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), mid_cap,
                                  lists + 3 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 3), gstart,
                                  ws.chain_starts.as<uint32_t>(), ws.chain_nc.as<int32_t>()));
+    PXG_RETURN_IF_ERROR(RunReductions());
     const uint32_t small_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kTinyMax + 1) + 1));
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
@@ -1261,8 +1272,8 @@ int32_t AggFinalizeImpl(Agg* a) {
                                  lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart, vals, at, qo));
     }
     uint32_t hm[6];
-    PXG_HIP(hipMemcpyAsync(hm, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    PXG_HIP(hipEventSynchronize(ctx->ev_meta));
+    std::memcpy(hm, pin + 64, 24);
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3], n_bchunks = hm[4];
     n_big_groups = n_big;
@@ -1278,12 +1289,17 @@ int32_t AggFinalizeImpl(Agg* a) {
     // workgroups), overlapping the mid digests and the key output on the main stream; the big
     // digests join it at the end of finalize.  Each quantile UDA forks again, so its sorts
     // start after the previous UDA's big digest has read the shared key buffers.
+    bool first_big = true;
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
       if (n_big > 0) {
-        PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+        // The first big path needs only what precedes the metadata readback (sorted values,
+        // chunk list), so it starts alongside the tiny / small digests.
+        if (first_big) PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_meta, 0));
+        else PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+        first_big = false;
         PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
                                      ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
                                      ws.keysA.as<uint64_t>()));
@@ -1343,13 +1359,18 @@ int32_t AggFinalizeImpl(Agg* a) {
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;
+  uint32_t* pin32 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 128);
   for (int k = 0; k < a->n_keys; ++k)
     if (a->key_types[k] == PXG_STRING)
-      PXG_HIP(hipMemcpyAsync(&totals[k], R.key_offsets[k].as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+      PXG_HIP(hipMemcpyAsync(pin32 + k, R.key_offsets[k].as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   uint32_t g_dev = 0;
-  PXG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(&g_dev, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 1, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < a->n_keys; ++k)
+    if (a->key_types[k] == PXG_STRING) totals[k] = pin32[k];
+  err = pin32[kMaxKeys];
+  g_dev = pin32[kMaxKeys + 1];
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
   if (g_dev != ngroups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, ngroups);
   for (int k = 0; k < a->n_keys && n_str > 0; ++k) {

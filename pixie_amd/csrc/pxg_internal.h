@@ -103,13 +103,15 @@ struct Ctx {
   // Second side stream: the big-group quantile merges overlap the mid digests and the key output.
   hipStream_t side2 = nullptr;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
+  hipEvent_t ev_meta = nullptr;  // finalize: the big-group metadata readback has landed
   bool profiling = false;
   std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
   int num_cus = 256;
-  // small pinned scratch for counters read back by the host
+  // Pinned scratch for counters read back by the host (async D2H, no staging copy):
+  // [0, 64) consume publish, [64, 128) finalize class counts, [128, 256) finalize totals.
   void* pinned = nullptr;
 
   hipEvent_t GetEvent();

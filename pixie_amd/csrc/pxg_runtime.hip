@@ -255,13 +255,17 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
       hipEventCreateWithFlags(&c->impl.ev_join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->impl.side2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_fork2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->impl.ev_join2, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->impl.ev_join2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_meta, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SetError(PXG_INTERNAL, "side stream / event creation failed");
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->impl.num_cus = prop.multiProcessorCount;
-  if (hipHostMalloc(&c->impl.pinned, 4096, hipHostMallocDefault) != hipSuccess) c->impl.pinned = nullptr;
+  if (hipHostMalloc(&c->impl.pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+    delete c;
+    return SetError(PXG_RESOURCE_UNAVAILABLE, "pinned host scratch allocation failed");
+  }
   *out = c;
   return PXG_OK;
 }
@@ -279,6 +283,7 @@ extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   hipStreamSynchronize(ctx->impl.side2);
   hipEventDestroy(ctx->impl.ev_fork2);
   hipEventDestroy(ctx->impl.ev_join2);
+  hipEventDestroy(ctx->impl.ev_meta);
   hipStreamDestroy(ctx->impl.side2);
   hipStreamDestroy(ctx->impl.stream);
   delete ctx;
