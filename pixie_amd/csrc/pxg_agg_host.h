@@ -80,7 +80,7 @@ struct Agg {
   // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).
   struct FinalizeWs {
     DevBuf skey[2], sval[2][kMaxVals], rank;
-    DevBuf hist, scan, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
+    DevBuf hist, scan, scan2, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
     DevBuf keysA, keysB, bstarts, big, bchunks;
     DevBuf chain_list, chain_nc, chain_starts;
   } ws;

@@ -1119,6 +1119,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     R.ready = true;
     return PXG_OK;
   }
+  bool keys_on_side2 = false;
   PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(n, a->cap) + 1)) + 64));
   void* scan_tmp = ws.scan.p;
   PXG_RETURN_IF_ERROR(ws.rank.Ensure(static_cast<size_t>(a->cap) * 4 + 16));
@@ -1128,6 +1129,46 @@ int32_t AggFinalizeImpl(Agg* a) {
   PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
   PXG_RETURN_IF_ERROR(Launch(ctx, "slot_gslot", SlotGslotKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
                              a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<const uint32_t>(), ws.gslot.as<uint32_t>()));
+
+  // Group keys out of the arena, on side stream 2 while the radix sort runs on the main
+  // stream (ConvertAggHashMapToRowBatch group columns, agg_node.cc:303-349).  String payloads
+  // are sized by the arena (an upper bound), so no count comes back to the host first.
+  {
+    KeyOutDev ko;
+    for (int k = 0; k < kMaxKeys; ++k) {
+      ko.fixed[k] = nullptr;
+      ko.len[k] = nullptr;
+    }
+    for (int k = 0; k < a->n_keys; ++k) {
+      const int t = a->key_types[k];
+      if (t == PXG_STRING) {
+        PXG_RETURN_IF_ERROR(R.key_offsets[k].Ensure((static_cast<size_t>(ngroups) + 1) * 4));
+        PXG_RETURN_IF_ERROR(R.key_data[k].Ensure(static_cast<size_t>(a->arena_words) * 8 + 16));
+        ko.len[k] = R.key_offsets[k].as<uint32_t>();
+      } else {
+        PXG_RETURN_IF_ERROR(R.key_fixed[k].Ensure(static_cast<size_t>(ngroups) * (t == PXG_UINT128 ? 16 : 8)));
+        ko.fixed[k] = R.key_fixed[k].as<uint64_t>();
+      }
+    }
+    if (a->n_keys > 0) {
+      PXG_RETURN_IF_ERROR(ws.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(ngroups) + 1) + 64));
+      PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                                   a->d_plan.as<const AggPlanDev>(), static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
+                                   a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
+      for (int k = 0; k < a->n_keys; ++k) {
+        if (a->key_types[k] != PXG_STRING) continue;
+        uint32_t* off = R.key_offsets[k].as<uint32_t>();
+        PXG_RETURN_IF_ERROR(ScanExclusiveU32On(ctx, ctx->side2, off, off, ngroups, off + ngroups, ws.scan2.p));
+        PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "key_string_copy", KeyStringCopyKernel, dim3(GridFor(ngroups, 256, 1 << 30)),
+                                     dim3(256), 0, a->d_plan.as<const AggPlanDev>(), k,
+                                     static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
+                                     a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(),
+                                     static_cast<const uint32_t*>(R.key_offsets[k].as<uint32_t>()), R.key_data[k].as<uint8_t>()));
+      }
+      keys_on_side2 = true;
+    }
+  }
 
   // 2. Stable LSD radix sort of (dense id, vals...) by dense id (ceil(log2(G + 1) / 8) passes);
   //    records without a group (deferred slots) get id G and sort last.  The staging itself is
@@ -1210,11 +1251,13 @@ int32_t AggFinalizeImpl(Agg* a) {
   uint32_t n_big_groups = 0;
   const uint32_t* chain_starts_big = nullptr;
   const int32_t* chain_nc_big = nullptr;
+  // On side stream 2, behind its merges; the boundary chains come from the side stream (its
+  // join event was recorded before the mid digests were issued).
   auto RunBigDigests = [&]() -> int32_t {
     if (big_pending.empty()) return PXG_OK;
-    PXG_RETURN_IF_ERROR(JoinSide2(ctx));
+    PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_join, 0));
     for (int u : big_pending) {
-      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0,
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(),
                                  ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big,
                                  R.uda_out[u].as<double>(), d_err));
@@ -1327,35 +1370,8 @@ int32_t AggFinalizeImpl(Agg* a) {
       }
     }
   }
-  // 5. Keys.
-  KeyOutDev ko;
-  for (int k = 0; k < kMaxKeys; ++k) {
-    ko.fixed[k] = nullptr;
-    ko.len[k] = nullptr;
-  }
-  for (int k = 0; k < a->n_keys; ++k) {
-    const int t = a->key_types[k];
-    if (t == PXG_STRING) {
-      PXG_RETURN_IF_ERROR(R.key_offsets[k].Ensure((static_cast<size_t>(ngroups) + 1) * 4));
-      ko.len[k] = R.key_offsets[k].as<uint32_t>();
-    } else {
-      PXG_RETURN_IF_ERROR(R.key_fixed[k].Ensure(static_cast<size_t>(ngroups) * (t == PXG_UINT128 ? 16 : 8)));
-      ko.fixed[k] = R.key_fixed[k].as<uint64_t>();
-    }
-  }
-  if (a->n_keys > 0) {
-    PXG_RETURN_IF_ERROR(Launch(ctx, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
-                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
-  }
-  int n_str = 0;
-  for (int k = 0; k < a->n_keys; ++k) {
-    if (a->key_types[k] != PXG_STRING) continue;
-    uint32_t* off = R.key_offsets[k].as<uint32_t>();
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, ngroups, off + ngroups, scan_tmp));
-    ++n_str;
-  }
   PXG_RETURN_IF_ERROR(RunBigDigests());
+  if (keys_on_side2 || n_big_groups > 0) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;
@@ -1373,15 +1389,8 @@ int32_t AggFinalizeImpl(Agg* a) {
   g_dev = pin32[kMaxKeys + 1];
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
   if (g_dev != ngroups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, ngroups);
-  for (int k = 0; k < a->n_keys && n_str > 0; ++k) {
-    if (a->key_types[k] != PXG_STRING) continue;
-    R.key_data_len[k] = totals[k];
-    PXG_RETURN_IF_ERROR(R.key_data[k].Ensure(static_cast<size_t>(totals[k]) + 16));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "key_string_copy", KeyStringCopyKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), k, static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
-                               a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(),
-                               static_cast<const uint32_t*>(R.key_offsets[k].as<uint32_t>()), R.key_data[k].as<uint8_t>()));
-  }
+  for (int k = 0; k < a->n_keys; ++k)
+    if (a->key_types[k] == PXG_STRING) R.key_data_len[k] = totals[k];
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   R.ready = true;
   return PXG_OK;

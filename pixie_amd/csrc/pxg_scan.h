@@ -15,5 +15,8 @@ constexpr int kScanTile = kScanBlock * kScanItems;
 size_t ScanScratchBytes(int64_t n);
 int32_t ScanExclusiveU64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, void* scratch);
 int32_t ScanExclusiveU32(Ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch);
+// The same on another stream of ctx (its own scratch: scans on different streams may overlap).
+int32_t ScanExclusiveU32On(Ctx* ctx, hipStream_t stream, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total,
+                           void* scratch);
 
 }  // namespace pxg

@@ -86,30 +86,35 @@ size_t ScanScratchBytes(int64_t n) {
 }
 
 template <typename T>
-static int32_t ScanImpl(Ctx* ctx, const T* in, T* out, int64_t n, T* total, uint8_t* scratch) {
+static int32_t ScanImpl(Ctx* ctx, hipStream_t stream, const T* in, T* out, int64_t n, T* total, uint8_t* scratch) {
   if (n <= 0) {
-    if (total) PXG_HIP(hipMemsetAsync(total, 0, sizeof(T), ctx->stream));
+    if (total) PXG_HIP(hipMemsetAsync(total, 0, sizeof(T), stream));
     return PXG_OK;
   }
   int64_t nblocks = (n + kScanTile - 1) / kScanTile;
   if (nblocks == 1) {
-    return Launch(ctx, "scan_downsweep", ScanDownsweepKernel<T>, dim3(1), dim3(kScanBlock), 0, in, out, n,
-                  static_cast<const T*>(nullptr), total);
+    return LaunchOn(ctx, stream, "scan_downsweep", ScanDownsweepKernel<T>, dim3(1), dim3(kScanBlock), 0, in, out, n,
+                    static_cast<const T*>(nullptr), total);
   }
   T* sums = reinterpret_cast<T*>(scratch);
   uint8_t* rest = scratch + (static_cast<size_t>(nblocks) + 16) * sizeof(uint64_t);
-  PXG_RETURN_IF_ERROR(Launch(ctx, "scan_reduce", ScanReduceKernel<T>, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock), 0,
-                             in, n, sums));
-  PXG_RETURN_IF_ERROR(ScanImpl<T>(ctx, sums, sums, nblocks, static_cast<T*>(nullptr), rest));
-  return Launch(ctx, "scan_downsweep", ScanDownsweepKernel<T>, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock), 0, in,
-                out, n, static_cast<const T*>(sums), total);
+  PXG_RETURN_IF_ERROR(LaunchOn(ctx, stream, "scan_reduce", ScanReduceKernel<T>, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock),
+                               0, in, n, sums));
+  PXG_RETURN_IF_ERROR(ScanImpl<T>(ctx, stream, sums, sums, nblocks, static_cast<T*>(nullptr), rest));
+  return LaunchOn(ctx, stream, "scan_downsweep", ScanDownsweepKernel<T>, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock), 0,
+                  in, out, n, static_cast<const T*>(sums), total);
 }
 
 int32_t ScanExclusiveU64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, void* scratch) {
-  return ScanImpl<uint64_t>(ctx, in, out, n, total, static_cast<uint8_t*>(scratch));
+  return ScanImpl<uint64_t>(ctx, ctx->stream, in, out, n, total, static_cast<uint8_t*>(scratch));
 }
 int32_t ScanExclusiveU32(Ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch) {
-  return ScanImpl<uint32_t>(ctx, in, out, n, total, static_cast<uint8_t*>(scratch));
+  return ScanImpl<uint32_t>(ctx, ctx->stream, in, out, n, total, static_cast<uint8_t*>(scratch));
+}
+
+int32_t ScanExclusiveU32On(Ctx* ctx, hipStream_t stream, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total,
+                           void* scratch) {
+  return ScanImpl<uint32_t>(ctx, stream, in, out, n, total, static_cast<uint8_t*>(scratch));
 }
 
 }  // namespace pxg
