@@ -823,8 +823,14 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   const int64_t rows = end - begin;
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
   PXG_RETURN_IF_ERROR(deferred[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
-  PXG_RETURN_IF_ERROR(d_ranges.Ensure(ranges.size() * sizeof(TileRange)));
-  PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), ranges.size() * sizeof(TileRange), hipMemcpyHostToDevice, ctx->stream));
+  // The tile ranges of a repeated consume (same table, same rows) are already on the device.
+  const size_t rbytes = ranges.size() * sizeof(TileRange);
+  if (rbytes != last_ranges.size() || std::memcmp(last_ranges.data(), ranges.data(), rbytes) != 0) {
+    PXG_RETURN_IF_ERROR(d_ranges.Ensure(rbytes));
+    PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), rbytes, hipMemcpyHostToDevice, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));  // `ranges` is pageable and goes out of scope
+    last_ranges.assign(reinterpret_cast<const uint8_t*>(ranges.data()), reinterpret_cast<const uint8_t*>(ranges.data()) + rbytes);
+  }
   PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
   void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t) = AggConsumeKernel;

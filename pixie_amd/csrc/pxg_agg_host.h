@@ -53,6 +53,7 @@ struct Agg {
                     // u32 @32 import inserts, @36 import error flags
   DevBuf deferred[2];
   DevBuf d_ranges;
+  std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint64_t inserted = 0;     // host mirror
@@ -80,7 +81,7 @@ struct Agg {
   // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).
   struct FinalizeWs {
     DevBuf skey[2], sval[2][kMaxVals], rank;
-    DevBuf hist, scan, scan2, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
+    DevBuf hist, scan, scan2, cgroup, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
     DevBuf keysA, keysB, bstarts, big, bchunks;
     DevBuf chain_list, chain_nc, chain_starts;
   } ws;

@@ -233,22 +233,25 @@ __global__ void GroupChunkCountKernel(const uint32_t* __restrict__ gstart, uint3
   cbase[g] = (gstart[g + 1] - gstart[g] + kRedChunk - 1) / kRedChunk;
 }
 
+// chunk -> group map (one thread per group writes its chunks), so a chunk's wave finds its
+// group with one load instead of a binary search over cbase.
+__global__ void ChunkGroupKernel(const uint32_t* __restrict__ cbase, uint32_t ngroups, uint32_t* __restrict__ cgroup) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  for (uint32_t c = cbase[g]; c < cbase[g + 1]; ++c) cgroup[c] = g;
+}
+
 // Partial state per (uda, chunk): SUM/MINSUM/MEAN = sum (int64 bits or double bits),
 // MIN/MAX = order-preserving int64 of the extreme (NaN skipped), COUNT unused.
 __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
-                                                         const uint32_t* __restrict__ cbase, uint32_t ngroups, ConstValPtrs vals,
-                                                         uint64_t* __restrict__ partial, uint64_t pstride) {
+                                                         const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ cgroup,
+                                                         uint32_t ngroups, ConstValPtrs vals, uint64_t* __restrict__ partial,
+                                                         uint64_t pstride) {
   const int lane = threadIdx.x & 63;
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nchunks = cbase[ngroups];
   if (w >= nchunks) return;
-  uint32_t lo = 0, hi = ngroups;  // last g with cbase[g] <= w
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (cbase[mid] <= w) lo = mid;
-    else hi = mid;
-  }
-  const uint32_t g = lo;
+  const uint32_t g = cgroup[w];
   const uint32_t s = gstart[g] + (w - cbase[g]) * kRedChunk;
   const uint32_t e = min(gstart[g + 1], s + kRedChunk);
   for (int u = 0; u < plan->n_udas; ++u) {
@@ -1231,9 +1234,12 @@ int32_t AggFinalizeImpl(Agg* a) {
                                ngroups, cbase));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
     PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 2 * 8));
+    PXG_RETURN_IF_ERROR(ws.cgroup.Ensure(max_chunks * 4 + 16));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                               static_cast<const uint32_t*>(cbase), ngroups, ws.cgroup.as<uint32_t>()));
     PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceKernel, dim3(static_cast<unsigned>((max_chunks * 64 + 255) / 256)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups, cv,
-                               ws.partial.as<uint64_t>(), max_chunks));
+                               a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase),
+                               ws.cgroup.as<const uint32_t>(), ngroups, cv, ws.partial.as<uint64_t>(), max_chunks));
   }
   uint8_t* states = nullptr;
   if (a->emit_states && a->state_rec > 0) {
