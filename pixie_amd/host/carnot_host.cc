@@ -2051,18 +2051,58 @@ class ExecutionGraph {
   const TableStore* store_ = nullptr;
 };
 
-// PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).
+// PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).  The buffer
+// is malloc'ed, sized up front and handed to the caller as is (pxc_free), so a result is
+// written once: no growth copies and no second copy-out.
 struct Writer {
-  std::vector<uint8_t> buf;
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  ~Writer() { std::free(p); }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    uint8_t* q = static_cast<uint8_t*>(std::realloc(p, c));
+    if (!q) throw std::bad_alloc();
+    p = q;
+    cap = c;
+  }
+  uint8_t* claim(size_t k) {
+    if (n + k > cap) reserve(std::max(cap * 2, n + k + 4096));
+    uint8_t* at = p + n;
+    n += k;
+    return at;
+  }
   template <typename V>
   void put(V v) {
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
-    buf.insert(buf.end(), p, p + sizeof(V));
+    std::memcpy(claim(sizeof(V)), &v, sizeof(V));
   }
-  void bytes(const void* p, size_t n) {
-    if (n) buf.insert(buf.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
+  void bytes(const void* src, size_t k) {
+    if (k) std::memcpy(claim(k), src, k);
+  }
+  uint8_t* release(int64_t* len) {
+    *len = static_cast<int64_t>(n);
+    if (!p) p = static_cast<uint8_t*>(std::malloc(1));
+    uint8_t* r = p;
+    p = nullptr;
+    n = cap = 0;
+    return r;
   }
 };
+
+// Bytes WriteBatch will append for rb.
+static size_t BatchBytes(const RowBatch& rb) {
+  const size_t n = static_cast<size_t>(rb.num_rows);
+  size_t b = 8 + 4 + 4;
+  for (auto& c : rb.cols) {
+    b += 4;
+    switch (c.type) {
+      case B: b += n; break;
+      case U: b += n * 16; break;
+      case S: b += 4 * (n + 1) + (n ? static_cast<size_t>(c.offsets[n] - c.offsets[0]) : 0); break;
+      default: b += n * 8; break;
+    }
+  }
+  return b;
+}
 
 static void WriteBatch(Writer* w, const RowBatch& rb) {
   w->put<int64_t>(rb.num_rows);
@@ -2078,7 +2118,18 @@ static void WriteBatch(Writer* w, const RowBatch& rb) {
       case U: w->bytes(c.values, n * 16); break;
       case S: {
         const int32_t o0 = n ? c.offsets[0] : 0;
-        for (size_t i = 0; i <= n; ++i) w->put<int32_t>(n ? c.offsets[i] - o0 : 0);
+        int32_t* dst = reinterpret_cast<int32_t*>(w->claim(4 * (n + 1)));
+        if (!n) {
+          const int32_t z = 0;
+          std::memcpy(dst, &z, 4);
+        } else if (o0 == 0) {
+          std::memcpy(dst, c.offsets, 4 * (n + 1));
+        } else {
+          for (size_t i = 0; i <= n; ++i) {
+            const int32_t v = c.offsets[i] - o0;
+            std::memcpy(dst + i, &v, 4);
+          }
+        }
         if (n) w->bytes(c.data + o0, static_cast<size_t>(c.offsets[n] - o0));
         break;
       }
@@ -2260,6 +2311,12 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   if (!s.ok()) return Fail(s);
   clk.Mark("execute (total)");
   Writer w;
+  size_t total = 8;
+  for (auto* sk : g.sinks_) {
+    total += 8 + sk->name.size();
+    for (auto& rb : sk->batches) total += BatchBytes(rb);
+  }
+  w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
   for (auto* sk : g.sinks_) {
@@ -2268,8 +2325,7 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
     w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
     for (auto& rb : sk->batches) WriteBatch(&w, rb);
   }
-  *out_len = static_cast<int64_t>(w.buf.size());
-  *out = CopyOut(w.buf);
+  *out = w.release(out_len);
   if (grpc_out) {  // "PXGS": per GRPC sink, its destination source id and RowBatchData messages
     Writer gw;
     gw.put<uint32_t>(0x53475850u);
@@ -2282,8 +2338,7 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
         gw.bytes(m.data(), m.size());
       }
     }
-    *grpc_out_len = static_cast<int64_t>(gw.buf.size());
-    *grpc_out = CopyOut(gw.buf);
+    *grpc_out = gw.release(grpc_out_len);
   }
   clk.Mark("PXRB serialise");
   return PXG_OK;
@@ -2341,7 +2396,6 @@ extern "C" int32_t pxc_rowbatch_from_proto(const uint8_t* msg, int64_t len, uint
   w.bytes(name.data(), name.size());
   w.put<uint32_t>(1);
   WriteBatch(&w, rb);
-  *out_len = static_cast<int64_t>(w.buf.size());
-  *out = CopyOut(w.buf);
+  *out = w.release(out_len);
   return PXG_OK;
 }
