@@ -413,17 +413,27 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
     const uint32_t n = gstart[g + 1] - gstart[g];
     cls = n <= kTinyMax ? 0 : (n <= kSmallMax ? 1 : (n <= mid_max ? 2 : 3));
   }
-  // Wave-aggregated list appends: one atomic per class per wave.
+  // Block-aggregated list appends: wave leaders reserve within the block in LDS, then one
+  // global atomic per class per block (the four class counters are hot addresses).
+  __shared__ uint32_t s_cnt[kNumClasses], s_base[kNumClasses];
+  if (threadIdx.x < kNumClasses) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t wofs[kNumClasses];
+  unsigned long long wm[kNumClasses];
 #pragma unroll
   for (int c = 0; c < kNumClasses; ++c) {
-    const unsigned long long m = __ballot(cls == c);
-    if (!m) continue;
-    const int leader = __ffsll(static_cast<long long>(m)) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&counts[c], static_cast<uint32_t>(__popcll(m)));
-    base = __shfl(base, leader, 64);
-    if (cls == c) lists[static_cast<uint64_t>(c) * ngroups + base + __popcll(m & lanemask_lt)] = g;
+    wm[c] = __ballot(cls == c);
+    const int leader = wm[c] ? __ffsll(static_cast<long long>(wm[c])) - 1 : 0;
+    uint32_t o = 0;
+    if (wm[c] && lane == leader) o = atomicAdd(&s_cnt[c], static_cast<uint32_t>(__popcll(wm[c])));
+    wofs[c] = __shfl(o, leader, 64);
   }
+  __syncthreads();
+  if (threadIdx.x < kNumClasses) s_base[threadIdx.x] = s_cnt[threadIdx.x] ? atomicAdd(&counts[threadIdx.x], s_cnt[threadIdx.x]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < kNumClasses; ++c)
+    if (cls == c) lists[static_cast<uint64_t>(c) * ngroups + s_base[c] + wofs[c] + __popcll(wm[c] & lanemask_lt)] = g;
 }
 
 __device__ __forceinline__ uint64_t BitonicStepWave(uint64_t x, int lane, int k, int j) {
