@@ -41,13 +41,23 @@ __global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* _
   __syncthreads();
   const int wid = threadIdx.x >> 6;
   const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
-#pragma unroll 4
+  // Every key load first, then every rank gather, then the counts: the tile's loads are all
+  // in flight together.
+  uint32_t kk[kRadixItems];
+#pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
     const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
-    if (i < n) {
-      const uint32_t key = DenseKey(keys[i], rank, cap, G);
-      atomicAdd(&h[wid][(key >> shift) & (kRadixBuckets - 1)], 1u);
-    }
+    kk[k] = i < n ? keys[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    kk[k] = i < n ? DenseKey(kk[k], rank, cap, G) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    if (i < n) atomicAdd(&h[wid][(kk[k] >> shift) & (kRadixBuckets - 1)], 1u);
   }
   __syncthreads();
   const int d = threadIdx.x;
