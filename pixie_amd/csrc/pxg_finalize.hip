@@ -1046,7 +1046,14 @@ __global__ void KeyStringCopyKernel(const AggPlanDev* __restrict__ plan, int key
   const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[key].a);
   const uint32_t len = static_cast<uint32_t>(k.v[key].b);
   uint8_t* dst = data + offs[g];
-  for (uint32_t i = 0; i < len; ++i) dst[i] = src[i];
+  // 8-byte unaligned word copies (gfx950 serves unaligned global accesses), bytes for the tail.
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t x;
+    __builtin_memcpy(&x, src + i, 8);
+    __builtin_memcpy(dst + i, &x, 8);
+  }
+  for (; i < len; ++i) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------------------
