@@ -8,6 +8,14 @@ pxg_agg_consume (filter + map + group-key hash + staging) -> [N>1: export partia
 RCCL all-to-all by key hash, import] -> pxg_agg_finalize (group sort, count/mean reductions,
 t-digest quantiles, key extraction) — finalized result columns on device.
 
+Legs after the timed region (none of them is inside it):
+  * engine_query: the unmodified binary C2 plan through the C++ engine (pxc_execute_plan).
+  * cpu_baseline + parity (rank 0, N=1): the CPU Carnot restatement (oracle/) runs the C2 plan
+    over the SAME rows (regenerated on the host, bit-identical to the device generator) as
+    1024-row RowBatches; its execution window is the baseline and its result is compared with
+    the device result (tests/parity.py bars) -> "parity".
+  * n1 (N=1): the north-star configuration, 1B rows of http_events on one GPU, same step.
+
 Prints ONE JSON line on rank 0 (the driver's contract).
 """
 from __future__ import annotations
@@ -23,6 +31,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 20250117
+N_PAIR_KEYS = 10_000_000
 KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_init", "slot_flags", "slot_gslot", "group_heads",
            "radix_hist", "radix_scatter",
            "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
@@ -39,12 +48,15 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows-per-gpu", type=int, default=None,
                     help="default: 100M at N=1 (configs[1], C2); 125M per GPU at N>1 (configs[3], C4: 1B rows at N=8)")
+    ap.add_argument("--n1-rows", type=int, default=1_000_000_000,
+                    help="rows of the north-star 1-GPU leg (N=1 only; 0 disables)")
+    ap.add_argument("--n1-steps", type=int, default=5)
     ap.add_argument("--gen-slice", type=int, default=16_000_000)
-    ap.add_argument("--cpu-sample-rows", type=int, default=160_000_000)
     ap.add_argument("--cpu-batch-rows", type=int, default=1024)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (cpu_baseline and parity)")
     ap.add_argument("--no-engine-leg", action="store_true",
                     help="skip the engine query leg (profiling runs: keeps per-kernel averages to the timed steps)")
+    ap.add_argument("--host-gen", action="store_true", help="generate on the host and upload (default: device generator)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
     ap.add_argument("--share-gpu0", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (with --backend gloo on a 1-GPU box)")
@@ -55,6 +67,25 @@ def parse():
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
+
+
+def alg_bytes_of(table, n):
+    """every referenced input column once, Arrow layout (INT64 8 B; STRING 4 B
+    offset + payload, from the table's own offsets)."""
+    from pixie_amd import plans as P
+    return 8 * n + 8 * n + table.device_bytes(P.HE["service"]) + table.device_bytes(P.HE["req_path"])
+
+
+def pmc_traffic(args, n):
+    if not os.path.exists(args.pmc_file):
+        return None
+    try:
+        pm = json.load(open(args.pmc_file))
+        if pm.get("rows_per_gpu") == n and pm.get("kernel") == "agg_consume":
+            return pm.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
 
 
 def main():
@@ -84,29 +115,28 @@ def main():
     ctx = Ctx(local_rank, handle=engine.ctx_handle())
     engine.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
     t0 = time.time()
-    svc_bytes = path_bytes = 0
-    for a in range(0, n, args.gen_slice):
-        m = min(args.gen_slice, n - a)
-        cols = datagen_http_events(SEED, row0 + a, m, n_pair_keys=10_000_000, threads=16)
-        svc_bytes += int(cols[2].offsets[-1])
-        path_bytes += int(cols[3].offsets[-1])
-        engine.append("http_events", cols)
-        del cols
-    assert engine.num_rows("http_events") == n
     table = Table(ctx, P.HTTP_TYPES, handle=engine.device_table("http_events"), owned=False)
-    log(rank, f"[bench] generated + uploaded {n} rows/rank in {time.time() - t0:.1f}s "
-              f"({table.num_chunks} chunks)")
-    # Algorithmic bytes: every referenced column once in Arrow layout.
-    alg_bytes = 8 * n + 8 * n + (4 * n + svc_bytes) + (4 * n + path_bytes)
+    if args.host_gen:
+        for a in range(0, n, args.gen_slice):
+            m = min(args.gen_slice, n - a)
+            engine.append("http_events", datagen_http_events(SEED, row0 + a, m, n_pair_keys=N_PAIR_KEYS, threads=16))
+    else:
+        table.append_http_events(SEED, row0, n, N_PAIR_KEYS)
+    assert engine.num_rows("http_events") == n
+    log(rank, f"[bench] {'host-generated + uploaded' if args.host_gen else 'device-generated'} {n} rows/rank "
+              f"in {time.time() - t0:.1f}s ({table.num_chunks} chunks)")
+    alg_bytes = alg_bytes_of(table, n)
 
     q = LinearQuery(P.c2_plan(with_pluck=True), P.HTTP_TYPES, expected_groups=65536)
     agg = q.make_agg(ctx)
+    exch = {"bytes_sent": 0, "bytes_recv": 0}
 
     def step():
         agg.reset()
         agg.consume(table)
         if world > 1:
-            exchange_partials(agg)
+            s, r = exchange_partials(agg)
+            exch["bytes_sent"], exch["bytes_recv"] = s, r
         return agg.finalize()
 
     for _ in range(args.warmup):
@@ -150,15 +180,8 @@ def main():
     value = total_rows * args.steps / elapsed
     avg_launch_ms = cons_ms / max(launches, 1)
     achieved = alg_bytes / (avg_launch_ms / 1000.0) / 1e9 if launches else None
-
-    traffic = None
-    if os.path.exists(args.pmc_file):
-        try:
-            pm = json.load(open(args.pmc_file))
-            if pm.get("rows_per_gpu") == n and pm.get("kernel") == "agg_consume":
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    dev_result = agg.result() if (world == 1 and rank == 0 and not args.no_cpu_baseline) else None
+    traffic = pmc_traffic(args, n)
 
     # Engine leg (N=1): the unmodified binary C2 plan through pxc_execute_plan over the stored
     # table: fused consume + finalize + result D2H + quantile JSON + pluck + PXRB serialisation.
@@ -177,9 +200,18 @@ def main():
                         "path": "pxc_execute_plan (C++ engine, include/pxcarnot.h) over the HBM-resident stored table: "
                                 "fused consume + finalize + result D2H + quantiles JSON + pluck_float64 + PXRB"}
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
+    cpu, par = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, par = oracle_leg(args, n, row0, dev_result)
+    elif world > 1:
+        par = {"skipped": "N>1: shard-exchange parity is tests/test_scale_parity.py (8-way) and tests/test_partial.py"}
+
+    # North-star leg (N=1): the same step over 1B rows on one GPU.
+    n1 = None
+    if world == 1 and args.n1_rows > 0:
+        agg.close()
+        engine.drop_table("http_events")
+        n1 = n1_leg(args, ctx, P, Table, LinearQuery)
 
     if rank == 0:
         line = {
@@ -194,7 +226,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64/f64",
-            "data": "synthetic http_events (counter-based splitmix64, seed 20250117; SURVEY.md §8d spec), HBM-resident",
+            "data": "synthetic http_events (counter-based splitmix64, seed 20250117; SURVEY.md §8d spec), generated in HBM",
             "config": {
                 "workload": "C2: Filter(resp_status>=400) -> Map(latency_ms=latency/1e6) -> BlockingAgg by (service, req_path): "
                             "count, mean, quantiles -> pluck p50/p99",
@@ -203,6 +235,7 @@ def main():
                 "algorithmic_bytes_per_row": alg_bytes / n,
                 "kernel_ms_per_step": kernel_ms,
                 "step_rate_gbs_algorithmic": alg_bytes * world / (ms_per_step / 1000.0) / 1e9,
+                "exchange_bytes_per_rank": exch if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -216,10 +249,13 @@ def main():
                 "avg_launch_ms": avg_launch_ms,
             },
             "cpu_baseline": cpu,
+            "parity": par,
             "engine_query": engine_query,
+            "n1": n1,
         }
         print(json.dumps(line), flush=True)
-    agg.close()
+    if world > 1 or args.n1_rows <= 0:
+        agg.close()
     table.close()
     ctx.close()
     engine.close()
@@ -227,25 +263,76 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args):
-    """The CPU Carnot restatement (oracle/, single thread) on a bounded sample of the same
-    workload: the first cpu_sample_rows rows of the same synthetic table, as RowBatches of
-    cpu_batch_rows rows, C2 plan.  Columns the plan does not read are not materialised."""
+def n1_leg(args, ctx, P, Table, LinearQuery):
+    """BASELINE north_star: 1B-row filter + group-by(service, req_path) with count/mean/p50/p99
+    on ONE GPU (the config the >= 60% of HBM roofline target is quoted on)."""
+    n = args.n1_rows
+    t0 = time.time()
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(SEED, 0, n, N_PAIR_KEYS)
+    gen_s = time.time() - t0
+    alg = alg_bytes_of(t, n)
+    q = LinearQuery(P.c2_plan(with_pluck=True), P.HTTP_TYPES, expected_groups=65536)
+    a = q.make_agg(ctx)
+
+    def step():
+        a.reset()
+        a.consume(t)
+        return a.finalize()
+
+    g = step()
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_profiling(True, only="agg_consume")
+    ctx.sync()
+    ts = time.perf_counter()
+    for _ in range(args.n1_steps):
+        g = step()
+    ctx.sync()
+    el = time.perf_counter() - ts
+    ctx.set_profiling(False)
+    l, ms = ctx.kernel_stats("agg_consume")
+    avg = ms / max(l, 1)
+    achieved = alg / (avg / 1000.0) / 1e9
+    out = {
+        "workload": "north_star: 1B-row http_events on 1 GPU, Filter(resp_status>=400) -> Map -> Agg by (service, req_path): "
+                    "count, mean, quantiles (p50/p99 plucked)",
+        "rows": n, "steps": args.n1_steps, "ms_per_step": el * 1000.0 / args.n1_steps,
+        "value": n * args.n1_steps / el, "unit": "rows/s", "groups": g, "selected_rows": a.rows_selected(),
+        "algorithmic_bytes_per_row": alg / n, "generate_s": gen_s,
+        "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n), "algorithmic_bytes_per_launch": alg,
+                     "avg_launch_ms": avg},
+        "cpu_baseline": "same CPU Carnot restatement as the top-level cpu_baseline (rows/s of one thread; the plan is per-row linear)",
+    }
+    a.close()
+    t.close()
+    return out
+
+
+def oracle_leg(args, n, row0, dev_result):
+    """The CPU Carnot restatement (oracle/, one thread) over the same n rows as the GPU table, as
+    cpu_batch_rows-row RowBatches, C2 plan: its execution window is cpu_baseline; its result is
+    the parity reference for the device result of the timed steps (tests/parity.py)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     try:
+        import numpy as np
         import oracle_client as oc
+        import parity
         from pixie_amd import plans as P
         from pixie_amd.device import datagen_http_events
-        m = args.cpu_sample_rows
         need = {P.HE["service"], P.HE["req_path"], P.HE["resp_status"], P.HE["latency"]}
-        batches = []
-        for a in range(0, m, args.gen_slice):
-            k = min(args.gen_slice, m - a)
-            cols = datagen_http_events(SEED, a, k, n_pair_keys=10_000_000, threads=16)
+        batches, keys, sel, vals = [], [], [], []
+        for a in range(0, n, args.gen_slice):
+            k = min(args.gen_slice, n - a)
+            cols = datagen_http_events(SEED, row0 + a, k, n_pair_keys=N_PAIR_KEYS, threads=16)
             batches.append([c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)])
+            keys.append([cols[P.HE["service"]], cols[P.HE["req_path"]]])
+            sel.append(cols[P.HE["resp_status"]].values >= 400)
+            vals.append(cols[P.HE["latency"]].values / 1e6)
             del cols
         tables = {"http_events": {"types": P.HTTP_TYPES, "batches": batches, "names": P.HTTP_NAMES}}
-        secs, _ = oc.time_plan(P.c2_plan(with_pluck=True), tables, batch_rows=args.cpu_batch_rows)
+        secs, res = oc.execute_plan_timed(P.c2_plan(with_pluck=False), tables, batch_rows=args.cpu_batch_rows)
         cpu_model = ""
         try:
             for line in open("/proc/cpuinfo"):
@@ -254,12 +341,27 @@ def cpu_baseline(args):
                     break
         except OSError:
             pass
-        return {"value": m / secs, "unit": "rows/s", "cores": 1, "kind": "port",
-                "sample": f"first {m} rows of the same synthetic table as {args.cpu_batch_rows}-row RowBatches, C2 plan, "
-                          f"1 thread of {cpu_model or 'host CPU'}; {secs:.2f} s execution window (first GenerateNext .. "
-                          f"last emit, BASELINE.md); CPU Carnot restated in oracle/ (reference unbuildable, SURVEY.md §8c)"}
-    except Exception as e:  # the baseline must never break the bench line
-        return {"value": None, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
+        cpu = {"value": n / secs, "unit": "rows/s", "cores": 1, "kind": "port",
+               "sample": f"all {n} rows of the bench table (regenerated on the host, bit-identical to the device generator) "
+                         f"as {args.cpu_batch_rows}-row RowBatches, C2 plan (quantiles JSON, no pluck), 1 thread of "
+                         f"{cpu_model or 'host CPU'}; {secs:.2f} s execution window (first GenerateNext .. last emit); "
+                         f"CPU Carnot restated in oracle/ (reference unbuildable, SURVEY.md §8c)"}
+        par = None
+        if dev_result is not None:
+            ref = res["output"][0]["cols"]
+            t0 = time.time()
+            rep = parity.compare_agg(dev_result, ref, 2, ["count", "rel", "quantiles"], parity.GroupValues(keys, sel, vals))
+            rep["rows"] = n
+            rep["check_s"] = round(time.time() - t0, 2)
+            rep["bars"] = ("groups/counts bit-exact; mean 1e-6 rel; quantiles <= 4 ULP for groups <= 8000 values, "
+                           "midpoint-rank bound 2*pi*sqrt(q(1-q))/1000 + 1/n above")
+            par = rep
+        return cpu, par
+    except Exception as e:  # the legs must never break the bench line
+        import traceback
+        traceback.print_exc()
+        return ({"value": None, "unit": "rows/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"},
+                {"ok": False, "error": f"oracle leg failed: {e}"})
 
 
 if __name__ == "__main__":

@@ -45,6 +45,11 @@ typedef struct {
   const uint8_t* batch_flags;
 } pxc_table;
 
+/* Threading: every pxc_* call that takes an engine holds the engine's lock for its duration,
+ * so concurrent callers are serialised (the store, group-count hints, aggregation cache and
+ * the engine's device stream are shared by all queries on one engine).  For concurrent query
+ * execution, create one engine per query thread (Carnot runs each query on its own task,
+ * src/vizier/services/agent/manager/exec.cc:84-97). */
 typedef struct pxc_engine pxc_engine;
 
 int32_t pxc_engine_create(int32_t device, pxc_engine** out);
@@ -111,6 +116,9 @@ int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t
                                 const pxc_table* tables, char** out);
 
 void pxc_free(void* p);
+/* QuantilesUDA::Finalize JSON (math_sketches.h:40-54, bytes as rapidjson's Writer emits them)
+ * for n groups of 7 doubles (p01..p99): one buffer of n NUL-terminated strings (pxc_free). */
+int32_t pxc_quantiles_json(const double* q7, int64_t n, char** out, int64_t* out_len);
 const char* pxc_last_error(void);
 
 #ifdef __cplusplus

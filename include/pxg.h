@@ -284,6 +284,17 @@ void pxg_result_free(pxg_column_out* cols, int32_t n_cols);
 int32_t pxg_agg_reset(pxg_agg* agg);
 /* Number of selected (post-filter) rows consumed since the last reset. */
 int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows);
+/* Sizes of an aggregation's device state (ExecNodeStats-style accounting, exec_node.h:41-128). */
+typedef struct {
+  int64_t table_capacity;   /* slots of the open-addressing group table */
+  int64_t groups;           /* groups inserted since the last reset */
+  int64_t rows_selected;    /* staged (post-filter) rows since the last reset */
+  int64_t key_arena_bytes;  /* published group-key records */
+  int64_t staging_capacity; /* staged rows the buffers hold without growing */
+  int32_t fast_path_keys;   /* key count of the register-key consume kernel; 0 = generic kernel */
+  int32_t reserved;
+} pxg_agg_stats;
+int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* stats);
 
 /* Partial aggregation (plan.proto:250-257).  Export serialises every group's key and UDA
  * state (quantile inputs as raw values) into n_parts device buffers partitioned by
@@ -335,6 +346,11 @@ int32_t pxg_join(pxg_table* build, pxg_table* probe, const pxg_join_spec* spec, 
 #define PXG_HTTP_EVENTS_NCOLS 10
 int32_t pxg_datagen_http_events(uint64_t seed, int64_t row_begin, int64_t nrows,
                                 int64_t n_addr_keys, int32_t n_threads, pxg_column_out* cols);
+/* The same rows generated on the device and appended to an http_events-shaped table (the 10
+ * columns above), bit-identical to pxg_datagen_http_events: big bench tables are built in HBM
+ * without host generation or PCIe upload.  Synchronises. */
+int32_t pxg_table_append_http_events(pxg_table* t, uint64_t seed, int64_t row_begin, int64_t nrows,
+                                     int64_t n_addr_keys);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 // the "CPU Carnot (restated)" baseline that bench.py times.
 
 #include "carnot_oracle.h"
+#include "../pixie_amd/host/json_double.h"
 
 #include <algorithm>
 #include <array>
@@ -313,32 +314,16 @@ Registry::Registry() {
 /*********************************************************************************************
  * UDAs (math_ops.h:583-772, math_sketches.h:33-82, agg_node_test.cc:44-72 test UDAs).
  *********************************************************************************************/
-std::string FormatJsonDouble(double v) {
-  // Shortest round-trip rendering, always with a '.' or exponent so that rapidjson reads it back
-  // as a double (IsDouble) — the property pluck_float64 depends on.
-  if (std::isnan(v) || std::isinf(v)) return "null";
-  char buf[64];
-  for (int prec = 1; prec <= 17; ++prec) {
-    snprintf(buf, sizeof(buf), "%.*g", prec, v);
-    if (std::strtod(buf, nullptr) == v) break;
-  }
-  std::string s(buf);
-  if (s.find_first_of(".eEn") == std::string::npos) s += ".0";
-  return s;
-}
-
+// QuantilesUDA::Finalize (math_sketches.h:40-54): rapidjson Document written by
+// rapidjson::Writer -- restated in pixie_amd/host/json_double.h (pinned by
+// tests/test_json_double.py against the reference's own known strings and rapidjson's rules).
 std::string QuantilesJson(TDigest* d) {
-  static const char* kNames[7] = {"p01", "p10", "p25", "p50", "p75", "p90", "p99"};
   static const double kQ[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
-  std::string s = "{";
-  for (int k = 0; k < 7; ++k) {
-    if (k) s += ",";
-    s += "\"";
-    s += kNames[k];
-    s += "\":";
-    s += FormatJsonDouble(d->quantile(kQ[k]));
-  }
-  return s + "}";
+  double q[7];
+  for (int k = 0; k < 7; ++k) q[k] = d->quantile(kQ[k]);
+  std::string s;
+  pxjson::AppendQuantilesJson(q, &s);
+  return s;
 }
 
 struct UDA {
@@ -1492,14 +1477,18 @@ static void SetErr(char* errbuf, int32_t errlen, const std::string& m) {
   }
 }
 
-extern "C" int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, const oracle_table* tables,
-                                       uint8_t** out, int64_t* out_len, char* errbuf, int32_t errlen) {
+extern "C" int32_t oracle_execute_plan_rebatched(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                                 int64_t batch_rows, double* seconds, uint8_t** out, int64_t* out_len,
+                                                 char* errbuf, int32_t errlen) {
   try {
     Json plan = ParseJson(plan_json);
-    auto tbl = ImportTables(ntables, tables);
+    auto tbl = ImportTables(ntables, tables, batch_rows);
     Graph g;
     g.Build(plan, tbl);
+    auto t0 = std::chrono::steady_clock::now();
     g.Execute();
+    auto t1 = std::chrono::steady_clock::now();
+    if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
     Writer w;
     w.put<uint32_t>(0x42525850u);  // "PXRB"
     w.put<uint32_t>(static_cast<uint32_t>(g.sinks.size()));
@@ -1520,6 +1509,11 @@ extern "C" int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, c
     SetErr(errbuf, errlen, e.what());
     return INTERNAL;
   }
+}
+
+extern "C" int32_t oracle_execute_plan(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                       uint8_t** out, int64_t* out_len, char* errbuf, int32_t errlen) {
+  return oracle_execute_plan_rebatched(plan_json, ntables, tables, 0, nullptr, out, out_len, errbuf, errlen);
 }
 
 extern "C" int32_t oracle_execute_plan_timed(const char* plan_json, int32_t ntables, const oracle_table* tables,
@@ -1593,4 +1587,54 @@ extern "C" double oracle_pluck_float64(const char* json, const char* key) {
   } catch (...) {
     return 0.0;
   }
+}
+
+// Parity helper for groups whose reference t-digest depends on insertion order (> 8000 values):
+// the midpoint empirical rank F(v) = (#{x < v} + #{x <= v}) / 2n of candidate quantile values
+// within their group.  Rows are grouped by the exact bytes of their key columns (RowTuple
+// equality, row_tuple.h:109-153); sel (optional) masks rows out.  Query q names its group by the
+// same key encoding -- per key column: STRING u32 length + bytes, UINT128 16 bytes, other types
+// their 8 value bytes -- at qkeys[qoffs[q], qoffs[q+1]); out[q * per_q + j] = rank of
+// qv[q * per_q + j] (NaN when the group has no rows).  qcount[q] receives the group's size.
+extern "C" int32_t oracle_group_ranks(const oracle_column* keys, int32_t nk, const uint8_t* sel, const double* vals, int64_t n,
+                                      int32_t nq, const uint8_t* qkeys, const int64_t* qoffs, const double* qv, int32_t per_q,
+                                      double* out, int64_t* qcount) {
+  std::unordered_map<std::string, int32_t> want;
+  for (int32_t q = 0; q < nq; ++q)
+    want.emplace(std::string(reinterpret_cast<const char*>(qkeys + qoffs[q]), static_cast<size_t>(qoffs[q + 1] - qoffs[q])), q);
+  std::vector<std::vector<double>> groups(static_cast<size_t>(nq));
+  std::string k;
+  for (int64_t r = 0; r < n; ++r) {
+    if (sel && !sel[r]) continue;
+    k.clear();
+    for (int32_t c = 0; c < nk; ++c) {
+      const oracle_column& col = keys[c];
+      if (col.type == STRING) {
+        const uint32_t len = static_cast<uint32_t>(col.offsets[r + 1] - col.offsets[r]);
+        k.append(reinterpret_cast<const char*>(&len), 4);
+        k.append(reinterpret_cast<const char*>(col.data) + col.offsets[r], len);
+      } else {
+        const size_t w = col.type == UINT128 ? 16 : 8;
+        k.append(static_cast<const char*>(col.values) + r * w, w);
+      }
+    }
+    auto it = want.find(k);
+    if (it != want.end()) groups[static_cast<size_t>(it->second)].push_back(vals[r]);
+  }
+  for (int32_t q = 0; q < nq; ++q) {
+    std::vector<double>& g = groups[static_cast<size_t>(q)];
+    std::sort(g.begin(), g.end());
+    qcount[q] = static_cast<int64_t>(g.size());
+    for (int32_t j = 0; j < per_q; ++j) {
+      const double v = qv[static_cast<int64_t>(q) * per_q + j];
+      double r = std::numeric_limits<double>::quiet_NaN();
+      if (!g.empty()) {
+        const auto lo = std::lower_bound(g.begin(), g.end(), v) - g.begin();
+        const auto hi = std::upper_bound(g.begin(), g.end(), v) - g.begin();
+        r = (static_cast<double>(lo) + static_cast<double>(hi)) / 2.0 / static_cast<double>(g.size());
+      }
+      out[static_cast<int64_t>(q) * per_q + j] = r;
+    }
+  }
+  return OK;
 }

@@ -57,6 +57,18 @@ int32_t oracle_execute_plan_timed_rebatched(const char* plan_json, int32_t ntabl
                                             double* seconds, int64_t* out_rows, char* errbuf,
                                             int32_t errlen);
 
+// Execute with every batch re-sliced into batch_rows-row RowBatches (0: as given), timing the
+// execution window into *seconds (may be NULL) and returning the result tables as PXRB.
+int32_t oracle_execute_plan_rebatched(const char* plan_json, int32_t ntables, const oracle_table* tables,
+                                      int64_t batch_rows, double* seconds, uint8_t** out, int64_t* out_len,
+                                      char* errbuf, int32_t errlen);
+
+// Midpoint empirical ranks of candidate quantile values within their groups (rank-bound parity
+// for groups whose reference digest depends on insertion order); see carnot_oracle.cc.
+int32_t oracle_group_ranks(const oracle_column* keys, int32_t nk, const uint8_t* sel, const double* vals,
+                           int64_t n, int32_t nq, const uint8_t* qkeys, const int64_t* qoffs,
+                           const double* qv, int32_t per_q, double* out, int64_t* qcount);
+
 void oracle_free(uint8_t* p);
 
 // QuantilesUDA on a value sequence (math_sketches.h:36-54): out[7] = p01,p10,p25,p50,p75,p90,p99.
@@ -64,7 +76,7 @@ void oracle_tdigest_quantiles(const double* vals, int64_t n, double* out7);
 // Two digests built from a and b, then merged (QuantilesUDA::Merge), then the quantiles.
 void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb,
                                     double* out7);
-// The JSON string QuantilesUDA::Finalize would produce (rapidjson-compatible %.17g rendering).
+// The JSON string QuantilesUDA::Finalize would produce (rapidjson Writer bytes, json_double.h).
 int32_t oracle_quantiles_json(const double* vals, int64_t n, char* buf, int32_t buflen);
 // pluck_float64 (json_ops.h:131-153).
 double oracle_pluck_float64(const char* json, const char* key);

@@ -69,6 +69,12 @@ class JoinSpec(C.Structure):
                 ("out_side", C.POINTER(C.c_int32)), ("out_col", C.POINTER(C.c_int32))]
 
 
+class AggStats(C.Structure):
+    _fields_ = [("table_capacity", C.c_int64), ("groups", C.c_int64), ("rows_selected", C.c_int64),
+                ("key_arena_bytes", C.c_int64), ("staging_capacity", C.c_int64), ("fast_path_keys", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 # Every symbol include/pxg.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pxg_abi_version", "pxg_last_error", "pxg_device_count", "pxg_ctx_create", "pxg_ctx_destroy",
@@ -77,8 +83,8 @@ EXPORTED = [
     "pxg_table_append_device", "pxg_table_flush", "pxg_table_num_rows", "pxg_table_num_chunks",
     "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_result_free",
-    "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_export_partial", "pxg_agg_import_partial",
-    "pxg_join", "pxg_datagen_http_events",
+    "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial",
+    "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events",
 ]
 
 _lib = None
@@ -137,11 +143,13 @@ def load() -> C.CDLL:
         "pxg_result_free": (None, [p(ColumnOut), i32]),
         "pxg_agg_reset": (i32, [vp]),
         "pxg_agg_rows_selected": (i32, [vp, p(i64)]),
+        "pxg_agg_info": (i32, [vp, p(AggStats)]),
         "pxg_agg_export_partial": (i32, [vp, i32, vp, i64, p(i64), p(i64)]),
         "pxg_agg_import_partial": (i32, [vp, vp, i64]),
         "pxg_join": (i32, [vp, vp, p(JoinSpec), p(vp), p(i64)]),
         "pxg_table_time_bound": (i32, [vp, i32, i64, i32, p(i64)]),
         "pxg_datagen_http_events": (i32, [C.c_uint64, i64, i64, i64, i32, p(ColumnOut)]),
+        "pxg_table_append_http_events": (i32, [vp, C.c_uint64, i64, i64, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -776,12 +776,13 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   const uint64_t n_new = tot >> kPublishCountShift;
   const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
   if (n_new > 0) {
+    // Slot words hold 32-bit arena offsets: refuse before any record is written.
+    if (arena_words + words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
     PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + kArenaSlack, arena_words * 8, ctx->stream));
     PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
                                d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
                                static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>()));
     arena_words += words;
-    if (arena_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
   }
   inserted += n_new;
   // The device-side fill count restarts from the exact number of groups.
@@ -861,8 +862,14 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   for (int round = 0; n_def > 0; ++round) {
     // Rows are deferred by a full table / overlong probe, or (fast path) by a long string key.
     // Grow unless this is the first retry and the table still has room for every deferred row.
+    // Growth is sized by groups, not rows: deferred rows mostly repeat groups, so the table
+    // grows geometrically (x4 per round, from at least 4x the groups it holds) and the retry
+    // defers again while it is still too small; 4 * (groups + deferred rows) caps it.
     const uint64_t want = static_cast<uint64_t>(inserted) + n_def;
-    if (round > 0 || fast_nk == 0 || want > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(4 * want)));
+    if (round > 0 || fast_nk == 0 || want > static_cast<uint64_t>(cap) * 3 / 8) {
+      const uint64_t geo = std::max<uint64_t>(static_cast<uint64_t>(cap) * 4, static_cast<uint64_t>(inserted) * 4);
+      PXG_RETURN_IF_ERROR(Grow(NextPow2(std::min<uint64_t>(geo, 4 * want))));
+    }
     PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
     PXG_RETURN_IF_ERROR(EnsureStage(st_n + n_def));
     PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
@@ -1079,7 +1086,8 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
   const int64_t expected = spec->expected_groups > 0 ? spec->expected_groups : 4096;
-  PXG_RETURN_IF_ERROR(a.EnsureTable(NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 4, 1024))));
+  a.min_cap = NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 4, 1024));
+  PXG_RETURN_IF_ERROR(a.EnsureTable(a.min_cap));
   PXG_RETURN_IF_ERROR(a.arena.Alloc(1 << 16));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
   *out = holder.release();
@@ -1104,6 +1112,19 @@ extern "C" int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin
   return agg->impl.ConsumeRange(&t, begin, end);
 }
 
+extern "C" int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* st) {
+  if (!agg || !st) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  const Agg& a = agg->impl;
+  st->table_capacity = a.cap;
+  st->groups = static_cast<int64_t>(a.inserted);
+  st->rows_selected = static_cast<int64_t>(a.st_n);
+  st->key_arena_bytes = static_cast<int64_t>(a.arena_words * 8);
+  st->staging_capacity = static_cast<int64_t>(a.st_cap);
+  st->fast_path_keys = a.fast_nk;
+  st->reserved = 0;
+  return PXG_OK;
+}
+
 extern "C" int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows) {
   if (!agg || !rows) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   *rows = static_cast<int64_t>(agg->impl.st_n);
@@ -1113,6 +1134,15 @@ extern "C" int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows) {
 extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   if (!agg) return SetError(PXG_INVALID_ARGUMENT, "agg is null");
   Agg& a = agg->impl;
+  // A table grown far beyond what the last run needed (e.g. an agg reused by a later, smaller
+  // query) is shrunk, so publication and finalize do not keep sweeping empty slots.
+  const uint32_t fit = NextPow2(std::max<uint64_t>(a.inserted * 4, a.min_cap));
+  if (a.cap > 16 * static_cast<uint64_t>(fit)) {
+    PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+    a.slots.Free();
+    a.cap = fit;
+    PXG_RETURN_IF_ERROR(a.slots.Alloc(static_cast<size_t>(a.cap) * 8));
+  }
   PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));  // stream-ordered before the next consume
   a.st_n = 0;

@@ -49,6 +49,7 @@ struct Agg {
   // Global open-addressing table.
   DevBuf slots;
   uint32_t cap = 0;
+  uint32_t min_cap = 1024;  // the capacity the creation hint asked for (reset never shrinks below)
   DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor;
                     // u32 @32 import inserts, @36 import error flags
   DevBuf deferred[2];

@@ -1117,8 +1117,21 @@ int32_t GroupStarts(Ctx* ctx, const uint32_t* skeys, uint64_t n, uint32_t G, uin
   return Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0, skeys, n, G, gstart);
 }
 
+// Side streams forked by finalize are joined back into the main stream on every exit path, so
+// an early error return never leaves side-stream kernels running on workspace buffers that a
+// later reset / Ensure could free or reallocate.
+struct SideJoinGuard {
+  Ctx* ctx;
+  bool side = false, side2 = false;
+  ~SideJoinGuard() {
+    if (side) (void)JoinSide(ctx);
+    if (side2) (void)JoinSide2(ctx);
+  }
+};
+
 int32_t AggFinalizeImpl(Agg* a) {
   Ctx* ctx = a->ctx;
+  SideJoinGuard guard{ctx};
   AggResult& R = a->res;
   Agg::FinalizeWs& ws = a->ws;
   R.Clear();
@@ -1183,6 +1196,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     if (a->n_keys > 0) {
       PXG_RETURN_IF_ERROR(ws.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(ngroups) + 1) + 64));
       PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+      guard.side2 = true;
       PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                                    a->d_plan.as<const AggPlanDev>(), static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
                                    a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
@@ -1331,6 +1345,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     const int32_t* chain_nc = ws.chain_nc.as<const int32_t>();
     // Chains: latency-bound (a few waves, ~1100 dependent steps each), on the side stream.
     PXG_RETURN_IF_ERROR(ForkSide(ctx));
+    guard.side = true;
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain_cap + 63) / 64), dim3(64), 0,
                                  lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), mid_cap,
                                  lists + 3 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 3), gstart,
@@ -1375,6 +1390,7 @@ int32_t AggFinalizeImpl(Agg* a) {
         // chunk list), so it starts alongside the tiny / small digests.
         if (first_big) PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_meta, 0));
         else PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+        guard.side2 = true;
         first_big = false;
         PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
                                      ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
@@ -1390,6 +1406,7 @@ int32_t AggFinalizeImpl(Agg* a) {
         }
       }
       PXG_RETURN_IF_ERROR(JoinSide(ctx));
+      guard.side = false;
       double* qo = R.uda_out[u].as<double>();
       if (cls[2] > 0)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
@@ -1405,6 +1422,7 @@ int32_t AggFinalizeImpl(Agg* a) {
   }
   PXG_RETURN_IF_ERROR(RunBigDigests());
   if (keys_on_side2 || n_big_groups > 0) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
+  guard.side2 = false;
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;

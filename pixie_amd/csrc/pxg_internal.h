@@ -78,6 +78,23 @@ struct DevBuf {
     bytes = cap;
     return PXG_OK;
   }
+  // Capacity >= n without power-of-two rounding (the caller picks the growth policy).
+  int32_t ReserveExact(size_t n, size_t keep, hipStream_t s) {
+    if (n <= bytes) return PXG_OK;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, n);
+    if (e != hipSuccess) return SetError(PXG_RESOURCE_UNAVAILABLE, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    if (keep && p) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return SetError(PXG_INTERNAL, "hipMemcpyAsync failed: %s", hipGetErrorString(e));
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return SetError(PXG_INTERNAL, "sync failed: %s", hipGetErrorString(e));
+    }
+    Free();
+    p = q;
+    bytes = n;
+    return PXG_OK;
+  }
   // Grow-only scratch: capacity >= n, contents not preserved.
   int32_t Ensure(size_t n) { return Reserve(n, 0, nullptr); }
   template <typename T>

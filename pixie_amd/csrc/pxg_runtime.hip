@@ -139,12 +139,16 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
     }
     if (take == 0) continue;  // sealed; next iteration opens a new chunk
     const int64_t r0 = ch->nrows, r1 = ch->nrows + take;
+    // Chunk capacity in rows: exact on the first append, then doubling up to kChunkRows (a
+    // power-of-two byte rounding would waste up to 2x HBM on a full chunk: 1B-row tables).
+    const int64_t cap_rows = r0 == 0 ? r1 : std::max<int64_t>(r1, std::min<int64_t>(kChunkRows, 2 * r0));
     for (int k = 0; k < ncols; ++k) {
       ChunkCol& cc = ch->cols[k];
       const int t = types[k];
       if (t != PXG_STRING) {
         const size_t w = TypeWidth(t);
-        PXG_RETURN_IF_ERROR(cc.values.Reserve(static_cast<size_t>(r1) * w + 16, static_cast<size_t>(r0) * w, ctx->stream));
+        if (cc.values.bytes < static_cast<size_t>(r1) * w + 16)
+          PXG_RETURN_IF_ERROR(cc.values.ReserveExact(static_cast<size_t>(cap_rows) * w + 16, static_cast<size_t>(r0) * w, ctx->stream));
         const uint8_t* src = static_cast<const uint8_t*>(cols[k].values) + static_cast<size_t>(done) * w;
         PXG_HIP(hipMemcpyAsync(cc.values.as<uint8_t>() + static_cast<size_t>(r0) * w, src, static_cast<size_t>(take) * w, kind,
                                ctx->stream));
@@ -160,8 +164,13 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
         PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
       }
       const int64_t bytes = static_cast<int64_t>(o_last) - o_first;
-      PXG_RETURN_IF_ERROR(cc.offsets.Reserve(static_cast<size_t>(r1 + 1) * 4 + 16, static_cast<size_t>(r0 + 1) * 4, ctx->stream));
-      PXG_RETURN_IF_ERROR(cc.data.Reserve(static_cast<size_t>(cc.data_len + bytes) + 16, static_cast<size_t>(cc.data_len), ctx->stream));
+      if (cc.offsets.bytes < static_cast<size_t>(r1 + 1) * 4 + 16)
+        PXG_RETURN_IF_ERROR(cc.offsets.ReserveExact(static_cast<size_t>(cap_rows + 1) * 4 + 16, static_cast<size_t>(r0 + 1) * 4, ctx->stream));
+      const size_t need = static_cast<size_t>(cc.data_len + bytes) + 16;
+      if (cc.data.bytes < need) {
+        const size_t grow = r0 == 0 ? need : std::max(need, std::min(2 * cc.data.bytes, static_cast<size_t>(kMaxChunkData) + 16));
+        PXG_RETURN_IF_ERROR(cc.data.ReserveExact(grow, static_cast<size_t>(cc.data_len), ctx->stream));
+      }
       PXG_HIP(hipMemcpyAsync(cc.data.as<uint8_t>() + cc.data_len, cols[k].data + o_first, static_cast<size_t>(bytes), kind, ctx->stream));
       const int32_t add = static_cast<int32_t>(cc.data_len);
       if (from_host) {

@@ -172,6 +172,11 @@ class Table:
     def flush(self) -> None:
         check(self.lib.pxg_table_flush(self.h))
 
+    def append_http_events(self, seed: int, row_begin: int, nrows: int, n_pair_keys: int = 10_000_000) -> None:
+        """Generate http_events rows on the device straight into this table (bit-identical to
+        datagen_http_events)."""
+        check(self.lib.pxg_table_append_http_events(self.h, seed, row_begin, nrows, n_pair_keys))
+
     @property
     def num_rows(self) -> int:
         return int(self.lib.pxg_table_num_rows(self.h))
@@ -302,6 +307,12 @@ class Agg:
     def import_partial(self, src) -> None:
         """Merge one exported part (a contiguous uint8 device tensor) into this agg."""
         check(self.lib.pxg_agg_import_partial(self.h, C.c_void_p(src.data_ptr()), src.numel()))
+
+    def info(self) -> dict:
+        """pxg_agg_info: device-state sizes (table capacity, groups, staged rows, ...)."""
+        st = _lib.AggStats()
+        check(self.lib.pxg_agg_info(self.h, C.byref(st)))
+        return {f: int(getattr(st, f)) for f, _ in st._fields_ if f != "reserved"}
 
     def rows_selected(self) -> int:
         n = C.c_int64()

@@ -14,7 +14,6 @@
 // math_sketches.h:40-54, and pluck_float64 of it, json_ops.h:131-153) is host-side output
 // formatting, as in the reference, where UDA Finalize runs on the host.
 #include <algorithm>
-#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -24,6 +23,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <sstream>
 #include <string>
@@ -33,6 +33,7 @@
 
 #include "../../include/pxcarnot.h"
 #include "../../include/pxg.h"
+#include "json_double.h"
 #include "planpb_wire.h"
 
 namespace pxc {
@@ -881,41 +882,22 @@ static const char* const kQuantileKeys[7] = {"p01", "p10", "p25", "p50", "p75", 
 
 // The QuantilesUDA::Finalize JSON strings (math_sketches.h:40-54) of G groups from their 7
 // doubles each, written straight into one STRING column.  Groups are split over host threads;
-// every thread renders into its own buffer, then the buffers are concatenated.  Values are
-// rendered shortest-round-trip, with ".0" appended to integral values (rapidjson's
-// Writer::Double form, so they parse back as doubles), NaN / inf as null.
+// every thread renders into its own buffer, then the buffers are concatenated.  Numbers are
+// rendered byte-for-byte as rapidjson's Writer does (json_double.h: Grisu2 + Prettify; a NaN /
+// inf value ends the object after its key, as Document::Accept stops there).
 static HostColumn RenderQuantilesJson(const double* d, int64_t G) {
   const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({16, static_cast<int64_t>(std::thread::hardware_concurrency()), G / 2048 + 1}));
-  std::vector<std::vector<char>> bufs(static_cast<size_t>(nt));
+  std::vector<std::string> bufs(static_cast<size_t>(nt));
   std::vector<std::vector<int32_t>> lens(static_cast<size_t>(nt));
   auto work = [&](int64_t t) {
     const int64_t g0 = G * t / nt, g1 = G * (t + 1) / nt;
-    std::vector<char>& b = bufs[static_cast<size_t>(t)];
+    std::string& b = bufs[static_cast<size_t>(t)];
     std::vector<int32_t>& l = lens[static_cast<size_t>(t)];
     b.reserve(static_cast<size_t>(g1 - g0) * 160);
     l.reserve(static_cast<size_t>(g1 - g0));
-    char tmp[64];
     for (int64_t g = g0; g < g1; ++g) {
       const size_t start = b.size();
-      b.push_back('{');
-      for (int k = 0; k < 7; ++k) {
-        if (k) b.push_back(',');
-        b.push_back('"');
-        b.insert(b.end(), kQuantileKeys[k], kQuantileKeys[k] + 3);
-        b.push_back('"');
-        b.push_back(':');
-        const double v = d[g * 7 + k];
-        if (std::isnan(v) || std::isinf(v)) {
-          b.insert(b.end(), {'n', 'u', 'l', 'l'});
-          continue;
-        }
-        auto r = std::to_chars(tmp, tmp + sizeof(tmp), v);
-        bool frac = false;
-        for (char* c = tmp; c < r.ptr; ++c) frac = frac || *c == '.' || *c == 'e';
-        b.insert(b.end(), tmp, r.ptr);
-        if (!frac) b.insert(b.end(), {'.', '0'});
-      }
-      b.push_back('}');
+      pxjson::AppendQuantilesJson(d + g * 7, &b);
       l.push_back(static_cast<int32_t>(b.size() - start));
     }
   };
@@ -1307,8 +1289,14 @@ class PostAggMapNode : public ExecNode {
       auto it = agg_->quantiles_raw_.find(static_cast<size_t>(o.col));
       if (it == agg_->quantiles_raw_.end()) return Err(PXG_UNIMPLEMENTED, "pluck_float64 of a column that is not a quantiles UDA");
       const double* d = static_cast<const double*>(it->second.values);
+      // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
+      // fails to parse: pluck_float64 returns 0.0 for every key of that group.
       std::vector<double> v(static_cast<size_t>(rb.num_rows));
-      for (int64_t g = 0; g < rb.num_rows; ++g) v[static_cast<size_t>(g)] = d[g * 7 + o.quantile];
+      for (int64_t g = 0; g < rb.num_rows; ++g) {
+        bool finite = true;
+        for (int k = 0; k < 7; ++k) finite = finite && !pxjson::IsNanOrInf(d[g * 7 + k]);
+        v[static_cast<size_t>(g)] = finite ? d[g * 7 + o.quantile] : 0.0;
+      }
       ob.cols.push_back(DoubleColumn(v));
     }
     ob.eow = rb.eow;
@@ -2143,6 +2131,9 @@ static void WriteBatch(Writer* w, const RowBatch& rb) {
 using namespace pxc;
 
 struct pxc_engine {
+  // One engine serves concurrent callers one call at a time: the store, the group-count hints,
+  // the aggregation cache and the ctx stream are shared by every query on it.
+  std::mutex mu;
   pxg_ctx* ctx = nullptr;
   TableStore store;
   std::map<std::string, int64_t> group_hints;
@@ -2156,6 +2147,21 @@ static int32_t Fail(const Status& s) {
 
 extern "C" const char* pxc_last_error(void) { return g_last_error.c_str(); }
 extern "C" void pxc_free(void* p) { std::free(p); }
+
+// QuantilesUDA::Finalize's JSON for n groups of 7 doubles (json_double.h), as one malloc'ed
+// buffer of n NUL-terminated strings (released with pxc_free).
+extern "C" int32_t pxc_quantiles_json(const double* q7, int64_t n, char** out, int64_t* out_len) {
+  if ((!q7 && n > 0) || n < 0 || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::string s;
+  for (int64_t g = 0; g < n; ++g) {
+    pxjson::AppendQuantilesJson(q7 + g * 7, &s);
+    s.push_back('\0');
+  }
+  *out_len = static_cast<int64_t>(s.size());
+  *out = static_cast<char*>(std::malloc(std::max<size_t>(s.size(), 1)));
+  if (!s.empty()) std::memcpy(*out, s.data(), s.size());
+  return PXG_OK;
+}
 
 extern "C" int32_t pxc_engine_create(int32_t device, pxc_engine** out) {
   if (!out) return Fail(Err(PXG_INVALID_ARGUMENT, "out is null"));
@@ -2215,6 +2221,7 @@ extern "C" int32_t pxc_explain_plan(const uint8_t* plan, int64_t plan_len, int32
 extern "C" int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                                            const pxc_table* tables, char** out) {
   if (!engine) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(engine->mu);
   return Explain(plan, plan_len, ntables, tables, &engine->store, out);
 }
 
@@ -2224,6 +2231,7 @@ extern "C" int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* pl
 extern "C" int32_t pxc_store_create_table(pxc_engine* e, const char* name, int32_t ncols, const int32_t* types,
                                           const char* const* names) {
   if (!e || !name || ncols <= 0 || !types) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(e->mu);
   if (e->store.count(name)) return Fail(Err(PXG_ALREADY_EXISTS, "table %s already exists", name));
   StoredTable st;
   for (int32_t c = 0; c < ncols; ++c) {
@@ -2242,6 +2250,7 @@ extern "C" int32_t pxc_store_create_table(pxc_engine* e, const char* name, int32
 
 extern "C" int32_t pxc_store_append(pxc_engine* e, const char* name, const pxg_column_view* cols, int64_t nrows) {
   if (!e || !name || (!cols && nrows > 0) || nrows < 0) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(e->mu);
   auto it = e->store.find(name);
   if (it == e->store.end()) return Fail(Err(PXG_NOT_FOUND, "Table '%s' not found", name));
   StoredTable& st = it->second;
@@ -2264,6 +2273,7 @@ extern "C" int32_t pxc_store_append(pxc_engine* e, const char* name, const pxg_c
 
 extern "C" int32_t pxc_store_drop_table(pxc_engine* e, const char* name) {
   if (!e || !name) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(e->mu);
   auto it = e->store.find(name);
   if (it == e->store.end()) return Fail(Err(PXG_NOT_FOUND, "Table '%s' not found", name));
   pxg_table_destroy(it->second.t);
@@ -2273,6 +2283,7 @@ extern "C" int32_t pxc_store_drop_table(pxc_engine* e, const char* name) {
 
 extern "C" int64_t pxc_store_num_rows(pxc_engine* e, const char* name) {
   if (!e || !name) return -1;
+  std::lock_guard<std::mutex> lock(e->mu);
   auto it = e->store.find(name);
   if (it == e->store.end()) return -1;
   if (pxg_table_flush(it->second.t) != PXG_OK) return -1;
@@ -2297,6 +2308,7 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
                            const GrpcInputs* grpc_inputs, uint8_t** out, int64_t* out_len, uint8_t** grpc_out,
                            int64_t* grpc_out_len) {
   if (!engine || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(engine->mu);
   StageClock clk;
   ExecutionGraph g;
   Status s = Lower(plan, plan_len, ntables, tables, &engine->store, &g, grpc_inputs);

@@ -66,6 +66,8 @@ def load() -> C.CDLL:
     lib.pxc_rowbatch_to_proto.restype = i32
     lib.pxc_rowbatch_from_proto.argtypes = [C.c_char_p, i64, p(vp), p(i64)]
     lib.pxc_rowbatch_from_proto.restype = i32
+    lib.pxc_quantiles_json.argtypes = [p(C.c_double), i64, p(vp), p(i64)]
+    lib.pxc_quantiles_json.restype = i32
     lib.pxc_free.argtypes = [vp]
     lib.pxc_free.restype = None
     lib.pxc_last_error.argtypes = []

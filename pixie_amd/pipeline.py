@@ -9,7 +9,6 @@ Filter/Map batches are not observable.  Plans without an Agg run as pxg_filter /
 """
 from __future__ import annotations
 
-import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -22,19 +21,30 @@ from .device import Agg, Column, Ctx, Table
 QUANTILE_KEYS = ["p01", "p10", "p25", "p50", "p75", "p90", "p99"]
 
 
-def format_json_double(v: float) -> str:
-    """Shortest round-trip double rendering with a '.' or exponent (a rapidjson double)."""
-    if math.isnan(v) or math.isinf(v):
-        return "null"
-    s = repr(float(v))
-    if "e" in s and "." not in s.split("e")[0]:
-        return s
-    return s
+def quantiles_json_column(q7: np.ndarray) -> Column:
+    """QuantilesUDA::Finalize strings (src/carnot/funcs/builtins/math_sketches.h:40-54) of G
+    groups of 7 doubles, rendered by the engine's rapidjson restatement (pxc_quantiles_json,
+    pixie_amd/host/json_double.h) so the Python lowering and the C++ engine emit the same bytes."""
+    import ctypes as C
+    from . import host_engine
+    lib = host_engine.load()
+    q = np.ascontiguousarray(np.asarray(q7, dtype=np.float64).reshape(-1, 7))
+    out = C.c_void_p()
+    n = C.c_int64()
+    code = lib.pxc_quantiles_json(q.ctypes.data_as(C.POINTER(C.c_double)), q.shape[0], C.byref(out), C.byref(n))
+    if code != 0:
+        raise RuntimeError(f"pxc_quantiles_json failed: {lib.pxc_last_error().decode()}")
+    try:
+        raw = C.string_at(out.value, n.value)
+    finally:
+        lib.pxc_free(out)
+    strs = raw.split(b"\0")[:q.shape[0]]
+    return Column.from_values(STRING, strs)
 
 
 def quantiles_json(q7: Sequence[float]) -> str:
-    """QuantilesUDA::Finalize rendering (src/carnot/funcs/builtins/math_sketches.h:40-54)."""
-    return "{" + ",".join(f'"{k}":{format_json_double(v)}' for k, v in zip(QUANTILE_KEYS, q7)) + "}"
+    """One group's QuantilesUDA::Finalize string."""
+    return quantiles_json_column(np.asarray(q7, dtype=np.float64).reshape(1, 7)).to_list()[0]
 
 
 def _ops(plan):
@@ -130,7 +140,7 @@ class LinearQuery:
         for j, c in enumerate(cols):
             if j >= nk and self.udas[j - nk].kind == _lib.UDA_QUANTILES:
                 qraw[j] = c.values
-                out.append(Column.from_values(STRING, [quantiles_json(r) for r in c.values]))
+                out.append(quantiles_json_column(c.values))
             else:
                 out.append(c)
         if self.post_map is None:
@@ -145,7 +155,10 @@ class LinearQuery:
                 src = int(e.func.args[0].column.index)
                 key = e.func.args[1].constant.string_value
                 if src in qraw and key in QUANTILE_KEYS:
-                    res.append(Column(FLOAT64, values=np.ascontiguousarray(qraw[src][:, QUANTILE_KEYS.index(key)])))
+                    q = qraw[src].reshape(-1, 7)
+                    # a NaN / inf quantile truncates the JSON, which pluck_float64 fails to parse: 0.0
+                    ok = np.isfinite(q).all(axis=1)
+                    res.append(Column(FLOAT64, values=np.ascontiguousarray(np.where(ok, q[:, QUANTILE_KEYS.index(key)], 0.0))))
                 else:
                     import json
                     vals = []

@@ -49,6 +49,9 @@ def load():
     lib.oracle_execute_plan_timed_rebatched.restype = C.c_int32
     lib.oracle_execute_plan_timed_rebatched.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.c_int64,
                                                         C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
+    lib.oracle_execute_plan_rebatched.restype = C.c_int32
+    lib.oracle_execute_plan_rebatched.argtypes = [C.c_char_p, C.c_int32, C.POINTER(OTable), C.c_int64, C.POINTER(C.c_double),
+                                                  C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.c_char_p, C.c_int32]
     lib.oracle_free.argtypes = [C.c_void_p]
     lib.oracle_tdigest_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
     lib.oracle_tdigest_merge_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
@@ -142,6 +145,27 @@ def execute_plan(plan, tables: Dict[str, dict]):
     finally:
         lib.oracle_free(out)
     return parse_pxrb(buf)
+
+
+def execute_plan_timed(plan, tables: Dict[str, dict], batch_rows: int = 0):
+    """(execution-window seconds, result tables) of one oracle run; batch_rows > 0 re-slices
+    every given batch into RowBatches of that many rows inside the oracle."""
+    from google.protobuf import json_format
+    lib = load()
+    js = json_format.MessageToJson(plan).encode()
+    t = _Tables(tables)
+    secs = C.c_double()
+    out = C.c_void_p()
+    n = C.c_int64()
+    err = C.create_string_buffer(1024)
+    code = lib.oracle_execute_plan_rebatched(js, t.n, t.arr, batch_rows, C.byref(secs), C.byref(out), C.byref(n), err, 1024)
+    if code != 0:
+        raise OracleError(code, err.value.decode())
+    try:
+        buf = C.string_at(out.value, n.value)
+    finally:
+        lib.oracle_free(out)
+    return secs.value, parse_pxrb(buf)
 
 
 def time_plan(plan, tables: Dict[str, dict], batch_rows: int = 0):
