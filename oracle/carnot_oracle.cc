@@ -976,6 +976,43 @@ struct AggNode : ExecNode {
   }
 };
 
+// LimitNode::ConsumeNextImpl (limit_node.cc:55-95): whole batches while they fit, then the
+// batch that reaches the limit sliced to [0, remainder) with eow / eos, the abortable sources
+// stopped (ExecState::StopSource), and every later batch dropped.
+struct LimitNode : ExecNode {
+  int64_t limit = 0, processed = 0;
+  bool reached = false;
+  std::vector<int64_t> selected;
+  std::vector<uint64_t> abortable;
+  std::set<uint64_t>* stopped = nullptr;
+  void ConsumeNext(const RowBatch& rb, size_t) override {
+    if (reached) return;
+    const int64_t remainder = limit - processed;
+    RowBatch out;
+    if (remainder > rb.num_rows) {
+      out.num_rows = rb.num_rows;
+      for (int64_t ci : selected) out.cols.push_back(rb.cols.at(ci));
+      processed += rb.num_rows;
+      out.eow = rb.eow;
+      out.eos = rb.eos;
+      Send(out);
+      return;
+    }
+    out.num_rows = remainder;
+    for (int64_t ci : selected) {
+      const Col& in = *rb.cols.at(ci);
+      auto c = std::make_shared<Col>(in.type);
+      for (int64_t r = 0; r < remainder; ++r) c->append_from(in, static_cast<size_t>(r));
+      out.cols.push_back(c);
+    }
+    out.eow = out.eos = true;
+    processed += remainder;
+    reached = true;
+    for (uint64_t id : abortable) stopped->insert(id);
+    Send(out);
+  }
+};
+
 struct SinkNode : ExecNode {
   std::string name;
   std::vector<RowBatch> batches;
@@ -983,6 +1020,7 @@ struct SinkNode : ExecNode {
 };
 
 struct SourceNode : ExecNode {
+  uint64_t id = 0;
   std::vector<RowBatch> batches;
   bool explicit_flags = false;
   size_t next = 0;
@@ -1195,6 +1233,7 @@ struct Graph {
   std::map<uint64_t, std::unique_ptr<ExecNode>> nodes;
   std::vector<SourceNode*> sources;
   std::vector<SinkNode*> sinks;
+  std::set<uint64_t> stopped;  // ExecState source_id_to_keep_running_map_ == false
 
   void Build(const Json& plan, const std::map<std::string, TableIn>& tables) {
     const Json& frags = plan["nodes"];
@@ -1272,6 +1311,7 @@ struct Graph {
         if (s->col_idxs.empty())
           for (size_t c = 0; c < it->second.types.size(); ++c) s->col_idxs.push_back(static_cast<int64_t>(c));
         for (auto c : s->col_idxs) s->out_types.push_back(it->second.types.at(c));
+        s->id = id;
         sources.push_back(s.get());
         node = std::move(s);
       } else if (op.has("filterOp")) {
@@ -1333,6 +1373,18 @@ struct Graph {
         n->rows_per_batch = j["rowsPerBatch"].as_i64();
         n->Init();
         node = std::move(n);
+      } else if (op.has("limitOp")) {
+        const Json& l = op["limitOp"];
+        auto n = std::make_unique<LimitNode>();
+        n->limit = l["limit"].as_i64();
+        for (size_t c = 0; c < l["columns"].size(); ++c) {
+          const int64_t ci = l["columns"].at(c)["index"].as_i64();
+          n->selected.push_back(ci);
+          n->out_types.push_back(in.at(ci));
+        }
+        for (size_t c = 0; c < l["abortableSrcs"].size(); ++c) n->abortable.push_back(l["abortableSrcs"].at(c).as_u64());
+        n->stopped = &stopped;
+        node = std::move(n);
       } else if (op.has("memSinkOp") || op.has("grpcSinkOp")) {
         auto n = std::make_unique<SinkNode>();
         if (op.has("memSinkOp")) n->name = op["memSinkOp"]["name"].as_str();
@@ -1357,8 +1409,8 @@ struct Graph {
     while (!running.empty()) {
       std::vector<SourceNode*> still;
       for (auto* s : running) {
-        for (int i = 0; i < 10 && !s->done; ++i) s->GenerateNext();
-        if (!s->done) still.push_back(s);
+        for (int i = 0; i < 10 && !s->done && !stopped.count(s->id); ++i) s->GenerateNext();
+        if (!s->done && !stopped.count(s->id)) still.push_back(s);
       }
       running = still;
     }

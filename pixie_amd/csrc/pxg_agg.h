@@ -57,7 +57,8 @@ struct AggTableDev {
   uint32_t mask;
   uint32_t limit;                 // inserts beyond this are deferred (table kept <= 50% full)
   unsigned int* counters;         // [0] groups in the table (flushed per tile), [2] deferred rows
-  uint32_t* deferred;
+  uint32_t* deferred;      // rowrefs of deferred rows
+  uint32_t* deferred_pos;  // their staging records (the retry fills in the slot)
   const uint64_t* arena;
 };
 

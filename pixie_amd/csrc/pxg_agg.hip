@@ -85,7 +85,11 @@ __device__ __forceinline__ void ProcessRow(const AggPlanDev* __restrict__ plan, 
     unsigned int base = 0;
     if (lane == leader) base = atomicAdd(&tab.counters[2], static_cast<unsigned int>(__popcll(dm)));
     base = __shfl(base, leader, 64);
-    if (slot == kDeferredSlot) tab.deferred[base + __popcll(dm & ((1ULL << lane) - 1))] = rowref;
+    if (slot == kDeferredSlot) {
+      const unsigned int at = base + __popcll(dm & ((1ULL << lane) - 1));
+      tab.deferred[at] = rowref;
+      tab.deferred_pos[at] = static_cast<uint32_t>(pos);
+    }
   }
   stg.slot[pos] = slot;
   const int nv = plan->n_vals;
@@ -174,29 +178,27 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
   if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
 }
 
-// Re-process deferred rows (already past the filter) after the table grew.
+// Re-process deferred rows (already past the filter) after the table grew.  Each row fills in
+// the slot of the staging record it already has (its values were staged with it), so a
+// deferral never adds records: the staging holds exactly one record per selected row.
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeListKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
-                                                                      const uint32_t* __restrict__ list, uint32_t n,
+                                                                      const uint32_t* __restrict__ list,
+                                                                      const uint32_t* __restrict__ list_pos, uint32_t n,
                                                                       AggTableDev tab, StageDev stg) {
-  __shared__ unsigned long long s_base;
   __shared__ unsigned int s_ins;
   if (threadIdx.x == 0) s_ins = 0;
   for (uint32_t t0 = blockIdx.x * kConsumeBlock; t0 < n; t0 += gridDim.x * kConsumeBlock) {
-    const uint32_t cnt = min(static_cast<uint32_t>(kConsumeBlock), n - t0);
-    if (threadIdx.x == 0) {
-      if (s_ins) {
-        atomicAdd(&tab.counters[0], s_ins);
-        s_ins = 0;
-      }
-      s_base = atomicAdd(stg.cursor, static_cast<unsigned long long>(cnt));
+    if (threadIdx.x == 0 && s_ins) {
+      atomicAdd(&tab.counters[0], s_ins);
+      s_ins = 0;
     }
     __syncthreads();
     const uint32_t i = t0 + threadIdx.x;
-    if (threadIdx.x < cnt) {
+    if (i < n) {
       const uint32_t ref = list[i];
       const uint32_t c = ref >> kChunkShift;
-      ProcessRow(plan, chunks, chunks[c], c, static_cast<int64_t>(ref & (kChunkRows - 1)), tab, stg, s_base + threadIdx.x, &s_ins);
+      ProcessRow(plan, chunks, chunks[c], c, static_cast<int64_t>(ref & (kChunkRows - 1)), tab, stg, list_pos[i], &s_ins);
     }
     __syncthreads();
   }
@@ -608,7 +610,11 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
           unsigned int dbase = 0;
           if (lane == leader) dbase = atomicAdd(&tab.counters[2], static_cast<unsigned int>(__popcll(dm)));
           dbase = __shfl(dbase, leader, 64);
-          if (slot == kDeferredSlot) tab.deferred[dbase + __popcll(dm & lanemask_lt)] = rowref;
+          if (slot == kDeferredSlot) {
+            const unsigned int at = dbase + __popcll(dm & lanemask_lt);
+            tab.deferred[at] = rowref;
+            tab.deferred_pos[at] = static_cast<uint32_t>(pos);
+          }
         }
         stg.slot[pos] = slot;
       }
@@ -698,6 +704,7 @@ static AggTableDev TableDev(Agg* a, int defer_buf) {
   t.limit = a->cap / 2;
   t.counters = a->counters.as<unsigned int>();
   t.deferred = a->deferred[defer_buf].as<uint32_t>();
+  t.deferred_pos = a->deferred_pos[defer_buf].as<uint32_t>();
   t.arena = a->arena.as<uint64_t>();
   return t;
 }
@@ -822,8 +829,11 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   }
   if (ranges.empty()) return PXG_OK;
   const int64_t rows = end - begin;
+  if (st_n + static_cast<uint64_t>(rows) >= (uint64_t(1) << 32))
+    return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
   PXG_RETURN_IF_ERROR(deferred[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
+  PXG_RETURN_IF_ERROR(deferred_pos[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
   // The tile ranges of a repeated consume (same table, same rows) are already on the device.
   const size_t rbytes = ranges.size() * sizeof(TileRange);
   if (rbytes != last_ranges.size() || std::memcmp(last_ranges.data(), ranges.data(), rbytes) != 0) {
@@ -871,11 +881,12 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
       PXG_RETURN_IF_ERROR(Grow(NextPow2(std::min<uint64_t>(geo, 4 * want))));
     }
     PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
-    PXG_RETURN_IF_ERROR(EnsureStage(st_n + n_def));
+    PXG_RETURN_IF_ERROR(deferred_pos[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
     PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
     PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume_list", AggConsumeListKernel, dim3(GridFor(n_def, kConsumeBlock, ctx->num_cus * 8)),
                                dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(),
-                               deferred[buf].as<const uint32_t>(), n_def, TableDev(this, 1 - buf), StageDevOf(this)));
+                               deferred[buf].as<const uint32_t>(), deferred_pos[buf].as<const uint32_t>(), n_def,
+                               TableDev(this, 1 - buf), StageDevOf(this)));
     PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
     buf = 1 - buf;
   }

@@ -52,7 +52,7 @@ struct Agg {
   uint32_t min_cap = 1024;  // the capacity the creation hint asked for (reset never shrinks below)
   DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor;
                     // u32 @32 import inserts, @36 import error flags
-  DevBuf deferred[2];
+  DevBuf deferred[2], deferred_pos[2];
   DevBuf d_ranges;
   std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
   DevBuf arena;

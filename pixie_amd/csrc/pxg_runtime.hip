@@ -94,6 +94,14 @@ static constexpr int64_t kStageRows = 1 << 20;
 static constexpr int64_t kStageBytes = 64 << 20;
 static constexpr int64_t kMaxChunkData = (int64_t(1) << 31) - 64;
 
+// One int32 from device memory, ordered after the work already issued on the ctx stream (the
+// stream is non-blocking: a plain hipMemcpy on the null stream would not wait for it).
+static int32_t ReadDeviceI32(Ctx* ctx, const int32_t* p, int32_t* out) {
+  PXG_HIP(hipMemcpyAsync(out, p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
 // Append rows [0, n) of `cols` (host or device pointers per `kind`) into the table's chunks.
 int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind kind) {
   const bool from_host = (kind == hipMemcpyHostToDevice);
@@ -117,8 +125,8 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
         o_first = off[done];
         o_last = off[done + take];
       } else {
-        PXG_HIP(hipMemcpy(&o_first, off + done, 4, hipMemcpyDeviceToHost));
-        PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+        PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done, &o_first));
+        PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done + take, &o_last));
       }
       int64_t bytes = static_cast<int64_t>(o_last) - o_first;
       while (ch->cols[k].data_len + bytes > kMaxChunkData && take > 1) {
@@ -126,7 +134,7 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
         if (from_host) {
           o_last = off[done + take];
         } else {
-          PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+          PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done + take, &o_last));
         }
         bytes = static_cast<int64_t>(o_last) - o_first;
       }
@@ -160,8 +168,8 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
         o_first = off[done];
         o_last = off[done + take];
       } else {
-        PXG_HIP(hipMemcpy(&o_first, off + done, 4, hipMemcpyDeviceToHost));
-        PXG_HIP(hipMemcpy(&o_last, off + done + take, 4, hipMemcpyDeviceToHost));
+        PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done, &o_first));
+        PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done + take, &o_last));
       }
       const int64_t bytes = static_cast<int64_t>(o_last) - o_first;
       if (cc.offsets.bytes < static_cast<size_t>(r1 + 1) * 4 + 16)

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -664,6 +665,8 @@ struct ExecState {
   // resets it and gives it back at Close, so the hash table and finalize workspaces keep their
   // grown device buffers instead of being freed and reallocated per query.
   std::multimap<std::string, pxg_agg*>* agg_cache = nullptr;
+  // ExecState::StopSource (exec_state.h:171-178): sources a Limit has finished with.
+  std::set<uint64_t> stopped_sources;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -711,6 +714,7 @@ class ExecNode {
 // Source nodes (exec_node.h:300-315): the graph pulls them until they have nothing left.
 class SourceNode : public ExecNode {
  public:
+  uint64_t node_id = 0;  // plan node id (LimitOperator.abortable_srcs names sources by it)
   virtual bool HasBatchesRemaining() const = 0;
   virtual Status GenerateNext(ExecState* s) = 0;
 };
@@ -1238,77 +1242,6 @@ class GpuAggNode : public ExecNode {
   std::string hint_source;  // the source table's name (set by the graph builder)
 };
 
-// Post-aggregation Map over the G result rows: column references and pluck_float64 of a
-// quantiles column (PluckAsFloat64UDF, json_ops.h:131-153, on the digest's own doubles).
-class PostAggMapNode : public ExecNode {
- public:
-  explicit PostAggMapNode(GpuAggNode* agg) : agg_(agg) {}
-  // pluck_float64 of a quantiles column reads the digest's doubles, not the JSON string.
-  bool ReadsColumnValue(size_t col) const override {
-    for (auto& o : outs_)
-      if (o.quantile < 0 && static_cast<size_t>(o.col) == col) return true;
-    return false;
-  }
-  std::string DebugString() const override { return "PostAggMapNode(column refs, pluck_float64)"; }
-
- protected:
-  struct Out {
-    int64_t col = 0;
-    int quantile = -1;  // >= 0: pluck of quantile key index
-  };
-  std::vector<Out> outs_;
-  Status InitImpl(const planpb::Operator& op) override {
-    for (auto& e : op.map.expressions) {
-      Out o;
-      if (e.kind == planpb::ScalarExpression::kColumn) {
-        o.col = static_cast<int64_t>(e.column.index);
-      } else if (e.kind == planpb::ScalarExpression::kFunc && e.func->name == "pluck_float64" && e.func->args.size() == 2 &&
-                 e.func->args[0].kind == planpb::ScalarExpression::kColumn &&
-                 e.func->args[1].kind == planpb::ScalarExpression::kConstant) {
-        o.col = static_cast<int64_t>(e.func->args[0].column.index);
-        const std::string& key = e.func->args[1].constant.string_value;
-        for (int k = 0; k < 7; ++k)
-          if (key == kQuantileKeys[k]) o.quantile = k;
-        if (o.quantile < 0) return Err(PXG_UNIMPLEMENTED, "pluck_float64 key %s is not a quantile key", key.c_str());
-      } else {
-        return Err(PXG_UNIMPLEMENTED, "post-aggregate Map supports column references and pluck_float64 only");
-      }
-      if (o.col < 0 || o.col >= static_cast<int64_t>(inputs_[0].size())) return Err(PXG_INVALID_ARGUMENT, "column out of range");
-      outs_.push_back(o);
-    }
-    return Status::OK();
-  }
-  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
-    RowBatch ob;
-    ob.num_rows = rb.num_rows;
-    for (auto& o : outs_) {
-      if (o.quantile < 0) {
-        ob.cols.push_back(rb.cols[static_cast<size_t>(o.col)]);
-        continue;
-      }
-      auto it = agg_->quantiles_raw_.find(static_cast<size_t>(o.col));
-      if (it == agg_->quantiles_raw_.end()) return Err(PXG_UNIMPLEMENTED, "pluck_float64 of a column that is not a quantiles UDA");
-      const double* d = static_cast<const double*>(it->second.values);
-      // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
-      // fails to parse: pluck_float64 returns 0.0 for every key of that group.
-      std::vector<double> v(static_cast<size_t>(rb.num_rows));
-      for (int64_t g = 0; g < rb.num_rows; ++g) {
-        bool finite = true;
-        for (int k = 0; k < 7; ++k) finite = finite && !pxjson::IsNanOrInf(d[g * 7 + k]);
-        v[static_cast<size_t>(g)] = finite ? d[g * 7 + o.quantile] : 0.0;
-      }
-      ob.cols.push_back(DoubleColumn(v));
-    }
-    ob.eow = rb.eow;
-    ob.eos = rb.eos;
-    return SendRowBatchToChildren(s, ob);
-  }
-
- private:
-  GpuAggNode* agg_;
-};
-
-// MemorySinkNode / GRPCSinkNode result table: collects the batches.
 // A zero-row batch of the given types (RowBatch::WithZeroRows).
 static RowBatch ZeroRowBatch(const RowDescriptor& types, bool eow, bool eos) {
   static const int32_t zero_off[2] = {0, 0};
@@ -1326,6 +1259,288 @@ static RowBatch ZeroRowBatch(const RowDescriptor& types, bool eow, bool eos) {
   rb.eos = eos;
   return rb;
 }
+
+// pluck_float64 (PluckAsFloat64UDF, json_ops.h:131-153) of a JSON string that did not come from
+// a device quantiles column: rapidjson's default parse of an object, the member's value if it
+// is a number with a fraction or exponent (IsDouble), else 0.0; a parse failure gives 0.0.
+static double PluckJson(const char* p, size_t n, const std::string& key) {
+  size_t i = 0;
+  auto ws = [&]() { while (i < n && (p[i] == ' ' || p[i] == '\t' || p[i] == '\n' || p[i] == '\r')) ++i; };
+  auto str = [&](std::string* out) -> bool {
+    if (i >= n || p[i] != '"') return false;
+    for (++i; i < n && p[i] != '"'; ++i) {
+      if (p[i] == '\\') { if (++i >= n) return false; }
+      if (out) out->push_back(p[i]);
+    }
+    if (i >= n) return false;
+    ++i;
+    return true;
+  };
+  // skip one JSON value; *dbl / *is_double receive a number's value / kind
+  std::function<bool(double*, bool*)> value = [&](double* dbl, bool* is_double) -> bool {
+    ws();
+    if (i >= n) return false;
+    const char c = p[i];
+    if (c == '"') return str(nullptr);
+    if (c == '{' || c == '[') {
+      const char close = c == '{' ? '}' : ']';
+      ++i;
+      ws();
+      if (i < n && p[i] == close) { ++i; return true; }
+      for (;;) {
+        if (close == '}') {
+          ws();
+          if (!str(nullptr)) return false;
+          ws();
+          if (i >= n || p[i] != ':') return false;
+          ++i;
+        }
+        if (!value(nullptr, nullptr)) return false;
+        ws();
+        if (i < n && p[i] == ',') { ++i; continue; }
+        if (i < n && p[i] == close) { ++i; return true; }
+        return false;
+      }
+    }
+    if (!std::strncmp(p + i, "true", std::min<size_t>(4, n - i)) && n - i >= 4) { i += 4; return true; }
+    if (!std::strncmp(p + i, "false", std::min<size_t>(5, n - i)) && n - i >= 5) { i += 5; return true; }
+    if (!std::strncmp(p + i, "null", std::min<size_t>(4, n - i)) && n - i >= 4) { i += 4; return true; }
+    const size_t s0 = i;
+    bool frac = false;
+    if (i < n && p[i] == '-') ++i;
+    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
+    while (i < n && ((p[i] >= '0' && p[i] <= '9') || p[i] == '.' || p[i] == 'e' || p[i] == 'E' || p[i] == '+' || p[i] == '-')) {
+      frac = frac || p[i] == '.' || p[i] == 'e' || p[i] == 'E';
+      ++i;
+    }
+    if (dbl) *dbl = std::strtod(std::string(p + s0, i - s0).c_str(), nullptr);
+    if (is_double) *is_double = frac;
+    return true;
+  };
+  double found = 0.0;
+  bool have = false;
+  ws();
+  if (i >= n || p[i] != '{') return 0.0;
+  ++i;
+  ws();
+  if (i < n && p[i] == '}') return 0.0;
+  for (;;) {
+    ws();
+    std::string k;
+    if (!str(&k)) return 0.0;
+    ws();
+    if (i >= n || p[i] != ':') return 0.0;
+    ++i;
+    double d = 0;
+    bool isd = false;
+    if (!value(&d, &isd)) return 0.0;
+    if (k == key && !have) {  // FindMember: the first member with the name
+      found = isd ? d : 0.0;
+      have = true;
+    }
+    ws();
+    if (i < n && p[i] == ',') { ++i; continue; }
+    if (i < n && p[i] == '}') { ++i; break; }
+    return 0.0;
+  }
+  ws();
+  return i == n ? found : 0.0;
+}
+
+// MapNode after an aggregate (map_node.cc:47-71) over the G result rows: any expression.
+// pluck_float64(column, 'key') sub-expressions become extra FLOAT64 input columns (from the
+// digest's own doubles when the column is a device quantiles UDA, else parsed from the JSON);
+// bare column references pass through; every other expression runs as one device program
+// (pxg_map) over the G rows.
+class PostAggMapNode : public ExecNode {
+ public:
+  explicit PostAggMapNode(GpuAggNode* agg) : agg_(agg) {}
+  // A quantiles column is read as a string only when some expression does more than pluck it.
+  bool ReadsColumnValue(size_t col) const override { return string_reads_.count(col) > 0; }
+  std::string DebugString() const override { return "PostAggMapNode(device map over the aggregate rows)"; }
+
+  // Rewrites one expression (pluck_float64 leaves -> extra columns) and compiles it.
+  static Status Lower(const planpb::ScalarExpression& e, const RowDescriptor& in, std::vector<std::pair<int64_t, std::string>>* plucks,
+                      std::set<size_t>* string_reads, planpb::ScalarExpression* out) {
+    if (e.kind == planpb::ScalarExpression::kFunc && e.func->name == "pluck_float64" && e.func->args.size() == 2 &&
+        e.func->args[0].kind == planpb::ScalarExpression::kColumn && e.func->args[1].kind == planpb::ScalarExpression::kConstant &&
+        e.func->args[1].constant.data_type == S) {
+      const uint64_t c = e.func->args[0].column.index;
+      if (c >= in.size() || in[c] != S) return Err(PXG_INVALID_ARGUMENT, "pluck_float64 of a non-STRING column");
+      int64_t j = -1;
+      for (size_t k = 0; k < plucks->size(); ++k)
+        if ((*plucks)[k].first == static_cast<int64_t>(c) && (*plucks)[k].second == e.func->args[1].constant.string_value) j = static_cast<int64_t>(k);
+      if (j < 0) {
+        j = static_cast<int64_t>(plucks->size());
+        plucks->push_back({static_cast<int64_t>(c), e.func->args[1].constant.string_value});
+      }
+      out->kind = planpb::ScalarExpression::kColumn;
+      out->column.index = in.size() + static_cast<uint64_t>(j);
+      return Status::OK();
+    }
+    *out = e;
+    if (e.kind == planpb::ScalarExpression::kColumn) {
+      if (e.column.index < in.size() && in[e.column.index] == S) string_reads->insert(e.column.index);
+      return Status::OK();
+    }
+    if (e.kind == planpb::ScalarExpression::kFunc) {
+      out->func = std::make_shared<planpb::ScalarFunc>(*e.func);
+      for (size_t a = 0; a < e.func->args.size(); ++a)
+        PXC_RETURN_IF_ERROR(Lower(e.func->args[a], in, plucks, string_reads, &out->func->args[a]));
+    }
+    return Status::OK();
+  }
+  static Status OutputTypes(const planpb::Operator& op, const RowDescriptor& in, RowDescriptor* out) {
+    std::vector<std::pair<int64_t, std::string>> plucks;
+    std::set<size_t> reads;
+    std::vector<planpb::ScalarExpression> lowered(op.map.expressions.size());
+    for (size_t i = 0; i < lowered.size(); ++i) PXC_RETURN_IF_ERROR(Lower(op.map.expressions[i], in, &plucks, &reads, &lowered[i]));
+    RowDescriptor env = in;
+    env.insert(env.end(), plucks.size(), F);
+    ExprCompiler comp(ColumnEnv(env));
+    for (auto& e : lowered) {
+      Program p;
+      PXC_RETURN_IF_ERROR(comp.Compile(e, &p));
+      out->push_back(p.result_type);
+    }
+    return Status::OK();
+  }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    const RowDescriptor& in = inputs_[0];
+    std::vector<planpb::ScalarExpression> lowered(op.map.expressions.size());
+    for (size_t i = 0; i < lowered.size(); ++i) PXC_RETURN_IF_ERROR(Lower(op.map.expressions[i], in, &plucks_, &string_reads_, &lowered[i]));
+    env_types_ = in;
+    env_types_.insert(env_types_.end(), plucks_.size(), F);
+    ExprCompiler comp(ColumnEnv(env_types_));
+    for (auto& e : lowered) {
+      Program p;
+      PXC_RETURN_IF_ERROR(comp.Compile(e, &p));
+      if (p.IsColumn()) {
+        passthrough_.push_back(p.insns[0].arg);
+      } else {
+        passthrough_.push_back(-1);
+        device_.push_back(p);
+      }
+    }
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    const int64_t G = rb.num_rows;
+    std::vector<HostColumn> env = rb.cols;
+    for (auto& pk : plucks_) {
+      std::vector<double> v(static_cast<size_t>(G));
+      auto it = agg_ ? agg_->quantiles_raw_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantiles_raw_.end()){};
+      int qk = -1;
+      for (int k = 0; k < 7; ++k)
+        if (pk.second == kQuantileKeys[k]) qk = k;
+      if (agg_ && it != agg_->quantiles_raw_.end()) {
+        // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
+        // fails to parse: pluck_float64 returns 0.0 for every key of that group.
+        const double* d = static_cast<const double*>(it->second.values);
+        for (int64_t g = 0; g < G; ++g) {
+          bool finite = true;
+          for (int k = 0; k < 7; ++k) finite = finite && !pxjson::IsNanOrInf(d[g * 7 + k]);
+          v[static_cast<size_t>(g)] = finite && qk >= 0 ? d[g * 7 + qk] : 0.0;
+        }
+      } else {
+        const HostColumn& c = rb.cols[static_cast<size_t>(pk.first)];
+        for (int64_t g = 0; g < G; ++g)
+          v[static_cast<size_t>(g)] = PluckJson(reinterpret_cast<const char*>(c.data) + c.offsets[g],
+                                                static_cast<size_t>(c.offsets[g + 1] - c.offsets[g]), pk.second);
+      }
+      env.push_back(DoubleColumn(v));
+    }
+    std::vector<HostColumn> dev_out;
+    if (!device_.empty() && G > 0) {
+      pxg_table* in = nullptr;
+      RowBatch eb;
+      eb.cols = env;
+      eb.num_rows = G;
+      PXC_RETURN_IF_ERROR(UploadBatch(s->ctx, eb, env_types_, &in));
+      std::vector<pxg_program> pv;
+      for (auto& p : device_) pv.push_back(p.View());
+      pxg_table* out = nullptr;
+      Status st = FromPxg(pxg_map(in, static_cast<int32_t>(pv.size()), pv.data(), 0, G, &out));
+      RowBatch ob;
+      if (st.ok()) st = FetchAll(out, static_cast<int32_t>(pv.size()), &ob);
+      if (out) pxg_table_destroy(out);
+      pxg_table_destroy(in);
+      PXC_RETURN_IF_ERROR(st);
+      dev_out = ob.cols;
+    }
+    RowBatch ob;
+    ob.num_rows = G;
+    size_t d = 0;
+    for (size_t i = 0; i < passthrough_.size(); ++i) {
+      if (passthrough_[i] >= 0) {
+        ob.cols.push_back(env[static_cast<size_t>(passthrough_[i])]);
+      } else if (G > 0) {
+        ob.cols.push_back(dev_out[d++]);
+      } else {
+        ob.cols.push_back(ZeroRowBatch({device_[d++].result_type}, false, false).cols[0]);
+      }
+    }
+    ob.eow = rb.eow;
+    ob.eos = rb.eos;
+    return SendRowBatchToChildren(s, ob);
+  }
+
+ private:
+  GpuAggNode* agg_;
+  std::vector<std::pair<int64_t, std::string>> plucks_;  // (input column, key) -> extra column
+  std::set<size_t> string_reads_;
+  RowDescriptor env_types_;
+  std::vector<int32_t> passthrough_;  // per output: env column, or -1 for the next device program
+  std::vector<Program> device_;
+};
+
+// LimitNode (limit_node.cc:55-95): forwards rows until `limit` have passed; the batch that
+// reaches the limit is cut there and carries eow / eos, later batches are dropped, and the
+// abortable sources are stopped (ExecState::StopSource).
+class LimitNode : public ExecNode {
+ public:
+  std::string DebugString() const override { return "LimitNode(" + std::to_string(limit_) + ")"; }
+
+ protected:
+  Status InitImpl(const planpb::Operator& op) override {
+    limit_ = op.limit.limit;
+    for (auto& c : op.limit.columns) {  // the output relation is exactly these (operators.cc:424-445)
+      if (c.index >= inputs_[0].size()) return Err(PXG_INVALID_ARGUMENT, "limit column out of range");
+      cols_.push_back(static_cast<size_t>(c.index));
+    }
+    srcs_ = op.limit.abortable_srcs;
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    if (reached_) return Status::OK();
+    const int64_t remainder = limit_ - processed_;
+    RowBatch ob;
+    for (size_t c : cols_) ob.cols.push_back(rb.cols[c]);
+    if (remainder > rb.num_rows) {
+      ob.num_rows = rb.num_rows;
+      ob.eow = rb.eow;
+      ob.eos = rb.eos;
+      processed_ += rb.num_rows;
+      return SendRowBatchToChildren(s, ob);
+    }
+    const int64_t keep = std::max<int64_t>(remainder, 0);
+    ob.num_rows = keep;
+    for (auto& c : ob.cols) c.length = keep;  // Slice(0, keep): same buffers, fewer rows
+    ob.eow = ob.eos = true;
+    processed_ += keep;
+    reached_ = true;
+    for (uint64_t id : srcs_) s->stopped_sources.insert(id);
+    return SendRowBatchToChildren(s, ob);
+  }
+
+ private:
+  int64_t limit_ = 0, processed_ = 0;
+  bool reached_ = false;
+  std::vector<size_t> cols_;
+  std::vector<uint64_t> srcs_;
+};
 
 // GpuEquijoinNode (EquijoinNode, equijoin_node.cc:53-470).  InitImpl maps left/right onto
 // build/probe exactly as the reference does: the probe table is the left parent when the output
@@ -1721,6 +1936,7 @@ class ExecutionGraph {
           if (it != grpc_inputs_->end()) msgs = &it->second;
         }
         auto* src = new GrpcSourceNode(id, msgs);
+        src->node_id = id;
         pool_.emplace_back(src);
         for (int32_t t : op.grpc_source_types)
           if (t < B || t > T) return Err(PXG_INVALID_ARGUMENT, "GRPC source column type %d", t);
@@ -1753,10 +1969,7 @@ class ExecutionGraph {
           auto* agg = dynamic_cast<GpuAggNode*>(built[ps[0]]);
           if (agg) {
             node = new PostAggMapNode(agg);
-            for (auto& e : op.map.expressions) {
-              if (e.kind == planpb::ScalarExpression::kColumn && e.column.index < cur.size()) out.push_back(cur[e.column.index]);
-              else out.push_back(F);
-            }
+            PXC_RETURN_IF_ERROR(PostAggMapNode::OutputTypes(op, cur, &out));
           } else {
             node = new GpuMapNode();
             ExprCompiler comp(ColumnEnv(cur));
@@ -1773,6 +1986,14 @@ class ExecutionGraph {
           Status st;
           out = AggOutputTypes(op, ColumnEnv(cur), &st);
           PXC_RETURN_IF_ERROR(st);
+          break;
+        }
+        case 7: {
+          node = new LimitNode();
+          for (auto& c : op.limit.columns) {
+            if (c.index >= cur.size()) return Err(PXG_INVALID_ARGUMENT, "limit column out of range");
+            out.push_back(cur[c.index]);
+          }
           break;
         }
         case 8: {
@@ -1833,7 +2054,7 @@ class ExecutionGraph {
     for (bool any = true; st.ok() && any;) {
       any = false;
       for (auto* src : sources_) {
-        if (!st.ok() || !src->HasBatchesRemaining()) continue;
+        if (!st.ok() || !src->HasBatchesRemaining() || s->stopped_sources.count(src->node_id)) continue;
         any = true;
         st = src->GenerateNext(s);
       }
@@ -1952,6 +2173,7 @@ class ExecutionGraph {
       dsrc = new DeviceSourceNode(ms.name, stored);
       src = dsrc;
     }
+    src->node_id = id;
     pool_.emplace_back(src);
     PXC_RETURN_IF_ERROR(src->Init(op, src_types, {}));
     sources_.push_back(src);

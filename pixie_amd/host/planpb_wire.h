@@ -197,9 +197,16 @@ enum OperatorType : int32_t {
   GRPC_SINK_OPERATOR = 9100,
 };
 
+struct LimitOperator {  // plan.proto:269-276
+  int64_t limit = 0;
+  std::vector<Column> columns;
+  std::vector<uint64_t> abortable_srcs;
+};
+
 struct Operator {  // plan.proto:82-110
   int32_t op_type = 0;
   int32_t which = 0;  // oneof field number
+  LimitOperator limit;
   MemorySourceOperator mem_source;
   MapOperator map;
   AggregateOperator agg;
@@ -403,6 +410,18 @@ inline void Decode(Reader r, Operator* op) {
         while (s.Next(&sf, &sw)) {
           if (sf == 1) Decode(s.Sub(), &op->filter.expression);
           else if (sf == 2) { op->filter.columns.emplace_back(); Decode(s.Sub(), &op->filter.columns.back()); }
+          else s.Skip(sw);
+        }
+        break;
+      }
+      case 7: {  // LimitOperator
+        op->which = 7;
+        Reader s = r.Sub();
+        uint32_t sf, sw;
+        while (s.Next(&sf, &sw)) {
+          if (sf == 1) op->limit.limit = static_cast<int64_t>(s.Varint());
+          else if (sf == 2) { op->limit.columns.emplace_back(); Decode(s.Sub(), &op->limit.columns.back()); }
+          else if (sf == 3) s.RepeatedVarint(sw, &op->limit.abortable_srcs);
           else s.Skip(sw);
         }
         break;

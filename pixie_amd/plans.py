@@ -123,6 +123,20 @@ def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Seque
     return op
 
 
+def limit_op(limit: int, columns: Sequence[int], abortable_srcs: Sequence[int] = (), node: int = 0):
+    """LimitOperator (plan.proto:269-276), as the PxL compiler inserts one before every result
+    sink (add_limit_to_batch_result_sink_rule.cc:40-68)."""
+    op = planpb.Operator()
+    op.op_type = 2300
+    op.limit_op.limit = limit
+    for c in columns:
+        cc = op.limit_op.columns.add()
+        cc.node = node
+        cc.index = c
+    op.limit_op.abortable_srcs.extend(abortable_srcs)
+    return op
+
+
 def sink_op(name: str, types: Sequence[int] = (), names: Sequence[str] = ()):
     op = planpb.Operator()
     op.op_type = 9000
@@ -231,6 +245,32 @@ def c2_plan(table: str = "http_events", with_pluck: bool = True):
         ops.append(pl)
     ops.append(sink_op("output"))
     return linear_plan(ops)
+
+
+def compiled_c2_plan(table: str = "http_events", limit: int = 10000):
+    """C2 in the shape the PxL compiler emits (compiler_test.cc:1265-1447): the aggregate followed
+    by an arithmetic Map (mean in seconds, error count + 1, p99 - p50 from the plucked
+    quantiles) and the Limit the compiler puts before the result sink (abortable: the source)."""
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES,
+                    [HE["service"], HE["req_path"], HE["resp_status"], HE["latency"]])
+    flt = filter_op(func("greaterThanEqual", [col(2), const(INT64, 400)], [INT64, INT64]), [0, 1, 2, 3])
+    mp = map_op([col(0), col(1), func("divide", [col(3), const(FLOAT64, 1e6)], [INT64, FLOAT64], fid=1)],
+                ["service", "req_path", "latency_ms"])
+    agg = agg_op([0, 1], [agg_expr("count", [col(2)], [FLOAT64], fid=2),
+                          agg_expr("mean", [col(2)], [FLOAT64], fid=3),
+                          agg_expr("quantiles", [col(2)], [FLOAT64], fid=4)],
+                 ["service", "req_path"], ["count", "mean", "latency_quantiles"])
+    p50 = func("pluck_float64", [col(4), const(STRING, "p50")], [STRING, STRING], fid=5)
+    p99 = func("pluck_float64", [col(4), const(STRING, "p99")], [STRING, STRING], fid=6)
+    post = map_op([col(0), col(1), func("add", [col(2), const(INT64, 1)], [INT64, INT64], fid=7),
+                   func("divide", [col(3), const(FLOAT64, 1000.0)], [FLOAT64, FLOAT64], fid=8),
+                   func("subtract", [p99, p50], [FLOAT64, FLOAT64], fid=9), p50,
+                   func("greaterThan", [func("multiply", [p50, const(FLOAT64, 2.0)], [FLOAT64, FLOAT64], fid=10), col(3)],
+                        [FLOAT64, FLOAT64], fid=11),
+                   col(4)],
+                  ["service", "req_path", "errors_plus_one", "mean_s", "p99_minus_p50", "p50", "skewed", "latency_quantiles"])
+    lim = limit_op(limit, list(range(8)), abortable_srcs=[1])
+    return linear_plan([src, flt, mp, agg, post, lim, sink_op("output")])
 
 
 def c3_plan(table: str = "http_events"):

@@ -242,9 +242,41 @@ join_case("unordered_many_matches", "592-687", P.JOIN_INNER, [(0, 1)], [(0, 1), 
            batch([[3, 6, 3, 6, 3], [103] * 5, [50, 50, 60, 60, 70]], False, False),
            batch([[6, 3, 6], [103] * 3, [70, 80, 80]], True, True)])
 
+# LimitNode (limit_node_test.cc, kLimitOperator1 / kLimitDropOperator1 = limit 10 over columns
+# {0, 1} / {0, 2}, test_proto.h:315-337).  ExecNodeTester feeds every batch with explicit flags.
+L = "src/carnot/exec/limit_node_test.cc"
+limit_cases = []
+c12 = [[1, 2, 3, 4, 5, 6, 1, 2, 3, 4, 5, 6], [1, 3, 6, 9, 12, 15, 1, 3, 6, 9, 12, 15]]
+lim = lambda n=10, cols=(0, 1): [P.limit_op(n, list(cols))]  # noqa: E731
+limit_cases.append(case("limit.single_batch", L + ":66-83", lim(), [I, I], [c12], [[True, True]], [I, I],
+                        [batch([c12[0][:10], c12[1][:10]], True, True)], ordered=True))
+limit_cases.append(case("limit.single_empty_batch", L + ":85-101", lim(), [I, I], [[[], []]], [[True, True]], [I, I],
+                        [batch([[], []], True, True)], ordered=True))
+limit_cases.append(case("limit.limit_zero", L + ":103-123", lim(0), [I, I], [c12], [[False, False]], [I, I],
+                        [batch([[], []], True, True)], ordered=True))
+limit_cases.append(case("limit.single_batch_exact_boundary", L + ":125-141", lim(), [I, I], [[c12[0][:10], c12[1][:10]]],
+                        [[False, False]], [I, I], [batch([c12[0][:10], c12[1][:10]], True, True)], ordered=True))
+limit_cases.append(case("limit.limits_records_split", L + ":143-170", lim(), [I, I],
+                        [[[1, 2, 3, 4, 5, 6], [1, 3, 6, 9, 12, 15]], [[1, 2, 3, 4, 5, 6], [1, 4, 6, 8, 10, 12]]],
+                        [[False, False], [True, True]], [I, I],
+                        [batch([[1, 2, 3, 4, 5, 6], [1, 3, 6, 9, 12, 15]], False, False),
+                         batch([[1, 2, 3, 4], [1, 4, 6, 8]], True, True)], ordered=True))
+limit_cases.append(case("limit.limits_exact_boundary", L + ":172-200", lim(), [I, I],
+                        [[[1, 2, 3, 4, 5, 6], [1, 3, 6, 9, 12, 15]], [[1, 2, 3, 4], [1, 4, 6, 8]]],
+                        [[False, False], [True, True]], [I, I],
+                        [batch([[1, 2, 3, 4, 5, 6], [1, 3, 6, 9, 12, 15]], False, False),
+                         batch([[1, 2, 3, 4], [1, 4, 6, 8]], True, True)], ordered=True))
+c3 = c12 + [[1, 4, 8, 12, 16, 20, 1, 4, 8, 12, 16, 20]]
+limit_cases.append(case("limit.drop_input_columns", L + ":216-237", lim(10, (0, 2)), [I, I, I], [c3], [[True, True]], [I, I],
+                        [batch([c3[0][:10], c3[2][:10]], True, True)], ordered=True))
+limit_cases.append(case("limit.drop_input_columns_fewer_than_limit", L + ":239-260", lim(10, (0, 2)), [I, I, I],
+                        [[c[:8] for c in c3]], [[True, True]], [I, I], [batch([c3[0][:8], c3[2][:8]], True, True)],
+                        ordered=True))
+
 doc = {
     "generator": "tests/golden/make_golden.py",
     "cases": cases,
+    "limit_cases": limit_cases,
     "join_cases": join_cases,
     # QuantilesUDA known answers (math_sketches_test.cc:30-70); EXPECT_DOUBLE_EQ = 4 ULP.
     "quantiles": [

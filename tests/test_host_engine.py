@@ -374,3 +374,66 @@ def test_store_errors(store_engine):
     assert e.value.code == 5
     store_engine.drop_table("t")
     assert store_engine.num_rows("t") == -1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", KAT["limit_cases"], ids=[c["name"] for c in KAT["limit_cases"]])
+def test_engine_matches_reference_limit_kat(engine, case):
+    """LimitNode (limit_node_test.cc) through the engine: slicing, eow/eos at the limit, limit 0,
+    dropped columns, later batches dropped."""
+    check_case_output(engine.execute(case_plan(case), case_tables(case))["out"], case)
+
+
+def test_compiled_c2_shape_lowers_with_device_post_map_and_limit():
+    txt = H.explain(P.compiled_c2_plan(), HTTP)
+    assert "GpuAggNode(fused filter/map chain)" in txt
+    assert "PostAggMapNode(device map over the aggregate rows) out=[STRING,STRING,INT64,FLOAT64,FLOAT64,FLOAT64,BOOLEAN,STRING]" in txt
+    assert "LimitNode(10000)" in txt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("limit", [10000, 37, 0])
+def test_engine_compiled_c2_with_arith_post_map_and_limit_matches_oracle(engine, limit):
+    """A compiler-shaped plan (compiler_test.cc:1265-1447): fused Filter/Map/Agg, then an
+    arithmetic Map over the aggregate (count + 1, mean / 1000, pluck(p99) - pluck(p50), a
+    comparison on a plucked value, the JSON passed through) and the Limit the compiler inserts
+    before the sink.  Aggregate row order is unspecified, so the limited rows must be a subset
+    of the oracle's unlimited result with equal values, and exactly min(limit, G) of them."""
+    from pixie_amd.device import datagen_http_events
+    cols = datagen_http_events(20250117, 0, 300_000, threads=8)
+    tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [[c.slice(a, min(a + 60_000, 300_000)) for c in cols]
+                                                                  for a in range(0, 300_000, 60_000)],
+                              "names": P.HTTP_NAMES}}
+    ref = oc.execute_plan(P.compiled_c2_plan(limit=1 << 40), tables)["output"]
+    dev = engine.execute(P.compiled_c2_plan(limit=limit), tables)["output"]
+    assert len(ref) == 1 and len(dev) == 1 and dev[0]["eow"] and dev[0]["eos"]
+    R = {r[:2]: r[2:] for r in rows(ref[0]["cols"])}
+    D = [r for r in rows(dev[0]["cols"])]
+    assert len(D) == min(limit, len(R))
+    for r in D:
+        w = R[r[:2]]
+        assert r[2] == w[0]                                     # count + 1
+        assert abs(r[3] - w[1]) <= 1e-6 * abs(w[1])             # mean / 1000
+        assert ulp_diff(r[5], w[3]) <= 4                        # plucked p50
+        assert abs(r[4] - w[2]) <= 1e-12 * max(1.0, abs(w[2]))  # p99 - p50
+        assert r[6] == w[4]                                     # p50 * 2 > mean
+        assert json.loads(r[7]) == pytest.approx(json.loads(w[5]), rel=1e-12)
+
+
+@pytest.mark.gpu
+def test_engine_limit_stops_the_source(engine):
+    """Filter -> Map -> Limit over a 40-batch table: the batch that reaches the limit is cut and
+    carries eow/eos, and no batch follows it (the source is aborted)."""
+    from pixie_amd.device import datagen_http_events
+    cols = datagen_http_events(3, 0, 400_000, threads=8)
+    tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [[c.slice(a, a + 10_000) for c in cols] for a in range(0, 400_000, 10_000)],
+                              "names": P.HTTP_NAMES}}
+    plan = P.linear_plan([P.source_op("http_events", P.HTTP_TYPES, P.HTTP_NAMES, list(range(10))),
+                          P.filter_op(P.func("greaterThanEqual", [P.col(5), P.const(2, 400)], [2, 2]), [2, 3, 6]),
+                          P.map_op([P.col(0), P.func("divide", [P.col(2), P.const(4, 1e6)], [2, 4])], ["svc", "ms"]),
+                          P.limit_op(5000, [0, 1], abortable_srcs=[1]), P.sink_op("out")])
+    ref = oc.execute_plan(plan, tables)["out"]
+    dev = engine.execute(plan, tables)["out"]
+    assert [(len(b["cols"][0]), b["eow"], b["eos"]) for b in dev] == [(len(b["cols"][0]), b["eow"], b["eos"]) for b in ref]
+    assert sum(len(b["cols"][0]) for b in dev) == 5000 and dev[-1]["eos"]
+    assert [rows(b["cols"]) for b in dev] == [rows(b["cols"]) for b in ref]

@@ -94,3 +94,8 @@ def test_unknown_udf_is_not_found():
     with pytest.raises(oc.OracleError) as e:
         oc.execute_plan(plan, {"t": {"types": [2], "batches": []}})
     assert e.value.code == 5
+
+
+@pytest.mark.parametrize("case", KAT["limit_cases"], ids=[c["name"] for c in KAT["limit_cases"]])
+def test_oracle_limit_node_kat(case):
+    check_case_output(oc.execute_plan(case_plan(case), case_tables(case))["out"], case)
