@@ -7,14 +7,18 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("PXC_TIMING", "1")
 from pixie_amd import plans as P  # noqa: E402
-from pixie_amd.device import datagen_http_events  # noqa: E402
+from pixie_amd.device import Ctx, Table, datagen_http_events  # noqa: E402
 from pixie_amd.host_engine import Engine  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 100_000_000
 e = Engine(0)
 e.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
-for a in range(0, n, 16_000_000):
-    e.append("http_events", datagen_http_events(20250117, a, min(16_000_000, n - a), n_pair_keys=10_000_000, threads=16))
+if "--host-gen" in sys.argv:
+    for a in range(0, n, 16_000_000):
+        e.append("http_events", datagen_http_events(20250117, a, min(16_000_000, n - a), n_pair_keys=10_000_000, threads=16))
+else:
+    ctx = Ctx(0, handle=e.ctx_handle())
+    Table(ctx, P.HTTP_TYPES, handle=e.device_table("http_events"), owned=False).append_http_events(20250117, 0, n)
 print("rows", e.num_rows("http_events"), flush=True)
 pb = P.c2_plan(with_pluck=True).SerializeToString()
 for i in range(4):
