@@ -115,6 +115,13 @@ pxg_ctx* pxc_engine_ctx(pxc_engine* engine);
 int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t plan_len, int32_t ntables,
                                 const pxc_table* tables, char** out);
 
+/* The engine's own lowering of a plan's (fused Filter/Map ->) aggregation as a pxg_agg over a
+ * device table named table_name with the given column types (the MemorySource is lowered as
+ * over a stored device table).  *n_keys / *n_udas and uda_kinds[0..n_udas) (pxg_uda_kind,
+ * capacity 16) describe its result columns.  Release with pxg_agg_destroy. */
+int32_t pxc_plan_create_agg(pxg_ctx* ctx, const uint8_t* plan, int64_t plan_len, const char* table_name,
+                            int32_t ncols, const int32_t* types, int64_t expected_groups, pxg_agg** out,
+                            int32_t* n_keys, int32_t* n_udas, int32_t* uda_kinds);
 void pxc_free(void* p);
 /* QuantilesUDA::Finalize JSON (math_sketches.h:40-54, bytes as rapidjson's Writer emits them)
  * for n groups of 7 doubles (p01..p99): one buffer of n NUL-terminated strings (pxc_free). */

@@ -218,6 +218,13 @@ int32_t pxg_table_time_bound(pxg_table* t, int32_t col, int64_t value, int32_t s
  * `select` order) of the passing rows, order preserved, into a new device table. */
 int32_t pxg_filter(pxg_table* in, const pxg_program* pred, int32_t n_select,
                    const int32_t* select, int64_t begin, int64_t end, pxg_table** out);
+/* pxg_filter over rows that are the concatenation of n_splits RowBatches (split_rows[i] rows
+ * each, summing to end - begin): one device pass for all of them, and out_split_rows[i]
+ * receives the number of output rows that came from batch i, so the caller emits one output
+ * batch per input batch exactly as FilterNode does (filter_node.cc:132-171). */
+int32_t pxg_filter_split(pxg_table* in, const pxg_program* pred, int32_t n_select,
+                         const int32_t* select, int64_t begin, int64_t end, int32_t n_splits,
+                         const int64_t* split_rows, int64_t* out_split_rows, pxg_table** out);
 /* MapNode: one output column per program (fixed-width results; a program that is a single
  * column reference of any type is passed through). */
 int32_t pxg_map(pxg_table* in, int32_t n_exprs, const pxg_program* exprs, int64_t begin,

@@ -81,7 +81,7 @@ EXPORTED = [
     "pxg_ctx_sync", "pxg_ctx_stream", "pxg_ctx_set_profiling", "pxg_ctx_profile_only", "pxg_ctx_kernel_stats",
     "pxg_ctx_reset_stats", "pxg_table_create", "pxg_table_destroy", "pxg_table_append",
     "pxg_table_append_device", "pxg_table_flush", "pxg_table_num_rows", "pxg_table_num_chunks",
-    "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_map", "pxg_agg_create",
+    "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_result_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial",
     "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events",
@@ -134,6 +134,7 @@ def load() -> C.CDLL:
         "pxg_table_device_bytes": (i64, [vp, i32]),
         "pxg_table_fetch": (i32, [vp, i32, i64, i64, p(ColumnOut)]),
         "pxg_filter": (i32, [vp, p(Program), i32, p(i32), i64, i64, p(vp)]),
+        "pxg_filter_split": (i32, [vp, p(Program), i32, p(i32), i64, i64, i32, p(i64), p(i64), p(vp)]),
         "pxg_map": (i32, [vp, i32, p(Program), i64, i64, p(vp)]),
         "pxg_agg_create": (i32, [vp, p(AggSpec), p(vp)]),
         "pxg_agg_destroy": (i32, [vp]),

@@ -111,8 +111,14 @@ struct PendingTiming {
   hipEvent_t start, stop;
 };
 
+// Grow-only workspace of the standalone Filter / Map operators (pxg_ops.hip).
+struct OpsWorkspace {
+  DevBuf prog, masks, tiles, scan, scan2;
+};
+
 struct Ctx {
   int device = 0;
+  OpsWorkspace ops;
   hipStream_t stream = nullptr;
   // Side stream for latency-bound work that overlaps the main stream (fork/join by events).
   hipStream_t side = nullptr;

@@ -1,8 +1,22 @@
-// Standalone FilterNode / MapNode over device tables (operator shapes the fused agg path
-// does not cover).  FilterNode::ConsumeNextImpl (filter_node.cc:132-171): evaluate the
-// predicate, then compact every selected column preserving row order (filter_node.cc:88-92).
+// Standalone FilterNode / MapNode over device tables (operator shapes the fused agg path does
+// not cover).
+//
+// FilterNode::ConsumeNextImpl (filter_node.cc:132-171): evaluate the predicate, then compact
+// every selected column, preserving row order (filter_node.cc:88-92).  On the device this is
+// ballot compaction: pass 1 streams the predicate's columns and writes one 64-row ballot word
+// per wave iteration plus one count per 4096-row tile; a small scan turns the tile counts into
+// output bases; pass 2 re-reads the ballot words, ranks every selected row inside its tile
+// (LDS prefix of the tile's ballot popcounts + the lane's popcount below it) and gathers every
+// selected column in one launch.  STRING columns: the gather writes lengths and source rows,
+// one scan makes the offsets, and a word-wise copy moves the payload (8-byte unaligned loads and
+// stores, gfx950 serves them in hardware).
+//
 // MapNode::ConsumeNextImpl (map_node.cc:64-71): one output column per expression; column
-// references are passed through.
+// references pass through (device-to-device copies).
+//
+// No per-call hipMalloc of workspace and no synchronous program upload: programs, ballot words,
+// tile counts and scan scratch live in the ctx's grow-only ops workspace; a call synchronises
+// once per chunk for the output sizes it must allocate.
 #include <algorithm>
 
 #include "pxg_internal.h"
@@ -11,64 +25,129 @@
 
 namespace pxg {
 
-struct ProgBuf {
-  DevBuf prog;
-  DevBuf pool;
-  DevBuf types;
-};
+constexpr int kOpsBlock = 256;
+constexpr int kOpsTileRows = 4096;                      // rows per workgroup tile
+constexpr int kOpsMasksPerTile = kOpsTileRows / 64;     // 64 ballot words
+constexpr int kOpsMasksPerWave = kOpsMasksPerTile / 4;  // 16 per wave
 
-static int32_t UploadProgram(Ctx* ctx, const pxg_program& p, const Table& t, ProgBuf* pb) {
-  DevProgram dp;
+// Device programs of one call, uploaded once into the ctx workspace.
+static int32_t UploadPrograms(Ctx* ctx, const pxg_program* progs, int n, const Table& t, const DevProgram** d_progs,
+                              const int32_t** d_types) {
+  std::vector<DevProgram> dp(static_cast<size_t>(std::max(n, 1)));
   std::vector<uint8_t> pool;
-  size_t off = 0;
-  PXG_RETURN_IF_ERROR(CompileProgram(p, t.types.data(), t.ncols, &dp, &pool, &off));
-  PXG_RETURN_IF_ERROR(pb->pool.Alloc(pool.size() + 16));
-  if (!pool.empty()) PXG_HIP(hipMemcpy(pb->pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
-  dp.pool = pb->pool.as<uint8_t>() + off;
-  PXG_RETURN_IF_ERROR(pb->prog.Alloc(sizeof(DevProgram)));
-  PXG_HIP(hipMemcpy(pb->prog.p, &dp, sizeof(DevProgram), hipMemcpyHostToDevice));
-  std::vector<int32_t> ty(kMaxCols, 0);
-  for (int k = 0; k < t.ncols; ++k) ty[k] = t.types[k];
-  PXG_RETURN_IF_ERROR(pb->types.Alloc(kMaxCols * 4));
-  PXG_HIP(hipMemcpy(pb->types.p, ty.data(), kMaxCols * 4, hipMemcpyHostToDevice));
-  (void)ctx;
+  std::vector<size_t> offs(static_cast<size_t>(std::max(n, 1)));
+  for (int i = 0; i < n; ++i) PXG_RETURN_IF_ERROR(CompileProgram(progs[i], t.types.data(), t.ncols, &dp[i], &pool, &offs[i]));
+  const size_t prog_bytes = dp.size() * sizeof(DevProgram);
+  const size_t types_off = (prog_bytes + 255) & ~size_t(255);
+  const size_t pool_off = types_off + kMaxCols * 4 + 256;
+  OpsWorkspace& w = ctx->ops;
+  PXG_RETURN_IF_ERROR(w.prog.Ensure(pool_off + pool.size() + 16));
+  uint8_t* base = w.prog.as<uint8_t>();
+  for (int i = 0; i < n; ++i) dp[i].pool = base + pool_off + offs[i];
+  std::vector<uint8_t> host(pool_off + pool.size(), 0);
+  std::memcpy(host.data(), dp.data(), prog_bytes);
+  for (int k = 0; k < t.ncols; ++k) std::memcpy(host.data() + types_off + 4 * k, &t.types[k], 4);
+  if (!pool.empty()) std::memcpy(host.data() + pool_off, pool.data(), pool.size());
+  PXG_HIP(hipMemcpyAsync(base, host.data(), host.size(), hipMemcpyHostToDevice, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));  // `host` is pageable and goes out of scope
+  *d_progs = reinterpret_cast<const DevProgram*>(base);
+  *d_types = reinterpret_cast<const int32_t*>(base + types_off);
   return PXG_OK;
 }
 
-__global__ void FilterFlagsKernel(const DevProgram* __restrict__ prog, const DevChunk* __restrict__ chunks, int chunk,
-                                  const int32_t* __restrict__ types, int64_t lo, int64_t n, uint32_t* __restrict__ flags) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  flags[i] = EvalProgram(prog, chunks[chunk], lo + i, types).a != 0 ? 1u : 0u;
+// Pass 1: ballot words of the predicate and per-tile selected counts.
+__global__ void __launch_bounds__(kOpsBlock) FilterMaskKernel(const DevProgram* __restrict__ prog, const DevChunk* __restrict__ chunks,
+                                                              int chunk, const int32_t* __restrict__ types, int64_t lo, int64_t n,
+                                                              unsigned long long* __restrict__ masks, uint32_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t s_cnt[kOpsBlock / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const DevChunk& ch = chunks[chunk];
+  const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * kOpsTileRows;
+  uint32_t cnt = 0;
+  for (int k = 0; k < kOpsMasksPerWave; ++k) {
+    const int64_t r = tile0 + (static_cast<int64_t>(wid) * kOpsMasksPerWave + k) * 64 + lane;
+    const bool pass = r < n && EvalProgram(prog, ch, lo + r, types).a != 0;
+    const unsigned long long m = __ballot(pass);
+    cnt += static_cast<uint32_t>(__popcll(m));
+    const int64_t mi = static_cast<int64_t>(blockIdx.x) * kOpsMasksPerTile + wid * kOpsMasksPerWave + k;
+    if (lane == 0) masks[mi] = m;
+  }
+  if (lane == 0) s_cnt[wid] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
-__global__ void FilterGatherFixedKernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int width,
-                                        const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos, int64_t lo, int64_t n) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n || !flags[i]) return;
-  const uint8_t* s = src + (lo + i) * width;
-  uint8_t* d = dst + static_cast<int64_t>(pos[i]) * width;
-  if (width == 8) *reinterpret_cast<uint64_t*>(d) = *reinterpret_cast<const uint64_t*>(s);
-  else if (width == 16) { reinterpret_cast<uint64_t*>(d)[0] = reinterpret_cast<const uint64_t*>(s)[0]; reinterpret_cast<uint64_t*>(d)[1] = reinterpret_cast<const uint64_t*>(s)[1]; }
-  else for (int b = 0; b < width; ++b) d[b] = s[b];
+struct GatherCols {
+  int32_t n;
+  int32_t width[kMaxCols];  // bytes per value; 0 = STRING
+  const uint8_t* src[kMaxCols];       // fixed values
+  const int32_t* src_off[kMaxCols];   // STRING offsets
+  uint8_t* dst[kMaxCols];             // fixed output values
+  uint32_t* dst_len[kMaxCols];        // STRING: length of output row (scanned to offsets later)
+  uint32_t* dst_src[kMaxCols];        // STRING: source row of output row
+};
+
+// Pass 2: rank every selected row (tile base + prefix of the tile's ballot popcounts + the
+// lane's bits below it) and gather every selected column.
+__global__ void __launch_bounds__(kOpsBlock) FilterGatherKernel(const unsigned long long* __restrict__ masks,
+                                                                const uint32_t* __restrict__ tile_base, int64_t lo, int64_t n,
+                                                                GatherCols gc) {
+  __shared__ uint32_t s_pre[kOpsMasksPerTile];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const int64_t mask0 = static_cast<int64_t>(blockIdx.x) * kOpsMasksPerTile;
+  if (threadIdx.x < kOpsMasksPerTile) {  // one wave: exclusive prefix of the 64 popcounts
+    const uint32_t c = static_cast<uint32_t>(__popcll(masks[mask0 + threadIdx.x]));
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    s_pre[threadIdx.x] = x - c;
+  }
+  __syncthreads();
+  const uint32_t base = tile_base[blockIdx.x];
+  for (int k = 0; k < kOpsMasksPerWave; ++k) {
+    const int mi = wid * kOpsMasksPerWave + k;
+    const unsigned long long m = masks[mask0 + mi];
+    if (!((m >> lane) & 1ULL)) continue;
+    const int64_t r = lo + static_cast<int64_t>(blockIdx.x) * kOpsTileRows + mi * 64 + lane;
+    const uint32_t pos = base + s_pre[mi] + static_cast<uint32_t>(__popcll(m & lanemask_lt));
+    for (int c = 0; c < gc.n; ++c) {
+      const int w = gc.width[c];
+      if (w == 8) {
+        reinterpret_cast<uint64_t*>(gc.dst[c])[pos] = reinterpret_cast<const uint64_t*>(gc.src[c])[r];
+      } else if (w == 16) {
+        reinterpret_cast<ulonglong2*>(gc.dst[c])[pos] = reinterpret_cast<const ulonglong2*>(gc.src[c])[r];
+      } else if (w == 1) {
+        gc.dst[c][pos] = gc.src[c][r];
+      } else {
+        gc.dst_len[c][pos] = static_cast<uint32_t>(gc.src_off[c][r + 1] - gc.src_off[c][r]);
+        gc.dst_src[c][pos] = static_cast<uint32_t>(r);
+      }
+    }
+  }
+  (void)n;
 }
 
-__global__ void FilterStrLenKernel(const int32_t* __restrict__ off, const uint32_t* __restrict__ flags, const uint32_t* __restrict__ pos,
-                                   int64_t lo, int64_t n, uint32_t* __restrict__ lens, uint32_t* __restrict__ src_row) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n || !flags[i]) return;
-  lens[pos[i]] = static_cast<uint32_t>(off[lo + i + 1] - off[lo + i]);
-  src_row[pos[i]] = static_cast<uint32_t>(lo + i);
-}
-
-__global__ void StrCopyKernel(const int32_t* __restrict__ soff, const uint8_t* __restrict__ sdata, const uint32_t* __restrict__ src_row,
-                              const uint32_t* __restrict__ doff, uint8_t* __restrict__ ddata, int64_t m) {
+// Word-wise string gather: output row i gets the bytes of source row src[i].
+__global__ void StrGatherKernel(const int32_t* __restrict__ soff, const uint8_t* __restrict__ sdata, const uint32_t* __restrict__ src,
+                                const uint32_t* __restrict__ doff, uint8_t* __restrict__ ddata, int64_t m) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  const uint32_t r = src_row[i];
-  const int32_t a = soff[r], b = soff[r + 1];
+  const uint32_t r = src[i];
+  const int32_t a = soff[r];
+  const uint32_t len = static_cast<uint32_t>(soff[r + 1] - a);
+  const uint8_t* s = sdata + a;
   uint8_t* d = ddata + doff[i];
-  for (int32_t k = a; k < b; ++k) d[k - a] = sdata[k];
+  uint32_t k = 0;
+  for (; k + 8 <= len; k += 8) {
+    uint64_t x;
+    __builtin_memcpy(&x, s + k, 8);
+    __builtin_memcpy(d + k, &x, 8);
+  }
+  for (; k < len; ++k) d[k] = s[k];
 }
 
 __global__ void MapEvalKernel(const DevProgram* __restrict__ prog, const DevChunk* __restrict__ chunks, int chunk,
@@ -86,8 +165,145 @@ __global__ void RebaseKernel(int32_t* __restrict__ dst, const int32_t* __restric
   if (i < n) dst[i] = src[i] - src[0];
 }
 
-static int32_t NewOutTable(Ctx* ctx, const std::vector<int32_t>& types, pxg_table** out) {
-  return NewTable(ctx, static_cast<int32_t>(types.size()), types.data(), out);
+static int32_t ReadU32(Ctx* ctx, const void* p, uint32_t* out) {
+  PXG_HIP(hipMemcpyAsync(out, p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+// Filter rows [begin, end) of t into a new table; per_split (optional) receives the selected
+// rows of each of n_splits consecutive input row ranges (split_rows[i] rows each).
+static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, const int32_t* select, int64_t begin, int64_t end,
+                          int32_t n_splits, const int64_t* split_rows, int64_t* per_split, pxg_table** out) {
+  Ctx* ctx = t.ctx;
+  PXG_RETURN_IF_ERROR(t.EnsureDeviceDescriptors());
+  if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
+  if (pred.result_type != PXG_BOOLEAN) return SetError(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
+  std::vector<int32_t> otypes;
+  for (int i = 0; i < n_select; ++i) {
+    if (select[i] < 0 || select[i] >= t.ncols) return SetError(PXG_INVALID_ARGUMENT, "selected column %d out of range", select[i]);
+    otypes.push_back(t.types[select[i]]);
+  }
+  if (n_splits > 0) {
+    int64_t tot = 0;
+    for (int i = 0; i < n_splits; ++i) tot += split_rows[i];
+    if (tot != end - begin) return SetError(PXG_INVALID_ARGUMENT, "split rows add up to %lld, range has %lld", (long long)tot, (long long)(end - begin));
+  }
+  const DevProgram* d_prog = nullptr;
+  const int32_t* d_types = nullptr;
+  PXG_RETURN_IF_ERROR(UploadPrograms(ctx, &pred, 1, t, &d_prog, &d_types));
+  pxg_table* ot = nullptr;
+  PXG_RETURN_IF_ERROR(NewTable(ctx, static_cast<int32_t>(otypes.size()), otypes.data(), &ot));
+  std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(ot, pxg_table_destroy);
+  Table& o = ot->impl;
+  OpsWorkspace& w = ctx->ops;
+  std::vector<unsigned long long> host_masks;
+  for (size_t c = 0; c < t.chunks.size(); ++c) {
+    const Chunk& ch = *t.chunks[c];
+    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
+    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
+    if (lo >= hi) continue;
+    const int64_t n = hi - lo;
+    const int64_t ntiles = (n + kOpsTileRows - 1) / kOpsTileRows;
+    const int64_t nmasks = ntiles * kOpsMasksPerTile;
+    PXG_RETURN_IF_ERROR(w.masks.Ensure(static_cast<size_t>(nmasks) * 8 + 64));
+    PXG_RETURN_IF_ERROR(w.tiles.Ensure(static_cast<size_t>(ntiles + 1) * 4 + 64));
+    PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(ntiles + 1) + 64));
+    uint32_t* tiles = w.tiles.as<uint32_t>();
+    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_mask", FilterMaskKernel, dim3(static_cast<unsigned>(ntiles)), dim3(kOpsBlock), 0, d_prog,
+                               t.d_chunks.as<const DevChunk>(), static_cast<int>(c), d_types, lo, n,
+                               w.masks.as<unsigned long long>(), tiles));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, tiles, tiles, ntiles, tiles + ntiles, w.scan.p));
+    uint32_t m = 0;
+    if (n_splits > 0) {  // ballot words back to the host: per-split counts by popcount
+      host_masks.resize(static_cast<size_t>(nmasks));
+      PXG_HIP(hipMemcpyAsync(host_masks.data(), w.masks.p, static_cast<size_t>(nmasks) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    PXG_RETURN_IF_ERROR(ReadU32(ctx, tiles + ntiles, &m));
+    if (n_splits > 0) {
+      // split i covers input rows [s0, s1) of [begin, end); this chunk covers [cb, cb + n)
+      const int64_t cb = ch.row_base + lo - begin;
+      int64_t s0 = 0;
+      for (int i = 0; i < n_splits; ++i) {
+        const int64_t s1 = s0 + split_rows[i];
+        const int64_t a = std::max(s0, cb) - cb, b = std::min(s1, cb + n) - cb;
+        for (int64_t r = a; r < b;) {
+          const int64_t wi = r >> 6;
+          const int64_t e = std::min(b, (wi + 1) << 6);
+          unsigned long long mk = host_masks[static_cast<size_t>(wi)] >> (r & 63);
+          const int64_t bits = e - r;
+          if (bits < 64) mk &= (1ULL << bits) - 1;
+          per_split[i] += __builtin_popcountll(mk);
+          r = e;
+        }
+        s0 = s1;
+      }
+    }
+    auto oc = std::make_unique<Chunk>();
+    oc->row_base = o.nrows;
+    oc->nrows = m;
+    oc->rows_cap = m;
+    oc->sealed = true;
+    oc->cols.resize(static_cast<size_t>(n_select));
+    GatherCols gc;
+    std::memset(&gc, 0, sizeof(gc));
+    gc.n = n_select;
+    std::vector<DevBuf> lens(static_cast<size_t>(n_select)), srcs(static_cast<size_t>(n_select));
+    for (int s = 0; s < n_select; ++s) {
+      const int ci = select[s];
+      const int ty = t.types[ci];
+      ChunkCol& dc = oc->cols[static_cast<size_t>(s)];
+      if (ty != PXG_STRING) {
+        const int wd = TypeWidth(ty);
+        gc.width[s] = wd;
+        PXG_RETURN_IF_ERROR(dc.values.Alloc(static_cast<size_t>(m) * wd + 16));
+        gc.src[s] = ch.cols[ci].values.as<const uint8_t>();
+        gc.dst[s] = dc.values.as<uint8_t>();
+      } else {
+        gc.width[s] = 0;
+        PXG_RETURN_IF_ERROR(dc.offsets.Alloc((static_cast<size_t>(m) + 1) * 4 + 16));
+        PXG_RETURN_IF_ERROR(srcs[s].Alloc(static_cast<size_t>(m) * 4 + 16));
+        gc.src_off[s] = ch.cols[ci].offsets.as<const int32_t>();
+        gc.dst_len[s] = dc.offsets.as<uint32_t>();
+        gc.dst_src[s] = srcs[s].as<uint32_t>();
+      }
+    }
+    if (m > 0 && n_select > 0)
+      PXG_RETURN_IF_ERROR(Launch(ctx, "filter_gather", FilterGatherKernel, dim3(static_cast<unsigned>(ntiles)), dim3(kOpsBlock), 0,
+                                 static_cast<const unsigned long long*>(w.masks.as<unsigned long long>()),
+                                 static_cast<const uint32_t*>(tiles), lo, n, gc));
+    // STRING columns: lengths -> offsets (one scan each), one sync for every payload size.
+    std::vector<uint32_t> bytes(static_cast<size_t>(n_select), 0);
+    bool any_str = false;
+    for (int s = 0; s < n_select; ++s) {
+      if (gc.width[s] != 0) continue;
+      any_str = true;
+      uint32_t* doff = gc.dst_len[s];
+      PXG_RETURN_IF_ERROR(w.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(m) + 1) + 64));
+      PXG_HIP(hipMemsetAsync(doff + m, 0, 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, doff, doff, static_cast<int64_t>(m) + 1, nullptr, w.scan2.p));
+      PXG_HIP(hipMemcpyAsync(&bytes[static_cast<size_t>(s)], doff + m, 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (any_str) PXG_HIP(hipStreamSynchronize(ctx->stream));
+    for (int s = 0; s < n_select; ++s) {
+      if (gc.width[s] != 0) continue;
+      const int ci = select[s];
+      ChunkCol& dc = oc->cols[static_cast<size_t>(s)];
+      PXG_RETURN_IF_ERROR(dc.data.Alloc(static_cast<size_t>(bytes[static_cast<size_t>(s)]) + 16));
+      dc.data_len = bytes[static_cast<size_t>(s)];
+      if (m > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "str_gather", StrGatherKernel, dim3(GridFor(m, 256, 1 << 30)), dim3(256), 0,
+                                   ch.cols[ci].offsets.as<const int32_t>(), ch.cols[ci].data.as<const uint8_t>(),
+                                   srcs[s].as<const uint32_t>(), static_cast<const uint32_t*>(gc.dst_len[s]), dc.data.as<uint8_t>(),
+                                   static_cast<int64_t>(m)));
+    }
+    PXG_HIP(hipStreamSynchronize(ctx->stream));  // srcs are freed at scope exit
+    o.nrows += m;
+    o.chunks.push_back(std::move(oc));
+    ++o.version;
+  }
+  *out = guard.release();
+  return PXG_OK;
 }
 
 }  // namespace pxg
@@ -97,85 +313,17 @@ using namespace pxg;
 extern "C" int32_t pxg_filter(pxg_table* inp, const pxg_program* pred, int32_t n_select, const int32_t* select, int64_t begin,
                               int64_t end, pxg_table** out) {
   if (!inp || !pred || !out || n_select < 0 || (n_select > 0 && !select)) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
-  Table& t = inp->impl;
-  Ctx* ctx = t.ctx;
-  PXG_RETURN_IF_ERROR(t.EnsureDeviceDescriptors());
-  if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
-  if (pred->result_type != PXG_BOOLEAN) return SetError(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
-  std::vector<int32_t> otypes;
-  for (int i = 0; i < n_select; ++i) {
-    if (select[i] < 0 || select[i] >= t.ncols) return SetError(PXG_INVALID_ARGUMENT, "selected column %d out of range", select[i]);
-    otypes.push_back(t.types[select[i]]);
-  }
-  ProgBuf pb;
-  PXG_RETURN_IF_ERROR(UploadProgram(ctx, *pred, t, &pb));
-  pxg_table* ot = nullptr;
-  PXG_RETURN_IF_ERROR(NewOutTable(ctx, otypes, &ot));
-  std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(ot, pxg_table_destroy);
-  Table& o = ot->impl;
-  for (size_t c = 0; c < t.chunks.size(); ++c) {
-    const Chunk& ch = *t.chunks[c];
-    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
-    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
-    if (lo >= hi) continue;
-    const int64_t n = hi - lo;
-    DevBuf flags, pos, scratch, total;
-    PXG_RETURN_IF_ERROR(flags.Alloc(n * 4));
-    PXG_RETURN_IF_ERROR(pos.Alloc(n * 4));
-    PXG_RETURN_IF_ERROR(scratch.Alloc(ScanScratchBytes(n) + 64));
-    PXG_RETURN_IF_ERROR(total.Alloc(16));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_flags", FilterFlagsKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0,
-                               pb.prog.as<const DevProgram>(), t.d_chunks.as<const DevChunk>(), static_cast<int>(c), pb.types.as<const int32_t>(),
-                               lo, n, flags.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, flags.as<const uint32_t>(), pos.as<uint32_t>(), n, total.as<uint32_t>(), scratch.p));
-    uint32_t m = 0;
-    PXG_HIP(hipMemcpyAsync(&m, total.p, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
-    auto oc = std::make_unique<Chunk>();
-    oc->row_base = o.nrows;
-    oc->nrows = m;
-    oc->rows_cap = m;
-    oc->sealed = true;
-    oc->cols.resize(n_select);
-    for (int s = 0; s < n_select; ++s) {
-      const int ci = select[s];
-      const int ty = t.types[ci];
-      ChunkCol& dc = oc->cols[s];
-      if (ty != PXG_STRING) {
-        const int w = TypeWidth(ty);
-        PXG_RETURN_IF_ERROR(dc.values.Alloc(static_cast<size_t>(m) * w + 16));
-        PXG_RETURN_IF_ERROR(Launch(ctx, "filter_gather", FilterGatherFixedKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0,
-                                   ch.cols[ci].values.as<const uint8_t>(), dc.values.as<uint8_t>(), w, flags.as<const uint32_t>(),
-                                   pos.as<const uint32_t>(), lo, n));
-      } else {
-        DevBuf src_row;
-        PXG_RETURN_IF_ERROR(dc.offsets.Alloc((static_cast<size_t>(m) + 1) * 4 + 16));
-        PXG_RETURN_IF_ERROR(src_row.Alloc(static_cast<size_t>(m) * 4 + 16));
-        PXG_RETURN_IF_ERROR(Launch(ctx, "filter_strlen", FilterStrLenKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0,
-                                   ch.cols[ci].offsets.as<const int32_t>(), flags.as<const uint32_t>(), pos.as<const uint32_t>(), lo, n,
-                                   dc.offsets.as<uint32_t>(), src_row.as<uint32_t>()));
-        DevBuf sc2;
-        PXG_RETURN_IF_ERROR(sc2.Alloc(ScanScratchBytes(m) + 64));
-        uint32_t* doff = dc.offsets.as<uint32_t>();
-        PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, doff, doff, m, doff + m, sc2.p));
-        uint32_t bytes = 0;
-        PXG_HIP(hipMemcpyAsync(&bytes, doff + m, 4, hipMemcpyDeviceToHost, ctx->stream));
-        PXG_HIP(hipStreamSynchronize(ctx->stream));
-        PXG_RETURN_IF_ERROR(dc.data.Alloc(static_cast<size_t>(bytes) + 16));
-        dc.data_len = bytes;
-        PXG_RETURN_IF_ERROR(Launch(ctx, "str_copy", StrCopyKernel, dim3(GridFor(m, 256, 1 << 30)), dim3(256), 0,
-                                   ch.cols[ci].offsets.as<const int32_t>(), ch.cols[ci].data.as<const uint8_t>(), src_row.as<const uint32_t>(),
-                                   static_cast<const uint32_t*>(doff), dc.data.as<uint8_t>(), static_cast<int64_t>(m)));
-        PXG_HIP(hipStreamSynchronize(ctx->stream));
-      }
-    }
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
-    o.nrows += m;
-    o.chunks.push_back(std::move(oc));
-    ++o.version;
-  }
-  *out = guard.release();
-  return PXG_OK;
+  return FilterImpl(inp->impl, *pred, n_select, select, begin, end, 0, nullptr, nullptr, out);
+}
+
+extern "C" int32_t pxg_filter_split(pxg_table* inp, const pxg_program* pred, int32_t n_select, const int32_t* select, int64_t begin,
+                                    int64_t end, int32_t n_splits, const int64_t* split_rows, int64_t* out_split_rows,
+                                    pxg_table** out) {
+  if (!inp || !pred || !out || n_select < 0 || (n_select > 0 && !select) || n_splits < 0 ||
+      (n_splits > 0 && (!split_rows || !out_split_rows)))
+    return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  for (int i = 0; i < n_splits; ++i) out_split_rows[i] = 0;
+  return FilterImpl(inp->impl, *pred, n_select, select, begin, end, n_splits, split_rows, out_split_rows, out);
 }
 
 extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* exprs, int64_t begin, int64_t end, pxg_table** out) {
@@ -185,17 +333,18 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
   PXG_RETURN_IF_ERROR(t.EnsureDeviceDescriptors());
   if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
   std::vector<int32_t> otypes;
-  std::vector<ProgBuf> pbs(n_exprs);
   for (int e = 0; e < n_exprs; ++e) {
     const pxg_program& p = exprs[e];
     const bool passthrough = p.n_insns == 1 && p.insns && p.insns[0].op == PXG_OP_COL;
     if (p.result_type == PXG_STRING && !passthrough)
       return SetError(PXG_UNIMPLEMENTED, "STRING-producing scalar UDFs are not implemented on device");
-    PXG_RETURN_IF_ERROR(UploadProgram(ctx, p, t, &pbs[e]));
     otypes.push_back(p.result_type);
   }
+  const DevProgram* d_progs = nullptr;
+  const int32_t* d_types = nullptr;
+  PXG_RETURN_IF_ERROR(UploadPrograms(ctx, exprs, n_exprs, t, &d_progs, &d_types));
   pxg_table* ot = nullptr;
-  PXG_RETURN_IF_ERROR(NewOutTable(ctx, otypes, &ot));
+  PXG_RETURN_IF_ERROR(NewTable(ctx, static_cast<int32_t>(otypes.size()), otypes.data(), &ot));
   std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(ot, pxg_table_destroy);
   Table& o = ot->impl;
   for (size_t c = 0; c < t.chunks.size(); ++c) {
@@ -209,17 +358,17 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
     oc->nrows = n;
     oc->rows_cap = n;
     oc->sealed = true;
-    oc->cols.resize(n_exprs);
+    oc->cols.resize(static_cast<size_t>(n_exprs));
     for (int e = 0; e < n_exprs; ++e) {
       const pxg_program& p = exprs[e];
-      ChunkCol& dc = oc->cols[e];
+      ChunkCol& dc = oc->cols[static_cast<size_t>(e)];
       const int ty = p.result_type;
       if (p.n_insns == 1 && p.insns[0].op == PXG_OP_COL) {
         const ChunkCol& sc = ch.cols[p.insns[0].arg];
         if (ty == PXG_STRING) {
-          int32_t o0 = 0, o1 = 0;
-          PXG_HIP(hipMemcpy(&o0, sc.offsets.as<int32_t>() + lo, 4, hipMemcpyDeviceToHost));
-          PXG_HIP(hipMemcpy(&o1, sc.offsets.as<int32_t>() + hi, 4, hipMemcpyDeviceToHost));
+          uint32_t o0 = 0, o1 = 0;
+          PXG_RETURN_IF_ERROR(ReadU32(ctx, sc.offsets.as<int32_t>() + lo, &o0));
+          PXG_RETURN_IF_ERROR(ReadU32(ctx, sc.offsets.as<int32_t>() + hi, &o1));
           PXG_RETURN_IF_ERROR(dc.offsets.Alloc((n + 1) * 4 + 16));
           PXG_RETURN_IF_ERROR(dc.data.Alloc(static_cast<size_t>(o1 - o0) + 16));
           dc.data_len = o1 - o0;
@@ -235,15 +384,14 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
       }
       const int w = TypeWidth(ty);
       PXG_RETURN_IF_ERROR(dc.values.Alloc(n * w + 16));
-      PXG_RETURN_IF_ERROR(Launch(ctx, "map_eval", MapEvalKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0,
-                                 pbs[e].prog.as<const DevProgram>(), t.d_chunks.as<const DevChunk>(), static_cast<int>(c),
-                                 pbs[e].types.as<const int32_t>(), lo, n, dc.values.as<uint8_t>(), w));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "map_eval", MapEvalKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0, d_progs + e,
+                                 t.d_chunks.as<const DevChunk>(), static_cast<int>(c), d_types, lo, n, dc.values.as<uint8_t>(), w));
     }
-    PXG_HIP(hipStreamSynchronize(ctx->stream));
     o.nrows += n;
     o.chunks.push_back(std::move(oc));
     ++o.version;
   }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
   *out = guard.release();
   return PXG_OK;
 }

@@ -242,6 +242,11 @@ class Table:
             pass
 
 
+@dataclass
+class _KindOnly:
+    kind: int
+
+
 class Agg:
     """pxg_agg: blocking (or windowed) group-by aggregation with device UDAs."""
 
@@ -264,6 +269,16 @@ class Agg:
         h = C.c_void_p()
         check(self.lib.pxg_agg_create(ctx.h, C.byref(spec), C.byref(h)))
         self.h = h
+
+    @classmethod
+    def from_handle(cls, ctx: Ctx, handle, n_keys: int, uda_kinds) -> "Agg":
+        """Wrap a pxg_agg created elsewhere (e.g. the engine's lowering, pxc_plan_create_agg)."""
+        a = cls.__new__(cls)
+        a.ctx, a.lib, a.h = ctx, ctx.lib, handle
+        a.keys = [None] * n_keys
+        a.udas = [_KindOnly(k) for k in uda_kinds]
+        a.filt = None
+        return a
 
     def consume(self, table: Table, begin: int = 0, end: Optional[int] = None) -> None:
         end = table.num_rows if end is None else end

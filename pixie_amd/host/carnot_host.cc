@@ -813,8 +813,88 @@ static Status FetchAll(pxg_table* t, int32_t ncols, RowBatch* rb) {
   return Status::OK();
 }
 
+// Rows [r0, r0 + n) of a host column, sharing its buffers (Arrow Slice).
+static HostColumn SliceColumn(const HostColumn& c, int64_t r0, int64_t n) {
+  HostColumn h = c;
+  h.length = n;
+  if (c.type == PXG_STRING) {
+    h.offsets = c.offsets + r0;  // absolute offsets into the same payload
+  } else {
+    const int w = c.type == B ? 1 : c.type == U ? 16 : 8;
+    h.values = static_cast<const uint8_t*>(c.values) + r0 * w;
+  }
+  return h;
+}
+
+// Coalescing of the small RowBatches PEM sources produce (pem_manager.cc:85-99) in front of the
+// standalone device operators: batches are staged into one device table (pinned staging) and
+// run together at kCoalesceRows staged rows or at eow / eos; the output is cut back into one
+// batch per input batch with the input batch's eow / eos, exactly what the per-batch reference
+// nodes emit (filter_node.cc:167-168, map_node.cc:67-68).
+class CoalescingDeviceNode : public ExecNode {
+ protected:
+  static constexpr int64_t kCoalesceRows = 1 << 16;
+  struct Pending {
+    int64_t rows;
+    bool eow, eos;
+  };
+  // Runs the device operator over the staged rows; fills `out` and the rows of each input batch.
+  virtual Status RunStaged(ExecState* s, pxg_table* staged, int64_t n, const std::vector<int64_t>& in_rows, RowBatch* out,
+                           std::vector<int64_t>* out_rows) = 0;
+  Status OpenImpl(ExecState* s) override {
+    if (!s->ctx) return Status::OK();
+    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(inputs_[0].size()), inputs_[0].data(), &staged_));
+    return Status::OK();
+  }
+  Status CloseImpl(ExecState*) override {
+    if (staged_) pxg_table_destroy(staged_);
+    staged_ = nullptr;
+    return Status::OK();
+  }
+  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
+    if (rb.num_rows > 0) {
+      std::vector<pxg_column_view> v;
+      for (auto& c : rb.cols) v.push_back(c.View());
+      PXG_CALL(pxg_table_append(staged_, v.data(), rb.num_rows));
+    }
+    pending_.push_back({rb.num_rows, rb.eow, rb.eos});
+    staged_rows_ += rb.num_rows;
+    if (staged_rows_ < kCoalesceRows && !rb.eow && !rb.eos) return Status::OK();
+    return Flush(s);
+  }
+
+ private:
+  Status Flush(ExecState* s) {
+    PXG_CALL(pxg_table_flush(staged_));
+    std::vector<int64_t> in_rows, out_rows;
+    for (auto& p : pending_) in_rows.push_back(p.rows);
+    RowBatch all;
+    PXC_RETURN_IF_ERROR(RunStaged(s, staged_, staged_rows_, in_rows, &all, &out_rows));
+    std::vector<Pending> pend;
+    pend.swap(pending_);
+    staged_rows_ = 0;
+    pxg_table_destroy(staged_);
+    staged_ = nullptr;
+    PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(inputs_[0].size()), inputs_[0].data(), &staged_));
+    int64_t r0 = 0;
+    for (size_t i = 0; i < pend.size(); ++i) {
+      RowBatch ob;
+      ob.num_rows = out_rows[i];
+      for (auto& c : all.cols) ob.cols.push_back(SliceColumn(c, r0, out_rows[i]));
+      ob.eow = pend[i].eow;
+      ob.eos = pend[i].eos;
+      r0 += out_rows[i];
+      PXC_RETURN_IF_ERROR(SendRowBatchToChildren(s, ob));
+    }
+    return Status::OK();
+  }
+  pxg_table* staged_ = nullptr;
+  std::vector<Pending> pending_;
+  int64_t staged_rows_ = 0;
+};
+
 // GpuFilterNode (FilterNode, filter_node.cc:78-171): one output batch per input batch.
-class GpuFilterNode : public ExecNode {
+class GpuFilterNode : public CoalescingDeviceNode {
  public:
   std::string DebugString() const override { return "GpuFilterNode"; }
   Program pred;
@@ -830,26 +910,22 @@ class GpuFilterNode : public ExecNode {
       for (size_t c = 0; c < inputs_[0].size(); ++c) select.push_back(static_cast<int32_t>(c));
     return Status::OK();
   }
-  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
-    pxg_table* in = nullptr;
-    PXC_RETURN_IF_ERROR(UploadBatch(s->ctx, rb, inputs_[0], &in));
-    pxg_table* out = nullptr;
+  Status RunStaged(ExecState*, pxg_table* staged, int64_t n, const std::vector<int64_t>& in_rows, RowBatch* out,
+                   std::vector<int64_t>* out_rows) override {
+    pxg_table* res = nullptr;
     const pxg_program p = pred.View();
-    int32_t code = pxg_filter(in, &p, static_cast<int32_t>(select.size()), select.data(), 0, rb.num_rows, &out);
-    RowBatch ob;
+    out_rows->assign(in_rows.size(), 0);
+    int32_t code = pxg_filter_split(staged, &p, static_cast<int32_t>(select.size()), select.data(), 0, n,
+                                    static_cast<int32_t>(in_rows.size()), in_rows.data(), out_rows->data(), &res);
     Status st = FromPxg(code);
-    if (st.ok()) st = FetchAll(out, static_cast<int32_t>(select.size()), &ob);
-    if (out) pxg_table_destroy(out);
-    pxg_table_destroy(in);
-    PXC_RETURN_IF_ERROR(st);
-    ob.eow = rb.eow;
-    ob.eos = rb.eos;
-    return SendRowBatchToChildren(s, ob);
+    if (st.ok()) st = FetchAll(res, static_cast<int32_t>(select.size()), out);
+    if (res) pxg_table_destroy(res);
+    return st;
   }
 };
 
 // GpuMapNode (MapNode, map_node.cc:47-71): one output column per expression.
-class GpuMapNode : public ExecNode {
+class GpuMapNode : public CoalescingDeviceNode {
  public:
   std::string DebugString() const override { return "GpuMapNode"; }
   std::vector<Program> exprs;
@@ -863,22 +939,17 @@ class GpuMapNode : public ExecNode {
     }
     return Status::OK();
   }
-  Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
-    pxg_table* in = nullptr;
-    PXC_RETURN_IF_ERROR(UploadBatch(s->ctx, rb, inputs_[0], &in));
+  Status RunStaged(ExecState*, pxg_table* staged, int64_t n, const std::vector<int64_t>& in_rows, RowBatch* out,
+                   std::vector<int64_t>* out_rows) override {
     std::vector<pxg_program> pv;
     for (auto& e : exprs) pv.push_back(e.View());
-    pxg_table* out = nullptr;
-    int32_t code = pxg_map(in, static_cast<int32_t>(pv.size()), pv.data(), 0, rb.num_rows, &out);
-    RowBatch ob;
+    pxg_table* res = nullptr;
+    int32_t code = pxg_map(staged, static_cast<int32_t>(pv.size()), pv.data(), 0, n, &res);
     Status st = FromPxg(code);
-    if (st.ok()) st = FetchAll(out, static_cast<int32_t>(pv.size()), &ob);
-    if (out) pxg_table_destroy(out);
-    pxg_table_destroy(in);
-    PXC_RETURN_IF_ERROR(st);
-    ob.eow = rb.eow;
-    ob.eos = rb.eos;
-    return SendRowBatchToChildren(s, ob);
+    if (st.ok()) st = FetchAll(res, static_cast<int32_t>(pv.size()), out);
+    if (res) pxg_table_destroy(res);
+    *out_rows = in_rows;
+    return st;
   }
 };
 
@@ -1175,6 +1246,15 @@ class GpuAggNode : public ExecNode {
  public:
   // Raw 7-double quantile columns of the last emitted batch (post-agg pluck reads them).
   std::map<size_t, HostColumn> quantiles_raw_;
+
+  // The device aggregation this node would run, handed to the caller (pxc_plan_create_agg).
+  Status CreateDeviceAgg(pxg_ctx* ctx, int64_t expected_groups, pxg_agg** out) {
+    expected_groups_ = expected_groups;
+    PXC_RETURN_IF_ERROR(CreateAgg(ctx));
+    *out = agg_;
+    agg_ = nullptr;
+    return Status::OK();
+  }
 
  private:
   Status CreateAgg(pxg_ctx* ctx) {
@@ -2084,6 +2164,13 @@ class ExecutionGraph {
     return os.str();
   }
 
+  // The first aggregation node of the lowered graph (fused or not), or null.
+  GpuAggNode* FirstAgg() const {
+    for (auto* n : lowered_)
+      if (auto* a = dynamic_cast<GpuAggNode*>(n)) return a;
+    return nullptr;
+  }
+
   std::vector<SinkNode*> sinks_;
   std::vector<GrpcSinkNode*> grpc_sinks_;
   // GRPCSource node id -> its RowBatchData messages in arrival order (set before Init).
@@ -2593,6 +2680,34 @@ extern "C" int32_t pxc_execute_plan_grpc(pxc_engine* engine, const uint8_t* plan
     for (int32_t m = 0; m < inputs[i].nmessages; ++m) v.push_back({inputs[i].messages[m], inputs[i].lengths[m]});
   }
   return ExecuteImpl(engine, plan, plan_len, ntables, tables, &in, out, out_len, grpc_out, grpc_out_len);
+}
+
+// The drop-in lowering of a plan's (fused) aggregation as a pxg_agg over a device table of the
+// given column types: the same ExecutionGraph lowering pxc_execute_plan runs (the MemorySource
+// is treated as a stored device table, so programs reference the table's own columns).  Lets a
+// caller drive pxg_agg_consume / pxg_agg_finalize on an HBM-resident table directly.
+extern "C" int32_t pxc_plan_create_agg(pxg_ctx* ctx, const uint8_t* plan, int64_t plan_len, const char* table_name,
+                                       int32_t ncols, const int32_t* types, int64_t expected_groups, pxg_agg** out,
+                                       int32_t* n_keys, int32_t* n_udas, int32_t* uda_kinds) {
+  if (!ctx || !table_name || ncols <= 0 || !types || !out || !n_keys || !n_udas || !uda_kinds)
+    return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  TableStore store;
+  StoredTable st;
+  st.types.assign(types, types + ncols);
+  st.names.assign(static_cast<size_t>(ncols), "");
+  store.emplace(table_name, std::move(st));
+  ExecutionGraph g;
+  Status s = Lower(plan, plan_len, 0, nullptr, &store, &g);
+  if (!s.ok()) return Fail(s);
+  GpuAggNode* a = g.FirstAgg();
+  if (!a) return Fail(Err(PXG_INVALID_ARGUMENT, "plan has no aggregate"));
+  if (a->udas.size() > 16) return Fail(Err(PXG_UNIMPLEMENTED, "more than 16 UDAs"));
+  s = a->CreateDeviceAgg(ctx, expected_groups, out);
+  if (!s.ok()) return Fail(s);
+  *n_keys = static_cast<int32_t>(a->keys.size());
+  *n_udas = static_cast<int32_t>(a->udas.size());
+  for (size_t u = 0; u < a->udas.size(); ++u) uda_kinds[u] = a->udas[u].kind;
+  return PXG_OK;
 }
 
 extern "C" int32_t pxc_rowbatch_to_proto(int32_t ncols, const pxg_column_view* cols, int64_t nrows, int32_t eow, int32_t eos,

@@ -66,6 +66,8 @@ def load() -> C.CDLL:
     lib.pxc_rowbatch_to_proto.restype = i32
     lib.pxc_rowbatch_from_proto.argtypes = [C.c_char_p, i64, p(vp), p(i64)]
     lib.pxc_rowbatch_from_proto.restype = i32
+    lib.pxc_plan_create_agg.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i32, p(i32), i64, p(vp), p(i32), p(i32), p(i32)]
+    lib.pxc_plan_create_agg.restype = i32
     lib.pxc_quantiles_json.argtypes = [p(C.c_double), i64, p(vp), p(i64)]
     lib.pxc_quantiles_json.restype = i32
     lib.pxc_free.argtypes = [vp]
@@ -282,3 +284,18 @@ class Engine:
         if self.h:
             self.lib.pxc_engine_destroy(self.h)
             self.h = C.c_void_p()
+
+
+def plan_agg(ctx, plan, table_name: str, types, expected_groups: int = 0):
+    """The engine's lowering of the plan's aggregation (pxc_plan_create_agg) as a
+    pixie_amd.device.Agg over a device table with the given column types."""
+    from .device import Agg
+    lib = load()
+    pb = plan.SerializeToString()
+    arr = (C.c_int32 * len(types))(*types)
+    h = C.c_void_p()
+    nk, nu = C.c_int32(), C.c_int32()
+    kinds = (C.c_int32 * 16)()
+    _check(lib.pxc_plan_create_agg(ctx.h, pb, len(pb), table_name.encode(), len(types), arr, expected_groups, C.byref(h),
+                                   C.byref(nk), C.byref(nu), kinds))
+    return Agg.from_handle(ctx, h, nk.value, [kinds[i] for i in range(nu.value)])
