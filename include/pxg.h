@@ -312,6 +312,10 @@ int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* stats);
 int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* dst, int64_t dst_capacity,
                                int64_t* part_offsets, int64_t* part_bytes);
 int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes);
+/* Import n_parts exported parts that lie in one device buffer (part i at src + part_offsets[i],
+ * part_bytes[i] bytes: e.g. what one all-to-all received from every rank) in one pass. */
+int32_t pxg_agg_import_partials(pxg_agg* agg, const void* src, int32_t n_parts,
+                                const int64_t* part_offsets, const int64_t* part_bytes);
 
 /* ---------------------------------------------------------------------------------------
  * Equijoin (EquijoinNode, src/carnot/exec/equijoin_node.cc:53-470).  A hash table is built on

@@ -780,8 +780,11 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   std::memcpy(c, pin + 8, 32);
   std::memcpy(n_deferred, c + 8, 4);
   std::memcpy(&st_n, c + 16, 8);
+
   const uint64_t n_new = tot >> kPublishCountShift;
   const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
+  uint32_t dev_groups = 0;  // exact: every successful insert CAS is counted (per-tile flushes)
+  std::memcpy(&dev_groups, c, 4);
   if (n_new > 0) {
     // Slot words hold 32-bit arena offsets: refuse before any record is written.
     if (arena_words + words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
@@ -791,7 +794,8 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
                                static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>()));
     arena_words += words;
   }
-  inserted += n_new;
+  // The device insert counter is exact (every successful insert CAS is counted).
+  inserted = std::max<uint64_t>(inserted + n_new, dev_groups);
   // The device-side fill count restarts from the exact number of groups.
   PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
   return PXG_OK;
@@ -807,8 +811,10 @@ static int32_t CheckTableTypes(const Agg& a, const Table& t) {
 }
 
 int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
+  HostClock clk;
   PXG_RETURN_IF_ERROR(CheckTableTypes(*this, *t));
   PXG_RETURN_IF_ERROR(t->EnsureDeviceDescriptors());
+  clk.Mark("consume: descriptors");
   if (t->chunks.size() > 255) return SetError(PXG_UNIMPLEMENTED, "tables are limited to 255 chunks per agg consume");
   const int64_t tile_rows = fast_nk > 0 ? kConsumeTile : kGenericTile;
   std::vector<TileRange> ranges;
@@ -834,6 +840,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
   PXG_RETURN_IF_ERROR(deferred[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
   PXG_RETURN_IF_ERROR(deferred_pos[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
+  clk.Mark("consume: staging ensure");
   // The tile ranges of a repeated consume (same table, same rows) are already on the device.
   const size_t rbytes = ranges.size() * sizeof(TileRange);
   if (rbytes != last_ranges.size() || std::memcmp(last_ranges.data(), ranges.data(), rbytes) != 0) {
@@ -866,8 +873,10 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
                              d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
                              static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this),
                              static_cast<uint32_t>(t->chunks.size())));
+  clk.Mark("consume: launch");
   uint32_t n_def = 0;
   PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
+  clk.Mark("consume: kernel + publish");
   int buf = 0;
   for (int round = 0; n_def > 0; ++round) {
     // Rows are deferred by a full table / overlong probe, or (fast path) by a long string key.

@@ -91,12 +91,14 @@ struct Agg {
   int32_t EnsureStage(uint64_t need);
   int32_t Grow(uint32_t new_cap);
   int32_t PublishNew(Table* t, uint32_t* n_deferred);
+
   int32_t ConsumeRange(Table* t, int64_t begin, int64_t end);
   int32_t ConsumeList(Table* t, const uint32_t* list, uint32_t n);
   int32_t Finalize();
   int32_t PrepareExport(int32_t n_parts);
   int32_t ExportPartial(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
   int32_t ImportPartial(const void* src, int64_t nbytes);
+  int32_t ImportPartials(const void* src, int32_t n, const int64_t* offs, const int64_t* sizes);
 };
 
 // Finalize stages (pxg_finalize.hip).

@@ -1132,6 +1132,7 @@ struct SideJoinGuard {
 int32_t AggFinalizeImpl(Agg* a) {
   Ctx* ctx = a->ctx;
   SideJoinGuard guard{ctx};
+  HostClock clk;
   AggResult& R = a->res;
   Agg::FinalizeWs& ws = a->ws;
   R.Clear();
@@ -1363,7 +1364,9 @@ int32_t AggFinalizeImpl(Agg* a) {
                                  lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart, vals, at, qo));
     }
     uint32_t hm[6];
+    clk.Mark("finalize: issue to meta");
     PXG_HIP(hipEventSynchronize(ctx->ev_meta));
+    clk.Mark("finalize: meta wait");
     std::memcpy(hm, pin + 64, 24);
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3], n_bchunks = hm[4];
@@ -1433,7 +1436,9 @@ int32_t AggFinalizeImpl(Agg* a) {
   uint32_t g_dev = 0;
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 1, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  clk.Mark("finalize: issue rest");
   PXG_HIP(hipStreamSynchronize(ctx->stream));
+  clk.Mark("finalize: final wait");
   for (int k = 0; k < a->n_keys; ++k)
     if (a->key_types[k] == PXG_STRING) totals[k] = pin32[k];
   err = pin32[kMaxKeys];

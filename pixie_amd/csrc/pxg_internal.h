@@ -3,7 +3,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -139,6 +142,21 @@ struct Ctx {
 
   hipEvent_t GetEvent();
   int32_t ResolveTimings();
+};
+
+// Opt-in host-side stage timing of the library (PXG_TIMING=1): one stderr line per stage.
+struct HostClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  static bool On() {
+    static const bool on = std::getenv("PXG_TIMING") != nullptr;
+    return on;
+  }
+  void Mark(const char* what) {
+    if (!On()) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[pxg] %-28s %9.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
 };
 
 // Launch helper: optional event bracketing on the launch stream (stats resolved lazily).

@@ -428,65 +428,100 @@ int32_t Agg::ExportPartial(int32_t n_parts, void* dst, int64_t dst_capacity, int
   return PXG_OK;
 }
 
-int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
-  if (nbytes < static_cast<int64_t>(sizeof(PartHeader))) return SetError(PXG_INVALID_ARGUMENT, "partial buffer of %lld bytes has no header", (long long)nbytes);
-  PartHeader H;
-  PXG_HIP(hipMemcpyAsync(&H, src, sizeof(H), hipMemcpyDeviceToHost, ctx->stream));
+// Merge n exported parts (part i at src + offs[i], sizes[i] bytes) in one pass: every header is
+// read back with one synchronisation, the arena / table / staging are sized once for all of
+// them, each part's keys and rows are imported by its own kernels, and one final readback
+// collects the insert count and error flags -- two host round trips for any number of parts.
+int32_t Agg::ImportPartials(const void* src, int32_t n, const int64_t* offs, const int64_t* sizes) {
+  if (n <= 0) return PXG_OK;
+  std::vector<PartHeader> H(static_cast<size_t>(n));
+  const uint8_t* base8 = static_cast<const uint8_t*>(src);
+  for (int i = 0; i < n; ++i) {
+    if (sizes[i] < static_cast<int64_t>(sizeof(PartHeader)))
+      return SetError(PXG_INVALID_ARGUMENT, "partial buffer of %lld bytes has no header", (long long)sizes[i]);
+    PXG_HIP(hipMemcpyAsync(&H[i], base8 + offs[i], sizeof(PartHeader), hipMemcpyDeviceToHost, ctx->stream));
+  }
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  if (H.magic != kPartMagic || H.version != kPartVersion) return SetError(PXG_INVALID_ARGUMENT, "not a pxg partial-agg buffer (magic %08x version %u)", H.magic, H.version);
-  if (H.plan_sig != PlanSig(*this) || H.n_keys != static_cast<uint32_t>(n_keys) || H.n_vals != static_cast<uint32_t>(n_vals))
-    return SetError(PXG_INVALID_ARGUMENT, "partial buffer was exported by an aggregation with different key/value types");
-  const PartLayout L = LayoutOf(H.n_groups, H.n_rows, H.key_words, n_vals);
-  if (static_cast<uint64_t>(nbytes) < L.bytes) return SetError(PXG_INVALID_ARGUMENT, "partial buffer truncated: %lld of %llu bytes", (long long)nbytes, (unsigned long long)L.bytes);
+  uint64_t tot_groups = 0, tot_rows = 0, tot_words = 0;
+  std::vector<PartLayout> L(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) {
+    const PartHeader& h = H[i];
+    if (h.magic != kPartMagic || h.version != kPartVersion)
+      return SetError(PXG_INVALID_ARGUMENT, "not a pxg partial-agg buffer (magic %08x version %u)", h.magic, h.version);
+    if (h.plan_sig != PlanSig(*this) || h.n_keys != static_cast<uint32_t>(n_keys) || h.n_vals != static_cast<uint32_t>(n_vals))
+      return SetError(PXG_INVALID_ARGUMENT, "partial buffer was exported by an aggregation with different key/value types");
+    L[i] = LayoutOf(h.n_groups, h.n_rows, h.key_words, n_vals);
+    if (static_cast<uint64_t>(sizes[i]) < L[i].bytes)
+      return SetError(PXG_INVALID_ARGUMENT, "partial buffer truncated: %lld of %llu bytes", (long long)sizes[i], (unsigned long long)L[i].bytes);
+    if (h.n_groups == 0 && h.n_rows != 0) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has rows but no groups");
+    tot_groups += h.n_groups;
+    tot_rows += h.n_rows;
+    tot_words += h.key_words;
+  }
   state_version++;
   res.ready = false;
-  if (H.n_groups == 0) {
-    if (H.n_rows != 0) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has rows but no groups");
-    return PXG_OK;
-  }
-  const uint8_t* p = static_cast<const uint8_t*>(src);
-  // Keys -> arena, then find-or-insert.  Size the table for <= 25% fill after the import.
-  const uint64_t base = arena_words;
-  if (base + H.key_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
-  PXG_RETURN_IF_ERROR(arena.Reserve((base + H.key_words) * 8 + kArenaSlack, base * 8, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(arena.as<uint64_t>() + base, p + L.keys, H.key_words * 8, hipMemcpyDeviceToDevice, ctx->stream));
-  arena_words += H.key_words;
-  uint64_t want = 4 * (inserted + H.n_groups);
+  if (tot_groups == 0) return PXG_OK;
+  // Keys -> arena (all parts back to back), then find-or-insert.  The table is sized for <= 25%
+  // fill after the import.
+  const uint64_t abase = arena_words;
+  if (abase + tot_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  PXG_RETURN_IF_ERROR(arena.Reserve((abase + tot_words) * 8 + kArenaSlack, abase * 8, ctx->stream));
+  uint64_t want = 4 * (inserted + tot_groups);
   if (want > cap) {
     uint64_t c = cap;
     while (c < want) c <<= 1;
     if (c > (uint64_t(1) << 31)) return SetError(PXG_RESOURCE_UNAVAILABLE, "group table would exceed 2^31 slots");
     PXG_RETURN_IF_ERROR(Grow(static_cast<uint32_t>(c)));
   }
-  PXG_RETURN_IF_ERROR(xc.remap.Ensure(H.n_groups * 4 + 16));
+  PXG_RETURN_IF_ERROR(xc.remap.Ensure(tot_groups * 4 + 16));
+  if (tot_rows > 0) PXG_RETURN_IF_ERROR(EnsureStage(st_n + tot_rows));
   uint8_t* meta = counters.as<uint8_t>();
   unsigned int* d_ins = reinterpret_cast<unsigned int*>(meta + 32);
   unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 36);
   PXG_HIP(hipMemsetAsync(meta + 32, 0, 8, ctx->stream));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "import_keys", ImportKeysKernel, dim3(GridFor(static_cast<int64_t>(H.n_groups), 256, 1 << 30)), dim3(256), 0,
-                             d_plan.as<const AggPlanDev>(), slots.as<unsigned long long>(), cap - 1, arena.as<const uint64_t>(), base,
-                             reinterpret_cast<const uint64_t*>(p + L.koff), H.n_groups, xc.remap.as<uint32_t>(), d_ins, d_err));
-  if (H.n_rows > 0) {
-    PXG_RETURN_IF_ERROR(EnsureStage(st_n + H.n_rows));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", ImportRowsKernel, dim3(GridFor(static_cast<int64_t>(H.n_rows), 256, 1 << 30)), dim3(256), 0,
-                               reinterpret_cast<const uint32_t*>(p + L.gid), H.n_rows, H.n_groups, xc.remap.as<const uint32_t>(),
-                               st_slot.as<uint32_t>() + st_n, d_err));
-    for (int v = 0; v < n_vals; ++v)
-      PXG_HIP(hipMemcpyAsync(st_val[v].as<uint64_t>() + st_n, p + L.vals + static_cast<uint64_t>(v) * H.n_rows * 8, H.n_rows * 8,
-                             hipMemcpyDeviceToDevice, ctx->stream));
+  uint64_t kw = abase, g0 = 0, r0 = st_n;
+  for (int i = 0; i < n; ++i) {
+    const PartHeader& h = H[i];
+    const uint8_t* p = base8 + offs[i];
+    if (h.n_groups == 0) continue;
+    uint32_t* remap = xc.remap.as<uint32_t>() + g0;
+    PXG_HIP(hipMemcpyAsync(arena.as<uint64_t>() + kw, p + L[i].keys, h.key_words * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "import_keys", ImportKeysKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)), dim3(256), 0,
+                               d_plan.as<const AggPlanDev>(), slots.as<unsigned long long>(), cap - 1, arena.as<const uint64_t>(), kw,
+                               reinterpret_cast<const uint64_t*>(p + L[i].koff), h.n_groups, remap, d_ins, d_err));
+    if (h.n_rows > 0) {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", ImportRowsKernel, dim3(GridFor(static_cast<int64_t>(h.n_rows), 256, 1 << 30)), dim3(256), 0,
+                                 reinterpret_cast<const uint32_t*>(p + L[i].gid), h.n_rows, h.n_groups,
+                                 static_cast<const uint32_t*>(remap), st_slot.as<uint32_t>() + r0, d_err));
+      for (int v = 0; v < n_vals; ++v)
+        PXG_HIP(hipMemcpyAsync(st_val[v].as<uint64_t>() + r0, p + L[i].vals + static_cast<uint64_t>(v) * h.n_rows * 8, h.n_rows * 8,
+                               hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    kw += h.key_words;
+    g0 += h.n_groups;
+    r0 += h.n_rows;
   }
-  uint32_t r[2];
-  PXG_HIP(hipMemcpyAsync(r, meta + 32, 8, hipMemcpyDeviceToHost, ctx->stream));
+  arena_words = kw;
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 240);
+  PXG_HIP(hipMemcpyAsync(pin, meta + 32, 8, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  if (r[1] & 1u) return SetError(PXG_INTERNAL, "group table full during partial import");
-  if (r[1] & 2u) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has a row whose group index is out of range");
-  inserted += r[0];
-  st_n += H.n_rows;
-  // Keep the device fill counter exact (the consume kernel's soft fill guard reads it).
+  const uint32_t r_ins = pin[0], r_err = pin[1];
+  if (r_err & 1u) return SetError(PXG_INTERNAL, "group table full during partial import");
+  if (r_err & 2u) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has a row whose group index is out of range");
+  inserted += r_ins;
+  st_n += tot_rows;
+  // Keep the device fill counter and staging cursor exact (the consume kernel reads both).
+  uint64_t* pin64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(ctx->pinned) + 248);
+  *pin64 = st_n;
   PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(counters.as<uint8_t>() + 16, &st_n, 8, hipMemcpyHostToDevice, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(counters.as<uint8_t>() + 16, pin64, 8, hipMemcpyHostToDevice, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   return PXG_OK;
+}
+
+int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
+  const int64_t off = 0;
+  return ImportPartials(src, 1, &off, &nbytes);
 }
 
 }  // namespace pxg
@@ -503,4 +538,11 @@ extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* d
 extern "C" int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes) {
   if (!agg || !src) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   return agg->impl.ImportPartial(src, nbytes);
+}
+
+extern "C" int32_t pxg_agg_import_partials(pxg_agg* agg, const void* src, int32_t n_parts, const int64_t* part_offsets,
+                                           const int64_t* part_bytes) {
+  if (!agg || (n_parts > 0 && (!src || !part_offsets || !part_bytes)) || n_parts < 0)
+    return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  return agg->impl.ImportPartials(src, n_parts, part_offsets, part_bytes);
 }

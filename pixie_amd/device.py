@@ -329,6 +329,13 @@ class Agg:
         check(self.lib.pxg_agg_info(self.h, C.byref(st)))
         return {f: int(getattr(st, f)) for f, _ in st._fields_ if f != "reserved"}
 
+    def import_partials(self, buf, offsets, sizes) -> None:
+        """Merge several exported parts lying in one uint8 device tensor (pxg_agg_import_partials)."""
+        n = len(offsets)
+        o = (C.c_int64 * max(n, 1))(*offsets)
+        z = (C.c_int64 * max(n, 1))(*sizes)
+        check(self.lib.pxg_agg_import_partials(self.h, C.c_void_p(buf.data_ptr()), n, o, z))
+
     def rows_selected(self) -> int:
         n = C.c_int64()
         check(self.lib.pxg_agg_rows_selected(self.h, C.byref(n)))

@@ -56,13 +56,20 @@ def exchange_partials(agg, group: Optional[dist.ProcessGroup] = None) -> Tuple[i
     if recv.device != agg_dev:
         recv = recv.to(agg_dev)
     # Every group this rank exported now lives on its owner; rebuild from the received parts
-    # (our own part included: it travelled rank -> rank through the same buffer).
+    # (our own part included: it travelled rank -> rank through the same buffer), all of them in
+    # one import call.
     agg.reset()
-    at = 0
+    offs, sizes, at = [], [], 0
     for src in range(world):
         if rs[src] > 0:
-            agg.import_partial(recv[at:at + rs[src]])
+            offs.append(at)
+            sizes.append(rs[src])
         at += rs[src]
+    if hasattr(agg, "import_partials"):
+        agg.import_partials(recv, offs, sizes)
+    else:
+        for o, z in zip(offs, sizes):
+            agg.import_partial(recv[o:o + z])
     return total, sum(rs)
 
 

@@ -846,10 +846,14 @@ class CoalescingDeviceNode : public ExecNode {
     PXG_CALL(pxg_table_create(s->ctx, static_cast<int32_t>(inputs_[0].size()), inputs_[0].data(), &staged_));
     return Status::OK();
   }
-  Status CloseImpl(ExecState*) override {
+  Status CloseImpl(ExecState* s) override {
+    // Batches a source sent after its eos (ExecNodeTester does) or before a stop are still
+    // owed their output batches; children close after this node (topological order).
+    Status st;
+    if (staged_ && !pending_.empty()) st = Flush(s);
     if (staged_) pxg_table_destroy(staged_);
     staged_ = nullptr;
-    return Status::OK();
+    return st;
   }
   Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
     if (rb.num_rows > 0) {

@@ -125,3 +125,50 @@ def test_import_rejects_foreign_and_truncated_buffers(ctx):
     for x in (a, other):
         x.close()
     t.close()
+
+
+def test_batched_import_equals_part_by_part(ctx):
+    """pxg_agg_import_partials (every received part in one buffer, one pass) must give exactly
+    what importing the parts one by one gives."""
+    import torch
+    cols = datagen_http_events(99, 0, 300_000, threads=8)
+    plan = P.c2_plan(with_pluck=False)
+    q = LinearQuery(plan, P.HTTP_TYPES)
+    bounds = [0, 80_000, 190_000, 300_000]
+    shards, tabs = [], []
+    for s in range(3):
+        t = Table(ctx, P.HTTP_TYPES)
+        t.append([c.slice(bounds[s], bounds[s + 1]) for c in cols])
+        a = q.make_agg(ctx)
+        a.consume(t)
+        shards.append(a)
+        tabs.append(t)
+    parts = []
+    for a in shards:
+        offs, nb = a.export_partial(2)
+        buf = torch.empty(max(sum(segments(offs, nb)), 8), dtype=torch.uint8, device="cuda")
+        a.export_partial(2, buf)
+        parts.append((buf, offs, nb))
+    for p in range(2):
+        one = q.make_agg(ctx)
+        for buf, offs, nb in parts:
+            one.import_partial(buf[offs[p]:offs[p] + nb[p]])
+        one.finalize()
+        A = _by_key(q.emit(one.result()), 2)
+        segs = [buf[offs[p]:offs[p] + nb[p]] for buf, offs, nb in parts]
+        pad = [(len(x) + 7) // 8 * 8 for x in segs]
+        cat = torch.zeros(sum(pad), dtype=torch.uint8, device="cuda")
+        at, o = 0, []
+        for x, w in zip(segs, pad):
+            cat[at:at + len(x)] = x
+            o.append(at)
+            at += w
+        batched = q.make_agg(ctx)
+        batched.import_partials(cat, o, [len(x) for x in segs])
+        batched.finalize()
+        B = _by_key(q.emit(batched.result()), 2)
+        assert A == B
+        one.close()
+        batched.close()
+    for x in shards + tabs:
+        x.close()

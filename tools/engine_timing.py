@@ -21,8 +21,17 @@ else:
     Table(ctx, P.HTTP_TYPES, handle=e.device_table("http_events"), owned=False).append_http_events(20250117, 0, n)
 print("rows", e.num_rows("http_events"), flush=True)
 pb = P.c2_plan(with_pluck=True).SerializeToString()
-for i in range(4):
+ctx = Ctx(0, handle=e.ctx_handle())
+names = ["agg_consume", "agg_consume_list", "agg_rehash", "stage_remap", "agg_publish_sizes", "agg_publish_write",
+         "radix_scatter", "quant_big_merge", "digest_chain"]
+for i in range(5):
+    ctx.reset_stats()
+    ctx.set_profiling(True)
     t = time.perf_counter()
     r = e.execute_raw(pb)
-    print(f"query {i}: {1000 * (time.perf_counter() - t):.2f} ms, {len(r)} bytes", file=sys.stderr, flush=True)
+    ms = 1000 * (time.perf_counter() - t)
+    ctx.set_profiling(False)
+    ks = {k: ctx.kernel_stats(k) for k in names}
+    ks = {k: (v[0], round(v[1], 3)) for k, v in ks.items() if v[0]}
+    print(f"query {i}: {ms:.2f} ms, {len(r)} bytes, kernels {ks}", file=sys.stderr, flush=True)
 e.close()
