@@ -363,6 +363,15 @@ int32_t pxg_datagen_http_events(uint64_t seed, int64_t row_begin, int64_t nrows,
 int32_t pxg_table_append_http_events(pxg_table* t, uint64_t seed, int64_t row_begin, int64_t nrows,
                                      int64_t n_addr_keys);
 
+/* ---------------------------------------------------------------------------------------
+ * Diagnostics (tests).  Centroid-boundary chains of the quantiles t-digest emulation for n
+ * group sizes d_w (device int64), computed by the per-wave speculative chain (wave = 1) or the
+ * single-lane sequential chain (wave = 0); boundaries to d_starts[i * cap ...], counts to
+ * d_nc[i] (-1: more than cap).  Synchronises.
+ * ------------------------------------------------------------------------------------- */
+int32_t pxg_digest_chains(pxg_ctx* ctx, const int64_t* d_w, int32_t n, int32_t wave, uint32_t* d_starts,
+                          int32_t cap, int32_t* d_nc);
+
 #ifdef __cplusplus
 }
 #endif

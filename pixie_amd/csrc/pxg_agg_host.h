@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "pxg_agg.h"
+#include "pxg_sort.h"
 
 namespace pxg {
 
@@ -85,6 +86,9 @@ struct Agg {
     DevBuf hist, scan, scan2, cgroup, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
     DevBuf keysA, keysB, bstarts, big, bchunks;
     DevBuf chain_list, chain_nc, chain_starts;
+    // big groups by selection (pxg_finalize.hip)
+    DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial;
+    RadixPassWs rs;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);

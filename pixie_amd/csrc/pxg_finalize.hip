@@ -32,38 +32,6 @@ __device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restr
   return k < cap ? rank[k] : G;
 }
 
-__global__ void __launch_bounds__(kRadixBlock) RadixHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
-                                                               const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G,
-                                                               int shift, uint32_t* __restrict__ hist, uint32_t nblocks) {
-  __shared__ uint32_t h[4][kRadixBuckets];
-  uint32_t* hf = &h[0][0];
-  for (int i = threadIdx.x; i < 4 * kRadixBuckets; i += kRadixBlock) hf[i] = 0;
-  __syncthreads();
-  const int wid = threadIdx.x >> 6;
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
-  // Every key load first, then every rank gather, then the counts: the tile's loads are all
-  // in flight together.
-  uint32_t kk[kRadixItems];
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
-    kk[k] = i < n ? keys[i] : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
-    kk[k] = i < n ? DenseKey(kk[k], rank, cap, G) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
-    if (i < n) atomicAdd(&h[wid][(kk[k] >> shift) & (kRadixBuckets - 1)], 1u);
-  }
-  __syncthreads();
-  const int d = threadIdx.x;
-  hist[static_cast<uint64_t>(d) * nblocks + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
-}
-
 // Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
 __device__ __forceinline__ void WaveSync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -71,41 +39,155 @@ __device__ __forceinline__ void WaveSync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Stable scatter.  Wave w of a block owns the contiguous quarter [w * 1024, (w + 1) * 1024) of
-// the block's 4096-item tile, in (k, lane) order, so a wave's running per-digit counts live in
-// its own LDS slice and need no block barrier inside the item loop: ranks within a wave come
-// from an 8-ballot match of the digit bits.  The tile is then reordered by digit in LDS and
-// written out in digit runs (consecutive threads -> consecutive addresses), instead of one
-// scattered 4- or 8-byte store per item.
-__global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
-                                                                  ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n,
-                                                                  const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G,
-                                                                  int shift, const uint32_t* __restrict__ offs, uint32_t nblocks) {
+// ---------------------------------------------------------------------------------------
+// Stable LSD radix sort, 8-bit digits, four kernels per pass: tile digit counts (RsHist),
+// digit totals (RsTotal), tile offsets (RsScan: one workgroup per digit scans that digit's
+// tile counts and adds the digit's base), and the scatter (RsScatter).  No tile ever waits on another: a decoupled look-back (one-sweep) was
+// measured slower here, its inclusive prefixes advancing only a few tiles per device-scope
+// round trip while ~1000 tiles start at once.
+// ---------------------------------------------------------------------------------------
+
+// Wave-aggregated LDS histogram add: lanes holding the same digit are matched with 8 ballots
+// and only the lowest of them adds the group's count, so skewed data (hot groups) does not
+// serialise on one LDS address.
+__device__ __forceinline__ void WaveHistAdd(uint32_t* h, uint32_t d, bool valid) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long peers = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < kRadixBits; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const unsigned long long m = __ballot(valid && bit);
+    peers &= bit ? m : ~m;
+  }
+  if (valid && (peers & ((1ULL << lane) - 1)) == 0) atomicAdd(&h[d], static_cast<uint32_t>(__popcll(peers)));
+}
+
+// Tile digit counts of one pass -> hist[d * ntiles + tile].  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
+// them instead of gathering again.
+__global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                            const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G, int shift,
+                                                            uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ dense_out) {
+  __shared__ uint32_t h[kRadixBuckets];
+  h[threadIdx.x] = 0;  // kRadixBlock == kRadixBuckets
+  __syncthreads();
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  uint32_t kk[kRadixItems];
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    kk[k] = i < n ? keys[i] : 0u;
+  }
+  if (rank) {
+#pragma unroll
+    for (int k = 0; k < kRadixItems; ++k) {
+      const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+      if (i < n) {
+        kk[k] = DenseKey(kk[k], rank, cap, G);
+        dense_out[i] = kk[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
+    WaveHistAdd(h, (kk[k] >> shift) & (kRadixBuckets - 1), i < n);
+  }
+  __syncthreads();
+  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Block d: digit d's total over all tiles (the digit bases come from these; per-tile atomics
+// into 256 global totals were a contention point).
+constexpr int kRsScanBlock = 256;
+__global__ void __launch_bounds__(kRsScanBlock) RsTotalKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                              uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s[kRsScanBlock];
+  const uint32_t* row = hist + static_cast<uint64_t>(blockIdx.x) * ntiles;
+  uint32_t tot = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += kRsScanBlock) tot += row[i];
+  s[threadIdx.x] = tot;
+  __syncthreads();
+  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ghist[blockIdx.x] = s[0];
+}
+
+// Block d: exclusive scan of digit d's tile counts, plus the digit's global base.
+__global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                             const uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s[kRsScanBlock];
+  const int t = threadIdx.x, d = blockIdx.x;
+  // the digit base: sum of the totals of digits < d
+  s[t] = t < d ? ghist[t] : 0u;
+  __syncthreads();
+  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
+    if (t < o) s[t] += s[t + o];
+    __syncthreads();
+  }
+  uint32_t carry = s[0];
+  __syncthreads();
+  uint32_t* row = hist + static_cast<uint64_t>(d) * ntiles;
+  const uint32_t per = (ntiles + kRsScanBlock - 1) / kRsScanBlock;  // contiguous run per thread
+  const uint32_t lo = min(ntiles, per * t), hi = min(ntiles, lo + per);
+  uint32_t tot = 0;
+  for (uint32_t i = lo; i < hi; ++i) tot += row[i];
+  s[t] = tot;
+  __syncthreads();
+  for (int o = 1; o < kRsScanBlock; o <<= 1) {
+    const uint32_t x = t >= o ? s[t - o] : 0u;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = carry + s[t] - tot;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = row[i];
+    row[i] = run;
+    run += c;
+  }
+}
+
+// One pass.  Wave w of a block owns the contiguous quarter [w * kPerWave, (w + 1) * kPerWave)
+// of the tile, in (k, lane) order, so a wave's running per-digit counts live in its own LDS
+// slice and need no block barrier inside the item loop: ranks within a wave come from an
+// 8-ballot match of the digit bits.  The tile is then reordered by digit in LDS and written
+// out in digit runs (consecutive threads -> consecutive addresses) instead of one scattered
+// store per item.  The first value stream is loaded up front so its latency overlaps the
+// ranking.
+__global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
+                                                               ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n, int shift,
+                                                               const uint32_t* __restrict__ offs, uint32_t ntiles) {
   constexpr int kWaves = kRadixBlock / 64;
   constexpr int kPerWave = kRadixTile / kWaves;
-  // 42 KB of LDS (3 blocks per CU): per-wave digit counts, turned in place into the tile-local
-  // start of each (wave, digit); one 8-byte-per-item staging buffer that carries the keys,
-  // then each value stream; the digit of every tile position.
   __shared__ uint32_t whist[kWaves][kRadixBuckets];
-  __shared__ uint32_t dstart[kRadixBuckets];         // tile-local start of each digit
-  __shared__ uint32_t gofs[kRadixBuckets];           // global start of this tile's digit run
+  __shared__ uint32_t dstart[kRadixBuckets];
+  __shared__ uint32_t gofs[kRadixBuckets];
   __shared__ uint64_t s_buf[kRadixTile];
   __shared__ uint8_t s_dig[kRadixTile];
   uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
+  gofs[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * ntiles + blockIdx.x];
   WaveSync();
   const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
   const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
   const int tn = static_cast<int>(min(static_cast<uint64_t>(kRadixTile), n - tile0));
   uint32_t part[kRadixItems], keys[kRadixItems], dig[kRadixItems];
+  uint64_t v0[kRadixItems];
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
+    keys[k] = i < n ? kin[i] : 0u;
+    v0[k] = (nvals > 0 && i < n) ? vin.p[0][i] : 0ULL;
+  }
 #pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
     const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
     const bool valid = i < n;
-    const uint32_t key = valid ? DenseKey(kin[i], rank, cap, G) : 0u;
-    const uint32_t d = (key >> shift) & (kRadixBuckets - 1);
+    const uint32_t d = (keys[k] >> shift) & (kRadixBuckets - 1);
     unsigned long long peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < kRadixBits; ++b) {
@@ -119,7 +201,6 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
     if (valid && r == 0) whist[wid][d] = pre + static_cast<uint32_t>(__popcll(peers));
     WaveSync();
     part[k] = pre + r;
-    keys[k] = key;
     dig[k] = d;
   }
   __syncthreads();
@@ -128,7 +209,6 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
     uint32_t tot = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) tot += whist[w][d];
-    // exclusive scan of the tile's digit totals (one digit per thread) through LDS
     dstart[d] = tot;
     __syncthreads();
     for (int o = 1; o < kRadixBuckets; o <<= 1) {
@@ -140,7 +220,6 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
     const uint32_t start = dstart[d] - tot;
     __syncthreads();
     dstart[d] = start;
-    gofs[d] = offs[static_cast<uint64_t>(d) * nblocks + blockIdx.x];
     uint32_t acc = start;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {  // in place: whist[w][d] becomes the start of (w, d)
@@ -160,18 +239,16 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
     }
   }
   __syncthreads();
-  // Keys out in digit runs.
   for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
     const uint32_t d = s_dig[j];
     kout[gofs[d] + (j - dstart[d])] = s_key[j];
   }
-  // Each value stream through the same LDS reordering (the staging buffer is reused).
   for (int v = 0; v < nvals; ++v) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kRadixItems; ++k) {
       const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-      if (i < n) s_buf[lpos[k]] = vin.p[v][i];
+      if (i < n) s_buf[lpos[k]] = v == 0 ? v0[k] : vin.p[v][i];
     }
     __syncthreads();
     for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
@@ -179,6 +256,45 @@ __global__ void __launch_bounds__(kRadixBlock) RadixScatterKernel(const uint32_t
       vout.p[v][gofs[d] + (j - dstart[d])] = s_buf[j];
     }
   }
+}
+
+// Sorts n records (dense key = DenseKey(keys[i]), values vin[0..nvals)) stably by dense key
+// into kbuf[0/1] / vbuf[0/1] (ping-pong); *skeys / *svals name the sorted streams.
+constexpr int kRsMaxPasses = 4;
+static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, ConstValPtrs vin,
+                                int nvals, uint64_t n, uint32_t* kbuf[2], ValPtrs vbuf[2], RadixPassWs& ws, const uint32_t** skeys,
+                                ConstValPtrs* svals) {
+  if (n == 0 || n >= (uint64_t(1) << 32)) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %llu records", static_cast<unsigned long long>(n));
+  int nbits = 1;
+  while ((uint64_t(1) << nbits) < static_cast<uint64_t>(G) + 1) ++nbits;
+  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
+  if (passes > kRsMaxPasses) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %u keys", G);
+  const uint32_t ntiles = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
+  PXG_RETURN_IF_ERROR(ws.hist.Ensure(static_cast<size_t>(ntiles) * kRadixBuckets * 4));
+  PXG_RETURN_IF_ERROR(ws.ghist.Ensure(static_cast<size_t>(kRsMaxPasses) * kRadixBuckets * 4));
+  uint32_t* ghist = ws.ghist.as<uint32_t>();
+  // With a rank map, the first histogram pass writes the dense keys into kbuf[1] (which the
+  // first scatter does not write) and the scatters read those.
+  const uint32_t* kin = keys;
+  for (int p = 0; p < passes; ++p) {
+    const int cur = p & 1;
+    const bool gather = p == 0 && rank != nullptr;
+    uint32_t* gh = ghist + p * kRadixBuckets;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RsHistKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, n, gather ? rank : nullptr, cap,
+                               G, p * kRadixBits, ws.hist.as<uint32_t>(), ntiles, gather ? kbuf[1] : nullptr));
+    if (gather) kin = kbuf[1];
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsTotalKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0,
+                               static_cast<const uint32_t*>(ws.hist.as<uint32_t>()), ntiles, gh));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsScanKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0, ws.hist.as<uint32_t>(), ntiles,
+                               static_cast<const uint32_t*>(gh)));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RsScatterKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, kbuf[cur], vin, vbuf[cur],
+                               nvals, n, p * kRadixBits, ws.hist.as<const uint32_t>(), ntiles));
+    kin = kbuf[cur];
+    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[cur].p[v];
+  }
+  *skeys = kin;
+  *svals = vin;
+  return PXG_OK;
 }
 
 // Dense group ids of the table's occupied slots, in slot order (rank = exclusive scan of the
@@ -509,63 +625,8 @@ __global__ void __launch_bounds__(256) QuantTinyKernel(const uint32_t* __restric
   if (lane < 7) out[static_cast<uint64_t>(g) * 7 + lane] = res;
 }
 
-
-// One wave per group with 64 < n <= 1024: bitonic sort in the wave's LDS slice, singleton
-// digest (W <= 1024 <= kSingletonMaxW).  Waves of a workgroup work on different groups and
-// never meet at a barrier.
-constexpr int kSmallWaves = 4;
-__global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nlist_p,
-                                                        const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
-                                                        int arg_type, double* __restrict__ out) {
-  __shared__ uint64_t keys[kSmallWaves][kSmallMax];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t li = blockIdx.x * kSmallWaves + wid;
-  if (li >= *nlist_p) return;
-  uint64_t* a = keys[wid];
-  const uint32_t g = list[li];
-  const uint32_t s = gstart[g];
-  const int n = static_cast<int>(gstart[g + 1] - s);
-  int P = 128;
-  while (P < n) P <<= 1;
-  uint64_t cv = 0, cneg = 0;
-  for (int i = lane; i < P; i += 64) {
-    uint64_t k = ~0ULL;
-    if (i < n) {
-      k = QKey(vals[s + i], arg_type);
-      cv += (k >= kNegInfKey && k <= kPosInfKey) ? 1 : 0;
-      cneg += k < kNegInfKey ? 1 : 0;
-    }
-    a[i] = k;
-  }
-  const int64_t W = static_cast<int64_t>(WaveSumU64(cv));
-  const int64_t lead = static_cast<int64_t>(WaveSumU64(cneg));
-  WaveSync();
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = lane; t < (P >> 1); t += 64) {
-        const int lo = 2 * t - (t & (j - 1));
-        const int hi = lo + j;
-        const uint64_t x = a[lo], y = a[hi];
-        if ((x > y) == ((lo & k) == 0)) {
-          a[lo] = y;
-          a[hi] = x;
-        }
-      }
-      WaveSync();
-    }
-  }
-  if (lane < 7) {
-    out[static_cast<uint64_t>(g) * 7 + lane] =
-        W == 0 ? __longlong_as_double(0x7FF8000000000000LL)
-               : SingletonQuantile(kQuantileQ[lane], W, [&](int64_t j) -> double { return QVal(a[lead + j]); });
-  }
-}
-
-constexpr int kMidMax = 4096;
-constexpr int kMidCentroids = 2048;
-
 // ---------------------------------------------------------------------------------------
-// Block merge sort of up to 16 * blockDim.x u64 keys in LDS (replaces the LDS bitonic sort:
+// Merge sort of up to 16 * (threads) u64 keys in LDS (replaces the LDS bitonic sort:
 // ~5x fewer LDS operations and 16 barriers instead of 78 for 4096 keys).  Each thread sorts
 // 16 keys in registers with a bitonic network, then log2(P/16) rounds merge pairs of sorted
 // runs: every thread finds its 16 outputs' start on the merge path (binary search) and merges
@@ -599,9 +660,15 @@ __device__ __forceinline__ void SortNetwork16(uint64_t (&r)[kMsIpt]) {
   }
 }
 
-// Sorts a[0, P) (logical indices, PadIdx layout), P a power of two in [16, 16 * blockDim.x].
-__device__ void BlockMergeSortLds(uint64_t* a, int P) {
-  const int t = threadIdx.x;
+// Sorts a[0, P) (logical indices, PadIdx layout), P a power of two in [16, 16 * nthreads],
+// by the nthreads threads t = 0.. of a workgroup (kWave = false: block barriers) or of one wave
+// (kWave = true: wave-local LDS ordering only).
+template <bool kWave>
+__device__ void MergeSortLds(uint64_t* a, int P, int t) {
+  auto sync = [] {
+    if (kWave) WaveSync();
+    else __syncthreads();
+  };
   const bool act = t * kMsIpt < P;
   uint64_t r[kMsIpt];
   if (act) {
@@ -611,7 +678,7 @@ __device__ void BlockMergeSortLds(uint64_t* a, int P) {
 #pragma unroll
     for (int i = 0; i < kMsIpt; ++i) a[PadIdx(t * kMsIpt + i)] = r[i];
   }
-  __syncthreads();
+  sync();
   for (int w = kMsIpt; w < P; w <<= 1) {
     if (act) {
       const int base = (t * kMsIpt) & ~(2 * w - 1);
@@ -640,14 +707,59 @@ __device__ void BlockMergeSortLds(uint64_t* a, int P) {
         }
       }
     }
-    __syncthreads();
+    sync();
     if (act) {
 #pragma unroll
       for (int k = 0; k < kMsIpt; ++k) a[PadIdx(t * kMsIpt + k)] = r[k];
     }
-    __syncthreads();
+    sync();
   }
 }
+__device__ __forceinline__ void BlockMergeSortLds(uint64_t* a, int P) { MergeSortLds<false>(a, P, threadIdx.x); }
+__device__ __forceinline__ void WaveMergeSortLds(uint64_t* a, int P) { MergeSortLds<true>(a, P, threadIdx.x & 63); }
+constexpr int kWaveSortMax = 64 * kMsIpt;  // 1024
+
+// One wave per group with 64 < n <= 1024: merge sort in the wave's LDS slice (WaveMergeSortLds),
+// singleton digest (W <= 1024 <= kSingletonMaxW).  Waves of a workgroup work on
+// different groups and never meet at a barrier.
+constexpr int kSmallWaves = 4;
+constexpr int kSmallPadded = kSmallMax + kSmallMax / 16;
+__global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nlist_p,
+                                                        const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
+                                                        int arg_type, double* __restrict__ out) {
+  __shared__ uint64_t keys[kSmallWaves][kSmallPadded];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t li = blockIdx.x * kSmallWaves + wid;
+  if (li >= *nlist_p) return;
+  uint64_t* a = keys[wid];
+  const uint32_t g = list[li];
+  const uint32_t s = gstart[g];
+  const int n = static_cast<int>(gstart[g + 1] - s);
+  int P = 128;
+  while (P < n) P <<= 1;
+  uint64_t cv = 0, cneg = 0;
+  for (int i = lane; i < P; i += 64) {
+    uint64_t k = ~0ULL;
+    if (i < n) {
+      k = QKey(vals[s + i], arg_type);
+      cv += (k >= kNegInfKey && k <= kPosInfKey) ? 1 : 0;
+      cneg += k < kNegInfKey ? 1 : 0;
+    }
+    a[PadIdx(i)] = k;
+  }
+  const int64_t W = static_cast<int64_t>(WaveSumU64(cv));
+  const int64_t lead = static_cast<int64_t>(WaveSumU64(cneg));
+  WaveSync();
+  WaveMergeSortLds(a, P);
+  if (lane < 7) {
+    out[static_cast<uint64_t>(g) * 7 + lane] =
+        W == 0 ? __longlong_as_double(0x7FF8000000000000LL)
+               : SingletonQuantile(kQuantileQ[lane], W, [&](int64_t j) -> double { return QVal(a[PadIdx(static_cast<int>(lead + j))]); });
+  }
+}
+
+constexpr int kMidMax = 4096;
+constexpr int kMidCentroids = 2048;
 
 
 // Lower bound of `key` in sorted a[0, n).
@@ -689,21 +801,24 @@ struct PreChain {
   int64_t W;
 };
 
-// Centroid-boundary chains (DigestBoundaries) of many groups at once, one thread per group:
-// the chain is sequential per group (~1100 steps for any W > kSingletonMaxW), so running it
-// inside each group's digest workgroup serialised the whole workgroup behind one lane.
+// Centroid-boundary chains of many groups at once, one wave per group (DigestBoundariesWave:
+// ~10 chain steps per round); the chain is sequential per group (~1000-1200 steps for any
+// W > kSingletonMaxW), so running it inside each group's digest workgroup serialised the
+// whole workgroup behind it.
 constexpr int kChainCap = 2048;
+constexpr int kChainWaves = 4;
 // Chain slots: list a (mid groups) at [0, a_cap), list b (big groups) at [a_cap, ...).
-__global__ void __launch_bounds__(64) DigestChainKernel(const uint32_t* __restrict__ list_a, const uint32_t* __restrict__ na_p,
-                                                        uint32_t a_cap, const uint32_t* __restrict__ list_b,
-                                                        const uint32_t* __restrict__ nb_p, const uint32_t* __restrict__ gstart,
-                                                        uint32_t* __restrict__ starts_out, int32_t* __restrict__ nc_out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(64 * kChainWaves) DigestChainKernel(const uint32_t* __restrict__ list_a, const uint32_t* __restrict__ na_p,
+                                                                      uint32_t a_cap, const uint32_t* __restrict__ list_b,
+                                                                      const uint32_t* __restrict__ nb_p, const uint32_t* __restrict__ gstart,
+                                                                      uint32_t* __restrict__ starts_out, int32_t* __restrict__ nc_out) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t na = *na_p, nb = *nb_p;
   if (i < a_cap ? i >= na : i - a_cap >= nb) return;
   const uint32_t g = i < a_cap ? list_a[i] : list_b[i - a_cap];
   const int64_t W = gstart[g + 1] - gstart[g];
-  nc_out[i] = W <= kSingletonMaxW ? -2 : static_cast<int32_t>(DigestBoundaries(W, starts_out + static_cast<uint64_t>(i) * kChainCap, kChainCap));
+  const int32_t nc = W <= kSingletonMaxW ? -2 : static_cast<int32_t>(DigestBoundariesWave(W, starts_out + static_cast<uint64_t>(i) * kChainCap, kChainCap));
+  if ((threadIdx.x & 63) == 0) nc_out[i] = nc;
 }
 
 __device__ __forceinline__ PreChain PreChainAt(const uint32_t* starts_all, const int32_t* nc_all, uint32_t i, int64_t n) {
@@ -816,7 +931,7 @@ struct BigChunk {
   uint32_t len;    // <= kMidMax
   uint32_t g_n;    // group size
   uint32_t passes; // merge passes the group needs (ceil(log2(g_n / kMidMax)))
-  uint32_t pad;
+  uint32_t bidx;   // index of its group in the big-group list
 };
 
 __global__ void __launch_bounds__(256) BigChunkSortKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
@@ -833,7 +948,8 @@ __global__ void __launch_bounds__(256) BigChunkSortKernel(const BigChunk* __rest
 struct BigGroup {
   uint64_t off;     // absolute staging offset of the group
   uint64_t n;
-  uint64_t eoff;    // prefix of element counts (for the flattened launch)
+  uint32_t c0;      // its first chunk
+  uint32_t nch;     // its chunk count
   uint32_t g;
   uint32_t passes;  // merge passes it needs: its sorted keys end in keysA (even) / keysB (odd)
 };
@@ -877,7 +993,8 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
       BigGroup B;
       B.off = off;
       B.n = n;
-      B.eoff = 0;
+      B.c0 = cbase;
+      B.nch = nch;
       B.g = g;
       B.passes = passes;
       groups[i] = B;
@@ -888,7 +1005,7 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
         C.len = min(static_cast<uint32_t>(kMidMax), n - c * kMidMax);
         C.g_n = n;
         C.passes = passes;
-        C.pad = 0;
+        C.bidx = i;
         chunks[cbase + c] = C;
       }
     }
@@ -1005,6 +1122,451 @@ __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restric
 }
 
 // ---------------------------------------------------------------------------------------
+// Big groups by selection.  A digest reads at most 4 centroid means per quantile, each the
+// mean of a known range of sorted ranks (the chain depends on W only), so a big group is never
+// sorted.  Its values are binned by splitters taken from a sorted sample (BigSample), the bins
+// are counted (BigHist), the bins holding the needed ranges' ends are chosen (BigPlan), their
+// values gathered while the ranks strictly inside a range are summed in place (BigCollect),
+// the gathered bins sorted (BigBinSort), and the means and quantiles formed (BigSelDigest).
+// Centroids of <= kSeqMean values (every centroid while W <= ~10000) get the reference's
+// incremental mean over their sorted values, as in BlockDigest; larger ones sum/count with a
+// fixed summation order (deterministic).  A group the path cannot serve (NaN values, a bin to
+// gather beyond LDS capacity: heavy duplicates, too many bins) is flagged; finalize then runs
+// the full sort + merge path (BigChunkSort / BigMergeTile / BigDigest) for the big groups.
+// ---------------------------------------------------------------------------------------
+constexpr int kSelBins = 1024;
+constexpr int kSelSample = 2048;  // two samples per bin
+constexpr int kSelMaxRanges = kNeed;
+constexpr int kSelMaxColl = 256;
+constexpr uint32_t kSelCollCap = kMidMax;
+constexpr uint8_t kTagColl = 0x80;
+
+struct BigPlan {
+  int32_t nc;        // centroids
+  int32_t n_ranges;  // distinct centroids the quantiles read
+  int32_t n_coll;    // bins to gather
+  int32_t fallback;  // 1: the full sort path serves this group
+  int32_t need_u[kNeed];  // DigestQuantile mean call (q * 4 + k) -> range
+  int32_t rj[kSelMaxRanges];
+  uint32_t rs[kSelMaxRanges], re[kSelMaxRanges];    // rank range [rs, re)
+  uint32_t rbs[kSelMaxRanges], rbe[kSelMaxRanges];  // bins of its first and last rank
+  uint16_t coll[kSelMaxColl];                       // bins to gather, ascending
+};
+
+static_assert(sizeof(BigPlan) % 4 == 0, "BigPlan is copied as words");
+
+// Bin of a sort key: the last b with S[b] <= key (S[0] = 0, S non-decreasing).
+__device__ __forceinline__ int SelBin(const uint64_t* S, uint64_t key) {
+  int b = 0;
+#pragma unroll
+  for (int step = kSelBins / 2; step >= 1; step >>= 1)
+    if (S[b + step] <= key) b += step;
+  return b;
+}
+// Bin holding rank r: the last b with bs[b] <= r (bs = exclusive prefix of the bin counts;
+// that bin is never empty since bs[b + 1] > r).
+__device__ __forceinline__ int BinOfRank(const uint32_t* bs, uint32_t r) {
+  int b = 0;
+#pragma unroll
+  for (int step = kSelBins / 2; step >= 1; step >>= 1)
+    if (bs[b + step] <= r) b += step;
+  return b;
+}
+
+// Splitters: kSelSample keys at evenly spaced positions of the group, sorted; S[b] = every
+// (kSelSample / kSelBins)-th of them, S[0] = 0.
+__global__ void __launch_bounds__(256) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
+                                                       const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl) {
+  if (blockIdx.x >= *nbig_p) return;
+  __shared__ uint64_t keys[PaddedLen(kSelSample)];
+  const BigGroup G = groups[blockIdx.x];
+  for (int j = threadIdx.x; j < kSelSample; j += blockDim.x) {
+    const uint64_t pos = (static_cast<uint64_t>(2 * j + 1) * G.n) / (2 * kSelSample);
+    keys[PadIdx(j)] = QKey(vals[G.off + pos], arg_type);
+  }
+  __syncthreads();
+  BlockMergeSortLds(keys, kSelSample);
+  uint64_t* S = spl + static_cast<uint64_t>(blockIdx.x) * kSelBins;
+  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) S[b] = b == 0 ? 0ULL : keys[PadIdx(b * (kSelSample / kSelBins))];
+}
+
+// Bin counts (and NaN count) per big group; one workgroup per 4096-value chunk.
+__global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
+                                                     const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
+                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ nan_cnt) {
+  if (blockIdx.x >= *nchunks_p) return;
+  __shared__ uint64_t S[kSelBins];
+  __shared__ uint32_t h[kSelBins];
+  __shared__ uint32_t s_nan;
+  const BigChunk c = chunks[blockIdx.x];
+  const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
+  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) {
+    S[b] = Sg[b];
+    h[b] = 0;
+  }
+  if (threadIdx.x == 0) s_nan = 0;
+  constexpr int kPer = kMidMax / 256;
+  uint64_t raw[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    raw[k] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
+  }
+  __syncthreads();
+  uint32_t nn = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = k * 256 + threadIdx.x;
+    if (i < static_cast<int>(c.len)) {
+      const uint64_t key = QKey(raw[k], arg_type);
+      nn += (key < kNegInfKey || key > kPosInfKey) ? 1u : 0u;
+      atomicAdd(&h[SelBin(S, key)], 1u);
+    }
+  }
+  if (nn) atomicAdd(&s_nan, nn);
+  __syncthreads();
+  uint32_t* H = hist + static_cast<uint64_t>(c.bidx) * kSelBins;
+  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x)
+    if (h[b]) atomicAdd(&H[b], h[b]);
+  if (threadIdx.x == 0 && s_nan) atomicAdd(&nan_cnt[c.bidx], s_nan);
+}
+
+// Per big group: bin starts, the centroids the quantiles read (DigestQuantile's recording
+// pass, as in BlockDigest), their rank ranges and bins, the bin tags (gather / inside range u)
+// and the gather offsets.
+__global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
+                                                     const uint32_t* __restrict__ chain_starts, const int32_t* __restrict__ chain_nc,
+                                                     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ nan_cnt,
+                                                     uint32_t* __restrict__ bstart_all, uint8_t* __restrict__ tag_all,
+                                                     uint32_t* __restrict__ cbase_all, BigPlan* __restrict__ plans,
+                                                     unsigned int* __restrict__ n_fallback) {
+  if (blockIdx.x >= *nbig_p) return;
+  __shared__ uint32_t bs[kSelBins + 1];
+  __shared__ uint8_t tg[kSelBins];
+  __shared__ uint32_t s_scan[256], s_scan2[256];
+  __shared__ BigPlan P;
+  __shared__ int32_t s_need[kNeed];
+  __shared__ int s_fb;
+  const int t = threadIdx.x;
+  const uint32_t bi = blockIdx.x;
+  const BigGroup G = groups[bi];
+  const int64_t W = static_cast<int64_t>(G.n);
+  const uint32_t* H = hist + static_cast<uint64_t>(bi) * kSelBins;
+  const uint32_t* starts = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
+  const int32_t nc = chain_nc[bi];
+  constexpr int kPer = kSelBins / 256;
+  // exclusive scan of the bin counts
+  uint32_t cnt[kPer], tot = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    cnt[k] = H[t * kPer + k];
+    tot += cnt[k];
+  }
+  s_scan[t] = tot;
+  if (t == 0) s_fb = (nan_cnt[bi] != 0 || nc < 0) ? 1 : 0;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t x = t >= o ? s_scan[t - o] : 0u;
+    __syncthreads();
+    s_scan[t] += x;
+    __syncthreads();
+  }
+  {
+    uint32_t run = s_scan[t] - tot;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      bs[t * kPer + k] = run;
+      run += cnt[k];
+    }
+    if (t == 255) bs[kSelBins] = run;
+  }
+  if (t < kNeed) s_need[t] = -1;
+  __syncthreads();
+  if (s_fb) {
+    if (t == 0) {
+      P.fallback = 1;
+      atomicAdd(n_fallback, 1u);
+    }
+    __syncthreads();
+    if (t == 0) plans[bi].fallback = 1;
+    return;
+  }
+  auto start = [&](int64_t j) -> int64_t { return starts[j]; };
+  if (t < 7) {
+    int k = 0;
+    (void)DigestQuantile(kQuantileQ[t], nc, W, start, [&](int64_t j) -> double {
+      if (k < 4) s_need[t * 4 + k] = static_cast<int32_t>(j);
+      ++k;
+      return 0.0;
+    });
+  }
+  for (int b = t; b < kSelBins; b += 256) tg[b] = 0;
+  __syncthreads();
+  if (t == 0) {
+    int nr = 0;
+    for (int i = 0; i < kNeed; ++i) {
+      const int32_t j = s_need[i];
+      int u = -1;
+      if (j >= 0) {
+        for (int v = 0; v < nr; ++v)
+          if (P.rj[v] == j) u = v;
+        if (u < 0) {
+          u = nr++;
+          const uint32_t s = starts[j];
+          const uint32_t e = j + 1 < nc ? starts[j + 1] : static_cast<uint32_t>(W);
+          P.rj[u] = j;
+          P.rs[u] = s;
+          P.re[u] = e;
+          P.rbs[u] = static_cast<uint32_t>(BinOfRank(bs, s));
+          P.rbe[u] = static_cast<uint32_t>(BinOfRank(bs, e - 1));
+        }
+      }
+      P.need_u[i] = u;
+    }
+    P.n_ranges = nr;
+    P.nc = nc;
+    P.fallback = 0;
+  }
+  __syncthreads();
+  // Tags: the end bins of every range (every bin of a small range) are gathered; the bins
+  // strictly inside a large range are summed in place.  Distinct ranges never share an inside
+  // bin, so the writes below never disagree.
+  for (int u = 0; u < P.n_ranges; ++u) {
+    const uint32_t b0 = P.rbs[u], b1 = P.rbe[u];
+    const bool small = P.re[u] - P.rs[u] <= static_cast<uint32_t>(kSeqMean);
+    for (uint32_t b = b0 + t; b <= b1; b += 256) {
+      if (small || b == b0 || b == b1) tg[b] = kTagColl;
+      else if (tg[b] == 0) tg[b] = static_cast<uint8_t>(u + 1);
+    }
+    __syncthreads();
+  }
+  // Gathered bins in ascending order and their offsets (relative to the group) in the
+  // candidate buffer.
+  uint32_t nf = 0, nv = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (tg[t * kPer + k] == kTagColl) {
+      ++nf;
+      nv += cnt[k];
+    }
+  }
+  s_scan[t] = nf;
+  s_scan2[t] = nv;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t x = t >= o ? s_scan[t - o] : 0u;
+    const uint32_t y = t >= o ? s_scan2[t - o] : 0u;
+    __syncthreads();
+    s_scan[t] += x;
+    s_scan2[t] += y;
+    __syncthreads();
+  }
+  {
+    uint32_t fi = s_scan[t] - nf, vo = s_scan2[t] - nv;
+    bool over = false;
+    uint32_t* cb = cbase_all + static_cast<uint64_t>(bi) * kSelBins;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = t * kPer + k;
+      if (tg[b] == kTagColl) {
+        if (fi < static_cast<uint32_t>(kSelMaxColl)) P.coll[fi] = static_cast<uint16_t>(b);
+        over = over || cnt[k] > kSelCollCap;
+        cb[b] = vo;
+        ++fi;
+        vo += cnt[k];
+      }
+    }
+    if (over) s_fb = 1;
+  }
+  __syncthreads();
+  const uint32_t n_coll = s_scan[255];
+  if (t == 0) {
+    P.n_coll = static_cast<int32_t>(n_coll);
+    if (n_coll > static_cast<uint32_t>(kSelMaxColl)) s_fb = 1;
+  }
+  __syncthreads();
+  if (t == 0 && s_fb) {
+    P.fallback = 1;
+    atomicAdd(n_fallback, 1u);
+  }
+  uint32_t* bso = bstart_all + static_cast<uint64_t>(bi) * (kSelBins + 1);
+  uint8_t* tgo = tag_all + static_cast<uint64_t>(bi) * kSelBins;
+  for (int b = t; b <= kSelBins; b += 256) bso[b] = bs[b];
+  for (int b = t; b < kSelBins; b += 256) tgo[b] = tg[b];
+  __syncthreads();
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&P);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(plans + bi);
+  for (int w = t; w < static_cast<int>(sizeof(BigPlan) / 4); w += 256) dst[w] = src[w];
+}
+
+// Gather the values of the tagged bins into the group's candidate region (any order: the bins
+// are sorted next) and sum the values inside each large range per chunk.  Sums are
+// deterministic: wave w takes chunk positions [1024 w, 1024 (w + 1)) in 16 rounds, each
+// round's values of one range are summed by a fixed shuffle tree, rounds and waves in order.
+__global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
+                                                        const BigPlan* __restrict__ plans, const uint64_t* __restrict__ vals, int arg_type,
+                                                        const uint64_t* __restrict__ spl, const uint8_t* __restrict__ tag_all,
+                                                        const uint32_t* __restrict__ cbase_all, uint32_t* __restrict__ cursor_all,
+                                                        uint64_t* __restrict__ cand, double* __restrict__ partial) {
+  if (blockIdx.x >= *nchunks_p) return;
+  const BigChunk c = chunks[blockIdx.x];
+  const BigPlan* P = plans + c.bidx;
+  if (P->fallback) return;
+  const int n_ranges = P->n_ranges;
+  __shared__ uint64_t S[kSelBins];
+  __shared__ uint8_t tg[kSelBins];
+  __shared__ double acc[4][kSelMaxRanges];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
+  const uint8_t* Tg = tag_all + static_cast<uint64_t>(c.bidx) * kSelBins;
+  for (int b = t; b < kSelBins; b += 256) {
+    S[b] = Sg[b];
+    tg[b] = Tg[b];
+  }
+  if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
+  constexpr int kRounds = kMidMax / 256;
+  uint64_t raw[kRounds];
+#pragma unroll
+  for (int r = 0; r < kRounds; ++r) {
+    const int i = wid * (kMidMax / 4) + r * 64 + lane;
+    raw[r] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
+  }
+  __syncthreads();
+  const uint32_t* cb = cbase_all + static_cast<uint64_t>(c.bidx) * kSelBins;
+  uint32_t* cur = cursor_all + static_cast<uint64_t>(c.bidx) * kSelBins;
+  uint64_t* cg = cand + c.g_off;
+  for (int r = 0; r < kRounds; ++r) {
+    const int i = wid * (kMidMax / 4) + r * 64 + lane;
+    int u = -1;
+    double v = 0.0;
+    if (i < static_cast<int>(c.len)) {
+      const uint64_t key = QKey(raw[r], arg_type);
+      const int b = SelBin(S, key);
+      const uint8_t tag = tg[b];
+      if (tag == kTagColl) {
+        const uint32_t slot = atomicAdd(&cur[b], 1u);
+        cg[cb[b] + slot] = key;
+      } else if (tag != 0) {
+        u = tag - 1;
+        v = QVal(key);
+      }
+    }
+    unsigned long long pend = __ballot(u >= 0);
+    while (pend) {
+      const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
+      const bool mine = u == uu;
+      const double s = WaveSumF64(mine ? v : 0.0);
+      if (lane == 0) acc[wid][uu] += s;
+      pend &= ~__ballot(mine);
+    }
+  }
+  __syncthreads();
+  for (int u = t; u < n_ranges; u += 256)
+    partial[static_cast<uint64_t>(blockIdx.x) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
+}
+
+// Sort the gathered bins of the big groups (blockIdx.y = big group): bins of <= 1024 values
+// one per wave (BigBinSortKernel, blockIdx.x * 4 + wave = index in the plan's list), larger
+// ones one per workgroup (BigBinSortLargeKernel, blockIdx.x = index).
+__global__ void __launch_bounds__(256) BigBinSortKernel(const BigGroup* __restrict__ groups, const BigPlan* __restrict__ plans,
+                                                        const uint32_t* __restrict__ hist, const uint32_t* __restrict__ cbase_all,
+                                                        uint64_t* __restrict__ cand) {
+  __shared__ uint64_t keys[4][PaddedLen(kWaveSortMax)];
+  const uint32_t bi = blockIdx.y;
+  const BigPlan* P = plans + bi;
+  const int ci = static_cast<int>(blockIdx.x) * 4 + static_cast<int>(threadIdx.x >> 6);
+  if (P->fallback || ci >= P->n_coll) return;
+  const int b = P->coll[ci];
+  const int n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
+  if (n <= 1 || n > kWaveSortMax) return;
+  const int lane = threadIdx.x & 63;
+  uint64_t* s = keys[threadIdx.x >> 6];
+  uint64_t* a = cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
+  int Pn = kMsIpt;
+  while (Pn < n) Pn <<= 1;
+  for (int i = lane; i < Pn; i += 64) s[PadIdx(i)] = i < n ? a[i] : ~0ULL;
+  WaveSync();
+  WaveMergeSortLds(s, Pn);
+  for (int i = lane; i < n; i += 64) a[i] = s[PadIdx(i)];
+}
+__global__ void __launch_bounds__(256) BigBinSortLargeKernel(const BigGroup* __restrict__ groups, const BigPlan* __restrict__ plans,
+                                                             const uint32_t* __restrict__ hist, const uint32_t* __restrict__ cbase_all,
+                                                             uint64_t* __restrict__ cand) {
+  const uint32_t bi = blockIdx.y;
+  const BigPlan* P = plans + bi;
+  if (P->fallback || static_cast<int>(blockIdx.x) >= P->n_coll) return;
+  const int b = P->coll[blockIdx.x];
+  const int n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
+  if (n <= kWaveSortMax) return;
+  __shared__ uint64_t keys[PaddedLen(kMidMax)];
+  uint64_t* a = cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
+  int Pn = kMsIpt;
+  while (Pn < n) Pn <<= 1;
+  for (int i = threadIdx.x; i < Pn; i += blockDim.x) keys[PadIdx(i)] = i < n ? a[i] : ~0ULL;
+  __syncthreads();
+  BlockMergeSortLds(keys, Pn);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = keys[PadIdx(i)];
+}
+
+// Centroid means and the seven quantiles of every big group served by the selection path.
+__global__ void __launch_bounds__(256) BigSelDigestKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
+                                                          const BigPlan* __restrict__ plans, const uint32_t* __restrict__ chain_starts,
+                                                          const uint32_t* __restrict__ bstart_all, const uint32_t* __restrict__ cbase_all,
+                                                          const uint64_t* __restrict__ cand, const double* __restrict__ partial,
+                                                          double* __restrict__ out) {
+  if (blockIdx.x >= *nbig_p) return;
+  const uint32_t bi = blockIdx.x;
+  if (plans[bi].fallback) return;
+  __shared__ BigPlan P;
+  __shared__ double mean_u[kSelMaxRanges];
+  __shared__ double red[4];
+  const int t = threadIdx.x;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(plans + bi);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&P);
+    for (int w = t; w < static_cast<int>(sizeof(BigPlan) / 4); w += 256) dst[w] = src[w];
+  }
+  __syncthreads();
+  const BigGroup G = groups[bi];
+  const int64_t W = static_cast<int64_t>(G.n);
+  const uint32_t* starts = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
+  const uint32_t* bs = bstart_all + static_cast<uint64_t>(bi) * (kSelBins + 1);
+  const uint32_t* cb = cbase_all + static_cast<uint64_t>(bi) * kSelBins;
+  const uint64_t* cg = cand + G.off;
+  auto rank_val = [&](int64_t r) -> double {
+    const int b = BinOfRank(bs, static_cast<uint32_t>(r));
+    return QVal(cg[cb[b] + (static_cast<uint32_t>(r) - bs[b])]);
+  };
+  if (t < P.n_ranges && P.re[t] - P.rs[t] <= static_cast<uint32_t>(kSeqMean)) mean_u[t] = CentroidMean(rank_val, P.rs[t], P.re[t]);
+  for (int u = 0; u < P.n_ranges; ++u) {  // uniform: large ranges, block sums
+    const uint32_t s = P.rs[u], e = P.re[u];
+    if (e - s <= static_cast<uint32_t>(kSeqMean)) continue;
+    const uint32_t b0 = P.rbs[u], b1 = P.rbe[u];
+    double acc = 0;
+    const uint32_t e0 = min(e, bs[b0 + 1]);
+    for (uint32_t r = s + t; r < e0; r += 256) acc += QVal(cg[cb[b0] + (r - bs[b0])]);
+    if (b1 != b0)
+      for (uint32_t r = bs[b1] + t; r < e; r += 256) acc += QVal(cg[cb[b1] + (r - bs[b1])]);
+    for (uint32_t k = t; k < G.nch; k += 256) acc += partial[static_cast<uint64_t>(G.c0 + k) * kSelMaxRanges + u];
+    acc = WaveSumF64(acc);
+    if ((t & 63) == 0) red[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) mean_u[u] = (red[0] + red[1] + red[2] + red[3]) / static_cast<double>(e - s);
+    __syncthreads();
+  }
+  __syncthreads();
+  if (t < 7) {
+    auto start = [&](int64_t j) -> int64_t { return starts[j]; };
+    int k = 0;
+    out[static_cast<uint64_t>(G.g) * 7 + t] = DigestQuantile(kQuantileQ[t], P.nc, W, start, [&](int64_t) -> double {
+      const int32_t u = P.need_u[t * 4 + (k < 4 ? k : 3)];
+      ++k;
+      return mean_u[u];
+    });
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Keys out of the arena.
 // ---------------------------------------------------------------------------------------
 struct KeyOutDev {
@@ -1059,56 +1621,38 @@ __global__ void KeyStringCopyKernel(const AggPlanDev* __restrict__ plan, int key
 // ---------------------------------------------------------------------------------------
 // Host orchestration.
 // ---------------------------------------------------------------------------------------
-static int Log2Ceil(uint64_t x) {
-  int b = 0;
-  while ((uint64_t(1) << b) < x) ++b;
-  return b;
-}
 
-// meta: u64 [0] rows with a valid slot | u32 @8 groups | u32 @16 digest error | u32 @32.. class counts
+// meta: u64 [0] rows with a valid slot | u32 @8 groups | u32 @16 digest error | u32 @20 big groups
+// left to the sort path | u32 @32.. class counts | u32 @48 big chunks, largest big group
 __global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
   if (threadIdx.x == 0) {
     *reinterpret_cast<unsigned long long*>(meta) = n;
     *reinterpret_cast<uint32_t*>(meta + 8) = 0;
     *reinterpret_cast<uint32_t*>(meta + 16) = 0;
+    *reinterpret_cast<uint32_t*>(meta + 20) = 0;
     for (int c = 0; c < kNumClasses; ++c) reinterpret_cast<uint32_t*>(meta + 32)[c] = 0;
   }
 }
 
 int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* vals,
                        uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals) {
-  if (n == 0 || n >= (uint64_t(1) << 32)) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %llu records", static_cast<unsigned long long>(n));
-  const int nbits = std::max(1, Log2Ceil(static_cast<uint64_t>(G) + 1));
-  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
-  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
-  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
   for (int b = 0; b < 2; ++b) {
     PXG_RETURN_IF_ERROR(ws.key[b].Ensure(n * 4 + 16));
     PXG_RETURN_IF_ERROR(ws.val[b].Ensure(n * 8 + 16));
   }
-  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
-  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(nh + 1)) + 64));
-  const uint32_t* kin = keys;
   ConstValPtrs vin;
-  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = nullptr;
-  vin.p[0] = vals;
-  int cur = 0;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = p * kRadixBits;
-    const uint32_t* rk = p == 0 ? rank : nullptr;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, n, rk, cap, G, shift,
-                               ws.hist.as<uint32_t>(), nblocks));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, ws.scan.p));
-    ValPtrs vout;
-    for (int v = 0; v < kMaxVals; ++v) vout.p[v] = nullptr;
-    vout.p[0] = ws.val[cur].as<uint64_t>();
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, ws.key[cur].as<uint32_t>(),
-                               vin, vout, 1, n, rk, cap, G, shift, ws.hist.as<const uint32_t>(), nblocks));
-    kin = ws.key[cur].as<const uint32_t>();
-    vin.p[0] = ws.val[cur].as<const uint64_t>();
-    cur ^= 1;
+  uint32_t* kbuf[2];
+  ValPtrs vbuf[2];
+  for (int v = 0; v < kMaxVals; ++v) {
+    vin.p[v] = nullptr;
+    vbuf[0].p[v] = vbuf[1].p[v] = nullptr;
   }
-  *skeys = kin;
+  vin.p[0] = vals;
+  for (int b = 0; b < 2; ++b) {
+    kbuf[b] = ws.key[b].as<uint32_t>();
+    vbuf[b].p[0] = ws.val[b].as<uint64_t>();
+  }
+  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, rank, cap, G, vin, 1, n, kbuf, vbuf, ws.rs, skeys, &vin));
   *svals = vin.p[0];
   return PXG_OK;
 }
@@ -1176,7 +1720,14 @@ int32_t AggFinalizeImpl(Agg* a) {
 
   // Group keys out of the arena, on side stream 2 while the radix sort runs on the main
   // stream (ConvertAggHashMapToRowBatch group columns, agg_node.cc:303-349).  String payloads
-  // are sized by the arena (an upper bound), so no count comes back to the host first.
+  // are sized by the arena (an upper bound), so no count comes back to the host first.  Side
+  // stream 2 forks here; its launches are issued after the sort's, so the host reaches the
+  // sort (the critical path) sooner.
+  if (a->n_keys > 0) {
+    PXG_RETURN_IF_ERROR(ForkSide2(ctx));
+    guard.side2 = true;
+  }
+  auto IssueKeys = [&]() -> int32_t {
   {
     KeyOutDev ko;
     for (int k = 0; k < kMaxKeys; ++k) {
@@ -1196,8 +1747,6 @@ int32_t AggFinalizeImpl(Agg* a) {
     }
     if (a->n_keys > 0) {
       PXG_RETURN_IF_ERROR(ws.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(ngroups) + 1) + 64));
-      PXG_RETURN_IF_ERROR(ForkSide2(ctx));
-      guard.side2 = true;
       PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "key_extract", KeyExtractKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                                    a->d_plan.as<const AggPlanDev>(), static_cast<const uint32_t*>(ws.gslot.as<uint32_t>()), ngroups,
                                    a->slots.as<const unsigned long long>(), a->arena.as<const uint64_t>(), ko));
@@ -1214,40 +1763,29 @@ int32_t AggFinalizeImpl(Agg* a) {
       keys_on_side2 = true;
     }
   }
-
+    return PXG_OK;
+  };
   // 2. Stable LSD radix sort of (dense id, vals...) by dense id (ceil(log2(G + 1) / 8) passes);
   //    records without a group (deferred slots) get id G and sort last.  The staging itself is
   //    left as it is (slots), so finalize can run again and export still works.
-  const int nbits = std::max(1, Log2Ceil(static_cast<uint64_t>(ngroups) + 1));
-  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
-  const uint32_t nblocks = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
   for (int b = 0; b < 2; ++b) {
     PXG_RETURN_IF_ERROR(ws.skey[b].Ensure(n * 4 + 16));
     for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(ws.sval[b][v].Ensure(n * 8 + 16));
   }
-  const uint64_t nh = static_cast<uint64_t>(kRadixBuckets) * nblocks;
-  PXG_RETURN_IF_ERROR(ws.hist.Ensure(nh * 4 + 64));
-  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(std::max<uint64_t>(nh, n), a->cap) + 1)) + 64));
+  PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(n, a->cap) + 1)) + 64));
   scan_tmp = ws.scan.p;
-  const uint32_t* kin = a->st_slot.as<const uint32_t>();
   ConstValPtrs vin;
-  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
-  int cur = 0;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = p * kRadixBits;
-    const uint32_t* rank = p == 0 ? ws.rank.as<const uint32_t>() : nullptr;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RadixHistKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin, n, rank, a->cap, ngroups,
-                               shift, ws.hist.as<uint32_t>(), nblocks));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.hist.as<uint32_t>(), ws.hist.as<uint32_t>(), static_cast<int64_t>(nh), nullptr, scan_tmp));
-    ValPtrs vout;
-    for (int v = 0; v < kMaxVals; ++v) vout.p[v] = v < a->n_vals ? ws.sval[cur][v].as<uint64_t>() : nullptr;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RadixScatterKernel, dim3(nblocks), dim3(kRadixBlock), 0, kin,
-                               ws.skey[cur].as<uint32_t>(), vin, vout, a->n_vals, n, rank, a->cap, ngroups, shift,
-                               ws.hist.as<const uint32_t>(), nblocks));
-    kin = ws.skey[cur].as<const uint32_t>();
-    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? ws.sval[cur][v].as<const uint64_t>() : nullptr;
-    cur ^= 1;
+  uint32_t* kbuf[2];
+  ValPtrs vbuf[2];
+  for (int b = 0; b < 2; ++b) {
+    kbuf[b] = ws.skey[b].as<uint32_t>();
+    for (int v = 0; v < kMaxVals; ++v) vbuf[b].p[v] = v < a->n_vals ? ws.sval[b][v].as<uint64_t>() : nullptr;
   }
+  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+  const uint32_t* kin = nullptr;
+  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, a->n_vals,
+                                       n, kbuf, vbuf, ws.rs, &kin, &vin));
+  PXG_RETURN_IF_ERROR(IssueKeys());
   const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
   // 3. Group starts (first index of every id).
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
@@ -1294,25 +1832,77 @@ int32_t AggFinalizeImpl(Agg* a) {
   return PXG_OK;
   };
   if (!any_q) PXG_RETURN_IF_ERROR(RunReductions());
-  // Big-group digests, after side stream 2's merges (see below).
-  std::vector<int> big_pending;
-  uint32_t n_big_groups = 0;
+  uint32_t n_big_groups = 0, n_bchunks = 0;
+  uint64_t big_max = 0;
   const uint32_t* chain_starts_big = nullptr;
   const int32_t* chain_nc_big = nullptr;
-  // On side stream 2, behind its merges; the boundary chains come from the side stream (its
-  // join event was recorded before the mid digests were issued).
-  auto RunBigDigests = [&]() -> int32_t {
-    if (big_pending.empty()) return PXG_OK;
-    PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_join, 0));
-    for (int u : big_pending) {
-      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(),
-                                 ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big,
-                                 R.uda_out[u].as<double>(), d_err));
+  uint32_t* d_bigmeta = reinterpret_cast<uint32_t*>(meta + 48);
+  unsigned int* d_fallback = reinterpret_cast<unsigned int*>(meta + 20);
+  // Full sort path of the big groups for quantile UDA u on stream st: chunk sort, merge
+  // passes, digests.  Runs after the boundary chains (st must be ordered after them).
+  auto BigSortPath = [&](hipStream_t st, int u) -> int32_t {
+    const uint64_t* vals = cv.p[a->uda_val[u]];
+    const int at = a->uda_arg_type[u];
+    PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
+    PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
+    PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(n_big_groups) * kBigCentroids * 4));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
+                                 ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
+                                 ws.keysA.as<uint64_t>()));
+    DevBuf* src = &ws.keysA;
+    DevBuf* dst = &ws.keysB;
+    uint32_t pass = 0;
+    for (uint64_t w = kMidMax; w < big_max; w *= 2, ++pass) {
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
+                                   ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), src->as<const uint64_t>(),
+                                   dst->as<uint64_t>(), w, pass));
+      std::swap(src, dst);
     }
-    big_pending.clear();
-    return PXG_OK;
+    return LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+                    static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
+                    ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err);
   };
+  // Selection path, first half (needs the sorted values and the chunk list only): sample,
+  // splitters, bin counts.
+  auto BigSelectFront = [&](int u) -> int32_t {
+    const uint64_t* vals = cv.p[a->uda_val[u]];
+    const int at = a->uda_arg_type[u];
+    const uint64_t nb = n_big_groups;
+    PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4, ctx->side2));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel, dim3(n_big_groups), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), vals, at, ws.sel_spl.as<uint64_t>()));
+    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3(n_bchunks), dim3(256), 0, ws.bchunks.as<const BigChunk>(),
+                    static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_cnt.as<uint32_t>(),
+                    ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins);
+  };
+  // Second half, after the chains: plan, gather + inside sums, bin sorts, digests.
+  auto BigSelectBack = [&](int u) -> int32_t {
+    const uint64_t* vals = cv.p[a->uda_val[u]];
+    const int at = a->uda_arg_type[u];
+    const uint64_t nb = n_big_groups;
+    uint32_t* hist = ws.sel_cnt.as<uint32_t>();
+    uint32_t* cursor = hist + nb * kSelBins;
+    uint32_t* nan_cnt = hist + 2 * nb * kSelBins;
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_plan", BigPlanKernel, dim3(n_big_groups), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), chain_starts_big, chain_nc_big,
+                                 static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), ws.sel_bstart.as<uint32_t>(),
+                                 ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3(n_bchunks), dim3(256), 0,
+                                 ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
+                                 vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_tag.as<const uint8_t>(),
+                                 ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel, dim3(kSelMaxColl / 4, n_big_groups), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), ws.sel_plan.as<const BigPlan>(), static_cast<const uint32_t*>(hist),
+                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortLargeKernel, dim3(kSelMaxColl, n_big_groups), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), ws.sel_plan.as<const BigPlan>(), static_cast<const uint32_t*>(hist),
+                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    return LaunchOn(ctx, ctx->side2, "quant_sel_digest", BigSelDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+                    static_cast<const uint32_t*>(d_cls + 3), ws.sel_plan.as<const BigPlan>(), chain_starts_big,
+                    ws.sel_bstart.as<const uint32_t>(), ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<const uint64_t>(),
+                    ws.sel_partial.as<const double>(), R.uda_out[u].as<double>());
+  };
+  bool big_select = false;
   // 4. Quantile digests.
   if (any_q) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
@@ -1344,24 +1934,30 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain_cap) * kChainCap * 4));
     const uint32_t* chain_starts = ws.chain_starts.as<const uint32_t>();
     const int32_t* chain_nc = ws.chain_nc.as<const int32_t>();
-    // Chains: latency-bound (a few waves, ~1100 dependent steps each), on the side stream.
+    // Chains: latency-bound (one wave per mid / big group, ~110 rounds each), on the side stream.
     PXG_RETURN_IF_ERROR(ForkSide(ctx));
     guard.side = true;
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain_cap + 63) / 64), dim3(64), 0,
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain_cap + kChainWaves - 1) / kChainWaves),
+                                 dim3(64 * kChainWaves), 0,
                                  lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), mid_cap,
                                  lists + 3 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 3), gstart,
                                  ws.chain_starts.as<uint32_t>(), ws.chain_nc.as<int32_t>()));
-    PXG_RETURN_IF_ERROR(RunReductions());
+    PXG_HIP(hipEventRecord(ctx->ev_chain, ctx->side));
+    // The small digests follow the chains on the side stream (neither needs the other); the
+    // reductions and the tiny digests run on the main stream meanwhile.
     const uint32_t small_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kTinyMax + 1) + 1));
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
-      const uint64_t* vals = cv.p[a->uda_val[u]];
-      const int at = a->uda_arg_type[u];
-      double* qo = R.uda_out[u].as<double>();
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "quant_small", QuantSmallKernel, dim3((small_cap + kSmallWaves - 1) / kSmallWaves),
+                                   dim3(256), 0, lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart,
+                                   cv.p[a->uda_val[u]], a->uda_arg_type[u], R.uda_out[u].as<double>()));
+    }
+    PXG_RETURN_IF_ERROR(RunReductions());
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
-                                 static_cast<const uint32_t*>(d_cls), gstart, vals, at, qo));
-      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_small", QuantSmallKernel, dim3((small_cap + kSmallWaves - 1) / kSmallWaves), dim3(256), 0,
-                                 lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart, vals, at, qo));
+                                 static_cast<const uint32_t*>(d_cls), gstart, cv.p[a->uda_val[u]], a->uda_arg_type[u],
+                                 R.uda_out[u].as<double>()));
     }
     uint32_t hm[6];
     clk.Mark("finalize: issue to meta");
@@ -1369,61 +1965,50 @@ int32_t AggFinalizeImpl(Agg* a) {
     clk.Mark("finalize: meta wait");
     std::memcpy(hm, pin + 64, 24);
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
-    const uint32_t n_big = cls[3], n_bchunks = hm[4];
+    const uint32_t n_big = cls[3];
     n_big_groups = n_big;
     chain_starts_big = chain_starts + static_cast<uint64_t>(mid_cap) * kChainCap;
     chain_nc_big = chain_nc + mid_cap;
-    const uint64_t big_max = hm[5];
-    if (n_big > 0) {
+    big_max = hm[5];
+    n_bchunks = hm[4];
+    // PXG_BIG_SORT=1 forces the full sort path for every big group (tests compare the two).
+    big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT");
+    if (big_select) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
-      PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
-      PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(n_big) * kBigCentroids * 4));
+      PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8));
+      PXG_RETURN_IF_ERROR(ws.sel_cnt.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * 4 + 16));
+      PXG_RETURN_IF_ERROR(ws.sel_bstart.Ensure(static_cast<size_t>(n_big) * (kSelBins + 1) * 4));
+      PXG_RETURN_IF_ERROR(ws.sel_tag.Ensure(static_cast<size_t>(n_big) * kSelBins));
+      PXG_RETURN_IF_ERROR(ws.sel_cbase.Ensure(static_cast<size_t>(n_big) * kSelBins * 4));
+      PXG_RETURN_IF_ERROR(ws.sel_plan.Ensure(static_cast<size_t>(n_big) * sizeof(BigPlan)));
+      PXG_RETURN_IF_ERROR(ws.sel_partial.Ensure(static_cast<size_t>(n_bchunks) * kSelMaxRanges * 8 + 16));
     }
-    // Big groups: chunk sort + merge passes on side stream 2 (their late passes hold few
-    // workgroups), overlapping the mid digests and the key output on the main stream; the big
-    // digests join it at the end of finalize.  Each quantile UDA forks again, so its sorts
-    // start after the previous UDA's big digest has read the shared key buffers.
-    bool first_big = true;
+    // Big groups on side stream 2, overlapping the mid digests and the key output on the main
+    // stream: the selection path's sample + bin counts start right after the metadata readback,
+    // the rest waits for the boundary chains.  Every quantile UDA's big work runs in order on
+    // side stream 2, so later UDAs reuse the workspace safely.
+    if (n_big > 0) {
+      PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_meta, 0));
+      guard.side2 = true;
+    }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
+      if (big_select) PXG_RETURN_IF_ERROR(BigSelectFront(u));
+      PXG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_chain, 0));  // mid digests read the chains
       if (n_big > 0) {
-        // The first big path needs only what precedes the metadata readback (sorted values,
-        // chunk list), so it starts alongside the tiny / small digests.
-        if (first_big) PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_meta, 0));
-        else PXG_RETURN_IF_ERROR(ForkSide2(ctx));
-        guard.side2 = true;
-        first_big = false;
-        PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
-                                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
-                                     ws.keysA.as<uint64_t>()));
-        DevBuf* src = &ws.keysA;
-        DevBuf* dst = &ws.keysB;
-        uint32_t pass = 0;
-        for (uint64_t w = kMidMax; w < big_max; w *= 2, ++pass) {
-          PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
-                                       ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta),
-                                       src->as<const uint64_t>(), dst->as<uint64_t>(), w, pass));
-          std::swap(src, dst);
-        }
+        PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_chain, 0));
+        PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(u) : BigSortPath(ctx->side2, u));
       }
-      PXG_RETURN_IF_ERROR(JoinSide(ctx));
-      guard.side = false;
       double* qo = R.uda_out[u].as<double>();
       if (cls[2] > 0)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
                                    gstart, chain_starts, chain_nc, static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
-      if (n_big > 0) {
-        big_pending.push_back(u);
-        // A later quantile UDA reuses the key buffers: its digest must run before that UDA's sorts.
-        bool more = false;
-        for (int v = u + 1; v < a->n_udas; ++v) more = more || a->uda_kind[v] == PXG_UDA_QUANTILES;
-        if (more) PXG_RETURN_IF_ERROR(RunBigDigests());
-      }
     }
   }
-  PXG_RETURN_IF_ERROR(RunBigDigests());
+  if (guard.side) PXG_RETURN_IF_ERROR(JoinSide(ctx));  // the small digests
+  guard.side = false;
   if (keys_on_side2 || n_big_groups > 0) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
   guard.side2 = false;
   // One sync for the digest error flag and every string-key total.
@@ -1436,6 +2021,7 @@ int32_t AggFinalizeImpl(Agg* a) {
   uint32_t g_dev = 0;
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 1, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 2, d_fallback, 4, hipMemcpyDeviceToHost, ctx->stream));
   clk.Mark("finalize: issue rest");
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   clk.Mark("finalize: final wait");
@@ -1443,6 +2029,39 @@ int32_t AggFinalizeImpl(Agg* a) {
     if (a->key_types[k] == PXG_STRING) totals[k] = pin32[k];
   err = pin32[kMaxKeys];
   g_dev = pin32[kMaxKeys + 1];
+  const uint32_t n_fallback = pin32[kMaxKeys + 2];
+  if (big_select && EnvFlag("PXG_DIAG_SEL")) {  // selection-path shape (tools/; one extra sync)
+    std::vector<BigPlan> plans(n_big_groups);
+    std::vector<uint32_t> hh(static_cast<size_t>(n_big_groups) * kSelBins);
+    std::vector<BigGroup> gg(n_big_groups);
+    PXG_HIP(hipMemcpy(plans.data(), ws.sel_plan.p, plans.size() * sizeof(BigPlan), hipMemcpyDeviceToHost));
+    PXG_HIP(hipMemcpy(hh.data(), ws.sel_cnt.p, hh.size() * 4, hipMemcpyDeviceToHost));
+    PXG_HIP(hipMemcpy(gg.data(), ws.big.p, gg.size() * sizeof(BigGroup), hipMemcpyDeviceToHost));
+    uint64_t coll = 0, cand = 0, big_bins = 0, maxbin = 0, rows = 0;
+    for (uint32_t i = 0; i < n_big_groups; ++i) {
+      rows += gg[i].n;
+      if (plans[i].fallback) continue;
+      coll += plans[i].n_coll;
+      for (int c = 0; c < plans[i].n_coll && c < kSelMaxColl; ++c) {
+        const uint32_t h = hh[static_cast<size_t>(i) * kSelBins + plans[i].coll[c]];
+        cand += h;
+        big_bins += h > static_cast<uint32_t>(kWaveSortMax) ? 1 : 0;
+        maxbin = std::max<uint64_t>(maxbin, h);
+      }
+    }
+    std::fprintf(stderr, "[pxg sel] big groups %u (%llu rows), chunks %u, fallback %u, gathered bins %llu (%llu values, %llu > %d, max %llu)\n",
+                 n_big_groups, (unsigned long long)rows, n_bchunks, n_fallback, (unsigned long long)coll, (unsigned long long)cand,
+                 (unsigned long long)big_bins, kWaveSortMax, (unsigned long long)maxbin);
+  }
+  if (big_select && n_fallback > 0) {
+    // Some big group could not be served by selection (NaN values, heavy duplicates): the full
+    // sort path recomputes every big group's quantiles (the chains are long done).
+    for (int u = 0; u < a->n_udas; ++u)
+      if (a->uda_kind[u] == PXG_UDA_QUANTILES) PXG_RETURN_IF_ERROR(BigSortPath(ctx->stream, u));
+    PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    err = pin32[kMaxKeys];
+  }
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
   if (g_dev != ngroups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, ngroups);
   for (int k = 0; k < a->n_keys; ++k)
@@ -1569,5 +2188,33 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
       p[0] = InitialFinalValue(a.uda_kind[u], a.uda_arg_type[u], a.uda_init[u]);
     }
   }
+  return PXG_OK;
+}
+
+// Diagnostics: chains for given W by either chain builder (tests compare them).
+__global__ void DiagChainKernel(const int64_t* __restrict__ w, int32_t n, int32_t wave, uint32_t* __restrict__ starts, int32_t cap,
+                                int32_t* __restrict__ nc) {
+  const int32_t i = static_cast<int32_t>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= n) return;
+  uint32_t* s = starts + static_cast<uint64_t>(i) * cap;
+  int64_t r;
+  if (wave == 2) {  // instrumented: cycles in evaluation / resolution, rounds, rounds with an exact-path lane
+    r = DigestBoundariesWave<true>(w[i], s, cap - 8, reinterpret_cast<uint64_t*>(s + cap - 8));
+  } else if (wave) {
+    r = DigestBoundariesWave(w[i], s, cap);
+  } else {
+    if ((threadIdx.x & 63) != 0) return;
+    r = DigestBoundaries(w[i], s, cap);
+  }
+  if ((threadIdx.x & 63) == 0) nc[i] = static_cast<int32_t>(r);
+}
+
+extern "C" int32_t pxg_digest_chains(pxg_ctx* ctx, const int64_t* d_w, int32_t n, int32_t wave, uint32_t* d_starts, int32_t cap,
+                                     int32_t* d_nc) {
+  if (!ctx || !d_w || !d_starts || !d_nc || n < 0 || cap <= 0) return SetError(PXG_INVALID_ARGUMENT, "bad pxg_digest_chains arguments");
+  if (n == 0) return PXG_OK;
+  Ctx* c = &ctx->impl;
+  PXG_RETURN_IF_ERROR(Launch(c, "diag_chain", DiagChainKernel, dim3((n + 3) / 4), dim3(256), 0, d_w, n, wave, d_starts, cap, d_nc));
+  PXG_HIP(hipStreamSynchronize(c->stream));
   return PXG_OK;
 }

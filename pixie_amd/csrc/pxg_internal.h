@@ -33,6 +33,12 @@
 
 namespace pxg {
 
+// Boolean environment switch (set and not "0"); read at each use, so tests can flip it.
+inline bool EnvFlag(const char* name) {
+  const char* e = std::getenv(name);
+  return e != nullptr && e[0] != 0 && !(e[0] == '0' && e[1] == 0);
+}
+
 // Device allocation that frees itself; capacity-tracked for growth.
 struct DevBuf {
   void* p = nullptr;
@@ -130,6 +136,7 @@ struct Ctx {
   hipStream_t side2 = nullptr;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   hipEvent_t ev_meta = nullptr;  // finalize: the big-group metadata readback has landed
+  hipEvent_t ev_chain = nullptr; // finalize: the digest boundary chains are done (side stream)
   bool profiling = false;
   std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;

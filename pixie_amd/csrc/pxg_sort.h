@@ -5,8 +5,14 @@
 
 namespace pxg {
 
+// Radix sort pass state: tile x digit counts / offsets and the global digit totals.
+struct RadixPassWs {
+  DevBuf hist, ghist;
+};
+
 struct RadixWs {
-  DevBuf key[2], val[2], hist, scan;
+  DevBuf key[2], val[2], scan;  // scan: scratch for the caller's own scans
+  RadixPassWs rs;
 };
 
 // Sorts n records by DenseKey(keys[i]) = rank ? (keys[i] < cap ? rank[keys[i]] : G) : keys[i],

@@ -106,6 +106,16 @@ __device__ __forceinline__ double SingletonQuantile(double q, int64_t W, ValF va
   return DigestQuantile(q, W, W, [](int64_t j) { return j; }, val);
 }
 
+// One step of the boundary chain: the centroid after the one starting at b starts at
+// max(b + 1, floor(wLimit(b))) (W when wLimit reaches W; b = 0 uses the initial limit
+// W * Q(1)).  A result >= W ends the chain.
+__device__ __forceinline__ int32_t ChainNext(int32_t b, double Wd, double invW, int32_t W32) {
+  const double wl = b == 0 ? Wd * IntegratedQ(1.0) : NextLimit(b, Wd, invW);
+  const double f = floor(wl);
+  const int32_t nb = f >= Wd ? W32 : static_cast<int32_t>(f);
+  return nb < b + 1 ? b + 1 : nb;
+}
+
 // Build the centroid boundaries for W unit weights.  Single thread.  Returns the centroid
 // count, or -1 if more than max_c centroids would be needed.
 __device__ inline int64_t DigestBoundaries(int64_t W, uint32_t* starts, int64_t max_c) {
@@ -114,18 +124,121 @@ __device__ inline int64_t DigestBoundaries(int64_t W, uint32_t* starts, int64_t 
   starts[nc++] = 0;
   const double Wd = static_cast<double>(W);
   const double invW = 1.0 / Wd;
-  double wl = Wd * IntegratedQ(1.0);
-  int32_t i = 1;
   const int32_t W32 = static_cast<int32_t>(W);  // W < 2^31 (staged rows are < 2^32 per agg)
+  int32_t b = 0;
   while (true) {
-    const double f = floor(wl);
-    int32_t b = f >= Wd ? W32 : static_cast<int32_t>(f);
-    if (b < i) b = i;
-    if (b >= W32) break;
+    const int32_t nb = ChainNext(b, Wd, invW, W32);
+    if (nb >= W32) break;
     if (nc >= max_c) return -1;
-    starts[nc++] = static_cast<uint32_t>(b);
-    wl = NextLimit(b, Wd, invW);
-    i = b + 1;
+    starts[nc++] = static_cast<uint32_t>(nb);
+    b = nb;
+  }
+  return nc;
+}
+
+// The same chain computed by one wave, ~10 steps per round instead of one: lane 0 evaluates
+// the step at the current boundary b; the k + 2 lanes of group k (k = 1..9) evaluate it at the
+// k + 2 integers just below the loss-free k-step prediction W * Q(L(b / W) + k) (+1 for
+// rounding), the window that holds the k-th next boundary, since each step's floor loses less
+// than one unit.  The round then follows the chain through the evaluated points (scalar
+// ballot + readlane per step) as far as it stays inside the windows.  Every boundary comes
+// from ChainNext at exactly the previous boundary, so the chain is bit-identical to
+// DigestBoundaries; the windows only decide how many steps a round advances.  Wave-uniform
+// control; `starts` written by the lanes holding the new boundaries.
+constexpr int kSpecGroups = 10;
+__device__ __forceinline__ void SpecLaneRole(int lane, int& k, int& d) {
+  k = 0;
+  d = 0;
+  if (lane == 0) return;
+  int base = 1;
+  k = 1;
+  while (lane >= base + k + 2) {
+    base += k + 2;
+    ++k;
+  }
+  d = lane - base;
+}
+
+template <bool kStats = false>
+__device__ __forceinline__ int64_t DigestBoundariesWave(int64_t W, uint32_t* starts, int64_t max_c, uint64_t* stats = nullptr) {
+  uint64_t st_eval = 0, st_res = 0, st_it = 0, st_exact = 0, t0 = 0, t1 = 0;
+  const int lane = threadIdx.x & 63;
+  if (W <= 0) return 0;
+  if (lane == 0) starts[0] = 0;
+  const double Wd = static_cast<double>(W);
+  const double invW = 1.0 / Wd;
+  const int32_t W32 = static_cast<int32_t>(W);
+  const int32_t Wu = __builtin_amdgcn_readfirstlane(W32);  // wave-uniform (scalar compares)
+  int k, d;
+  SpecLaneRole(lane, k, d);
+  const double ck = cos(static_cast<double>(k) * (kPi / kDelta));
+  const double sk = sin(static_cast<double>(k) * (kPi / kDelta));
+  int64_t nc = 1;
+  int32_t b = 0;
+  while (true) {
+    if (kStats) t0 = __builtin_readcyclecounter();
+    int32_t top = b;
+    if (k > 0) {
+      const double t = 2.0 * (static_cast<double>(b) * invW) - 1.0;
+      top = W32;
+      if (t <= ck) {  // else the k-step rotation passes the end of the scale
+        const double s = sqrt(fmax(0.0, (1.0 - t) * (1.0 + t)));
+        const double p = Wd * ((t * ck + s * sk + 1.0) * 0.5);
+        top = p >= Wd ? W32 : static_cast<int32_t>(floor(p)) + 1;
+      }
+      if (top < b + k) top = b + k;
+    }
+    const int32_t x = top - d;
+    const bool ok = x >= b + k && x < W32;
+    const int32_t fx = ok ? ChainNext(x, Wd, invW, W32) : -1;
+    if (kStats) {
+      const double tt = 2.0 * (static_cast<double>(x) * invW) - 1.0;
+      const double ss = sqrt(fmax(0.0, (1.0 - tt) * (1.0 + tt)));
+      const double wl = Wd * ((tt * 0.99999506519785548 + ss * 0.0031415874858795635 + 1.0) * 0.5);
+      const bool ex = ok && x > 0 && (tt >= 0.99999506519785548 - 1e-9 || fabs(wl - rint(wl)) < 1e-9 * fmax(1.0, wl));
+      st_exact += __ballot(ex) ? 1 : 0;
+      t1 = __builtin_readcyclecounter();
+      st_eval += t1 - t0;
+      ++st_it;
+    }
+    // Follow the chain with scalar arithmetic, branch-free: the next boundary after cur sits
+    // in group kk's window at offset top_kk - cur, i.e. in lane base_kk + top_kk - cur (a
+    // uniform index, so a plain readlane); the new boundaries are collected into lanes 0..
+    int32_t cur = b, mine = 0;
+    int cnt = 0;
+    bool live = true, done = false;
+    int base = 1;
+#pragma unroll
+    for (int kk = 0; kk < kSpecGroups; ++kk) {
+      int32_t nx;
+      if (kk == 0) {
+        nx = __builtin_amdgcn_readlane(fx, 0);
+      } else {
+        const int32_t off = __builtin_amdgcn_readlane(top, base) - cur;
+        const bool inwin = off >= 0 && off < kk + 2;
+        live = live && inwin;
+        nx = __builtin_amdgcn_readlane(fx, base + (inwin ? off : 0));
+        base += kk + 2;
+      }
+      const bool fin = live && nx >= Wu;
+      done = done || fin;
+      live = live && !fin;
+      if (live && lane == cnt) mine = nx;
+      cnt += live ? 1 : 0;
+      cur = live ? nx : cur;
+    }
+    if (nc + cnt > max_c) return -1;
+    if (lane < cnt) starts[nc + lane] = static_cast<uint32_t>(mine);
+    nc += cnt;
+    b = cur;
+    if (kStats) st_res += __builtin_readcyclecounter() - t1;
+    if (done) break;
+  }
+  if (kStats && (threadIdx.x & 63) == 0) {
+    stats[0] = st_eval;
+    stats[1] = st_res;
+    stats[2] = st_it;
+    stats[3] = st_exact;
   }
   return nc;
 }

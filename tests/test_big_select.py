@@ -1,0 +1,142 @@
+"""Big-group quantiles by selection (pxg_finalize.hip BigSample..BigSelDigest) against the full
+sort + merge path (PXG_BIG_SORT=1) and the CPU restatement, and the per-wave speculative
+boundary chain against the sequential one.  Bars: identical digests (bit-exact) for groups
+whose centroids all hold <= 16 values (W <= ~10000, incremental means in sorted order on both
+paths); 1e-12 relative above that (centroid sums in a different fixed order); groups the
+selection path cannot serve (NaN values, heavy duplicates) fall back to the sort path and are
+bit-exact again."""
+import ctypes as C
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_client as oc
+from device_runner import run_plan
+from kat import rows, ulp_diff
+from pixie_amd import _lib
+from pixie_amd import plans as P
+from pixie_amd.device import Column
+
+pytestmark = pytest.mark.gpu
+NAMES = ["p01", "p10", "p25", "p50", "p75", "p90", "p99"]
+QS = [0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99]
+
+
+def _chains(ctx, ws, wave, cap=2048):
+    import torch
+    w = torch.tensor(ws, dtype=torch.int64, device="cuda")
+    starts = torch.zeros(len(ws) * cap, dtype=torch.int32, device="cuda")
+    nc = torch.zeros(len(ws), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    _lib.check(_lib.load().pxg_digest_chains(ctx.h, C.c_void_p(w.data_ptr()), len(ws), wave, C.c_void_p(starts.data_ptr()), cap,
+                                             C.c_void_p(nc.data_ptr())))
+    return starts.view(len(ws), cap).cpu().numpy(), nc.cpu().numpy()
+
+
+def test_speculative_chain_matches_sequential(ctx):
+    rng = np.random.default_rng(3)
+    ws = list(range(1, 4200)) + list(range(7900, 10300, 7)) + [int(x) for x in rng.integers(10_000, 3_000_000, 400)] + \
+        [2**20, 2**24 - 1, 123_456_789]
+    s_seq, n_seq = _chains(ctx, ws, 0)
+    s_wave, n_wave = _chains(ctx, ws, 1)
+    assert (n_seq == n_wave).all(), [(w, a, b) for w, a, b in zip(ws, n_seq, n_wave) if a != b][:5]
+    for i, n in enumerate(n_seq):
+        if n > 0:
+            assert (s_seq[i, :n] == s_wave[i, :n]).all(), ws[i]
+    # a chain longer than its capacity reports -1 on both builders
+    s1, n1 = _chains(ctx, [5000, 50_000], 1, cap=64)
+    s0, n0 = _chains(ctx, [5000, 50_000], 0, cap=64)
+    assert list(n1) == list(n0) == [-1, -1]
+
+
+def _groups(fallback):
+    rng = np.random.default_rng(11)
+    spec = [
+        ("u4097", rng.uniform(0, 1, 4097)),
+        ("l5000", rng.lognormal(2.0, 1.3, 5000)),
+        ("n8000", rng.normal(-3, 2, 8000)),
+        ("l9999", rng.lognormal(0.5, 0.7, 9999)),
+        ("l12000", rng.lognormal(3.0, 0.9, 12_000)),
+        ("n40000", rng.normal(0, 1e6, 40_000)),
+        ("l250000", rng.lognormal(1.6, 1.0, 250_000)),
+        ("grid", np.round(rng.lognormal(4, 1, 90_000), 1)),     # many ties
+        ("m2000", rng.normal(0, 1, 2000)),
+        ("t10", rng.normal(0, 1, 10)),
+    ]
+    if fallback == "dup":
+        spec.append(("dup", np.full(20_000, 7.25)))                          # one value
+        spec.append(("few", rng.integers(0, 4, 30_000).astype(np.float64)))  # four values
+    elif fallback == "nan":
+        spec.append(("nan", np.where(rng.uniform(size=6000) < 0.01, np.nan, rng.normal(5, 1, 6000))))
+    keys, vals = [], []
+    for k, v in spec:
+        keys += [k] * len(v)
+        vals.append(v)
+    vals = np.concatenate(vals)
+    perm = rng.permutation(len(keys))
+    return [keys[i] for i in perm], vals[perm], {k: len(v) for k, v in spec}
+
+
+def _run(ctx, keys, vals, force_sort):
+    plan = P.linear_plan([P.source_op("t", [5, 4], ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("quantiles", [P.col(1)], [4]), P.agg_expr("count", [P.col(1)], [4], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": [5, 4], "batches": [[Column.from_values(5, keys), Column(4, values=vals)]]}}
+    old = os.environ.get("PXG_BIG_SORT")
+    if force_sort:
+        os.environ["PXG_BIG_SORT"] = "1"
+    else:
+        os.environ.pop("PXG_BIG_SORT", None)
+    try:
+        out = run_plan(ctx, plan, tables)
+    finally:
+        if old is None:
+            os.environ.pop("PXG_BIG_SORT", None)
+        else:
+            os.environ["PXG_BIG_SORT"] = old
+    return plan, tables, {r[0]: (json.loads(r[1]), r[2]) for r in rows(out[0]["cols"])}
+
+
+@pytest.mark.parametrize("fallback", [None, "dup", "nan"])
+def test_selection_path_matches_sort_path(ctx, fallback):
+    """Without fallback groups the two paths differ only in big-centroid summation order; with
+    one (duplicates beyond a bin's capacity, NaN values) finalize hands every big group to the
+    sort path, so all results are identical."""
+    keys, vals, sizes = _groups(fallback)
+    _, _, sel = _run(ctx, keys, vals, force_sort=False)
+    _, _, srt = _run(ctx, keys, vals, force_sort=True)
+    assert set(sel) == set(srt) == set(sizes)
+    for k, n in sizes.items():
+        qa, ca = sel[k]
+        qb, cb = srt[k]
+        assert ca == cb == n
+        for name in NAMES:
+            a, b = qa[name], qb[name]
+            if n <= 10_000 or fallback:
+                assert a == b or (a != a and b != b), (k, name, a, b)
+            else:
+                assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
+
+
+def test_selection_path_against_restatement(ctx):
+    keys, vals, sizes = _groups(None)
+    plan, tables, dev = _run(ctx, keys, vals, force_sort=False)
+    ref = {r[0]: (json.loads(r[1]), r[2]) for r in rows(oc.execute_plan(plan, tables)["out"][0]["cols"])}
+    karr = np.array(keys, dtype=object)
+    for k, n in sizes.items():
+        rq, dq = ref[k][0], dev[k][0]
+        assert ref[k][1] == dev[k][1] == n
+        if n <= 8000:
+            for name in NAMES:
+                assert (rq[name] != rq[name] and dq[name] != dq[name]) or ulp_diff(rq[name], dq[name]) <= 4, (k, name, rq[name], dq[name])
+        else:
+            s = np.sort(vals[karr == k])
+            s = s[~np.isnan(s)]
+            for q, name in zip(QS, NAMES):
+                bound = 2 * math.pi * math.sqrt(q * (1 - q)) / 1000 + 1 / len(s)
+                r_dev = (np.searchsorted(s, dq[name], "left") + np.searchsorted(s, dq[name], "right")) / 2 / len(s)
+                r_ref = (np.searchsorted(s, rq[name], "left") + np.searchsorted(s, rq[name], "right")) / 2 / len(s)
+                assert abs(r_dev - r_ref) <= bound, (k, name, dq[name], rq[name])
