@@ -191,11 +191,17 @@ def main():
         engine.execute_raw(pb)
         ctx.sync()
         reps = max(3, min(args.steps, 10))
-        te = time.perf_counter()
+        times = []
         for _ in range(reps):
+            tq = time.perf_counter()
             res = engine.execute_raw(pb)
-        te = time.perf_counter() - te
-        engine_query = {"ms_per_query": te * 1000.0 / reps, "rows_per_s": n * reps / te, "queries": reps,
+            times.append(time.perf_counter() - tq)
+        te = sum(times)
+        st = sorted(times)
+        # Per-query spread: some boxes stall an occasional query start by 10-30 ms while every
+        # kernel's own time is unchanged, so the median is reported beside the mean.
+        engine_query = {"ms_per_query": te * 1000.0 / reps, "ms_median": st[len(st) // 2] * 1000.0,
+                        "ms_min": st[0] * 1000.0, "ms_max": st[-1] * 1000.0, "rows_per_s": n * reps / te, "queries": reps,
                         "result_bytes": len(res),
                         "path": "pxc_execute_plan (C++ engine, include/pxcarnot.h) over the HBM-resident stored table: "
                                 "fused consume + finalize + result D2H + quantiles JSON + pluck_float64 + PXRB"}

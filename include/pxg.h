@@ -215,7 +215,10 @@ int32_t pxg_table_time_bound(pxg_table* t, int32_t col, int64_t value, int32_t s
  * Filter and Map over a device table (non-fused operator shapes).
  * ------------------------------------------------------------------------------------- */
 /* FilterNode: evaluates pred over rows [begin,end) and writes the selected columns (in
- * `select` order) of the passing rows, order preserved, into a new device table. */
+ * `select` order) of the passing rows, order preserved, into a new device table.  Row counts
+ * and sizes are known to the host on return; the column contents are written in order on the
+ * ctx stream (device consumers need no sync; pxg_table_fetch synchronises).  Output columns
+ * come from the ctx's buffer pool, which pxg_table_destroy refills. */
 int32_t pxg_filter(pxg_table* in, const pxg_program* pred, int32_t n_select,
                    const int32_t* select, int64_t begin, int64_t end, pxg_table** out);
 /* pxg_filter over rows that are the concatenation of n_splits RowBatches (split_rows[i] rows
@@ -226,7 +229,7 @@ int32_t pxg_filter_split(pxg_table* in, const pxg_program* pred, int32_t n_selec
                          const int32_t* select, int64_t begin, int64_t end, int32_t n_splits,
                          const int64_t* split_rows, int64_t* out_split_rows, pxg_table** out);
 /* MapNode: one output column per program (fixed-width results; a program that is a single
- * column reference of any type is passed through). */
+ * column reference of any type is passed through).  Same completion rule as pxg_filter. */
 int32_t pxg_map(pxg_table* in, int32_t n_exprs, const pxg_program* exprs, int64_t begin,
                 int64_t end, pxg_table** out);
 

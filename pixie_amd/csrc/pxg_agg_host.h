@@ -87,7 +87,7 @@ struct Agg {
     DevBuf keysA, keysB, bstarts, big, bchunks;
     DevBuf chain_list, chain_nc, chain_starts;
     // big groups by selection (pxg_finalize.hip)
-    DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial;
+    DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list;
     RadixPassWs rs;
   } ws;
 

@@ -1239,7 +1239,8 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
                                                      const uint32_t* __restrict__ hist, const uint32_t* __restrict__ nan_cnt,
                                                      uint32_t* __restrict__ bstart_all, uint8_t* __restrict__ tag_all,
                                                      uint32_t* __restrict__ cbase_all, BigPlan* __restrict__ plans,
-                                                     unsigned int* __restrict__ n_fallback) {
+                                                     unsigned int* __restrict__ n_fallback, uint32_t* __restrict__ bin_lists,
+                                                     uint32_t list_cap, uint32_t* __restrict__ list_cnt) {
   if (blockIdx.x >= *nbig_p) return;
   __shared__ uint32_t bs[kSelBins + 1];
   __shared__ uint8_t tg[kSelBins];
@@ -1334,12 +1335,9 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
   for (int u = 0; u < P.n_ranges; ++u) {
     const uint32_t b0 = P.rbs[u], b1 = P.rbe[u];
     const bool small = P.re[u] - P.rs[u] <= static_cast<uint32_t>(kSeqMean);
-    for (uint32_t b = b0 + t; b <= b1; b += 256) {
-      if (small || b == b0 || b == b1) tg[b] = kTagColl;
-      else if (tg[b] == 0) tg[b] = static_cast<uint8_t>(u + 1);
-    }
-    __syncthreads();
+    for (uint32_t b = b0 + t; b <= b1; b += 256) tg[b] = (small || b == b0 || b == b1) ? kTagColl : static_cast<uint8_t>(u + 1);
   }
+  __syncthreads();
   // Gathered bins in ascending order and their offsets (relative to the group) in the
   // candidate buffer.
   uint32_t nf = 0, nv = 0;
@@ -1389,6 +1387,24 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
     P.fallback = 1;
     atomicAdd(n_fallback, 1u);
   }
+  // The gathered bins join the global sort lists (<= kWaveSortMax values: list 0, one wave
+  // each; larger: list 1, one workgroup each), entries (group << 11) | bin.
+  __shared__ uint32_t s_lc[2], s_lb[2];
+  if (t < 2) s_lc[t] = 0;
+  __syncthreads();
+  const bool listed = !s_fb && t < P.n_coll;
+  uint32_t my_list = 0, my_pos = 0, my_entry = 0;
+  if (listed) {
+    const int b = P.coll[t];
+    my_list = H[b] > static_cast<uint32_t>(kWaveSortMax) ? 1u : 0u;
+    my_pos = atomicAdd(&s_lc[my_list], 1u);
+    my_entry = (bi << 11) | static_cast<uint32_t>(b);
+  }
+  __syncthreads();
+  if (t < 2 && s_lc[t]) s_lb[t] = atomicAdd(&list_cnt[t], s_lc[t]);
+  __syncthreads();
+  if (listed && H[P.coll[t]] > 1) bin_lists[my_list * list_cap + s_lb[my_list] + my_pos] = my_entry;
+  else if (listed) bin_lists[my_list * list_cap + s_lb[my_list] + my_pos] = 0xFFFFFFFFu;  // nothing to sort
   uint32_t* bso = bstart_all + static_cast<uint64_t>(bi) * (kSelBins + 1);
   uint8_t* tgo = tag_all + static_cast<uint64_t>(bi) * kSelBins;
   for (int b = t; b <= kSelBins; b += 256) bso[b] = bs[b];
@@ -1465,47 +1481,54 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
     partial[static_cast<uint64_t>(blockIdx.x) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
 }
 
-// Sort the gathered bins of the big groups (blockIdx.y = big group): bins of <= 1024 values
-// one per wave (BigBinSortKernel, blockIdx.x * 4 + wave = index in the plan's list), larger
-// ones one per workgroup (BigBinSortLargeKernel, blockIdx.x = index).
-__global__ void __launch_bounds__(256) BigBinSortKernel(const BigGroup* __restrict__ groups, const BigPlan* __restrict__ plans,
-                                                        const uint32_t* __restrict__ hist, const uint32_t* __restrict__ cbase_all,
-                                                        uint64_t* __restrict__ cand) {
+// Sort the gathered bins of the big groups, grid-stride over the lists BigPlan filled: bins
+// of <= 1024 values one per wave (BigBinSortKernel), larger ones one per workgroup
+// (BigBinSortLargeKernel).
+__device__ __forceinline__ uint64_t* BinOfEntry(uint32_t e, const BigGroup* __restrict__ groups, const uint32_t* __restrict__ hist,
+                                                 const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand, int* n) {
+  const uint32_t bi = e >> 11, b = e & 2047u;
+  *n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
+  return cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
+}
+__global__ void __launch_bounds__(256) BigBinSortKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ list_cnt, const uint32_t* __restrict__ hist,
+                                                        const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand) {
   __shared__ uint64_t keys[4][PaddedLen(kWaveSortMax)];
-  const uint32_t bi = blockIdx.y;
-  const BigPlan* P = plans + bi;
-  const int ci = static_cast<int>(blockIdx.x) * 4 + static_cast<int>(threadIdx.x >> 6);
-  if (P->fallback || ci >= P->n_coll) return;
-  const int b = P->coll[ci];
-  const int n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
-  if (n <= 1 || n > kWaveSortMax) return;
+  const uint32_t cnt = *list_cnt;
   const int lane = threadIdx.x & 63;
   uint64_t* s = keys[threadIdx.x >> 6];
-  uint64_t* a = cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
-  int Pn = kMsIpt;
-  while (Pn < n) Pn <<= 1;
-  for (int i = lane; i < Pn; i += 64) s[PadIdx(i)] = i < n ? a[i] : ~0ULL;
-  WaveSync();
-  WaveMergeSortLds(s, Pn);
-  for (int i = lane; i < n; i += 64) a[i] = s[PadIdx(i)];
+  for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < cnt; j += gridDim.x * 4) {
+    const uint32_t e = list[j];
+    if (e == 0xFFFFFFFFu) continue;
+    int n;
+    uint64_t* a = BinOfEntry(e, groups, hist, cbase_all, cand, &n);
+    int Pn = kMsIpt;
+    while (Pn < n) Pn <<= 1;
+    for (int i = lane; i < Pn; i += 64) s[PadIdx(i)] = i < n ? a[i] : ~0ULL;
+    WaveSync();
+    WaveMergeSortLds(s, Pn);
+    for (int i = lane; i < n; i += 64) a[i] = s[PadIdx(i)];
+    WaveSync();
+  }
 }
-__global__ void __launch_bounds__(256) BigBinSortLargeKernel(const BigGroup* __restrict__ groups, const BigPlan* __restrict__ plans,
-                                                             const uint32_t* __restrict__ hist, const uint32_t* __restrict__ cbase_all,
-                                                             uint64_t* __restrict__ cand) {
-  const uint32_t bi = blockIdx.y;
-  const BigPlan* P = plans + bi;
-  if (P->fallback || static_cast<int>(blockIdx.x) >= P->n_coll) return;
-  const int b = P->coll[blockIdx.x];
-  const int n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
-  if (n <= kWaveSortMax) return;
+__global__ void __launch_bounds__(256) BigBinSortLargeKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ list,
+                                                             const uint32_t* __restrict__ list_cnt, const uint32_t* __restrict__ hist,
+                                                             const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand) {
   __shared__ uint64_t keys[PaddedLen(kMidMax)];
-  uint64_t* a = cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
-  int Pn = kMsIpt;
-  while (Pn < n) Pn <<= 1;
-  for (int i = threadIdx.x; i < Pn; i += blockDim.x) keys[PadIdx(i)] = i < n ? a[i] : ~0ULL;
-  __syncthreads();
-  BlockMergeSortLds(keys, Pn);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = keys[PadIdx(i)];
+  const uint32_t cnt = *list_cnt;
+  for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
+    const uint32_t e = list[j];
+    if (e == 0xFFFFFFFFu) continue;
+    int n;
+    uint64_t* a = BinOfEntry(e, groups, hist, cbase_all, cand, &n);
+    int Pn = kMsIpt;
+    while (Pn < n) Pn <<= 1;
+    for (int i = threadIdx.x; i < Pn; i += blockDim.x) keys[PadIdx(i)] = i < n ? a[i] : ~0ULL;
+    __syncthreads();
+    BlockMergeSortLds(keys, Pn);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = keys[PadIdx(i)];
+    __syncthreads();
+  }
 }
 
 // Centroid means and the seven quantiles of every big group served by the selection path.
@@ -1868,7 +1891,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     const uint64_t* vals = cv.p[a->uda_val[u]];
     const int at = a->uda_arg_type[u];
     const uint64_t nb = n_big_groups;
-    PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4, ctx->side2));
+    PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4 + 16, ctx->side2));
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel, dim3(n_big_groups), dim3(256), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), vals, at, ws.sel_spl.as<uint64_t>()));
     return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3(n_bchunks), dim3(256), 0, ws.bchunks.as<const BigChunk>(),
@@ -1883,19 +1906,26 @@ int32_t AggFinalizeImpl(Agg* a) {
     uint32_t* hist = ws.sel_cnt.as<uint32_t>();
     uint32_t* cursor = hist + nb * kSelBins;
     uint32_t* nan_cnt = hist + 2 * nb * kSelBins;
+    uint32_t* list_cnt = nan_cnt + nb;
+    const uint32_t list_cap = static_cast<uint32_t>(nb * kSelMaxColl);
+    uint32_t* lists = ws.sel_list.as<uint32_t>();
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_plan", BigPlanKernel, dim3(n_big_groups), dim3(256), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), chain_starts_big, chain_nc_big,
                                  static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), ws.sel_bstart.as<uint32_t>(),
-                                 ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback));
+                                 ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback, lists,
+                                 list_cap, list_cnt));
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3(n_bchunks), dim3(256), 0,
                                  ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
                                  vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_tag.as<const uint8_t>(),
                                  ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>()));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel, dim3(kSelMaxColl / 4, n_big_groups), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), ws.sel_plan.as<const BigPlan>(), static_cast<const uint32_t*>(hist),
-                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortLargeKernel, dim3(kSelMaxColl, n_big_groups), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), ws.sel_plan.as<const BigPlan>(), static_cast<const uint32_t*>(hist),
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel,
+                                 dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists), static_cast<const uint32_t*>(list_cnt),
+                                 static_cast<const uint32_t*>(hist), ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortLargeKernel,
+                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(256), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists + list_cap),
+                                 static_cast<const uint32_t*>(list_cnt + 1), static_cast<const uint32_t*>(hist),
                                  ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
     return LaunchOn(ctx, ctx->side2, "quant_sel_digest", BigSelDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
                     static_cast<const uint32_t*>(d_cls + 3), ws.sel_plan.as<const BigPlan>(), chain_starts_big,
@@ -1977,6 +2007,7 @@ int32_t AggFinalizeImpl(Agg* a) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8));
       PXG_RETURN_IF_ERROR(ws.sel_cnt.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * 4 + 16));
+      PXG_RETURN_IF_ERROR(ws.sel_list.Ensure(static_cast<size_t>(n_big) * kSelMaxColl * 2 * 4 + 16));
       PXG_RETURN_IF_ERROR(ws.sel_bstart.Ensure(static_cast<size_t>(n_big) * (kSelBins + 1) * 4));
       PXG_RETURN_IF_ERROR(ws.sel_tag.Ensure(static_cast<size_t>(n_big) * kSelBins));
       PXG_RETURN_IF_ERROR(ws.sel_cbase.Ensure(static_cast<size_t>(n_big) * kSelBins * 4));

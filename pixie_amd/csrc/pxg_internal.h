@@ -122,12 +122,23 @@ struct PendingTiming {
 
 // Grow-only workspace of the standalone Filter / Map operators (pxg_ops.hip).
 struct OpsWorkspace {
-  DevBuf prog, masks, tiles, scan, scan2;
+  DevBuf prog, masks, tiles, scan, scan2, gsrc;
+};
+
+// Per-context cache of device buffers released by destroyed operator output tables, so the
+// standalone Filter / Map do not hipMalloc (and their tables' destruction does not hipFree,
+// which synchronises the device) on every call.  Reuse is ordered by the ctx stream: every
+// kernel that reads a released buffer was issued on that stream before the next user's.
+struct BufPool {
+  std::multimap<size_t, void*> free;
+  size_t cached = 0;
+  size_t cap = size_t(16) << 30;
 };
 
 struct Ctx {
   int device = 0;
   OpsWorkspace ops;
+  BufPool pool;
   hipStream_t stream = nullptr;
   // Side stream for latency-bound work that overlaps the main stream (fork/join by events).
   hipStream_t side = nullptr;
@@ -144,12 +155,20 @@ struct Ctx {
   std::vector<hipEvent_t> free_events;
   int num_cus = 256;
   // Pinned scratch for counters read back by the host (async D2H, no staging copy):
-  // [0, 64) consume publish, [64, 128) finalize class counts, [128, 256) finalize totals.
+  // [0, 64) consume publish, [64, 128) finalize class counts, [128, 256) finalize totals,
+  // [kPinnedOps, kPinnedBytes) standalone Filter / Map per-chunk counts.
   void* pinned = nullptr;
+  static constexpr size_t kPinnedOps = 4096, kPinnedBytes = 65536;
 
   hipEvent_t GetEvent();
   int32_t ResolveTimings();
 };
+
+// Buffer pool (BufPool): a cached buffer of at least `bytes` (and at most twice that), else a
+// new one; Release hands a DevBuf's memory to the pool (b is left empty).
+int32_t PoolAlloc(Ctx* ctx, DevBuf& b, size_t bytes);
+void PoolRelease(Ctx* ctx, DevBuf& b);
+void PoolClear(Ctx* ctx);
 
 // Opt-in host-side stage timing of the library (PXG_TIMING=1): one stderr line per stage.
 struct HostClock {

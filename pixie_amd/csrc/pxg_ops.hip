@@ -14,9 +14,10 @@
 // MapNode::ConsumeNextImpl (map_node.cc:64-71): one output column per expression; column
 // references pass through (device-to-device copies).
 //
-// No per-call hipMalloc of workspace and no synchronous program upload: programs, ballot words,
-// tile counts and scan scratch live in the ctx's grow-only ops workspace; a call synchronises
-// once per chunk for the output sizes it must allocate.
+// No per-call hipMalloc: programs, ballot words, tile counts, scan scratch and string source
+// rows live in the ctx's grow-only ops workspace, output columns come from the ctx buffer pool
+// (refilled by pxg_table_destroy).  A filter synchronises twice per call whatever the chunk
+// count (selected counts; string payload sizes), a map once (passed-through string extents).
 #include <algorithm>
 
 #include "pxg_internal.h"
@@ -64,13 +65,39 @@ __global__ void __launch_bounds__(kOpsBlock) FilterMaskKernel(const DevProgram* 
   const DevChunk& ch = chunks[chunk];
   const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * kOpsTileRows;
   uint32_t cnt = 0;
-  for (int k = 0; k < kOpsMasksPerWave; ++k) {
-    const int64_t r = tile0 + (static_cast<int64_t>(wid) * kOpsMasksPerWave + k) * 64 + lane;
-    const bool pass = r < n && EvalProgram(prog, ch, lo + r, types).a != 0;
-    const unsigned long long m = __ballot(pass);
-    cnt += static_cast<uint32_t>(__popcll(m));
-    const int64_t mi = static_cast<int64_t>(blockIdx.x) * kOpsMasksPerTile + wid * kOpsMasksPerWave + k;
-    if (lane == 0) masks[mi] = m;
+  if (prog->shape == kShapeCol || prog->shape == kShapeColOpConst) {
+    // Fast shapes (col, col op const over a fixed-width column): the wave's 16 loads are issued
+    // together, then evaluated.
+    const DevCol& col = ch.cols[prog->col];
+    const int ty = types[prog->col];
+    uint64_t raw[kOpsMasksPerWave];
+#pragma unroll
+    for (int k = 0; k < kOpsMasksPerWave; ++k) {
+      const int64_t r = tile0 + (static_cast<int64_t>(wid) * kOpsMasksPerWave + k) * 64 + lane;
+      raw[k] = r < n ? LoadCol(col, ty, lo + r).a : 0ULL;
+    }
+#pragma unroll
+    for (int k = 0; k < kOpsMasksPerWave; ++k) {
+      const int64_t r = tile0 + (static_cast<int64_t>(wid) * kOpsMasksPerWave + k) * 64 + lane;
+      uint64_t v = raw[k];
+      if (prog->shape == kShapeColOpConst) {
+        if (prog->conv) v = Conv(prog->conv, v);
+        v = BinOp(prog->binop, v, static_cast<uint64_t>(prog->cimm));
+      }
+      const unsigned long long m = __ballot(r < n && v != 0);
+      cnt += static_cast<uint32_t>(__popcll(m));
+      const int64_t mi = static_cast<int64_t>(blockIdx.x) * kOpsMasksPerTile + wid * kOpsMasksPerWave + k;
+      if (lane == 0) masks[mi] = m;
+    }
+  } else {
+    for (int k = 0; k < kOpsMasksPerWave; ++k) {
+      const int64_t r = tile0 + (static_cast<int64_t>(wid) * kOpsMasksPerWave + k) * 64 + lane;
+      const bool pass = r < n && EvalProgram(prog, ch, lo + r, types).a != 0;
+      const unsigned long long m = __ballot(pass);
+      cnt += static_cast<uint32_t>(__popcll(m));
+      const int64_t mi = static_cast<int64_t>(blockIdx.x) * kOpsMasksPerTile + wid * kOpsMasksPerWave + k;
+      if (lane == 0) masks[mi] = m;
+    }
   }
   if (lane == 0) s_cnt[wid] = cnt;
   __syncthreads();
@@ -165,14 +192,11 @@ __global__ void RebaseKernel(int32_t* __restrict__ dst, const int32_t* __restric
   if (i < n) dst[i] = src[i] - src[0];
 }
 
-static int32_t ReadU32(Ctx* ctx, const void* p, uint32_t* out) {
-  PXG_HIP(hipMemcpyAsync(out, p, 4, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
-  return PXG_OK;
-}
-
 // Filter rows [begin, end) of t into a new table; per_split (optional) receives the selected
-// rows of each of n_splits consecutive input row ranges (split_rows[i] rows each).
+// rows of each of n_splits consecutive input row ranges (split_rows[i] rows each).  Three
+// phases over all chunks at once, so a call synchronises twice (selected counts; string
+// payload sizes) however many chunks the table has: masks + tile scans, then the gathers and
+// string length scans, then the payload copies.  Output columns come from the ctx pool.
 static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, const int32_t* select, int64_t begin, int64_t end,
                           int32_t n_splits, const int64_t* split_rows, int64_t* per_split, pxg_table** out) {
   Ctx* ctx = t.ctx;
@@ -180,15 +204,45 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
   if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
   if (pred.result_type != PXG_BOOLEAN) return SetError(PXG_INVALID_ARGUMENT, "Predicate expression must be a boolean");
   std::vector<int32_t> otypes;
+  int n_str = 0;
   for (int i = 0; i < n_select; ++i) {
     if (select[i] < 0 || select[i] >= t.ncols) return SetError(PXG_INVALID_ARGUMENT, "selected column %d out of range", select[i]);
     otypes.push_back(t.types[select[i]]);
+    n_str += t.types[select[i]] == PXG_STRING ? 1 : 0;
   }
   if (n_splits > 0) {
     int64_t tot = 0;
     for (int i = 0; i < n_splits; ++i) tot += split_rows[i];
     if (tot != end - begin) return SetError(PXG_INVALID_ARGUMENT, "split rows add up to %lld, range has %lld", (long long)tot, (long long)(end - begin));
   }
+  struct Part {
+    size_t c;
+    int64_t lo, n, ntiles, mask0, tile0;
+    uint32_t m = 0;
+    uint64_t gsrc0 = 0;  // per string column: m source rows at gsrc0 + s_str * m
+  };
+  std::vector<Part> parts;
+  int64_t nmasks = 0, ntile_words = 0;
+  for (size_t c = 0; c < t.chunks.size(); ++c) {
+    const Chunk& ch = *t.chunks[c];
+    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
+    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
+    if (lo >= hi) continue;
+    Part p;
+    p.c = c;
+    p.lo = lo;
+    p.n = hi - lo;
+    p.ntiles = (p.n + kOpsTileRows - 1) / kOpsTileRows;
+    p.mask0 = nmasks;
+    p.tile0 = ntile_words;
+    nmasks += p.ntiles * kOpsMasksPerTile;
+    ntile_words += p.ntiles + 1;
+    parts.push_back(p);
+  }
+  const size_t pin_cap = (Ctx::kPinnedBytes - Ctx::kPinnedOps) / 4;
+  if (parts.size() * static_cast<size_t>(std::max(n_str, 1)) > pin_cap)
+    return SetError(PXG_UNIMPLEMENTED, "filter over %zu chunks", parts.size());
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps);
   const DevProgram* d_prog = nullptr;
   const int32_t* d_types = nullptr;
   PXG_RETURN_IF_ERROR(UploadPrograms(ctx, &pred, 1, t, &d_prog, &d_types));
@@ -197,40 +251,46 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
   std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(ot, pxg_table_destroy);
   Table& o = ot->impl;
   OpsWorkspace& w = ctx->ops;
+  int64_t max_tiles = 1;
+  for (const Part& p : parts) max_tiles = std::max(max_tiles, p.ntiles);
+  PXG_RETURN_IF_ERROR(w.masks.Ensure(static_cast<size_t>(nmasks) * 8 + 64));
+  PXG_RETURN_IF_ERROR(w.tiles.Ensure(static_cast<size_t>(ntile_words) * 4 + 64));
+  PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(max_tiles + 1) + 64));
+  // Phase A: ballot words, tile counts -> tile bases and the chunk's selected count.
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const Part& p = parts[i];
+    uint32_t* tiles = w.tiles.as<uint32_t>() + p.tile0;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_mask", FilterMaskKernel, dim3(static_cast<unsigned>(p.ntiles)), dim3(kOpsBlock), 0, d_prog,
+                               t.d_chunks.as<const DevChunk>(), static_cast<int>(p.c), d_types, p.lo, p.n,
+                               w.masks.as<unsigned long long>() + p.mask0, tiles));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, tiles, tiles, p.ntiles, tiles + p.ntiles, w.scan.p));
+    PXG_HIP(hipMemcpyAsync(pin + i, tiles + p.ntiles, 4, hipMemcpyDeviceToHost, ctx->stream));
+  }
   std::vector<unsigned long long> host_masks;
-  for (size_t c = 0; c < t.chunks.size(); ++c) {
-    const Chunk& ch = *t.chunks[c];
-    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
-    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
-    if (lo >= hi) continue;
-    const int64_t n = hi - lo;
-    const int64_t ntiles = (n + kOpsTileRows - 1) / kOpsTileRows;
-    const int64_t nmasks = ntiles * kOpsMasksPerTile;
-    PXG_RETURN_IF_ERROR(w.masks.Ensure(static_cast<size_t>(nmasks) * 8 + 64));
-    PXG_RETURN_IF_ERROR(w.tiles.Ensure(static_cast<size_t>(ntiles + 1) * 4 + 64));
-    PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(ntiles + 1) + 64));
-    uint32_t* tiles = w.tiles.as<uint32_t>();
-    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_mask", FilterMaskKernel, dim3(static_cast<unsigned>(ntiles)), dim3(kOpsBlock), 0, d_prog,
-                               t.d_chunks.as<const DevChunk>(), static_cast<int>(c), d_types, lo, n,
-                               w.masks.as<unsigned long long>(), tiles));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, tiles, tiles, ntiles, tiles + ntiles, w.scan.p));
-    uint32_t m = 0;
-    if (n_splits > 0) {  // ballot words back to the host: per-split counts by popcount
-      host_masks.resize(static_cast<size_t>(nmasks));
-      PXG_HIP(hipMemcpyAsync(host_masks.data(), w.masks.p, static_cast<size_t>(nmasks) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    PXG_RETURN_IF_ERROR(ReadU32(ctx, tiles + ntiles, &m));
-    if (n_splits > 0) {
+  if (n_splits > 0) {  // ballot words back to the host: per-split counts by popcount
+    host_masks.resize(static_cast<size_t>(nmasks));
+    PXG_HIP(hipMemcpyAsync(host_masks.data(), w.masks.p, static_cast<size_t>(nmasks) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  uint64_t gsrc_words = 0;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    parts[i].m = pin[i];
+    parts[i].gsrc0 = gsrc_words;
+    gsrc_words += static_cast<uint64_t>(parts[i].m) * n_str;
+  }
+  if (n_splits > 0) {
+    for (const Part& p : parts) {
+      const Chunk& ch = *t.chunks[p.c];
       // split i covers input rows [s0, s1) of [begin, end); this chunk covers [cb, cb + n)
-      const int64_t cb = ch.row_base + lo - begin;
+      const int64_t cb = ch.row_base + p.lo - begin;
       int64_t s0 = 0;
       for (int i = 0; i < n_splits; ++i) {
         const int64_t s1 = s0 + split_rows[i];
-        const int64_t a = std::max(s0, cb) - cb, b = std::min(s1, cb + n) - cb;
+        const int64_t a = std::max(s0, cb) - cb, b = std::min(s1, cb + p.n) - cb;
         for (int64_t r = a; r < b;) {
           const int64_t wi = r >> 6;
           const int64_t e = std::min(b, (wi + 1) << 6);
-          unsigned long long mk = host_masks[static_cast<size_t>(wi)] >> (r & 63);
+          unsigned long long mk = host_masks[static_cast<size_t>(p.mask0 + wi)] >> (r & 63);
           const int64_t bits = e - r;
           if (bits < 64) mk &= (1ULL << bits) - 1;
           per_split[i] += __builtin_popcountll(mk);
@@ -239,16 +299,24 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
         s0 = s1;
       }
     }
+  }
+  // Phase B: output chunks, the gathers, string lengths -> offsets.
+  PXG_RETURN_IF_ERROR(w.gsrc.Ensure(gsrc_words * 4 + 64));
+  std::vector<GatherCols> gcs(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const Part& p = parts[i];
+    const Chunk& ch = *t.chunks[p.c];
+    const uint32_t m = p.m;
     auto oc = std::make_unique<Chunk>();
     oc->row_base = o.nrows;
     oc->nrows = m;
     oc->rows_cap = m;
     oc->sealed = true;
     oc->cols.resize(static_cast<size_t>(n_select));
-    GatherCols gc;
+    GatherCols& gc = gcs[i];
     std::memset(&gc, 0, sizeof(gc));
     gc.n = n_select;
-    std::vector<DevBuf> lens(static_cast<size_t>(n_select)), srcs(static_cast<size_t>(n_select));
+    int si = 0;
     for (int s = 0; s < n_select; ++s) {
       const int ci = select[s];
       const int ty = t.types[ci];
@@ -256,52 +324,60 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
       if (ty != PXG_STRING) {
         const int wd = TypeWidth(ty);
         gc.width[s] = wd;
-        PXG_RETURN_IF_ERROR(dc.values.Alloc(static_cast<size_t>(m) * wd + 16));
+        PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.values, static_cast<size_t>(m) * wd + 16));
         gc.src[s] = ch.cols[ci].values.as<const uint8_t>();
         gc.dst[s] = dc.values.as<uint8_t>();
       } else {
         gc.width[s] = 0;
-        PXG_RETURN_IF_ERROR(dc.offsets.Alloc((static_cast<size_t>(m) + 1) * 4 + 16));
-        PXG_RETURN_IF_ERROR(srcs[s].Alloc(static_cast<size_t>(m) * 4 + 16));
+        PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.offsets, (static_cast<size_t>(m) + 1) * 4 + 16));
         gc.src_off[s] = ch.cols[ci].offsets.as<const int32_t>();
         gc.dst_len[s] = dc.offsets.as<uint32_t>();
-        gc.dst_src[s] = srcs[s].as<uint32_t>();
+        gc.dst_src[s] = w.gsrc.as<uint32_t>() + p.gsrc0 + static_cast<uint64_t>(si) * m;
+        ++si;
       }
     }
     if (m > 0 && n_select > 0)
-      PXG_RETURN_IF_ERROR(Launch(ctx, "filter_gather", FilterGatherKernel, dim3(static_cast<unsigned>(ntiles)), dim3(kOpsBlock), 0,
-                                 static_cast<const unsigned long long*>(w.masks.as<unsigned long long>()),
-                                 static_cast<const uint32_t*>(tiles), lo, n, gc));
-    // STRING columns: lengths -> offsets (one scan each), one sync for every payload size.
-    std::vector<uint32_t> bytes(static_cast<size_t>(n_select), 0);
-    bool any_str = false;
+      PXG_RETURN_IF_ERROR(Launch(ctx, "filter_gather", FilterGatherKernel, dim3(static_cast<unsigned>(p.ntiles)), dim3(kOpsBlock), 0,
+                                 static_cast<const unsigned long long*>(w.masks.as<unsigned long long>() + p.mask0),
+                                 static_cast<const uint32_t*>(w.tiles.as<uint32_t>() + p.tile0), p.lo, p.n, gc));
+    si = 0;
     for (int s = 0; s < n_select; ++s) {
       if (gc.width[s] != 0) continue;
-      any_str = true;
       uint32_t* doff = gc.dst_len[s];
       PXG_RETURN_IF_ERROR(w.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(m) + 1) + 64));
       PXG_HIP(hipMemsetAsync(doff + m, 0, 4, ctx->stream));
       PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, doff, doff, static_cast<int64_t>(m) + 1, nullptr, w.scan2.p));
-      PXG_HIP(hipMemcpyAsync(&bytes[static_cast<size_t>(s)], doff + m, 4, hipMemcpyDeviceToHost, ctx->stream));
+      PXG_HIP(hipMemcpyAsync(pin + i * n_str + si, doff + m, 4, hipMemcpyDeviceToHost, ctx->stream));
+      ++si;
     }
-    if (any_str) PXG_HIP(hipStreamSynchronize(ctx->stream));
-    for (int s = 0; s < n_select; ++s) {
-      if (gc.width[s] != 0) continue;
-      const int ci = select[s];
-      ChunkCol& dc = oc->cols[static_cast<size_t>(s)];
-      PXG_RETURN_IF_ERROR(dc.data.Alloc(static_cast<size_t>(bytes[static_cast<size_t>(s)]) + 16));
-      dc.data_len = bytes[static_cast<size_t>(s)];
-      if (m > 0)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "str_gather", StrGatherKernel, dim3(GridFor(m, 256, 1 << 30)), dim3(256), 0,
-                                   ch.cols[ci].offsets.as<const int32_t>(), ch.cols[ci].data.as<const uint8_t>(),
-                                   srcs[s].as<const uint32_t>(), static_cast<const uint32_t*>(gc.dst_len[s]), dc.data.as<uint8_t>(),
-                                   static_cast<int64_t>(m)));
-    }
-    PXG_HIP(hipStreamSynchronize(ctx->stream));  // srcs are freed at scope exit
     o.nrows += m;
     o.chunks.push_back(std::move(oc));
-    ++o.version;
   }
+  // Phase C: string payloads.
+  if (n_str > 0) {
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < parts.size(); ++i) {
+      const Part& p = parts[i];
+      const Chunk& ch = *t.chunks[p.c];
+      Chunk& oc = *o.chunks[i];
+      int si = 0;
+      for (int s = 0; s < n_select; ++s) {
+        if (gcs[i].width[s] != 0) continue;
+        const int ci = select[s];
+        ChunkCol& dc = oc.cols[static_cast<size_t>(s)];
+        const uint32_t bytes = pin[i * n_str + si];
+        PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.data, static_cast<size_t>(bytes) + 16));
+        dc.data_len = bytes;
+        if (p.m > 0)
+          PXG_RETURN_IF_ERROR(Launch(ctx, "str_gather", StrGatherKernel, dim3(GridFor(p.m, 256, 1 << 30)), dim3(256), 0,
+                                     ch.cols[ci].offsets.as<const int32_t>(), ch.cols[ci].data.as<const uint8_t>(),
+                                     static_cast<const uint32_t*>(gcs[i].dst_src[s]), static_cast<const uint32_t*>(gcs[i].dst_len[s]),
+                                     dc.data.as<uint8_t>(), static_cast<int64_t>(p.m)));
+        ++si;
+      }
+    }
+  }
+  ++o.version;
   *out = guard.release();
   return PXG_OK;
 }
@@ -333,12 +409,14 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
   PXG_RETURN_IF_ERROR(t.EnsureDeviceDescriptors());
   if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "bad row range");
   std::vector<int32_t> otypes;
+  int n_str_pass = 0;
   for (int e = 0; e < n_exprs; ++e) {
     const pxg_program& p = exprs[e];
     const bool passthrough = p.n_insns == 1 && p.insns && p.insns[0].op == PXG_OP_COL;
     if (p.result_type == PXG_STRING && !passthrough)
       return SetError(PXG_UNIMPLEMENTED, "STRING-producing scalar UDFs are not implemented on device");
     otypes.push_back(p.result_type);
+    n_str_pass += p.result_type == PXG_STRING ? 1 : 0;
   }
   const DevProgram* d_progs = nullptr;
   const int32_t* d_types = nullptr;
@@ -347,12 +425,39 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
   PXG_RETURN_IF_ERROR(NewTable(ctx, static_cast<int32_t>(otypes.size()), otypes.data(), &ot));
   std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(ot, pxg_table_destroy);
   Table& o = ot->impl;
+  struct Part {
+    size_t c;
+    int64_t lo, n;
+  };
+  std::vector<Part> parts;
   for (size_t c = 0; c < t.chunks.size(); ++c) {
     const Chunk& ch = *t.chunks[c];
     const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
     const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
-    if (lo >= hi) continue;
-    const int64_t n = hi - lo;
+    if (lo < hi) parts.push_back({c, lo, hi - lo});
+  }
+  // Passed-through STRING columns: every chunk's first / last offset in one readback.
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps);
+  if (n_str_pass > 0) {
+    if (parts.size() * n_str_pass * 2 > (Ctx::kPinnedBytes - Ctx::kPinnedOps) / 4)
+      return SetError(PXG_UNIMPLEMENTED, "map over %zu chunks", parts.size());
+    size_t k = 0;
+    for (const Part& p : parts) {
+      const Chunk& ch = *t.chunks[p.c];
+      for (int e = 0; e < n_exprs; ++e) {
+        if (exprs[e].result_type != PXG_STRING) continue;
+        const int32_t* so = ch.cols[exprs[e].insns[0].arg].offsets.as<int32_t>();
+        PXG_HIP(hipMemcpyAsync(pin + k, so + p.lo, 4, hipMemcpyDeviceToHost, ctx->stream));
+        PXG_HIP(hipMemcpyAsync(pin + k + 1, so + p.lo + p.n, 4, hipMemcpyDeviceToHost, ctx->stream));
+        k += 2;
+      }
+    }
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  size_t k = 0;
+  for (const Part& p : parts) {
+    const Chunk& ch = *t.chunks[p.c];
+    const int64_t lo = p.lo, n = p.n;
     auto oc = std::make_unique<Chunk>();
     oc->row_base = o.nrows;
     oc->nrows = n;
@@ -360,38 +465,37 @@ extern "C" int32_t pxg_map(pxg_table* inp, int32_t n_exprs, const pxg_program* e
     oc->sealed = true;
     oc->cols.resize(static_cast<size_t>(n_exprs));
     for (int e = 0; e < n_exprs; ++e) {
-      const pxg_program& p = exprs[e];
+      const pxg_program& pr = exprs[e];
       ChunkCol& dc = oc->cols[static_cast<size_t>(e)];
-      const int ty = p.result_type;
-      if (p.n_insns == 1 && p.insns[0].op == PXG_OP_COL) {
-        const ChunkCol& sc = ch.cols[p.insns[0].arg];
+      const int ty = pr.result_type;
+      if (pr.n_insns == 1 && pr.insns[0].op == PXG_OP_COL) {
+        const ChunkCol& sc = ch.cols[pr.insns[0].arg];
         if (ty == PXG_STRING) {
-          uint32_t o0 = 0, o1 = 0;
-          PXG_RETURN_IF_ERROR(ReadU32(ctx, sc.offsets.as<int32_t>() + lo, &o0));
-          PXG_RETURN_IF_ERROR(ReadU32(ctx, sc.offsets.as<int32_t>() + hi, &o1));
-          PXG_RETURN_IF_ERROR(dc.offsets.Alloc((n + 1) * 4 + 16));
-          PXG_RETURN_IF_ERROR(dc.data.Alloc(static_cast<size_t>(o1 - o0) + 16));
+          const uint32_t o0 = pin[k], o1 = pin[k + 1];
+          k += 2;
+          PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.offsets, (n + 1) * 4 + 16));
+          PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.data, static_cast<size_t>(o1 - o0) + 16));
           dc.data_len = o1 - o0;
           PXG_RETURN_IF_ERROR(Launch(ctx, "map_rebase", RebaseKernel, dim3(GridFor(n + 1, 256, 1 << 30)), dim3(256), 0,
                                      dc.offsets.as<int32_t>(), sc.offsets.as<const int32_t>() + lo, n + 1));
-          PXG_HIP(hipMemcpyAsync(dc.data.p, sc.data.as<uint8_t>() + o0, o1 - o0, hipMemcpyDeviceToDevice, ctx->stream));
+          if (o1 > o0)
+            PXG_HIP(hipMemcpyAsync(dc.data.p, sc.data.as<uint8_t>() + o0, o1 - o0, hipMemcpyDeviceToDevice, ctx->stream));
         } else {
           const int w = TypeWidth(ty);
-          PXG_RETURN_IF_ERROR(dc.values.Alloc(n * w + 16));
+          PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.values, n * w + 16));
           PXG_HIP(hipMemcpyAsync(dc.values.p, sc.values.as<uint8_t>() + lo * w, n * w, hipMemcpyDeviceToDevice, ctx->stream));
         }
         continue;
       }
       const int w = TypeWidth(ty);
-      PXG_RETURN_IF_ERROR(dc.values.Alloc(n * w + 16));
+      PXG_RETURN_IF_ERROR(PoolAlloc(ctx, dc.values, n * w + 16));
       PXG_RETURN_IF_ERROR(Launch(ctx, "map_eval", MapEvalKernel, dim3(GridFor(n, 256, 1 << 30)), dim3(256), 0, d_progs + e,
-                                 t.d_chunks.as<const DevChunk>(), static_cast<int>(c), d_types, lo, n, dc.values.as<uint8_t>(), w));
+                                 t.d_chunks.as<const DevChunk>(), static_cast<int>(p.c), d_types, lo, n, dc.values.as<uint8_t>(), w));
     }
     o.nrows += n;
     o.chunks.push_back(std::move(oc));
-    ++o.version;
   }
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  ++o.version;
   *out = guard.release();
   return PXG_OK;
 }

@@ -22,6 +22,55 @@ int TypeWidth(int type) {
   }
 }
 
+int32_t PoolAlloc(Ctx* ctx, DevBuf& b, size_t bytes) {
+  PoolRelease(ctx, b);
+  if (bytes == 0) bytes = 16;
+  BufPool& pool = ctx->pool;
+  auto it = pool.free.lower_bound(bytes);
+  if (it != pool.free.end() && it->first <= 2 * bytes + (size_t(1) << 20)) {
+    b.p = it->second;
+    b.bytes = it->first;
+    pool.cached -= it->first;
+    pool.free.erase(it);
+    return PXG_OK;
+  }
+  // New buffers are rounded up (1 MiB granules past 1 MiB) so later requests of similar size reuse them.
+  const size_t gran = bytes > (size_t(1) << 20) ? (size_t(1) << 20) : 4096;
+  const size_t n = (bytes + gran - 1) / gran * gran;
+  hipError_t e = hipMalloc(&b.p, n);
+  if (e != hipSuccess) {
+    PoolClear(ctx);
+    e = hipMalloc(&b.p, n);
+  }
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return SetError(PXG_RESOURCE_UNAVAILABLE, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+  }
+  b.bytes = n;
+  return PXG_OK;
+}
+
+void PoolRelease(Ctx* ctx, DevBuf& b) {
+  if (!b.p) return;
+  BufPool& pool = ctx->pool;
+  pool.free.emplace(b.bytes, b.p);
+  pool.cached += b.bytes;
+  b.p = nullptr;
+  b.bytes = 0;
+  while (pool.cached > pool.cap && !pool.free.empty()) {  // evict the largest
+    auto last = std::prev(pool.free.end());
+    (void)hipFree(last->second);
+    pool.cached -= last->first;
+    pool.free.erase(last);
+  }
+}
+
+void PoolClear(Ctx* ctx) {
+  for (auto& kv : ctx->pool.free) (void)hipFree(kv.second);
+  ctx->pool.free.clear();
+  ctx->pool.cached = 0;
+}
+
 hipEvent_t Ctx::GetEvent() {
   if (!free_events.empty()) {
     hipEvent_t e = free_events.back();
@@ -77,12 +126,12 @@ int32_t Table::EnsureDeviceDescriptors() {
   if (d_chunks_version == version) return PXG_OK;
   std::vector<DevChunk> h(std::max<size_t>(chunks.size(), 1));
   for (size_t i = 0; i < chunks.size(); ++i) h[i] = Descriptor(i);
-  if (d_chunks.bytes < h.size() * sizeof(DevChunk)) PXG_RETURN_IF_ERROR(d_chunks.Alloc(h.size() * sizeof(DevChunk) * 2));
+  if (d_chunks.bytes < h.size() * sizeof(DevChunk)) PXG_RETURN_IF_ERROR(PoolAlloc(ctx, d_chunks, h.size() * sizeof(DevChunk) * 2));
   PXG_HIP(hipMemcpyAsync(d_chunks.p, h.data(), h.size() * sizeof(DevChunk), hipMemcpyHostToDevice, ctx->stream));
   if (!d_types.p) {
     std::vector<int32_t> t(kMaxCols, 0);
     for (int k = 0; k < ncols; ++k) t[k] = types[k];
-    PXG_RETURN_IF_ERROR(d_types.Alloc(kMaxCols * sizeof(int32_t)));
+    PXG_RETURN_IF_ERROR(PoolAlloc(ctx, d_types, kMaxCols * sizeof(int32_t)));
     PXG_HIP(hipMemcpyAsync(d_types.p, t.data(), kMaxCols * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
   }
   PXG_HIP(hipStreamSynchronize(ctx->stream));
@@ -280,7 +329,7 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->impl.num_cus = prop.multiProcessorCount;
-  if (hipHostMalloc(&c->impl.pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&c->impl.pinned, Ctx::kPinnedBytes, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return SetError(PXG_RESOURCE_UNAVAILABLE, "pinned host scratch allocation failed");
   }
@@ -291,6 +340,7 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
 extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   if (!ctx) return PXG_OK;
   hipStreamSynchronize(ctx->impl.stream);
+  PoolClear(&ctx->impl);
   ctx->impl.ResolveTimings();
   for (auto e : ctx->impl.free_events) hipEventDestroy(e);
   if (ctx->impl.pinned) hipHostFree(ctx->impl.pinned);
@@ -370,7 +420,17 @@ extern "C" int32_t pxg_table_create(pxg_ctx* ctx, int32_t ncols, const int32_t* 
 
 extern "C" int32_t pxg_table_destroy(pxg_table* t) {
   if (!t) return PXG_OK;
-  hipStreamSynchronize(t->impl.ctx->stream);
+  // Column buffers go to the ctx pool (no device-wide sync); what is left is freed.
+  Ctx* ctx = t->impl.ctx;
+  for (auto& ch : t->impl.chunks) {
+    for (auto& col : ch->cols) {
+      PoolRelease(ctx, col.values);
+      PoolRelease(ctx, col.offsets);
+      PoolRelease(ctx, col.data);
+    }
+  }
+  PoolRelease(ctx, t->impl.d_chunks);
+  PoolRelease(ctx, t->impl.d_types);
   delete t;
   return PXG_OK;
 }
