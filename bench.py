@@ -129,13 +129,27 @@ def main():
     # The engine's own lowering of the C2 plan (the drop-in path's fused Filter/Map/Agg), driven
     # directly on the HBM-resident table so the timed step is exactly the device hot path.
     agg = plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
-    exch = {"bytes_sent": 0, "bytes_recv": 0}
+    exch = {"bytes_sent": 0, "bytes_recv": 0, "via": None}
+    # N > 1: libpxg's own RCCL communicator (pxg_comm_init / pxg_agg_alltoall, one rank per
+    # GPU over xGMI); torch.distributed only carries the unique id.  A gloo run (CPU rehearsal)
+    # exchanges through torch.distributed instead.
+    comm = None
+    if world > 1 and args.backend == "nccl":
+        from pixie_amd.device import Comm
+        obj = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = Comm(ctx, rank, world, obj[0])
 
     def step():
         agg.reset()
         agg.consume(table)
         if world > 1:
-            s, r = exchange_partials(agg)
+            if comm is not None:
+                s, r = agg.alltoall(comm)
+                exch["via"] = "pxg_agg_alltoall (RCCL grouped send/recv on the ctx stream)"
+            else:
+                s, r = exchange_partials(agg)
+                exch["via"] = "torch.distributed all_to_all_single (" + args.backend + ")"
             exch["bytes_sent"], exch["bytes_recv"] = s, r
         return agg.finalize()
 
@@ -265,6 +279,8 @@ def main():
             "n1": n1,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1 or args.n1_rows <= 0:
         agg.close()
     table.close()

@@ -164,6 +164,7 @@ typedef struct {
 typedef struct pxg_ctx pxg_ctx;
 typedef struct pxg_table pxg_table;
 typedef struct pxg_agg pxg_agg;
+typedef struct pxg_comm pxg_comm;
 
 int32_t pxg_abi_version(void);
 const char* pxg_last_error(void);
@@ -319,6 +320,23 @@ int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes);
  * part_bytes[i] bytes: e.g. what one all-to-all received from every rank) in one pass. */
 int32_t pxg_agg_import_partials(pxg_agg* agg, const void* src, int32_t n_parts,
                                 const int64_t* part_offsets, const int64_t* part_bytes);
+
+/* ---------------------------------------------------------------------------------------
+ * Intra-node exchange over RCCL / xGMI (the PEM-partial -> Kelvin-finalize hop,
+ * src/carnot/planner/distributed/splitter/partial_op_mgr/partial_op_mgr.cc:69-83, which the
+ * reference runs over GRPCSink/GRPCSource).  One rank per GPU.
+ * ------------------------------------------------------------------------------------- */
+#define PXG_COMM_ID_BYTES 128
+/* An RCCL unique id (PXG_COMM_ID_BYTES bytes); one rank makes it, every rank passes it on. */
+int32_t pxg_comm_unique_id(uint8_t* id_out, int32_t id_bytes);
+/* Communicator of `nranks` ranks over ctx's device; collective (every rank calls it). */
+int32_t pxg_comm_init(pxg_ctx* ctx, int32_t rank, int32_t nranks, const uint8_t* id, int32_t id_bytes, pxg_comm** out);
+int32_t pxg_comm_destroy(pxg_comm* comm);
+/* Re-partition agg's state across the ranks by hash(group key): export nranks parts, exchange
+ * the byte counts and the parts (grouped ncclSend/ncclRecv on the ctx stream), reset agg and
+ * import what arrived.  Afterwards every group lives on exactly one rank; finalize locally.
+ * Collective.  bytes_sent / bytes_recv (optional) receive this rank's traffic. */
+int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes_sent, int64_t* bytes_recv);
 
 /* ---------------------------------------------------------------------------------------
  * Equijoin (EquijoinNode, src/carnot/exec/equijoin_node.cc:53-470).  A hash table is built on

@@ -341,6 +341,13 @@ class Agg:
         check(self.lib.pxg_agg_rows_selected(self.h, C.byref(n)))
         return int(n.value)
 
+    def alltoall(self, comm: "Comm") -> Tuple[int, int]:
+        """Re-partition this agg's state across the communicator's ranks by group-key hash over
+        RCCL (pxg_agg_alltoall).  Collective.  Returns (bytes sent, bytes received)."""
+        s, r = C.c_int64(), C.c_int64()
+        check(self.lib.pxg_agg_alltoall(self.h, comm.h, C.byref(s), C.byref(r)))
+        return int(s.value), int(r.value)
+
     def close(self) -> None:
         if self.h:
             self.lib.pxg_agg_destroy(self.h)
@@ -369,3 +376,27 @@ def datagen_http_events(seed: int, row_begin: int, nrows: int, n_pair_keys: int 
 HTTP_EVENTS_SCHEMA = [("time_", TIME64NS), ("upid", UINT128), ("service", STRING), ("req_path", STRING),
                       ("remote_addr", STRING), ("resp_status", INT64), ("latency", INT64),
                       ("req_body_size", INT64), ("resp_body_size", INT64), ("pod", STRING)]
+
+
+class Comm:
+    """RCCL communicator of libpxg (pxg_comm_*): one rank per GPU, over the ctx's device."""
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * Comm.ID_BYTES)()
+        check(load().pxg_comm_unique_id(buf, Comm.ID_BYTES))
+        return bytes(buf)
+
+    def __init__(self, ctx: "Ctx", rank: int, nranks: int, uid: bytes):
+        self.lib = load()
+        buf = (C.c_uint8 * Comm.ID_BYTES).from_buffer_copy(uid[:Comm.ID_BYTES])
+        h = C.c_void_p()
+        check(self.lib.pxg_comm_init(ctx.h, rank, nranks, buf, Comm.ID_BYTES, C.byref(h)))
+        self.h = h
+        self.rank, self.nranks = rank, nranks
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.pxg_comm_destroy(self.h)
+            self.h = None
