@@ -122,6 +122,17 @@ int32_t pxc_engine_explain_plan(pxc_engine* engine, const uint8_t* plan, int64_t
 int32_t pxc_plan_create_agg(pxg_ctx* ctx, const uint8_t* plan, int64_t plan_len, const char* table_name,
                             int32_t ncols, const int32_t* types, int64_t expected_groups, pxg_agg** out,
                             int32_t* n_keys, int32_t* n_udas, int32_t* uda_kinds);
+/* Execution statistics (ExecNodeStats, src/carnot/exec/exec_node.h:41-125; carnot.cc:379-420).
+ * With analyze on, every later query collects per-node total / self time and extra metrics as
+ * well as the always-kept rows / bytes / batches in and out.  pxc_engine_last_stats returns the
+ * last query's stats as a JSON object (malloc'ed, NUL-terminated; release with pxc_free):
+ * {"bytes_processed", "rows_processed" (the sources' output, exec_graph.cc:333-347),
+ *  "nodes": [{"node_id", "name", "bytes_output", "records_output", "batches_output",
+ *             "bytes_input", "records_input", "batches_input", "total_execution_time_ns",
+ *             "self_execution_time_ns", "extra_metrics", "extra_info"}, ...]} (field names of
+ * queryresultspb.OperatorExecutionStats). */
+int32_t pxc_engine_set_analyze(pxc_engine* engine, int32_t on);
+int32_t pxc_engine_last_stats(pxc_engine* engine, char** out, int64_t* out_len);
 void pxc_free(void* p);
 /* QuantilesUDA::Finalize JSON (math_sketches.h:40-54, bytes as rapidjson's Writer emits them)
  * for n groups of 7 doubles (p01..p99): one buffer of n NUL-terminated strings (pxc_free). */

@@ -667,7 +667,68 @@ struct ExecState {
   std::multimap<std::string, pxg_agg*>* agg_cache = nullptr;
   // ExecState::StopSource (exec_state.h:171-178): sources a Limit has finished with.
   std::set<uint64_t> stopped_sources;
+  // Collect per-node timers and extra metrics (Carnot's `analyze`, carnot.cc:379-420).
+  bool collect_exec_stats = false;
 };
+
+// ExecNodeStats (src/carnot/exec/exec_node.h:41-125): rows / bytes / batches in and out, the
+// node's total time and the time spent in its children (self = total - children), extra
+// metrics and info.  Row and byte counts are always kept (the sources' counts are the query's
+// bytes_processed / rows_processed, exec_graph.cc:333-347); timers and extras only when the
+// query collects stats.  Bytes follow RowBatch::NumBytes (row_batch.cc:67-79): fixed-width
+// values by type width, STRING by the string lengths.
+static int64_t RowBatchNumBytes(const RowBatch& rb);
+struct ExecNodeStats {
+  bool collect = false;
+  int64_t bytes_input = 0, rows_input = 0, batches_input = 0;
+  int64_t bytes_output = 0, rows_output = 0, batches_output = 0;
+  int64_t total_ns = 0, children_ns = 0;
+  std::map<std::string, double> extra_metrics;
+  std::map<std::string, std::string> extra_info;
+  std::chrono::steady_clock::time_point total_t0, child_t0;
+  void AddInputStats(const RowBatch& rb) {
+    ++batches_input;
+    rows_input += rb.num_rows;
+    bytes_input += RowBatchNumBytes(rb);
+  }
+  void AddOutputStats(const RowBatch& rb) {
+    ++batches_output;
+    rows_output += rb.num_rows;
+    bytes_output += RowBatchNumBytes(rb);
+  }
+  void ResumeTotalTimer() {
+    if (collect) total_t0 = std::chrono::steady_clock::now();
+  }
+  void StopTotalTimer() {
+    if (collect) total_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - total_t0).count();
+  }
+  void ResumeChildTimer() {
+    if (collect) child_t0 = std::chrono::steady_clock::now();
+  }
+  void StopChildTimer() {
+    if (collect) children_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - child_t0).count();
+  }
+  void AddExtraMetric(const std::string& k, double v) {
+    if (collect) extra_metrics[k] = v;
+  }
+  void AddExtraInfo(const std::string& k, const std::string& v) {
+    if (collect) extra_info[k] = v;
+  }
+};
+
+static int64_t RowBatchNumBytes(const RowBatch& rb) {
+  if (rb.num_rows == 0) return 0;
+  int64_t b = 0;
+  for (const HostColumn& c : rb.cols) {
+    switch (c.type) {
+      case PXG_STRING: b += c.offsets ? static_cast<int64_t>(c.offsets[c.length]) - c.offsets[0] : 0; break;
+      case PXG_BOOLEAN: b += c.length; break;
+      case PXG_UINT128: b += 16 * c.length; break;
+      default: b += 8 * c.length; break;
+    }
+  }
+  return b;
+}
 
 // ---------------------------------------------------------------------------------------
 // ExecNode NVI (src/carnot/exec/exec_node.h:145-315).
@@ -686,8 +747,14 @@ class ExecNode {
   // exec_node.h:213-226: eos implies eow.
   Status ConsumeNext(ExecState* s, const RowBatch& rb, size_t parent_index) {
     if (rb.eos && !rb.eow) return Err(PXG_INTERNAL, "RowBatch has eos set without eow");
-    return ConsumeNextImpl(s, rb, parent_index);
+    stats_.AddInputStats(rb);
+    stats_.ResumeTotalTimer();
+    Status st = ConsumeNextImpl(s, rb, parent_index);
+    stats_.StopTotalTimer();
+    return st;
   }
+  ExecNodeStats* stats() { return &stats_; }
+  uint64_t plan_id = 0;  // the plan node this ExecNode runs
   void AddChild(ExecNode* child, size_t parent_index) { children_.push_back({child, parent_index}); }
   // Whether this node can observe the value of input column `col` (conservative default).
   // Lets a producer skip rendering a column no consumer reads.
@@ -703,9 +770,13 @@ class ExecNode {
   virtual Status ConsumeNextImpl(ExecState*, const RowBatch&, size_t) { return Err(PXG_INTERNAL, "not a consumer"); }
   // exec_node.h:285-297: depth-first push to every child.
   Status SendRowBatchToChildren(ExecState* s, const RowBatch& rb) {
+    stats_.ResumeChildTimer();
     for (auto& c : children_) PXC_RETURN_IF_ERROR(c.first->ConsumeNext(s, rb, c.second));
+    stats_.StopChildTimer();
+    stats_.AddOutputStats(rb);
     return Status::OK();
   }
+  ExecNodeStats stats_;
   RowDescriptor output_;
   std::vector<RowDescriptor> inputs_;
   std::vector<std::pair<ExecNode*, size_t>> children_;
@@ -716,7 +787,15 @@ class SourceNode : public ExecNode {
  public:
   uint64_t node_id = 0;  // plan node id (LimitOperator.abortable_srcs names sources by it)
   virtual bool HasBatchesRemaining() const = 0;
-  virtual Status GenerateNext(ExecState* s) = 0;
+  Status GenerateNext(ExecState* s) {
+    stats_.ResumeTotalTimer();
+    Status st = GenerateNextImpl(s);
+    stats_.StopTotalTimer();
+    return st;
+  }
+
+ protected:
+  virtual Status GenerateNextImpl(ExecState* s) = 0;
 };
 
 // MemorySourceNode (memory_source_node.cc:54-124) over a host table's RowBatches.
@@ -731,7 +810,7 @@ class MemorySourceNode : public SourceNode {
     return next_ < std::max<int32_t>(table_->nbatches, 1) && !done_;
   }
   // GenerateNext: one RowBatch (column-projected) to the children.
-  Status GenerateNext(ExecState* s) override {
+  Status GenerateNextImpl(ExecState* s) override {
     RowBatch rb;
     const int32_t nb = table_->nbatches;
     if (nb == 0) {  // empty table: one zero-row batch with eow/eos (memory_source_node.cc:107-118)
@@ -1019,6 +1098,7 @@ class GpuAggNode : public ExecNode {
   bool has_filter = false;
   Program filter;
   bool fused_ = false;
+  std::vector<uint64_t> fused_ids;  // plan ids of the Filter / Map operators fused into this node
   bool device_input = false;  // fed by a stored table through ConsumeTable
   RowDescriptor source_types;
 
@@ -1216,6 +1296,11 @@ class GpuAggNode : public ExecNode {
     int64_t groups = 0;
     PXG_CALL(pxg_agg_finalize(agg_, &groups));
     if (hints_) (*hints_)[HintKey()] = std::max<int64_t>(groups, 1);
+    if (stats_.collect) {
+      int64_t sel = 0;
+      if (pxg_agg_rows_selected(agg_, &sel) == PXG_OK) stats_.AddExtraMetric("rows_aggregated", static_cast<double>(sel));
+      stats_.AddExtraMetric("groups", static_cast<double>(groups));
+    }
     clk.Mark("agg finalize");
     std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
     PXG_CALL(pxg_agg_result(agg_, out.data(), static_cast<int32_t>(out.size())));
@@ -1858,7 +1943,7 @@ class GrpcSourceNode : public SourceNode {
   GrpcSourceNode(uint64_t id, const std::vector<std::pair<const uint8_t*, int64_t>>* msgs) : id_(id), msgs_(msgs) {}
   std::string DebugString() const override { return "GrpcSourceNode(" + std::to_string(id_) + ")"; }
   bool HasBatchesRemaining() const override { return !sent_eos_; }
-  Status GenerateNext(ExecState* s) override {
+  Status GenerateNextImpl(ExecState* s) override {
     if (!msgs_ || next_ >= msgs_->size())
       return Err(PXG_INVALID_ARGUMENT, "GRPC source %llu ran out of row batches before eos", (unsigned long long)id_);
     RowBatch rb;
@@ -1893,10 +1978,24 @@ class DeviceSourceNode : public SourceNode {
   DeviceSourceNode(std::string name, const StoredTable* st) : name_(std::move(name)), st_(st) {}
   std::string DebugString() const override { return "MemorySourceNode(" + name_ + ", HBM-resident)"; }
   bool HasBatchesRemaining() const override { return !done_; }
+  // RowBatch::NumBytes of the projected columns over [lo, hi): exact for the whole table
+  // (string payload = device bytes - offsets), proportional for a sub-range.
+  int64_t RangeBytes() const {
+    const int64_t n = pxg_table_num_rows(st_->t);
+    if (n <= 0 || hi_ <= lo_) return 0;
+    int64_t b = 0;
+    for (int64_t c : idxs_) {
+      const int32_t t = st_->types[static_cast<size_t>(c)];
+      int64_t cb = pxg_table_device_bytes(st_->t, static_cast<int32_t>(c));
+      if (t == PXG_STRING) cb -= 4 * n;
+      b += cb;
+    }
+    return hi_ - lo_ == n ? b : static_cast<int64_t>(static_cast<double>(b) * (hi_ - lo_) / n);
+  }
   GpuAggNode* fused_agg = nullptr;
   const std::vector<int64_t>& idxs() const { return idxs_; }
 
-  Status GenerateNext(ExecState* s) override {
+  Status GenerateNextImpl(ExecState* s) override {
     if (!ranged_) {
       PXC_RETURN_IF_ERROR(Range());
       ranged_ = true;
@@ -1904,7 +2003,14 @@ class DeviceSourceNode : public SourceNode {
     }
     if (fused_agg) {
       done_ = true;
-      return fused_agg->ConsumeTable(s, st_->t, lo_, hi_);
+      // The agg reads the stored table in place: the range counts as one output batch.
+      ++stats_.batches_output;
+      stats_.rows_output += hi_ - lo_;
+      stats_.bytes_output += RangeBytes();
+      stats_.ResumeChildTimer();
+      Status st = fused_agg->ConsumeTable(s, st_->t, lo_, hi_);
+      stats_.StopChildTimer();
+      return st;
     }
     const int64_t end = std::min(hi_, cur_ + kBatchRows);
     RowBatch rb;
@@ -2021,6 +2127,7 @@ class ExecutionGraph {
         }
         auto* src = new GrpcSourceNode(id, msgs);
         src->node_id = id;
+        src->plan_id = id;
         pool_.emplace_back(src);
         for (int32_t t : op.grpc_source_types)
           if (t < B || t > T) return Err(PXG_INVALID_ARGUMENT, "GRPC source column type %d", t);
@@ -2117,6 +2224,7 @@ class ExecutionGraph {
         default: return Err(PXG_UNIMPLEMENTED, "operator (oneof field %d) has no device node", op.which);
       }
       pool_.emplace_back(node);
+      node->plan_id = id;
       PXC_RETURN_IF_ERROR(node->Init(op, out, ins));
       for (size_t k = 0; k < ps.size(); ++k) built[ps[k]]->AddChild(node, k);
       built[id] = node;
@@ -2130,6 +2238,7 @@ class ExecutionGraph {
   // ExecuteSources (exec_graph.cc:177-289).
   Status Execute(ExecState* s) {
     StageClock clk;
+    for (auto& n : pool_) n->stats()->collect = s->collect_exec_stats;
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Prepare(s));
     for (auto& n : pool_) PXC_RETURN_IF_ERROR(n->Open(s));
     clk.Mark("prepare + open");
@@ -2150,6 +2259,52 @@ class ExecutionGraph {
     }
     clk.Mark("close");
     return st;
+  }
+
+  // ExecutionGraph::GetStats (exec_graph.cc:333-347) plus, per node in plan order, the
+  // OperatorExecutionStats fields carnot.cc:386-420 reports under `analyze`, as JSON.
+  std::string StatsJson() {
+    int64_t bytes = 0, rows = 0;
+    for (auto* src : sources_) {
+      bytes += src->stats()->bytes_output;
+      rows += src->stats()->rows_output;
+    }
+    std::vector<ExecNode*> nodes;
+    for (auto& n : pool_) nodes.push_back(n.get());
+    std::stable_sort(nodes.begin(), nodes.end(), [](ExecNode* a, ExecNode* b) { return a->plan_id < b->plan_id; });
+    std::ostringstream os;
+    auto q = [](const std::string& x) {
+      std::string o = "\"";
+      for (char c : x) {
+        if (c == '"' || c == '\\') o.push_back('\\');
+        if (static_cast<unsigned char>(c) >= 0x20) o.push_back(c);
+      }
+      return o + "\"";
+    };
+    os << "{\"bytes_processed\":" << bytes << ",\"rows_processed\":" << rows << ",\"nodes\":[";
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      ExecNodeStats* st = nodes[i]->stats();
+      if (st->collect) st->AddExtraMetric("batches_output", static_cast<double>(st->batches_output));
+      os << (i ? "," : "") << "{\"node_id\":" << nodes[i]->plan_id << ",\"name\":" << q(nodes[i]->DebugString())
+         << ",\"bytes_output\":" << st->bytes_output << ",\"records_output\":" << st->rows_output
+         << ",\"batches_output\":" << st->batches_output << ",\"bytes_input\":" << st->bytes_input
+         << ",\"records_input\":" << st->rows_input << ",\"batches_input\":" << st->batches_input
+         << ",\"total_execution_time_ns\":" << st->total_ns << ",\"self_execution_time_ns\":" << (st->total_ns - st->children_ns);
+      if (auto* a = dynamic_cast<GpuAggNode*>(nodes[i])) {
+        os << ",\"fused_node_ids\":[";
+        for (size_t k = 0; k < a->fused_ids.size(); ++k) os << (k ? "," : "") << a->fused_ids[k];
+        os << "]";
+      }
+      os << ",\"extra_metrics\":{";
+      size_t k = 0;
+      for (auto& kv : st->extra_metrics) os << (k++ ? "," : "") << q(kv.first) << ":" << kv.second;
+      os << "},\"extra_info\":{";
+      k = 0;
+      for (auto& kv : st->extra_info) os << (k++ ? "," : "") << q(kv.first) << ":" << q(kv.second);
+      os << "}}";
+    }
+    os << "]}";
+    return os.str();
   }
 
   std::string Explain() const {
@@ -2265,6 +2420,7 @@ class ExecutionGraph {
       src = dsrc;
     }
     src->node_id = id;
+    src->plan_id = id;
     pool_.emplace_back(src);
     PXC_RETURN_IF_ERROR(src->Init(op, src_types, {}));
     sources_.push_back(src);
@@ -2324,6 +2480,8 @@ class ExecutionGraph {
     }
     auto* agg = new GpuAggNode();
     pool_.emplace_back(agg);
+    agg->plan_id = agg_id;
+    for (uint64_t cid : chain) agg->fused_ids.push_back(cid);
     agg->env = env;
     agg->has_filter = has_filter;
     agg->filter = filter;
@@ -2451,6 +2609,8 @@ struct pxc_engine {
   TableStore store;
   std::map<std::string, int64_t> group_hints;
   std::multimap<std::string, pxg_agg*> agg_cache;
+  bool analyze = false;    // collect per-node timers / extras (pxc_engine_set_analyze)
+  std::string last_stats;  // the last query's execution stats (pxc_engine_last_stats)
 };
 
 static int32_t Fail(const Status& s) {
@@ -2605,6 +2765,23 @@ extern "C" int64_t pxc_store_num_rows(pxc_engine* e, const char* name) {
 
 extern "C" pxg_ctx* pxc_engine_ctx(pxc_engine* e) { return e ? e->ctx : nullptr; }
 
+extern "C" int32_t pxc_engine_set_analyze(pxc_engine* e, int32_t on) {
+  if (!e) return Fail(Err(PXG_INVALID_ARGUMENT, "engine is null"));
+  std::lock_guard<std::mutex> lock(e->mu);
+  e->analyze = on != 0;
+  return PXG_OK;
+}
+
+extern "C" int32_t pxc_engine_last_stats(pxc_engine* e, char** out, int64_t* out_len) {
+  if (!e || !out || !out_len) return Fail(Err(PXG_INVALID_ARGUMENT, "bad arguments"));
+  std::lock_guard<std::mutex> lock(e->mu);
+  char* p = static_cast<char*>(std::malloc(e->last_stats.size() + 1));
+  std::memcpy(p, e->last_stats.c_str(), e->last_stats.size() + 1);
+  *out = p;
+  *out_len = static_cast<int64_t>(e->last_stats.size());
+  return PXG_OK;
+}
+
 extern "C" pxg_table* pxc_store_device_table(pxc_engine* e, const char* name) {
   if (!e || !name) return nullptr;
   auto it = e->store.find(name);
@@ -2632,7 +2809,9 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   st.ctx = engine->ctx;
   st.group_hints = &engine->group_hints;
   st.agg_cache = &engine->agg_cache;
+  st.collect_exec_stats = engine->analyze;
   s = g.Execute(&st);
+  engine->last_stats = g.StatsJson();
   if (!s.ok()) return Fail(s);
   clk.Mark("execute (total)");
   Writer w;

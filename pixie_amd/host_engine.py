@@ -70,6 +70,10 @@ def load() -> C.CDLL:
     lib.pxc_plan_create_agg.restype = i32
     lib.pxc_quantiles_json.argtypes = [p(C.c_double), i64, p(vp), p(i64)]
     lib.pxc_quantiles_json.restype = i32
+    lib.pxc_engine_set_analyze.argtypes = [vp, i32]
+    lib.pxc_engine_set_analyze.restype = i32
+    lib.pxc_engine_last_stats.argtypes = [vp, p(vp), p(i64)]
+    lib.pxc_engine_last_stats.restype = i32
     lib.pxc_free.argtypes = [vp]
     lib.pxc_free.restype = None
     lib.pxc_last_error.argtypes = []
@@ -204,6 +208,21 @@ class Engine:
 
     def ctx_handle(self) -> int:
         return int(self.lib.pxc_engine_ctx(self.h))
+
+    def set_analyze(self, on: bool) -> None:
+        """Collect per-node timers and extra metrics for later queries (Carnot's analyze)."""
+        _check(self.lib.pxc_engine_set_analyze(self.h, 1 if on else 0))
+
+    def last_stats(self) -> dict:
+        """The last query's execution stats (pxc_engine_last_stats JSON, include/pxcarnot.h)."""
+        import json
+        out = C.c_void_p()
+        n = C.c_int64()
+        _check(self.lib.pxc_engine_last_stats(self.h, C.byref(out), C.byref(n)))
+        try:
+            return json.loads(C.string_at(out.value, n.value).decode())
+        finally:
+            self.lib.pxc_free(out)
 
     def execute_raw(self, pb: bytes, tables: Dict[str, dict] = None) -> bytes:
         """pxc_execute_plan on serialized plan bytes; returns the PXRB result bytes."""
