@@ -15,6 +15,7 @@
 // formatting, as in the reference, where UDA Finalize runs on the host.
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -813,6 +814,10 @@ class MemorySourceNode : public SourceNode {
   Status GenerateNextImpl(ExecState* s) override {
     RowBatch rb;
     const int32_t nb = table_->nbatches;
+    if (nb == 0 && streaming_) {  // an infinite stream over an empty table has nothing ready
+      done_ = true;
+      return Status::OK();
+    }
     if (nb == 0) {  // empty table: one zero-row batch with eow/eos (memory_source_node.cc:107-118)
       for (size_t c = 0; c < idxs_.size(); ++c) {
         HostColumn hc;
@@ -846,14 +851,19 @@ class MemorySourceNode : public SourceNode {
     } else {
       rb.eow = rb.eos = (b == nb - 1);
     }
+    if (streaming_) {  // an infinite stream sends no eow / eos; it has sent all there is
+      rb.eow = rb.eos = false;
+      if (next_ >= nb) done_ = true;
+    }
     if (rb.eos) done_ = true;
     return SendRowBatchToChildren(s, rb);
   }
 
  protected:
   Status InitImpl(const planpb::Operator& op) override {
-    if (op.mem_source.has_start_time || op.mem_source.has_stop_time || op.mem_source.streaming)
-      return Err(PXG_UNIMPLEMENTED, "time-bounded or streaming MemorySource needs a stored table (pxc_store_*)");
+    if (op.mem_source.has_start_time || op.mem_source.has_stop_time)
+      return Err(PXG_UNIMPLEMENTED, "a time-bounded MemorySource needs a stored table (pxc_store_*)");
+    streaming_ = op.mem_source.streaming;
     idxs_ = op.mem_source.column_idxs;
     if (idxs_.empty())
       for (int32_t c = 0; c < table_->ncols; ++c) idxs_.push_back(c);
@@ -867,6 +877,7 @@ class MemorySourceNode : public SourceNode {
   std::vector<int64_t> idxs_;
   int32_t next_ = 0;
   bool done_ = false;
+  bool streaming_ = false;
 };
 
 // Uploads a RowBatch into a fresh device table.
@@ -1896,18 +1907,24 @@ struct StoredTable {
 };
 using TableStore = std::map<std::string, StoredTable>;
 
-// UnionNode, unordered (union_node.cc:268-289): every parent's batch is forwarded with its
-// columns picked by the parent's column mapping; eow / eos are set once every parent has sent
-// eos.  A union with a time_ column merges by time in the reference (order_by_time,
-// operators.cc:543): not supported here.
+// UnionNode (union_node.cc).  Unordered (union_node.cc:268-289): every parent's batch is
+// forwarded with its columns picked by the parent's column mapping; eow / eos are set once every
+// parent has sent eos.  With a time_ output column (order_by_time, operators.cc:543) the parents'
+// rows are merged by time (union_node.cc:172-258): the parent whose cursor row has the smallest
+// time_ (ties: the lower parent index) supplies rows while its time stays <= the runner-up's, a
+// parent without buffered rows stalls the merge until it delivers, output goes out in batches of
+// rows_per_batch (default 1024) and, once every parent is at eos, as a last eow/eos batch.  A
+// pending partial batch is also flushed when more than kFlushTimeout passed since the last flush
+// (union_node.cc:127-146).  Rows are copied as runs (a parent's rows up to the runner-up's time)
+// rather than one by one; the order is the reference's row for row.
 class UnionNode : public ExecNode {
  public:
-  std::string DebugString() const override { return "UnionNode(unordered)"; }
+  static constexpr int64_t kDefaultRowsPerBatch = 1024;  // kDefaultUnionRowBatchSize
+  static constexpr std::chrono::milliseconds kFlushTimeout{1000};  // kDefaultDataFlushTimeoutMillis
+  std::string DebugString() const override { return ordered_ ? "UnionNode(ordered by time_)" : "UnionNode(unordered)"; }
 
  protected:
   Status InitImpl(const planpb::Operator& op) override {
-    for (auto& n : op.union_names)
-      if (n == "time_") return Err(PXG_UNIMPLEMENTED, "time-ordered Union is not supported");
     maps_ = op.union_mappings;
     if (maps_.size() != inputs_.size()) return Err(PXG_INVALID_ARGUMENT, "Union has %zu column mappings for %zu parents", maps_.size(), inputs_.size());
     for (size_t p = 0; p < maps_.size(); ++p) {
@@ -1917,22 +1934,172 @@ class UnionNode : public ExecNode {
           return Err(PXG_INVALID_ARGUMENT, "Union column mapping %zu:%zu is invalid", p, c);
     }
     eos_.assign(inputs_.size(), false);
+    for (size_t c = 0; c < op.union_names.size(); ++c)
+      if (op.union_names[c] == "time_") time_out_ = static_cast<int64_t>(c);
+    ordered_ = time_out_ >= 0;
+    if (ordered_) {
+      if (output_[static_cast<size_t>(time_out_)] != PXG_TIME64NS && output_[static_cast<size_t>(time_out_)] != PXG_INT64)
+        return Err(PXG_INVALID_ARGUMENT, "Union time_ column is not TIME64NS");
+      rows_per_batch_ = op.union_rows_per_batch ? static_cast<int64_t>(op.union_rows_per_batch) : kDefaultRowsPerBatch;
+      queue_.resize(inputs_.size());
+      cursor_.assign(inputs_.size(), 0);
+      ResetBuilders();
+      last_flush_ = std::chrono::steady_clock::now();
+    }
     return Status::OK();
   }
   Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t parent) override {
+    if (ordered_) {
+      queue_[parent].push_back(rb);
+      PurgeEmpty(parent);
+      PXC_RETURN_IF_ERROR(Merge(s));
+      if (!sent_eos_ && built_ > 0 && std::chrono::steady_clock::now() - last_flush_ > kFlushTimeout) return Flush(s);
+      return Status::OK();
+    }
     if (rb.eos) eos_[parent] = true;
-    bool all = true;
-    for (bool e : eos_) all = all && e;
     RowBatch out;
     out.num_rows = rb.num_rows;
     for (int64_t i : maps_[parent]) out.cols.push_back(rb.cols[static_cast<size_t>(i)]);
-    out.eow = out.eos = all;
+    out.eow = out.eos = AllEos();
     return SendRowBatchToChildren(s, out);
   }
 
  private:
+  struct Builder {
+    int32_t type = 0;
+    std::shared_ptr<OwnedColumn> col;
+  };
+  bool AllEos() const {
+    for (bool e : eos_)
+      if (!e) return false;
+    return true;
+  }
+  void ResetBuilders() {
+    builders_.assign(output_.size(), Builder{});
+    for (size_t c = 0; c < output_.size(); ++c) {
+      builders_[c].type = output_[c];
+      builders_[c].col = std::make_shared<OwnedColumn>();
+      if (output_[c] == PXG_STRING) builders_[c].col->offsets.push_back(0);
+    }
+    built_ = 0;
+  }
+  // CacheNextRowBatch (union_node.cc:240-258): drop leading zero-row batches, noting their eos.
+  void PurgeEmpty(size_t p) {
+    auto& q = queue_[p];
+    while (!q.empty() && q.front().num_rows == 0) {
+      if (q.front().eos) eos_[p] = true;
+      q.pop_front();
+    }
+  }
+  int64_t TimeAt(size_t p) const {
+    const RowBatch& rb = queue_[p].front();
+    return static_cast<const int64_t*>(rb.cols[static_cast<size_t>(maps_[p][static_cast<size_t>(time_out_)])].values)[cursor_[p]];
+  }
+  // Copies rows [r0, r1) of parent p's front batch into the output builders.
+  void AppendRun(size_t p, int64_t r0, int64_t r1) {
+    const RowBatch& rb = queue_[p].front();
+    for (size_t c = 0; c < builders_.size(); ++c) {
+      const HostColumn& in = rb.cols[static_cast<size_t>(maps_[p][c])];
+      OwnedColumn& o = *builders_[c].col;
+      if (in.type == PXG_STRING) {
+        const int32_t a = in.offsets[r0], b = in.offsets[r1];
+        const int32_t base = o.offsets.back();
+        for (int64_t r = r0; r < r1; ++r) o.offsets.push_back(base + in.offsets[r + 1] - a);
+        o.data.insert(o.data.end(), in.data + a, in.data + b);
+      } else {
+        const int w = in.type == B ? 1 : in.type == U ? 16 : 8;
+        const uint8_t* v = static_cast<const uint8_t*>(in.values);
+        o.values.insert(o.values.end(), v + r0 * w, v + r1 * w);
+      }
+    }
+    built_ += r1 - r0;
+  }
+  Status Flush(ExecState* s) {
+    const bool eos = AllEos();
+    RowBatch out;
+    out.num_rows = built_;
+    for (auto& b : builders_) {
+      HostColumn hc;
+      hc.type = b.type;
+      hc.length = built_;
+      if (b.type == PXG_STRING) {
+        b.col->data.resize(b.col->data.size() + 16, 0);
+        hc.offsets = b.col->offsets.data();
+        hc.data = b.col->data.data();
+      } else {
+        b.col->values.resize(b.col->values.size() + 16, 0);
+        hc.values = b.col->values.data();
+      }
+      hc.owner = b.col;
+      out.cols.push_back(hc);
+    }
+    out.eow = out.eos = eos;
+    ResetBuilders();
+    last_flush_ = std::chrono::steady_clock::now();
+    if (eos) sent_eos_ = true;
+    return SendRowBatchToChildren(s, out);
+  }
+  Status FlushIfFullOrEos(ExecState* s) {
+    if (built_ < rows_per_batch_ && !AllEos()) return Status::OK();
+    return Flush(s);
+  }
+  // MergeData (union_node.cc:172-238).
+  Status Merge(ExecState* s) {
+    while (!sent_eos_) {
+      std::vector<size_t> live;
+      for (size_t p = 0; p < queue_.size(); ++p) {
+        if (eos_[p]) continue;
+        if (queue_[p].empty()) return Status::OK();  // a parent without data stalls the merge
+        live.push_back(p);
+      }
+      if (live.empty()) return FlushIfFullOrEos(s);
+      std::sort(live.begin(), live.end(), [this](size_t a, size_t b) {
+        const int64_t ta = TimeAt(a), tb = TimeAt(b);
+        return ta < tb || (ta == tb && a < b);
+      });
+      const size_t p = live[0];
+      const bool limited = live.size() > 1;
+      const size_t q = limited ? live[1] : 0;
+      const int64_t tq = limited ? TimeAt(q) : 0;
+      while (!queue_[p].empty()) {
+        const RowBatch& rb = queue_[p].front();
+        const int64_t* t = static_cast<const int64_t*>(rb.cols[static_cast<size_t>(maps_[p][static_cast<size_t>(time_out_)])].values);
+        const int64_t r0 = cursor_[p], n = rb.num_rows;
+        const bool last = rb.eos;
+        const int64_t cap = r0 + (rows_per_batch_ - built_);
+        const int64_t stop = std::min(n, cap);
+        int64_t r1 = r0;
+        if (limited) {
+          while (r1 < stop && (t[r1] < tq || (t[r1] == tq && p < q))) ++r1;
+        } else {
+          r1 = stop;
+        }
+        if (r1 > r0) AppendRun(p, r0, r1);
+        cursor_[p] = r1;
+        if (r1 == n) {  // `rb` is released here
+          if (last) eos_[p] = true;
+          queue_[p].pop_front();
+          cursor_[p] = 0;
+          PurgeEmpty(p);
+        }
+        if (r1 > r0) PXC_RETURN_IF_ERROR(FlushIfFullOrEos(s));
+        if (r1 < stop) break;  // the runner-up's time is next
+      }
+    }
+    return Status::OK();
+  }
+
   std::vector<std::vector<int64_t>> maps_;
   std::vector<bool> eos_;
+  bool ordered_ = false;
+  int64_t time_out_ = -1;
+  int64_t rows_per_batch_ = kDefaultRowsPerBatch;
+  std::vector<std::deque<RowBatch>> queue_;
+  std::vector<int64_t> cursor_;
+  std::vector<Builder> builders_;
+  int64_t built_ = 0;
+  bool sent_eos_ = false;
+  std::chrono::steady_clock::time_point last_flush_;
 };
 
 // GRPCSourceNode (grpc_source_node.cc:52-87): RowBatches received from a remote GRPCSink, in
@@ -2014,6 +2181,10 @@ class DeviceSourceNode : public SourceNode {
     }
     const int64_t end = std::min(hi_, cur_ + kBatchRows);
     RowBatch rb;
+    if (ms_.streaming && end <= cur_) {  // caught up: nothing ready (NextBatchReady false)
+      done_ = true;
+      return Status::OK();
+    }
     if (end <= cur_) {
       rb = ZeroRowBatch(output_, true, true);
     } else {
@@ -2023,17 +2194,16 @@ class DeviceSourceNode : public SourceNode {
         PXG_CALL(pxg_table_fetch(st_->t, static_cast<int32_t>(c), cur_, end, &o));
         rb.cols.push_back(FromOut(o));
       }
-      rb.eow = rb.eos = end >= hi_;
+      rb.eow = rb.eos = end >= hi_ && !ms_.streaming;  // an infinite stream never ends its window
     }
     cur_ = end;
-    done_ = rb.eos;
+    done_ = rb.eos || (ms_.streaming && cur_ >= hi_);
     return SendRowBatchToChildren(s, rb);
   }
 
  protected:
   Status InitImpl(const planpb::Operator& op) override {
     const planpb::MemorySourceOperator& ms = op.mem_source;
-    if (ms.streaming) return Err(PXG_UNIMPLEMENTED, "streaming MemorySource (infinite stream) is not supported");
     idxs_ = ms.column_idxs;
     if (idxs_.empty())
       for (size_t c = 0; c < st_->types.size(); ++c) idxs_.push_back(static_cast<int64_t>(c));
@@ -2425,6 +2595,9 @@ class ExecutionGraph {
     PXC_RETURN_IF_ERROR(src->Init(op, src_types, {}));
     sources_.push_back(src);
     (*built)[id] = src;
+    // An infinite stream never reaches eos, so a blocking agg below it never emits: it is not
+    // fused (the source's batches go through the ordinary nodes).
+    if (ms.streaming) return Status::OK();
 
     std::vector<uint64_t> chain;
     uint64_t agg_id = 0;

@@ -220,6 +220,7 @@ struct Operator {  // plan.proto:82-110
   std::vector<std::string> grpc_source_names;
   std::vector<std::string> union_names;              // UnionOperator (plan.proto:283-295)
   std::vector<std::vector<int64_t>> union_mappings;  // per parent: input column of each output column
+  uint64_t union_rows_per_batch = 0;                 // 0: kDefaultUnionRowBatchSize (union_node.h:41)
 };
 
 struct PlanNode {
@@ -491,6 +492,8 @@ inline void Decode(Reader r, Operator* op) {
               else m.Skip(mw);
             }
             op->union_mappings.push_back(idx);
+          } else if (sf == 3) {
+            op->union_rows_per_batch = s.Varint();
           } else {
             s.Skip(sw);
           }

@@ -108,7 +108,7 @@ def agg_op(groups: Sequence[int], values: Sequence, group_names: Sequence[str] =
 
 
 def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Sequence[int],
-              start_time: int = None, stop_time: int = None):
+              start_time: int = None, stop_time: int = None, streaming: bool = False):
     op = planpb.Operator()
     op.op_type = 1000
     m = op.mem_source_op
@@ -120,6 +120,8 @@ def source_op(name: str, types: Sequence[int], names: Sequence[str], idxs: Seque
         m.start_time.value = start_time
     if stop_time is not None:
         m.stop_time.value = stop_time
+    if streaming:
+        m.streaming = True
     return op
 
 
@@ -377,11 +379,13 @@ def grpc_source_op(types: Sequence[int], names: Sequence[str]):
     return op
 
 
-def union_op(names: Sequence[str], mappings: Sequence[Sequence[int]]):
+def union_op(names: Sequence[str], mappings: Sequence[Sequence[int]], rows_per_batch: int = 0):
     """UnionOperator (plan.proto:283-295)."""
     op = planpb.Operator()
     op.op_type = 2400
     op.union_op.column_names.extend(names)
+    if rows_per_batch:
+        op.union_op.rows_per_batch = rows_per_batch
     for m in mappings:
         op.union_op.column_mappings.add().column_indexes.extend(m)
     return op

@@ -124,12 +124,10 @@ def test_kelvin_fragment_lowers_to_grpc_sources_union_and_merge_agg():
     assert "GrpcSinkNode(-> grpc source 100)" in pem and "fused" in pem
 
 
-def test_time_ordered_union_is_unimplemented():
+def test_time_ordered_union_lowers_to_the_merge():
     plan = P.dag_plan([(1, P.grpc_source_op([TIME64NS], ["time_"]), []), (2, P.grpc_source_op([TIME64NS], ["time_"]), []),
                        (3, P.union_op(["time_"], [[0], [0]]), [1, 2]), (4, P.sink_op("out"), [3])])
-    with pytest.raises(H.PxcError) as e:
-        H.explain(plan, {})
-    assert e.value.code == 10
+    assert "UnionNode(ordered by time_)" in H.explain(plan, {})
 
 
 # ------------------------------------------------------------------------------------------
