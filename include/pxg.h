@@ -303,7 +303,8 @@ typedef struct {
   int64_t key_arena_bytes;  /* published group-key records */
   int64_t staging_capacity; /* staged rows the buffers hold without growing */
   int32_t fast_path_keys;   /* key count of the register-key consume kernel; 0 = generic kernel */
-  int32_t reserved;
+  int32_t big_sort_groups;  /* last finalize: big quantile groups the selection path handed to the
+                               full sort path (NaN values, a gathered bin > 16384 values) */
 } pxg_agg_stats;
 int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* stats);
 

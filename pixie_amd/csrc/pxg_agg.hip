@@ -1141,7 +1141,7 @@ extern "C" int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* st) {
   st->key_arena_bytes = static_cast<int64_t>(a.arena_words * 8);
   st->staging_capacity = static_cast<int64_t>(a.st_cap);
   st->fast_path_keys = a.fast_nk;
-  st->reserved = 0;
+  st->big_sort_groups = static_cast<int32_t>(a.last_big_sort_groups);
   return PXG_OK;
 }
 

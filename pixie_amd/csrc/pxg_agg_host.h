@@ -58,6 +58,7 @@ struct Agg {
   std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
+  uint32_t last_big_sort_groups = 0;  // pxg_agg_stats.big_sort_groups
   uint64_t inserted = 0;     // host mirror
 
   // Staging (one record per selected row).

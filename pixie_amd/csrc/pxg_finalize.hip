@@ -1134,11 +1134,17 @@ __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restric
 // gather beyond LDS capacity: heavy duplicates, too many bins) is flagged; finalize then runs
 // the full sort + merge path (BigChunkSort / BigMergeTile / BigDigest) for the big groups.
 // ---------------------------------------------------------------------------------------
-constexpr int kSelBins = 1024;
-constexpr int kSelSample = 2048;  // two samples per bin
+// 4096 bins keep the gathered bins of a multi-million-value group (the largest C2 group at
+// 1B rows holds ~6.9M values: ~1.7K per bin) far below the largest LDS sort (16384 keys).
+constexpr int kSelBins = 4096;
+constexpr int kSelBinBits = 12;
+constexpr int kSelSample = 8192;  // two samples per bin
+constexpr int kSelSampleThreads = kSelSample / kMsIpt;
 constexpr int kSelMaxRanges = kNeed;
 constexpr int kSelMaxColl = 256;
-constexpr uint32_t kSelCollCap = kMidMax;
+constexpr int kSelHugeThreads = 1024;
+constexpr uint32_t kSelCollCap = kSelHugeThreads * kMsIpt;  // 16384
+constexpr int kSelLists = 3;  // gathered bins: <= 1024 values (wave), <= 4096 (256 threads), larger (1024 threads)
 constexpr uint8_t kTagColl = 0x80;
 
 struct BigPlan {
@@ -1175,7 +1181,7 @@ __device__ __forceinline__ int BinOfRank(const uint32_t* bs, uint32_t r) {
 
 // Splitters: kSelSample keys at evenly spaced positions of the group, sorted; S[b] = every
 // (kSelSample / kSelBins)-th of them, S[0] = 0.
-__global__ void __launch_bounds__(256) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
+__global__ void __launch_bounds__(kSelSampleThreads) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
                                                        const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl) {
   if (blockIdx.x >= *nbig_p) return;
   __shared__ uint64_t keys[PaddedLen(kSelSample)];
@@ -1388,20 +1394,21 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
     atomicAdd(n_fallback, 1u);
   }
   // The gathered bins join the global sort lists (<= kWaveSortMax values: list 0, one wave
-  // each; larger: list 1, one workgroup each), entries (group << 11) | bin.
-  __shared__ uint32_t s_lc[2], s_lb[2];
-  if (t < 2) s_lc[t] = 0;
+  // each; <= kMidMax: list 1, one workgroup each; larger: list 2, one 1024-thread workgroup
+  // each), entries (group << kSelBinBits) | bin.
+  __shared__ uint32_t s_lc[kSelLists], s_lb[kSelLists];
+  if (t < kSelLists) s_lc[t] = 0;
   __syncthreads();
   const bool listed = !s_fb && t < P.n_coll;
   uint32_t my_list = 0, my_pos = 0, my_entry = 0;
   if (listed) {
     const int b = P.coll[t];
-    my_list = H[b] > static_cast<uint32_t>(kWaveSortMax) ? 1u : 0u;
+    my_list = H[b] > static_cast<uint32_t>(kMidMax) ? 2u : H[b] > static_cast<uint32_t>(kWaveSortMax) ? 1u : 0u;
     my_pos = atomicAdd(&s_lc[my_list], 1u);
-    my_entry = (bi << 11) | static_cast<uint32_t>(b);
+    my_entry = (bi << kSelBinBits) | static_cast<uint32_t>(b);
   }
   __syncthreads();
-  if (t < 2 && s_lc[t]) s_lb[t] = atomicAdd(&list_cnt[t], s_lc[t]);
+  if (t < kSelLists && s_lc[t]) s_lb[t] = atomicAdd(&list_cnt[t], s_lc[t]);
   __syncthreads();
   if (listed && H[P.coll[t]] > 1) bin_lists[my_list * list_cap + s_lb[my_list] + my_pos] = my_entry;
   else if (listed) bin_lists[my_list * list_cap + s_lb[my_list] + my_pos] = 0xFFFFFFFFu;  // nothing to sort
@@ -1486,7 +1493,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
 // (BigBinSortLargeKernel).
 __device__ __forceinline__ uint64_t* BinOfEntry(uint32_t e, const BigGroup* __restrict__ groups, const uint32_t* __restrict__ hist,
                                                  const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand, int* n) {
-  const uint32_t bi = e >> 11, b = e & 2047u;
+  const uint32_t bi = e >> kSelBinBits, b = e & (kSelBins - 1u);
   *n = static_cast<int>(hist[static_cast<uint64_t>(bi) * kSelBins + b]);
   return cand + groups[bi].off + cbase_all[static_cast<uint64_t>(bi) * kSelBins + b];
 }
@@ -1515,6 +1522,26 @@ __global__ void __launch_bounds__(256) BigBinSortLargeKernel(const BigGroup* __r
                                                              const uint32_t* __restrict__ list_cnt, const uint32_t* __restrict__ hist,
                                                              const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand) {
   __shared__ uint64_t keys[PaddedLen(kMidMax)];
+  const uint32_t cnt = *list_cnt;
+  for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
+    const uint32_t e = list[j];
+    if (e == 0xFFFFFFFFu) continue;
+    int n;
+    uint64_t* a = BinOfEntry(e, groups, hist, cbase_all, cand, &n);
+    int Pn = kMsIpt;
+    while (Pn < n) Pn <<= 1;
+    for (int i = threadIdx.x; i < Pn; i += blockDim.x) keys[PadIdx(i)] = i < n ? a[i] : ~0ULL;
+    __syncthreads();
+    BlockMergeSortLds(keys, Pn);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = keys[PadIdx(i)];
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kSelHugeThreads) BigBinSortHugeKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ list,
+                                                                         const uint32_t* __restrict__ list_cnt, const uint32_t* __restrict__ hist,
+                                                                         const uint32_t* __restrict__ cbase_all, uint64_t* __restrict__ cand) {
+  __shared__ uint64_t keys[PaddedLen(static_cast<int>(kSelCollCap))];
   const uint32_t cnt = *list_cnt;
   for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
     const uint32_t e = list[j];
@@ -1892,7 +1919,7 @@ int32_t AggFinalizeImpl(Agg* a) {
     const int at = a->uda_arg_type[u];
     const uint64_t nb = n_big_groups;
     PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4 + 16, ctx->side2));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel, dim3(n_big_groups), dim3(256), 0,
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel, dim3(n_big_groups), dim3(kSelSampleThreads), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), vals, at, ws.sel_spl.as<uint64_t>()));
     return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3(n_bchunks), dim3(256), 0, ws.bchunks.as<const BigChunk>(),
                     static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_cnt.as<uint32_t>(),
@@ -1926,6 +1953,11 @@ int32_t AggFinalizeImpl(Agg* a) {
                                  dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(256), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists + list_cap),
                                  static_cast<const uint32_t*>(list_cnt + 1), static_cast<const uint32_t*>(hist),
+                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortHugeKernel,
+                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(kSelHugeThreads), 0,
+                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists + 2 * list_cap),
+                                 static_cast<const uint32_t*>(list_cnt + 2), static_cast<const uint32_t*>(hist),
                                  ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
     return LaunchOn(ctx, ctx->side2, "quant_sel_digest", BigSelDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
                     static_cast<const uint32_t*>(d_cls + 3), ws.sel_plan.as<const BigPlan>(), chain_starts_big,
@@ -2007,7 +2039,7 @@ int32_t AggFinalizeImpl(Agg* a) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8));
       PXG_RETURN_IF_ERROR(ws.sel_cnt.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * 4 + 16));
-      PXG_RETURN_IF_ERROR(ws.sel_list.Ensure(static_cast<size_t>(n_big) * kSelMaxColl * 2 * 4 + 16));
+      PXG_RETURN_IF_ERROR(ws.sel_list.Ensure(static_cast<size_t>(n_big) * kSelMaxColl * kSelLists * 4 + 16));
       PXG_RETURN_IF_ERROR(ws.sel_bstart.Ensure(static_cast<size_t>(n_big) * (kSelBins + 1) * 4));
       PXG_RETURN_IF_ERROR(ws.sel_tag.Ensure(static_cast<size_t>(n_big) * kSelBins));
       PXG_RETURN_IF_ERROR(ws.sel_cbase.Ensure(static_cast<size_t>(n_big) * kSelBins * 4));
@@ -2060,7 +2092,8 @@ int32_t AggFinalizeImpl(Agg* a) {
     if (a->key_types[k] == PXG_STRING) totals[k] = pin32[k];
   err = pin32[kMaxKeys];
   g_dev = pin32[kMaxKeys + 1];
-  const uint32_t n_fallback = pin32[kMaxKeys + 2];
+  const uint32_t n_fallback = big_select ? pin32[kMaxKeys + 2] : 0;
+  a->last_big_sort_groups = big_select ? n_fallback : n_big_groups;
   if (big_select && EnvFlag("PXG_DIAG_SEL")) {  // selection-path shape (tools/; one extra sync)
     std::vector<BigPlan> plans(n_big_groups);
     std::vector<uint32_t> hh(static_cast<size_t>(n_big_groups) * kSelBins);
