@@ -70,7 +70,10 @@ __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __re
   __shared__ uint32_t h[kRadixBuckets];
   h[threadIdx.x] = 0;  // kRadixBlock == kRadixBuckets
   __syncthreads();
-  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  // XCD-aware: neighbouring tiles (whose counts share hist lines, and whose digit runs share
+  // output lines in the scatter) run on one XCD, so their partial-line writes meet in one L2.
+  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
+  const uint64_t base = static_cast<uint64_t>(tile) * kRadixTile;
   uint32_t kk[kRadixItems];
 #pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
@@ -93,7 +96,7 @@ __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __re
     WaveHistAdd(h, (kk[k] >> shift) & (kRadixBuckets - 1), i < n);
   }
   __syncthreads();
-  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + blockIdx.x] = h[threadIdx.x];
+  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + tile] = h[threadIdx.x];
 }
 
 // Block d: digit d's total over all tiles (the digit bases come from these; per-tile atomics
@@ -169,10 +172,11 @@ __global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* _
   uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);  // as in RsHistKernel
   for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
-  gofs[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * ntiles + blockIdx.x];
+  gofs[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * ntiles + tile];
   WaveSync();
-  const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kRadixTile;
+  const uint64_t tile0 = static_cast<uint64_t>(tile) * kRadixTile;
   const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
   const int tn = static_cast<int>(min(static_cast<uint64_t>(kRadixTile), n - tile0));
   uint32_t part[kRadixItems], keys[kRadixItems], dig[kRadixItems];
@@ -1145,6 +1149,13 @@ constexpr int kSelMaxColl = 256;
 constexpr int kSelHugeThreads = 1024;
 constexpr uint32_t kSelCollCap = kSelHugeThreads * kMsIpt;  // 16384
 constexpr int kSelLists = 3;  // gathered bins: <= 1024 values (wave), <= 4096 (256 threads), larger (1024 threads)
+
+// Bins actually used by a group of n values (the rest hold splitter ~0 and stay empty): <= 2048
+// values per bin on average, so a gathered bin beyond kSelCollCap is a ~1e-6 event per bin;
+// small big groups keep the small sample and the short splitter loads.
+__device__ __forceinline__ int SelNb(uint64_t n) {
+  return n > (uint64_t(1) << 22) ? kSelBins : n > (uint64_t(1) << 21) ? kSelBins / 2 : kSelBins / 4;
+}
 constexpr uint8_t kTagColl = 0x80;
 
 struct BigPlan {
@@ -1186,14 +1197,15 @@ __global__ void __launch_bounds__(kSelSampleThreads) BigSampleKernel(const BigGr
   if (blockIdx.x >= *nbig_p) return;
   __shared__ uint64_t keys[PaddedLen(kSelSample)];
   const BigGroup G = groups[blockIdx.x];
-  for (int j = threadIdx.x; j < kSelSample; j += blockDim.x) {
-    const uint64_t pos = (static_cast<uint64_t>(2 * j + 1) * G.n) / (2 * kSelSample);
+  const int nb = SelNb(G.n), ns = 2 * nb;
+  for (int j = threadIdx.x; j < ns; j += blockDim.x) {
+    const uint64_t pos = (static_cast<uint64_t>(2 * j + 1) * G.n) / (2 * static_cast<uint64_t>(ns));
     keys[PadIdx(j)] = QKey(vals[G.off + pos], arg_type);
   }
   __syncthreads();
-  BlockMergeSortLds(keys, kSelSample);
+  BlockMergeSortLds(keys, ns);
   uint64_t* S = spl + static_cast<uint64_t>(blockIdx.x) * kSelBins;
-  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) S[b] = b == 0 ? 0ULL : keys[PadIdx(b * (kSelSample / kSelBins))];
+  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) S[b] = b == 0 ? 0ULL : b < nb ? keys[PadIdx(2 * b)] : ~0ULL;
 }
 
 // Bin counts (and NaN count) per big group; one workgroup per 4096-value chunk.
@@ -1205,9 +1217,10 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
   __shared__ uint32_t h[kSelBins];
   __shared__ uint32_t s_nan;
   const BigChunk c = chunks[blockIdx.x];
+  const int nb = SelNb(c.g_n);
   const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
   for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) {
-    S[b] = Sg[b];
+    S[b] = b < nb ? Sg[b] : ~0ULL;
     h[b] = 0;
   }
   if (threadIdx.x == 0) s_nan = 0;
@@ -1232,7 +1245,7 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
   if (nn) atomicAdd(&s_nan, nn);
   __syncthreads();
   uint32_t* H = hist + static_cast<uint64_t>(c.bidx) * kSelBins;
-  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x)
+  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x)  // bins >= nb only see all-ones keys
     if (h[b]) atomicAdd(&H[b], h[b]);
   if (threadIdx.x == 0 && s_nan) atomicAdd(&nan_cnt[c.bidx], s_nan);
 }
@@ -1440,11 +1453,12 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
   __shared__ uint8_t tg[kSelBins];
   __shared__ double acc[4][kSelMaxRanges];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int nb = SelNb(c.g_n);
   const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
   const uint8_t* Tg = tag_all + static_cast<uint64_t>(c.bidx) * kSelBins;
   for (int b = t; b < kSelBins; b += 256) {
-    S[b] = Sg[b];
-    tg[b] = Tg[b];
+    S[b] = b < nb ? Sg[b] : ~0ULL;
+    tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
   }
   if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
   constexpr int kRounds = kMidMax / 256;
