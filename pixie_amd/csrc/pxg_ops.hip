@@ -111,7 +111,7 @@ struct GatherCols {
   const int32_t* src_off[kMaxCols];   // STRING offsets
   uint8_t* dst[kMaxCols];             // fixed output values
   uint32_t* dst_len[kMaxCols];        // STRING: length of output row (scanned to offsets later)
-  uint32_t* dst_src[kMaxCols];        // STRING: source row of output row
+  uint32_t* dst_src[kMaxCols];        // STRING: source payload byte offset of output row
 };
 
 // Pass 2: rank every selected row (tile base + prefix of the tile's ballot popcounts + the
@@ -135,46 +135,108 @@ __global__ void __launch_bounds__(kOpsBlock) FilterGatherKernel(const unsigned l
   }
   __syncthreads();
   const uint32_t base = tile_base[blockIdx.x];
+  // Every selected row of the wave's 16 ballot words is placed first; then each column's loads
+  // for all of them are issued together (16 in flight per lane) before the stores.
+  uint32_t sel = 0, pos[kOpsMasksPerWave];
+#pragma unroll
   for (int k = 0; k < kOpsMasksPerWave; ++k) {
     const int mi = wid * kOpsMasksPerWave + k;
     const unsigned long long m = masks[mask0 + mi];
-    if (!((m >> lane) & 1ULL)) continue;
-    const int64_t r = lo + static_cast<int64_t>(blockIdx.x) * kOpsTileRows + mi * 64 + lane;
-    const uint32_t pos = base + s_pre[mi] + static_cast<uint32_t>(__popcll(m & lanemask_lt));
-    for (int c = 0; c < gc.n; ++c) {
-      const int w = gc.width[c];
-      if (w == 8) {
-        reinterpret_cast<uint64_t*>(gc.dst[c])[pos] = reinterpret_cast<const uint64_t*>(gc.src[c])[r];
-      } else if (w == 16) {
-        reinterpret_cast<ulonglong2*>(gc.dst[c])[pos] = reinterpret_cast<const ulonglong2*>(gc.src[c])[r];
-      } else if (w == 1) {
-        gc.dst[c][pos] = gc.src[c][r];
-      } else {
-        gc.dst_len[c][pos] = static_cast<uint32_t>(gc.src_off[c][r + 1] - gc.src_off[c][r]);
-        gc.dst_src[c][pos] = static_cast<uint32_t>(r);
+    sel |= static_cast<uint32_t>((m >> lane) & 1ULL) << k;
+    pos[k] = base + s_pre[mi] + static_cast<uint32_t>(__popcll(m & lanemask_lt));
+  }
+  if (!sel) return;
+  const int64_t r0 = lo + static_cast<int64_t>(blockIdx.x) * kOpsTileRows + wid * kOpsMasksPerWave * 64 + lane;
+  for (int c = 0; c < gc.n; ++c) {
+    const int w = gc.width[c];
+    if (w == 8) {
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(gc.src[c]) + r0;
+      uint64_t* dst = reinterpret_cast<uint64_t*>(gc.dst[c]);
+      uint64_t v[kOpsMasksPerWave];
+#pragma unroll
+      for (int k = 0; k < kOpsMasksPerWave; ++k) v[k] = (sel >> k) & 1 ? src[k * 64] : 0ULL;
+#pragma unroll
+      for (int k = 0; k < kOpsMasksPerWave; ++k)
+        if ((sel >> k) & 1) dst[pos[k]] = v[k];
+    } else if (w == 0) {
+      const int32_t* off = gc.src_off[c] + r0;
+      int32_t a[kOpsMasksPerWave], b[kOpsMasksPerWave];
+#pragma unroll
+      for (int k = 0; k < kOpsMasksPerWave; ++k) {
+        a[k] = (sel >> k) & 1 ? off[k * 64] : 0;
+        b[k] = (sel >> k) & 1 ? off[k * 64 + 1] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kOpsMasksPerWave; ++k)
+        if ((sel >> k) & 1) {
+          gc.dst_len[c][pos[k]] = static_cast<uint32_t>(b[k] - a[k]);
+          gc.dst_src[c][pos[k]] = static_cast<uint32_t>(a[k]);
+        }
+    } else {
+      for (int k = 0; k < kOpsMasksPerWave; ++k) {
+        if (!((sel >> k) & 1)) continue;
+        const int64_t r = r0 + k * 64;
+        if (w == 16) reinterpret_cast<ulonglong2*>(gc.dst[c])[pos[k]] = reinterpret_cast<const ulonglong2*>(gc.src[c])[r];
+        else gc.dst[c][pos[k]] = gc.src[c][r];
       }
     }
   }
   (void)n;
 }
 
-// Word-wise string gather: output row i gets the bytes of source row src[i].
-__global__ void StrGatherKernel(const int32_t* __restrict__ soff, const uint8_t* __restrict__ sdata, const uint32_t* __restrict__ src,
-                                const uint32_t* __restrict__ doff, uint8_t* __restrict__ ddata, int64_t m) {
+// String payload gather: output row i gets len = doff[i + 1] - doff[i] bytes from source byte
+// offset src[i] (recorded by the gather pass, so no dependent offset load here).  Copies are
+// unaligned 16 / 8 / 4-byte moves (gfx950 serves them in hardware); the last move of a string
+// overlaps the previous one and ends exactly at len, so a thread never writes outside its own
+// string and there is no byte-by-byte tail.  All loads of a string are issued before its stores.
+template <int W>
+struct Word;
+template <>
+struct Word<16> { using T = ulonglong2; };
+template <>
+struct Word<8> { using T = uint64_t; };
+template <>
+struct Word<4> { using T = uint32_t; };
+template <int W>
+__device__ __forceinline__ typename Word<W>::T LoadU(const uint8_t* p) {
+  typename Word<W>::T x;
+  __builtin_memcpy(&x, p, W);
+  return x;
+}
+template <int W>
+__device__ __forceinline__ void StoreU(uint8_t* p, typename Word<W>::T x) { __builtin_memcpy(p, &x, W); }
+
+__global__ void StrGatherKernel(const uint8_t* __restrict__ sdata, const uint32_t* __restrict__ src, const uint32_t* __restrict__ doff,
+                                uint8_t* __restrict__ ddata, int64_t m) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  const uint32_t r = src[i];
-  const int32_t a = soff[r];
-  const uint32_t len = static_cast<uint32_t>(soff[r + 1] - a);
-  const uint8_t* s = sdata + a;
-  uint8_t* d = ddata + doff[i];
-  uint32_t k = 0;
-  for (; k + 8 <= len; k += 8) {
-    uint64_t x;
-    __builtin_memcpy(&x, s + k, 8);
-    __builtin_memcpy(d + k, &x, 8);
+  const uint32_t o0 = doff[i];
+  const uint32_t len = doff[i + 1] - o0;
+  const uint8_t* s = sdata + src[i];
+  uint8_t* d = ddata + o0;
+  if (len >= 16) {
+    if (len <= 48) {  // the common case: at most three 16-byte moves, loads first
+      const ulonglong2 a = LoadU<16>(s), c = LoadU<16>(s + len - 16);
+      const ulonglong2 b = len > 32 ? LoadU<16>(s + 16) : a;
+      StoreU<16>(d, a);
+      if (len > 32) StoreU<16>(d + 16, b);
+      StoreU<16>(d + len - 16, c);
+    } else {
+      uint32_t k = 0;
+      for (; k + 16 < len; k += 16) StoreU<16>(d + k, LoadU<16>(s + k));
+      StoreU<16>(d + len - 16, LoadU<16>(s + len - 16));
+    }
+  } else if (len >= 8) {
+    const uint64_t a = LoadU<8>(s), b = LoadU<8>(s + len - 8);
+    StoreU<8>(d, a);
+    StoreU<8>(d + len - 8, b);
+  } else if (len >= 4) {
+    const uint32_t a = LoadU<4>(s), b = LoadU<4>(s + len - 4);
+    StoreU<4>(d, a);
+    StoreU<4>(d + len - 4, b);
+  } else {
+    for (uint32_t k = 0; k < len; ++k) d[k] = s[k];
   }
-  for (; k < len; ++k) d[k] = s[k];
 }
 
 __global__ void MapEvalKernel(const DevProgram* __restrict__ prog, const DevChunk* __restrict__ chunks, int chunk,
@@ -370,8 +432,7 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
         dc.data_len = bytes;
         if (p.m > 0)
           PXG_RETURN_IF_ERROR(Launch(ctx, "str_gather", StrGatherKernel, dim3(GridFor(p.m, 256, 1 << 30)), dim3(256), 0,
-                                     ch.cols[ci].offsets.as<const int32_t>(), ch.cols[ci].data.as<const uint8_t>(),
-                                     static_cast<const uint32_t*>(gcs[i].dst_src[s]), static_cast<const uint32_t*>(gcs[i].dst_len[s]),
+                                     ch.cols[ci].data.as<const uint8_t>(), static_cast<const uint32_t*>(gcs[i].dst_src[s]), static_cast<const uint32_t*>(gcs[i].dst_len[s]),
                                      dc.data.as<uint8_t>(), static_cast<int64_t>(p.m)));
         ++si;
       }

@@ -322,3 +322,27 @@ def test_device_join_hot_key_and_scale(ctx):
     sums = np.bincount(bkey.astype(np.int64), weights=bpay.astype(np.float64), minlength=50_000)
     assert abs(float(bp.astype(np.float64).sum()) - float(sums[pkey.astype(np.int64)].sum())) < 1e-3 * float(bp.sum())
     out.close(); B.close(); Pt.close()
+
+
+def test_standalone_filter_string_lengths(ctx):
+    """Filter compaction of STRING columns whose lengths cover every copy path of the payload
+    gather (0..3 bytes, 4..7, 8..15, 16..48, > 48) next to INT64 / BOOLEAN / UINT128 columns,
+    bit-exact and in order against the CPU restatement (FilterNode, filter_node.cc:78-171)."""
+    rng = np.random.default_rng(41)
+    n = 70_000
+    lens = np.concatenate([np.arange(0, 130), rng.integers(0, 130, n - 130)])
+    alphabet = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789/-_.", dtype=np.uint8)
+    strs = [alphabet[rng.integers(0, len(alphabet), L)].tobytes().decode() for L in lens]
+    keep = rng.integers(0, 2, n)
+    cols = [Column(2, values=keep.astype(np.int64)), Column.from_values(5, strs),
+            Column(1, values=(rng.integers(0, 2, n)).astype(np.uint8)),
+            Column.from_values(3, [(int(a) << 64) | int(b) for a, b in zip(rng.integers(0, 2**62, n), rng.integers(0, 2**62, n))])]
+    tables = {"t": {"types": [2, 5, 1, 3], "batches": [cols]}}
+    plan = P.linear_plan([P.source_op("t", [2, 5, 1, 3], ["k", "s", "b", "u"], [0, 1, 2, 3]),
+                          P.filter_op(P.func("equal", [P.col(0), P.const(2, 1)], [2, 2]), [1, 2, 3, 0]),
+                          P.sink_op("out")])
+    ref = oc.execute_plan(plan, tables)["out"]
+    dev = run_plan(ctx, plan, tables)
+    assert len(ref) == len(dev) == 1
+    assert rows(ref[0]["cols"]) == rows(dev[0]["cols"])
+    assert dev[0]["rows"] == int(keep.sum())
