@@ -1190,14 +1190,18 @@ __device__ __forceinline__ int BinOfRank(const uint32_t* bs, uint32_t r) {
   return b;
 }
 
-// Splitters: kSelSample keys at evenly spaced positions of the group, sorted; S[b] = every
-// (kSelSample / kSelBins)-th of them, S[0] = 0.
-__global__ void __launch_bounds__(kSelSampleThreads) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
-                                                       const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl) {
+// Splitters: 2 * nb keys at evenly spaced positions of the group, sorted; S[b] = every second
+// of them (b < nb), S[0] = 0, S[b >= nb] = ~0 (empty bins).  Two launches: groups sampling
+// <= 4096 keys (256 threads, 35 KB of LDS) and the few sampling 8192 (512 threads, 70 KB), so
+// the common case is not held to the large kernel's occupancy.
+template <int NS>
+__global__ void __launch_bounds__(NS / kMsIpt) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
+                                                               const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl) {
   if (blockIdx.x >= *nbig_p) return;
-  __shared__ uint64_t keys[PaddedLen(kSelSample)];
   const BigGroup G = groups[blockIdx.x];
   const int nb = SelNb(G.n), ns = 2 * nb;
+  if (ns > NS || (NS > kSelSample / 2 && ns <= kSelSample / 2)) return;  // the other launch's group
+  __shared__ uint64_t keys[PaddedLen(NS)];
   for (int j = threadIdx.x; j < ns; j += blockDim.x) {
     const uint64_t pos = (static_cast<uint64_t>(2 * j + 1) * G.n) / (2 * static_cast<uint64_t>(ns));
     keys[PadIdx(j)] = QKey(vals[G.off + pos], arg_type);
@@ -1208,46 +1212,72 @@ __global__ void __launch_bounds__(kSelSampleThreads) BigSampleKernel(const BigGr
   for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) S[b] = b == 0 ? 0ULL : b < nb ? keys[PadIdx(2 * b)] : ~0ULL;
 }
 
-// Bin counts (and NaN count) per big group; one workgroup per 4096-value chunk.
+// Bin counts (and NaN count) per big group.  A workgroup takes cpb consecutive 4096-value
+// chunks (a group's chunks are consecutive; cpb = SelChunksPerBlock, up to 8 while the grid
+// still fills the chip): the splitters are loaded and the LDS counts flushed to the group's
+// global histogram once per group it meets, not once per chunk.
+// BigCollect (per-chunk range sums, latency-bound gathers) wants more blocks in flight than
+// BigHist (whose per-group flush is the cost it saves), hence the larger per-CU target.
+static uint32_t SelChunksPerBlock(uint32_t nchunks, int num_cus, uint32_t blocks_per_cu) {
+  return std::max<uint32_t>(1, std::min<uint32_t>(8, nchunks / (blocks_per_cu * static_cast<uint32_t>(num_cus))));
+}
 __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                      const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
-                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ nan_cnt) {
-  if (blockIdx.x >= *nchunks_p) return;
+                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ nan_cnt, uint32_t cpb) {
+  const uint32_t nchunks = *nchunks_p;
+  const uint32_t c0 = blockIdx.x * cpb;
+  if (c0 >= nchunks) return;
+  const uint32_t c1 = min(nchunks, c0 + cpb);
   __shared__ uint64_t S[kSelBins];
   __shared__ uint32_t h[kSelBins];
   __shared__ uint32_t s_nan;
-  const BigChunk c = chunks[blockIdx.x];
-  const int nb = SelNb(c.g_n);
-  const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
-  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) {
-    S[b] = b < nb ? Sg[b] : ~0ULL;
-    h[b] = 0;
-  }
-  if (threadIdx.x == 0) s_nan = 0;
   constexpr int kPer = kMidMax / 256;
-  uint64_t raw[kPer];
+  uint32_t cur = 0xFFFFFFFFu;
+  int nb = 0;
+  for (uint32_t ci = c0; ci < c1; ++ci) {
+    const BigChunk c = chunks[ci];
+    uint64_t raw[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = k * 256 + threadIdx.x;
-    raw[k] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
-  }
-  __syncthreads();
-  uint32_t nn = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = k * 256 + threadIdx.x;
-    if (i < static_cast<int>(c.len)) {
-      const uint64_t key = QKey(raw[k], arg_type);
-      nn += (key < kNegInfKey || key > kPosInfKey) ? 1u : 0u;
-      atomicAdd(&h[SelBin(S, key)], 1u);
+    for (int k = 0; k < kPer; ++k) {
+      const int i = k * 256 + threadIdx.x;
+      raw[k] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
     }
+    if (c.bidx != cur) {
+      if (cur != 0xFFFFFFFFu) {  // flush the previous group's counts
+        __syncthreads();
+        uint32_t* H = hist + static_cast<uint64_t>(cur) * kSelBins;
+        for (int b = threadIdx.x; b < kSelBins; b += 256)
+          if (h[b]) atomicAdd(&H[b], h[b]);
+        if (threadIdx.x == 0 && s_nan) atomicAdd(&nan_cnt[cur], s_nan);
+        __syncthreads();
+      }
+      cur = c.bidx;
+      nb = SelNb(c.g_n);
+      const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
+      for (int b = threadIdx.x; b < kSelBins; b += 256) {
+        S[b] = b < nb ? Sg[b] : ~0ULL;
+        h[b] = 0;
+      }
+      if (threadIdx.x == 0) s_nan = 0;
+      __syncthreads();
+    }
+    uint32_t nn = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = k * 256 + threadIdx.x;
+      if (i < static_cast<int>(c.len)) {
+        const uint64_t key = QKey(raw[k], arg_type);
+        nn += (key < kNegInfKey || key > kPosInfKey) ? 1u : 0u;
+        atomicAdd(&h[SelBin(S, key)], 1u);
+      }
+    }
+    if (nn) atomicAdd(&s_nan, nn);
   }
-  if (nn) atomicAdd(&s_nan, nn);
   __syncthreads();
-  uint32_t* H = hist + static_cast<uint64_t>(c.bidx) * kSelBins;
-  for (int b = threadIdx.x; b < kSelBins; b += blockDim.x)  // bins >= nb only see all-ones keys
+  uint32_t* H = hist + static_cast<uint64_t>(cur) * kSelBins;
+  for (int b = threadIdx.x; b < kSelBins; b += 256)  // bins >= nb only see all-ones keys
     if (h[b]) atomicAdd(&H[b], h[b]);
-  if (threadIdx.x == 0 && s_nan) atomicAdd(&nan_cnt[c.bidx], s_nan);
+  if (threadIdx.x == 0 && s_nan) atomicAdd(&nan_cnt[cur], s_nan);
 }
 
 // Per big group: bin starts, the centroids the quantiles read (DigestQuantile's recording
@@ -1439,67 +1469,79 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
 // are sorted next) and sum the values inside each large range per chunk.  Sums are
 // deterministic: wave w takes chunk positions [1024 w, 1024 (w + 1)) in 16 rounds, each
 // round's values of one range are summed by a fixed shuffle tree, rounds and waves in order.
+// A workgroup takes cpb consecutive chunks (as BigHistKernel); splitters and tags are reloaded
+// only when the group changes.
 __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                         const BigPlan* __restrict__ plans, const uint64_t* __restrict__ vals, int arg_type,
                                                         const uint64_t* __restrict__ spl, const uint8_t* __restrict__ tag_all,
                                                         const uint32_t* __restrict__ cbase_all, uint32_t* __restrict__ cursor_all,
-                                                        uint64_t* __restrict__ cand, double* __restrict__ partial) {
-  if (blockIdx.x >= *nchunks_p) return;
-  const BigChunk c = chunks[blockIdx.x];
-  const BigPlan* P = plans + c.bidx;
-  if (P->fallback) return;
-  const int n_ranges = P->n_ranges;
+                                                        uint64_t* __restrict__ cand, double* __restrict__ partial, uint32_t cpb) {
+  const uint32_t nchunks = *nchunks_p;
+  const uint32_t c0 = blockIdx.x * cpb;
+  if (c0 >= nchunks) return;
+  const uint32_t c1 = min(nchunks, c0 + cpb);
   __shared__ uint64_t S[kSelBins];
   __shared__ uint8_t tg[kSelBins];
   __shared__ double acc[4][kSelMaxRanges];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int nb = SelNb(c.g_n);
-  const uint64_t* Sg = spl + static_cast<uint64_t>(c.bidx) * kSelBins;
-  const uint8_t* Tg = tag_all + static_cast<uint64_t>(c.bidx) * kSelBins;
-  for (int b = t; b < kSelBins; b += 256) {
-    S[b] = b < nb ? Sg[b] : ~0ULL;
-    tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
-  }
-  if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
   constexpr int kRounds = kMidMax / 256;
-  uint64_t raw[kRounds];
+  uint32_t cur = 0xFFFFFFFFu;
+  for (uint32_t ci = c0; ci < c1; ++ci) {
+    const BigChunk c = chunks[ci];
+    const BigPlan* P = plans + c.bidx;
+    if (P->fallback) continue;  // uniform
+    const int n_ranges = P->n_ranges;
+    uint64_t raw[kRounds];
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    const int i = wid * (kMidMax / 4) + r * 64 + lane;
-    raw[r] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
-  }
-  __syncthreads();
-  const uint32_t* cb = cbase_all + static_cast<uint64_t>(c.bidx) * kSelBins;
-  uint32_t* cur = cursor_all + static_cast<uint64_t>(c.bidx) * kSelBins;
-  uint64_t* cg = cand + c.g_off;
-  for (int r = 0; r < kRounds; ++r) {
-    const int i = wid * (kMidMax / 4) + r * 64 + lane;
-    int u = -1;
-    double v = 0.0;
-    if (i < static_cast<int>(c.len)) {
-      const uint64_t key = QKey(raw[r], arg_type);
-      const int b = SelBin(S, key);
-      const uint8_t tag = tg[b];
-      if (tag == kTagColl) {
-        const uint32_t slot = atomicAdd(&cur[b], 1u);
-        cg[cb[b] + slot] = key;
-      } else if (tag != 0) {
-        u = tag - 1;
-        v = QVal(key);
+    for (int r = 0; r < kRounds; ++r) {
+      const int i = wid * (kMidMax / 4) + r * 64 + lane;
+      raw[r] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
+    }
+    __syncthreads();  // the previous chunk's acc / S / tg readers are done
+    if (c.bidx != cur) {
+      cur = c.bidx;
+      const int nb = SelNb(c.g_n);
+      const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
+      const uint8_t* Tg = tag_all + static_cast<uint64_t>(cur) * kSelBins;
+      for (int b = t; b < kSelBins; b += 256) {
+        S[b] = b < nb ? Sg[b] : ~0ULL;
+        tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
       }
     }
-    unsigned long long pend = __ballot(u >= 0);
-    while (pend) {
-      const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
-      const bool mine = u == uu;
-      const double s = WaveSumF64(mine ? v : 0.0);
-      if (lane == 0) acc[wid][uu] += s;
-      pend &= ~__ballot(mine);
+    if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
+    __syncthreads();
+    const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
+    uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
+    uint64_t* cg = cand + c.g_off;
+    for (int r = 0; r < kRounds; ++r) {
+      const int i = wid * (kMidMax / 4) + r * 64 + lane;
+      int u = -1;
+      double v = 0.0;
+      if (i < static_cast<int>(c.len)) {
+        const uint64_t key = QKey(raw[r], arg_type);
+        const int b = SelBin(S, key);
+        const uint8_t tag = tg[b];
+        if (tag == kTagColl) {
+          const uint32_t slot = atomicAdd(&cc[b], 1u);
+          cg[cb[b] + slot] = key;
+        } else if (tag != 0) {
+          u = tag - 1;
+          v = QVal(key);
+        }
+      }
+      unsigned long long pend = __ballot(u >= 0);
+      while (pend) {
+        const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
+        const bool mine = u == uu;
+        const double sm = WaveSumF64(mine ? v : 0.0);
+        if (lane == 0) acc[wid][uu] += sm;
+        pend &= ~__ballot(mine);
+      }
     }
+    __syncthreads();
+    for (int u = t; u < n_ranges; u += 256)
+      partial[static_cast<uint64_t>(ci) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
   }
-  __syncthreads();
-  for (int u = t; u < n_ranges; u += 256)
-    partial[static_cast<uint64_t>(blockIdx.x) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
 }
 
 // Sort the gathered bins of the big groups, grid-stride over the lists BigPlan filled: bins
@@ -1933,11 +1975,17 @@ int32_t AggFinalizeImpl(Agg* a) {
     const int at = a->uda_arg_type[u];
     const uint64_t nb = n_big_groups;
     PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4 + 16, ctx->side2));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel, dim3(n_big_groups), dim3(kSelSampleThreads), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), vals, at, ws.sel_spl.as<uint64_t>()));
-    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3(n_bchunks), dim3(256), 0, ws.bchunks.as<const BigChunk>(),
-                    static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_cnt.as<uint32_t>(),
-                    ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins);
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(n_big_groups),
+                                 dim3(kSelSample / 2 / kMsIpt), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
+                                 vals, at, ws.sel_spl.as<uint64_t>()));
+    if (big_max > (uint64_t(1) << 22))
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_big_groups),
+                                   dim3(kSelSampleThreads), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
+                                   vals, at, ws.sel_spl.as<uint64_t>()));
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 2);
+    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
+                    ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
+                    ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);
   };
   // Second half, after the chains: plan, gather + inside sums, bin sorts, digests.
   auto BigSelectBack = [&](int u) -> int32_t {
@@ -1955,10 +2003,11 @@ int32_t AggFinalizeImpl(Agg* a) {
                                  static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), ws.sel_bstart.as<uint32_t>(),
                                  ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback, lists,
                                  list_cap, list_cnt));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3(n_bchunks), dim3(256), 0,
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 8);
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                                  ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
                                  vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_tag.as<const uint8_t>(),
-                                 ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>()));
+                                 ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>(), cpb));
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel,
                                  dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0,
                                  ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists), static_cast<const uint32_t*>(list_cnt),
