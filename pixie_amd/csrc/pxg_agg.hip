@@ -16,7 +16,13 @@ namespace pxg {
 
 constexpr int kConsumeBlock = 256;
 constexpr int kGenericTile = 4096;   // rows per workgroup tile of the generic kernel (16 per thread)
-constexpr int kConsumeTile = 16384;  // rows per workgroup tile of the fast kernel
+// Rows per workgroup tile of the fast kernel: 16384, or 32768 when the launch has enough
+// tiles for >= 8 rounds of resident workgroups (fewer phase-2 barriers per row; at 100M rows the
+// larger tiles lose more to the last round's imbalance than they gain: 1.42 -> 1.79 ms at
+// 32768, while 1B rows go 13.16 -> 12.93 ms; 65536 tiles: 13.59 ms).  Row offsets within a tile
+// are u16 in LDS.
+constexpr int kConsumeTile = 16384;
+constexpr int kConsumeTileMax = 32768;
 constexpr int kSelCap = 16384;       // selected rows collected before phase 2 runs (LDS)
 constexpr int kSubRows = 8192;       // rows per phase-1 sub-batch (32 per thread in flight)
 
@@ -25,7 +31,7 @@ struct TileRange {
   int64_t lo;     // local row range within the chunk
   int64_t hi;
   int32_t chunk;
-  int32_t pad;
+  int32_t tile_rows;  // rows per tile (fast kernel; the generic kernel uses kGenericTile)
 };
 
 constexpr uint32_t kMaxProbe = 256;  // longer probe sequences defer the row (table grows)
@@ -497,7 +503,7 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
 // (2) or after key load + hash (3) and write garbage slots (tools/consume_diag.py; never
 // followed by finalize).
 //
-// One workgroup per tile of kConsumeTile rows (grid-stride).  Phase 1 runs in sub-batches of
+// One workgroup per tile of rg.tile_rows rows (grid-stride).  Phase 1 runs in sub-batches of
 // kSubRows rows: every thread evaluates the predicate for 32 rows (32 independent loads in
 // flight), then the passing rows are compacted into LDS with per-wave ballots and one LDS
 // prefix over the 4 waves.  Phase 2 processes the compacted rows densely and appends one
@@ -512,7 +518,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
                                                                       int64_t ntiles, AggTableDev tab, StageDev stg,
                                                                       uint32_t nchunks) {
   constexpr int kPer = kSubRows / kConsumeBlock;
-  constexpr int kSubBatches = kConsumeTile / kSubRows;
+
   constexpr int kWaves = kConsumeBlock / 64;
   __shared__ uint16_t s_sel[kSelCap];
   __shared__ uint32_t s_wcnt[2][kWaves];
@@ -532,8 +538,9 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
     while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
     const TileRange rg = ranges[ri];
     const DevChunk& ch = chunks[rg.chunk];
-    const int64_t row0 = rg.lo + (t - rg.tile0) * kConsumeTile;
-    const int64_t row1 = min(row0 + kConsumeTile, rg.hi);
+    const int64_t row0 = rg.lo + (t - rg.tile0) * rg.tile_rows;
+    const int64_t row1 = min(row0 + rg.tile_rows, rg.hi);
+    const int kSubBatches = rg.tile_rows / kSubRows;
     uint32_t total = 0;
 #pragma unroll 1
     for (int sb = 0; sb < kSubBatches; ++sb) {
@@ -816,7 +823,17 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_RETURN_IF_ERROR(t->EnsureDeviceDescriptors());
   clk.Mark("consume: descriptors");
   if (t->chunks.size() > 255) return SetError(PXG_UNIMPLEMENTED, "tables are limited to 255 chunks per agg consume");
-  const int64_t tile_rows = fast_nk > 0 ? kConsumeTile : kGenericTile;
+  int64_t tile_rows = fast_nk > 0 ? kConsumeTile : kGenericTile;
+  if (fast_nk > 0) {
+    const int64_t rounds8 = static_cast<int64_t>(ctx->num_cus) * 4 * 8;  // 4 resident workgroups per CU
+    while (tile_rows < kConsumeTileMax && (end - begin) / (2 * tile_rows) >= rounds8) tile_rows *= 2;
+    static const int64_t forced = [] {  // tests: PXG_CONSUME_TILE=32768 / 65536 at small sizes
+      const char* e = std::getenv("PXG_CONSUME_TILE");
+      const int64_t v = e ? std::atoll(e) : 0;
+      return (v == 16384 || v == 32768 || v == 65536) ? v : 0;
+    }();
+    if (forced) tile_rows = forced;
+  }
   std::vector<TileRange> ranges;
   int64_t ntiles = 0;
   for (size_t c = 0; c < t->chunks.size(); ++c) {
@@ -829,7 +846,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     r.lo = lo;
     r.hi = hi;
     r.chunk = static_cast<int32_t>(c);
-    r.pad = 0;
+    r.tile_rows = static_cast<int32_t>(tile_rows);
     ranges.push_back(r);
     ntiles += (hi - lo + tile_rows - 1) / tile_rows;
   }
