@@ -1172,13 +1172,14 @@ struct BigPlan {
 
 static_assert(sizeof(BigPlan) % 4 == 0, "BigPlan is copied as words");
 
-// Bin of a sort key: the last b with S[b] <= key (S[0] = 0, S non-decreasing).
-__device__ __forceinline__ int SelBin(const uint64_t* S, uint64_t key) {
+// Bin of a sort key: the last b with S[b] <= key (S[0] = 0, S non-decreasing).  A group using
+// nb < kSelBins bins has S[b >= nb] = ~0: only an all-ones key lands there (bin kSelBins - 1),
+// so the search runs over [0, nb) and then checks that one case.
+__device__ __forceinline__ int SelBin(const uint64_t* S, uint64_t key, int nb) {
   int b = 0;
-#pragma unroll
-  for (int step = kSelBins / 2; step >= 1; step >>= 1)
+  for (int step = nb >> 1; step >= 1; step >>= 1)
     if (S[b + step] <= key) b += step;
-  return b;
+  return key == ~0ULL ? kSelBins - 1 : b;
 }
 // Bin holding rank r: the last b with bs[b] <= r (bs = exclusive prefix of the bin counts;
 // that bin is never empty since bs[b + 1] > r).
@@ -1202,9 +1203,20 @@ __global__ void __launch_bounds__(NS / kMsIpt) BigSampleKernel(const BigGroup* _
   const int nb = SelNb(G.n), ns = 2 * nb;
   if (ns > NS || (NS > kSelSample / 2 && ns <= kSelSample / 2)) return;  // the other launch's group
   __shared__ uint64_t keys[PaddedLen(NS)];
-  for (int j = threadIdx.x; j < ns; j += blockDim.x) {
-    const uint64_t pos = (static_cast<uint64_t>(2 * j + 1) * G.n) / (2 * static_cast<uint64_t>(ns));
-    keys[PadIdx(j)] = QKey(vals[G.off + pos], arg_type);
+  // ns is a power of two: position (2j + 1) n / (2 ns) by a shift; every load of a thread is
+  // issued before any is used.
+  const int sh = __ffs(2 * ns) - 1;
+  constexpr int kPerT = NS / (NS / kMsIpt);
+  uint64_t raw[kPerT];
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q) {
+    const int j = q * blockDim.x + threadIdx.x;
+    raw[q] = j < ns ? vals[G.off + ((static_cast<uint64_t>(2 * j + 1) * G.n) >> sh)] : 0ULL;
+  }
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q) {
+    const int j = q * blockDim.x + threadIdx.x;
+    if (j < ns) keys[PadIdx(j)] = QKey(raw[q], arg_type);
   }
   __syncthreads();
   BlockMergeSortLds(keys, ns);
@@ -1268,7 +1280,7 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
       if (i < static_cast<int>(c.len)) {
         const uint64_t key = QKey(raw[k], arg_type);
         nn += (key < kNegInfKey || key > kPosInfKey) ? 1u : 0u;
-        atomicAdd(&h[SelBin(S, key)], 1u);
+        atomicAdd(&h[SelBin(S, key, nb)], 1u);
       }
     }
     if (nn) atomicAdd(&s_nan, nn);
@@ -1486,6 +1498,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   constexpr int kRounds = kMidMax / 256;
   uint32_t cur = 0xFFFFFFFFu;
+  int nb = kSelBins;
   for (uint32_t ci = c0; ci < c1; ++ci) {
     const BigChunk c = chunks[ci];
     const BigPlan* P = plans + c.bidx;
@@ -1500,7 +1513,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
     __syncthreads();  // the previous chunk's acc / S / tg readers are done
     if (c.bidx != cur) {
       cur = c.bidx;
-      const int nb = SelNb(c.g_n);
+      nb = SelNb(c.g_n);
       const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
       const uint8_t* Tg = tag_all + static_cast<uint64_t>(cur) * kSelBins;
       for (int b = t; b < kSelBins; b += 256) {
@@ -1519,7 +1532,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
       double v = 0.0;
       if (i < static_cast<int>(c.len)) {
         const uint64_t key = QKey(raw[r], arg_type);
-        const int b = SelBin(S, key);
+        const int b = SelBin(S, key, nb);
         const uint8_t tag = tg[b];
         if (tag == kTagColl) {
           const uint32_t slot = atomicAdd(&cc[b], 1u);
