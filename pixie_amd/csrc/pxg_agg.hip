@@ -262,6 +262,13 @@ __device__ __forceinline__ void LoadOffsetPair(const int32_t* __restrict__ offs,
 // First round trip of a row's keys: the offset pair of every STRING key (start, length) and the
 // value of every fixed-width key.  Phase 2 issues it one row ahead, so it overlaps the previous
 // row's probe instead of heading each row's dependent load chain.
+// Key type i of the plan; S: the kernel is specialised for plans whose keys are all STRING (C2,
+// C3's (pod, remote_addr)), which drops the fixed-width branches and their registers.
+template <bool S>
+__device__ __forceinline__ int KeyT(const AggPlanDev* __restrict__ plan, int i) {
+  return S ? static_cast<int>(PXG_STRING) : plan->key_types[i];
+}
+
 template <int NK>
 struct KeyHeads {
   int32_t o0[NK];
@@ -269,11 +276,11 @@ struct KeyHeads {
   uint64_t a[NK], b[NK];
 };
 
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ void LoadKeyHeads(const AggPlanDev* __restrict__ plan, const DevChunk& ch, int64_t r, KeyHeads<NK>& h) {
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    const int t = plan->key_types[i];
+    const int t = KeyT<S>(plan, i);
     const DevCol& col = ch.cols[plan->keys[i].col];
     if (t == PXG_STRING) {
       int32_t o0, o1;
@@ -293,7 +300,7 @@ __device__ __forceinline__ void LoadKeyHeads(const AggPlanDev* __restrict__ plan
 
 // Second round trip: the string payload words.  Returns false when a string key is too long for
 // the register path.
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ bool LoadKeyBodies(const AggPlanDev* __restrict__ plan, const DevChunk& ch, const KeyHeads<NK>& h,
                                               FastKeys<NK>& k) {
   const uint8_t* ptr[NK];
@@ -301,7 +308,7 @@ __device__ __forceinline__ bool LoadKeyBodies(const AggPlanDev* __restrict__ pla
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
     k.len[i] = h.len[i];
-    if (plan->key_types[i] == PXG_STRING) {
+    if (KeyT<S>(plan, i) == PXG_STRING) {
       ptr[i] = ch.cols[plan->keys[i].col].data + h.o0[i];
       ok = ok && h.len[i] <= 8u * kFastStrWords;
     } else {
@@ -312,16 +319,16 @@ __device__ __forceinline__ bool LoadKeyBodies(const AggPlanDev* __restrict__ pla
   if (!ok) return false;
 #pragma unroll
   for (int i = 0; i < NK; ++i)
-    if (plan->key_types[i] == PXG_STRING) LoadStrWords(ptr[i], k.len[i], k.w[i]);
+    if (KeyT<S>(plan, i) == PXG_STRING) LoadStrWords(ptr[i], k.len[i], k.w[i]);
   return true;
 }
 
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ uint64_t HashFastKeys(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& k) {
   uint64_t h = 0x243F6A8885A308D3ULL;
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    const int t = plan->key_types[i];
+    const int t = KeyT<S>(plan, i);
     uint64_t hk;
     if (t == PXG_STRING) {
       uint64_t s = 0x13198A2E03707344ULL;
@@ -343,12 +350,12 @@ __device__ __forceinline__ uint64_t HashFastKeys(const AggPlanDev* __restrict__ 
   return h;
 }
 
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ bool FastKeysEqual(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& x, const FastKeys<NK>& y) {
   bool eq = true;
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    const int t = plan->key_types[i];
+    const int t = KeyT<S>(plan, i);
     if (t == PXG_STRING) {
       eq = eq && x.len[i] == y.len[i];
 #pragma unroll
@@ -363,14 +370,14 @@ __device__ __forceinline__ bool FastKeysEqual(const AggPlanDev* __restrict__ pla
 // Equality against an arena key record (pxg_keys.h layout).  The record's word offsets are
 // taken from the probing key's own lengths (a record with different lengths is unequal
 // anyway), so every word is requested at once; the over-read stays inside kArenaSlack.
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ bool FastKeysEqualArena(const AggPlanDev* __restrict__ plan, const FastKeys<NK>& x,
                                                    const uint64_t* __restrict__ rec) {
   bool eq = true;
   int w = 0;
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    const int t = plan->key_types[i];
+    const int t = KeyT<S>(plan, i);
     if (t == PXG_STRING) {
       eq = eq && rec[w] == x.len[i];
       const int nw = static_cast<int>((x.len[i] + 7) >> 3);
@@ -399,28 +406,28 @@ struct KeyCols {
   const uint8_t* dat[NK];  // STRING payload, or the values of a fixed-width key
 };
 
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ KeyCols<NK> KeyColsOf(const AggPlanDev* __restrict__ plan, const DevChunk& ch) {
   KeyCols<NK> kc;
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
     const DevCol& col = ch.cols[plan->keys[i].col];
     kc.off[i] = col.offsets;
-    kc.dat[i] = plan->key_types[i] == PXG_STRING ? col.data : col.values;
+    kc.dat[i] = KeyT<S>(plan, i) == PXG_STRING ? col.data : col.values;
   }
   return kc;
 }
 
 // Equality against the keys of row r (a group's representative row), compared word by word
 // as the row's payload words arrive; nothing of the row's key is kept in registers.
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ plan, const KeyCols<NK>& kc, int64_t r,
                                                  const FastKeys<NK>& x) {
   bool eq = true;
   const uint8_t* ptr[NK];
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    const int t = plan->key_types[i];
+    const int t = KeyT<S>(plan, i);
     if (t == PXG_STRING) {
       int32_t o0, o1;
       LoadOffsetPair(kc.off[i], r, &o0, &o1);
@@ -438,7 +445,7 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
   if (!eq) return false;
 #pragma unroll
   for (int i = 0; i < NK; ++i) {
-    if (plan->key_types[i] != PXG_STRING) continue;
+    if (KeyT<S>(plan, i) != PXG_STRING) continue;
     uint64_t w[kFastStrWords];
     LoadStrWords(ptr[i], x.len[i], w);
 #pragma unroll
@@ -447,7 +454,7 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
   return eq;
 }
 
-template <int NK>
+template <int NK, bool S = false>
 __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                                      const KeyCols<NK>* __restrict__ s_kc, uint32_t n_lds_chunks,
                                                      const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
@@ -485,11 +492,11 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
       const uint32_t ref = static_cast<uint32_t>(w);
       bool eq;
       if (w & kKindArena) {
-        eq = FastKeysEqualArena<NK>(plan, keys, tab.arena + ref);
+        eq = FastKeysEqualArena<NK, S>(plan, keys, tab.arena + ref);
       } else {
         const uint32_t c = ref >> kChunkShift;
-        const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK>(plan, chunks[c]);
-        eq = FastKeysEqualRow<NK>(plan, kc, static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
+        const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK, S>(plan, chunks[c]);
+        eq = FastKeysEqualRow<NK, S>(plan, kc, static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
       }
       if (eq) return pos;
     }
@@ -517,6 +524,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
                                                                       const TileRange* __restrict__ ranges, int nranges,
                                                                       int64_t ntiles, AggTableDev tab, StageDev stg,
                                                                       uint32_t nchunks) {
+  constexpr bool S = (MODE & 4) != 0;  // all keys STRING
   constexpr int kPer = kSubRows / kConsumeBlock;
 
   constexpr int kWaves = kConsumeBlock / 64;
@@ -531,7 +539,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   const int nv = plan->n_vals;
   if (threadIdx.x == 0) s_ins = 0;
   const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
-  for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK>(plan, chunks[c]);
+  for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
   __syncthreads();
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
     int ri = 0;
@@ -586,7 +594,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
       __syncthreads();
       const uint64_t base = s_base;
       KeyHeads<NK> heads = {};
-      if (MODE != 2 && threadIdx.x < total) LoadKeyHeads<NK>(plan, ch, row0 + s_sel[threadIdx.x], heads);
+      if ((MODE & 3) != 2 && threadIdx.x < total) LoadKeyHeads<NK, S>(plan, ch, row0 + s_sel[threadIdx.x], heads);
       for (uint32_t i = threadIdx.x; i < total; i += kConsumeBlock) {
         const int64_t local = row0 + s_sel[i];
         const uint64_t pos = base + i;
@@ -596,20 +604,20 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
         uint32_t slot = kDeferredSlot;
         const uint32_t rowref = (static_cast<uint32_t>(rg.chunk) << kChunkShift) | static_cast<uint32_t>(local);
         bool have_keys = false;
-        if (MODE != 2) {
-          have_keys = LoadKeyBodies<NK>(plan, ch, heads, k);
+        if ((MODE & 3) != 2) {
+          have_keys = LoadKeyBodies<NK, S>(plan, ch, heads, k);
           // the next row's heads, in flight during this row's hash and probe
-          if (i + kConsumeBlock < total) LoadKeyHeads<NK>(plan, ch, row0 + s_sel[i + kConsumeBlock], heads);
+          if (i + kConsumeBlock < total) LoadKeyHeads<NK, S>(plan, ch, row0 + s_sel[i + kConsumeBlock], heads);
         }
-        if (MODE == 2) {
+        if ((MODE & 3) == 2) {
           slot = 0;
         } else if (have_keys) {
-          const uint64_t h = HashFastKeys<NK>(plan, k);
-          if (MODE == 3) {
+          const uint64_t h = HashFastKeys<NK, S>(plan, k);
+          if ((MODE & 3) == 3) {
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          slot = FastFindOrInsert<NK>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
+          slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -885,6 +893,19 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     PXG_FAST_CASE(4)
 #undef PXG_FAST_CASE
     default: break;
+  }
+  if (fast_nk > 0 && (diag & 3) == 0) {  // all-STRING keys: the specialised production kernel
+    bool all_str = true;
+    for (int i = 0; i < n_keys; ++i) all_str = all_str && key_types[i] == PXG_STRING;
+    if (all_str) {
+      switch (fast_nk) {
+        case 1: kern = AggConsumeFastKernel<1, 4>; break;
+        case 2: kern = AggConsumeFastKernel<2, 4>; break;
+        case 3: kern = AggConsumeFastKernel<3, 4>; break;
+        case 4: kern = AggConsumeFastKernel<4, 4>; break;
+        default: break;
+      }
+    }
   }
   PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", kern, dim3(grid), dim3(kConsumeBlock), 0,
                              d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
