@@ -875,7 +875,12 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     last_ranges.assign(reinterpret_cast<const uint8_t*>(ranges.data()), reinterpret_cast<const uint8_t*>(ranges.data()) + rbytes);
   }
   PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 8));
+  static const int64_t bpc = [] {  // workgroups per CU of the grid (experiments: PXG_CONSUME_BPC)
+    const char* e = std::getenv("PXG_CONSUME_BPC");
+    const int64_t v = e ? std::atoll(e) : 0;
+    return v > 0 ? v : 8;
+  }();
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * bpc));
   void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t) = AggConsumeKernel;
   static const int diag = [] {
     const char* e = std::getenv("PXG_DIAG_CONSUME");
