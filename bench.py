@@ -58,9 +58,11 @@ def parse():
     ap.add_argument("--no-engine-leg", action="store_true",
                     help="skip the engine query leg (profiling runs: keeps per-kernel averages to the timed steps)")
     ap.add_argument("--host-gen", action="store_true", help="generate on the host and upload (default: device generator)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--backend", default="nccl",
+                    help="N>1 data path: nccl = libpxg's RCCL communicator over xGMI (pxg_agg_alltoall); "
+                         "gloo = torch.distributed all_to_all on the host (CPU rehearsal). The control plane is gloo.")
     ap.add_argument("--share-gpu0", action="store_true",
-                    help="rehearsal only: every rank uses cuda:0 (with --backend gloo on a 1-GPU box)")
+                    help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; RCCL allows it)")
     ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"))
     return ap.parse_args()
 
@@ -100,7 +102,9 @@ def main():
         local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group(args.backend, init_method="env://")
+        # Control plane only (the unique id, barriers, the max over ranks) on gloo; the data path
+        # is libpxg's own RCCL communicator (backend "nccl"), so torch never opens an NCCL group.
+        dist.init_process_group("gloo", init_method="env://")
 
     from pixie_amd import plans as P
     from pixie_amd.device import Ctx, Table, datagen_http_events
@@ -185,7 +189,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     ctx.set_profiling(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     launches, cons_ms = ctx.kernel_stats("agg_consume")
