@@ -160,3 +160,8 @@ def test_two_processes_share_gpu0_exchange_matches_oracle(tmp_path, mode):
     for x in res:
         assert x["sent"] > 0 and x["recv"] > 0
     print("exchange via", [x["via"] for x in res])
+    if mode == "rccl" and any(x["via"] != "rccl" for x in res):
+        # RCCL refuses two ranks on one device ("invalid usage": duplicate GPU), so on a one-GPU
+        # box the ranks exchanged over gloo; the result above is still checked, but the RCCL
+        # multi-rank transport itself is not exercised here (world 1 covers pxg_agg_alltoall).
+        pytest.skip("RCCL refuses two ranks on one GPU; exchange fell back to gloo (result checked)")
