@@ -140,6 +140,8 @@ def main():
     # exchanges through torch.distributed instead.
     comm = None
     if world > 1 and args.backend == "nccl":
+        # every rank is on this node (--nnodes=1): RCCL's bootstrap socket stays on loopback
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         from pixie_amd.device import Comm
         obj = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
