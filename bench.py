@@ -80,14 +80,17 @@ def alg_bytes_of(table, n):
 
 
 def pmc_traffic(args, n):
-    if not os.path.exists(args.pmc_file):
-        return None
-    try:
-        pm = json.load(open(args.pmc_file))
+    """HBM bytes per agg_consume launch from a committed PMC summary for this row count
+    (tools/pmc_summary.py output; C2 and the 1B-row n1 configuration each have one)."""
+    for path in (args.pmc_file, os.path.join(REPO, "profiles", "pmc_agg_consume_n1.json")):
+        if not os.path.exists(path):
+            continue
+        try:
+            pm = json.load(open(path))
+        except Exception:
+            continue
         if pm.get("rows_per_gpu") == n and pm.get("kernel") == "agg_consume":
             return pm.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
     return None
 
 
