@@ -233,6 +233,9 @@ def main():
     filter_map = None
     if world == 1 and not args.no_engine_leg:
         filter_map = filter_map_leg(ctx, table, n, P)
+    c3 = None
+    if world == 1 and not args.no_engine_leg:
+        c3 = c3_leg(args, ctx, table, n, P, plan_agg)
 
     cpu, par = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -286,6 +289,7 @@ def main():
             "parity": par,
             "engine_query": engine_query,
             "filter_map": filter_map,
+            "c3": c3,
             "n1": n1,
         }
         print(json.dumps(line), flush=True)
@@ -341,6 +345,41 @@ def filter_map_leg(ctx, table, n, P, reps=5):
                          "algorithmic_bytes": alg, "achieved": alg / (filt_ms / 1000.0) / 1e9 if filt_ms else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / (filt_ms / 1000.0) / 1e9 / HBM_PEAK_GBS if filt_ms else None}}
+
+
+def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
+    """BASELINE config C3: the high-cardinality group-by, (pod, remote_addr) over the same
+    100M-row table (10M distinct pairs, ~7M groups after the filter): count, mean(latency),
+    sum(resp_body_size).  Parity for this shape is tests/test_scale_parity.py."""
+    alg = 24 * n + table.device_bytes(P.HE["pod"]) + table.device_bytes(P.HE["remote_addr"])
+    a = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=8_000_000)
+
+    def step():
+        a.reset()
+        a.consume(table)
+        return a.finalize()
+
+    g = step()
+    ctx.sync()
+    ctx.reset_stats()
+    ctx.set_profiling(True, only="agg_consume")
+    ctx.sync()
+    ts = time.perf_counter()
+    for _ in range(steps):
+        g = step()
+    ctx.sync()
+    el = time.perf_counter() - ts
+    ctx.set_profiling(False)
+    l, ms = ctx.kernel_stats("agg_consume")
+    avg = ms / max(l, 1)
+    achieved = alg / (avg / 1000.0) / 1e9
+    out = {"workload": "C3: Filter(resp_status>=400) -> Agg by (pod, remote_addr): count, mean(latency), sum(resp_body_size)",
+           "rows": n, "steps": steps, "groups": g, "selected_rows": a.rows_selected(), "ms_per_step": el * 1000.0 / steps,
+           "value": n * steps / el, "unit": "rows/s", "algorithmic_bytes_per_row": alg / n,
+           "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg}}
+    a.close()
+    return out
 
 
 def n1_leg(args, ctx, P, Table, plan_agg):
