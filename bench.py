@@ -352,7 +352,14 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
     100M-row table (10M distinct pairs, ~7M groups after the filter): count, mean(latency),
     sum(resp_body_size).  Parity for this shape is tests/test_scale_parity.py."""
     alg = 24 * n + table.device_bytes(P.HE["pod"]) + table.device_bytes(P.HE["remote_addr"])
-    a = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=8_000_000)
+    # The group-count hint comes from a first, untimed run without one, as the engine's
+    # group-count statistics size the next run of the same plan (DESIGN.md §4.4).
+    probe = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=0)
+    probe.reset()
+    probe.consume(table)
+    hint = probe.finalize()
+    probe.close()
+    a = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=hint)
 
     def step():
         a.reset()

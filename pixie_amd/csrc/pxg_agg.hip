@@ -1149,7 +1149,12 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
   const int64_t expected = spec->expected_groups > 0 ? spec->expected_groups : 4096;
-  a.min_cap = NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 4, 1024));
+  // The smallest table that holds the expected groups at <= 3/8 load, the fill the post-consume
+  // growth rule keeps (ConsumeRange): an exact hint (the engine's group-count statistics) never
+  // triggers a rehash, and the table is no larger than that, since publication, finalize's
+  // dense ranking and every reset sweep all of it (C3, 5.07M groups: 32M -> 16M slots, step
+  // 7.96 -> 7.18 ms at an exact hint; the probe kernel itself is unchanged).
+  a.min_cap = NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 8 / 3 + 1, 1024));
   PXG_RETURN_IF_ERROR(a.EnsureTable(a.min_cap));
   PXG_RETURN_IF_ERROR(a.arena.Alloc(1 << 16));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
