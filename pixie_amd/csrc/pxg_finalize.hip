@@ -443,6 +443,80 @@ __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __res
   }
 }
 
+// The same partial states with one thread per chunk and a sequential loop, for aggregations
+// whose groups average a handful of rows (C3: ~2.4 rows per group over 5M groups), where a
+// wave per chunk would leave 60 of its 64 lanes idle and pay six shuffle steps per UDA.
+// Neighbouring threads take neighbouring groups, so their loads stay close to coalesced.
+__global__ void __launch_bounds__(256) ChunkReduceThreadKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
+                                                               const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ cgroup,
+                                                               uint32_t ngroups, ConstValPtrs vals, uint64_t* __restrict__ partial,
+                                                               uint64_t pstride) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nchunks = cbase[ngroups];
+  if (w >= nchunks) return;
+  const uint32_t g = cgroup[w];
+  const uint32_t s = gstart[g] + (w - cbase[g]) * kRedChunk;
+  const uint32_t e = min(gstart[g + 1], s + kRedChunk);
+  for (int u = 0; u < plan->n_udas; ++u) {
+    const int kind = plan->uda_kind[u];
+    const int at = plan->uda_arg_type[u];
+    const int vi = plan->uda_val[u];
+    if (kind == PXG_UDA_COUNT || kind == PXG_UDA_QUANTILES) continue;
+    const uint64_t* v = vals.p[vi];
+    uint64_t r = 0;
+    if (kind == PXG_UDA_MEAN_MERGE) {
+      const uint64_t* sz = vals.p[plan->uda_val2[u]];
+      double acc = 0;
+      uint64_t n = 0;
+      for (uint32_t i = s; i < e; ++i) {
+        acc += AsF(v[i]);
+        n += sz[i];
+      }
+      r = FBits(acc);
+      partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
+    } else if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
+      if (at == PXG_FLOAT64) {
+        double acc = 0;
+        for (uint32_t i = s; i < e; ++i) acc += AsF(v[i]);
+        r = FBits(acc);
+      } else if (kind == PXG_UDA_MEAN) {
+        double acc = 0;
+        for (uint32_t i = s; i < e; ++i) acc += static_cast<double>(static_cast<int64_t>(v[i]));
+        r = FBits(acc);
+      } else {
+        uint64_t acc = 0;
+        for (uint32_t i = s; i < e; ++i) acc += v[i];
+        r = acc;
+      }
+    } else if (kind == PXG_UDA_MAX) {
+      int64_t m = INT64_MIN;
+      for (uint32_t i = s; i < e; ++i) {
+        const uint64_t x = v[i];
+        if (at == PXG_FLOAT64) {
+          if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o > m ? o : m; }
+        } else {
+          const int64_t y = static_cast<int64_t>(x);
+          m = y > m ? y : m;
+        }
+      }
+      r = static_cast<uint64_t>(m);
+    } else if (kind == PXG_UDA_MIN) {
+      int64_t m = INT64_MAX;
+      for (uint32_t i = s; i < e; ++i) {
+        const uint64_t x = v[i];
+        if (at == PXG_FLOAT64) {
+          if (!isnan(AsF(x))) { const int64_t o = OrderedFromDouble(x); m = o < m ? o : m; }
+        } else {
+          const int64_t y = static_cast<int64_t>(x);
+          m = y < m ? y : m;
+        }
+      }
+      r = static_cast<uint64_t>(m);
+    }
+    partial[static_cast<uint64_t>(u) * pstride + w] = r;
+  }
+}
+
 // UDA Finalize per group (math_ops.h: CountUDA/SumUDA/MeanUDA/MinUDA/MaxUDA).  With
 // plan->emit_states every group's states are also written in Serialize() layout (partial agg).
 __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
@@ -1936,9 +2010,15 @@ int32_t AggFinalizeImpl(Agg* a) {
     PXG_RETURN_IF_ERROR(ws.cgroup.Ensure(max_chunks * 4 + 16));
     PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                                static_cast<const uint32_t*>(cbase), ngroups, ws.cgroup.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceKernel, dim3(static_cast<unsigned>((max_chunks * 64 + 255) / 256)), dim3(256), 0,
-                               a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase),
-                               ws.cgroup.as<const uint32_t>(), ngroups, cv, ws.partial.as<uint64_t>(), max_chunks));
+    if (n < 32 * static_cast<uint64_t>(ngroups)) {  // groups average < 32 rows: a thread per chunk
+      PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceThreadKernel, dim3(static_cast<unsigned>((max_chunks + 255) / 256)),
+                                 dim3(256), 0, a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase),
+                                 ws.cgroup.as<const uint32_t>(), ngroups, cv, ws.partial.as<uint64_t>(), max_chunks));
+    } else {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceKernel, dim3(static_cast<unsigned>((max_chunks * 64 + 255) / 256)),
+                                 dim3(256), 0, a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase),
+                                 ws.cgroup.as<const uint32_t>(), ngroups, cv, ws.partial.as<uint64_t>(), max_chunks));
+    }
   }
   uint8_t* states = nullptr;
   if (a->emit_states && a->state_rec > 0) {
