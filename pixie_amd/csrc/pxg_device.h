@@ -326,6 +326,37 @@ __device__ inline Val EvalProgram(const DevProgram* __restrict__ p, const DevChu
 // XCD-aware remap of a linear block id (bijective for any grid size): blocks that the
 // dispatcher places on one XCD (b % 8 equal) get consecutive logical ids so neighbouring
 // tiles share an L2 (cdna_hip_programming.md §5.5 T1).
+// Copy len bytes with unaligned 16 / 8 / 4-byte moves (gfx950 serves them in hardware); the last
+// move overlaps the previous one and ends exactly at len, so nothing outside [dst, dst + len) is
+// written and nothing outside [src, src + len) is read, and there is no byte-by-byte tail.
+__device__ __forceinline__ void CopyBytesOverlap(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len) {
+  if (len >= 16) {
+    uint32_t k = 0;
+    for (; k + 16 < len; k += 16) {
+      ulonglong2 x;
+      __builtin_memcpy(&x, src + k, 16);
+      __builtin_memcpy(dst + k, &x, 16);
+    }
+    ulonglong2 x;
+    __builtin_memcpy(&x, src + len - 16, 16);
+    __builtin_memcpy(dst + len - 16, &x, 16);
+  } else if (len >= 8) {
+    uint64_t a, b;
+    __builtin_memcpy(&a, src, 8);
+    __builtin_memcpy(&b, src + len - 8, 8);
+    __builtin_memcpy(dst, &a, 8);
+    __builtin_memcpy(dst + len - 8, &b, 8);
+  } else if (len >= 4) {
+    uint32_t a, b;
+    __builtin_memcpy(&a, src, 4);
+    __builtin_memcpy(&b, src + len - 4, 4);
+    __builtin_memcpy(dst, &a, 4);
+    __builtin_memcpy(dst + len - 4, &b, 4);
+  } else {
+    for (uint32_t k = 0; k < len; ++k) dst[k] = src[k];
+  }
+}
+
 __device__ __forceinline__ uint32_t XcdRemap(uint32_t orig, uint32_t nwg) {
   uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;

@@ -1800,15 +1800,7 @@ __global__ void KeyStringCopyKernel(const AggPlanDev* __restrict__ plan, int key
   LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
   const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[key].a);
   const uint32_t len = static_cast<uint32_t>(k.v[key].b);
-  uint8_t* dst = data + offs[g];
-  // 8-byte unaligned word copies (gfx950 serves unaligned global accesses), bytes for the tail.
-  uint32_t i = 0;
-  for (; i + 8 <= len; i += 8) {
-    uint64_t x;
-    __builtin_memcpy(&x, src + i, 8);
-    __builtin_memcpy(dst + i, &x, 8);
-  }
-  for (; i < len; ++i) dst[i] = src[i];
+  CopyBytesOverlap(data + offs[g], src, len);
 }
 
 // ---------------------------------------------------------------------------------------
