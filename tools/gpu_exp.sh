@@ -1,5 +1,8 @@
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/pytest_q.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/c3_prof.py > gpurun_out/prof_c3.log 2>&1 && \
-timeout -k 10 500 python -u bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err
+for r in 1 2; do
+ for pkg in $GRAFT_REPO_ROOT/ab_sub $GRAFT_REPO_ROOT; do
+  timeout -k 10 120 python -u ab_sub/diag.py $pkg 100000000 5 >> gpurun_out/ab_sub.log 2>&1 || exit 1
+  timeout -k 10 200 python -u ab_sub/diag.py $pkg 1000000000 3 >> gpurun_out/ab_sub.log 2>&1 || exit 1
+ done
+done
