@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--n1-rows", type=int, default=1_000_000_000,
                     help="rows of the north-star 1-GPU leg (N=1 only; 0 disables)")
     ap.add_argument("--n1-steps", type=int, default=5)
+    ap.add_argument("--no-n1-parity", action="store_true",
+                    help="skip the n1 leg's full-size parity check against the generator ground truth")
     ap.add_argument("--gen-slice", type=int, default=16_000_000)
     ap.add_argument("--cpu-batch-rows", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (cpu_baseline and parity)")
@@ -63,7 +65,12 @@ def parse():
                          "gloo = torch.distributed all_to_all on the host (CPU rehearsal). The control plane is gloo.")
     ap.add_argument("--share-gpu0", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; RCCL allows it)")
-    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"),
+                    help="committed PMC summary used for roofline.traffic only when the live PMC leg cannot run")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live PMC leg (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this build's consume)")
+    ap.add_argument("--pmc-child", type=int, default=0, metavar="ROWS",
+                    help=argparse.SUPPRESS)  # internal: the consume-only workload the PMC leg profiles
     return ap.parse_args()
 
 
@@ -79,9 +86,62 @@ def alg_bytes_of(table, n):
     return 8 * n + 8 * n + table.device_bytes(P.HE["service"]) + table.device_bytes(P.HE["req_path"])
 
 
+def pmc_child(rows):
+    """The workload the PMC leg profiles: the C2 consume (reset + consume, the timed step's
+    dominant kernel) over `rows` device-generated rows, 3 launches."""
+    from pixie_amd import plans as P
+    from pixie_amd.device import Ctx, Table
+    from pixie_amd.host_engine import plan_agg
+    ctx = Ctx(0)
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(SEED, 0, rows, N_PAIR_KEYS)
+    a = plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
+    for _ in range(3):
+        a.reset()
+        a.consume(t)
+    ctx.sync()
+    a.close()
+    t.close()
+    ctx.close()
+
+
+def pmc_leg(n):
+    """roofline.traffic measured for THIS build: two rocprofv3 --pmc passes (FETCH_SIZE and
+    WRITE_SIZE do not fit one TCC pass) over a child process running the consume on n rows,
+    summarised per launch by tools/pmc_summary.py (FETCH_SIZE doubled: the gfx950 correction of
+    MI355X_MICROARCH.md §HBM).  Returns the summary dict or None."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_summary as ps
+    d = tempfile.mkdtemp(prefix="pxg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        res = {}
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(d, counter)
+            cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv",
+                   "--", sys.executable, os.path.abspath(__file__), "--pmc-child", str(n)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=200)
+            if r.returncode != 0:
+                return {"error": f"rocprofv3 --pmc {counter} exited {r.returncode}"}
+            res[counter], res[counter + "_launches"] = ps.counter_avg(out, r"AggConsume(Fast)?Kernel", counter)
+        return {"hbm_bytes_per_launch": (2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024,
+                "hbm_read_bytes_per_launch": 2 * res["FETCH_SIZE"] * 1024, "hbm_write_bytes_per_launch": res["WRITE_SIZE"] * 1024,
+                "launches": [res["FETCH_SIZE_launches"], res["WRITE_SIZE_launches"]], "rows": n,
+                "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build (bench.py --pmc-child), "
+                          "FETCH_SIZE x2 (gfx950), KiB -> bytes"}
+    except Exception as e:  # the legs must never break the bench line
+        return {"error": f"pmc leg failed: {e}"}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def pmc_traffic(args, n):
     """HBM bytes per agg_consume launch from a committed PMC summary for this row count
-    (tools/pmc_summary.py output; C2 and the 1B-row n1 configuration each have one)."""
+    (tools/pmc_summary.py output): the fallback when the live PMC leg cannot run."""
     for path in (args.pmc_file, os.path.join(REPO, "profiles", "pmc_agg_consume_n1.json")):
         if not os.path.exists(path):
             continue
@@ -96,6 +156,9 @@ def pmc_traffic(args, n):
 
 def main():
     args = parse()
+    if args.pmc_child:
+        pmc_child(args.pmc_child)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -250,6 +313,21 @@ def main():
         engine.drop_table("http_events")
         n1 = n1_leg(args, ctx, P, Table, plan_agg)
 
+    # Live PMC traffic of this build's consume kernel (N=1, after every timed leg; child
+    # processes under rocprofv3, so nothing of it touches the timed region).
+    traffic_src = "committed file " + os.path.relpath(args.pmc_file, REPO) if traffic is not None else None
+    pmc = None
+    if world == 1 and not args.no_pmc:
+        pmc = pmc_leg(n)
+        if pmc and "hbm_bytes_per_launch" in pmc:
+            traffic, traffic_src = pmc["hbm_bytes_per_launch"], pmc["source"]
+        if n1 is not None:
+            p1 = pmc_leg(args.n1_rows)
+            if p1 and "hbm_bytes_per_launch" in p1:
+                n1["roofline"]["traffic"] = p1["hbm_bytes_per_launch"]
+                n1["roofline"]["traffic_source"] = p1["source"]
+            n1["roofline"]["traffic_detail"] = p1
+
     if rank == 0:
         line = {
             "metric": "rows/sec + achieved HBM GB/s, http_events filter+group-by agg, 1/2/4/8 MI355X",
@@ -282,6 +360,8 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "traffic_detail": pmc,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": avg_launch_ms,
             },
@@ -419,6 +499,11 @@ def n1_leg(args, ctx, P, Table, plan_agg):
     l, ms = ctx.kernel_stats("agg_consume")
     avg = ms / max(l, 1)
     achieved = alg / (avg / 1000.0) / 1e9
+    par = None
+    if not args.no_n1_parity:
+        # Outside the timed region: the result of the last timed step against the generator's
+        # ground truth for all n rows (tests/parity.py::check_c2_against_truth).
+        par = n1_parity(a.result(), n)
     out = {
         "workload": "north_star: 1B-row http_events on 1 GPU, Filter(resp_status>=400) -> Map -> Agg by (service, req_path): "
                     "count, mean, quantiles (p50/p99 plucked)",
@@ -426,13 +511,30 @@ def n1_leg(args, ctx, P, Table, plan_agg):
         "value": n * args.n1_steps / el, "unit": "rows/s", "groups": g, "selected_rows": a.rows_selected(),
         "algorithmic_bytes_per_row": alg / n, "generate_s": gen_s,
         "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n), "algorithmic_bytes_per_launch": alg,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n),
+                     "traffic_source": "committed file (replaced by the live PMC leg when it runs)", "algorithmic_bytes_per_launch": alg,
                      "avg_launch_ms": avg},
         "cpu_baseline": "same CPU Carnot restatement as the top-level cpu_baseline (rows/s of one thread; the plan is per-row linear)",
+        "parity": par,
     }
     a.close()
     t.close()
     return out
+
+
+def n1_parity(dev, n):
+    """Full-size parity of the 1B-row result: every group key and count bit-exact, every mean
+    within 1e-6 (sum(mean*count) within 1e-9) of the generator's exact sums, quantiles of the 20
+    largest groups within the rank bound and of 200 seeded <= 8000-value groups within 4 ULP of
+    the oracle t-digest fed each group's values in row order (test infrastructure, tests/parity.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        import parity
+        return parity.check_c2_against_truth(dev, SEED, 0, n, threads=16)
+    except Exception as e:  # the legs must never break the bench line
+        import traceback
+        traceback.print_exc()
+        return {"ok": False, "error": f"n1 parity failed: {e}"}
 
 
 def oracle_leg(args, n, row0, dev_result):

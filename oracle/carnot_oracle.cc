@@ -1665,6 +1665,9 @@ extern "C" int32_t oracle_group_ranks(const oracle_column* keys, int32_t nk, con
         const uint32_t len = static_cast<uint32_t>(col.offsets[r + 1] - col.offsets[r]);
         k.append(reinterpret_cast<const char*>(&len), 4);
         k.append(reinterpret_cast<const char*>(col.data) + col.offsets[r], len);
+      } else if (col.type == BOOLEAN) {  // 1 byte per row, widened to the 8-byte query encoding
+        char b[8] = {static_cast<const char*>(col.values)[r], 0, 0, 0, 0, 0, 0, 0};
+        k.append(b, 8);
       } else {
         const size_t w = col.type == UINT128 ? 16 : 8;
         k.append(static_cast<const char*>(col.values) + r * w, w);

@@ -28,6 +28,26 @@ struct Comm {
     if (r_ != ncclSuccess) return SetError(PXG_INTERNAL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
   } while (0)
 
+// An RCCL group that is closed on every exit path: an ncclSend / ncclRecv that fails between
+// ncclGroupStart and ncclGroupEnd must not leave the group open for later calls on the
+// communicator.
+struct NcclGroup {
+  bool open = false;
+  int32_t Start() {
+    PXG_NCCL(ncclGroupStart());
+    open = true;
+    return PXG_OK;
+  }
+  int32_t End() {
+    open = false;
+    PXG_NCCL(ncclGroupEnd());
+    return PXG_OK;
+  }
+  ~NcclGroup() {
+    if (open) (void)ncclGroupEnd();
+  }
+};
+
 }  // namespace pxg
 
 struct pxg_comm {
@@ -93,12 +113,15 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   if (static_cast<size_t>(2 * n) * 8 > Ctx::kPinnedBytes - Ctx::kPinnedOps) return SetError(PXG_UNIMPLEMENTED, "%d ranks", n);
   for (int p = 0; p < n; ++p) pin[p] = seg[p];
   PXG_HIP(hipMemcpyAsync(d_send_cnt, pin, static_cast<size_t>(n) * 8, hipMemcpyHostToDevice, ctx->stream));
-  PXG_NCCL(ncclGroupStart());
-  for (int p = 0; p < n; ++p) {
-    PXG_NCCL(ncclSend(d_send_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
-    PXG_NCCL(ncclRecv(d_recv_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+  {
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    for (int p = 0; p < n; ++p) {
+      PXG_NCCL(ncclSend(d_send_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+      PXG_NCCL(ncclRecv(d_recv_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+    }
+    PXG_RETURN_IF_ERROR(grp.End());
   }
-  PXG_NCCL(ncclGroupEnd());
   PXG_HIP(hipMemcpyAsync(pin + n, d_recv_cnt, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   std::vector<int64_t> rs(pin + n, pin + 2 * n);
@@ -109,17 +132,22 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   }
   // 3. The parts: all-to-all(v) as grouped point-to-point sends over xGMI.
   PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(rtotal) + 64));
-  PXG_NCCL(ncclGroupStart());
-  int64_t so = 0, ro = 0;
-  for (int p = 0; p < n; ++p) {
-    if (seg[p] > 0) PXG_NCCL(ncclSend(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), ncclUint8, p, C.nccl, ctx->stream));
-    if (rs[p] > 0) PXG_NCCL(ncclRecv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), ncclUint8, p, C.nccl, ctx->stream));
-    so += seg[p];
-    ro += rs[p];
+  {
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    int64_t so = 0, ro = 0;
+    for (int p = 0; p < n; ++p) {
+      if (seg[p] > 0) PXG_NCCL(ncclSend(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), ncclUint8, p, C.nccl, ctx->stream));
+      if (rs[p] > 0) PXG_NCCL(ncclRecv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), ncclUint8, p, C.nccl, ctx->stream));
+      so += seg[p];
+      ro += rs[p];
+    }
+    PXG_RETURN_IF_ERROR(grp.End());
   }
-  PXG_NCCL(ncclGroupEnd());
   // 4. Every group this rank exported now lives on its owner: rebuild from the received parts
-  //    (our own part included), all of them in one import.
+  //    (our own part included), all of them in one import.  The local state is dropped first:
+  //    if the import fails, the aggregation is left empty (the caller must reset and rerun the
+  //    query; the exported groups are on their owners' ranks, not here).
   PXG_RETURN_IF_ERROR(pxg_agg_reset(agg));
   std::vector<int64_t> poffs, psizes;
   int64_t at = 0;

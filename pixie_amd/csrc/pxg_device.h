@@ -323,9 +323,6 @@ __device__ inline Val EvalProgram(const DevProgram* __restrict__ p, const DevChu
   return st[0];
 }
 
-// XCD-aware remap of a linear block id (bijective for any grid size): blocks that the
-// dispatcher places on one XCD (b % 8 equal) get consecutive logical ids so neighbouring
-// tiles share an L2 (cdna_hip_programming.md §5.5 T1).
 // Copy len bytes with unaligned 16 / 8 / 4-byte moves (gfx950 serves them in hardware); the last
 // move overlaps the previous one and ends exactly at len, so nothing outside [dst, dst + len) is
 // written and nothing outside [src, src + len) is read, and there is no byte-by-byte tail.
@@ -357,6 +354,9 @@ __device__ __forceinline__ void CopyBytesOverlap(uint8_t* __restrict__ dst, cons
   }
 }
 
+// XCD-aware remap of a linear block id (bijective for any grid size): blocks that the
+// dispatcher places on one XCD (b % 8 equal) get consecutive logical ids so neighbouring
+// tiles share an L2 (cdna_hip_programming.md §5.5 T1).
 __device__ __forceinline__ uint32_t XcdRemap(uint32_t orig, uint32_t nwg) {
   uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;

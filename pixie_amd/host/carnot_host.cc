@@ -761,6 +761,7 @@ class ExecNode {
   // Lets a producer skip rendering a column no consumer reads.
   virtual bool ReadsColumnValue(size_t /*col*/) const { return true; }
   const RowDescriptor& output_descriptor() const { return output_; }
+  const std::vector<std::pair<ExecNode*, size_t>>& children() const { return children_; }
   virtual std::string DebugString() const = 0;
 
  protected:
@@ -788,6 +789,8 @@ class SourceNode : public ExecNode {
  public:
   uint64_t node_id = 0;  // plan node id (LimitOperator.abortable_srcs names sources by it)
   virtual bool HasBatchesRemaining() const = 0;
+  // An infinite stream (MemorySourceOperator.streaming) that sends no eow / eos per batch.
+  virtual bool IsStreaming() const { return false; }
   Status GenerateNext(ExecState* s) {
     stats_.ResumeTotalTimer();
     Status st = GenerateNextImpl(s);
@@ -878,6 +881,9 @@ class MemorySourceNode : public SourceNode {
   int32_t next_ = 0;
   bool done_ = false;
   bool streaming_ = false;
+
+ public:
+  bool IsStreaming() const override { return streaming_; }
 };
 
 // Uploads a RowBatch into a fresh device table.
@@ -921,7 +927,15 @@ static HostColumn SliceColumn(const HostColumn& c, int64_t r0, int64_t n) {
 // run together at kCoalesceRows staged rows or at eow / eos; the output is cut back into one
 // batch per input batch with the input batch's eow / eos, exactly what the per-batch reference
 // nodes emit (filter_node.cc:167-168, map_node.cc:67-68).
+//
+// Coalescing changes when a batch leaves the node, not what it holds.  Two plan shapes would see
+// the difference, so there the node runs every batch as it arrives (eager): below an infinite
+// stream (no eow / eos per batch, so staged rows would wait for Close), and above a Limit
+// (which stops its abortable sources as soon as it has its rows, limit_node.cc:55).
 class CoalescingDeviceNode : public ExecNode {
+ public:
+  void set_eager() { eager_ = true; }
+
  protected:
   static constexpr int64_t kCoalesceRows = 1 << 16;
   struct Pending {
@@ -953,7 +967,7 @@ class CoalescingDeviceNode : public ExecNode {
     }
     pending_.push_back({rb.num_rows, rb.eow, rb.eos});
     staged_rows_ += rb.num_rows;
-    if (staged_rows_ < kCoalesceRows && !rb.eow && !rb.eos) return Status::OK();
+    if (!eager_ && staged_rows_ < kCoalesceRows && !rb.eow && !rb.eos) return Status::OK();
     return Flush(s);
   }
 
@@ -985,6 +999,7 @@ class CoalescingDeviceNode : public ExecNode {
   pxg_table* staged_ = nullptr;
   std::vector<Pending> pending_;
   int64_t staged_rows_ = 0;
+  bool eager_ = false;
 };
 
 // GpuFilterNode (FilterNode, filter_node.cc:78-171): one output batch per input batch.
@@ -2145,6 +2160,7 @@ class DeviceSourceNode : public SourceNode {
   DeviceSourceNode(std::string name, const StoredTable* st) : name_(std::move(name)), st_(st) {}
   std::string DebugString() const override { return "MemorySourceNode(" + name_ + ", HBM-resident)"; }
   bool HasBatchesRemaining() const override { return !done_; }
+  bool IsStreaming() const override { return ms_.streaming; }
   // RowBatch::NumBytes of the projected columns over [lo, hi): exact for the whole table
   // (string payload = device bytes - offsets), proportional for a sub-range.
   int64_t RangeBytes() const {
@@ -2402,7 +2418,35 @@ class ExecutionGraph {
     }
     if (sources_.empty()) return Err(PXG_UNIMPLEMENTED, "plan must start with a MemorySource or GRPCSource");
     if (sinks_.empty() && grpc_sinks_.empty()) return Err(PXG_INVALID_ARGUMENT, "plan has no sink");
+    MarkEagerCoalescing();
     return Status::OK();
+  }
+
+  // CoalescingDeviceNode's two eager cases: reachable from a streaming source, or with a
+  // LimitNode reachable below it.
+  void MarkEagerCoalescing() {
+    std::set<ExecNode*> below_stream;
+    std::vector<ExecNode*> stack;
+    for (auto* src : sources_)
+      if (src->IsStreaming()) stack.push_back(src);
+    while (!stack.empty()) {
+      ExecNode* n = stack.back();
+      stack.pop_back();
+      if (!below_stream.insert(n).second) continue;
+      for (auto& c : n->children()) stack.push_back(c.first);
+    }
+    std::function<bool(ExecNode*, std::set<ExecNode*>*)> limit_below = [&](ExecNode* n, std::set<ExecNode*>* seen) {
+      if (!seen->insert(n).second) return false;
+      for (auto& c : n->children())
+        if (dynamic_cast<LimitNode*>(c.first) || limit_below(c.first, seen)) return true;
+      return false;
+    };
+    for (auto& up : pool_) {
+      auto* cn = dynamic_cast<CoalescingDeviceNode*>(up.get());
+      if (!cn) continue;
+      std::set<ExecNode*> seen;
+      if (below_stream.count(cn) || limit_below(cn, &seen)) cn->set_eager();
+    }
   }
 
   // ExecuteSources (exec_graph.cc:177-289).

@@ -259,3 +259,151 @@ def take_rows(c: Column, idx: np.ndarray) -> Column:
     offs[1:] = np.cumsum(lens)
     flat = np.repeat(starts - offs[:-1], lens) + np.arange(int(offs[-1]))
     return Column(STRING, offsets=offs.astype(np.int32), data=np.concatenate([c.data[flat], np.zeros(16, np.uint8)]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Ground truth straight from the generator (oracle/http_events_truth.cc) for the C2 shape at the
+# 1B-row north_star size, where the row-at-a-time restatement cannot hold the table.
+# ---------------------------------------------------------------------------------------------
+def http_events_key_tables():
+    """(service strings, path strings) of the synthetic generator, as bytes, by index."""
+    lib = oc.load()
+    lib.oracle_http_events_tables.restype = None
+    sb = C.create_string_buffer(64 * 16)
+    so = (C.c_int32 * 65)()
+    pb = C.create_string_buffer(1024 * 48)
+    po = (C.c_int32 * 1025)()
+    lib.oracle_http_events_tables(sb, so, pb, po)
+    svc = [sb.raw[so[k]:so[k + 1]] for k in range(64)]
+    paths = [pb.raw[po[k]:po[k + 1]] for k in range(1024)]
+    return svc, paths
+
+
+def c2_truth(seed: int, row0: int, n: int, collect: Optional[np.ndarray] = None, n_pair_keys: int = 10_000_000,
+             threads: int = 16, status_min: int = 400):
+    """Per (service index, canonical path index) group g = s * 1024 + p of rows [row0, row0 + n):
+    counts, exact int64 latency sums and (groups flagged in `collect`) the values latency/1e6 in
+    row order, as (counts, lat_sum, voff, vals)."""
+    lib = oc.load()
+    lib.oracle_http_events_c2_truth.restype = C.c_int64
+    G = 64 * 1024
+    counts = np.zeros(G, np.int64)
+    sums = np.zeros(G, np.int64)
+    vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    if collect is None:
+        r = lib.oracle_http_events_c2_truth(C.c_uint64(seed), C.c_int64(row0), C.c_int64(n), C.c_int64(n_pair_keys),
+                                            C.c_int32(threads), C.c_int64(status_min), vp(counts), vp(sums), None, None,
+                                            None, C.c_int64(0))
+        if r < 0:
+            raise RuntimeError("oracle_http_events_c2_truth failed")
+        return counts, sums, None, None
+    flags = np.ascontiguousarray(collect, dtype=np.uint8)
+    voff = np.zeros(G + 1, np.int64)
+    cap = int(collect.astype(bool).sum()) and int(n)  # upper bound refined below
+    # Capacity: a first counts-only pass would double the scan; size from the flagged groups'
+    # expected share instead and retry once with the exact total if it was too small.
+    cap = min(cap, max(1 << 20, int(n // 4)))
+    for _ in range(2):
+        vals = np.empty(max(cap, 1), np.float64)
+        r = lib.oracle_http_events_c2_truth(C.c_uint64(seed), C.c_int64(row0), C.c_int64(n), C.c_int64(n_pair_keys),
+                                            C.c_int32(threads), C.c_int64(status_min), vp(counts), vp(sums), vp(flags),
+                                            vp(voff), vp(vals), C.c_int64(cap))
+        if r >= 0:
+            return counts, sums, voff, vals[:r]
+        cap = int(counts[flags.astype(bool)].sum())
+    raise RuntimeError("oracle_http_events_c2_truth: value capacity")
+
+
+def check_c2_against_truth(dev: Sequence[Column], seed: int, row0: int, n: int, n_big: int = 20, n_small: int = 200,
+                           rng_seed: int = 7, threads: int = 16) -> Dict:
+    """Full-size parity of a device C2 aggregate (service, req_path, count, mean, quantiles raw 7
+    doubles) over generator rows [row0, row0 + n) against generator ground truth:
+      * every group's key and count bit-exact (the group set is the set of distinct selected
+        (service, req_path) byte strings), so also sum(count) = selected rows;
+      * every mean within 1e-6 relative of (exact int64 latency sum) / 1e6 / count, and
+        sum(mean * count) within 1e-9 relative of sum(latency) / 1e6;
+      * quantiles of the n_big largest groups (millions of values at 1B rows) within the
+        midpoint-rank bound of the oracle t-digest fed the group's values in row order
+        (TDigest(1000).add per row, math_sketches.h:36-54), and of n_small seeded groups of
+        <= 8000 values within 4 ULP of it."""
+    t0 = __import__("time").time()
+    svc, paths = http_events_key_tables()
+    svc_id = {s: i for i, s in enumerate(svc)}
+    path_id: Dict[bytes, int] = {}
+    for i, p in enumerate(paths):
+        path_id.setdefault(p, i)
+    rep: Dict = {"rows": n, "groups_dev": len(dev[0])}
+    raw = [dev[0].data.tobytes(), dev[1].data.tobytes()]
+    offs = [dev[0].offsets, dev[1].offsets]
+    G = len(dev[0])
+    gid = np.empty(G, np.int64)
+    for i in range(G):
+        s = raw[0][offs[0][i]:offs[0][i + 1]]
+        p = raw[1][offs[1][i]:offs[1][i + 1]]
+        if s not in svc_id or p not in path_id:
+            rep.update(ok=False, error=f"device group key not in the generator's tables: {s!r}, {p!r}")
+            return rep
+        gid[i] = svc_id[s] * 1024 + path_id[p]
+    if len(np.unique(gid)) != G:
+        rep.update(ok=False, error="duplicate device groups")
+        return rep
+    dcount = np.asarray(dev[2].values, np.int64)
+    dmean = np.asarray(dev[3].values, np.float64)
+    dq = quantile_matrix(dev[4])
+    rng = np.random.default_rng(rng_seed)
+    big = np.argsort(-dcount, kind="stable")[:n_big]
+    small_pool = np.flatnonzero(dcount <= EXACT_MAX)
+    small = rng.choice(small_pool, size=min(n_small, len(small_pool)), replace=False) if len(small_pool) else small_pool
+    flags = np.zeros(64 * 1024, np.uint8)
+    flags[gid[big]] = 1
+    flags[gid[small]] = 1
+    counts, sums, voff, vals = c2_truth(seed, row0, n, flags, threads=threads)
+    rep["truth_s"] = round(__import__("time").time() - t0, 2)
+    tg = np.flatnonzero(counts)
+    rep["groups_ref"] = int(len(tg))
+    rep["selected_rows_ref"] = int(counts.sum())
+    rep["selected_rows_dev"] = int(dcount.sum())
+    ok = rep["groups_ref"] == G and np.array_equal(np.sort(gid), tg)
+    rep["group_set_exact"] = bool(ok)
+    cnt_ok = bool(ok and np.array_equal(dcount, counts[gid]))
+    rep["counts_bit_exact"] = cnt_ok
+    ok &= cnt_ok
+    ref_mean = sums[gid].astype(np.float64) / 1e6 / np.maximum(counts[gid], 1)
+    rel = np.abs(dmean - ref_mean) / np.abs(ref_mean)
+    rep["mean_max_rel"] = float(rel.max()) if G else 0.0
+    ok &= rep["mean_max_rel"] <= 1e-6
+    tot_dev = float(np.sum(dmean * dcount))
+    tot_ref = float(sums.sum()) / 1e6
+    rep["sum_mean_count_rel"] = abs(tot_dev - tot_ref) / tot_ref if tot_ref else 0.0
+    ok &= rep["sum_mean_count_rel"] <= 1e-9
+    # quantiles
+    lib = oc.load()
+    max_ulp, worst_excess, big_sizes = 0, -1.0, []
+    for i in small:
+        g = gid[i]
+        v = vals[voff[g]:voff[g] + counts[g]]
+        ref = np.zeros(7)
+        lib.oracle_tdigest_quantiles(v.ctypes.data_as(C.POINTER(C.c_double)), len(v), ref.ctypes.data_as(C.POINTER(C.c_double)))
+        max_ulp = max(max_ulp, int(ulp(dq[i], ref).max()))
+    for i in big:
+        g = gid[i]
+        v = vals[voff[g]:voff[g] + counts[g]]
+        big_sizes.append(int(len(v)))
+        ref = np.zeros(7)
+        lib.oracle_tdigest_quantiles(v.ctypes.data_as(C.POINTER(C.c_double)), len(v), ref.ctypes.data_as(C.POINTER(C.c_double)))
+        sv = np.sort(v)
+        nn = len(sv)
+
+        def rank(x):
+            return (np.searchsorted(sv, x, "left") + np.searchsorted(sv, x, "right")) / (2.0 * nn)
+        for j, q in enumerate(QS):
+            ex = abs(rank(dq[i][j]) - rank(ref[j])) - rank_bound(q, nn)
+            worst_excess = max(worst_excess, float(ex)) if not np.isnan(ex) else float("inf")
+    rep["quantiles"] = {"groups_exact": int(len(small)), "max_ulp": max_ulp, "ulp_bar": 4,
+                        "groups_rank": int(len(big)), "largest_group": max(big_sizes) if big_sizes else 0,
+                        "rank_checked_values": int(sum(big_sizes)), "max_rank_excess": worst_excess,
+                        "rank_bar": "2*pi*sqrt(q(1-q))/1000 + 1/n vs the oracle digest fed row order"}
+    ok &= max_ulp <= 4 and worst_excess <= 0
+    rep["ok"] = bool(ok)
+    rep["check_s"] = round(__import__("time").time() - t0, 2)
+    return rep

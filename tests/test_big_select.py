@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle_client as oc
+import parity
 from device_runner import run_plan
 from kat import rows, ulp_diff
 from pixie_amd import _lib
@@ -202,3 +203,16 @@ def test_selection_serves_multi_million_groups(ctx):
         for name in NAMES:
             a, b = sel[k][0][name], srt[k][0][name]
             assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
+    # Against the oracle, not only the sort path: each group's values in row order through the
+    # restated TDigest(1000) (math_sketches.h:36-54); <= 8000 values 4 ULP, above the rank bound.
+    for i, (k, _) in enumerate(spec):
+        v = vals_p[kp == i]
+        ref = oc.tdigest_quantiles(v)
+        sv = np.sort(v)
+        for j, name in enumerate(NAMES):
+            d = sel[k][0][name]
+            if len(v) <= parity.EXACT_MAX:
+                assert parity.ulp(np.array([d]), np.array([ref[j]]))[0] <= 4, (k, name, d, ref[j])
+            else:
+                rank = lambda x: (np.searchsorted(sv, x, "left") + np.searchsorted(sv, x, "right")) / (2.0 * len(sv))  # noqa: E731
+                assert abs(rank(d) - rank(ref[j])) <= parity.rank_bound(parity.QS[j], len(sv)), (k, name, d, ref[j])

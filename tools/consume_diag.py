@@ -13,12 +13,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def child(rows, steps):
     sys.path.insert(0, REPO)
     from pixie_amd import plans as P
-    from pixie_amd.device import Ctx, Table, datagen_http_events
+    from pixie_amd.device import Ctx, Table
     from pixie_amd.pipeline import LinearQuery
     ctx = Ctx(0)
     t = Table(ctx, P.HTTP_TYPES)
-    for a in range(0, rows, 16_000_000):
-        t.append(datagen_http_events(20250117, a, min(16_000_000, rows - a), n_pair_keys=10_000_000, threads=16))
+    t.append_http_events(20250117, 0, rows, 10_000_000)
     t.flush()
     q = LinearQuery(P.c2_plan(with_pluck=True), P.HTTP_TYPES, expected_groups=65536)
     agg = q.make_agg(ctx)
