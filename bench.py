@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (cpu_baseline and parity)")
     ap.add_argument("--no-engine-leg", action="store_true",
                     help="skip the engine query leg (profiling runs: keeps per-kernel averages to the timed steps)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (bin + join) leg")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 (carnot_csv, CSV parse included) leg")
+    ap.add_argument("--c5-rows", type=int, default=20_000_000)
     ap.add_argument("--host-gen", action="store_true", help="generate on the host and upload (default: device generator)")
     ap.add_argument("--backend", default="nccl",
                     help="N>1 data path: nccl = libpxg's RCCL communicator over xGMI (pxg_agg_alltoall); "
@@ -300,6 +303,13 @@ def main():
     if world == 1 and not args.no_engine_leg:
         c3 = c3_leg(args, ctx, table, n, P, plan_agg)
 
+    c5 = None
+    if world == 1 and not args.no_engine_leg and not args.no_c5:
+        c5 = c5_leg(args, engine, ctx, P)
+    c1 = None
+    if world == 1 and not args.no_engine_leg and not args.no_c1:
+        c1 = c1_leg(args, P)
+
     cpu, par = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, par = oracle_leg(args, n, row0, dev_result)
@@ -370,6 +380,8 @@ def main():
             "engine_query": engine_query,
             "filter_map": filter_map,
             "c3": c3,
+            "c5": c5,
+            "c1": c1,
             "n1": n1,
         }
         print(json.dumps(line), flush=True)
@@ -467,6 +479,145 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
                         "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg}}
     a.close()
     return out
+
+
+def c5_leg(args, engine, ctx, P, reps=5):
+    """BASELINE config C5: conn_stats bin(time_, 10 s) x (upid, remote_addr) sums joined to pod
+    metadata (plans.c5_plan: MemorySource -> Map(bin) -> Agg -> Equijoin <- MemorySource), the
+    unmodified plan through the C++ engine over HBM-resident stored tables (pxc_execute_plan):
+    fused consume with the bin key, finalize, device equijoin, result D2H + PXRB.  Timed at
+    --c5-rows rows; parity and the CPU baseline (oracle, one thread) on a 1M-row table of the
+    same shape (the restated agg + join runs ~0.2M rows/s).  Roofline: agg_consume over the
+    five referenced conn_stats columns (time_ 8 + upid 16 + remote_addr 4 + payload + two INT64)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        from pixie_amd import synth
+        shape = dict(n_pods=1000, n_addrs=100, span_s=300)
+
+        def store(n, rpb):
+            tabs = synth.c5_tables(SEED, n, rows_per_batch=rpb, **shape)
+            for name, t in tabs.items():
+                engine.create_table(name, t["types"], t["names"])
+                for b in t["batches"]:
+                    engine.append(name, b)
+            return tabs
+
+        def drop():
+            engine.drop_table("conn_stats")
+            engine.drop_table("pod_metadata")
+
+        pb = P.c5_plan().SerializeToString()
+        # parity + CPU baseline at 1M rows
+        import oracle_client as oc
+        from kat import rows as kat_rows
+        small = 1_000_000
+        tabs = store(small, 1 << 16)
+        dev = engine.execute(P.c5_plan())["output"]
+        secs, ref = oc.execute_plan_timed(P.c5_plan(), tabs)
+        ref = ref["output"]
+        rows_d = sorted(r for b in dev for r in kat_rows(b["cols"]))
+        rows_r = sorted(r for b in ref for r in kat_rows(b["cols"]))
+        parity = {"rows": small, "output_rows": len(rows_r), "ok": rows_d == rows_r,
+                  "bar": "output rows (time bin, upid, remote_addr, pod, namespace, sums) identical as a multiset"}
+        cpu = {"value": small / secs, "unit": "rows/s", "cores": 1, "kind": "port",
+               "sample": f"{small} conn_stats rows as 65536-row RowBatches, C5 plan, oracle/ one thread, {secs:.2f} s window"}
+        drop()
+        del tabs
+        n = args.c5_rows
+        store(n, 1 << 20)
+        t = engine.device_table("conn_stats")
+        from pixie_amd.device import Table
+        tt = Table(ctx, P.CONN_TYPES, handle=t, owned=False)
+        c = {nm: i for i, nm in enumerate(P.CONN_NAMES)}
+        alg = 8 * n + 16 * n + tt.device_bytes(c["remote_addr"]) + 16 * n
+        engine.execute_raw(pb)
+        ctx.sync()
+        ctx.reset_stats()
+        ctx.set_profiling(True)
+        times = []
+        res = b""
+        for _ in range(reps):
+            tq = time.perf_counter()
+            res = engine.execute_raw(pb)
+            times.append(time.perf_counter() - tq)
+        ctx.sync()
+        ctx.set_profiling(False)
+        kms = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS + ["join_build", "join_slot_flags", "join_probe_count", "join_unprobed_count", "join_probe_write", "join_unprobed_write", "join_gather",
+                                                                               "agg_consume_list"]
+               if ctx.kernel_stats(k)[0]}
+        l, ms = ctx.kernel_stats("agg_consume")
+        avg = ms / max(l, 1)
+        st = sorted(times)
+        out = {"workload": "C5: conn_stats bin(time_, 10s) x (upid, remote_addr) sum(bytes_sent), sum(bytes_recv), "
+                           "inner equijoin on upid to pod_metadata (pxc_execute_plan over stored tables)",
+               "rows": n, "queries": reps, "ms_per_query": sum(times) * 1000 / reps, "ms_median": st[len(st) // 2] * 1000,
+               "ms_min": st[0] * 1000, "value": n * reps / sum(times), "unit": "rows/s", "result_bytes": len(res),
+               "kernel_ms_per_query": kms, "algorithmic_bytes_per_row": alg / n,
+               "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": alg / (avg / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS, "avg_launch_ms": avg},
+               "parity": parity, "cpu_baseline": cpu, "shape": shape}
+        drop()
+        return out
+    except Exception as e:  # the legs must never break the bench line
+        import traceback
+        traceback.print_exc()
+        return {"error": f"c5 leg failed: {e}"}
+
+
+def c1_leg(args, P, n=1_000_000, reps=3):
+    """BASELINE config C1: carnot_executable's shape -- a 1M-row http_events CSV (type row, name
+    row), groupby(service).agg(count, mean(latency)) -- through pixie_amd/lib/carnot_csv (CSV
+    parse into --rowbatch_size 100-row RowBatches, the reference default, then the engine), wall
+    time including the CSV parse (carnot_executable.cc:232-277), next to the oracle's execution
+    window over the same parsed rows (one thread)."""
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        import oracle_client as oc
+        from pixie_amd.device import datagen_http_events
+        exe = os.path.join(REPO, "pixie_amd", "lib", "carnot_csv")
+        cols = datagen_http_events(SEED, 0, n, threads=16)
+        svc, lat = cols[P.HE["service"]], cols[P.HE["latency"]]
+        d = tempfile.mkdtemp(prefix="pxg_c1_", dir=os.environ.get("TMPDIR", "/tmp"))
+        csv, pbf, outf = os.path.join(d, "in.csv"), os.path.join(d, "plan.pb"), os.path.join(d, "out.csv")
+        raw = svc.data.tobytes()
+        o = svc.offsets
+        with open(csv, "w") as f:
+            f.write("string,int64\nservice,latency\n")
+            f.write("".join(f"{raw[o[i]:o[i + 1]].decode()},{int(lat.values[i])}\n" for i in range(n)))
+        types, names = [P.STRING, P.INT64], ["service", "latency"]
+        plan = P.linear_plan([P.source_op("csv_table", types, names, [0, 1]),
+                              P.agg_op([0], [P.agg_expr("count", [P.col(1)], [P.INT64]), P.agg_expr("mean", [P.col(1)], [P.INT64], fid=1)],
+                                       ["service"], ["count", "mean"]),
+                              P.sink_op("output")])
+        with open(pbf, "wb") as f:
+            f.write(plan.SerializeToString())
+        walls, stats = [], []
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            r = subprocess.run([exe, f"--input_file={csv}", f"--output_file={outf}", f"--plan_file={pbf}", "--rowbatch_size=100"],
+                               capture_output=True, text=True, timeout=300)
+            walls.append(time.perf_counter() - t0)
+            if r.returncode != 0:
+                return {"error": r.stderr[-500:]}
+            stats.append(json.loads([ln for ln in r.stderr.splitlines() if ln.startswith("{")][-1]))
+        walls, stats = walls[1:], stats[1:]
+        groups = sum(1 for _ in open(outf))
+        batches = [[c.slice(a, min(a + 100, n)) for c in (svc, lat)] for a in range(0, n, 100)]
+        secs, _ = oc.execute_plan_timed(plan, {"csv_table": {"types": types, "names": names, "batches": batches}})
+        best = min(range(reps), key=lambda i: walls[i])
+        return {"workload": "C1: carnot_csv (carnot_executable harness) 1M-row http_events CSV, groupby(service): count, mean(latency), "
+                            "--rowbatch_size 100",
+                "rows": n, "groups": groups, "runs": reps, "wall_s_median": sorted(walls)[reps // 2], "wall_s_min": walls[best],
+                "harness_stats_best": stats[best], "rows_per_s_wall": n / sorted(walls)[reps // 2],
+                "cpu_baseline": {"value": n / secs, "unit": "rows/s", "cores": 1, "kind": "port",
+                                 "sample": f"oracle over the same {n} parsed rows as 100-row RowBatches (execution window "
+                                           f"{secs:.3f} s, CSV parse excluded)"}}
+    except Exception as e:  # the legs must never break the bench line
+        import traceback
+        traceback.print_exc()
+        return {"error": f"c1 leg failed: {e}"}
 
 
 def n1_leg(args, ctx, P, Table, plan_agg):
