@@ -36,6 +36,8 @@ struct TileRange {
 
 constexpr uint32_t kMaxProbe = 256;  // longer probe sequences defer the row (table grows)
 
+struct HotImage;  // the hot-group cache image (below)
+
 // Probe for the row's group; insert it (CAS of an empty slot word) when absent.  Inserts are
 // counted in the workgroup's LDS counter (`s_ins`) and flushed once per tile, so no per-row
 // atomic ever targets a shared global address.  The table fill check reads the flushed global
@@ -120,7 +122,8 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
                                                                   const DevChunk* __restrict__ chunks,
                                                                   const TileRange* __restrict__ ranges, int nranges,
                                                                   int64_t ntiles, AggTableDev tab, StageDev stg,
-                                                                  uint32_t /*nchunks: signature shared with the fast path*/) {
+                                                                  uint32_t /*nchunks: signature shared with the fast path*/,
+                                                                  const HotImage* /*hot: fast path only*/) {
   constexpr int kPer = kGenericTile / kConsumeBlock;
   constexpr int kWaves = kConsumeBlock / 64;
   __shared__ int32_t s_sel[kGenericTile];
@@ -506,6 +509,168 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
   return kDeferredSlot;
 }
 
+// ---------------------------------------------------------------------------------------
+// Hot-group cache: the north_star's LDS-resident per-workgroup hash table in front of the global
+// open-addressing table (the reference loop it serves: agg_node.cc:235-271 with the RowTuple
+// map probe, row_tuple.h:140-153).  A consume over many rows runs as two launches.  The prefix
+// launch (a few % of the rows) fills the global table as usual; HotCountKernel counts its staged
+// rows per slot and HotBuildKernel keeps the kHot most frequent groups as an image: a tag table
+// plus one 64-byte record per group (the global slot, the key lengths and the key bytes as
+// tail-masked words, the layout FastKeys holds in registers).  Every workgroup of the main launch
+// copies the image into LDS; a row whose key hashes to a cached tag is compared word by word
+// against the LDS record and takes its slot without touching the global table or the group's
+// representative row (6 divergent gathers saved per row: the slot word and the representative's
+// offsets and payload).  Rows of other groups -- misses -- probe the global table as before.
+// The image only names slots; a hit yields exactly the slot the global probe would find, so
+// results do not depend on the cache.
+// ---------------------------------------------------------------------------------------
+constexpr int kHot = 256;          // cached groups (top-256 (service, path) pairs: ~56 % of C2 rows)
+constexpr int kHotTags = 1024;     // LDS tag table, <= 25 % full
+constexpr int kHotProbe = 4;       // tag probes per row (a miss costs at most these LDS reads)
+constexpr int kHotRecWords = 8;    // header word + up to 7 key words (56 key bytes)
+constexpr int kSelCapHot = 12288;  // selection buffer of the hot variant (3 workgroups per CU)
+
+struct HotImage {
+  uint32_t tags[kHotTags];                // (tag22 << 10) | (record + 1); 0 = empty
+  uint64_t recs[kHot][kHotRecWords];      // [0] = slot | len_i << (32 + 8 i); key words follow
+};
+
+__device__ __forceinline__ uint32_t HotIdx(uint64_t h) { return static_cast<uint32_t>(h >> 20) & (kHotTags - 1); }
+__device__ __forceinline__ uint32_t HotTag(uint64_t h) { return static_cast<uint32_t>(h >> 42); }  // 22 bits
+
+// Exact key equality against an LDS record (RowTuple equality: same lengths, same bytes).
+template <int NK>
+__device__ __forceinline__ bool HotEqual(const uint64_t* rec, const FastKeys<NK>& k) {
+  const uint64_t h0 = rec[0];
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) eq = eq && ((h0 >> (32 + 8 * i)) & 255u) == k.len[i];
+  if (!eq) return false;  // equal lengths: the record holds every word compared below
+  int pos = 1;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int nw = static_cast<int>((k.len[i] + 7) >> 3);
+#pragma unroll
+    for (int j = 0; j < kFastStrWords; ++j)
+      if (j < nw) eq = eq && rec[pos + j] == k.w[i][j];
+    pos += nw;
+  }
+  return eq;
+}
+
+// Per-slot row counts of the staging records [0, *cursor) (the prefix launch's rows).  Each
+// workgroup aggregates into a direct-mapped LDS table first, so a hot slot costs one global
+// atomic per workgroup, not one per row.
+constexpr int kHotCountLds = 4096;
+__global__ void __launch_bounds__(256) HotCountKernel(const uint32_t* __restrict__ st_slot, const unsigned long long* __restrict__ cursor,
+                                                      uint32_t cap, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t key[kHotCountLds], c[kHotCountLds];
+  for (int i = threadIdx.x; i < kHotCountLds; i += 256) {
+    key[i] = 0xFFFFFFFFu;
+    c[i] = 0;
+  }
+  __syncthreads();
+  const uint64_t n = *cursor;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<uint64_t>(gridDim.x) * 256) {
+    const uint32_t sl = st_slot[i];
+    if (sl >= cap) continue;  // deferred rows
+    const uint32_t h = sl & (kHotCountLds - 1);
+    uint32_t old = key[h];
+    if (old == 0xFFFFFFFFu) old = atomicCAS(&key[h], 0xFFFFFFFFu, sl);
+    if (old == 0xFFFFFFFFu || old == sl) atomicAdd(&c[h], 1u);
+    else atomicAdd(&cnt[sl], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHotCountLds; i += 256)
+    if (c[i]) atomicAdd(&cnt[key[i]], c[i]);
+}
+
+// One workgroup: choose the kHot most frequent slots (whole power-of-two count bins from the top,
+// the boundary bin filled in any order), build their records from the representative rows
+// (or arena records of groups published by an earlier consume) and the LDS tag table.
+template <int NK>
+__global__ void __launch_bounds__(1024) HotBuildKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
+                                                       const unsigned long long* __restrict__ slots, uint32_t cap,
+                                                       const uint64_t* __restrict__ arena, const uint32_t* __restrict__ cnt,
+                                                       HotImage* __restrict__ out) {
+  __shared__ uint32_t lh[33];
+  __shared__ uint32_t s_tags[kHotTags];
+  __shared__ uint32_t s_pick[kHot];
+  __shared__ uint32_t s_n, s_take;
+  const int tid = threadIdx.x;
+  if (tid < 33) lh[tid] = 0;
+  for (int i = tid; i < kHotTags; i += 1024) s_tags[i] = 0;
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < cap; i += 1024) {
+    const uint32_t c = cnt[i];
+    if (c) atomicAdd(&lh[32 - __clz(c)], 1u);  // bin = floor(log2 c) + 1
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    int b = 32;
+    while (b >= 1 && acc + lh[b] <= static_cast<uint32_t>(kHot)) acc += lh[b--];
+    s_take = static_cast<uint32_t>(b);  // bins above b whole; bin b fills what is left
+  }
+  __syncthreads();
+  const uint32_t take = s_take;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (uint32_t i = tid; i < cap; i += 1024) {
+      const uint32_t c = cnt[i];
+      if (!c) continue;
+      const uint32_t bin = 32 - __clz(c);
+      if (pass == 0 ? bin > take : (bin == take && take > 0)) {
+        const uint32_t r = atomicAdd(&s_n, 1u);
+        if (r < static_cast<uint32_t>(kHot)) s_pick[r] = i;
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t n = min(s_n, static_cast<uint32_t>(kHot));
+  for (uint32_t r = tid; r < static_cast<uint32_t>(kHot); r += 1024) {
+    uint64_t rec[kHotRecWords] = {};
+    if (r < n) {
+      const uint32_t sl = s_pick[r];
+      const unsigned long long w = slots[sl];
+      KeySet k;
+      const uint32_t ref = static_cast<uint32_t>(w);
+      if (w & kKindArena) LoadKeysArena(plan, arena + ref, k);
+      else LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
+      bool ok = w != 0;
+      int pos = 1;
+      uint64_t lens = 0;
+      for (int i = 0; i < NK && ok; ++i) {
+        const uint32_t len = static_cast<uint32_t>(k.v[i].b);
+        const int nw = static_cast<int>((len + 7) >> 3);
+        if (len > 8u * kFastStrWords || pos + nw > kHotRecWords) {
+          ok = false;
+          break;
+        }
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[i].a);
+        for (int j = 0; j < nw; ++j) rec[pos + j] = LoadWordU(src + 8 * j) & TailMask(len - 8u * j);
+        pos += nw;
+        lens |= static_cast<uint64_t>(len) << (8 * i);
+      }
+      if (ok) {
+        rec[0] = static_cast<uint64_t>(sl) | (lens << 32);
+        const uint64_t h = HashKeys(plan, k);  // bit-identical to HashFastKeys
+        uint32_t idx = HotIdx(h);
+        const uint32_t e = (HotTag(h) << 10) | (r + 1);
+        for (int p = 0; p < kHotTags; ++p) {
+          if (atomicCAS(&s_tags[idx], 0u, e) == 0u) break;
+          idx = (idx + 1) & (kHotTags - 1);
+        }
+      } else {
+        for (int j = 0; j < kHotRecWords; ++j) rec[j] = 0;
+      }
+    }
+    for (int j = 0; j < kHotRecWords; ++j) out->recs[r][j] = rec[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < kHotTags; i += 1024) out->tags[i] = s_tags[i];
+}
+
 // MODE: 0 = production; 2 / 3 are timing-only diagnostic builds that stop after the filter
 // (2) or after key load + hash (3) and write garbage slots (tools/consume_diag.py; never
 // followed by finalize).
@@ -518,17 +683,20 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
 // that ends phase 2 waits for the slowest probe chain of the block, and more rows per barrier
 // amortise that wait (4096 -> 8192 -> 16384 rows per tile: 1.80 -> 1.64 -> 1.38 ms at C2).
 // Phase 2 is flushed early when the selection buffer could overflow (selectivity > 1/2).
-template <int NK, int MODE>
+template <int NK, int MODE, bool PAIRS = false, bool HOT = false>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
                                                                       int64_t ntiles, AggTableDev tab, StageDev stg,
-                                                                      uint32_t nchunks) {
+                                                                      uint32_t nchunks, const HotImage* __restrict__ hot) {
   constexpr bool S = (MODE & 4) != 0;  // all keys STRING
   constexpr int kPer = kSubRows / kConsumeBlock;
 
   constexpr int kWaves = kConsumeBlock / 64;
-  __shared__ uint16_t s_sel[kSelCap];
+  constexpr int kCap = HOT ? kSelCapHot : kSelCap;
+  __shared__ uint16_t s_sel[kCap];
+  __shared__ uint32_t s_htag[HOT ? kHotTags : 1];
+  __shared__ uint64_t s_hrec[HOT ? kHot : 1][kHotRecWords];
   __shared__ uint32_t s_wcnt[2][kWaves];
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
@@ -540,6 +708,10 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   if (threadIdx.x == 0) s_ins = 0;
   const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
   for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
+  if constexpr (HOT) {
+    for (int i = threadIdx.x; i < kHotTags; i += kConsumeBlock) s_htag[i] = hot->tags[i];
+    for (int i = threadIdx.x; i < kHot * kHotRecWords; i += kConsumeBlock) s_hrec[i / kHotRecWords][i % kHotRecWords] = hot->recs[i / kHotRecWords][i % kHotRecWords];
+  }
   __syncthreads();
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
     int ri = 0;
@@ -549,40 +721,88 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
     const int64_t row0 = rg.lo + (t - rg.tile0) * rg.tile_rows;
     const int64_t row1 = min(row0 + rg.tile_rows, rg.hi);
     const int kSubBatches = rg.tile_rows / kSubRows;
+    // The filter column streamed two rows per lane with 16-byte loads (an 8-byte column, even
+    // tile start): 8-byte loads stream at ~3.7 TB/s on gfx950, 16-byte ones at ~5.7 TB/s
+    // (tools/stream_probe.hip, profiles/r03_stream_probe*.log).  Uniform per tile.
+    // PAIRS: chosen on the host (an 8-byte filter column, every range starting at an even row).
     uint32_t total = 0;
 #pragma unroll 1
     for (int sb = 0; sb < kSubBatches; ++sb) {
       const int64_t sb0 = row0 + static_cast<int64_t>(sb) * kSubRows;
-      bool pass[kPer];
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
-        pass[k] = r < row1;
-        if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
-      }
-      unsigned long long m[kPer];
       uint32_t wtot = 0;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        m[k] = __ballot(pass[k]);
-        wtot += static_cast<uint32_t>(__popcll(m[k]));
-      }
-      if (lane == 0) s_wcnt[sb & 1][wid] = wtot;
-      __syncthreads();
       uint32_t wbase = total, sbtot = 0;
+      if constexpr (PAIRS) {
+        constexpr int kPairs = kPer / 2;
+        const uint64_t* fv = reinterpret_cast<const uint64_t*>(ch.cols[plan->filter.col].values);
+        // Pass bits per lane (bit k: pair k), not ballot words: 2 registers instead of 32
+        // scalar pairs live across the barrier; the ballots are re-taken after it.
+        uint32_t be = 0, bo = 0;
+        const ulonglong2* fv2 = reinterpret_cast<const ulonglong2*>(fv);
+        const DevProgram* fp = &plan->filter;
+        const int64_t r0 = sb0 + 2 * static_cast<int64_t>(threadIdx.x);
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
-        const uint32_t c = s_wcnt[sb & 1][w];
-        wbase += w < wid ? c : 0;
-        sbtot += c;
-      }
+        for (int k = 0; k < kPairs; ++k) {
+          const int64_t r = r0 + 2 * k * kConsumeBlock;
+          ulonglong2 v = make_ulonglong2(0, 0);
+          if (r + 1 < row1) v = fv2[r >> 1];
+          else if (r < row1) v.x = fv[r];
+          be |= static_cast<uint32_t>(r < row1 && ApplyShape(fp, v.x) != 0) << k;
+          bo |= static_cast<uint32_t>(r + 1 < row1 && ApplyShape(fp, v.y) != 0) << k;
+        }
+        // The wave's count as a lane reduction (no ballot words live across the barrier).
+        uint32_t c = static_cast<uint32_t>(__popc(be) + __popc(bo));
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = static_cast<uint16_t>(sb * kSubRows + k * kConsumeBlock + threadIdx.x);
-        wbase += static_cast<uint32_t>(__popcll(m[k]));
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        wtot = c;
+        if (lane == 0) s_wcnt[sb & 1][wid] = wtot;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+          const uint32_t c = s_wcnt[sb & 1][w];
+          wbase += w < wid ? c : 0;
+          sbtot += c;
+        }
+        // Row order inside the wave: lane l's even row follows both rows of every lower lane.
+#pragma unroll
+        for (int k = 0; k < kPairs; ++k) {
+          const bool pe = (be >> k) & 1u, po = (bo >> k) & 1u;
+          const unsigned long long me = __ballot(pe), mo = __ballot(po);
+          const uint32_t at = wbase + static_cast<uint32_t>(__popcll(me & lanemask_lt) + __popcll(mo & lanemask_lt));
+          const uint16_t off = static_cast<uint16_t>(sb * kSubRows + 2 * (k * kConsumeBlock + threadIdx.x));
+          if (pe) s_sel[at] = off;
+          if (po) s_sel[at + (pe ? 1 : 0)] = static_cast<uint16_t>(off + 1);
+          wbase += static_cast<uint32_t>(__popcll(me) + __popcll(mo));
+        }
+      } else {
+        bool pass[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+          const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
+          pass[k] = r < row1;
+          if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
+        }
+        unsigned long long m[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+          m[k] = __ballot(pass[k]);
+          wtot += static_cast<uint32_t>(__popcll(m[k]));
+        }
+        if (lane == 0) s_wcnt[sb & 1][wid] = wtot;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+          const uint32_t c = s_wcnt[sb & 1][w];
+          wbase += w < wid ? c : 0;
+          sbtot += c;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+          if (pass[k]) s_sel[wbase + __popcll(m[k] & lanemask_lt)] = static_cast<uint16_t>(sb * kSubRows + k * kConsumeBlock + threadIdx.x);
+          wbase += static_cast<uint32_t>(__popcll(m[k]));
+        }
       }
       total += sbtot;
-      if (sb + 1 < kSubBatches && total + kSubRows <= kSelCap) continue;
+      if (sb + 1 < kSubBatches && total + kSubRows <= kCap) continue;
       // Phase 2 over the rows collected so far.
       if (threadIdx.x == 0) {
         if (s_ins) {
@@ -617,7 +837,26 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
+          bool hit = false;
+          if constexpr (HOT) {
+            uint32_t idx = HotIdx(h);
+            const uint32_t tg = HotTag(h);
+#pragma unroll
+            for (int p = 0; p < kHotProbe; ++p) {
+              const uint32_t e = s_htag[idx];
+              if (e == 0) break;
+              if ((e >> 10) == tg) {
+                const uint64_t* rec = s_hrec[(e & 1023u) - 1];
+                if (HotEqual<NK>(rec, k)) {
+                  slot = static_cast<uint32_t>(rec[0]);
+                  hit = true;
+                  break;
+                }
+              }
+              idx = (idx + 1) & (kHotTags - 1);
+            }
+          }
+          if (!hit) slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -842,22 +1081,44 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     }();
     if (forced) tile_rows = forced;
   }
-  std::vector<TileRange> ranges;
-  int64_t ntiles = 0;
-  for (size_t c = 0; c < t->chunks.size(); ++c) {
-    const Chunk& ch = *t->chunks[c];
-    const int64_t lo = std::max(begin, ch.row_base) - ch.row_base;
-    const int64_t hi = std::min(end, ch.row_base + ch.nrows) - ch.row_base;
-    if (lo >= hi) continue;
-    TileRange r;
-    r.tile0 = ntiles;
-    r.lo = lo;
-    r.hi = hi;
-    r.chunk = static_cast<int32_t>(c);
-    r.tile_rows = static_cast<int32_t>(tile_rows);
-    ranges.push_back(r);
-    ntiles += (hi - lo + tile_rows - 1) / tile_rows;
+  static const int diag = [] {
+    const char* e = std::getenv("PXG_DIAG_CONSUME");
+    return e ? std::atoi(e) : 0;
+  }();
+  const bool hot_ok = fast_nk > 0 && (diag & 3) == 0 && !EnvFlag("PXG_NO_HOT");
+  bool all_str = true;
+  for (int i = 0; i < n_keys; ++i) all_str = all_str && key_types[i] == PXG_STRING;
+  // Two launches (hot-group cache, HotBuildKernel above) for large all-STRING-key consumes: a
+  // prefix of ~2 % of the rows (>= 2M), then the rest with the LDS cache of its top groups.
+  int64_t prefix = 0;
+  if (hot_ok && all_str && end - begin >= (int64_t(1) << 23)) {
+    prefix = std::max<int64_t>(int64_t(1) << 21, (end - begin) / 50);
+    prefix = (prefix + kConsumeTile - 1) / kConsumeTile * kConsumeTile;
   }
+  // Tile ranges of [b, e) in `rs` (tiles of `tr` rows, appended; tile0 counted from t0).
+  auto make_ranges = [&](int64_t b, int64_t e, int64_t tr, std::vector<TileRange>* rs) {
+    int64_t nt = 0;
+    for (size_t c = 0; c < t->chunks.size(); ++c) {
+      const Chunk& ch = *t->chunks[c];
+      const int64_t lo = std::max(b, ch.row_base) - ch.row_base;
+      const int64_t hi = std::min(e, ch.row_base + ch.nrows) - ch.row_base;
+      if (lo >= hi) continue;
+      TileRange r;
+      r.tile0 = nt;
+      r.lo = lo;
+      r.hi = hi;
+      r.chunk = static_cast<int32_t>(c);
+      r.tile_rows = static_cast<int32_t>(tr);
+      rs->push_back(r);
+      nt += (hi - lo + tr - 1) / tr;
+    }
+    return nt;
+  };
+  std::vector<TileRange> ranges;
+  const int64_t ntiles_a = prefix > 0 ? make_ranges(begin, begin + prefix, kConsumeTile, &ranges) : 0;
+  const size_t nranges_a = ranges.size();
+  const int64_t ntiles = make_ranges(begin + prefix, end, tile_rows, &ranges);
+  const size_t nranges_b = ranges.size() - nranges_a;
   if (ranges.empty()) return PXG_OK;
   const int64_t rows = end - begin;
   if (st_n + static_cast<uint64_t>(rows) >= (uint64_t(1) << 32))
@@ -880,42 +1141,85 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     const int64_t v = e ? std::atoll(e) : 0;
     return v > 0 ? v : 8;
   }();
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * bpc));
-  void (*kern)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t) = AggConsumeKernel;
-  static const int diag = [] {
-    const char* e = std::getenv("PXG_DIAG_CONSUME");
-    return e ? std::atoi(e) : 0;
-  }();
-  switch (fast_nk * 4 + (diag & 3)) {
+  using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t,
+                          const HotImage*);
+  // 16-byte pair loads of the filter column: an 8-byte column, every tile starting at an even
+  // row (device column buffers are allocated 256-byte aligned).
+  bool pairs = hplan.has_filter && !EnvFlag("PXG_NO_PAIRS");
+  if (pairs) {
+    const int ft = hplan.col_types[hplan.filter.col];
+    pairs = ft == PXG_INT64 || ft == PXG_FLOAT64 || ft == PXG_TIME64NS;
+    for (const TileRange& r : ranges) pairs = pairs && (r.lo & 1) == 0;
+    for (const auto& c : t->chunks) pairs = pairs && (reinterpret_cast<uintptr_t>(c->cols[hplan.filter.col].values.p) & 15) == 0;
+  }
+  auto pick = [&](bool hot) -> KernFn {
+    KernFn kern = AggConsumeKernel;
+    switch (fast_nk * 4 + (diag & 3)) {
 #define PXG_FAST_CASE(nk)                                           \
   case nk * 4 + 0:                                                  \
   case nk * 4 + 1: kern = AggConsumeFastKernel<nk, 0>; break;       \
   case nk * 4 + 2: kern = AggConsumeFastKernel<nk, 2>; break;       \
   case nk * 4 + 3: kern = AggConsumeFastKernel<nk, 3>; break;
-    PXG_FAST_CASE(1)
-    PXG_FAST_CASE(2)
-    PXG_FAST_CASE(3)
-    PXG_FAST_CASE(4)
+      PXG_FAST_CASE(1)
+      PXG_FAST_CASE(2)
+      PXG_FAST_CASE(3)
+      PXG_FAST_CASE(4)
 #undef PXG_FAST_CASE
-    default: break;
-  }
-  if (fast_nk > 0 && (diag & 3) == 0) {  // all-STRING keys: the specialised production kernel
-    bool all_str = true;
-    for (int i = 0; i < n_keys; ++i) all_str = all_str && key_types[i] == PXG_STRING;
-    if (all_str) {
+      default: break;
+    }
+    if (fast_nk == 0 || (diag & 3) != 0) return kern;
+    if (all_str) {  // all-STRING keys: the specialised production kernels
+#define PXG_STR_CASE(nk)                                                                   \
+  case nk:                                                                                 \
+    if (hot) kern = pairs ? AggConsumeFastKernel<nk, 4, true, true> : AggConsumeFastKernel<nk, 4, false, true>; \
+    else kern = pairs ? AggConsumeFastKernel<nk, 4, true> : AggConsumeFastKernel<nk, 4>;     \
+    break;
       switch (fast_nk) {
-        case 1: kern = AggConsumeFastKernel<1, 4>; break;
-        case 2: kern = AggConsumeFastKernel<2, 4>; break;
-        case 3: kern = AggConsumeFastKernel<3, 4>; break;
-        case 4: kern = AggConsumeFastKernel<4, 4>; break;
+        PXG_STR_CASE(1)
+        PXG_STR_CASE(2)
+        PXG_STR_CASE(3)
+        PXG_STR_CASE(4)
+        default: break;
+      }
+#undef PXG_STR_CASE
+    } else if (pairs) {
+      switch (fast_nk) {
+        case 1: kern = AggConsumeFastKernel<1, 0, true>; break;
+        case 2: kern = AggConsumeFastKernel<2, 0, true>; break;
+        case 3: kern = AggConsumeFastKernel<3, 0, true>; break;
+        case 4: kern = AggConsumeFastKernel<4, 0, true>; break;
         default: break;
       }
     }
+    return kern;
+  };
+  const TileRange* d_rg = d_ranges.as<const TileRange>();
+  const HotImage* d_hot = nullptr;
+  if (prefix > 0) {
+    // Launch A: the prefix, no cache.  Then the per-slot counts of its staged rows and the image.
+    const int grid_a = static_cast<int>(std::min<int64_t>(ntiles_a, static_cast<int64_t>(ctx->num_cus) * bpc));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(false), dim3(grid_a), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
+                               t->d_chunks.as<const DevChunk>(), d_rg, static_cast<int>(nranges_a), ntiles_a, TableDev(this, 0),
+                               StageDevOf(this), static_cast<uint32_t>(t->chunks.size()), d_hot));
+    PXG_RETURN_IF_ERROR(hot_cnt.Ensure(static_cast<size_t>(cap) * 4));
+    PXG_RETURN_IF_ERROR(hot_img.Ensure(sizeof(HotImage)));
+    PXG_HIP(hipMemsetAsync(hot_cnt.p, 0, static_cast<size_t>(cap) * 4, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_hot_count", HotCountKernel, dim3(ctx->num_cus), dim3(256), 0, st_slot.as<const uint32_t>(),
+                               reinterpret_cast<const unsigned long long*>(counters.as<uint8_t>() + 16), cap, hot_cnt.as<uint32_t>()));
+    void (*build)(const AggPlanDev*, const DevChunk*, const unsigned long long*, uint32_t, const uint64_t*, const uint32_t*, HotImage*) =
+        fast_nk == 1 ? HotBuildKernel<1> : fast_nk == 2 ? HotBuildKernel<2> : fast_nk == 3 ? HotBuildKernel<3> : HotBuildKernel<4>;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_hot_build", build, dim3(1), dim3(1024), 0, d_plan.as<const AggPlanDev>(),
+                               t->d_chunks.as<const DevChunk>(), slots.as<const unsigned long long>(), cap, arena.as<const uint64_t>(),
+                               hot_cnt.as<const uint32_t>(), hot_img.as<HotImage>()));
+    d_hot = hot_img.as<const HotImage>();
   }
-  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", kern, dim3(grid), dim3(kConsumeBlock), 0,
-                             d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_ranges.as<const TileRange>(),
-                             static_cast<int>(ranges.size()), ntiles, TableDev(this, 0), StageDevOf(this),
-                             static_cast<uint32_t>(t->chunks.size())));
+  if (nranges_b > 0) {
+    const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * bpc));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(d_hot != nullptr), dim3(grid), dim3(kConsumeBlock), 0,
+                               d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_rg + nranges_a,
+                               static_cast<int>(nranges_b), ntiles, TableDev(this, 0), StageDevOf(this),
+                               static_cast<uint32_t>(t->chunks.size()), d_hot));
+  }
   clk.Mark("consume: launch");
   uint32_t n_def = 0;
   PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));

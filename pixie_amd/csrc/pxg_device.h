@@ -252,6 +252,22 @@ __device__ __forceinline__ uint64_t EvalShape(const DevProgram* __restrict__ p, 
   return BinOp(p->binop, x, static_cast<uint64_t>(p->cimm));
 }
 
+// A fast shape applied to an already loaded value of its (fixed-width) column.
+__device__ __forceinline__ uint64_t ApplyShape(const DevProgram* __restrict__ p, uint64_t v) {
+  if (p->shape == kShapeCol) return v;
+  const uint64_t x = p->conv ? Conv(p->conv, v) : v;
+  return BinOp(p->binop, x, static_cast<uint64_t>(p->cimm));
+}
+
+// Whether rows of a fast shape's column can be read two at a time with 16-byte loads: an 8-byte
+// column whose values start 16-byte aligned (the pair loads then start at even rows).
+__device__ __forceinline__ bool PairLoadable(const DevProgram* __restrict__ p, const DevChunk& ch,
+                                             const int32_t* __restrict__ col_types) {
+  const int t = col_types[p->col];
+  return (t == PXG_INT64 || t == PXG_FLOAT64 || t == PXG_TIME64NS) &&
+         (reinterpret_cast<uintptr_t>(ch.cols[p->col].values) & 15) == 0;
+}
+
 // Evaluate a program on row r of chunk ch.  Uniform control flow across the wave (every lane
 // runs the same program); the generic path keeps its stack in private memory.
 __device__ inline Val EvalProgram(const DevProgram* __restrict__ p, const DevChunk& ch, int64_t r,
