@@ -74,6 +74,11 @@ def parse():
                     help="skip the live PMC leg (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this build's consume)")
     ap.add_argument("--pmc-child", type=int, default=0, metavar="ROWS",
                     help=argparse.SUPPRESS)  # internal: the consume-only workload the PMC leg profiles
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="shard processes of the supplementary CPU baseline (SURVEY.md §8d: P PEMs + merge); "
+                         "16 = the GPU box's CPU share; 0 disables")
+    ap.add_argument("--cpu-shard-child", type=int, nargs=3, default=None, metavar=("ROW0", "ROWS", "BATCH"),
+                    help=argparse.SUPPRESS)  # internal: one shard process of the parallel CPU baseline
     return ap.parse_args()
 
 
@@ -161,6 +166,9 @@ def main():
     args = parse()
     if args.pmc_child:
         pmc_child(args.pmc_child)
+        return
+    if args.cpu_shard_child:
+        cpu_shard_child(*args.cpu_shard_child)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -313,6 +321,8 @@ def main():
     cpu, par = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, par = oracle_leg(args, n, row0, dev_result)
+        if cpu is not None and args.cpu_procs > 0:
+            cpu["parallel"] = cpu_parallel_leg(args, n, row0)
     elif world > 1:
         par = {"skipped": "N>1: shard-exchange parity is tests/test_scale_parity.py (8-way) and tests/test_partial.py"}
 
@@ -686,6 +696,54 @@ def n1_parity(dev, n):
         import traceback
         traceback.print_exc()
         return {"ok": False, "error": f"n1 parity failed: {e}"}
+
+
+def cpu_shard_child(row0, rows, batch_rows):
+    """One shard process of the parallel CPU baseline: the C2 plan over rows [row0, row0+rows)
+    through the CPU Carnot restatement (one thread); prints its execution window."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_client as oc
+    from pixie_amd import plans as P
+    from pixie_amd.device import datagen_http_events
+    need = {P.HE["service"], P.HE["req_path"], P.HE["resp_status"], P.HE["latency"]}
+    cols = datagen_http_events(SEED, row0, rows, n_pair_keys=N_PAIR_KEYS, threads=1)
+    batch = [c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)]
+    tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [batch], "names": P.HTTP_NAMES}}
+    secs, res = oc.execute_plan_timed(P.c2_plan(with_pluck=False), tables, batch_rows=batch_rows)
+    print(json.dumps({"secs": secs, "rows": rows, "groups": len(res["output"][0]["cols"][0])}), flush=True)
+
+
+def cpu_parallel_leg(args, n, row0):
+    """Supplementary CPU baseline (P PEMs): P processes, each running the C2
+    plan over its own 1/P row shard with the CPU Carnot restatement, started together; the value
+    is n / the slowest shard's execution window.  The PEM -> Kelvin merge is left out (quantiles
+    have no Serialize in the reference, udf.h:367, so it cannot be split at all), which makes this
+    an upper bound for the CPU.  Processes are children (fresh interpreters), never forks."""
+    import subprocess
+    procs = args.cpu_procs
+    try:
+        per = (n + procs - 1) // procs
+        kids = []
+        for p in range(procs):
+            a = p * per
+            k = min(per, n - a)
+            if k <= 0:
+                break
+            kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-shard-child", str(row0 + a), str(k),
+                                          str(args.cpu_batch_rows)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL))
+        outs = []
+        for kp in kids:
+            o, _ = kp.communicate(timeout=600)
+            if kp.returncode != 0:
+                return {"error": f"shard process exited {kp.returncode}"}
+            outs.append(json.loads(o.decode().strip().splitlines()[-1]))
+        slow = max(o["secs"] for o in outs)
+        return {"value": n / slow, "unit": "rows/s", "cores": len(outs), "kind": "port",
+                "sample": f"all {n} rows in {len(outs)} shard processes of {per} rows (one thread each, started together), "
+                          f"C2 plan per shard; slowest execution window {slow:.2f} s (mean {sum(o['secs'] for o in outs) / len(outs):.2f} s); "
+                          f"PEM-side only, no merge (quantiles have no Serialize, udf.h:367): an upper bound for P PEMs"}
+    except Exception as e:  # the legs must never break the bench line
+        return {"error": f"parallel cpu leg failed: {e}"}
 
 
 def oracle_leg(args, n, row0, dev_result):

@@ -63,6 +63,7 @@ struct Agg {
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint32_t last_big_sort_groups = 0;  // pxg_agg_stats.big_sort_groups
   uint64_t inserted = 0;     // host mirror
+  uint64_t last_groups = 0;  // groups of the last run with any (table sizing across resets)
 
   // Staging (one record per selected row).
   DevBuf st_slot;

@@ -1847,14 +1847,18 @@ class GpuEquijoinNode : public ExecNode {
     for (int64_t b = 0; b < nprobe; b += rows_per_batch_) ranges.push_back({b, std::min(nprobe, b + rows_per_batch_)});
     for (int64_t b = nprobe; b < n; b += rows_per_batch_) ranges.push_back({b, std::min(n, b + rows_per_batch_)});
     if (ranges.empty()) return SendRowBatchToChildren(s, ZeroRowBatch(output_, true, true));
+    // One device-to-host fetch per output column; the batches are slices of it (a fetch per
+    // batch and column cost ~140 us each: 2634 batches of C5 took 370 ms).
+    std::vector<HostColumn> full;
+    for (size_t c = 0; c < out_side_.size(); ++c) {
+      pxg_column_out o{};
+      PXG_CALL(pxg_table_fetch(out, static_cast<int32_t>(c), 0, n, &o));
+      full.push_back(FromOut(o));
+    }
     for (size_t r = 0; r < ranges.size(); ++r) {
       RowBatch ob;
       ob.num_rows = ranges[r].second - ranges[r].first;
-      for (size_t c = 0; c < out_side_.size(); ++c) {
-        pxg_column_out o{};
-        PXG_CALL(pxg_table_fetch(out, static_cast<int32_t>(c), ranges[r].first, ranges[r].second, &o));
-        ob.cols.push_back(FromOut(o));
-      }
+      for (auto& fc : full) ob.cols.push_back(SliceColumn(fc, ranges[r].first, ob.num_rows));
       ob.eow = ob.eos = r + 1 == ranges.size();
       PXC_RETURN_IF_ERROR(SendRowBatchToChildren(s, ob));
     }
