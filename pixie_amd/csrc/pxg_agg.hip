@@ -32,12 +32,9 @@ struct TileRange {
   int64_t hi;
   int32_t chunk;
   int32_t tile_rows;  // rows per tile (fast kernel; the generic kernel uses kGenericTile)
-  int32_t pay_end[kMaxKeys];  // payload bytes of each STRING group-key column of the chunk (streamed kernel)
 };
 
 constexpr uint32_t kMaxProbe = 256;  // longer probe sequences defer the row (table grows)
-
-struct HotImage;  // the hot-group cache image (below)
 
 // Probe for the row's group; insert it (CAS of an empty slot word) when absent.  Inserts are
 // counted in the workgroup's LDS counter (`s_ins`) and flushed once per tile, so no per-row
@@ -123,8 +120,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeKernel(const AggPlanD
                                                                   const DevChunk* __restrict__ chunks,
                                                                   const TileRange* __restrict__ ranges, int nranges,
                                                                   int64_t ntiles, AggTableDev tab, StageDev stg,
-                                                                  uint32_t /*nchunks: signature shared with the fast path*/,
-                                                                  const HotImage* /*hot: fast path only*/) {
+                                                                  uint32_t /*nchunks: signature shared with the fast path*/) {
   constexpr int kPer = kGenericTile / kConsumeBlock;
   constexpr int kWaves = kConsumeBlock / 64;
   __shared__ int32_t s_sel[kGenericTile];
@@ -510,168 +506,6 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
   return kDeferredSlot;
 }
 
-// ---------------------------------------------------------------------------------------
-// Hot-group cache: the north_star's LDS-resident per-workgroup hash table in front of the global
-// open-addressing table (the reference loop it serves: agg_node.cc:235-271 with the RowTuple
-// map probe, row_tuple.h:140-153).  A consume over many rows runs as two launches.  The prefix
-// launch (a few % of the rows) fills the global table as usual; HotCountKernel counts its staged
-// rows per slot and HotBuildKernel keeps the kHot most frequent groups as an image: a tag table
-// plus one 64-byte record per group (the global slot, the key lengths and the key bytes as
-// tail-masked words, the layout FastKeys holds in registers).  Every workgroup of the main launch
-// copies the image into LDS; a row whose key hashes to a cached tag is compared word by word
-// against the LDS record and takes its slot without touching the global table or the group's
-// representative row (6 divergent gathers saved per row: the slot word and the representative's
-// offsets and payload).  Rows of other groups -- misses -- probe the global table as before.
-// The image only names slots; a hit yields exactly the slot the global probe would find, so
-// results do not depend on the cache.
-// ---------------------------------------------------------------------------------------
-constexpr int kHot = 256;          // cached groups (top-256 (service, path) pairs: ~56 % of C2 rows)
-constexpr int kHotTags = 1024;     // LDS tag table, <= 25 % full
-constexpr int kHotProbe = 4;       // tag probes per row (a miss costs at most these LDS reads)
-constexpr int kHotRecWords = 8;    // header word + up to 7 key words (56 key bytes)
-constexpr int kSelCapHot = 12288;  // selection buffer of the hot variant (3 workgroups per CU)
-
-struct HotImage {
-  uint32_t tags[kHotTags];                // (tag22 << 10) | (record + 1); 0 = empty
-  uint64_t recs[kHot][kHotRecWords];      // [0] = slot | len_i << (32 + 8 i); key words follow
-};
-
-__device__ __forceinline__ uint32_t HotIdx(uint64_t h) { return static_cast<uint32_t>(h >> 20) & (kHotTags - 1); }
-__device__ __forceinline__ uint32_t HotTag(uint64_t h) { return static_cast<uint32_t>(h >> 42); }  // 22 bits
-
-// Exact key equality against an LDS record (RowTuple equality: same lengths, same bytes).
-template <int NK>
-__device__ __forceinline__ bool HotEqual(const uint64_t* rec, const FastKeys<NK>& k) {
-  const uint64_t h0 = rec[0];
-  bool eq = true;
-#pragma unroll
-  for (int i = 0; i < NK; ++i) eq = eq && ((h0 >> (32 + 8 * i)) & 255u) == k.len[i];
-  if (!eq) return false;  // equal lengths: the record holds every word compared below
-  int pos = 1;
-#pragma unroll
-  for (int i = 0; i < NK; ++i) {
-    const int nw = static_cast<int>((k.len[i] + 7) >> 3);
-#pragma unroll
-    for (int j = 0; j < kFastStrWords; ++j)
-      if (j < nw) eq = eq && rec[pos + j] == k.w[i][j];
-    pos += nw;
-  }
-  return eq;
-}
-
-// Per-slot row counts of the staging records [0, *cursor) (the prefix launch's rows).  Each
-// workgroup aggregates into a direct-mapped LDS table first, so a hot slot costs one global
-// atomic per workgroup, not one per row.
-constexpr int kHotCountLds = 4096;
-__global__ void __launch_bounds__(256) HotCountKernel(const uint32_t* __restrict__ st_slot, const unsigned long long* __restrict__ cursor,
-                                                      uint32_t cap, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t key[kHotCountLds], c[kHotCountLds];
-  for (int i = threadIdx.x; i < kHotCountLds; i += 256) {
-    key[i] = 0xFFFFFFFFu;
-    c[i] = 0;
-  }
-  __syncthreads();
-  const uint64_t n = *cursor;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<uint64_t>(gridDim.x) * 256) {
-    const uint32_t sl = st_slot[i];
-    if (sl >= cap) continue;  // deferred rows
-    const uint32_t h = sl & (kHotCountLds - 1);
-    uint32_t old = key[h];
-    if (old == 0xFFFFFFFFu) old = atomicCAS(&key[h], 0xFFFFFFFFu, sl);
-    if (old == 0xFFFFFFFFu || old == sl) atomicAdd(&c[h], 1u);
-    else atomicAdd(&cnt[sl], 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kHotCountLds; i += 256)
-    if (c[i]) atomicAdd(&cnt[key[i]], c[i]);
-}
-
-// One workgroup: choose the kHot most frequent slots (whole power-of-two count bins from the top,
-// the boundary bin filled in any order), build their records from the representative rows
-// (or arena records of groups published by an earlier consume) and the LDS tag table.
-template <int NK>
-__global__ void __launch_bounds__(1024) HotBuildKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
-                                                       const unsigned long long* __restrict__ slots, uint32_t cap,
-                                                       const uint64_t* __restrict__ arena, const uint32_t* __restrict__ cnt,
-                                                       HotImage* __restrict__ out) {
-  __shared__ uint32_t lh[33];
-  __shared__ uint32_t s_tags[kHotTags];
-  __shared__ uint32_t s_pick[kHot];
-  __shared__ uint32_t s_n, s_take;
-  const int tid = threadIdx.x;
-  if (tid < 33) lh[tid] = 0;
-  for (int i = tid; i < kHotTags; i += 1024) s_tags[i] = 0;
-  if (tid == 0) s_n = 0;
-  __syncthreads();
-  for (uint32_t i = tid; i < cap; i += 1024) {
-    const uint32_t c = cnt[i];
-    if (c) atomicAdd(&lh[32 - __clz(c)], 1u);  // bin = floor(log2 c) + 1
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    int b = 32;
-    while (b >= 1 && acc + lh[b] <= static_cast<uint32_t>(kHot)) acc += lh[b--];
-    s_take = static_cast<uint32_t>(b);  // bins above b whole; bin b fills what is left
-  }
-  __syncthreads();
-  const uint32_t take = s_take;
-  for (int pass = 0; pass < 2; ++pass) {
-    for (uint32_t i = tid; i < cap; i += 1024) {
-      const uint32_t c = cnt[i];
-      if (!c) continue;
-      const uint32_t bin = 32 - __clz(c);
-      if (pass == 0 ? bin > take : (bin == take && take > 0)) {
-        const uint32_t r = atomicAdd(&s_n, 1u);
-        if (r < static_cast<uint32_t>(kHot)) s_pick[r] = i;
-      }
-    }
-    __syncthreads();
-  }
-  const uint32_t n = min(s_n, static_cast<uint32_t>(kHot));
-  for (uint32_t r = tid; r < static_cast<uint32_t>(kHot); r += 1024) {
-    uint64_t rec[kHotRecWords] = {};
-    if (r < n) {
-      const uint32_t sl = s_pick[r];
-      const unsigned long long w = slots[sl];
-      KeySet k;
-      const uint32_t ref = static_cast<uint32_t>(w);
-      if (w & kKindArena) LoadKeysArena(plan, arena + ref, k);
-      else LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
-      bool ok = w != 0;
-      int pos = 1;
-      uint64_t lens = 0;
-      for (int i = 0; i < NK && ok; ++i) {
-        const uint32_t len = static_cast<uint32_t>(k.v[i].b);
-        const int nw = static_cast<int>((len + 7) >> 3);
-        if (len > 8u * kFastStrWords || pos + nw > kHotRecWords) {
-          ok = false;
-          break;
-        }
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[i].a);
-        for (int j = 0; j < nw; ++j) rec[pos + j] = LoadWordU(src + 8 * j) & TailMask(len - 8u * j);
-        pos += nw;
-        lens |= static_cast<uint64_t>(len) << (8 * i);
-      }
-      if (ok) {
-        rec[0] = static_cast<uint64_t>(sl) | (lens << 32);
-        const uint64_t h = HashKeys(plan, k);  // bit-identical to HashFastKeys
-        uint32_t idx = HotIdx(h);
-        const uint32_t e = (HotTag(h) << 10) | (r + 1);
-        for (int p = 0; p < kHotTags; ++p) {
-          if (atomicCAS(&s_tags[idx], 0u, e) == 0u) break;
-          idx = (idx + 1) & (kHotTags - 1);
-        }
-      } else {
-        for (int j = 0; j < kHotRecWords; ++j) rec[j] = 0;
-      }
-    }
-    for (int j = 0; j < kHotRecWords; ++j) out->recs[r][j] = rec[j];
-  }
-  __syncthreads();
-  for (int i = tid; i < kHotTags; i += 1024) out->tags[i] = s_tags[i];
-}
-
 // MODE: 0 = production; 2 / 3 are timing-only diagnostic builds that stop after the filter
 // (2) or after key load + hash (3) and write garbage slots (tools/consume_diag.py; never
 // followed by finalize).
@@ -684,20 +518,18 @@ __global__ void __launch_bounds__(1024) HotBuildKernel(const AggPlanDev* __restr
 // that ends phase 2 waits for the slowest probe chain of the block, and more rows per barrier
 // amortise that wait (4096 -> 8192 -> 16384 rows per tile: 1.80 -> 1.64 -> 1.38 ms at C2).
 // Phase 2 is flushed early when the selection buffer could overflow (selectivity > 1/2).
-template <int NK, int MODE, bool PAIRS = false, bool HOT = false>
+template <int NK, int MODE, bool PAIRS = false>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
                                                                       int64_t ntiles, AggTableDev tab, StageDev stg,
-                                                                      uint32_t nchunks, const HotImage* __restrict__ hot) {
+                                                                      uint32_t nchunks) {
   constexpr bool S = (MODE & 4) != 0;  // all keys STRING
   constexpr int kPer = kSubRows / kConsumeBlock;
 
   constexpr int kWaves = kConsumeBlock / 64;
-  constexpr int kCap = HOT ? kSelCapHot : kSelCap;
+  constexpr int kCap = kSelCap;
   __shared__ uint16_t s_sel[kCap];
-  __shared__ uint32_t s_htag[HOT ? kHotTags : 1];
-  __shared__ uint64_t s_hrec[HOT ? kHot : 1][kHotRecWords];
   __shared__ uint32_t s_wcnt[2][kWaves];
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
@@ -709,10 +541,6 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   if (threadIdx.x == 0) s_ins = 0;
   const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
   for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
-  if constexpr (HOT) {
-    for (int i = threadIdx.x; i < kHotTags; i += kConsumeBlock) s_htag[i] = hot->tags[i];
-    for (int i = threadIdx.x; i < kHot * kHotRecWords; i += kConsumeBlock) s_hrec[i / kHotRecWords][i % kHotRecWords] = hot->recs[i / kHotRecWords][i % kHotRecWords];
-  }
   __syncthreads();
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
     int ri = 0;
@@ -838,26 +666,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          bool hit = false;
-          if constexpr (HOT) {
-            uint32_t idx = HotIdx(h);
-            const uint32_t tg = HotTag(h);
-#pragma unroll
-            for (int p = 0; p < kHotProbe; ++p) {
-              const uint32_t e = s_htag[idx];
-              if (e == 0) break;
-              if ((e >> 10) == tg) {
-                const uint64_t* rec = s_hrec[(e & 1023u) - 1];
-                if (HotEqual<NK>(rec, k)) {
-                  slot = static_cast<uint32_t>(rec[0]);
-                  hit = true;
-                  break;
-                }
-              }
-              idx = (idx + 1) & (kHotTags - 1);
-            }
-          }
-          if (!hit) slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
+          slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -881,327 +690,6 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
 }
 
 // ---------------------------------------------------------------------------------------
-// Streamed keys (north_star: coalesced column scans).  The fast kernel above gathers every
-// selected row's string offsets and payload with divergent loads: ~5 instructions per row whose
-// 64 lanes touch up to 64 different lines each, and the texture addresser that serves them is
-// the measured limiter (TA busy 81 %).  Here the key columns are read the way the
-// filter column is: per window of `win_rows` rows, the offsets and the payload byte range of
-// every STRING key are streamed with coalesced 16-byte loads (64 lanes -> 8 lines per
-// instruction) into LDS, and phase 2 reads each selected row's key out of LDS.  The next
-// window's loads are issued into registers before the current window's rows are hashed and
-// probed, so HBM streams while the probes wait.  The payload start of a window is the end
-// offset of the previous one (already in LDS); a row whose string runs past the loaded window
-// (an unusually long window) takes the global gather instead.  Group table, hot image,
-// representative comparison, deferral and staging are those of the fast kernel.
-// ---------------------------------------------------------------------------------------
-constexpr int kStSelCap = 4096;                                   // selected rows per phase-2 flush (u16 in LDS)
-constexpr int kStSubRows = 2048;                                  // phase-1 sub-batch: 8 rows per thread
-constexpr int kStWinMaxRows = 1024;                               // rows per key window (upper bound)
-constexpr int kStPayBytes = 36864;                                // LDS payload window of all keys together
-constexpr int kStPayPieces = kStPayBytes / 16;
-constexpr int kStPiecesPerThread = kStPayPieces / kConsumeBlock;  // 9 x 16 B in flight per thread
-constexpr int kStOffPieces = (kStWinMaxRows + 8) / 4;             // 258 x 16 B offsets pieces per key
-constexpr int kStMaxWins = kConsumeTileMax / 256 + 2;             // windows per flush (win_rows >= 256)
-static_assert(kStPayPieces % kConsumeBlock == 0, "payload pieces per thread");
-
-struct StreamCfg {
-  int32_t win_rows;                  // rows per window, a multiple of 64 in [256, kStWinMaxRows]
-  int32_t pieces_pre[kMaxKeys + 1];  // prefix of each key's window in 16-byte pieces (LDS layout)
-};
-
-// One window's loads in registers: payload pieces p = tid + 256 j, offsets pieces tid and tid + 256.
-template <int NK>
-struct StPrefetch {
-  ulonglong2 pay[kStPiecesPerThread];
-  int4 off[NK][2];
-};
-
-// Issues the loads of window [w0, w1) (chunk-local rows) whose payload starts at byte pst[k].
-template <int NK>
-__device__ __forceinline__ void StIssue(const AggPlanDev* __restrict__ plan, const DevChunk& ch, const TileRange& rg,
-                                        const StreamCfg& cfg, int64_t w0, int64_t w1, const int32_t* pst, StPrefetch<NK>& pf) {
-  const int tid = threadIdx.x;
-  const int64_t oa = w0 & ~int64_t(3);
-  const int noff = static_cast<int>((w1 + 1 - oa + 3) >> 2);
-#pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int4* src = reinterpret_cast<const int4*>(ch.cols[plan->keys[k].col].offsets + oa);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int p = tid + j * kConsumeBlock;
-      pf.off[k][j] = p < noff ? src[p] : make_int4(0, 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < kStPiecesPerThread; ++j) {
-    const int p = tid + j * kConsumeBlock;
-    ulonglong2 v = make_ulonglong2(0, 0);
-    if (p < cfg.pieces_pre[NK]) {
-      int k = 0;
-#pragma unroll
-      for (int i = 1; i < NK; ++i) k += p >= cfg.pieces_pre[i] ? 1 : 0;
-      const int64_t a = static_cast<int64_t>(pst[k] & ~15) + 16 * static_cast<int64_t>(p - cfg.pieces_pre[k]);
-      if (a < rg.pay_end[k]) v = *reinterpret_cast<const ulonglong2*>(ch.cols[plan->keys[k].col].data + a);
-    }
-    pf.pay[j] = v;
-  }
-}
-
-template <int NK>
-__device__ __forceinline__ void StStore(const StPrefetch<NK>& pf, ulonglong2* s_pay, int4 (*s_off)[kStOffPieces]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    s_off[k][tid] = pf.off[k][0];
-    if (tid + kConsumeBlock < kStOffPieces) s_off[k][tid + kConsumeBlock] = pf.off[k][1];
-  }
-#pragma unroll
-  for (int j = 0; j < kStPiecesPerThread; ++j) s_pay[tid + j * kConsumeBlock] = pf.pay[j];
-}
-
-// Payload words of a string at byte b of the LDS window (8-byte aligned reads, funnel shifts),
-// tail-masked like LoadStrWords.
-__device__ __forceinline__ void LdsStrWords(const uint64_t* s, uint32_t b, uint32_t len, uint64_t* w) {
-  const uint32_t wi = b >> 3, sh = (b & 7u) * 8u;
-  const uint32_t nw = (len + 7u) >> 3;
-  uint64_t prev = s[wi];
-#pragma unroll
-  for (int j = 0; j < kFastStrWords; ++j) {
-    uint64_t x = 0;
-    if (static_cast<uint32_t>(j) < nw) {
-      const uint64_t nx = s[wi + j + 1];
-      x = sh ? (prev >> sh) | (nx << (64u - sh)) : prev;
-      prev = nx;
-    }
-    const int rem = static_cast<int>(len) - 8 * j;
-    w[j] = rem >= 8 ? x : (rem > 0 ? (x & ((1ULL << (rem * 8)) - 1)) : 0);
-  }
-}
-
-template <int NK, bool HOT>
-__global__ void __launch_bounds__(kConsumeBlock, 2) AggConsumeStreamKernel(const AggPlanDev* __restrict__ plan,
-                                                                        const DevChunk* __restrict__ chunks,
-                                                                        const TileRange* __restrict__ ranges, int nranges,
-                                                                        int64_t ntiles, AggTableDev tab, StageDev stg,
-                                                                        uint32_t nchunks, const HotImage* __restrict__ hot,
-                                                                        StreamCfg cfg) {
-  constexpr bool S = true;  // all keys STRING
-  constexpr int kPer = kStSubRows / kConsumeBlock;
-  constexpr int kPairs = kPer / 2;
-  constexpr int kWaves = kConsumeBlock / 64;
-  __shared__ uint16_t s_sel[kStSelCap];
-  __shared__ ulonglong2 s_pay[kStPayPieces + 1];
-  __shared__ int4 s_off[NK][kStOffPieces];
-  __shared__ uint16_t s_ws[kStMaxWins + 1];
-  __shared__ int32_t s_pst[NK];
-  __shared__ uint32_t s_htag[HOT ? kHotTags : 1];
-  __shared__ uint64_t s_hrec[HOT ? kHot : 1][kHotRecWords];
-  __shared__ uint32_t s_wcnt[2][kWaves];
-  __shared__ unsigned int s_ins;
-  __shared__ unsigned long long s_base;
-  __shared__ KeyCols<NK> s_kc[kLdsChunks];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
-  const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
-  const int nv = plan->n_vals;
-  const int WR = cfg.win_rows;
-  const uint64_t* s_pay64 = reinterpret_cast<const uint64_t*>(s_pay);
-  const int32_t* s_off32[NK];
-#pragma unroll
-  for (int k = 0; k < NK; ++k) s_off32[k] = reinterpret_cast<const int32_t*>(s_off[k]);
-  if (threadIdx.x == 0) s_ins = 0;
-  const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
-  for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
-  if constexpr (HOT) {
-    for (int i = threadIdx.x; i < kHotTags; i += kConsumeBlock) s_htag[i] = hot->tags[i];
-    for (int i = threadIdx.x; i < kHot * kHotRecWords; i += kConsumeBlock) s_hrec[i / kHotRecWords][i % kHotRecWords] = hot->recs[i / kHotRecWords][i % kHotRecWords];
-  }
-  __syncthreads();
-  for (int64_t t = bid; t < ntiles; t += gridDim.x) {
-    int ri = 0;
-    while (ri + 1 < nranges && ranges[ri + 1].tile0 <= t) ++ri;
-    const TileRange rg = ranges[ri];
-    const DevChunk& ch = chunks[rg.chunk];
-    const int64_t row0 = rg.lo + (t - rg.tile0) * rg.tile_rows;
-    const int64_t row1 = min(row0 + rg.tile_rows, rg.hi);
-    const int tn = static_cast<int>(row1 - row0);
-    const int nsub = (tn + kStSubRows - 1) / kStSubRows;
-    const uint64_t* fv = reinterpret_cast<const uint64_t*>(ch.cols[plan->filter.col].values);
-    const ulonglong2* fv2 = reinterpret_cast<const ulonglong2*>(fv);
-    const DevProgram* fp = &plan->filter;
-    uint32_t total = 0;
-    int sp0 = 0;  // first tile-relative row of the rows collected since the last flush
-#pragma unroll 1
-    for (int sb = 0; sb < nsub; ++sb) {
-      // Phase 1: the filter column two rows per lane with 16-byte loads, compacted into s_sel in
-      // ascending row order (the windows below rely on it): wave w owns the contiguous quarter
-      // [w * 512, (w + 1) * 512) of the sub-batch, pair load k of lane l rows k * 128 + 2 l (+1).
-      constexpr int kWaveRows = kStSubRows / kWaves;
-      const int64_t sb0 = row0 + static_cast<int64_t>(sb) * kStSubRows;
-      uint32_t be = 0, bo = 0;
-      const int64_t r0 = sb0 + wid * kWaveRows + 2 * lane;
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k) {
-        const int64_t r = r0 + k * 128;
-        ulonglong2 v = make_ulonglong2(0, 0);
-        if (r + 1 < row1) v = fv2[r >> 1];
-        else if (r < row1) v.x = fv[r];
-        be |= static_cast<uint32_t>(r < row1 && ApplyShape(fp, v.x) != 0) << k;
-        bo |= static_cast<uint32_t>(r + 1 < row1 && ApplyShape(fp, v.y) != 0) << k;
-      }
-      uint32_t c = static_cast<uint32_t>(__popc(be) + __popc(bo));
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-      if (lane == 0) s_wcnt[sb & 1][wid] = c;
-      __syncthreads();
-      uint32_t wbase = total, sbtot = 0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
-        const uint32_t cw = s_wcnt[sb & 1][w];
-        wbase += w < wid ? cw : 0;
-        sbtot += cw;
-      }
-#pragma unroll
-      for (int k = 0; k < kPairs; ++k) {
-        const bool pe = (be >> k) & 1u, po = (bo >> k) & 1u;
-        const unsigned long long me = __ballot(pe), mo = __ballot(po);
-        const uint32_t at = wbase + static_cast<uint32_t>(__popcll(me & lanemask_lt) + __popcll(mo & lanemask_lt));
-        const uint16_t off = static_cast<uint16_t>(sb * kStSubRows + wid * kWaveRows + k * 128 + 2 * lane);
-        if (pe) s_sel[at] = off;
-        if (po) s_sel[at + (pe ? 1 : 0)] = static_cast<uint16_t>(off + 1);
-        wbase += static_cast<uint32_t>(__popcll(me) + __popcll(mo));
-      }
-      static_assert(kPairs * 128 == kWaveRows, "phase-1 rows per wave");
-      total += sbtot;
-      if (sb + 1 < nsub && total + kStSubRows <= kStSelCap) continue;
-      const int sp1 = min(tn, (sb + 1) * kStSubRows);
-      // Phase 2 over the rows of [sp0, sp1), window by window.
-      const int nwin = (sp1 - sp0 + WR - 1) / WR;
-      if (threadIdx.x == 0) {
-        if (s_ins) {
-          atomicAdd(&tab.counters[0], s_ins);
-          s_ins = 0;
-        }
-        s_base = total ? atomicAdd(stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
-      }
-      if (threadIdx.x < NK) s_pst[threadIdx.x] = ch.cols[plan->keys[threadIdx.x].col].offsets[row0 + sp0];
-      __syncthreads();  // s_sel, s_base, s_pst complete
-      if (total > 0) {  // uniform
-      // Window starts in s_sel (rows are in ascending order).
-      for (uint32_t i = threadIdx.x; i < total; i += kConsumeBlock) {
-        const int wi = (static_cast<int>(s_sel[i]) - sp0) / WR;
-        const int wp = i == 0 ? -1 : (static_cast<int>(s_sel[i - 1]) - sp0) / WR;
-        for (int w = wp + 1; w <= wi; ++w) s_ws[w] = static_cast<uint16_t>(i);
-        if (i + 1 == total)
-          for (int w = wi + 1; w <= nwin; ++w) s_ws[w] = static_cast<uint16_t>(total);
-      }
-      int32_t pst[NK];
-#pragma unroll
-      for (int k = 0; k < NK; ++k) pst[k] = s_pst[k];
-      const uint64_t base = s_base;
-      StPrefetch<NK> pf;
-      int64_t w0 = row0 + sp0;
-      int64_t w1 = min(w0 + WR, row0 + sp1);
-      StIssue<NK>(plan, ch, rg, cfg, w0, w1, pst, pf);
-      StStore<NK>(pf, s_pay, s_off);
-      __syncthreads();
-#pragma unroll 1
-      for (int w = 0; w < nwin; ++w) {
-        // This window's layout: payload of key k starts at byte a0[k] of the chunk's payload.
-        int32_t a0[NK], avail[NK];
-#pragma unroll
-        for (int k = 0; k < NK; ++k) {
-          a0[k] = pst[k] & ~15;
-          avail[k] = min(16 * (cfg.pieces_pre[k + 1] - cfg.pieces_pre[k]), rg.pay_end[k] - a0[k]);
-        }
-        const int64_t oa = w0 & ~int64_t(3);
-        const int64_t nw0 = w1;
-        const int64_t nw1 = min(nw0 + WR, row0 + sp1);
-        if (w + 1 < nwin) {
-#pragma unroll
-          for (int k = 0; k < NK; ++k) pst[k] = s_off32[k][w1 - oa];
-          StIssue<NK>(plan, ch, rg, cfg, nw0, nw1, pst, pf);
-        }
-        const uint32_t i1 = min(static_cast<uint32_t>(s_ws[w + 1]), total), i0 = min(static_cast<uint32_t>(s_ws[w]), i1);
-        for (uint32_t i = i0 + threadIdx.x; i < i1; i += kConsumeBlock) {
-          const int64_t local = row0 + s_sel[i];
-          const uint64_t pos = base + i;
-          const bool in_win = local >= w0 && local < w1;  // always (rows ascend); else the list kernel redoes the row
-          for (int v = 0; v < nv; ++v) stg.vals[v][pos] = EvalShape(&plan->vals[v], ch, local, plan->col_types);
-          FastKeys<NK> k;
-          bool have_keys = in_win;
-#pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-            const int64_t li = in_win ? local - oa : 0;
-            const int32_t o0 = s_off32[kk][li], o1 = s_off32[kk][li + 1];
-            const uint32_t len = static_cast<uint32_t>(o1 - o0);
-            k.len[kk] = len;
-            have_keys = have_keys && len <= 8u * kFastStrWords;
-            if (have_keys) {
-              if (o1 - a0[kk] <= avail[kk]) {
-                LdsStrWords(s_pay64 + 2 * cfg.pieces_pre[kk], static_cast<uint32_t>(o0 - a0[kk]), len, k.w[kk]);
-              } else {
-                LoadStrWords(ch.cols[plan->keys[kk].col].data + o0, len, k.w[kk]);
-              }
-            }
-          }
-          uint32_t slot = kDeferredSlot;
-          const uint32_t rowref = (static_cast<uint32_t>(rg.chunk) << kChunkShift) | static_cast<uint32_t>(local);
-          if (have_keys) {
-            const uint64_t h = HashFastKeys<NK, S>(plan, k);
-            bool hit = false;
-            if constexpr (HOT) {
-              uint32_t idx = HotIdx(h);
-              const uint32_t tg = HotTag(h);
-#pragma unroll
-              for (int p = 0; p < kHotProbe; ++p) {
-                const uint32_t e = s_htag[idx];
-                if (e == 0) break;
-                if ((e >> 10) == tg) {
-                  const uint64_t* rec = s_hrec[(e & 1023u) - 1];
-                  if (HotEqual<NK>(rec, k)) {
-                    slot = static_cast<uint32_t>(rec[0]);
-                    hit = true;
-                    break;
-                  }
-                }
-                idx = (idx + 1) & (kHotTags - 1);
-              }
-            }
-            if (!hit) slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
-          }
-          const unsigned long long dm = __ballot(slot == kDeferredSlot);
-          if (dm) {
-            const int leader = __ffsll(static_cast<long long>(dm)) - 1;
-            unsigned int dbase = 0;
-            if (lane == leader) dbase = atomicAdd(&tab.counters[2], static_cast<unsigned int>(__popcll(dm)));
-            dbase = __shfl(dbase, leader, 64);
-            if (slot == kDeferredSlot) {
-              const unsigned int at = dbase + __popcll(dm & lanemask_lt);
-              tab.deferred[at] = rowref;
-              tab.deferred_pos[at] = static_cast<uint32_t>(pos);
-            }
-          }
-          stg.slot[pos] = slot;
-        }
-        __syncthreads();  // every row of window w read its keys
-        if (w + 1 < nwin) {
-          StStore<NK>(pf, s_pay, s_off);
-          w0 = nw0;
-          w1 = nw1;
-        }
-        __syncthreads();
-      }
-      } else {
-        __syncthreads();  // s_pst / s_base are rewritten by the next flush
-      }
-      total = 0;
-      sp0 = sp1;
-    }
-  }
-  if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
-}
-
 // Publication: every slot still holding a row reference (kind 0) gets its key copied into the
 // arena.  sizes[i] = (1 << 40) | words, so one exclusive scan yields both the record offsets
 // and (total >> 40) the number of published groups.
@@ -1349,12 +837,12 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, cap, total, sc));
   uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
   PXG_HIP(hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 48, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  uint8_t c[32];
+  uint8_t c[48];
   uint64_t tot = 0;
   std::memcpy(&tot, pin, 8);
-  std::memcpy(c, pin + 8, 32);
+  std::memcpy(c, pin + 8, 48);
   std::memcpy(n_deferred, c + 8, 4);
   std::memcpy(&st_n, c + 16, 8);
 
@@ -1408,19 +896,23 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     const char* e = std::getenv("PXG_DIAG_CONSUME");
     return e ? std::atoi(e) : 0;
   }();
-  // The hot-group cache and the 16-byte filter pair loads of the fast kernel both measured slower
-  // (tools/ab_run.sh, r03: C2 1.44 ms base vs 1.52 pairs / 1.69 hot / 1.54 both; 1B rows 12.7 vs
-  // 13.9 / 14.7 / 13.2): opt-in only (PXG_HOT=1, PXG_PAIRS=1).
-  const bool hot_ok = fast_nk > 0 && (diag & 3) == 0 && EnvFlag("PXG_HOT");
+  // 16-byte filter pair loads measured slower in this kernel (tools/ab_run.sh, r03: C2 1.44 vs
+  // 1.52 ms, 1B rows 12.7 vs 13.9 ms): opt-in only (PXG_PAIRS=1).
   bool all_str = true;
   for (int i = 0; i < n_keys; ++i) all_str = all_str && key_types[i] == PXG_STRING;
-  // Two launches (hot-group cache, HotBuildKernel above) for large all-STRING-key consumes: a
-  // prefix of ~2 % of the rows (>= 2M), then the rest with the LDS cache of its top groups.
-  int64_t prefix = 0;
-  if (hot_ok && all_str && end - begin >= (int64_t(1) << 23)) {
-    prefix = std::max<int64_t>(int64_t(1) << 21, (end - begin) / 50);
-    prefix = (prefix + kConsumeTile - 1) / kConsumeTile * kConsumeTile;
+  // 16-byte pair loads of the filter column: an 8-byte column, every tile starting at an even
+  // row (device column buffers are allocated 256-byte aligned).
+  bool pairs_ok = hplan.has_filter;
+  if (pairs_ok) {
+    const int ft = hplan.col_types[hplan.filter.col];
+    pairs_ok = ft == PXG_INT64 || ft == PXG_FLOAT64 || ft == PXG_TIME64NS;
+    for (const auto& c : t->chunks) {  // every range's first row (tiles start there)
+      const int64_t lo = std::max(begin, c->row_base) - c->row_base;
+      if (lo < c->nrows && c->row_base < end) pairs_ok = pairs_ok && (lo & 1) == 0;
+    }
+    for (const auto& c : t->chunks) pairs_ok = pairs_ok && (reinterpret_cast<uintptr_t>(c->cols[hplan.filter.col].values.p) & 15) == 0;
   }
+  const bool pairs = pairs_ok && EnvFlag("PXG_PAIRS");
   // Tile ranges of [b, e) in `rs` (tiles of `tr` rows, appended; tile0 counted from t0).
   auto make_ranges = [&](int64_t b, int64_t e, int64_t tr, std::vector<TileRange>* rs) {
     int64_t nt = 0;
@@ -1435,18 +927,13 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
       r.hi = hi;
       r.chunk = static_cast<int32_t>(c);
       r.tile_rows = static_cast<int32_t>(tr);
-      for (int k = 0; k < kMaxKeys; ++k)
-        r.pay_end[k] = k < n_keys && key_types[k] == PXG_STRING ? static_cast<int32_t>(ch.cols[hplan.keys[k].col].data_len) : 0;
       rs->push_back(r);
       nt += (hi - lo + tr - 1) / tr;
     }
     return nt;
   };
   std::vector<TileRange> ranges;
-  const int64_t ntiles_a = prefix > 0 ? make_ranges(begin, begin + prefix, kConsumeTile, &ranges) : 0;
-  const size_t nranges_a = ranges.size();
-  const int64_t ntiles = make_ranges(begin + prefix, end, tile_rows, &ranges);
-  const size_t nranges_b = ranges.size() - nranges_a;
+  const int64_t ntiles = make_ranges(begin, end, tile_rows, &ranges);
   if (ranges.empty()) return PXG_OK;
   const int64_t rows = end - begin;
   if (st_n + static_cast<uint64_t>(rows) >= (uint64_t(1) << 32))
@@ -1469,42 +956,8 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     const int64_t v = e ? std::atoll(e) : 0;
     return v > 0 ? v : 8;
   }();
-  using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t,
-                          const HotImage*);
-  // 16-byte pair loads of the filter column: an 8-byte column, every tile starting at an even
-  // row (device column buffers are allocated 256-byte aligned).
-  bool pairs_ok = hplan.has_filter;
-  if (pairs_ok) {
-    const int ft = hplan.col_types[hplan.filter.col];
-    pairs_ok = ft == PXG_INT64 || ft == PXG_FLOAT64 || ft == PXG_TIME64NS;
-    for (const TileRange& r : ranges) pairs_ok = pairs_ok && (r.lo & 1) == 0;
-    for (const auto& c : t->chunks) pairs_ok = pairs_ok && (reinterpret_cast<uintptr_t>(c->cols[hplan.filter.col].values.p) & 15) == 0;
-  }
-  const bool pairs = pairs_ok && EnvFlag("PXG_PAIRS");
-  // Streamed keys (AggConsumeStreamKernel): all-STRING keys, an 8-byte filter column, and key
-  // windows of >= 256 rows that fit the LDS payload window with ~12 % headroom over the table's
-  // average bytes per row (longer strings keep the gather kernel).
-  StreamCfg scfg{};
-  bool stream = all_str && pairs_ok && fast_nk > 0 && (diag & 3) == 0 && tile_rows <= kConsumeTileMax && EnvFlag("PXG_STREAM");
-  if (stream) {
-    double rows_sum = 0, bytes[kMaxKeys] = {0, 0, 0, 0}, all = 0;
-    for (const auto& c : t->chunks) {
-      rows_sum += static_cast<double>(c->nrows);
-      for (int k = 0; k < fast_nk; ++k) bytes[k] += static_cast<double>(c->cols[hplan.keys[k].col].data_len);
-    }
-    for (int k = 0; k < fast_nk; ++k) all += bytes[k] / std::max(rows_sum, 1.0);
-    int wr = static_cast<int>((kStPayBytes - 48.0 * fast_nk) / (std::max(all, 1.0) * 1.12));
-    wr = std::min(kStWinMaxRows, wr & ~63);
-    stream = wr >= 256;
-    scfg.win_rows = wr;
-    scfg.pieces_pre[0] = 0;
-    for (int k = 0; k < kMaxKeys; ++k) {
-      const int pk = k < fast_nk ? static_cast<int>((bytes[k] / std::max(rows_sum, 1.0) * wr * 1.12 + 47.0) / 16.0) : 0;
-      scfg.pieces_pre[k + 1] = scfg.pieces_pre[k] + pk;
-    }
-    stream = stream && scfg.pieces_pre[kMaxKeys] <= kStPayPieces;
-  }
-  auto pick = [&](bool hot) -> KernFn {
+  using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t);
+  auto pick = [&]() -> KernFn {
     KernFn kern = AggConsumeKernel;
     switch (fast_nk * 4 + (diag & 3)) {
 #define PXG_FAST_CASE(nk)                                           \
@@ -1532,43 +985,11 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     return kern;
   };
   const TileRange* d_rg = d_ranges.as<const TileRange>();
-  const HotImage* d_hot = nullptr;
-  if (prefix > 0) {
-    // Launch A: the prefix, no cache.  Then the per-slot counts of its staged rows and the image.
-    const int grid_a = static_cast<int>(std::min<int64_t>(ntiles_a, static_cast<int64_t>(ctx->num_cus) * bpc));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(false), dim3(grid_a), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
-                               t->d_chunks.as<const DevChunk>(), d_rg, static_cast<int>(nranges_a), ntiles_a, TableDev(this, 0),
-                               StageDevOf(this), static_cast<uint32_t>(t->chunks.size()), d_hot));
-    PXG_RETURN_IF_ERROR(hot_cnt.Ensure(static_cast<size_t>(cap) * 4));
-    PXG_RETURN_IF_ERROR(hot_img.Ensure(sizeof(HotImage)));
-    PXG_HIP(hipMemsetAsync(hot_cnt.p, 0, static_cast<size_t>(cap) * 4, ctx->stream));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_hot_count", HotCountKernel, dim3(ctx->num_cus), dim3(256), 0, st_slot.as<const uint32_t>(),
-                               reinterpret_cast<const unsigned long long*>(counters.as<uint8_t>() + 16), cap, hot_cnt.as<uint32_t>()));
-    void (*build)(const AggPlanDev*, const DevChunk*, const unsigned long long*, uint32_t, const uint64_t*, const uint32_t*, HotImage*) =
-        fast_nk == 1 ? HotBuildKernel<1> : fast_nk == 2 ? HotBuildKernel<2> : fast_nk == 3 ? HotBuildKernel<3> : HotBuildKernel<4>;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_hot_build", build, dim3(1), dim3(1024), 0, d_plan.as<const AggPlanDev>(),
-                               t->d_chunks.as<const DevChunk>(), slots.as<const unsigned long long>(), cap, arena.as<const uint64_t>(),
-                               hot_cnt.as<const uint32_t>(), hot_img.as<HotImage>()));
-    d_hot = hot_img.as<const HotImage>();
-  }
-  if (nranges_b > 0 && stream) {
-    using StreamFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t,
-                              const HotImage*, StreamCfg);
-    const bool h = d_hot != nullptr;
-    StreamFn sk = fast_nk == 1 ? (h ? AggConsumeStreamKernel<1, true> : AggConsumeStreamKernel<1, false>)
-                : fast_nk == 2 ? (h ? AggConsumeStreamKernel<2, true> : AggConsumeStreamKernel<2, false>)
-                : fast_nk == 3 ? (h ? AggConsumeStreamKernel<3, true> : AggConsumeStreamKernel<3, false>)
-                               : (h ? AggConsumeStreamKernel<4, true> : AggConsumeStreamKernel<4, false>);
-    const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * 2));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", sk, dim3(grid), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
-                               t->d_chunks.as<const DevChunk>(), d_rg + nranges_a, static_cast<int>(nranges_b), ntiles,
-                               TableDev(this, 0), StageDevOf(this), static_cast<uint32_t>(t->chunks.size()), d_hot, scfg));
-  } else if (nranges_b > 0) {
+  {
     const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * bpc));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(d_hot != nullptr), dim3(grid), dim3(kConsumeBlock), 0,
-                               d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(), d_rg + nranges_a,
-                               static_cast<int>(nranges_b), ntiles, TableDev(this, 0), StageDevOf(this),
-                               static_cast<uint32_t>(t->chunks.size()), d_hot));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(), dim3(grid), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
+                               t->d_chunks.as<const DevChunk>(), d_rg, static_cast<int>(ranges.size()), ntiles, TableDev(this, 0),
+                               StageDevOf(this), static_cast<uint32_t>(t->chunks.size())));
   }
   clk.Mark("consume: launch");
   uint32_t n_def = 0;

@@ -56,9 +56,6 @@ struct Agg {
   DevBuf deferred[2], deferred_pos[2];
   DevBuf d_ranges;
   std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
-  // Hot-group image of the two-launch consume (pxg_agg.hip, HotBuildKernel): per-slot row
-  // counts of the prefix launch, and the LDS table image the main launch loads per workgroup.
-  DevBuf hot_cnt, hot_img;
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint32_t last_big_sort_groups = 0;  // pxg_agg_stats.big_sort_groups

@@ -370,6 +370,13 @@ __device__ __forceinline__ void CopyBytesOverlap(uint8_t* __restrict__ dst, cons
   }
 }
 
+// Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // XCD-aware remap of a linear block id (bijective for any grid size): blocks that the
 // dispatcher places on one XCD (b % 8 equal) get consecutive logical ids so neighbouring
 // tiles share an L2 (cdna_hip_programming.md §5.5 T1).

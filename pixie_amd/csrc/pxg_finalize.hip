@@ -32,12 +32,6 @@ __device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restr
   return k < cap ? rank[k] : G;
 }
 
-// Wave-local LDS ordering for lanes of one wave exchanging data through LDS.
-__device__ __forceinline__ void WaveSync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // ---------------------------------------------------------------------------------------
 // Stable LSD radix sort, 8-bit digits, four kernels per pass: tile digit counts (RsHist),
@@ -519,13 +513,19 @@ __global__ void __launch_bounds__(256) ChunkReduceThreadKernel(const AggPlanDev*
 
 // UDA Finalize per group (math_ops.h: CountUDA/SumUDA/MeanUDA/MinUDA/MaxUDA).  With
 // plan->emit_states every group's states are also written in Serialize() layout (partial agg).
-__global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
-                                   const uint32_t* __restrict__ cbase, uint32_t ngroups, const uint64_t* __restrict__ partial,
-                                   uint64_t pstride, UdaOut out, uint8_t* __restrict__ states) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngroups) return;
-  const uint64_t cnt = gstart[g + 1] - gstart[g];
-  const uint32_t c0 = cbase[g], c1 = cbase[g + 1];
+// One thread per group combines its chunk partials in order; a group of more than
+// kCombineWaveChunks chunks is combined by its whole wave instead (lane i takes chunks i, i + 64,
+// ..., then a fixed shuffle tree), so the largest groups (3400 chunks at 1B rows) are not one
+// thread's chain of dependent loads (0.41 ms at 1B rows).
+constexpr uint32_t kCombineWaveChunks = 32;
+
+template <bool WAVE>
+__device__ __forceinline__ void CombineGroup(const AggPlanDev* __restrict__ plan, uint32_t g, uint64_t cnt, uint32_t c0, uint32_t c1,
+                                             const uint64_t* __restrict__ partial, uint64_t pstride, UdaOut out,
+                                             uint8_t* __restrict__ states) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t cs = WAVE ? c0 + lane : c0, step = WAVE ? 64 : 1;
+  const bool writer = !WAVE || lane == 0;
   for (int u = 0; u < plan->n_udas; ++u) {
     const int kind = plan->uda_kind[u];
     const int at = plan->uda_arg_type[u];
@@ -537,19 +537,22 @@ __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const ui
       case PXG_UDA_MINSUM:
         if (at == PXG_FLOAT64) {
           double acc = 0;
-          for (uint32_t c = c0; c < c1; ++c) acc += AsF(p[c]);
+          for (uint32_t c = cs; c < c1; c += step) acc += AsF(p[c]);
+          if (WAVE) acc = WaveSumF64(acc);
           r = FBits(acc);
         } else {
           uint64_t acc = 0;
-          for (uint32_t c = c0; c < c1; ++c) acc += p[c];
+          for (uint32_t c = cs; c < c1; c += step) acc += p[c];
+          if (WAVE) acc = WaveSumU64(acc);
           r = acc + static_cast<uint64_t>(plan->uda_init[u]);
         }
         break;
       case PXG_UDA_MEAN: {
         double acc = 0;
-        for (uint32_t c = c0; c < c1; ++c) acc += AsF(p[c]);
+        for (uint32_t c = cs; c < c1; c += step) acc += AsF(p[c]);
+        if (WAVE) acc = WaveSumF64(acc);
         r = FBits(acc / static_cast<double>(cnt));
-        if (states) {  // MeanInfo {uint64 size; double count} (math_ops.h:621-624)
+        if (states && writer) {  // MeanInfo {uint64 size; double count} (math_ops.h:621-624)
           uint64_t* st = reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]);
           st[0] = cnt;
           st[1] = FBits(acc);
@@ -560,31 +563,57 @@ __global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const ui
         const uint64_t* pn = partial + static_cast<uint64_t>(plan->n_udas + u) * pstride;
         double acc = 0;
         uint64_t n = 0;
-        for (uint32_t c = c0; c < c1; ++c) {
+        for (uint32_t c = cs; c < c1; c += step) {
           acc += AsF(p[c]);
           n += pn[c];
+        }
+        if (WAVE) {
+          acc = WaveSumF64(acc);
+          n = WaveSumU64(n);
         }
         r = FBits(acc / static_cast<double>(n));
         break;
       }
       case PXG_UDA_MAX: {
         int64_t m = at == PXG_FLOAT64 ? OrderedFromDouble(FBits(kDblMin)) : INT64_MIN;  // MaxUDA init numeric_limits<T>::min()
-        for (uint32_t c = c0; c < c1; ++c) { const int64_t x = static_cast<int64_t>(p[c]); m = x > m ? x : m; }
+        for (uint32_t c = cs; c < c1; c += step) { const int64_t x = static_cast<int64_t>(p[c]); m = x > m ? x : m; }
+        if (WAVE) m = WaveMaxI64(m);
         r = at == PXG_FLOAT64 ? DoubleFromOrdered(m) : static_cast<uint64_t>(m);
         break;
       }
       case PXG_UDA_MIN: {
         int64_t m = at == PXG_FLOAT64 ? OrderedFromDouble(FBits(kDblMax)) : INT64_MAX;
-        for (uint32_t c = c0; c < c1; ++c) { const int64_t x = static_cast<int64_t>(p[c]); m = x < m ? x : m; }
+        for (uint32_t c = cs; c < c1; c += step) { const int64_t x = static_cast<int64_t>(p[c]); m = x < m ? x : m; }
+        if (WAVE) m = WaveMinI64(m);
         r = at == PXG_FLOAT64 ? DoubleFromOrdered(m) : static_cast<uint64_t>(m);
         break;
       }
       default: continue;  // QUANTILES: digest kernels
     }
-    out.p[u][g] = r;
-    // count, sum, min, max: the state is the finalized 8-byte value (math_ops.h:602-757).
-    if (states && kind != PXG_UDA_MEAN)
-      *reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]) = r;
+    if (writer) {
+      out.p[u][g] = r;
+      // count, sum, min, max: the state is the finalized 8-byte value (math_ops.h:602-757).
+      if (states && kind != PXG_UDA_MEAN)
+        *reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]) = r;
+    }
+  }
+}
+
+__global__ void GroupCombineKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
+                                   const uint32_t* __restrict__ cbase, uint32_t ngroups, const uint64_t* __restrict__ partial,
+                                   uint64_t pstride, UdaOut out, uint8_t* __restrict__ states) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = g < ngroups;
+  const uint32_t c0 = valid ? cbase[g] : 0, c1 = valid ? cbase[g + 1] : 0;
+  const uint64_t cnt = valid ? gstart[g + 1] - gstart[g] : 0;
+  const bool wide = valid && c1 - c0 > kCombineWaveChunks;
+  if (valid && !wide) CombineGroup<false>(plan, g, cnt, c0, c1, partial, pstride, out, states);
+  unsigned long long wm = __ballot(wide);
+  while (wm) {  // wave-uniform loop over the wave's wide groups
+    const int src = __ffsll(static_cast<long long>(wm)) - 1;
+    wm &= wm - 1;
+    CombineGroup<true>(plan, __shfl(g, src, 64), __shfl(cnt, src, 64), __shfl(c0, src, 64), __shfl(c1, src, 64), partial, pstride, out,
+                       states);
   }
 }
 
@@ -1039,6 +1068,7 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
                                                               const uint32_t* __restrict__ gstart, BigGroup* __restrict__ groups,
                                                               BigChunk* __restrict__ chunks, uint32_t* __restrict__ meta_out) {
   __shared__ uint32_t scan[kSetupBlock];
+  __shared__ uint32_t s_off[kSetupBlock], s_n[kSetupBlock], s_pass[kSetupBlock];
   __shared__ uint32_t s_max;
   const uint32_t nbig = *count;
   const int t = threadIdx.x;
@@ -1064,10 +1094,9 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
     }
     const uint32_t cbase = carry + scan[t] - nch;
     const uint32_t tot = scan[kSetupBlock - 1];
-    __syncthreads();
+    uint32_t passes = 0;
+    for (uint64_t r = kMidMax; r < n; r *= 2) ++passes;
     if (i < nbig) {
-      uint32_t passes = 0;
-      for (uint64_t r = kMidMax; r < n; r *= 2) ++passes;
       BigGroup B;
       B.off = off;
       B.n = n;
@@ -1076,17 +1105,33 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
       B.g = g;
       B.passes = passes;
       groups[i] = B;
-      for (uint32_t c = 0; c < nch; ++c) {
-        BigChunk C;
-        C.off = static_cast<uint64_t>(off) + static_cast<uint64_t>(c) * kMidMax;
-        C.g_off = off;
-        C.len = min(static_cast<uint32_t>(kMidMax), n - c * kMidMax);
-        C.g_n = n;
-        C.passes = passes;
-        C.bidx = i;
-        chunks[cbase + c] = C;
-      }
     }
+    s_off[t] = off;
+    s_n[t] = n;
+    s_pass[t] = passes;
+    __syncthreads();
+    // The round's chunks, all threads together (one thread per group wrote up to ~1700 chunks of
+    // the largest 1B-row group in a row): chunk c belongs to the group whose inclusive scan
+    // first exceeds c.
+    const uint32_t nvalid = min(static_cast<uint32_t>(kSetupBlock), nbig - b0);
+    for (uint32_t c = t; c < tot; c += kSetupBlock) {
+      uint32_t lo = 0, hi = nvalid - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (scan[mid] <= c) lo = mid + 1;
+        else hi = mid;
+      }
+      const uint32_t j = lo, k = c - (scan[j] - (s_n[j] + kMidMax - 1) / kMidMax);
+      BigChunk C;
+      C.off = static_cast<uint64_t>(s_off[j]) + static_cast<uint64_t>(k) * kMidMax;
+      C.g_off = s_off[j];
+      C.len = min(static_cast<uint32_t>(kMidMax), s_n[j] - k * kMidMax);
+      C.g_n = s_n[j];
+      C.passes = s_pass[j];
+      C.bidx = b0 + j;
+      chunks[carry + c] = C;
+    }
+    __syncthreads();  // scan / s_* are rewritten by the next round
     carry += tot;
   }
   __syncthreads();

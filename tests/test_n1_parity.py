@@ -31,7 +31,29 @@ def test_c2_at_1b_rows_matches_generator_truth(ctx, n):
         a.close()
         t.close()
     print(rep)
+    assert "groups_ref" in rep, rep
     assert g == rep["groups_ref"]
     assert rep["selected_rows_dev"] == rep["selected_rows_ref"]
     assert rep["ok"], rep
     assert rep["quantiles"]["largest_group"] > 5_000_000
+
+
+@pytest.mark.parametrize("n", [3 * (1 << 24) + 4100])
+def test_c2_across_full_chunks_matches_generator_truth(ctx, n):
+    """Three full 2^24-row chunks and a partial one: the streamed consume's windows cross chunk
+    boundaries inside a workgroup's run (its offsets run ahead of its payloads there)."""
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(SEED, 0, n, 10_000_000)
+    a = plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
+    try:
+        a.reset()
+        a.consume(t)
+        g = a.finalize()
+        rep = parity.check_c2_against_truth(a.result(), SEED, 0, n, threads=16)
+    finally:
+        a.close()
+        t.close()
+    assert "groups_ref" in rep, rep
+    assert g == rep["groups_ref"]
+    assert rep["selected_rows_dev"] == rep["selected_rows_ref"]
+    assert rep["ok"], rep

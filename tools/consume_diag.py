@@ -28,9 +28,8 @@ def child(rows, steps):
         agg.reset(); agg.consume(t)
     ctx.sync(); ctx.set_profiling(False)
     n, ms = ctx.kernel_stats("agg_consume")
-    hc = ctx.kernel_stats("agg_hot_count")[1] + ctx.kernel_stats("agg_hot_build")[1]
     print(json.dumps({"mode": os.environ.get("PXG_DIAG_CONSUME", "0"), "launches_per_step": n / steps,
-                      "consume_ms_per_step": ms / steps, "hot_build_ms_per_step": hc / steps,
+                      "consume_ms_per_step": ms / steps,
                       "ms_per_launch": ms / max(n, 1)}), flush=True)
 
 
