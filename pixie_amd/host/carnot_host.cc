@@ -158,6 +158,34 @@ static HostColumn StringColumn(const std::vector<std::string>& vals) {
   return hc;
 }
 
+// G empty strings (one zeroed offsets array, no per-row std::string).
+static HostColumn EmptyStringColumn(int64_t n) {
+  auto o = std::make_shared<OwnedColumn>();
+  o->offsets.assign(static_cast<size_t>(n) + 1, 0);
+  o->data.assign(16, 0);
+  HostColumn hc;
+  hc.type = PXG_STRING;
+  hc.length = n;
+  hc.offsets = o->offsets.data();
+  hc.data = o->data.data();
+  hc.owner = o;
+  return hc;
+}
+
+static HostColumn DoubleColumn(std::vector<double>&& vals) {
+  // Takes the vector's buffer (no copy); values stays 8 bytes past the end readable via the pad.
+  auto o = std::make_shared<OwnedColumn>();
+  const size_t n = vals.size();
+  o->values.resize(n * 8 + 8);
+  if (n) std::memcpy(o->values.data(), vals.data(), n * 8);
+  HostColumn hc;
+  hc.type = PXG_FLOAT64;
+  hc.length = static_cast<int64_t>(n);
+  hc.values = o->values.data();
+  hc.owner = o;
+  return hc;
+}
+
 static HostColumn DoubleColumn(const std::vector<double>& vals) {
   auto o = std::make_shared<OwnedColumn>();
   o->values.resize(vals.size() * 8 + 8);
@@ -1343,7 +1371,7 @@ class GpuAggNode : public ExecNode {
         // A column no consumer reads as a string (the pluck-only C2 shape) stays unrendered:
         // G empty strings keep the batch's relation.
         ob.cols.push_back(observed ? RenderQuantilesJson(static_cast<const double*>(hc.values), hc.length)
-                                   : StringColumn(std::vector<std::string>(static_cast<size_t>(hc.length))));
+                                   : EmptyStringColumn(hc.length));
       } else {
         ob.cols.push_back(hc);
       }
@@ -1624,6 +1652,7 @@ class PostAggMapNode : public ExecNode {
   Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t) override {
     const int64_t G = rb.num_rows;
     std::vector<HostColumn> env = rb.cols;
+    finite_.clear();
     for (auto& pk : plucks_) {
       std::vector<double> v(static_cast<size_t>(G));
       auto it = agg_ ? agg_->quantiles_raw_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantiles_raw_.end()){};
@@ -1632,20 +1661,27 @@ class PostAggMapNode : public ExecNode {
         if (pk.second == kQuantileKeys[k]) qk = k;
       if (agg_ && it != agg_->quantiles_raw_.end()) {
         // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
-        // fails to parse: pluck_float64 returns 0.0 for every key of that group.
+        // fails to parse: pluck_float64 returns 0.0 for every key of that group.  The per-group
+        // finiteness is computed once per raw column (C2 plucks two keys of one column).
         const double* d = static_cast<const double*>(it->second.values);
-        for (int64_t g = 0; g < G; ++g) {
-          bool finite = true;
-          for (int k = 0; k < 7; ++k) finite = finite && !pxjson::IsNanOrInf(d[g * 7 + k]);
-          v[static_cast<size_t>(g)] = finite && qk >= 0 ? d[g * 7 + qk] : 0.0;
+        std::vector<uint8_t>& fin = finite_[pk.first];
+        if (static_cast<int64_t>(fin.size()) != G) {
+          fin.resize(static_cast<size_t>(G));
+          for (int64_t g = 0; g < G; ++g) {
+            bool f = true;
+            for (int k = 0; k < 7; ++k) f = f && !pxjson::IsNanOrInf(d[g * 7 + k]);
+            fin[static_cast<size_t>(g)] = f ? 1 : 0;
+          }
         }
+        if (qk >= 0)
+          for (int64_t g = 0; g < G; ++g) v[static_cast<size_t>(g)] = fin[static_cast<size_t>(g)] ? d[g * 7 + qk] : 0.0;
       } else {
         const HostColumn& c = rb.cols[static_cast<size_t>(pk.first)];
         for (int64_t g = 0; g < G; ++g)
           v[static_cast<size_t>(g)] = PluckJson(reinterpret_cast<const char*>(c.data) + c.offsets[g],
                                                 static_cast<size_t>(c.offsets[g + 1] - c.offsets[g]), pk.second);
       }
-      env.push_back(DoubleColumn(v));
+      env.push_back(DoubleColumn(std::move(v)));
     }
     std::vector<HostColumn> dev_out;
     if (!device_.empty() && G > 0) {
@@ -1684,6 +1720,7 @@ class PostAggMapNode : public ExecNode {
 
  private:
   GpuAggNode* agg_;
+  std::map<int64_t, std::vector<uint8_t>> finite_;  // per plucked raw column: group's 7 quantiles all finite
   std::vector<std::pair<int64_t, std::string>> plucks_;  // (input column, key) -> extra column
   std::set<size_t> string_reads_;
   RowDescriptor env_types_;
