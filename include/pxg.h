@@ -305,6 +305,8 @@ typedef struct {
   int32_t fast_path_keys;   /* key count of the register-key consume kernel; 0 = generic kernel */
   int32_t big_sort_groups;  /* last finalize: big quantile groups the selection path handed to the
                                full sort path (NaN values, a gathered bin > 16384 values) */
+  int32_t hc_mode;          /* 1: this run stages partition records (high-cardinality mode) */
+  int32_t hc_partition_bits;/* last high-cardinality finalize: log2 of its partition count */
 } pxg_agg_stats;
 int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* stats);
 

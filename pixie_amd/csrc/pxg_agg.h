@@ -62,10 +62,29 @@ struct AggTableDev {
   const uint64_t* arena;
 };
 
+// High-cardinality (partitioned) staging, pxg_hc.hip: one fixed-stride record per selected row
+// whose keys fit (word 0: STRING key lengths, 16 bits per key; then every key's words, tail-masked;
+// then the value streams), the top half of its key hash (the partition bits) and the sort value
+// (low hash half << 32 | record index; ~0 = a hole left by a row that went to the table path).
+constexpr int kHcStrWords = 3;  // STRING keys of <= 24 bytes ride in the record
+constexpr int kHcMaxVals = 4;
+constexpr int kHcMaxStride = 1 + kMaxKeys * kHcStrWords + kHcMaxVals;
+constexpr uint64_t kHcHole = ~0ULL;
+
+struct HcStageDev {
+  uint64_t* rec;
+  uint32_t* key;
+  uint64_t* sv;
+  unsigned long long* cursor;
+  int32_t stride, kwords;
+  int32_t kw[kMaxKeys], koff[kMaxKeys];
+};
+
 struct StageDev {
   uint32_t* slot;
   uint64_t* vals[kMaxVals];
   unsigned long long* cursor;
+  HcStageDev hc;
 };
 
 }  // namespace pxg

@@ -518,7 +518,12 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
 // that ends phase 2 waits for the slowest probe chain of the block, and more rows per barrier
 // amortise that wait (4096 -> 8192 -> 16384 rows per tile: 1.80 -> 1.64 -> 1.38 ms at C2).
 // Phase 2 is flushed early when the selection buffer could overflow (selectivity > 1/2).
-template <int NK, int MODE, bool PAIRS = false>
+//
+// HC (high-cardinality mode, pxg_hc.hip): phase 2 writes one partition record per row instead
+// of probing the global table; a row with a STRING key longer than kHcStrWords words leaves a
+// hole there and takes the table path (a staging record whose slot the generic list kernel
+// fills in, like any deferred row), so the two paths hold disjoint key sets.
+template <int NK, int MODE, bool PAIRS = false, bool HC = false>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
@@ -638,7 +643,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
           atomicAdd(&tab.counters[0], s_ins);
           s_ins = 0;
         }
-        s_base = total ? atomicAdd(stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
+        s_base = total ? atomicAdd(HC ? stg.hc.cursor : stg.cursor, static_cast<unsigned long long>(total)) : 0ULL;
       }
       __syncthreads();
       const uint64_t base = s_base;
@@ -647,6 +652,64 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
       for (uint32_t i = threadIdx.x; i < total; i += kConsumeBlock) {
         const int64_t local = row0 + s_sel[i];
         const uint64_t pos = base + i;
+        if constexpr (HC) {
+          uint64_t x[kHcMaxVals];
+#pragma unroll
+          for (int v = 0; v < kHcMaxVals; ++v) x[v] = v < nv ? EvalShape(&plan->vals[v], ch, local, plan->col_types) : 0;
+          FastKeys<NK> k;
+          bool fit = LoadKeyBodies<NK, S>(plan, ch, heads, k);
+          if (i + kConsumeBlock < total) LoadKeyHeads<NK, S>(plan, ch, row0 + s_sel[i + kConsumeBlock], heads);
+#pragma unroll
+          for (int q = 0; q < NK; ++q) fit = fit && (KeyT<S>(plan, q) != PXG_STRING || k.len[q] <= 8u * kHcStrWords);
+          if (fit) {
+            const uint64_t h = HashFastKeys<NK, S>(plan, k);
+            uint64_t* r = stg.hc.rec + pos * static_cast<uint64_t>(stg.hc.stride);
+            uint64_t lens = 0;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) lens |= static_cast<uint64_t>(k.len[q]) << (16 * q);
+            r[0] = lens;
+#pragma unroll
+            for (int q = 0; q < NK; ++q) {
+#pragma unroll
+              for (int j = 0; j < kHcStrWords; ++j)
+                if (j < stg.hc.kw[q]) r[stg.hc.koff[q] + j] = k.w[q][j];
+            }
+#pragma unroll
+            for (int v = 0; v < kHcMaxVals; ++v)
+              if (v < nv) r[stg.hc.kwords + v] = x[v];
+            stg.hc.key[pos] = static_cast<uint32_t>(h >> 32);
+            stg.hc.sv[pos] = (h << 32) | pos;
+          } else {
+            stg.hc.key[pos] = 0xFFFFFFFFu;
+            stg.hc.sv[pos] = kHcHole;
+          }
+          // Rows with a long key: a staging record for the table path, deferred (one cursor and
+          // one list append per wave).
+          const unsigned long long lm = __ballot(!fit);
+          if (lm) {
+            const int leader = __ffsll(static_cast<long long>(lm)) - 1;
+            const unsigned int cnt = static_cast<unsigned int>(__popcll(lm));
+            unsigned long long sb = 0;
+            unsigned int db = 0;
+            if (lane == leader) {
+              sb = atomicAdd(stg.cursor, static_cast<unsigned long long>(cnt));
+              db = atomicAdd(&tab.counters[2], cnt);
+            }
+            sb = __shfl(sb, leader, 64);
+            db = __shfl(db, leader, 64);
+            if (!fit) {
+              const unsigned int rk = static_cast<unsigned int>(__popcll(lm & lanemask_lt));
+              const uint64_t sp = sb + rk;
+#pragma unroll
+              for (int v = 0; v < kHcMaxVals; ++v)
+                if (v < nv) stg.vals[v][sp] = x[v];
+              stg.slot[sp] = kDeferredSlot;
+              tab.deferred[db + rk] = (static_cast<uint32_t>(rg.chunk) << kChunkShift) | static_cast<uint32_t>(local);
+              tab.deferred_pos[db + rk] = static_cast<uint32_t>(sp);
+            }
+          }
+          continue;
+        }
         // Value streams first: independent of the key chain, their loads overlap it.
         for (int v = 0; v < nv; ++v) stg.vals[v][pos] = EvalShape(&plan->vals[v], ch, local, plan->col_types);
         FastKeys<NK> k;
@@ -779,6 +842,11 @@ static StageDev StageDevOf(Agg* a) {
   s.slot = a->st_slot.as<uint32_t>();
   for (int v = 0; v < kMaxVals; ++v) s.vals[v] = v < a->n_vals ? a->st_val[v].as<uint64_t>() : nullptr;
   s.cursor = reinterpret_cast<unsigned long long*>(a->counters.as<uint8_t>() + 16);
+  s.hc = a->hc_layout;
+  s.hc.rec = a->hc_rec.as<uint64_t>();
+  s.hc.key = a->hc_key.as<uint32_t>();
+  s.hc.sv = a->hc_sv.as<uint64_t>();
+  s.hc.cursor = reinterpret_cast<unsigned long long*>(a->counters.as<uint8_t>() + 48);
   return s;
 }
 
@@ -800,6 +868,27 @@ int32_t Agg::EnsureStage(uint64_t need) {
   for (int v = 0; v < n_vals; ++v) PXG_RETURN_IF_ERROR(st_val[v].Reserve(c * 8, st_n * 8, ctx->stream));
   st_cap = c;
   return PXG_OK;
+}
+
+int32_t Agg::EnsureHc(uint64_t need) {
+  if (need <= hc_cap) return PXG_OK;
+  const uint64_t c = std::max<uint64_t>(need, hc_cap * 2);
+  const uint64_t sw = static_cast<uint64_t>(hc_layout.stride) * 8;
+  PXG_RETURN_IF_ERROR(hc_rec.Reserve(c * sw + 64, hc_n * sw, ctx->stream));
+  PXG_RETURN_IF_ERROR(hc_key.Reserve(c * 4 + 16, hc_n * 4, ctx->stream));
+  PXG_RETURN_IF_ERROR(hc_sv.Reserve(c * 8 + 16, hc_n * 8, ctx->stream));
+  hc_cap = c;
+  return PXG_OK;
+}
+
+int64_t HcMinGroups() {
+  const char* e = std::getenv("PXG_HC_MIN_GROUPS");
+  return e ? std::atoll(e) : (int64_t(1) << 20);
+}
+
+bool Agg::HcNext() const {
+  const int64_t m = HcMinGroups();
+  return hc_ok && m > 0 && std::max<int64_t>(hint_groups, static_cast<int64_t>(last_groups)) >= m && !EnvFlag("PXG_NO_HC");
 }
 
 int32_t Agg::Grow(uint32_t new_cap) {
@@ -837,14 +926,15 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, sizes, sizes, cap, total, sc));
   uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
   PXG_HIP(hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 48, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 56, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  uint8_t c[48];
+  uint8_t c[56];
   uint64_t tot = 0;
   std::memcpy(&tot, pin, 8);
-  std::memcpy(c, pin + 8, 48);
+  std::memcpy(c, pin + 8, 56);
   std::memcpy(n_deferred, c + 8, 4);
   std::memcpy(&st_n, c + 16, 8);
+  std::memcpy(&hc_n, c + 48, 8);
 
   const uint64_t n_new = tot >> kPublishCountShift;
   const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
@@ -938,6 +1028,13 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   const int64_t rows = end - begin;
   if (st_n + static_cast<uint64_t>(rows) >= (uint64_t(1) << 32))
     return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
+  // High-cardinality mode is decided once per run, at its first consume.
+  if (st_n == 0 && hc_n == 0 && inserted == 0 && arena_words == 0) hc_active = HcNext();
+  if (hc_active) {
+    if (hc_n + static_cast<uint64_t>(rows) >= (uint64_t(1) << 32) - 1)
+      return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
+    PXG_RETURN_IF_ERROR(EnsureHc(hc_n + static_cast<uint64_t>(rows)));
+  }
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + static_cast<uint64_t>(rows)));
   PXG_RETURN_IF_ERROR(deferred[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
   PXG_RETURN_IF_ERROR(deferred_pos[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
@@ -971,6 +1068,19 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
       PXG_FAST_CASE(4)
 #undef PXG_FAST_CASE
       default: break;
+    }
+    if (hc_active) {  // partition records (fast_nk > 0 by eligibility)
+      switch (fast_nk * 2 + (all_str ? 1 : 0)) {
+#define PXG_HC_CASE(nk)                                                     \
+  case nk * 2 + 0: return AggConsumeFastKernel<nk, 0, false, true>;         \
+  case nk * 2 + 1: return AggConsumeFastKernel<nk, 4, false, true>;
+        PXG_HC_CASE(1)
+        PXG_HC_CASE(2)
+        PXG_HC_CASE(3)
+        PXG_HC_CASE(4)
+#undef PXG_HC_CASE
+        default: break;
+      }
     }
     if (fast_nk == 0 || (diag & 3) != 0) return kern;
     if (all_str) {  // all-STRING keys: the specialised production kernels (PXG_PAIRS=1: 16-byte filter loads)
@@ -1220,6 +1330,37 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   for (auto& pf : pool_fix) pf.first->pool = a.d_pool.as<uint8_t>() + pf.second;
   PXG_RETURN_IF_ERROR(a.d_plan.Alloc(sizeof(AggPlanDev)));
   a.fast_nk = FastPathKeys(a.hplan);
+  // High-cardinality mode: fast-path keys, integer SUM / MEAN / MINSUM and integer MIN / MAX (LDS
+  // integer atomics: order-independent, so the partition tables give deterministic results),
+  // at most kHcMaxVals value streams and 4 accumulated UDAs.
+  {
+    bool ok = a.fast_nk > 0 && !a.windowed && !a.emit_states && a.n_vals <= kHcMaxVals;
+    int acc = 0;
+    for (int u = 0; u < a.n_udas && ok; ++u) {
+      const int k = a.uda_kind[u], at = a.uda_arg_type[u];
+      const bool int_arg = at == PXG_INT64 || at == PXG_BOOLEAN;
+      switch (k) {
+        case PXG_UDA_COUNT: break;
+        case PXG_UDA_SUM:
+        case PXG_UDA_MEAN: ok = int_arg; ++acc; break;
+        case PXG_UDA_MINSUM: ++acc; break;
+        case PXG_UDA_MIN:
+        case PXG_UDA_MAX: ok = at == PXG_INT64 || at == PXG_TIME64NS; ++acc; break;
+        default: ok = false;
+      }
+    }
+    a.hc_ok = ok && acc <= 4;
+    int32_t w = 1;
+    for (int k = 0; k < a.n_keys; ++k) {
+      const int t = a.key_types[k];
+      a.hc_layout.koff[k] = w;
+      a.hc_layout.kw[k] = t == PXG_STRING ? kHcStrWords : (t == PXG_UINT128 ? 2 : 1);
+      w += a.hc_layout.kw[k];
+    }
+    a.hc_layout.kwords = w;
+    a.hc_layout.stride = w + a.n_vals;
+  }
+  a.hint_groups = spec->expected_groups;
   PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
@@ -1230,6 +1371,8 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   // dense ranking and every reset sweep all of it (C3, 5.07M groups: 32M -> 16M slots, step
   // 7.96 -> 7.18 ms at an exact hint; the probe kernel itself is unchanged).
   a.min_cap = NextPow2(std::max<uint64_t>(static_cast<uint64_t>(expected) * 8 / 3 + 1, 1024));
+  // A high-cardinality run keeps only the rows with long keys in the table.
+  if (a.HcNext()) a.min_cap = 1 << 16;
   PXG_RETURN_IF_ERROR(a.EnsureTable(a.min_cap));
   PXG_RETURN_IF_ERROR(a.arena.Alloc(1 << 16));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
@@ -1260,17 +1403,19 @@ extern "C" int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* st) {
   const Agg& a = agg->impl;
   st->table_capacity = a.cap;
   st->groups = static_cast<int64_t>(a.inserted);
-  st->rows_selected = static_cast<int64_t>(a.st_n);
+  st->rows_selected = static_cast<int64_t>(a.hc_active ? a.hc_n : a.st_n);
   st->key_arena_bytes = static_cast<int64_t>(a.arena_words * 8);
   st->staging_capacity = static_cast<int64_t>(a.st_cap);
   st->fast_path_keys = a.fast_nk;
   st->big_sort_groups = static_cast<int32_t>(a.last_big_sort_groups);
+  st->hc_mode = a.hc_active ? 1 : 0;
+  st->hc_partition_bits = a.last_hc_pbits;
   return PXG_OK;
 }
 
 extern "C" int32_t pxg_agg_rows_selected(pxg_agg* agg, int64_t* rows) {
   if (!agg || !rows) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
-  *rows = static_cast<int64_t>(agg->impl.st_n);
+  *rows = static_cast<int64_t>(agg->impl.hc_active ? agg->impl.hc_n : agg->impl.st_n);
   return PXG_OK;
 }
 
@@ -1282,8 +1427,9 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   // The group count of the last run survives the reset that ends it (the engine resets an agg
   // after its emit and again when a later query takes it from the cache; sizing by the second
   // reset's zero count shrank C5's 3M-group table back to the hint every query: 5 rehash rounds).
-  if (a.inserted > 0) a.last_groups = a.inserted;
-  const uint32_t fit = NextPow2(std::max<uint64_t>(a.last_groups * 4, a.min_cap));
+  if (a.hc_active && a.res.ready && a.res.n_groups > 0) a.last_groups = static_cast<uint64_t>(a.res.n_groups);
+  else if (a.inserted > 0) a.last_groups = a.inserted;
+  const uint32_t fit = NextPow2(std::max<uint64_t>(a.HcNext() ? 0 : a.last_groups * 4, a.min_cap));
   if (a.cap > 16 * static_cast<uint64_t>(fit)) {
     PXG_HIP(hipStreamSynchronize(a.ctx->stream));
     a.slots.Free();
@@ -1293,6 +1439,8 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));  // stream-ordered before the next consume
   a.st_n = 0;
+  a.hc_n = 0;
+  a.hc_active = false;
   a.arena_words = 0;
   a.inserted = 0;
   a.state_version++;

@@ -68,6 +68,26 @@ struct Agg {
   uint64_t st_cap = 0;
   uint64_t st_n = 0;  // host mirror of the cursor
 
+  // High-cardinality mode (pxg_hc.hip): chosen at the first consume after create / reset when
+  // the plan qualifies (hc_ok) and the hint or the last run says >= kHcMinGroups groups.  Rows
+  // are staged as partition records instead of probing the global table; finalize partitions
+  // them by hash and aggregates each partition in one workgroup's LDS table.
+  bool hc_ok = false;      // plan-level eligibility (pxg_agg_create)
+  bool hc_active = false;  // this run stages partition records
+  int64_t hint_groups = 0;
+  HcStageDev hc_layout{};  // stride / key words (pointers filled per launch)
+  DevBuf hc_rec, hc_key, hc_sv;
+  uint64_t hc_cap = 0;
+  uint64_t hc_n = 0;  // host mirror of the record cursor (counters @48)
+  int32_t last_hc_pbits = 0;  // partition bits of the last finalize (pxg_agg_stats)
+  int32_t EnsureHc(uint64_t need);
+  bool HcNext() const;     // would the next run after a reset be high-cardinality?
+  int32_t FinalizeHc();
+  // Moves staged partition records into the table state (export / import need it): every
+  // record's key goes to the arena and finds or inserts its group, its values become a staging
+  // record.  No-op outside high-cardinality mode; afterwards the run continues on the table.
+  int32_t SpillHc();
+
   AggResult res;
   DevBuf scratch;
   // Bumped by every consume / import / reset: export caches its partition per version.
@@ -91,6 +111,8 @@ struct Agg {
     // big groups by selection (pxg_finalize.hip)
     DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list;
     RadixPassWs rs;
+    // high-cardinality finalize
+    DevBuf hc_k[2], hc_v[2], hc_starts, hc_rep, hc_meta;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);
@@ -107,8 +129,14 @@ struct Agg {
   int32_t ImportPartials(const void* src, int32_t n, const int64_t* offs, const int64_t* sizes);
 };
 
-// Finalize stages (pxg_finalize.hip).
+// Finalize stages (pxg_finalize.hip): the table path, then (high-cardinality mode) the
+// partition records appended after its groups (pxg_hc.hip).
 int32_t AggFinalizeImpl(Agg* agg);
+int32_t AggFinalizeTable(Agg* agg);
+
+// Groups the hint (or the last run) must reach before a qualifying plan stages partition
+// records (PXG_HC_MIN_GROUPS overrides; tests use it at small sizes, 0 disables).
+int64_t HcMinGroups();
 
 }  // namespace pxg
 

@@ -97,6 +97,7 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   const int32_t n = C.nranks;
   // 1. Sizes of the n parts, then the parts themselves (the export synchronises once).
   std::vector<int64_t> offs(n), bytes(n), seg(n);
+  PXG_RETURN_IF_ERROR(a.SpillHc());
   PXG_RETURN_IF_ERROR(a.ExportPartial(n, nullptr, 0, offs.data(), bytes.data()));
   int64_t total = 0;
   for (int p = 0; p < n; ++p) {

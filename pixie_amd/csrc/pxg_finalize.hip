@@ -259,12 +259,15 @@ __global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* _
 // Sorts n records (dense key = DenseKey(keys[i]), values vin[0..nvals)) stably by dense key
 // into kbuf[0/1] / vbuf[0/1] (ping-pong); *skeys / *svals name the sorted streams.
 constexpr int kRsMaxPasses = 4;
+// shift0 / fixed_bits (partition sorts, pxg_hc.hip): sort by bits [shift0, shift0 + fixed_bits)
+// of the raw keys instead (no rank map).
 static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, ConstValPtrs vin,
                                 int nvals, uint64_t n, uint32_t* kbuf[2], ValPtrs vbuf[2], RadixPassWs& ws, const uint32_t** skeys,
-                                ConstValPtrs* svals) {
+                                ConstValPtrs* svals, int shift0 = 0, int fixed_bits = 0) {
   if (n == 0 || n >= (uint64_t(1) << 32)) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %llu records", static_cast<unsigned long long>(n));
   int nbits = 1;
   while ((uint64_t(1) << nbits) < static_cast<uint64_t>(G) + 1) ++nbits;
+  if (fixed_bits > 0) nbits = fixed_bits;
   const int passes = (nbits + kRadixBits - 1) / kRadixBits;
   if (passes > kRsMaxPasses) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %u keys", G);
   const uint32_t ntiles = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
@@ -279,14 +282,14 @@ static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* 
     const bool gather = p == 0 && rank != nullptr;
     uint32_t* gh = ghist + p * kRadixBuckets;
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RsHistKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, n, gather ? rank : nullptr, cap,
-                               G, p * kRadixBits, ws.hist.as<uint32_t>(), ntiles, gather ? kbuf[1] : nullptr));
+                               G, shift0 + p * kRadixBits, ws.hist.as<uint32_t>(), ntiles, gather ? kbuf[1] : nullptr));
     if (gather) kin = kbuf[1];
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsTotalKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0,
                                static_cast<const uint32_t*>(ws.hist.as<uint32_t>()), ntiles, gh));
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsScanKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0, ws.hist.as<uint32_t>(), ntiles,
                                static_cast<const uint32_t*>(gh)));
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RsScatterKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, kbuf[cur], vin, vbuf[cur],
-                               nvals, n, p * kRadixBits, ws.hist.as<const uint32_t>(), ntiles));
+                               nvals, n, shift0 + p * kRadixBits, ws.hist.as<const uint32_t>(), ntiles));
     kin = kbuf[cur];
     for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[cur].p[v];
   }
@@ -1887,6 +1890,29 @@ int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uin
   return PXG_OK;
 }
 
+int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* vals, uint64_t n, DevBuf kb[2], DevBuf vb[2],
+                      RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals) {
+  for (int b = 0; b < 2; ++b) {
+    PXG_RETURN_IF_ERROR(kb[b].Ensure(n * 4 + 16));
+    PXG_RETURN_IF_ERROR(vb[b].Ensure(n * 8 + 16));
+  }
+  ConstValPtrs vin;
+  uint32_t* kbuf[2];
+  ValPtrs vbuf[2];
+  for (int v = 0; v < kMaxVals; ++v) {
+    vin.p[v] = nullptr;
+    vbuf[0].p[v] = vbuf[1].p[v] = nullptr;
+  }
+  vin.p[0] = vals;
+  for (int b = 0; b < 2; ++b) {
+    kbuf[b] = kb[b].as<uint32_t>();
+    vbuf[b].p[0] = vb[b].as<uint64_t>();
+  }
+  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, nullptr, 0, 0, vin, 1, n, kbuf, vbuf, ws, skeys, &vin, shift0, nbits));
+  *svals = vin.p[0];
+  return PXG_OK;
+}
+
 int32_t GroupStarts(Ctx* ctx, const uint32_t* skeys, uint64_t n, uint32_t G, uint32_t* gstart) {
   return Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0, skeys, n, G, gstart);
 }
@@ -1903,7 +1929,7 @@ struct SideJoinGuard {
   }
 };
 
-int32_t AggFinalizeImpl(Agg* a) {
+int32_t AggFinalizeTable(Agg* a) {
   Ctx* ctx = a->ctx;
   SideJoinGuard guard{ctx};
   HostClock clk;

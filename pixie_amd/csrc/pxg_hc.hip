@@ -1,0 +1,512 @@
+// High-cardinality aggregation: partitioned LDS hash tables instead of one global table.
+//
+// Reference: the same AggNode hash aggregation (agg_node.cc:209-271 AggHashMap lookup/insert,
+// ConvertAggHashMapToRowBatch agg_node.cc:303-349).  With millions of groups (C3: ~5-7M
+// (pod, remote_addr) groups from 12M selected rows) a global open-addressing table makes every
+// row a chain of random HBM round trips (probe, representative-row compare, key publication,
+// key extraction), so this mode restructures the work around partitions that fit in LDS:
+//
+//   consume  (AggConsumeFastKernel<..., HC>): one fixed-stride record per selected row (key
+//            words + values, pxg_agg.h HcStageDev), written densely, plus its key hash.
+//   sort     the (hash high half, low half | record index) pairs by the top `pbits` hash bits
+//            (stable LSD radix passes over the partition bits only).
+//   agg      one workgroup per partition (~128-256 records): an LDS open-addressing table of
+//            kHcTable entries {tag, representative record}, exact key compare against the
+//            representative record, LDS integer atomics for count / sum / min / max; the
+//            partition's groups are then emitted densely (one global atomic per partition).
+//   keys     string keys: one scan of the lengths, one copy from the representative records.
+//
+// Results are order-independent integer reductions, so they do not depend on the partition
+// count or on the order threads meet in LDS.  A partition whose distinct keys overflow its
+// table sets a flag and the whole pass reruns with 4x the partitions (kept records and hashes
+// are unchanged).
+#include <algorithm>
+#include <cstdlib>
+
+#include "pxg_agg_host.h"
+#include "pxg_keys.h"
+#include "pxg_scan.h"
+#include "pxg_sort.h"
+
+namespace pxg {
+
+constexpr int kHcBlock = 256;
+constexpr int kHcTable = 1024;  // LDS entries per partition (records per partition average <= 256)
+constexpr int kHcMaxAcc = 4;
+constexpr int kHcKeyWords = 1 + kMaxKeys * kHcStrWords;
+constexpr int kHcRecsLog2 = 8;  // partitions are sized for ~2^kHcRecsLog2 records
+
+enum HcAccOp : int32_t { kHcAdd = 0, kHcMin = 1, kHcMax = 2 };
+
+struct HcAggPlan {
+  int32_t stride, kwords, nk, n_udas, nacc;
+  int32_t ktype[kMaxKeys], koff[kMaxKeys];
+  int32_t uda_kind[kMaxUdas], uda_acc[kMaxUdas];
+  int64_t uda_init[kMaxUdas];
+  int32_t acc_op[kHcMaxAcc], acc_word[kHcMaxAcc];
+};
+
+struct HcOut {
+  uint64_t* uda[kMaxUdas];
+  uint64_t* kfix[kMaxKeys];  // fixed-width keys (UINT128: 2 words per group, BOOLEAN: bytes)
+  uint32_t* klen[kMaxKeys];  // STRING: lengths, turned into offsets by the scan
+  uint32_t* rep;             // representative record of every group (local group index)
+  uint32_t g0;               // groups the table path already wrote
+};
+
+// starts[p] = first sorted record of partition p (p in [0, P]); partition = key >> shift.
+__global__ void HcPartStartsKernel(const uint32_t* __restrict__ skeys, uint64_t n, int shift, uint32_t P, uint32_t* __restrict__ starts) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  const int64_t prev = i == 0 ? -1 : static_cast<int64_t>(skeys[i - 1] >> shift);
+  const int64_t cur = i == n ? static_cast<int64_t>(P) : static_cast<int64_t>(skeys[i] >> shift);
+  for (int64_t p = prev + 1; p <= cur; ++p) starts[p] = static_cast<uint32_t>(i);
+}
+
+__device__ __forceinline__ unsigned long long HcAccInit(int op) {
+  return op == kHcMin ? static_cast<unsigned long long>(INT64_MAX) : (op == kHcMax ? static_cast<unsigned long long>(INT64_MIN) : 0ULL);
+}
+
+// One group's outputs (UDA Finalize, math_ops.h CountUDA / SumUDA / MeanUDA / MinUDA / MaxUDA).
+// MEAN over integer arguments divides the exact integer sum (the reference accumulates the
+// same values in a double; both agree to rounding).
+__device__ __forceinline__ void HcEmit(const HcAggPlan& hp, const HcOut& out, uint32_t g, uint32_t ridx, uint32_t cnt,
+                                       const unsigned long long* s_acc, int slot, const uint64_t* __restrict__ rec) {
+  const uint64_t* r = rec + static_cast<uint64_t>(ridx) * hp.stride;
+  out.rep[g - out.g0] = ridx;
+  const uint64_t lens = r[0];
+  for (int k = 0; k < hp.nk; ++k) {
+    const int t = hp.ktype[k];
+    const uint64_t* kw = r + hp.koff[k];
+    if (t == PXG_STRING) {
+      out.klen[k][g] = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
+    } else if (t == PXG_UINT128) {
+      out.kfix[k][2 * g] = kw[0];
+      out.kfix[k][2 * g + 1] = kw[1];
+    } else if (t == PXG_BOOLEAN) {
+      reinterpret_cast<uint8_t*>(out.kfix[k])[g] = static_cast<uint8_t>(kw[0]);
+    } else {
+      out.kfix[k][g] = kw[0];
+    }
+  }
+  for (int u = 0; u < hp.n_udas; ++u) {
+    const int a = hp.uda_acc[u];
+    const unsigned long long acc = a >= 0 ? s_acc[a * kHcTable + slot] : 0ULL;
+    uint64_t v;
+    switch (hp.uda_kind[u]) {
+      case PXG_UDA_COUNT: v = cnt; break;
+      case PXG_UDA_MEAN: v = FBits(static_cast<double>(static_cast<int64_t>(acc)) / static_cast<double>(cnt)); break;
+      case PXG_UDA_SUM:
+      case PXG_UDA_MINSUM: v = acc + static_cast<uint64_t>(hp.uda_init[u]); break;
+      default: v = acc; break;  // MIN / MAX (integer)
+    }
+    out.uda[u][g] = v;
+  }
+}
+
+// One workgroup per partition (grid-stride).  meta[0]: groups emitted, meta[1]: overflow flag.
+__global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint64_t* __restrict__ rec, const uint64_t* __restrict__ sv,
+                                                       const uint32_t* __restrict__ starts, uint32_t nparts, HcOut out,
+                                                       uint32_t* __restrict__ meta) {
+  extern __shared__ unsigned long long s_dyn[];
+  unsigned long long* s_ent = s_dyn;                                  // [kHcTable]: tag << 32 | rep record
+  unsigned long long* s_acc = s_dyn + kHcTable;                       // [nacc][kHcTable]
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn + kHcTable * (1 + hp.nacc));  // [kHcTable]
+  constexpr int kWaves = kHcBlock / 64;
+  constexpr int kPerThr = kHcTable / kHcBlock;
+  __shared__ uint32_t s_wsum[kWaves];
+  __shared__ uint32_t s_gbase;
+  __shared__ int s_ovf;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (uint32_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    for (int t = threadIdx.x; t < kHcTable; t += kHcBlock) {
+      s_ent[t] = 0;
+      s_cnt[t] = 0;
+      for (int a = 0; a < hp.nacc; ++a) s_acc[a * kHcTable + t] = HcAccInit(hp.acc_op[a]);
+    }
+    if (threadIdx.x == 0) s_ovf = 0;
+    __syncthreads();
+    const uint32_t s = starts[p], e = starts[p + 1];
+    for (uint32_t i = s + threadIdx.x; i < e; i += kHcBlock) {
+      const uint64_t v = sv[i];
+      if (v == kHcHole) continue;
+      const uint32_t idx = static_cast<uint32_t>(v);
+      const uint64_t* r = rec + static_cast<uint64_t>(idx) * hp.stride;
+      uint64_t w[kHcKeyWords];
+#pragma unroll
+      for (int j = 0; j < kHcKeyWords; ++j) w[j] = j < hp.kwords ? r[j] : 0;
+      const uint32_t lo = static_cast<uint32_t>(v >> 32);
+      const uint32_t tag = lo | 0x80000000u;  // an entry is never 0
+      const unsigned long long mine = (static_cast<unsigned long long>(tag) << 32) | idx;
+      uint32_t pos = lo & (kHcTable - 1);
+      int slot = -1;
+      for (int probe = 0; probe < kHcTable; ++probe) {
+        unsigned long long cur = __hip_atomic_load(&s_ent[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+          unsigned long long expected = 0;
+          if (__hip_atomic_compare_exchange_strong(&s_ent[pos], &expected, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            slot = static_cast<int>(pos);
+            break;
+          }
+          cur = expected;
+        }
+        if (static_cast<uint32_t>(cur >> 32) == tag) {
+          const uint64_t* q = rec + static_cast<uint64_t>(static_cast<uint32_t>(cur)) * hp.stride;
+          bool eq = true;
+#pragma unroll
+          for (int j = 0; j < kHcKeyWords; ++j)
+            if (j < hp.kwords) eq = eq && q[j] == w[j];
+          if (eq) {
+            slot = static_cast<int>(pos);
+            break;
+          }
+        }
+        pos = (pos + 1) & (kHcTable - 1);
+      }
+      if (slot < 0) {
+        s_ovf = 1;
+        continue;
+      }
+      atomicAdd(&s_cnt[slot], 1u);
+      for (int a = 0; a < hp.nacc; ++a) {
+        const unsigned long long x = r[hp.acc_word[a]];
+        unsigned long long* dst = &s_acc[a * kHcTable + slot];
+        const int op = hp.acc_op[a];
+        if (op == kHcAdd) atomicAdd(dst, x);
+        else if (op == kHcMin) atomicMin(reinterpret_cast<long long*>(dst), static_cast<long long>(x));
+        else atomicMax(reinterpret_cast<long long*>(dst), static_cast<long long>(x));
+      }
+    }
+    __syncthreads();
+    if (s_ovf) {  // uniform: the host reruns with more partitions
+      if (threadIdx.x == 0) atomicOr(&meta[1], 1u);
+      __syncthreads();
+      continue;
+    }
+    // Emit: thread t owns entries [t * kPerThr, (t + 1) * kPerThr); a block scan of the counts
+    // and one global atomic place the partition's groups.
+    uint32_t occ = 0;
+#pragma unroll
+    for (int k = 0; k < kPerThr; ++k) occ |= (s_ent[threadIdx.x * kPerThr + k] != 0 ? 1u : 0u) << k;
+    const uint32_t c = static_cast<uint32_t>(__popc(occ));
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t x = s_wsum[w];
+      wbase += w < wid ? x : 0u;
+      tot += x;
+    }
+    if (threadIdx.x == 0) s_gbase = tot ? atomicAdd(&meta[0], tot) : 0u;
+    __syncthreads();
+    uint32_t g = out.g0 + s_gbase + wbase + incl - c;
+#pragma unroll
+    for (int k = 0; k < kPerThr; ++k) {
+      if (!((occ >> k) & 1u)) continue;
+      const int slot = threadIdx.x * kPerThr + k;
+      HcEmit(hp, out, g, static_cast<uint32_t>(s_ent[slot]), s_cnt[slot], s_acc, slot, rec);
+      ++g;
+    }
+    __syncthreads();  // the next partition reuses the LDS table
+  }
+}
+
+struct HcKeyCopy {
+  uint32_t* off[kMaxKeys];  // R.key_offsets[k] + g0 (null: not a STRING key)
+  uint8_t* data[kMaxKeys];  // R.key_data[k]
+  uint32_t dbase[kMaxKeys]; // bytes the table path wrote before (offsets are rebased by it)
+};
+
+// String key bytes of every group from its representative record (local group l).
+__global__ void HcKeyCopyKernel(const uint32_t* __restrict__ rep, uint32_t ngroups, const uint64_t* __restrict__ rec, int32_t stride, int nk,
+                                HcKeyCopy kc, HcAggPlan hp) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l > ngroups) return;
+  for (int k = 0; k < nk; ++k) {
+    uint32_t* off = kc.off[k];
+    if (!off) continue;
+    if (l == ngroups) {  // the total (written by the scan)
+      if (kc.dbase[k]) off[l] += kc.dbase[k];
+      continue;
+    }
+    const uint64_t* r = rec + static_cast<uint64_t>(rep[l]) * stride;
+    const uint32_t len = static_cast<uint32_t>((r[0] >> (16 * k)) & 0xFFFF);
+    const uint32_t o = off[l] + kc.dbase[k];
+    if (kc.dbase[k]) off[l] = o;
+    CopyBytesOverlap(kc.data[k] + o, reinterpret_cast<const uint8_t*>(r + hp.koff[k]), len);
+  }
+}
+
+static HcAggPlan MakeHcPlan(const Agg& a) {
+  HcAggPlan hp;
+  std::memset(&hp, 0, sizeof(hp));
+  hp.stride = a.hc_layout.stride;
+  hp.kwords = a.hc_layout.kwords;
+  hp.nk = a.n_keys;
+  hp.n_udas = a.n_udas;
+  for (int k = 0; k < a.n_keys; ++k) {
+    hp.ktype[k] = a.key_types[k];
+    hp.koff[k] = a.hc_layout.koff[k];
+  }
+  for (int u = 0; u < a.n_udas; ++u) {
+    const int kind = a.uda_kind[u];
+    hp.uda_kind[u] = kind;
+    hp.uda_init[u] = a.hplan.uda_init[u];
+    hp.uda_acc[u] = -1;
+    if (kind == PXG_UDA_COUNT) continue;
+    const int i = hp.nacc++;
+    hp.uda_acc[u] = i;
+    hp.acc_op[i] = kind == PXG_UDA_MIN ? kHcMin : (kind == PXG_UDA_MAX ? kHcMax : kHcAdd);
+    hp.acc_word[i] = a.hc_layout.kwords + a.uda_val[u];
+  }
+  return hp;
+}
+
+int32_t Agg::FinalizeHc() {
+  AggResult& R = res;
+  const uint64_t n = hc_n;
+  const uint32_t g0 = static_cast<uint32_t>(R.n_groups);
+  R.ready = false;
+  if (n == 0) {
+    R.ready = true;
+    return PXG_OK;
+  }
+  const HcAggPlan hp = MakeHcPlan(*this);
+  FinalizeWs& w = ws;
+  PXG_RETURN_IF_ERROR(w.hc_meta.Ensure(64));
+  PXG_RETURN_IF_ERROR(w.hc_rep.Ensure(n * 4 + 16));
+  // Result buffers for up to n more groups, keeping the table path's g0 groups.
+  const uint64_t cap_g = static_cast<uint64_t>(g0) + n;
+  uint64_t dbase[kMaxKeys] = {0};
+  for (int u = 0; u < n_udas; ++u) PXG_RETURN_IF_ERROR(R.uda_out[u].Reserve(cap_g * 8, static_cast<size_t>(g0) * 8, ctx->stream));
+  for (int k = 0; k < n_keys; ++k) {
+    const int t = key_types[k];
+    if (t == PXG_STRING) {
+      dbase[k] = static_cast<uint64_t>(R.key_data_len[k]);
+      PXG_RETURN_IF_ERROR(R.key_offsets[k].Reserve((cap_g + 1) * 4, static_cast<size_t>(g0) * 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(R.key_data[k].Reserve(dbase[k] + n * 8 * kHcStrWords + 16, dbase[k], ctx->stream));
+    } else {
+      const size_t wd = t == PXG_UINT128 ? 16 : 8;
+      PXG_RETURN_IF_ERROR(R.key_fixed[k].Reserve(cap_g * wd, static_cast<size_t>(g0) * wd, ctx->stream));
+    }
+  }
+  for (int k = 0; k < n_keys; ++k)
+    if (dbase[k] + n * 8 * kHcStrWords >= (uint64_t(1) << 31)) return SetError(PXG_UNIMPLEMENTED, "string key column over 2 GiB");
+  HcOut out;
+  std::memset(&out, 0, sizeof(out));
+  for (int u = 0; u < n_udas; ++u) out.uda[u] = R.uda_out[u].as<uint64_t>();
+  for (int k = 0; k < n_keys; ++k) {
+    if (key_types[k] == PXG_STRING) out.klen[k] = R.key_offsets[k].as<uint32_t>();
+    else out.kfix[k] = R.key_fixed[k].as<uint64_t>();
+  }
+  out.rep = w.hc_rep.as<uint32_t>();
+  out.g0 = g0;
+  const size_t lds = static_cast<size_t>(kHcTable) * (8 + 8 * hp.nacc + 4);
+  uint32_t* meta = w.hc_meta.as<uint32_t>();
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 192);
+  int pbits = 1;
+  while (pbits < 28 && (n >> (pbits + kHcRecsLog2)) > 0) ++pbits;
+  const char* fe = std::getenv("PXG_HC_PBITS");  // tests: the first pass's partition count
+  const int forced = fe ? std::atoi(fe) : 0;
+  if (forced > 0 && forced <= 28) pbits = forced;
+  uint32_t G = 0;
+  for (;;) {
+    const uint32_t P = 1u << pbits;
+    const int shift = 32 - pbits;
+    const uint32_t* sk = nullptr;
+    const uint64_t* svs = nullptr;
+    PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, hc_sv.as<const uint64_t>(), n, w.hc_k, w.hc_v, w.rs, &sk,
+                                      &svs));
+    PXG_RETURN_IF_ERROR(w.hc_starts.Ensure((static_cast<size_t>(P) + 1) * 4));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_part_starts", HcPartStartsKernel, dim3(GridFor(static_cast<int64_t>(n) + 1, 256, 1 << 30)), dim3(256), 0,
+                               sk, n, shift, P, w.hc_starts.as<uint32_t>()));
+    PXG_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
+    const uint32_t grid = std::min<uint32_t>(P, 1u << 16);
+    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_agg", HcAggKernel, dim3(grid), dim3(kHcBlock), lds, hp, hc_rec.as<const uint64_t>(), svs,
+                               w.hc_starts.as<const uint32_t>(), P, out, meta));
+    PXG_HIP(hipMemcpyAsync(pin, meta, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    G = pin[0];
+    if (pin[1] == 0) break;
+    if (pbits >= 28) return SetError(PXG_INTERNAL, "high-cardinality partitions overflow their LDS tables at 2^28 partitions");
+    pbits = std::min(28, pbits + 2);
+  }
+  last_hc_pbits = pbits;
+  // String keys: lengths -> offsets (scan), then the bytes.
+  bool any_str = false;
+  HcKeyCopy kc;
+  std::memset(&kc, 0, sizeof(kc));
+  for (int k = 0; k < n_keys; ++k) {
+    if (key_types[k] != PXG_STRING) continue;
+    any_str = true;
+    uint32_t* off = R.key_offsets[k].as<uint32_t>() + g0;
+    PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(G) + 1) + 64));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, G, off + G, w.scan.p));
+    kc.off[k] = off;
+    kc.data[k] = R.key_data[k].as<uint8_t>();
+    kc.dbase[k] = static_cast<uint32_t>(dbase[k]);
+  }
+  uint32_t* pin32 = pin + 4;
+  if (any_str && G > 0) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_key_copy", HcKeyCopyKernel, dim3(GridFor(static_cast<int64_t>(G) + 1, 256, 1 << 30)), dim3(256), 0,
+                               static_cast<const uint32_t*>(out.rep), G, hc_rec.as<const uint64_t>(), hp.stride, n_keys, kc, hp));
+    for (int k = 0; k < n_keys; ++k)
+      if (kc.off[k]) PXG_HIP(hipMemcpyAsync(pin32 + k, kc.off[k] + G, 4, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < n_keys; ++k)
+    if (kc.off[k]) R.key_data_len[k] = G > 0 ? pin32[k] : static_cast<int64_t>(dbase[k]);
+  R.n_groups = static_cast<int64_t>(g0) + G;
+  R.ready = true;
+  return PXG_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Spill: partition records -> table state (arena keys, slots, staging records), so export /
+// import (which work on the table state) see every group.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restrict__ plan, HcAggPlan hp, const uint64_t* __restrict__ rec,
+                                                     const uint32_t* __restrict__ hkey, const uint64_t* __restrict__ sv, uint64_t n,
+                                                     int32_t rec_words, uint64_t abase, uint64_t* __restrict__ arena,
+                                                     unsigned long long* __restrict__ slots, uint32_t mask, uint32_t* __restrict__ st_slot,
+                                                     StageDev stg, int nv, unsigned int* __restrict__ counters) {
+  __shared__ unsigned int s_ins;
+  if (threadIdx.x == 0) s_ins = 0;
+  __syncthreads();
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool live = i < n && sv[i] != kHcHole;
+  uint32_t slot = kDeferredSlot;
+  if (live) {
+    const uint64_t* r = rec + i * hp.stride;
+    // Compact arena record (pxg_keys.h layout) in this record's fixed-size arena slot.
+    const uint64_t at = abase + i * static_cast<uint64_t>(rec_words);
+    uint64_t* ar = arena + at;
+    int wo = 0;
+    for (int k = 0; k < hp.nk; ++k) {
+      const int t = hp.ktype[k];
+      const uint64_t* kw = r + hp.koff[k];
+      if (t == PXG_STRING) {
+        const uint32_t len = static_cast<uint32_t>((r[0] >> (16 * k)) & 0xFFFF);
+        ar[wo] = len;
+        const int nw = static_cast<int>((len + 7) >> 3);
+        for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j];
+        wo += 1 + nw;
+      } else if (t == PXG_UINT128) {
+        ar[wo] = kw[0];
+        ar[wo + 1] = kw[1];
+        wo += 2;
+      } else {
+        ar[wo] = kw[0];
+        wo += 1;
+      }
+    }
+    KeySet mine;
+    LoadKeysArena(plan, ar, mine);
+    const uint64_t h = (static_cast<uint64_t>(hkey[i]) << 32) | (sv[i] >> 32);
+    const uint32_t tag = SlotTag(h);
+    const unsigned long long desired = MakeSlotWord(tag, kKindArena, static_cast<uint32_t>(at));
+    uint32_t pos = static_cast<uint32_t>(h) & mask;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+      unsigned long long w = __hip_atomic_load(&slots[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0) {
+        unsigned long long expected = 0;
+        if (__hip_atomic_compare_exchange_strong(&slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          atomicAdd(&s_ins, 1u);
+          slot = pos;
+          break;
+        }
+        w = expected;
+      }
+      if (static_cast<uint32_t>(w >> 33) == tag) {
+        KeySet other;
+        LoadKeysArena(plan, arena + static_cast<uint32_t>(w), other);
+        if (KeysEqual(plan, mine, other)) {
+          slot = pos;
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+    if (slot == kDeferredSlot) atomicOr(&counters[9], 1u);  // table full: cannot happen at <= 25% fill
+  }
+  // Staging records of the live rows, compacted per wave (one cursor atomic per wave).
+  const int lane = threadIdx.x & 63;
+  const unsigned long long m = __ballot(live);
+  if (m) {
+    const int leader = __ffsll(static_cast<long long>(m)) - 1;
+    unsigned long long b = 0;
+    if (lane == leader) b = atomicAdd(stg.cursor, static_cast<unsigned long long>(__popcll(m)));
+    b = __shfl(b, leader, 64);
+    if (live) {
+      const uint64_t sp = b + __popcll(m & ((1ULL << lane) - 1));
+      st_slot[sp] = slot;
+      const uint64_t* r = rec + i * hp.stride;
+      for (int v = 0; v < nv; ++v) stg.vals[v][sp] = r[hp.kwords + v];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_ins) atomicAdd(&counters[0], s_ins);
+}
+
+static uint32_t HcNextPow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return static_cast<uint32_t>(std::min<uint64_t>(p, uint64_t(1) << 31));
+}
+
+int32_t Agg::SpillHc() {
+  if (!hc_active) return PXG_OK;
+  hc_active = false;
+  const uint64_t n = hc_n;
+  hc_n = 0;
+  if (n == 0) return PXG_OK;
+  const HcAggPlan hp = MakeHcPlan(*this);
+  int32_t rec_words = 0;
+  for (int k = 0; k < n_keys; ++k) rec_words += key_types[k] == PXG_STRING ? 1 + kHcStrWords : hc_layout.kw[k];
+  const uint64_t abase = arena_words;
+  if (abase + n * rec_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  PXG_RETURN_IF_ERROR(arena.Reserve((abase + n * rec_words) * 8 + kArenaSlack, abase * 8, ctx->stream));
+  const uint64_t want = 4 * (inserted + n);
+  if (want > (uint64_t(1) << 31)) return SetError(PXG_RESOURCE_UNAVAILABLE, "group table would exceed 2^31 slots");
+  if (want > cap) PXG_RETURN_IF_ERROR(Grow(HcNextPow2(want)));
+  PXG_RETURN_IF_ERROR(EnsureStage(st_n + n));
+  uint8_t* cb = counters.as<uint8_t>();
+  PXG_HIP(hipMemsetAsync(cb + 36, 0, 4, ctx->stream));
+  StageDev stg;
+  std::memset(&stg, 0, sizeof(stg));
+  for (int v = 0; v < n_vals; ++v) stg.vals[v] = st_val[v].as<uint64_t>();
+  stg.cursor = reinterpret_cast<unsigned long long*>(cb + 16);
+  PXG_RETURN_IF_ERROR(Launch(ctx, "hc_spill", HcSpillKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), hp, hc_rec.as<const uint64_t>(), hc_key.as<const uint32_t>(),
+                             hc_sv.as<const uint64_t>(), n, rec_words, abase, arena.as<uint64_t>(), slots.as<unsigned long long>(), cap - 1,
+                             st_slot.as<uint32_t>(), stg, n_vals, counters.as<unsigned int>()));
+  arena_words = abase + n * rec_words;
+  uint8_t* pin = static_cast<uint8_t*>(ctx->pinned) + 224;
+  PXG_HIP(hipMemcpyAsync(pin, cb, 40, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  uint32_t groups = 0, err = 0;
+  std::memcpy(&groups, pin, 4);
+  std::memcpy(&err, pin + 36, 4);
+  std::memcpy(&st_n, pin + 16, 8);
+  if (err) return SetError(PXG_INTERNAL, "group table full while spilling partition records");
+  inserted = groups;
+  state_version++;
+  return PXG_OK;
+}
+
+int32_t AggFinalizeImpl(Agg* a) {
+  PXG_RETURN_IF_ERROR(AggFinalizeTable(a));  // the table path (high-cardinality mode: rows with long keys)
+  if (!a->hc_active) return PXG_OK;
+  return a->FinalizeHc();
+}
+
+}  // namespace pxg

@@ -532,11 +532,13 @@ extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* d
                                           int64_t* part_bytes) {
   if (!agg || !part_offsets || !part_bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   if (n_parts < 1 || n_parts > kMaxParts) return SetError(PXG_INVALID_ARGUMENT, "n_parts must be in [1, %d]", kMaxParts);
+  PXG_RETURN_IF_ERROR(agg->impl.SpillHc());
   return agg->impl.ExportPartial(n_parts, dst, dst_capacity, part_offsets, part_bytes);
 }
 
 extern "C" int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes) {
   if (!agg || !src) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  PXG_RETURN_IF_ERROR(agg->impl.SpillHc());
   return agg->impl.ImportPartial(src, nbytes);
 }
 
@@ -544,5 +546,6 @@ extern "C" int32_t pxg_agg_import_partials(pxg_agg* agg, const void* src, int32_
                                            const int64_t* part_bytes) {
   if (!agg || (n_parts > 0 && (!src || !part_offsets || !part_bytes)) || n_parts < 0)
     return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  PXG_RETURN_IF_ERROR(agg->impl.SpillHc());
   return agg->impl.ImportPartials(src, n_parts, part_offsets, part_bytes);
 }

@@ -231,7 +231,9 @@ class Table:
         return Table(self.ctx, types, handle=h), nprobe.value
 
     def close(self) -> None:
-        if self.h and self.owned:
+        # A table outliving its context (a test that failed before closing it) is not freed:
+        # the context's device state is gone by then.
+        if self.h and self.owned and getattr(self.ctx, "h", None):
             self.lib.pxg_table_destroy(self.h)
         self.h = None
 
@@ -349,9 +351,9 @@ class Agg:
         return int(s.value), int(r.value)
 
     def close(self) -> None:
-        if self.h:
+        if self.h and getattr(self.ctx, "h", None):
             self.lib.pxg_agg_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
