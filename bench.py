@@ -39,7 +39,8 @@ KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_in
            "quant_sel_sample", "quant_sel_hist", "quant_sel_plan", "quant_sel_collect", "quant_sel_bin_sort", "quant_sel_digest",
            "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",
            "export_slot_part", "export_group_rank", "export_row_digit", "export_write_groups", "export_write_rows",
-           "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows"]
+           "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows",
+           "hc_part_starts", "hc_agg", "hc_key_copy", "hc_spill"]
 
 
 def parse():
@@ -470,6 +471,18 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
 
     g = step()
     ctx.sync()
+    # per-kernel breakdown from one untimed, event-bracketed step
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    step()
+    ctx.sync()
+    ctx.set_profiling(False)
+    kernel_ms = {}
+    for name in KERNELS:
+        kl, kms = ctx.kernel_stats(name)
+        if kl:
+            kernel_ms[name] = round(kms, 4)
+    mode = a.info()
     ctx.reset_stats()
     ctx.set_profiling(True, only="agg_consume")
     ctx.sync()
@@ -483,6 +496,8 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
     avg = ms / max(l, 1)
     achieved = alg / (avg / 1000.0) / 1e9
     out = {"workload": "C3: Filter(resp_status>=400) -> Agg by (pod, remote_addr): count, mean(latency), sum(resp_body_size)",
+           "mode": "high-cardinality (partition records + LDS tables, pxg_hc.hip)" if mode.get("hc_mode") else "global table",
+           "partition_bits": mode.get("hc_partition_bits"), "kernel_ms_per_step": kernel_ms,
            "rows": n, "steps": steps, "groups": g, "selected_rows": a.rows_selected(), "ms_per_step": el * 1000.0 / steps,
            "value": n * steps / el, "unit": "rows/s", "algorithmic_bytes_per_row": alg / n,
            "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -62,20 +62,22 @@ struct AggTableDev {
   const uint64_t* arena;
 };
 
-// High-cardinality (partitioned) staging, pxg_hc.hip: one fixed-stride record per selected row
-// whose keys fit (word 0: STRING key lengths, 16 bits per key; then every key's words, tail-masked;
-// then the value streams), the top half of its key hash (the partition bits) and the sort value
-// (low hash half << 32 | record index; ~0 = a hole left by a row that went to the table path).
+// High-cardinality (partitioned) staging, pxg_hc.hip: one record per selected row whose keys
+// fit, stored as `stride` word streams (stream j of record i at rec[j * cap + i], so the consume
+// kernel's stores and the partition sort's loads are coalesced): word 0 holds the STRING key
+// lengths (16 bits per key; ~0 marks a hole left by a row that took the table path), then every
+// key's words (tail-masked), then the value streams.  key[i] = the top half of the key hash
+// (partition bits on top).
 constexpr int kHcStrWords = 3;  // STRING keys of <= 24 bytes ride in the record
 constexpr int kHcMaxVals = 4;
-constexpr int kHcMaxStride = 1 + kMaxKeys * kHcStrWords + kHcMaxVals;
+constexpr int kHcMaxStride = 16;  // record streams the partition sort moves (kMaxVals)
 constexpr uint64_t kHcHole = ~0ULL;
 
 struct HcStageDev {
   uint64_t* rec;
   uint32_t* key;
-  uint64_t* sv;
   unsigned long long* cursor;
+  uint64_t cap;  // words per stream
   int32_t stride, kwords;
   int32_t kw[kMaxKeys], koff[kMaxKeys];
 };

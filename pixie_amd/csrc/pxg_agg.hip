@@ -661,9 +661,10 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
           if (i + kConsumeBlock < total) LoadKeyHeads<NK, S>(plan, ch, row0 + s_sel[i + kConsumeBlock], heads);
 #pragma unroll
           for (int q = 0; q < NK; ++q) fit = fit && (KeyT<S>(plan, q) != PXG_STRING || k.len[q] <= 8u * kHcStrWords);
+          uint64_t* r = stg.hc.rec + pos;
+          const uint64_t cap = stg.hc.cap;
           if (fit) {
             const uint64_t h = HashFastKeys<NK, S>(plan, k);
-            uint64_t* r = stg.hc.rec + pos * static_cast<uint64_t>(stg.hc.stride);
             uint64_t lens = 0;
 #pragma unroll
             for (int q = 0; q < NK; ++q) lens |= static_cast<uint64_t>(k.len[q]) << (16 * q);
@@ -672,16 +673,15 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             for (int q = 0; q < NK; ++q) {
 #pragma unroll
               for (int j = 0; j < kHcStrWords; ++j)
-                if (j < stg.hc.kw[q]) r[stg.hc.koff[q] + j] = k.w[q][j];
+                if (j < stg.hc.kw[q]) r[(stg.hc.koff[q] + j) * cap] = k.w[q][j];
             }
 #pragma unroll
             for (int v = 0; v < kHcMaxVals; ++v)
-              if (v < nv) r[stg.hc.kwords + v] = x[v];
+              if (v < nv) r[(stg.hc.kwords + v) * cap] = x[v];
             stg.hc.key[pos] = static_cast<uint32_t>(h >> 32);
-            stg.hc.sv[pos] = (h << 32) | pos;
           } else {
+            r[0] = kHcHole;
             stg.hc.key[pos] = 0xFFFFFFFFu;
-            stg.hc.sv[pos] = kHcHole;
           }
           // Rows with a long key: a staging record for the table path, deferred (one cursor and
           // one list append per wave).
@@ -845,7 +845,7 @@ static StageDev StageDevOf(Agg* a) {
   s.hc = a->hc_layout;
   s.hc.rec = a->hc_rec.as<uint64_t>();
   s.hc.key = a->hc_key.as<uint32_t>();
-  s.hc.sv = a->hc_sv.as<uint64_t>();
+  s.hc.cap = a->hc_cap;
   s.hc.cursor = reinterpret_cast<unsigned long long*>(a->counters.as<uint8_t>() + 48);
   return s;
 }
@@ -873,10 +873,15 @@ int32_t Agg::EnsureStage(uint64_t need) {
 int32_t Agg::EnsureHc(uint64_t need) {
   if (need <= hc_cap) return PXG_OK;
   const uint64_t c = std::max<uint64_t>(need, hc_cap * 2);
-  const uint64_t sw = static_cast<uint64_t>(hc_layout.stride) * 8;
-  PXG_RETURN_IF_ERROR(hc_rec.Reserve(c * sw + 64, hc_n * sw, ctx->stream));
+  const int sw = hc_layout.stride;
+  DevBuf nr;
+  PXG_RETURN_IF_ERROR(nr.Alloc(c * sw * 8 + 64));
+  if (hc_n > 0)  // stream j moves from j * hc_cap to j * c
+    for (int j = 0; j < sw; ++j)
+      PXG_HIP(hipMemcpyAsync(nr.as<uint64_t>() + j * c, hc_rec.as<uint64_t>() + j * hc_cap, hc_n * 8, hipMemcpyDeviceToDevice, ctx->stream));
   PXG_RETURN_IF_ERROR(hc_key.Reserve(c * 4 + 16, hc_n * 4, ctx->stream));
-  PXG_RETURN_IF_ERROR(hc_sv.Reserve(c * 8 + 16, hc_n * 8, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  hc_rec = std::move(nr);
   hc_cap = c;
   return PXG_OK;
 }
@@ -1334,7 +1339,7 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   // integer atomics: order-independent, so the partition tables give deterministic results),
   // at most kHcMaxVals value streams and 4 accumulated UDAs.
   {
-    bool ok = a.fast_nk > 0 && !a.windowed && !a.emit_states && a.n_vals <= kHcMaxVals;
+    bool ok = a.fast_nk > 0 && !a.windowed && !a.emit_states && a.n_vals <= kHcMaxVals && kMaxVals >= kHcMaxStride;
     int acc = 0;
     for (int u = 0; u < a.n_udas && ok; ++u) {
       const int k = a.uda_kind[u], at = a.uda_arg_type[u];
@@ -1359,6 +1364,7 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
     }
     a.hc_layout.kwords = w;
     a.hc_layout.stride = w + a.n_vals;
+    a.hc_ok = a.hc_ok && a.hc_layout.stride <= kHcMaxStride;
   }
   a.hint_groups = spec->expected_groups;
   PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));

@@ -76,7 +76,7 @@ struct Agg {
   bool hc_active = false;  // this run stages partition records
   int64_t hint_groups = 0;
   HcStageDev hc_layout{};  // stride / key words (pointers filled per launch)
-  DevBuf hc_rec, hc_key, hc_sv;
+  DevBuf hc_rec, hc_key;
   uint64_t hc_cap = 0;
   uint64_t hc_n = 0;  // host mirror of the record cursor (counters @48)
   int32_t last_hc_pbits = 0;  // partition bits of the last finalize (pxg_agg_stats)
@@ -112,7 +112,7 @@ struct Agg {
     DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list;
     RadixPassWs rs;
     // high-cardinality finalize
-    DevBuf hc_k[2], hc_v[2], hc_starts, hc_rep, hc_meta;
+    DevBuf hc_k[2], hc_v[2], hc_starts, hc_kscr, hc_meta;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);

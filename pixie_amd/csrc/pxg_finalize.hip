@@ -1890,26 +1890,23 @@ int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uin
   return PXG_OK;
 }
 
-int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* vals, uint64_t n, DevBuf kb[2], DevBuf vb[2],
-                      RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals) {
+int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* vals, uint64_t vstride, int nvals, uint64_t n,
+                      DevBuf kb[2], DevBuf vb[2], RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals) {
+  if (nvals < 1 || nvals > kMaxVals) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %d streams", nvals);
   for (int b = 0; b < 2; ++b) {
     PXG_RETURN_IF_ERROR(kb[b].Ensure(n * 4 + 16));
-    PXG_RETURN_IF_ERROR(vb[b].Ensure(n * 8 + 16));
+    PXG_RETURN_IF_ERROR(vb[b].Ensure(n * 8 * nvals + 16));
   }
   ConstValPtrs vin;
   uint32_t* kbuf[2];
   ValPtrs vbuf[2];
   for (int v = 0; v < kMaxVals; ++v) {
-    vin.p[v] = nullptr;
-    vbuf[0].p[v] = vbuf[1].p[v] = nullptr;
+    vin.p[v] = v < nvals ? vals + v * vstride : nullptr;
+    for (int b = 0; b < 2; ++b) vbuf[b].p[v] = v < nvals ? vb[b].as<uint64_t>() + v * n : nullptr;
   }
-  vin.p[0] = vals;
-  for (int b = 0; b < 2; ++b) {
-    kbuf[b] = kb[b].as<uint32_t>();
-    vbuf[b].p[0] = vb[b].as<uint64_t>();
-  }
-  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, nullptr, 0, 0, vin, 1, n, kbuf, vbuf, ws, skeys, &vin, shift0, nbits));
-  *svals = vin.p[0];
+  for (int b = 0; b < 2; ++b) kbuf[b] = kb[b].as<uint32_t>();
+  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, nullptr, 0, 0, vin, nvals, n, kbuf, vbuf, ws, skeys, &vin, shift0, nbits));
+  *svals = vin.p[0];  // stream v at *svals + v * n
   return PXG_OK;
 }
 

@@ -6,20 +6,20 @@
 // row a chain of random HBM round trips (probe, representative-row compare, key publication,
 // key extraction), so this mode restructures the work around partitions that fit in LDS:
 //
-//   consume  (AggConsumeFastKernel<..., HC>): one fixed-stride record per selected row (key
-//            words + values, pxg_agg.h HcStageDev), written densely, plus its key hash.
-//   sort     the (hash high half, low half | record index) pairs by the top `pbits` hash bits
-//            (stable LSD radix passes over the partition bits only).
-//   agg      one workgroup per partition (~128-256 records): an LDS open-addressing table of
-//            kHcTable entries {tag, representative record}, exact key compare against the
-//            representative record, LDS integer atomics for count / sum / min / max; the
-//            partition's groups are then emitted densely (one global atomic per partition).
-//   keys     string keys: one scan of the lengths, one copy from the representative records.
+//   consume  (AggConsumeFastKernel<..., HC>): one record per selected row (key words + values,
+//            pxg_agg.h HcStageDev) written densely as word streams, plus its key-hash top half.
+//   sort     the records by the top `pbits` hash bits (stable LSD radix passes over the
+//            partition bits only, every record stream moved with coalesced loads and runs).
+//   agg      one workgroup per partition (~1024 records, contiguous after the sort): an LDS
+//            open-addressing table of kHcTable entries {tag, representative record}, exact key
+//            compare against the representative, LDS integer atomics for count / sum / min /
+//            max; the partition's groups are then emitted densely (one global atomic each).
+//   keys     string keys: one scan of the lengths, one copy from a dense key scratch.
 //
 // Results are order-independent integer reductions, so they do not depend on the partition
 // count or on the order threads meet in LDS.  A partition whose distinct keys overflow its
-// table sets a flag and the whole pass reruns with 4x the partitions (kept records and hashes
-// are unchanged).
+// table sets a flag and the whole pass reruns with 4x the partitions (the staged records are
+// unchanged).
 #include <algorithm>
 #include <cstdlib>
 
@@ -34,11 +34,12 @@ constexpr int kHcBlock = 256;
 constexpr int kHcTable = 1024;  // LDS entries per partition (records per partition average <= 256)
 constexpr int kHcMaxAcc = 4;
 constexpr int kHcKeyWords = 1 + kMaxKeys * kHcStrWords;
-constexpr int kHcRecsLog2 = 8;  // partitions are sized for ~2^kHcRecsLog2 records
+constexpr int kHcRecsLog2 = 10;  // partitions are sized for ~2^kHcRecsLog2 records (<= ~400 groups)
 
 enum HcAccOp : int32_t { kHcAdd = 0, kHcMin = 1, kHcMax = 2 };
 
 struct HcAggPlan {
+  uint64_t n;  // records (the distance between two sorted record streams)
   int32_t stride, kwords, nk, n_udas, nacc;
   int32_t ktype[kMaxKeys], koff[kMaxKeys];
   int32_t uda_kind[kMaxUdas], uda_acc[kMaxUdas];
@@ -50,7 +51,7 @@ struct HcOut {
   uint64_t* uda[kMaxUdas];
   uint64_t* kfix[kMaxKeys];  // fixed-width keys (UINT128: 2 words per group, BOOLEAN: bytes)
   uint32_t* klen[kMaxKeys];  // STRING: lengths, turned into offsets by the scan
-  uint32_t* rep;             // representative record of every group (local group index)
+  uint64_t* kscr;            // the representative's key words, kwords per group (STRING keys), or null
   uint32_t g0;               // groups the table path already wrote
 };
 
@@ -67,28 +68,45 @@ __device__ __forceinline__ unsigned long long HcAccInit(int op) {
   return op == kHcMin ? static_cast<unsigned long long>(INT64_MAX) : (op == kHcMax ? static_cast<unsigned long long>(INT64_MIN) : 0ULL);
 }
 
-// One group's outputs (UDA Finalize, math_ops.h CountUDA / SumUDA / MeanUDA / MinUDA / MaxUDA).
-// MEAN over integer arguments divides the exact integer sum (the reference accumulates the
-// same values in a double; both agree to rounding).
-__device__ __forceinline__ void HcEmit(const HcAggPlan& hp, const HcOut& out, uint32_t g, uint32_t ridx, uint32_t cnt,
-                                       const unsigned long long* s_acc, int slot, const uint64_t* __restrict__ rec) {
-  const uint64_t* r = rec + static_cast<uint64_t>(ridx) * hp.stride;
-  out.rep[g - out.g0] = ridx;
-  const uint64_t lens = r[0];
-  for (int k = 0; k < hp.nk; ++k) {
+// One group's key outputs from its representative's key words: STRING lengths (offsets after
+// the scan), fixed-width keys, and the words into the key scratch (stream-major, so the string
+// copy after the scan streams it).
+template <int KW>
+__device__ __forceinline__ void HcEmitKeys(const HcAggPlan& hp, const HcOut& out, uint32_t g, const uint64_t* w) {
+  const uint32_t l = g - out.g0;
+  if (out.kscr) {
+#pragma unroll
+    for (int j = 0; j < KW; ++j) out.kscr[static_cast<uint64_t>(j) * hp.n + l] = w[j];
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxKeys; ++k) {
+    if (k >= hp.nk) break;
     const int t = hp.ktype[k];
-    const uint64_t* kw = r + hp.koff[k];
+    const int o = hp.koff[k];
+    uint64_t k0 = 0, k1 = 0;
+#pragma unroll
+    for (int j = 1; j < KW; ++j) {
+      k0 = j == o ? w[j] : k0;
+      k1 = j == o + 1 ? w[j] : k1;
+    }
     if (t == PXG_STRING) {
-      out.klen[k][g] = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
+      out.klen[k][g] = static_cast<uint32_t>((w[0] >> (16 * k)) & 0xFFFF);
     } else if (t == PXG_UINT128) {
-      out.kfix[k][2 * g] = kw[0];
-      out.kfix[k][2 * g + 1] = kw[1];
+      out.kfix[k][2 * g] = k0;
+      out.kfix[k][2 * g + 1] = k1;
     } else if (t == PXG_BOOLEAN) {
-      reinterpret_cast<uint8_t*>(out.kfix[k])[g] = static_cast<uint8_t>(kw[0]);
+      reinterpret_cast<uint8_t*>(out.kfix[k])[g] = static_cast<uint8_t>(k0);
     } else {
-      out.kfix[k][g] = kw[0];
+      out.kfix[k][g] = k0;
     }
   }
+}
+
+// One group's UDA outputs (UDA Finalize, math_ops.h CountUDA / SumUDA / MeanUDA / MinUDA /
+// MaxUDA).  MEAN over integer arguments divides the exact integer sum (the reference accumulates
+// the same values in a double; both agree to rounding).
+__device__ __forceinline__ void HcEmitVals(const HcAggPlan& hp, const HcOut& out, uint32_t g, uint32_t cnt, const unsigned long long* s_acc,
+                                           int slot) {
   for (int u = 0; u < hp.n_udas; ++u) {
     const int a = hp.uda_acc[u];
     const unsigned long long acc = a >= 0 ? s_acc[a * kHcTable + slot] : 0ULL;
@@ -104,8 +122,59 @@ __device__ __forceinline__ void HcEmit(const HcAggPlan& hp, const HcOut& out, ui
   }
 }
 
+// Linear probe of the partition table from `pos`: the slot of the record's group (inserting
+// it when absent), or -1 when the table is full.  With `defer`, a tag match is returned as a
+// candidate (*cand = true) without comparing keys, so the caller can issue the compares of
+// several records at once; without it every tag match is compared here.
+template <int KW>
+__device__ __forceinline__ int HcProbe(unsigned long long* s_ent, uint32_t pos, unsigned long long mine, const uint64_t* w,
+                                       const HcAggPlan& hp, const uint64_t* __restrict__ rec, bool defer, bool* cand) {
+  const uint32_t tag = static_cast<uint32_t>(mine >> 32);
+  *cand = false;
+  for (int probe = 0; probe < kHcTable; ++probe) {
+    unsigned long long cur = __hip_atomic_load(&s_ent[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == 0) {
+      unsigned long long expected = 0;
+      if (__hip_atomic_compare_exchange_strong(&s_ent[pos], &expected, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP))
+        return static_cast<int>(pos);
+      cur = expected;
+    }
+    if (static_cast<uint32_t>(cur >> 32) == tag) {
+      if (defer) {
+        *cand = true;
+        return static_cast<int>(pos);
+      }
+      const uint64_t* q = rec + static_cast<uint32_t>(cur);
+      bool eq = true;
+#pragma unroll
+      for (int j = 0; j < KW; ++j) eq = eq && q[j * hp.n] == w[j];
+      if (eq) return static_cast<int>(pos);
+    }
+    pos = (pos + 1) & (kHcTable - 1);
+  }
+  return -1;
+}
+
+// Probe hash of a record's key words (any function of the words works: the partition came
+// from the consume hash, this only spreads a partition's keys over its LDS table).
+template <int KW>
+__device__ __forceinline__ uint64_t HcWordsHash(const uint64_t* w) {
+  uint64_t h = 0x9E3779B97F4A7C15ULL;
+#pragma unroll
+  for (int j = 0; j < KW; ++j) h = Fmix64(h ^ (w[j] + 0xC2B2AE3D27D4EB4FULL * (j + 1)));
+  return h;
+}
+
 // One workgroup per partition (grid-stride).  meta[0]: groups emitted, meta[1]: overflow flag.
-__global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint64_t* __restrict__ rec, const uint64_t* __restrict__ sv,
+// A partition's records are contiguous in the sorted streams (`rec`, stream j at rec + j * n).
+// Records are taken kHcR per thread at a time: their key words are all requested before the
+// first LDS probe, and the representative compares of the batch are issued together after
+// every record has found its candidate slot.  KW: key words per record (hp.kwords), a template
+// so the batch's registers are sized exactly.
+constexpr int kHcR = 4;
+template <int KW>
+__global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint64_t* __restrict__ rec,
                                                        const uint32_t* __restrict__ starts, uint32_t nparts, HcOut out,
                                                        uint32_t* __restrict__ meta) {
   extern __shared__ unsigned long long s_dyn[];
@@ -118,7 +187,9 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
   __shared__ uint32_t s_gbase;
   __shared__ int s_ovf;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t n = hp.n;
   for (uint32_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const uint32_t s = starts[p], e = starts[p + 1];
     for (int t = threadIdx.x; t < kHcTable; t += kHcBlock) {
       s_ent[t] = 0;
       s_cnt[t] = 0;
@@ -126,56 +197,77 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
     }
     if (threadIdx.x == 0) s_ovf = 0;
     __syncthreads();
-    const uint32_t s = starts[p], e = starts[p + 1];
-    for (uint32_t i = s + threadIdx.x; i < e; i += kHcBlock) {
-      const uint64_t v = sv[i];
-      if (v == kHcHole) continue;
-      const uint32_t idx = static_cast<uint32_t>(v);
-      const uint64_t* r = rec + static_cast<uint64_t>(idx) * hp.stride;
-      uint64_t w[kHcKeyWords];
+    // A partition of at most one batch keeps its records in registers through the emit, and
+    // each group's representative writes the group's keys from them.
+    const bool single = e - s <= static_cast<uint32_t>(kHcBlock * kHcR);
+    uint64_t w[kHcR][KW];
+    bool live[kHcR];
+    int slot[kHcR];
 #pragma unroll
-      for (int j = 0; j < kHcKeyWords; ++j) w[j] = j < hp.kwords ? r[j] : 0;
-      const uint32_t lo = static_cast<uint32_t>(v >> 32);
-      const uint32_t tag = lo | 0x80000000u;  // an entry is never 0
-      const unsigned long long mine = (static_cast<unsigned long long>(tag) << 32) | idx;
-      uint32_t pos = lo & (kHcTable - 1);
-      int slot = -1;
-      for (int probe = 0; probe < kHcTable; ++probe) {
-        unsigned long long cur = __hip_atomic_load(&s_ent[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == 0) {
-          unsigned long long expected = 0;
-          if (__hip_atomic_compare_exchange_strong(&s_ent[pos], &expected, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            slot = static_cast<int>(pos);
-            break;
-          }
-          cur = expected;
-        }
-        if (static_cast<uint32_t>(cur >> 32) == tag) {
-          const uint64_t* q = rec + static_cast<uint64_t>(static_cast<uint32_t>(cur)) * hp.stride;
-          bool eq = true;
+    for (int q = 0; q < kHcR; ++q) {
+      live[q] = false;
+      slot[q] = -1;
+    }
+    for (uint32_t b0 = s; b0 < e; b0 += kHcBlock * kHcR) {
 #pragma unroll
-          for (int j = 0; j < kHcKeyWords; ++j)
-            if (j < hp.kwords) eq = eq && q[j] == w[j];
-          if (eq) {
-            slot = static_cast<int>(pos);
-            break;
-          }
-        }
-        pos = (pos + 1) & (kHcTable - 1);
+      for (int q = 0; q < kHcR; ++q) {
+        const uint32_t i = b0 + q * kHcBlock + threadIdx.x;
+        const uint32_t ii = i < e ? i : s;  // in range, ignored
+#pragma unroll
+        for (int j = 0; j < KW; ++j) w[q][j] = rec[j * n + ii];
+        live[q] = i < e && w[q][0] != kHcHole;
       }
-      if (slot < 0) {
-        s_ovf = 1;
-        continue;
+      bool cand[kHcR];
+      unsigned long long mine[kHcR];
+#pragma unroll
+      for (int q = 0; q < kHcR; ++q) {
+        slot[q] = -1;
+        cand[q] = false;
+        const uint64_t h = HcWordsHash<KW>(w[q]);
+        mine[q] = (static_cast<unsigned long long>(static_cast<uint32_t>(h >> 32) | 0x80000000u) << 32) |
+                  (b0 + q * kHcBlock + threadIdx.x);
+        if (!live[q]) continue;
+        slot[q] = HcProbe<KW>(s_ent, static_cast<uint32_t>(h) & (kHcTable - 1), mine[q], w[q], hp, rec, true, &cand[q]);
       }
-      atomicAdd(&s_cnt[slot], 1u);
+      // The candidates' representative key words, all requested before the compares (a
+      // non-candidate reads the partition's first record and ignores it).
+      bool eq[kHcR];
+#pragma unroll
+      for (int q = 0; q < kHcR; ++q) {
+        const uint32_t ri = cand[q] ? static_cast<uint32_t>(s_ent[slot[q]]) : s;
+        eq[q] = true;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) eq[q] = eq[q] && rec[j * n + ri] == w[q][j];
+      }
+#pragma unroll
+      for (int q = 0; q < kHcR; ++q) {
+        if (!cand[q] || eq[q]) continue;
+        // a tag collision: keep probing past it, comparing as we go
+        bool c2;
+        slot[q] = HcProbe<KW>(s_ent, (static_cast<uint32_t>(slot[q]) + 1) & (kHcTable - 1), mine[q], w[q], hp, rec, false, &c2);
+      }
+#pragma unroll
+      for (int q = 0; q < kHcR; ++q) {
+        if (live[q] && slot[q] < 0) s_ovf = 1;
+        if (live[q] && slot[q] >= 0) atomicAdd(&s_cnt[slot[q]], 1u);
+      }
       for (int a = 0; a < hp.nacc; ++a) {
-        const unsigned long long x = r[hp.acc_word[a]];
-        unsigned long long* dst = &s_acc[a * kHcTable + slot];
         const int op = hp.acc_op[a];
-        if (op == kHcAdd) atomicAdd(dst, x);
-        else if (op == kHcMin) atomicMin(reinterpret_cast<long long*>(dst), static_cast<long long>(x));
-        else atomicMax(reinterpret_cast<long long*>(dst), static_cast<long long>(x));
+        const uint64_t* vs = rec + static_cast<uint64_t>(hp.acc_word[a]) * n;
+        uint64_t x[kHcR];
+#pragma unroll
+        for (int q = 0; q < kHcR; ++q) {
+          const uint32_t i = b0 + q * kHcBlock + threadIdx.x;
+          x[q] = vs[i < e ? i : s];
+        }
+#pragma unroll
+        for (int q = 0; q < kHcR; ++q) {
+          if (!live[q] || slot[q] < 0) continue;
+          unsigned long long* dst = &s_acc[a * kHcTable + slot[q]];
+          if (op == kHcAdd) atomicAdd(dst, x[q]);
+          else if (op == kHcMin) atomicMin(reinterpret_cast<long long*>(dst), static_cast<long long>(x[q]));
+          else atomicMax(reinterpret_cast<long long*>(dst), static_cast<long long>(x[q]));
+        }
       }
     }
     __syncthreads();
@@ -201,9 +293,9 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
     uint32_t wbase = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
-      const uint32_t x = s_wsum[w];
-      wbase += w < wid ? x : 0u;
-      tot += x;
+      const uint32_t y = s_wsum[w];
+      wbase += w < wid ? y : 0u;
+      tot += y;
     }
     if (threadIdx.x == 0) s_gbase = tot ? atomicAdd(&meta[0], tot) : 0u;
     __syncthreads();
@@ -211,9 +303,27 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
 #pragma unroll
     for (int k = 0; k < kPerThr; ++k) {
       if (!((occ >> k) & 1u)) continue;
-      const int slot = threadIdx.x * kPerThr + k;
-      HcEmit(hp, out, g, static_cast<uint32_t>(s_ent[slot]), s_cnt[slot], s_acc, slot, rec);
+      const int sl = threadIdx.x * kPerThr + k;
+      HcEmitVals(hp, out, g, s_cnt[sl], s_acc, sl);
+      if (single) {
+        s_cnt[sl] = g;  // the group's output row, for its representative below
+      } else {
+        const uint32_t ri = static_cast<uint32_t>(s_ent[sl]);
+        uint64_t rw[KW];
+#pragma unroll
+        for (int j = 0; j < KW; ++j) rw[j] = rec[j * n + ri];
+        HcEmitKeys<KW>(hp, out, g, rw);
+      }
       ++g;
+    }
+    if (single) {
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kHcR; ++q) {
+        if (!live[q] || slot[q] < 0) continue;
+        const uint32_t i = s + q * kHcBlock + threadIdx.x;
+        if (static_cast<uint32_t>(s_ent[slot[q]]) == i) HcEmitKeys<KW>(hp, out, s_cnt[slot[q]], w[q]);
+      }
     }
     __syncthreads();  // the next partition reuses the LDS table
   }
@@ -225,11 +335,12 @@ struct HcKeyCopy {
   uint32_t dbase[kMaxKeys]; // bytes the table path wrote before (offsets are rebased by it)
 };
 
-// String key bytes of every group from its representative record (local group l).
-__global__ void HcKeyCopyKernel(const uint32_t* __restrict__ rep, uint32_t ngroups, const uint64_t* __restrict__ rec, int32_t stride, int nk,
-                                HcKeyCopy kc, HcAggPlan hp) {
+// String key bytes of every group (local group l) from the key scratch HcEmitKeys wrote
+// (word j of group l at kscr[j * kcap + l]).
+__global__ void HcKeyCopyKernel(const uint64_t* __restrict__ kscr, uint64_t kcap, uint32_t ngroups, int nk, HcKeyCopy kc, HcAggPlan hp) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l > ngroups) return;
+  const uint64_t lens = l < ngroups ? kscr[l] : 0;
   for (int k = 0; k < nk; ++k) {
     uint32_t* off = kc.off[k];
     if (!off) continue;
@@ -237,13 +348,34 @@ __global__ void HcKeyCopyKernel(const uint32_t* __restrict__ rep, uint32_t ngrou
       if (kc.dbase[k]) off[l] += kc.dbase[k];
       continue;
     }
-    const uint64_t* r = rec + static_cast<uint64_t>(rep[l]) * stride;
-    const uint32_t len = static_cast<uint32_t>((r[0] >> (16 * k)) & 0xFFFF);
+    const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
+    uint64_t kw[kHcStrWords];
+#pragma unroll
+    for (int j = 0; j < kHcStrWords; ++j) kw[j] = kscr[static_cast<uint64_t>(hp.koff[k] + j) * kcap + l];
     const uint32_t o = off[l] + kc.dbase[k];
     if (kc.dbase[k]) off[l] = o;
-    CopyBytesOverlap(kc.data[k] + o, reinterpret_cast<const uint8_t*>(r + hp.koff[k]), len);
+    CopyBytesOverlap(kc.data[k] + o, reinterpret_cast<const uint8_t*>(kw), len);
   }
 }
+
+using HcAggFn = void (*)(HcAggPlan, const uint64_t*, const uint32_t*, uint32_t, HcOut, uint32_t*);
+static HcAggFn HcAggFor(int kwords) {
+  switch (kwords) {
+    case 2: return HcAggKernel<2>;
+    case 3: return HcAggKernel<3>;
+    case 4: return HcAggKernel<4>;
+    case 5: return HcAggKernel<5>;
+    case 6: return HcAggKernel<6>;
+    case 7: return HcAggKernel<7>;
+    case 8: return HcAggKernel<8>;
+    case 9: return HcAggKernel<9>;
+    case 10: return HcAggKernel<10>;
+    case 11: return HcAggKernel<11>;
+    case 12: return HcAggKernel<12>;
+    default: return HcAggKernel<13>;
+  }
+}
+static_assert(kHcKeyWords == 13, "HcAggFor covers 2..13 key words");
 
 static HcAggPlan MakeHcPlan(const Agg& a) {
   HcAggPlan hp;
@@ -279,10 +411,10 @@ int32_t Agg::FinalizeHc() {
     R.ready = true;
     return PXG_OK;
   }
-  const HcAggPlan hp = MakeHcPlan(*this);
+  HcAggPlan hp = MakeHcPlan(*this);
+  hp.n = n;
   FinalizeWs& w = ws;
   PXG_RETURN_IF_ERROR(w.hc_meta.Ensure(64));
-  PXG_RETURN_IF_ERROR(w.hc_rep.Ensure(n * 4 + 16));
   // Result buffers for up to n more groups, keeping the table path's g0 groups.
   const uint64_t cap_g = static_cast<uint64_t>(g0) + n;
   uint64_t dbase[kMaxKeys] = {0};
@@ -307,7 +439,12 @@ int32_t Agg::FinalizeHc() {
     if (key_types[k] == PXG_STRING) out.klen[k] = R.key_offsets[k].as<uint32_t>();
     else out.kfix[k] = R.key_fixed[k].as<uint64_t>();
   }
-  out.rep = w.hc_rep.as<uint32_t>();
+  bool any_str_key = false;
+  for (int k = 0; k < n_keys; ++k) any_str_key = any_str_key || key_types[k] == PXG_STRING;
+  if (any_str_key) {
+    PXG_RETURN_IF_ERROR(w.hc_kscr.Ensure(n * static_cast<uint64_t>(hp.kwords) * 8 + 16));
+    out.kscr = w.hc_kscr.as<uint64_t>();
+  }
   out.g0 = g0;
   const size_t lds = static_cast<size_t>(kHcTable) * (8 + 8 * hp.nacc + 4);
   uint32_t* meta = w.hc_meta.as<uint32_t>();
@@ -322,16 +459,16 @@ int32_t Agg::FinalizeHc() {
     const uint32_t P = 1u << pbits;
     const int shift = 32 - pbits;
     const uint32_t* sk = nullptr;
-    const uint64_t* svs = nullptr;
-    PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, hc_sv.as<const uint64_t>(), n, w.hc_k, w.hc_v, w.rs, &sk,
-                                      &svs));
+    const uint64_t* srec = nullptr;
+    PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, hc_rec.as<const uint64_t>(), hc_cap, hp.stride, n,
+                                      w.hc_k, w.hc_v, w.rs, &sk, &srec));
     PXG_RETURN_IF_ERROR(w.hc_starts.Ensure((static_cast<size_t>(P) + 1) * 4));
     PXG_RETURN_IF_ERROR(Launch(ctx, "hc_part_starts", HcPartStartsKernel, dim3(GridFor(static_cast<int64_t>(n) + 1, 256, 1 << 30)), dim3(256), 0,
                                sk, n, shift, P, w.hc_starts.as<uint32_t>()));
     PXG_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
     const uint32_t grid = std::min<uint32_t>(P, 1u << 16);
-    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_agg", HcAggKernel, dim3(grid), dim3(kHcBlock), lds, hp, hc_rec.as<const uint64_t>(), svs,
-                               w.hc_starts.as<const uint32_t>(), P, out, meta));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_agg", HcAggFor(hp.kwords), dim3(grid), dim3(kHcBlock), lds, hp, srec, w.hc_starts.as<const uint32_t>(), P,
+                               out, meta));
     PXG_HIP(hipMemcpyAsync(pin, meta, 8, hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));
     G = pin[0];
@@ -357,7 +494,7 @@ int32_t Agg::FinalizeHc() {
   uint32_t* pin32 = pin + 4;
   if (any_str && G > 0) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "hc_key_copy", HcKeyCopyKernel, dim3(GridFor(static_cast<int64_t>(G) + 1, 256, 1 << 30)), dim3(256), 0,
-                               static_cast<const uint32_t*>(out.rep), G, hc_rec.as<const uint64_t>(), hp.stride, n_keys, kc, hp));
+                               static_cast<const uint64_t*>(out.kscr), hp.n, G, n_keys, kc, hp));
     for (int k = 0; k < n_keys; ++k)
       if (kc.off[k]) PXG_HIP(hipMemcpyAsync(pin32 + k, kc.off[k] + G, 4, hipMemcpyDeviceToHost, ctx->stream));
   }
@@ -374,34 +511,33 @@ int32_t Agg::FinalizeHc() {
 // import (which work on the table state) see every group.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restrict__ plan, HcAggPlan hp, const uint64_t* __restrict__ rec,
-                                                     const uint32_t* __restrict__ hkey, const uint64_t* __restrict__ sv, uint64_t n,
-                                                     int32_t rec_words, uint64_t abase, uint64_t* __restrict__ arena,
+                                                     uint64_t rcap, uint64_t n, int32_t rec_words, uint64_t abase, uint64_t* __restrict__ arena,
                                                      unsigned long long* __restrict__ slots, uint32_t mask, uint32_t* __restrict__ st_slot,
                                                      StageDev stg, int nv, unsigned int* __restrict__ counters) {
   __shared__ unsigned int s_ins;
   if (threadIdx.x == 0) s_ins = 0;
   __syncthreads();
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const bool live = i < n && sv[i] != kHcHole;
+  const uint64_t lens = i < n ? rec[i] : kHcHole;
+  const bool live = lens != kHcHole;
   uint32_t slot = kDeferredSlot;
   if (live) {
-    const uint64_t* r = rec + i * hp.stride;
     // Compact arena record (pxg_keys.h layout) in this record's fixed-size arena slot.
     const uint64_t at = abase + i * static_cast<uint64_t>(rec_words);
     uint64_t* ar = arena + at;
     int wo = 0;
     for (int k = 0; k < hp.nk; ++k) {
       const int t = hp.ktype[k];
-      const uint64_t* kw = r + hp.koff[k];
+      const uint64_t* kw = rec + static_cast<uint64_t>(hp.koff[k]) * rcap + i;
       if (t == PXG_STRING) {
-        const uint32_t len = static_cast<uint32_t>((r[0] >> (16 * k)) & 0xFFFF);
+        const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
         ar[wo] = len;
         const int nw = static_cast<int>((len + 7) >> 3);
-        for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j];
+        for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j * rcap];
         wo += 1 + nw;
       } else if (t == PXG_UINT128) {
         ar[wo] = kw[0];
-        ar[wo + 1] = kw[1];
+        ar[wo + 1] = kw[rcap];
         wo += 2;
       } else {
         ar[wo] = kw[0];
@@ -410,7 +546,7 @@ __global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restric
     }
     KeySet mine;
     LoadKeysArena(plan, ar, mine);
-    const uint64_t h = (static_cast<uint64_t>(hkey[i]) << 32) | (sv[i] >> 32);
+    const uint64_t h = HashKeys(plan, mine);
     const uint32_t tag = SlotTag(h);
     const unsigned long long desired = MakeSlotWord(tag, kKindArena, static_cast<uint32_t>(at));
     uint32_t pos = static_cast<uint32_t>(h) & mask;
@@ -449,8 +585,7 @@ __global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restric
     if (live) {
       const uint64_t sp = b + __popcll(m & ((1ULL << lane) - 1));
       st_slot[sp] = slot;
-      const uint64_t* r = rec + i * hp.stride;
-      for (int v = 0; v < nv; ++v) stg.vals[v][sp] = r[hp.kwords + v];
+      for (int v = 0; v < nv; ++v) stg.vals[v][sp] = rec[static_cast<uint64_t>(hp.kwords + v) * rcap + i];
     }
   }
   __syncthreads();
@@ -486,8 +621,8 @@ int32_t Agg::SpillHc() {
   for (int v = 0; v < n_vals; ++v) stg.vals[v] = st_val[v].as<uint64_t>();
   stg.cursor = reinterpret_cast<unsigned long long*>(cb + 16);
   PXG_RETURN_IF_ERROR(Launch(ctx, "hc_spill", HcSpillKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             d_plan.as<const AggPlanDev>(), hp, hc_rec.as<const uint64_t>(), hc_key.as<const uint32_t>(),
-                             hc_sv.as<const uint64_t>(), n, rec_words, abase, arena.as<uint64_t>(), slots.as<unsigned long long>(), cap - 1,
+                             d_plan.as<const AggPlanDev>(), hp, hc_rec.as<const uint64_t>(), hc_cap, n, rec_words, abase,
+                             arena.as<uint64_t>(), slots.as<unsigned long long>(), cap - 1,
                              st_slot.as<uint32_t>(), stg, n_vals, counters.as<unsigned int>()));
   arena_words = abase + n * rec_words;
   uint8_t* pin = static_cast<uint8_t*>(ctx->pinned) + 224;

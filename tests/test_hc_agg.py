@@ -210,3 +210,25 @@ def test_export_spills_partition_records_to_the_table(ctx, hc_env):
     _check_c3(ref, out)
     for x in aggs + tabs:
         x.close()
+
+
+def test_partitions_of_many_batches(ctx, hc_env):
+    """Two partitions of ~25K records (a few hundred groups each): every partition takes many
+    record batches, and the representative keys are re-read at emit (the multi-batch path)."""
+    hc_env.setenv("PXG_HC_PBITS", "1")
+    rng = np.random.default_rng(21)
+    n = 50_000
+    keys = [f"k{int(i)}" for i in rng.integers(0, 600, n)]
+    ik = rng.integers(0, 3, n)
+    v = rng.integers(-50, 50, n)
+    types = [5, 2, 2]
+    plan = P.linear_plan([P.source_op("t", types, ["k", "i", "v"], [0, 1, 2]),
+                          P.agg_op([0, 1], [P.agg_expr("count", [P.col(2)], [2]), P.agg_expr("sum", [P.col(2)], [2], fid=1),
+                                            P.agg_expr("max", [P.col(2)], [2], fid=2)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": types, "batches": [[Column.from_values(5, keys), Column.from_values(2, ik.tolist()),
+                                                 Column.from_values(2, v.tolist())]]}}
+    ref = oc.execute_plan(plan, tables)["out"][0]["cols"]
+    dev = run_plan(ctx, plan, tables, expected_groups=1000)[0]["cols"]
+    assert len(rows(ref)) > 1500
+    assert rows_match(rows(dev), rows(ref), ordered=False, tol_ulp=0)
