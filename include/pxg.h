@@ -291,6 +291,12 @@ int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups);
  * group-major); the host node renders the JSON string (math_sketches.h:40-54). */
 int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
 void pxg_result_free(pxg_column_out* cols, int32_t n_cols);
+/* Host buffers for result hand-off (no reference counterpart: replaces the per-query malloc of
+ * the engine's result bytes).  Large requests come from a pool of pinned blocks reused across
+ * queries (no page faults, full-speed DMA), small ones from malloc; pxg_host_free releases
+ * either, and also accepts any malloc'ed pointer. */
+void* pxg_host_alloc(int64_t bytes);
+void pxg_host_free(void* p);
 /* ClearAggState (agg_node.cc:173-180): drop all groups (windowed emit). */
 int32_t pxg_agg_reset(pxg_agg* agg);
 /* Number of selected (post-filter) rows consumed since the last reset. */

@@ -2402,23 +2402,23 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
     o.type = a.key_types[k];
     o.length = rows;
     if (o.type == PXG_STRING) {
-      o.offsets = static_cast<int32_t*>(std::malloc((rows + 1) * 4));
-      o.data = static_cast<uint8_t*>(std::malloc(a.res.key_data_len[k] + 16));
+      o.offsets = static_cast<int32_t*>(ResultAlloc((rows + 1) * 4));
+      o.data = static_cast<uint8_t*>(ResultAlloc(a.res.key_data_len[k] + 16));
       o.data_len = a.res.key_data_len[k];
       if (G > 0) {
-        PXG_HIP(hipMemcpy(o.offsets, a.res.key_offsets[k].p, (G + 1) * 4, hipMemcpyDeviceToHost));
-        PXG_HIP(hipMemcpy(o.data, a.res.key_data[k].p, o.data_len, hipMemcpyDeviceToHost));
+        PXG_HIP(hipMemcpyAsync(o.offsets, a.res.key_offsets[k].p, (G + 1) * 4, hipMemcpyDeviceToHost, a.ctx->stream));
+        PXG_HIP(hipMemcpyAsync(o.data, a.res.key_data[k].p, o.data_len, hipMemcpyDeviceToHost, a.ctx->stream));
       } else {
         o.offsets[0] = 0;
       }
     } else {
       const size_t w = TypeWidth(o.type);
-      o.values = std::malloc(std::max<size_t>(rows * w, 1));
+      o.values = ResultAlloc(std::max<size_t>(rows * w, 1));
       if (G > 0) {
         if (o.type == PXG_BOOLEAN) {
-          PXG_HIP(hipMemcpy(o.values, a.res.key_fixed[k].p, G, hipMemcpyDeviceToHost));
+          PXG_HIP(hipMemcpyAsync(o.values, a.res.key_fixed[k].p, G, hipMemcpyDeviceToHost, a.ctx->stream));
         } else {
-          PXG_HIP(hipMemcpy(o.values, a.res.key_fixed[k].p, G * w, hipMemcpyDeviceToHost));
+          PXG_HIP(hipMemcpyAsync(o.values, a.res.key_fixed[k].p, G * w, hipMemcpyDeviceToHost, a.ctx->stream));
         }
       }
     }
@@ -2428,12 +2428,12 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
     o.type = PXG_STRING;
     o.length = rows;
     const int64_t rec = a.state_rec;
-    o.offsets = static_cast<int32_t*>(std::malloc((rows + 1) * 4));
-    o.data = static_cast<uint8_t*>(std::malloc(rows * rec + 16));
+    o.offsets = static_cast<int32_t*>(ResultAlloc((rows + 1) * 4));
+    o.data = static_cast<uint8_t*>(ResultAlloc(rows * rec + 16));
     o.data_len = rows * rec;
     for (int64_t g = 0; g <= rows; ++g) o.offsets[g] = static_cast<int32_t>(g * rec);
     if (!synth) {
-      if (G > 0 && rec > 0) PXG_HIP(hipMemcpy(o.data, a.res.states.p, G * rec, hipMemcpyDeviceToHost));
+      if (G > 0 && rec > 0) PXG_HIP(hipMemcpyAsync(o.data, a.res.states.p, G * rec, hipMemcpyDeviceToHost, a.ctx->stream));
     } else {
       // Initial states serialized (no-groups agg over zero rows): Mean {0, 0.0}, the rest as
       // their initial value.
@@ -2447,6 +2447,7 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
         }
       }
     }
+    PXG_HIP(hipStreamSynchronize(a.ctx->stream));
     return PXG_OK;
   }
   for (int u = 0; u < a.n_udas; ++u) {
@@ -2455,9 +2456,9 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
     o.length = rows;
     const bool q = a.uda_kind[u] == PXG_UDA_QUANTILES;
     const size_t per = q ? 56 : 8;
-    o.values = std::malloc(std::max<size_t>(rows * per, 8));
+    o.values = ResultAlloc(std::max<size_t>(rows * per, 8));
     if (!synth) {
-      PXG_HIP(hipMemcpy(o.values, a.res.uda_out[u].p, G * per, hipMemcpyDeviceToHost));
+      PXG_HIP(hipMemcpyAsync(o.values, a.res.uda_out[u].p, G * per, hipMemcpyDeviceToHost, a.ctx->stream));
       continue;
     }
     // Initial UDA states finalized (AggNode no-groups emit over zero rows, agg_node.cc:182-207).
@@ -2468,6 +2469,7 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
       p[0] = InitialFinalValue(a.uda_kind[u], a.uda_arg_type[u], a.uda_init[u]);
     }
   }
+  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
   return PXG_OK;
 }
 

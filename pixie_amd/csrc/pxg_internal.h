@@ -294,6 +294,10 @@ struct Table {
 struct pxg_table;
 namespace pxg {
 int32_t NewTable(Ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out);
+// Host buffers of pxg_column_out results (pxg_result_free releases them): large ones are pinned
+// pool blocks, reused across results.
+void* ResultAlloc(size_t n);
+void ResultFree(void* p);
 }
 
 struct pxg_ctx {

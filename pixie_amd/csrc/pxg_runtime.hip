@@ -7,6 +7,8 @@
 // a few large Arrow-layout arrays instead of thousands of 100-row batches.
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "pxg_internal.h"
 #include "pxg_scan.h"
@@ -596,12 +598,67 @@ extern "C" int32_t pxg_table_time_bound(pxg_table* tp, int32_t col, int64_t valu
   return PXG_OK;
 }
 
+namespace pxg {
+// Host buffers of large results come from a pool of pinned blocks (power-of-two classes), so a
+// result copy is a DMA into memory that is already resident: no page faults on fresh pages and
+// no bounce through the runtime's staging buffers.  pxg_result_free hands them back.
+namespace {
+constexpr size_t kPinnedMinBytes = size_t(1) << 16;
+constexpr size_t kPinnedKeepBytes = size_t(1) << 29;  // retained free blocks
+std::mutex g_pin_mu;
+std::map<void*, size_t> g_pin_live;                      // block -> class bytes
+std::map<size_t, std::vector<void*>> g_pin_free;
+size_t g_pin_kept = 0;
+}  // namespace
+
+void* ResultAlloc(size_t n) {
+  if (n < kPinnedMinBytes) return std::malloc(std::max<size_t>(n, 1));
+  size_t c = kPinnedMinBytes;
+  while (c < n) c <<= 1;
+  std::lock_guard<std::mutex> lock(g_pin_mu);
+  auto& fl = g_pin_free[c];
+  void* p = nullptr;
+  if (!fl.empty()) {
+    p = fl.back();
+    fl.pop_back();
+    g_pin_kept -= c;
+  } else if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
+    return std::malloc(n);
+  }
+  g_pin_live[p] = c;
+  return p;
+}
+
+void ResultFree(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lock(g_pin_mu);
+    auto it = g_pin_live.find(p);
+    if (it != g_pin_live.end()) {
+      const size_t c = it->second;
+      g_pin_live.erase(it);
+      if (g_pin_kept + c <= kPinnedKeepBytes) {
+        g_pin_free[c].push_back(p);
+        g_pin_kept += c;
+      } else {
+        (void)hipHostFree(p);
+      }
+      return;
+    }
+  }
+  std::free(p);
+}
+}  // namespace pxg
+
+extern "C" void* pxg_host_alloc(int64_t bytes) { return pxg::ResultAlloc(bytes > 0 ? static_cast<size_t>(bytes) : 1); }
+extern "C" void pxg_host_free(void* p) { pxg::ResultFree(p); }
+
 extern "C" void pxg_result_free(pxg_column_out* cols, int32_t n) {
   if (!cols) return;
   for (int32_t i = 0; i < n; ++i) {
-    std::free(cols[i].values);
-    std::free(cols[i].offsets);
-    std::free(cols[i].data);
+    pxg::ResultFree(cols[i].values);
+    pxg::ResultFree(cols[i].offsets);
+    pxg::ResultFree(cols[i].data);
     cols[i].values = nullptr;
     cols[i].offsets = nullptr;
     cols[i].data = nullptr;
