@@ -41,28 +41,18 @@ __device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restr
 // round trip while ~1000 tiles start at once.
 // ---------------------------------------------------------------------------------------
 
-// Wave-aggregated LDS histogram add: lanes holding the same digit are matched with 8 ballots
-// and only the lowest of them adds the group's count, so skewed data (hot groups) does not
-// serialise on one LDS address.
-__device__ __forceinline__ void WaveHistAdd(uint32_t* h, uint32_t d, bool valid) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long peers = __ballot(valid);
-#pragma unroll
-  for (int b = 0; b < kRadixBits; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const unsigned long long m = __ballot(valid && bit);
-    peers &= bit ? m : ~m;
-  }
-  if (valid && (peers & ((1ULL << lane) - 1)) == 0) atomicAdd(&h[d], static_cast<uint32_t>(__popcll(peers)));
-}
-
 // Tile digit counts of one pass -> hist[d * ntiles + tile].  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
 // them instead of gathering again.
 __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
                                                             const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G, int shift,
                                                             uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ dense_out) {
-  __shared__ uint32_t h[kRadixBuckets];
-  h[threadIdx.x] = 0;  // kRadixBlock == kRadixBuckets
+  // One LDS histogram per wave, plain LDS atomics (a hot digit serialises only within its wave;
+  // the 8-ballot match of WaveHistAdd cost more ALU than the conflicts it saved here).
+  constexpr int kWaves = kRadixBlock / 64;
+  __shared__ uint32_t h[kWaves][kRadixBuckets];
+  const int wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) h[w][threadIdx.x] = 0;  // kRadixBlock == kRadixBuckets
   __syncthreads();
   // XCD-aware: neighbouring tiles (whose counts share hist lines, and whose digit runs share
   // output lines in the scatter) run on one XCD, so their partial-line writes meet in one L2.
@@ -87,10 +77,13 @@ __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __re
 #pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
     const uint64_t i = base + static_cast<uint64_t>(k) * kRadixBlock + threadIdx.x;
-    WaveHistAdd(h, (kk[k] >> shift) & (kRadixBuckets - 1), i < n);
+    if (i < n) atomicAdd(&h[wid][(kk[k] >> shift) & (kRadixBuckets - 1)], 1u);
   }
   __syncthreads();
-  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + tile] = h[threadIdx.x];
+  uint32_t t = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) t += h[w][threadIdx.x];
+  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + tile] = t;
 }
 
 // Block d: digit d's total over all tiles (the digit bases come from these; per-tile atomics
@@ -111,11 +104,17 @@ __global__ void __launch_bounds__(kRsScanBlock) RsTotalKernel(const uint32_t* __
   if (threadIdx.x == 0) ghist[blockIdx.x] = s[0];
 }
 
-// Block d: exclusive scan of digit d's tile counts, plus the digit's global base.
+// Block d: exclusive scan of digit d's tile counts, plus the digit's global base.  Each wave
+// scans a contiguous quarter of the row with coalesced loads (4 x 64 counts per step, a wave
+// prefix by shuffles); the quarters' totals are combined through LDS first.
 __global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
                                                              const uint32_t* __restrict__ ghist) {
+  constexpr int kWaves = kRsScanBlock / 64;
+  constexpr int kU = 4;
   __shared__ uint32_t s[kRsScanBlock];
+  __shared__ uint32_t s_w[kWaves];
   const int t = threadIdx.x, d = blockIdx.x;
+  const int lane = t & 63, wid = t >> 6;
   // the digit base: sum of the totals of digits < d
   s[t] = t < d ? ghist[t] : 0u;
   __syncthreads();
@@ -123,26 +122,36 @@ __global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restric
     if (t < o) s[t] += s[t + o];
     __syncthreads();
   }
-  uint32_t carry = s[0];
-  __syncthreads();
+  const uint32_t carry = s[0];
   uint32_t* row = hist + static_cast<uint64_t>(d) * ntiles;
-  const uint32_t per = (ntiles + kRsScanBlock - 1) / kRsScanBlock;  // contiguous run per thread
-  const uint32_t lo = min(ntiles, per * t), hi = min(ntiles, lo + per);
+  const uint32_t per = (ntiles + kWaves - 1) / kWaves;
+  const uint32_t q0 = min(ntiles, per * wid), q1 = min(ntiles, q0 + per);
   uint32_t tot = 0;
-  for (uint32_t i = lo; i < hi; ++i) tot += row[i];
-  s[t] = tot;
+  for (uint32_t i = q0 + lane; i < q1; i += 64) tot += row[i];
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) s_w[wid] = tot;
   __syncthreads();
-  for (int o = 1; o < kRsScanBlock; o <<= 1) {
-    const uint32_t x = t >= o ? s[t - o] : 0u;
-    __syncthreads();
-    s[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = carry + s[t] - tot;
-  for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t c = row[i];
-    row[i] = run;
-    run += c;
+  uint32_t run = carry;
+  for (int w = 0; w < wid; ++w) run += s_w[w];
+  for (uint32_t i0 = q0; i0 < q1; i0 += 64 * kU) {
+    uint32_t c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + u * 64 + lane;
+      c[u] = i < q1 ? row[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      uint32_t incl = c[u];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t i = i0 + u * 64 + lane;
+      if (i < q1) row[i] = run + incl - c[u];
+      run += __shfl(incl, 63, 64);
+    }
   }
 }
 
@@ -360,12 +369,18 @@ __global__ void GroupChunkCountKernel(const uint32_t* __restrict__ gstart, uint3
   cbase[g] = (gstart[g + 1] - gstart[g] + kRedChunk - 1) / kRedChunk;
 }
 
-// chunk -> group map (one thread per group writes its chunks), so a chunk's wave finds its
-// group with one load instead of a binary search over cbase.
-__global__ void ChunkGroupKernel(const uint32_t* __restrict__ cbase, uint32_t ngroups, uint32_t* __restrict__ cgroup) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngroups) return;
-  for (uint32_t c = cbase[g]; c < cbase[g + 1]; ++c) cgroup[c] = g;
+// chunk -> group map: one thread per chunk finds its group by binary search over cbase (a thread
+// per group writing its chunks left the largest group's thread ~3400 sequential stores at 1B rows).
+__global__ void ChunkGroupKernel(const uint32_t* __restrict__ cbase, uint32_t ngroups, uint32_t* __restrict__ cgroup, uint32_t max_chunks) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= max_chunks || c >= cbase[ngroups]) return;
+  uint32_t lo = 0, hi = ngroups;  // last g with cbase[g] <= c
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cbase[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  cgroup[c] = lo;
 }
 
 // Partial state per (uda, chunk): SUM/MINSUM/MEAN = sum (int64 bits or double bits),
@@ -1395,16 +1410,20 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
       if (threadIdx.x == 0) s_nan = 0;
       __syncthreads();
     }
+    // Every value's bin first (16 independent searches in flight), then the LDS counts: an
+    // atomic between two searches would order the next search's LDS reads behind it.
     uint32_t nn = 0;
+    int bin[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
+      const uint64_t key = QKey(raw[k], arg_type);
       const int i = k * 256 + threadIdx.x;
-      if (i < static_cast<int>(c.len)) {
-        const uint64_t key = QKey(raw[k], arg_type);
-        nn += (key < kNegInfKey || key > kPosInfKey) ? 1u : 0u;
-        atomicAdd(&h[SelBin(S, key, nb)], 1u);
-      }
+      nn += (i < static_cast<int>(c.len) && (key < kNegInfKey || key > kPosInfKey)) ? 1u : 0u;
+      bin[k] = SelBin(S, key, nb);
     }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (k * 256 + static_cast<int>(threadIdx.x) < static_cast<int>(c.len)) atomicAdd(&h[bin[k]], 1u);
     if (nn) atomicAdd(&s_nan, nn);
   }
   __syncthreads();
@@ -1648,13 +1667,19 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
     const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
     uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
     uint64_t* cg = cand + c.g_off;
+    // Bins of the whole chunk first (independent searches in flight), then the gathers and
+    // the inside-range sums.
+    int bins[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) bins[r] = SelBin(S, QKey(raw[r], arg_type), nb);
+#pragma unroll
     for (int r = 0; r < kRounds; ++r) {
       const int i = wid * (kMidMax / 4) + r * 64 + lane;
       int u = -1;
       double v = 0.0;
       if (i < static_cast<int>(c.len)) {
         const uint64_t key = QKey(raw[r], arg_type);
-        const int b = SelBin(S, key, nb);
+        const int b = bins[r];
         const uint8_t tag = tg[b];
         if (tag == kTagColl) {
           const uint32_t slot = atomicAdd(&cc[b], 1u);
@@ -2068,8 +2093,8 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
     PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 2 * 8));
     PXG_RETURN_IF_ERROR(ws.cgroup.Ensure(max_chunks * 4 + 16));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                               static_cast<const uint32_t*>(cbase), ngroups, ws.cgroup.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(static_cast<unsigned>((max_chunks + 255) / 256)), dim3(256), 0,
+                               static_cast<const uint32_t*>(cbase), ngroups, ws.cgroup.as<uint32_t>(), static_cast<uint32_t>(max_chunks)));
     if (n < 32 * static_cast<uint64_t>(ngroups)) {  // groups average < 32 rows: a thread per chunk
       PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_reduce", ChunkReduceThreadKernel, dim3(static_cast<unsigned>((max_chunks + 255) / 256)),
                                  dim3(256), 0, a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase),
