@@ -1670,10 +1670,12 @@ class PostAggMapNode : public ExecNode {
         std::vector<uint8_t>& fin = finite_[pk.first];
         if (static_cast<int64_t>(fin.size()) != G) {
           fin.resize(static_cast<size_t>(G));
+          // NaN / inf <=> all exponent bits set; branch-free over the 7 values so it vectorises.
+          const uint64_t* bits = static_cast<const uint64_t*>(it->second.values);
           for (int64_t g = 0; g < G; ++g) {
-            bool f = true;
-            for (int k = 0; k < 7; ++k) f = f && !pxjson::IsNanOrInf(d[g * 7 + k]);
-            fin[static_cast<size_t>(g)] = f ? 1 : 0;
+            uint32_t bad = 0;
+            for (int k = 0; k < 7; ++k) bad |= ((bits[g * 7 + k] >> 52) & 0x7FF) == 0x7FF ? 1u : 0u;
+            fin[static_cast<size_t>(g)] = static_cast<uint8_t>(bad ^ 1u);
           }
         }
         for (int64_t g = 0; g < G; ++g) v[g] = (qk >= 0 && fin[static_cast<size_t>(g)]) ? d[g * 7 + qk] : 0.0;

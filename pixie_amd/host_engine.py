@@ -235,6 +235,16 @@ class Engine:
         finally:
             self.lib.pxc_free(out)
 
+    def execute_bytes_len(self, pb: bytes) -> int:
+        """pxc_execute_plan on serialized plan bytes over the stored tables; the PXRB result is
+        produced and released without copying it into Python (the timing harness's call: the
+        result buffer is what a host-language binding would hand on).  Returns its length."""
+        out = C.c_void_p()
+        n = C.c_int64()
+        _check(self.lib.pxc_execute_plan(self.h, pb, len(pb), 0, None, C.byref(out), C.byref(n)))
+        self.lib.pxc_free(out)
+        return int(n.value)
+
     def execute(self, plan, tables: Dict[str, dict] = None):
         """Run the plan's first fragment; returns {sink: [{'rows','eow','eos','cols'}]}."""
         pb = plan.SerializeToString()
