@@ -77,6 +77,7 @@ struct HcStageDev {
   uint64_t* rec;
   uint32_t* key;
   unsigned long long* cursor;
+  unsigned int* maxlen;  // [kMaxKeys]: the longest STRING key staged (finalize sorts only its words)
   uint64_t cap;  // words per stream
   int32_t stride, kwords;
   int32_t kw[kMaxKeys], koff[kMaxKeys];

@@ -539,7 +539,9 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   __shared__ unsigned int s_ins;
   __shared__ unsigned long long s_base;
   __shared__ KeyCols<NK> s_kc[kLdsChunks];
+  __shared__ unsigned int s_mlen[NK];  // HC: the workgroup's longest STRING key per key
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (HC && threadIdx.x < NK) s_mlen[threadIdx.x] = 0;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   const uint32_t bid = XcdRemap(blockIdx.x, gridDim.x);
   const int nv = plan->n_vals;
@@ -667,7 +669,10 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             const uint64_t h = HashFastKeys<NK, S>(plan, k);
             uint64_t lens = 0;
 #pragma unroll
-            for (int q = 0; q < NK; ++q) lens |= static_cast<uint64_t>(k.len[q]) << (16 * q);
+            for (int q = 0; q < NK; ++q) {
+              lens |= static_cast<uint64_t>(k.len[q]) << (16 * q);
+              if (KeyT<S>(plan, q) == PXG_STRING) atomicMax(&s_mlen[q], k.len[q]);
+            }
             r[0] = lens;
 #pragma unroll
             for (int q = 0; q < NK; ++q) {
@@ -750,6 +755,10 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
     }
   }
   if (threadIdx.x == 0 && s_ins) atomicAdd(&tab.counters[0], s_ins);
+  if constexpr (HC) {
+    __syncthreads();
+    if (threadIdx.x < NK && s_mlen[threadIdx.x]) atomicMax(&stg.hc.maxlen[threadIdx.x], s_mlen[threadIdx.x]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -847,6 +856,7 @@ static StageDev StageDevOf(Agg* a) {
   s.hc.key = a->hc_key.as<uint32_t>();
   s.hc.cap = a->hc_cap;
   s.hc.cursor = reinterpret_cast<unsigned long long*>(a->counters.as<uint8_t>() + 48);
+  s.hc.maxlen = a->hc_maxlen.as<unsigned int>();
   return s;
 }
 
@@ -932,6 +942,7 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
   PXG_HIP(hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 56, hipMemcpyDeviceToHost, ctx->stream));
+  if (hc_active) PXG_HIP(hipMemcpyAsync(pin + 64, hc_maxlen.p, sizeof(hc_maxlen_h), hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   uint8_t c[56];
   uint64_t tot = 0;
@@ -940,6 +951,7 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   std::memcpy(n_deferred, c + 8, 4);
   std::memcpy(&st_n, c + 16, 8);
   std::memcpy(&hc_n, c + 48, 8);
+  if (hc_active) std::memcpy(hc_maxlen_h, pin + 64, sizeof(hc_maxlen_h));
 
   const uint64_t n_new = tot >> kPublishCountShift;
   const uint64_t words = tot & ((uint64_t(1) << kPublishCountShift) - 1);
@@ -1370,6 +1382,8 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
+  PXG_RETURN_IF_ERROR(a.hc_maxlen.Alloc(sizeof(a.hc_maxlen_h)));
+  PXG_HIP(hipMemsetAsync(a.hc_maxlen.p, 0, sizeof(a.hc_maxlen_h), a.ctx->stream));
   const int64_t expected = spec->expected_groups > 0 ? spec->expected_groups : 4096;
   // The smallest table that holds the expected groups at <= 3/8 load, the fill the post-consume
   // growth rule keeps (ConsumeRange): an exact hint (the engine's group-count statistics) never
@@ -1444,6 +1458,8 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   }
   PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));  // stream-ordered before the next consume
+  PXG_HIP(hipMemsetAsync(a.hc_maxlen.p, 0, sizeof(a.hc_maxlen_h), a.ctx->stream));
+  std::memset(a.hc_maxlen_h, 0, sizeof(a.hc_maxlen_h));
   a.st_n = 0;
   a.hc_n = 0;
   a.hc_active = false;

@@ -77,6 +77,8 @@ struct Agg {
   int64_t hint_groups = 0;
   HcStageDev hc_layout{};  // stride / key words (pointers filled per launch)
   DevBuf hc_rec, hc_key;
+  DevBuf hc_maxlen;                       // u32 [kMaxKeys], device
+  uint32_t hc_maxlen_h[kMaxKeys] = {0};   // host mirror (read with the publish counters)
   uint64_t hc_cap = 0;
   uint64_t hc_n = 0;  // host mirror of the record cursor (counters @48)
   int32_t last_hc_pbits = 0;  // partition bits of the last finalize (pxg_agg_stats)

@@ -1367,8 +1367,17 @@ __global__ void __launch_bounds__(NS / kMsIpt) BigSampleKernel(const BigGroup* _
 // global histogram once per group it meets, not once per chunk.
 // BigCollect (per-chunk range sums, latency-bound gathers) wants more blocks in flight than
 // BigHist (whose per-group flush is the cost it saves), hence the larger per-CU target.
-static uint32_t SelChunksPerBlock(uint32_t nchunks, int num_cus, uint32_t blocks_per_cu) {
-  return std::max<uint32_t>(1, std::min<uint32_t>(8, nchunks / (blocks_per_cu * static_cast<uint32_t>(num_cus))));
+static uint32_t SelChunksPerBlock(uint32_t nchunks, int num_cus, uint32_t blocks_per_cu, uint32_t cap = 8) {
+  return std::max<uint32_t>(1, std::min<uint32_t>(cap, nchunks / (blocks_per_cu * static_cast<uint32_t>(num_cus))));
+}
+// quant_sel_hist: every block flushes its LDS histogram (up to kSelBins device atomics) and loads
+// its group's splitters, so blocks take more chunks than the collect pass: up to 32 (1B rows:
+// 0.77 -> 0.60 ms average over the profiled launches, tools/n1_selhist_ab.sh; PXG_SEL_HIST_CPB
+// overrides).
+static uint32_t SelHistCap() {
+  const char* e = std::getenv("PXG_SEL_HIST_CPB");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? static_cast<uint32_t>(v) : 32;
 }
 __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                      const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
@@ -1915,7 +1924,7 @@ int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uin
   return PXG_OK;
 }
 
-int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* vals, uint64_t vstride, int nvals, uint64_t n,
+int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* const* vals, int nvals, uint64_t n,
                       DevBuf kb[2], DevBuf vb[2], RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals) {
   if (nvals < 1 || nvals > kMaxVals) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %d streams", nvals);
   for (int b = 0; b < 2; ++b) {
@@ -1926,7 +1935,7 @@ int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, con
   uint32_t* kbuf[2];
   ValPtrs vbuf[2];
   for (int v = 0; v < kMaxVals; ++v) {
-    vin.p[v] = v < nvals ? vals + v * vstride : nullptr;
+    vin.p[v] = v < nvals ? vals[v] : nullptr;
     for (int b = 0; b < 2; ++b) vbuf[b].p[v] = v < nvals ? vb[b].as<uint64_t>() + v * n : nullptr;
   }
   for (int b = 0; b < 2; ++b) kbuf[b] = kb[b].as<uint32_t>();
@@ -2160,7 +2169,7 @@ int32_t AggFinalizeTable(Agg* a) {
       PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_big_groups),
                                    dim3(kSelSampleThreads), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
                                    vals, at, ws.sel_spl.as<uint64_t>()));
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 2);
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 2, SelHistCap());
     return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
                     ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);

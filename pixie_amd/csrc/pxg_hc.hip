@@ -330,6 +330,7 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
 }
 
 struct HcKeyCopy {
+  int32_t kw[kMaxKeys];     // the key's words in the scratch
   uint32_t* off[kMaxKeys];  // R.key_offsets[k] + g0 (null: not a STRING key)
   uint8_t* data[kMaxKeys];  // R.key_data[k]
   uint32_t dbase[kMaxKeys]; // bytes the table path wrote before (offsets are rebased by it)
@@ -351,7 +352,7 @@ __global__ void HcKeyCopyKernel(const uint64_t* __restrict__ kscr, uint64_t kcap
     const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
     uint64_t kw[kHcStrWords];
 #pragma unroll
-    for (int j = 0; j < kHcStrWords; ++j) kw[j] = kscr[static_cast<uint64_t>(hp.koff[k] + j) * kcap + l];
+    for (int j = 0; j < kHcStrWords; ++j) kw[j] = j < kc.kw[k] ? kscr[static_cast<uint64_t>(hp.koff[k] + j) * kcap + l] : 0;
     const uint32_t o = off[l] + kc.dbase[k];
     if (kc.dbase[k]) off[l] = o;
     CopyBytesOverlap(kc.data[k] + o, reinterpret_cast<const uint8_t*>(kw), len);
@@ -361,6 +362,7 @@ __global__ void HcKeyCopyKernel(const uint64_t* __restrict__ kscr, uint64_t kcap
 using HcAggFn = void (*)(HcAggPlan, const uint64_t*, const uint32_t*, uint32_t, HcOut, uint32_t*);
 static HcAggFn HcAggFor(int kwords) {
   switch (kwords) {
+    case 1: return HcAggKernel<1>;
     case 2: return HcAggKernel<2>;
     case 3: return HcAggKernel<3>;
     case 4: return HcAggKernel<4>;
@@ -375,19 +377,33 @@ static HcAggFn HcAggFor(int kwords) {
     default: return HcAggKernel<13>;
   }
 }
-static_assert(kHcKeyWords == 13, "HcAggFor covers 2..13 key words");
+static_assert(kHcKeyWords == 13, "HcAggFor covers 1..13 key words");
 
-static HcAggPlan MakeHcPlan(const Agg& a) {
+// The partition pass's record layout.  With `compact`, a STRING key keeps only the words its
+// longest staged value needs (the rest of its streams are all zero: C3's remote_addr fits 2 of
+// its 3 words), so the sort moves and hc_agg reads fewer streams; src[j] names the staged stream
+// of compacted word j.  Without it (spill) the staged layout as is.
+static HcAggPlan MakeHcPlan(const Agg& a, bool compact = false, int32_t* src = nullptr, int32_t* kwc = nullptr) {
   HcAggPlan hp;
   std::memset(&hp, 0, sizeof(hp));
-  hp.stride = a.hc_layout.stride;
-  hp.kwords = a.hc_layout.kwords;
   hp.nk = a.n_keys;
   hp.n_udas = a.n_udas;
+  int w = 1;
+  if (src) src[0] = 0;
   for (int k = 0; k < a.n_keys; ++k) {
     hp.ktype[k] = a.key_types[k];
-    hp.koff[k] = a.hc_layout.koff[k];
+    int kw = a.hc_layout.kw[k];
+    if (compact && a.key_types[k] == PXG_STRING) kw = std::min<int>(kw, static_cast<int>((a.hc_maxlen_h[k] + 7) / 8));
+    hp.koff[k] = w;
+    if (kwc) kwc[k] = kw;
+    for (int j = 0; j < kw; ++j)
+      if (src) src[w + j] = a.hc_layout.koff[k] + j;
+    w += kw;
   }
+  hp.kwords = w;
+  for (int v = 0; v < a.n_vals; ++v)
+    if (src) src[w + v] = a.hc_layout.kwords + v;
+  hp.stride = w + a.n_vals;
   for (int u = 0; u < a.n_udas; ++u) {
     const int kind = a.uda_kind[u];
     hp.uda_kind[u] = kind;
@@ -397,7 +413,7 @@ static HcAggPlan MakeHcPlan(const Agg& a) {
     const int i = hp.nacc++;
     hp.uda_acc[u] = i;
     hp.acc_op[i] = kind == PXG_UDA_MIN ? kHcMin : (kind == PXG_UDA_MAX ? kHcMax : kHcAdd);
-    hp.acc_word[i] = a.hc_layout.kwords + a.uda_val[u];
+    hp.acc_word[i] = hp.kwords + a.uda_val[u];
   }
   return hp;
 }
@@ -411,8 +427,12 @@ int32_t Agg::FinalizeHc() {
     R.ready = true;
     return PXG_OK;
   }
-  HcAggPlan hp = MakeHcPlan(*this);
+  int32_t src[kHcMaxStride];
+  int32_t kwc[kMaxKeys];
+  HcAggPlan hp = MakeHcPlan(*this, true, src, kwc);
   hp.n = n;
+  const uint64_t* streams[kHcMaxStride];
+  for (int j = 0; j < hp.stride; ++j) streams[j] = hc_rec.as<const uint64_t>() + static_cast<uint64_t>(src[j]) * hc_cap;
   FinalizeWs& w = ws;
   PXG_RETURN_IF_ERROR(w.hc_meta.Ensure(64));
   // Result buffers for up to n more groups, keeping the table path's g0 groups.
@@ -460,8 +480,8 @@ int32_t Agg::FinalizeHc() {
     const int shift = 32 - pbits;
     const uint32_t* sk = nullptr;
     const uint64_t* srec = nullptr;
-    PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, hc_rec.as<const uint64_t>(), hc_cap, hp.stride, n,
-                                      w.hc_k, w.hc_v, w.rs, &sk, &srec));
+    PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, streams, hp.stride, n, w.hc_k, w.hc_v, w.rs, &sk,
+                                      &srec));
     PXG_RETURN_IF_ERROR(w.hc_starts.Ensure((static_cast<size_t>(P) + 1) * 4));
     PXG_RETURN_IF_ERROR(Launch(ctx, "hc_part_starts", HcPartStartsKernel, dim3(GridFor(static_cast<int64_t>(n) + 1, 256, 1 << 30)), dim3(256), 0,
                                sk, n, shift, P, w.hc_starts.as<uint32_t>()));
@@ -488,6 +508,7 @@ int32_t Agg::FinalizeHc() {
     PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(G) + 1) + 64));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, G, off + G, w.scan.p));
     kc.off[k] = off;
+    kc.kw[k] = kwc[k];
     kc.data[k] = R.key_data[k].as<uint8_t>();
     kc.dbase[k] = static_cast<uint32_t>(dbase[k]);
   }

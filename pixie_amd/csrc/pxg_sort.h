@@ -22,9 +22,9 @@ int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uin
                        uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals);
 
 // Sorts n records stably by bits [shift0, shift0 + nbits) of keys[i], moving nvals u64 value
-// streams with them (stream v of record i at vals[v * vstride + i]).  Ping-pong buffers kb / vb
-// are grown as needed; on return stream v sorted is at *svals + v * n.
-int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* vals, uint64_t vstride, int nvals, uint64_t n,
+// streams with them (vals[v][i]).  Ping-pong buffers kb / vb are grown as needed; on return
+// stream v sorted is at *svals + v * n.
+int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* const* vals, int nvals, uint64_t n,
                       DevBuf kb[2], DevBuf vb[2], RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals);
 
 // gstart[k] = first index of dense key k in the sorted keys, gstart[G] = count of keys < G.

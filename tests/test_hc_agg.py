@@ -232,3 +232,24 @@ def test_partitions_of_many_batches(ctx, hc_env):
     dev = run_plan(ctx, plan, tables, expected_groups=1000)[0]["cols"]
     assert len(rows(ref)) > 1500
     assert rows_match(rows(dev), rows(ref), ordered=False, tol_ulp=0)
+
+
+def test_all_empty_and_short_string_keys(ctx, hc_env):
+    """The partition pass keeps only the words the longest staged key needs: a key column of
+    empty strings keeps none (the record is the lengths word alone), short keys keep one."""
+    rng = np.random.default_rng(9)
+    n = 30_000
+    ints = rng.integers(0, 2000, n)
+    short = [f"{int(i) % 97:x}" for i in rng.integers(0, 1 << 30, n)]
+    v = rng.integers(0, 100, n)
+    types = [5, 2, 5, 2]
+    batch = [Column.from_values(5, [""] * n), Column.from_values(2, ints.tolist()), Column.from_values(5, short),
+             Column.from_values(2, v.tolist())]
+    tables = {"t": {"types": types, "batches": [batch]}}
+    for gcols in ([0], [0, 1], [2, 0], [2, 1]):
+        plan = P.linear_plan([P.source_op("t", types, ["e", "i", "s", "v"], [0, 1, 2, 3]),
+                              P.agg_op(gcols, [P.agg_expr("count", [P.col(3)], [2]), P.agg_expr("sum", [P.col(3)], [2], fid=1)]),
+                              P.sink_op("out")])
+        ref = oc.execute_plan(plan, tables)["out"][0]["cols"]
+        dev = run_plan(ctx, plan, tables, expected_groups=5000)[0]["cols"]
+        assert rows_match(rows(dev), rows(ref), ordered=False, tol_ulp=0), gcols
