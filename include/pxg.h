@@ -290,6 +290,16 @@ int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups);
  * QUANTILES the column is FLOAT64 with 7 values per group (p01,p10,p25,p50,p75,p90,p99,
  * group-major); the host node renders the JSON string (math_sketches.h:40-54). */
 int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
+/* pxg_agg_result with skip[c] != 0 leaving value column c without buffers (type and length
+ * set; the caller reads it another way, e.g. pxg_agg_quantile_lanes). */
+int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip);
+/* The quantile lanes a post-aggregate pluck_float64 reads (MapNode over the AggNode output,
+ * math_sketches.h:40-54 + the pluck UDF): for every group, the lanes set in lane_mask (bit k =
+ * p01,p10,p25,p50,p75,p90,p99[k]) packed in lane order into host_out (popcount(mask) doubles
+ * per group), and host_finite[g] = 1 when all 7 quantiles of the group are finite (a NaN / inf
+ * one truncates the reference's JSON, which pluck then fails to parse: 0.0 for every key).
+ * Host buffers hold n_groups * popcount(mask) doubles / n_groups bytes. */
+int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t lane_mask, double* host_out, uint8_t* host_finite);
 void pxg_result_free(pxg_column_out* cols, int32_t n_cols);
 /* Host buffers for result hand-off (no reference counterpart: replaces the per-query malloc of
  * the engine's result bytes).  Large requests come from a pool of pinned blocks reused across

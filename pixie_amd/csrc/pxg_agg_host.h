@@ -18,6 +18,7 @@ struct AggResult {
   int64_t key_data_len[kMaxKeys] = {0};
   DevBuf uda_out[kMaxUdas];     // 8 B per group (QUANTILES: 7 doubles per group)
   DevBuf states;                // emit_states: state_rec bytes per group (Serialize layout)
+  DevBuf lanes;                 // pxg_agg_quantile_lanes scratch
   // Forget the result; device buffers stay allocated for the next finalize.
   void Clear() {
     n_groups = 0;

@@ -2422,6 +2422,48 @@ static uint64_t InitialFinalValue(int kind, int at, int64_t init) {
 }
 
 extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols) {
+  return pxg_agg_result_skip(agg, cols, n_cols, nullptr);
+}
+
+// Selected quantile lanes, packed, plus whether all 7 of a group's quantiles are finite (a NaN /
+// inf one makes the reference's JSON unparsable, so pluck_float64 yields 0.0 for every key).
+__global__ void QuantLanesKernel(const double* __restrict__ q, uint64_t G, uint32_t mask, int nsel, double* __restrict__ out,
+                                 uint8_t* __restrict__ fin) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  bool f = true;
+  int o = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double v = q[g * 7 + k];
+    f = f && !isnan(v) && !isinf(v);
+    if ((mask >> k) & 1u) out[g * nsel + o++] = v;
+  }
+  fin[g] = f ? 1 : 0;
+}
+
+extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t lane_mask, double* host_out, uint8_t* host_finite) {
+  if (!agg || !host_finite || (lane_mask && !host_out)) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Agg& a = agg->impl;
+  if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
+  if (uda < 0 || uda >= a.n_udas || a.uda_kind[uda] != PXG_UDA_QUANTILES)
+    return SetError(PXG_INVALID_ARGUMENT, "aggregate %d is not a quantiles UDA", uda);
+  lane_mask &= 0x7Fu;
+  const int nsel = __builtin_popcount(lane_mask);
+  const uint64_t G = static_cast<uint64_t>(a.res.n_groups);
+  if (G == 0) return PXG_OK;
+  PXG_RETURN_IF_ERROR(a.res.lanes.Ensure(G * (8 * nsel + 1) + 16));
+  double* d_out = a.res.lanes.as<double>();
+  uint8_t* d_fin = reinterpret_cast<uint8_t*>(d_out + G * nsel);
+  PXG_RETURN_IF_ERROR(Launch(a.ctx, "quant_lanes", QuantLanesKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                             a.res.uda_out[uda].as<const double>(), G, lane_mask, nsel, d_out, d_fin));
+  if (nsel) PXG_HIP(hipMemcpyAsync(host_out, d_out, G * nsel * 8, hipMemcpyDeviceToHost, a.ctx->stream));
+  PXG_HIP(hipMemcpyAsync(host_finite, d_fin, G, hipMemcpyDeviceToHost, a.ctx->stream));
+  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip) {
   if (!agg || !cols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   Agg& a = agg->impl;
   if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
@@ -2488,6 +2530,7 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
     pxg_column_out& o = cols[a.n_keys + u];
     o.type = a.uda_out_type[u];
     o.length = rows;
+    if (skip && skip[a.n_keys + u] && !synth) continue;  // left without buffers (the caller fetches it otherwise)
     const bool q = a.uda_kind[u] == PXG_UDA_QUANTILES;
     const size_t per = q ? 56 : 8;
     o.values = ResultAlloc(std::max<size_t>(rows * per, 8));

@@ -790,6 +790,8 @@ class ExecNode {
   // Whether this node can observe the value of input column `col` (conservative default).
   // Lets a producer skip rendering a column no consumer reads.
   virtual bool ReadsColumnValue(size_t /*col*/) const { return true; }
+  // Quantile lanes (bit k = kQuantileKeys[k]) this node plucks from input column col.
+  virtual uint32_t PluckedLanes(size_t /*col*/) const { return 0x7Fu; }
   const RowDescriptor& output_descriptor() const { return output_; }
   const std::vector<std::pair<ExecNode*, size_t>>& children() const { return children_; }
   virtual std::string DebugString() const = 0;
@@ -1359,21 +1361,50 @@ class GpuAggNode : public ExecNode {
     }
     clk.Mark("agg finalize");
     std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
-    PXG_CALL(pxg_agg_result(agg_, out.data(), static_cast<int32_t>(out.size())));
+    // A quantiles column no consumer reads as a string (the pluck-only C2 shape) is not copied
+    // out: only the plucked lanes and a per-group finiteness flag come back (pluck on the device).
+    std::vector<uint8_t> skip(out.size(), 0);
+    std::vector<uint32_t> lanes(out.size(), 0);
+    quantiles_raw_.clear();
+    quantile_lanes_.clear();
+    for (size_t c = keys.size(); c < out.size() && !emit_states; ++c) {
+      if (udas[c - keys.size()].kind != PXG_UDA_QUANTILES) continue;
+      bool observed = false;
+      for (auto& ch : children_) {
+        observed = observed || ch.first->ReadsColumnValue(c);
+        lanes[c] |= ch.first->PluckedLanes(c);
+      }
+      skip[c] = observed ? 0 : 1;
+    }
+    PXG_CALL(pxg_agg_result_skip(agg_, out.data(), static_cast<int32_t>(out.size()), skip.data()));
+    const int64_t G = out.empty() ? 0 : out[0].length;
+    for (size_t c = 0; c < out.size(); ++c) {
+      if (!skip[c] || groups == 0) continue;
+      QuantLanes ql;
+      ql.mask = lanes[c] & 0x7Fu;
+      ql.nsel = __builtin_popcount(ql.mask);
+      double* vals = nullptr;
+      ql.vals = PooledDoubleColumn(G * ql.nsel, &vals);
+      void* fb = pxg_host_alloc(G + 16);
+      if (!fb) return Err(PXG_RESOURCE_UNAVAILABLE, "host buffer of %lld bytes", (long long)G);
+      ql.finite = std::shared_ptr<void>(fb, [](void* q) { pxg_host_free(q); });
+      PXG_CALL(pxg_agg_quantile_lanes(agg_, static_cast<int32_t>(c - keys.size()), ql.mask, vals, static_cast<uint8_t*>(fb)));
+      quantile_lanes_[c] = ql;
+    }
     clk.Mark("agg result D2H");
     RowBatch ob;
-    ob.num_rows = out.empty() ? 0 : out[0].length;
+    ob.num_rows = G;
     for (size_t c = 0; c < out.size(); ++c) {
       const bool q = !emit_states && c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
+      if (q && skip[c]) {  // G empty strings keep the batch's relation
+        pxg_result_free(&out[c], 1);
+        ob.cols.push_back(EmptyStringColumn(out[c].length));
+        continue;
+      }
       HostColumn hc = FromOut(out[c]);
       if (q) {  // QuantilesUDA::Finalize JSON (math_sketches.h:40-54) from the 7 device doubles
         quantiles_raw_[c] = hc;
-        bool observed = false;
-        for (auto& ch : children_) observed = observed || ch.first->ReadsColumnValue(c);
-        // A column no consumer reads as a string (the pluck-only C2 shape) stays unrendered:
-        // G empty strings keep the batch's relation.
-        ob.cols.push_back(observed ? RenderQuantilesJson(static_cast<const double*>(hc.values), hc.length)
-                                   : EmptyStringColumn(hc.length));
+        ob.cols.push_back(RenderQuantilesJson(static_cast<const double*>(hc.values), hc.length));
       } else {
         ob.cols.push_back(hc);
       }
@@ -1389,8 +1420,16 @@ class GpuAggNode : public ExecNode {
   }
 
  public:
-  // Raw 7-double quantile columns of the last emitted batch (post-agg pluck reads them).
+  // Raw 7-double quantile columns of the last emitted batch (post-agg pluck reads them), and
+  // for pluck-only columns the plucked lanes fetched on the device instead.
   std::map<size_t, HostColumn> quantiles_raw_;
+  struct QuantLanes {
+    uint32_t mask = 0;
+    int nsel = 0;
+    HostColumn vals;               // G * nsel doubles, lanes in bit order
+    std::shared_ptr<void> finite;  // G bytes: all 7 quantiles finite
+  };
+  std::map<size_t, QuantLanes> quantile_lanes_;
 
   // The device aggregation this node would run, handed to the caller (pxc_plan_create_agg).
   Status CreateDeviceAgg(pxg_ctx* ctx, int64_t expected_groups, pxg_agg** out) {
@@ -1582,6 +1621,14 @@ class PostAggMapNode : public ExecNode {
   explicit PostAggMapNode(GpuAggNode* agg) : agg_(agg) {}
   // A quantiles column is read as a string only when some expression does more than pluck it.
   bool ReadsColumnValue(size_t col) const override { return string_reads_.count(col) > 0; }
+  uint32_t PluckedLanes(size_t col) const override {
+    uint32_t m = 0;
+    for (auto& pk : plucks_)
+      if (pk.first == static_cast<int64_t>(col))
+        for (int k = 0; k < 7; ++k)
+          if (pk.second == kQuantileKeys[k]) m |= 1u << k;
+    return m;
+  }
   std::string DebugString() const override { return "PostAggMapNode(device map over the aggregate rows)"; }
 
   // Rewrites one expression (pluck_float64 leaves -> extra columns) and compiles it.
@@ -1659,10 +1706,17 @@ class PostAggMapNode : public ExecNode {
       double* v = nullptr;
       HostColumn vc = PooledDoubleColumn(G, &v);
       auto it = agg_ ? agg_->quantiles_raw_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantiles_raw_.end()){};
+      auto lt = agg_ ? agg_->quantile_lanes_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantile_lanes_.end()){};
       int qk = -1;
       for (int k = 0; k < 7; ++k)
         if (pk.second == kQuantileKeys[k]) qk = k;
-      if (agg_ && it != agg_->quantiles_raw_.end()) {
+      if (agg_ && lt != agg_->quantile_lanes_.end()) {  // plucked on the device
+        const auto& ql = lt->second;
+        const double* d = static_cast<const double*>(ql.vals.values);
+        const uint8_t* fin = static_cast<const uint8_t*>(ql.finite.get());
+        const int at = qk >= 0 && ((ql.mask >> qk) & 1u) ? __builtin_popcount(ql.mask & ((1u << qk) - 1)) : -1;
+        for (int64_t g = 0; g < G; ++g) v[g] = (at >= 0 && fin[g]) ? d[g * ql.nsel + at] : 0.0;
+      } else if (agg_ && it != agg_->quantiles_raw_.end()) {
         // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
         // fails to parse: pluck_float64 returns 0.0 for every key of that group.  The per-group
         // finiteness is computed once per raw column (C2 plucks two keys of one column).

@@ -12,6 +12,7 @@ from kat import case_plan, case_tables, check_case_output, expected_rows, load_k
 from pixie_amd import host_engine as H
 from pixie_amd import planpb
 from pixie_amd import plans as P
+from pixie_amd.device import Column
 
 KAT = load_kat()
 HTTP = {"http_events": {"types": P.HTTP_TYPES, "batches": []}}
@@ -437,3 +438,31 @@ def test_engine_limit_stops_the_source(engine):
     assert [(len(b["cols"][0]), b["eow"], b["eos"]) for b in dev] == [(len(b["cols"][0]), b["eow"], b["eos"]) for b in ref]
     assert sum(len(b["cols"][0]) for b in dev) == 5000 and dev[-1]["eos"]
     assert [rows(b["cols"]) for b in dev] == [rows(b["cols"]) for b in ref]
+
+
+@pytest.mark.gpu
+def test_engine_device_pluck_nan_quantiles_and_unplucked_keys(engine):
+    """Pluck on the device (pxg_agg_quantile_lanes): a group with a NaN value has NaN quantiles,
+    whose reference JSON is truncated, so every pluck of that group is 0.0; a pluck of a key the
+    JSON lacks is 0.0; plucks of the same column share one lane fetch."""
+    nan = float("nan")
+    keys = ["a"] * 5 + ["b"] * 3 + ["c"] * 4
+    vals = [1.0, 2.0, 3.0, 4.0, 5.0, 1.0, nan, 2.0, -1.5, 0.25, 7.0, 7.0]
+    types = [5, 4]
+    agg = P.agg_op([0], [P.agg_expr("quantiles", [P.col(1)], [4]), P.agg_expr("count", [P.col(1)], [4], fid=1)])
+    pl = P.map_op([P.col(0), P.col(2),
+                   P.func("pluck_float64", [P.col(1), P.const(5, "p50")], [5, 5], fid=5),
+                   P.func("pluck_float64", [P.col(1), P.const(5, "p99")], [5, 5], fid=6),
+                   P.func("pluck_float64", [P.col(1), P.const(5, "p42")], [5, 5], fid=7),
+                   P.func("pluck_float64", [P.col(1), P.const(5, "p01")], [5, 5], fid=8)],
+                  ["k", "n", "p50", "p99", "p42", "p01"])
+    plan = P.linear_plan([P.source_op("t", types, ["k", "v"], [0, 1]), agg, pl, P.sink_op("out")])
+    tables = {"t": {"types": types, "batches": [[Column.from_values(5, keys), Column.from_values(4, vals)]]}}
+    ref = sorted(rows(oc.execute_plan(plan, tables)["out"][0]["cols"]))
+    dev = sorted(rows(engine.execute(plan, tables)["out"][0]["cols"]))
+    assert len(ref) == len(dev) == 3
+    for r, d in zip(ref, dev):
+        assert r[:2] == d[:2]
+        for a, b in zip(r[2:], d[2:]):
+            assert ulp_diff(a, b) <= 4, (r, d)
+    assert dict((d[0], d[2:]) for d in dev)["b"] == (0.0, 0.0, 0.0, 0.0)
