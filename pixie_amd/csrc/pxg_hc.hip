@@ -31,7 +31,7 @@
 namespace pxg {
 
 constexpr int kHcBlock = 256;
-constexpr int kHcTable = 1024;  // LDS entries per partition (records per partition average <= 256)
+constexpr int kHcTable = 1024;  // LDS entries per partition (~1024 records, ~300-400 groups at C3)
 constexpr int kHcMaxAcc = 4;
 constexpr int kHcKeyWords = 1 + kMaxKeys * kHcStrWords;
 constexpr int kHcRecsLog2 = 10;  // partitions are sized for ~2^kHcRecsLog2 records (<= ~400 groups)
