@@ -1145,6 +1145,16 @@ static HostColumn RenderQuantilesJson(const double* d, int64_t G) {
 // Filter / Map chain in front of it, `filter` and the substituted key / argument programs
 // evaluate that chain inside the consume kernel.  Blocking: emits one batch at eos; windowed:
 // one batch per eow, then ClearAggState (agg_node.cc:169-180).
+// Pluck-only quantile columns fetched as their plucked lanes (pxg_agg_quantile_lanes);
+// PXC_DEVICE_PLUCK=0 copies the 7 doubles per group and plucks on the host instead.
+static bool DevicePluck() {
+  static const bool on = [] {
+    const char* e = std::getenv("PXC_DEVICE_PLUCK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 class GpuAggNode : public ExecNode {
  public:
   std::string DebugString() const override {
@@ -1374,7 +1384,7 @@ class GpuAggNode : public ExecNode {
         observed = observed || ch.first->ReadsColumnValue(c);
         lanes[c] |= ch.first->PluckedLanes(c);
       }
-      skip[c] = observed ? 0 : 1;
+      skip[c] = observed || !DevicePluck() ? 0 : 1;
     }
     PXG_CALL(pxg_agg_result_skip(agg_, out.data(), static_cast<int32_t>(out.size()), skip.data()));
     const int64_t G = out.empty() ? 0 : out[0].length;
