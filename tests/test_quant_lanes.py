@@ -19,7 +19,10 @@ def test_quantile_lanes_match_full_result(ctx):
     n = 20_000
     keys = [f"g{int(i)}" for i in rng.integers(0, 300, n)]
     vals = rng.lognormal(0.0, 1.0, n)
-    vals[rng.integers(0, n, 40)] = np.nan          # some groups get NaN quantiles
+    vals[rng.integers(0, n, 40)] = np.nan          # skipped by the digest
+    karr = np.array(keys)
+    vals[karr == "g7"] = np.inf                     # every quantile of g7 is infinite
+    vals[(karr == "g8") & (rng.random(n) < 0.5)] = -np.inf
     plan = P.linear_plan([P.source_op("t", [5, 4], ["k", "v"], [0, 1]),
                           P.agg_op([0], [P.agg_expr("count", [P.col(1)], [4]), P.agg_expr("quantiles", [P.col(1)], [4], fid=1)]),
                           P.sink_op("out")])
