@@ -323,6 +323,8 @@ typedef struct {
                                full sort path (NaN values, a gathered bin > 16384 values) */
   int32_t hc_mode;          /* 1: this run stages partition records (high-cardinality mode) */
   int32_t hc_partition_bits;/* last high-cardinality finalize: log2 of its partition count */
+  int32_t hc_reruns;        /* last high-cardinality finalize: partition passes rerun because a
+                               partition's distinct keys overflowed its LDS table */
 } pxg_agg_stats;
 int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* stats);
 

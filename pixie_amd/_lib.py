@@ -72,7 +72,8 @@ class JoinSpec(C.Structure):
 class AggStats(C.Structure):
     _fields_ = [("table_capacity", C.c_int64), ("groups", C.c_int64), ("rows_selected", C.c_int64),
                 ("key_arena_bytes", C.c_int64), ("staging_capacity", C.c_int64), ("fast_path_keys", C.c_int32),
-                ("big_sort_groups", C.c_int32), ("hc_mode", C.c_int32), ("hc_partition_bits", C.c_int32)]
+                ("big_sort_groups", C.c_int32), ("hc_mode", C.c_int32), ("hc_partition_bits", C.c_int32),
+                ("hc_reruns", C.c_int32)]
 
 
 # Every symbol include/pxg.h declares (checked by tests/test_abi.py).

@@ -1430,6 +1430,7 @@ extern "C" int32_t pxg_agg_info(pxg_agg* agg, pxg_agg_stats* st) {
   st->big_sort_groups = static_cast<int32_t>(a.last_big_sort_groups);
   st->hc_mode = a.hc_active ? 1 : 0;
   st->hc_partition_bits = a.last_hc_pbits;
+  st->hc_reruns = a.last_hc_reruns;
   return PXG_OK;
 }
 

@@ -83,6 +83,7 @@ struct Agg {
   uint64_t hc_cap = 0;
   uint64_t hc_n = 0;  // host mirror of the record cursor (counters @48)
   int32_t last_hc_pbits = 0;  // partition bits of the last finalize (pxg_agg_stats)
+  int32_t last_hc_reruns = 0; // partition passes the last finalize reran (pxg_agg_stats)
   int32_t EnsureHc(uint64_t need);
   bool HcNext() const;     // would the next run after a reset be high-cardinality?
   int32_t FinalizeHc();

@@ -2472,6 +2472,13 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
   const int64_t G = a.res.n_groups;
   const bool synth = a.n_keys == 0 && G == 0;  // AggregateGroupByNone over no rows
   const int64_t rows = synth ? 1 : G;
+  // The copies below are queued into pooled pinned blocks: an early error return must not leave
+  // one in flight, or the caller's pxg_result_free could hand a block to the next query while a
+  // DMA still writes into it.
+  struct DrainOnExit {
+    hipStream_t s;
+    ~DrainOnExit() { (void)hipStreamSynchronize(s); }
+  } drain{a.ctx->stream};
   for (int c = 0; c < n_cols; ++c) std::memset(&cols[c], 0, sizeof(cols[c]));
   for (int k = 0; k < a.n_keys; ++k) {
     pxg_column_out& o = cols[k];

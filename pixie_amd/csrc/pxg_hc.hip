@@ -34,17 +34,22 @@ constexpr int kHcBlock = 256;
 constexpr int kHcTable = 1024;  // LDS entries per partition (~1024 records, ~300-400 groups at C3)
 constexpr int kHcMaxAcc = 4;
 constexpr int kHcKeyWords = 1 + kMaxKeys * kHcStrWords;
-constexpr int kHcRecsLog2 = 10;  // partitions are sized for ~2^kHcRecsLog2 records (<= ~400 groups)
+constexpr int kHcGroupsLog2 = 9;  // the first pass sizes partitions for ~2^kHcGroupsLog2 groups (~50 % table fill)
 
-enum HcAccOp : int32_t { kHcAdd = 0, kHcMin = 1, kHcMax = 2 };
+// kHcAddWide: an exact 128-bit two's-complement sum (low word in the accumulator, high word in
+// its acc_hi array), for MEAN over INT64: MeanUDA accumulates `double sum += arg`
+// (math_ops.h:586-589), which cannot wrap, so a 64-bit integer sum that passes 2^63 must not
+// either.
+enum HcAccOp : int32_t { kHcAdd = 0, kHcMin = 1, kHcMax = 2, kHcAddWide = 3 };
 
 struct HcAggPlan {
   uint64_t n;  // records (the distance between two sorted record streams)
-  int32_t stride, kwords, nk, n_udas, nacc;
+  int32_t stride, kwords, nk, n_udas, nacc, nhi;
   int32_t ktype[kMaxKeys], koff[kMaxKeys];
   int32_t uda_kind[kMaxUdas], uda_acc[kMaxUdas];
   int64_t uda_init[kMaxUdas];
   int32_t acc_op[kHcMaxAcc], acc_word[kHcMaxAcc];
+  int32_t acc_hi[kHcMaxAcc];  // kHcAddWide: LDS array of the high words (nacc + j), else -1
 };
 
 struct HcOut {
@@ -102,9 +107,17 @@ __device__ __forceinline__ void HcEmitKeys(const HcAggPlan& hp, const HcOut& out
   }
 }
 
+// The 128-bit two's-complement integer hi:lo as a double.  Inside the int64 range it is the
+// int64's conversion (exact rounding); beyond it |x| >= 2^63, so the two-term sum's rounding
+// error stays within a few ulps (no cancellation).
+__device__ __forceinline__ double WideToDouble(int64_t hi, uint64_t lo) {
+  const bool fits = (hi == 0 && static_cast<int64_t>(lo) >= 0) || (hi == -1 && static_cast<int64_t>(lo) < 0);
+  return fits ? static_cast<double>(static_cast<int64_t>(lo)) : static_cast<double>(hi) * 18446744073709551616.0 + static_cast<double>(lo);
+}
+
 // One group's UDA outputs (UDA Finalize, math_ops.h CountUDA / SumUDA / MeanUDA / MinUDA /
-// MaxUDA).  MEAN over integer arguments divides the exact integer sum (the reference accumulates
-// the same values in a double; both agree to rounding).
+// MaxUDA).  MEAN over integer arguments divides the exact 128-bit integer sum (the reference
+// accumulates the same values in a double; both agree to rounding, and neither wraps).
 __device__ __forceinline__ void HcEmitVals(const HcAggPlan& hp, const HcOut& out, uint32_t g, uint32_t cnt, const unsigned long long* s_acc,
                                            int slot) {
   for (int u = 0; u < hp.n_udas; ++u) {
@@ -113,7 +126,12 @@ __device__ __forceinline__ void HcEmitVals(const HcAggPlan& hp, const HcOut& out
     uint64_t v;
     switch (hp.uda_kind[u]) {
       case PXG_UDA_COUNT: v = cnt; break;
-      case PXG_UDA_MEAN: v = FBits(static_cast<double>(static_cast<int64_t>(acc)) / static_cast<double>(cnt)); break;
+      case PXG_UDA_MEAN: {
+        const int hi = a >= 0 ? hp.acc_hi[a] : -1;
+        const int64_t h = hi >= 0 ? static_cast<int64_t>(s_acc[hi * kHcTable + slot]) : (static_cast<int64_t>(acc) >> 63);
+        v = FBits(WideToDouble(h, acc) / static_cast<double>(cnt));
+        break;
+      }
       case PXG_UDA_SUM:
       case PXG_UDA_MINSUM: v = acc + static_cast<uint64_t>(hp.uda_init[u]); break;
       default: v = acc; break;  // MIN / MAX (integer)
@@ -180,7 +198,7 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
   extern __shared__ unsigned long long s_dyn[];
   unsigned long long* s_ent = s_dyn;                                  // [kHcTable]: tag << 32 | rep record
   unsigned long long* s_acc = s_dyn + kHcTable;                       // [nacc][kHcTable]
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn + kHcTable * (1 + hp.nacc));  // [kHcTable]
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_dyn + kHcTable * (1 + hp.nacc + hp.nhi));  // [kHcTable]
   constexpr int kWaves = kHcBlock / 64;
   constexpr int kPerThr = kHcTable / kHcBlock;
   __shared__ uint32_t s_wsum[kWaves];
@@ -194,6 +212,7 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
       s_ent[t] = 0;
       s_cnt[t] = 0;
       for (int a = 0; a < hp.nacc; ++a) s_acc[a * kHcTable + t] = HcAccInit(hp.acc_op[a]);
+      for (int a = 0; a < hp.nhi; ++a) s_acc[(hp.nacc + a) * kHcTable + t] = 0;
     }
     if (threadIdx.x == 0) s_ovf = 0;
     __syncthreads();
@@ -264,8 +283,14 @@ __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint
         for (int q = 0; q < kHcR; ++q) {
           if (!live[q] || slot[q] < 0) continue;
           unsigned long long* dst = &s_acc[a * kHcTable + slot[q]];
-          if (op == kHcAdd) atomicAdd(dst, x[q]);
-          else if (op == kHcMin) atomicMin(reinterpret_cast<long long*>(dst), static_cast<long long>(x[q]));
+          if (op == kHcAdd) {
+            atomicAdd(dst, x[q]);
+          } else if (op == kHcAddWide) {
+            // low word, then the carry out of it plus the sign extension of x into the high word
+            const unsigned long long old = atomicAdd(dst, x[q]);
+            const unsigned long long inc = static_cast<unsigned long long>(static_cast<int64_t>(x[q]) >> 63) + (old + x[q] < old ? 1ULL : 0ULL);
+            if (inc) atomicAdd(&s_acc[hp.acc_hi[a] * kHcTable + slot[q]], inc);
+          } else if (op == kHcMin) atomicMin(reinterpret_cast<long long*>(dst), static_cast<long long>(x[q]));
           else atomicMax(reinterpret_cast<long long*>(dst), static_cast<long long>(x[q]));
         }
       }
@@ -412,9 +437,10 @@ static HcAggPlan MakeHcPlan(const Agg& a, bool compact = false, int32_t* src = n
     if (kind == PXG_UDA_COUNT) continue;
     const int i = hp.nacc++;
     hp.uda_acc[u] = i;
-    hp.acc_op[i] = kind == PXG_UDA_MIN ? kHcMin : (kind == PXG_UDA_MAX ? kHcMax : kHcAdd);
+    hp.acc_op[i] = kind == PXG_UDA_MIN ? kHcMin : (kind == PXG_UDA_MAX ? kHcMax : (kind == PXG_UDA_MEAN ? kHcAddWide : kHcAdd));
     hp.acc_word[i] = hp.kwords + a.uda_val[u];
   }
+  for (int i = 0; i < hp.nacc; ++i) hp.acc_hi[i] = hp.acc_op[i] == kHcAddWide ? hp.nacc + hp.nhi++ : -1;
   return hp;
 }
 
@@ -466,15 +492,22 @@ int32_t Agg::FinalizeHc() {
     out.kscr = w.hc_kscr.as<uint64_t>();
   }
   out.g0 = g0;
-  const size_t lds = static_cast<size_t>(kHcTable) * (8 + 8 * hp.nacc + 4);
+  const size_t lds = static_cast<size_t>(kHcTable) * (8 + 8 * (hp.nacc + hp.nhi) + 4);
   uint32_t* meta = w.hc_meta.as<uint32_t>();
   uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 192);
+  // The first pass aims at ~2^kHcGroupsLog2 groups per partition (a half-full LDS table) from
+  // the expected group count: the hint or the last run (both count every group), else the
+  // records (all distinct).  Sizing by records alone gave ~1024 groups per partition for
+  // near-unique keys, i.e. about half the partitions overflowed and the pass ran twice.
+  uint64_t est = std::max<uint64_t>(last_groups, hint_groups > 0 ? static_cast<uint64_t>(hint_groups) : 0);
+  if (est == 0 || est > n) est = n;
   int pbits = 1;
-  while (pbits < 28 && (n >> (pbits + kHcRecsLog2)) > 0) ++pbits;
+  while (pbits < 28 && (est >> (pbits + kHcGroupsLog2)) > 0) ++pbits;
   const char* fe = std::getenv("PXG_HC_PBITS");  // tests: the first pass's partition count
   const int forced = fe ? std::atoi(fe) : 0;
   if (forced > 0 && forced <= 28) pbits = forced;
   uint32_t G = 0;
+  last_hc_reruns = 0;
   for (;;) {
     const uint32_t P = 1u << pbits;
     const int shift = 32 - pbits;
@@ -495,6 +528,7 @@ int32_t Agg::FinalizeHc() {
     if (pin[1] == 0) break;
     if (pbits >= 28) return SetError(PXG_INTERNAL, "high-cardinality partitions overflow their LDS tables at 2^28 partitions");
     pbits = std::min(28, pbits + 2);
+    ++last_hc_reruns;
   }
   last_hc_pbits = pbits;
   // String keys: lengths -> offsets (scan), then the bytes.
@@ -503,8 +537,14 @@ int32_t Agg::FinalizeHc() {
   std::memset(&kc, 0, sizeof(kc));
   for (int k = 0; k < n_keys; ++k) {
     if (key_types[k] != PXG_STRING) continue;
-    any_str = true;
     uint32_t* off = R.key_offsets[k].as<uint32_t>() + g0;
+    if (G == 0) {
+      // No partition groups (e.g. every staged key was long and took the table path): the
+      // offsets end where the table path's bytes end.
+      PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(off), static_cast<int>(dbase[k]), 1, ctx->stream));
+      continue;
+    }
+    any_str = true;
     PXG_RETURN_IF_ERROR(w.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(G) + 1) + 64));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, off, off, G, off + G, w.scan.p));
     kc.off[k] = off;
@@ -637,6 +677,7 @@ int32_t Agg::SpillHc() {
   PXG_RETURN_IF_ERROR(EnsureStage(st_n + n));
   uint8_t* cb = counters.as<uint8_t>();
   PXG_HIP(hipMemsetAsync(cb + 36, 0, 4, ctx->stream));
+  PXG_HIP(hipMemsetAsync(cb + 48, 0, 8, ctx->stream));  // the record cursor, mirrored into hc_n by PublishNew
   StageDev stg;
   std::memset(&stg, 0, sizeof(stg));
   for (int v = 0; v < n_vals; ++v) stg.vals[v] = st_val[v].as<uint64_t>();

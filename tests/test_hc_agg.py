@@ -253,3 +253,84 @@ def test_all_empty_and_short_string_keys(ctx, hc_env):
         ref = oc.execute_plan(plan, tables)["out"][0]["cols"]
         dev = run_plan(ctx, plan, tables, expected_groups=5000)[0]["cols"]
         assert rows_match(rows(dev), rows(ref), ordered=False, tol_ulp=0), gcols
+
+
+def _agg_hc(ctx, plan, tables, hint):
+    """run_plan through one agg, returning (cols, info) so a test can see which mode ran."""
+    src = plan.nodes[0].nodes[0].op.mem_source_op
+    tin = tables[src.name]
+    q = LinearQuery(plan, tin["types"], expected_groups=hint)
+    t = Table(ctx, tin["types"])
+    for b in tin["batches"]:
+        t.append(b)
+    t.flush()
+    a = q.make_agg(ctx)
+    a.consume(t)
+    info = a.info()
+    a.finalize()
+    cols = q.emit(a.result())
+    a.close()
+    t.close()
+    return cols, info
+
+
+def test_int64_mean_past_2_63_does_not_wrap(ctx, hc_env):
+    """MeanUDA accumulates `double sum += arg` (math_ops.h:586-589), so a group whose INT64 sum
+    passes 2^63 still has the right mean.  The partition tables sum MEAN arguments as exact
+    128-bit integers; the table path sums doubles: both must match the oracle, and each other.
+    (SUM over INT64 wraps in the reference, and here, bit-exactly.)"""
+    rng = np.random.default_rng(62)
+    ngroups = 6000
+    sizes = rng.integers(2, 9, ngroups)
+    gid = np.repeat(np.arange(ngroups), sizes)
+    rng.shuffle(gid)
+    n = len(gid)
+    sign = np.where(np.arange(ngroups) % 3 == 0, -1, 1)  # a third of the groups all negative
+    mag = (1 << 62) - rng.integers(0, 1 << 40, n)
+    v = [int(sign[g]) * int(m) for g, m in zip(gid, mag)]
+    keys = [f"g{int(g):05d}" for g in gid]
+    types = [5, 2]
+    plan = P.linear_plan([P.source_op("t", types, ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("mean", [P.col(1)], [2]), P.agg_expr("sum", [P.col(1)], [2], fid=1),
+                                         P.agg_expr("count", [P.col(1)], [2], fid=2)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": types, "batches": [[Column.from_values(5, keys), Column.from_values(2, v)]]}}
+    R = _by_key(oc.execute_plan(plan, tables)["out"][0]["cols"], 1)
+    hc_cols, hc_info = _agg_hc(ctx, plan, tables, 5000)
+    assert hc_info["hc_mode"] == 1, hc_info
+    H = _by_key(hc_cols, 1)
+    hc_env.setenv("PXG_NO_HC", "1")
+    tb_cols, tb_info = _agg_hc(ctx, plan, tables, 5000)
+    assert tb_info["hc_mode"] == 0, tb_info
+    T = _by_key(tb_cols, 1)
+    assert set(R) == set(H) == set(T) and len(R) == ngroups
+    wrapped = 0
+    for k, (mean, s, c) in R.items():
+        assert H[k][1:] == (s, c) and T[k][1:] == (s, c), k  # sum wraps identically, counts exact
+        assert abs(H[k][0] - mean) <= 1e-9 * abs(mean), (k, H[k][0], mean)
+        assert abs(T[k][0] - mean) <= 1e-9 * abs(mean), (k, T[k][0], mean)
+        assert abs(H[k][0] - T[k][0]) <= 1e-12 * abs(mean), k
+        wrapped += (mean > 0) != (s > 0)
+    assert wrapped > 1000  # most groups' 64-bit sums wrapped; the means did not
+
+
+def test_every_key_long_leaves_no_partition_groups(ctx, hc_env):
+    """All STRING keys longer than the records hold: every staged record is a hole, the
+    partition pass finds no group, and the table path's groups and key offsets stand alone."""
+    rng = np.random.default_rng(24)
+    n = 20_000
+    pool = ["K" * 30 + f"{i:05d}" for i in range(700)]
+    keys = [pool[i] for i in rng.integers(0, len(pool), n)]
+    v = rng.integers(-1000, 1000, n)
+    types = [5, 2]
+    plan = P.linear_plan([P.source_op("t", types, ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("count", [P.col(1)], [2]), P.agg_expr("sum", [P.col(1)], [2], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": types, "batches": [[Column.from_values(5, keys), Column.from_values(2, v.tolist())]]}}
+    ref = oc.execute_plan(plan, tables)["out"][0]["cols"]
+    cols, info = _agg_hc(ctx, plan, tables, 5000)
+    assert info["hc_mode"] == 1, info
+    off = cols[0].offsets if hasattr(cols[0], "offsets") else None
+    if off is not None:
+        assert list(off)[-1] == sum(len(s) for s in cols[0].to_list())
+    assert rows_match(rows(cols), rows(ref), ordered=False, tol_ulp=0)
