@@ -40,7 +40,8 @@ KERNELS = ["agg_consume", "agg_publish_sizes", "agg_publish_write", "finalize_in
            "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",
            "export_slot_part", "export_group_rank", "export_row_digit", "export_write_groups", "export_write_rows",
            "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows",
-           "hc_part_starts", "hc_agg", "hc_key_copy", "hc_spill"]
+           "hc_part_starts", "hc_agg", "hc_key_copy", "hc_spill",
+           "split_sample", "split_ids", "split_hist", "split_scan", "split_scatter"]
 
 
 def parse():
@@ -78,6 +79,11 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="shard processes of the supplementary CPU baseline (SURVEY.md §8d: P PEMs + merge); "
                          "16 = the GPU box's CPU share; 0 disables")
+    ap.add_argument("--cpu-timing-rows", type=int, default=25_000_000,
+                    help="rows of the pinned 1-core CPU baseline sample (median of --cpu-timing-reps runs after a warm-up)")
+    ap.add_argument("--cpu-timing-reps", type=int, default=5)
+    ap.add_argument("--cpu-timing-child", type=int, nargs=3, default=None, metavar=("ROWS", "REPS", "BATCH"),
+                    help=argparse.SUPPRESS)  # internal: the pinned CPU baseline process
     ap.add_argument("--cpu-shard-child", type=int, nargs=3, default=None, metavar=("ROW0", "ROWS", "BATCH"),
                     help=argparse.SUPPRESS)  # internal: one shard process of the parallel CPU baseline
     return ap.parse_args()
@@ -167,6 +173,9 @@ def main():
     args = parse()
     if args.pmc_child:
         pmc_child(args.pmc_child)
+        return
+    if args.cpu_timing_child:
+        cpu_timing_child(*args.cpu_timing_child)
         return
     if args.cpu_shard_child:
         cpu_shard_child(*args.cpu_shard_child)
@@ -561,7 +570,7 @@ def c5_leg(args, engine, ctx, P, reps=5):
         ctx.reset_stats()
         ctx.set_profiling(True)
         times = []
-        res = b""
+        res_len = 0
         for _ in range(reps):
             tq = time.perf_counter()
             res_len = engine.execute_bytes_len(pb)
@@ -577,7 +586,7 @@ def c5_leg(args, engine, ctx, P, reps=5):
         out = {"workload": "C5: conn_stats bin(time_, 10s) x (upid, remote_addr) sum(bytes_sent), sum(bytes_recv), "
                            "inner equijoin on upid to pod_metadata (pxc_execute_plan over stored tables)",
                "rows": n, "queries": reps, "ms_per_query": sum(times) * 1000 / reps, "ms_median": st[len(st) // 2] * 1000,
-               "ms_min": st[0] * 1000, "value": n * reps / sum(times), "unit": "rows/s", "result_bytes": len(res),
+               "ms_min": st[0] * 1000, "value": n * reps / sum(times), "unit": "rows/s", "result_bytes": int(res_len),
                "kernel_ms_per_query": kms, "algorithmic_bytes_per_row": alg / n,
                "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": alg / (avg / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS, "avg_launch_ms": avg},
@@ -664,6 +673,21 @@ def n1_leg(args, ctx, P, Table, plan_agg):
 
     g = step()
     ctx.sync()
+    # Per-kernel breakdown of the 1B-row step from one untimed, fully event-bracketed step
+    # (sum of launch durations per kernel name; finalize runs on three streams, so the kernels
+    # overlap and their sum exceeds the step's span).
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    t_prof = time.perf_counter()
+    step()
+    ctx.sync()
+    prof_step_ms = (time.perf_counter() - t_prof) * 1000.0
+    ctx.set_profiling(False)
+    kernel_ms = {}
+    for name in KERNELS:
+        l, ms = ctx.kernel_stats(name)
+        if l:
+            kernel_ms[name] = round(ms, 4)
     ctx.reset_stats()
     ctx.set_profiling(True, only="agg_consume")
     ctx.sync()
@@ -687,6 +711,8 @@ def n1_leg(args, ctx, P, Table, plan_agg):
         "rows": n, "steps": args.n1_steps, "ms_per_step": el * 1000.0 / args.n1_steps,
         "value": n * args.n1_steps / el, "unit": "rows/s", "groups": g, "selected_rows": a.rows_selected(),
         "algorithmic_bytes_per_row": alg / n, "generate_s": gen_s,
+        "kernel_ms_per_step": kernel_ms, "profiled_step_ms": round(prof_step_ms, 3),
+        "finalize_ms_per_step": round(el * 1000.0 / args.n1_steps - avg, 3),
         "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n),
                      "traffic_source": "committed file (replaced by the live PMC leg when it runs)", "algorithmic_bytes_per_launch": alg,
@@ -727,6 +753,41 @@ def cpu_shard_child(row0, rows, batch_rows):
     tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [batch], "names": P.HTTP_NAMES}}
     secs, res = oc.execute_plan_timed(P.c2_plan(with_pluck=False), tables, batch_rows=batch_rows)
     print(json.dumps({"secs": secs, "rows": rows, "groups": len(res["output"][0]["cols"][0])}), flush=True)
+
+
+def cpu_timing_child(rows, reps, batch_rows):
+    """The primary CPU baseline: this process pins itself to core 0 before it
+    builds anything, generates `rows` rows of the bench table, runs the C2 plan through the CPU
+    Carnot restatement once as a warm-up and `reps` more times, and prints every execution
+    window (first GenerateNext .. last emit)."""
+    os.sched_setaffinity(0, {0})
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_client as oc
+    from pixie_amd import plans as P
+    from pixie_amd.device import datagen_http_events
+    need = {P.HE["service"], P.HE["req_path"], P.HE["resp_status"], P.HE["latency"]}
+    cols = datagen_http_events(SEED, 0, rows, n_pair_keys=N_PAIR_KEYS, threads=1)
+    batch = [c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)]
+    tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [batch], "names": P.HTTP_NAMES}}
+    secs = []
+    for _ in range(reps + 1):
+        s, _res = oc.execute_plan_timed(P.c2_plan(with_pluck=False), tables, batch_rows=batch_rows)
+        secs.append(s)
+    print(json.dumps({"warmup_secs": secs[0], "secs": secs[1:], "rows": rows, "cpus": sorted(os.sched_getaffinity(0))}), flush=True)
+
+
+def cpu_timing_leg(args):
+    """Runs cpu_timing_child in a fresh interpreter (never a fork of this GPU process)."""
+    import subprocess
+    try:
+        kid = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-timing-child", str(args.cpu_timing_rows),
+                              str(args.cpu_timing_reps), str(args.cpu_batch_rows)], stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, timeout=900)
+        if kid.returncode != 0:
+            return {"error": f"cpu timing process exited {kid.returncode}"}
+        return json.loads(kid.stdout.decode().strip().splitlines()[-1])
+    except Exception as e:  # the legs must never break the bench line
+        return {"error": f"cpu timing leg failed: {e}"}
 
 
 def cpu_parallel_leg(args, n, row0):
@@ -798,6 +859,22 @@ def oracle_leg(args, n, row0, dev_result):
                          f"as {args.cpu_batch_rows}-row RowBatches, C2 plan (quantiles JSON, no pluck), 1 thread of "
                          f"{cpu_model or 'host CPU'}; {secs:.2f} s execution window (first GenerateNext .. last emit); "
                          f"CPU Carnot restated in oracle/ (reference unbuildable, SURVEY.md §8c)"}
+        # the primary number is the median of 5 runs after a warm-up, on core 0.
+        if args.cpu_timing_reps > 0:
+            tm = cpu_timing_leg(args)
+            if "secs" in tm and tm["secs"]:
+                med = sorted(tm["secs"])[len(tm["secs"]) // 2]
+                k = tm["rows"]
+                cpu = {"value": k / med, "unit": "rows/s", "cores": 1, "kind": "port",
+                       "sample": f"the first {k} rows of the bench table (bit-identical host regeneration) as {args.cpu_batch_rows}-row "
+                                 f"RowBatches, C2 plan (quantiles JSON, no pluck), one process pinned to core {tm['cpus']} of "
+                                 f"{cpu_model or 'host CPU'}: median of {len(tm['secs'])} execution windows after 1 warm-up "
+                                 f"({', '.join(f'{x:.2f}' for x in tm['secs'])} s; first GenerateNext .. last emit); "
+                                 f"CPU Carnot restated in oracle/ (reference unbuildable, SURVEY.md §8c)",
+                       "runs_s": tm["secs"], "warmup_s": tm["warmup_secs"],
+                       "full_table": {"rows": n, "secs": secs, "value": n / secs, "pinned": False}}
+            else:
+                cpu["timing_error"] = tm.get("error")
         par = None
         if dev_result is not None:
             ref = res["output"][0]["cols"]

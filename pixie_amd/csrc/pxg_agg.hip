@@ -454,7 +454,10 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
   return eq;
 }
 
-template <int NK, bool S = false>
+// TAGONLY: timing-only diagnostic (PXG_DIAG_CONSUME=1): a tag match is taken as the group without
+// the representative compare, which prices that compare (tools/consume_diag.py; wrong groups on
+// a tag collision, never followed by a checked finalize).
+template <int NK, bool S = false, bool TAGONLY = false>
 __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                                      const KeyCols<NK>* __restrict__ s_kc, uint32_t n_lds_chunks,
                                                      const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
@@ -488,6 +491,7 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
       w = expected;  // lost the race: the winner's word decides below
     }
     // Phase B: exact key comparison against the slot's representative.
+    if (TAGONLY && static_cast<uint32_t>(w >> 33) == tag) return pos;
     if (static_cast<uint32_t>(w >> 33) == tag) {
       const uint32_t ref = static_cast<uint32_t>(w);
       bool eq;
@@ -506,9 +510,9 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
   return kDeferredSlot;
 }
 
-// MODE: 0 = production; 2 / 3 are timing-only diagnostic builds that stop after the filter
-// (2) or after key load + hash (3) and write garbage slots (tools/consume_diag.py; never
-// followed by finalize).
+// MODE: 0 = production; 1 / 2 / 3 are timing-only diagnostic builds: 1 probes without the
+// representative compare (tag match = hit), 2 stops after the filter, 3 after key load + hash
+// (garbage slots; tools/consume_diag.py; never followed by a checked finalize).
 //
 // One workgroup per tile of rg.tile_rows rows (grid-stride).  Phase 1 runs in sub-batches of
 // kSubRows rows: every thread evaluates the predicate for 32 rows (32 independent loads in
@@ -734,7 +738,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          slot = FastFindOrInsert<NK, S>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
+          slot = FastFindOrInsert<NK, S, (MODE & 3) == 1>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -1075,8 +1079,8 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     KernFn kern = AggConsumeKernel;
     switch (fast_nk * 4 + (diag & 3)) {
 #define PXG_FAST_CASE(nk)                                           \
-  case nk * 4 + 0:                                                  \
-  case nk * 4 + 1: kern = AggConsumeFastKernel<nk, 0>; break;       \
+  case nk * 4 + 0: kern = AggConsumeFastKernel<nk, 0>; break;       \
+  case nk * 4 + 1: kern = all_str ? AggConsumeFastKernel<nk, 5> : AggConsumeFastKernel<nk, 1>; break; \
   case nk * 4 + 2: kern = AggConsumeFastKernel<nk, 2>; break;       \
   case nk * 4 + 3: kern = AggConsumeFastKernel<nk, 3>; break;
       PXG_FAST_CASE(1)

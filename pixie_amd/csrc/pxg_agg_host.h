@@ -117,6 +117,9 @@ struct Agg {
     RadixPassWs rs;
     // high-cardinality finalize
     DevBuf hc_k[2], hc_v[2], hc_starts, hc_kscr, hc_meta;
+    // staging split (pxg_finalize.hip): sampled slot counts, flag scan, bucket x tile counts,
+    // bucket totals / bases
+    DevBuf split_cnt, split_flags, split_hist, split_tot;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);

@@ -1901,6 +1901,402 @@ __global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Staging split (large aggregations).  Finalize only needs each group's records contiguous
+// (every reduction and digest below works on a group's range; the quantile kernels sort the
+// values they read).  The LSD radix sort gets that with two full passes over all records at
+// ~65K groups.  Here the groups a sample says are large ("designated", at most kSplitMaxBig)
+// are partitioned out of the staging in ONE counting pass, each into its own contiguous range,
+// and only the remaining records go through the radix sort: at the north_star size the
+// designated groups hold ~80 % of the records.  (The work replaced is agg_node.cc:273-349's
+// flush + per-group finalize; how records get grouped is this implementation's choice.)
+//
+// Group ids: the rest groups take [0, Gr) and the designated ones [Gr, G), both in slot order;
+// buckets: 0 = rest, 1 + j = designated group Gr + j, nd + 1 = records without a group.  The
+// final layout is [rest records sorted by id | designated records by id | no group], so gstart
+// stays monotone and every kernel after the grouping is unchanged.  A group the sample misses
+// goes through the sort; one it over-estimates is classified by its true count: the sample
+// decides the cost, never the result.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t kSplitStride = 128;    // every 128th staged record is sampled
+constexpr uint32_t kSplitMinRows = 8192;  // designate a group whose sampled estimate reaches this
+constexpr uint32_t kSplitMaxBig = 2046;   // rest + designated + no-group buckets <= kSplitBuckets
+constexpr int kSplitBuckets = 2048;
+constexpr int kSplitHash = 4096;          // LDS map designated slot -> bucket (<= 50 % full)
+constexpr uint32_t kSplitEmpty = 0xFFFFFFFFu;
+constexpr int kSplitBlock = 256;
+constexpr uint32_t kSplitTile = 32768;    // records per tile of the split's (bucket x tile) counts
+constexpr int kSplitItems = 8;            // scatter: records per thread per sub-tile
+constexpr int kSplitSub = kSplitBlock * kSplitItems;
+constexpr int kSampleTable = 4096;
+constexpr int kSamplePerThread = 16;
+
+// Sampled per-slot counts: each block aggregates 4096 samples in an LDS table, then adds its
+// distinct slots' counts to scnt (one global atomic per distinct slot per block, so a hot
+// group sees one per block, not one per sample).  A slot that finds no LDS entry within 32
+// probes is dropped: such a block met thousands of distinct cold slots, none of them large.
+__global__ void __launch_bounds__(256) SplitSampleKernel(const uint32_t* __restrict__ slot, uint64_t n, uint32_t cap,
+                                                         uint32_t* __restrict__ scnt) {
+  __shared__ uint32_t s_key[kSampleTable];
+  __shared__ uint32_t s_cnt[kSampleTable];
+  for (int i = threadIdx.x; i < kSampleTable; i += 256) {
+    s_key[i] = 0xFFFFFFFFu;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  const uint64_t j0 = static_cast<uint64_t>(blockIdx.x) * 256 * kSamplePerThread;
+  uint32_t sv[kSamplePerThread];
+#pragma unroll
+  for (int k = 0; k < kSamplePerThread; ++k) {
+    const uint64_t r = (j0 + static_cast<uint64_t>(k) * 256 + threadIdx.x) * kSplitStride;
+    sv[k] = r < n ? slot[r] : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int k = 0; k < kSamplePerThread; ++k) {
+    const uint32_t x = sv[k];
+    if (x >= cap) continue;
+    uint32_t h = (x * 0x9E3779B1u) >> 20;
+    for (int p = 0; p < 32; ++p) {
+      uint32_t cur = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (cur == 0xFFFFFFFFu) {
+        cur = atomicCAS(&s_key[h], 0xFFFFFFFFu, x);
+        if (cur == 0xFFFFFFFFu) cur = x;
+      }
+      if (cur == x) {
+        atomicAdd(&s_cnt[h], 1u);
+        break;
+      }
+      h = (h + 1) & (kSampleTable - 1);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSampleTable; i += 256)
+    if (s_cnt[i]) atomicAdd(&scnt[s_key[i]], s_cnt[i]);
+}
+
+// lvl[l] = occupied slots whose sample count has floor(log2) == l: the designation threshold
+// is raised by powers of two until at most kSplitMaxBig slots reach it, so the cap keeps the
+// largest groups rather than the first ones in slot order.
+__global__ void SplitLevelsKernel(const uint32_t* __restrict__ scnt, uint32_t cap, uint32_t* __restrict__ lvl) {
+  __shared__ uint32_t s_l[32];
+  if (threadIdx.x < 32) s_l[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = i < cap ? scnt[i] : 0u;
+  if (c) atomicAdd(&s_l[31 - __clz(c)], 1u);
+  __syncthreads();
+  if (threadIdx.x < 32 && s_l[threadIdx.x]) atomicAdd(&lvl[threadIdx.x], s_l[threadIdx.x]);
+}
+
+__device__ __forceinline__ uint32_t SplitThreshold(const uint32_t* __restrict__ lvl, uint32_t min_samples) {
+  uint32_t above = 0;  // slots with a count >= 2^(l + 1)
+  int L = 32;
+  for (int l = 31; l >= 0; --l) {
+    above += lvl[l];
+    if (above > kSplitMaxBig) break;
+    L = l;
+  }
+  const uint32_t p = L >= 32 ? 0xFFFFFFFFu : (1u << L);
+  return max(min_samples, p);
+}
+
+// flags[slot] = designated << 32 | occupied (one u64 scan gives both ranks).
+__global__ void SplitFlagsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
+                                 const uint32_t* __restrict__ lvl, uint32_t min_samples, uint64_t* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const uint32_t t = SplitThreshold(lvl, min_samples);
+  const bool occ = slots[i] != 0;
+  const bool des = occ && scnt[i] >= t;
+  flags[i] = (static_cast<uint64_t>(des) << 32) | static_cast<uint64_t>(occ);
+}
+
+__device__ __forceinline__ uint32_t SplitNd(const uint64_t* __restrict__ ftotal) {
+  return min(static_cast<uint32_t>(*ftotal >> 32), kSplitMaxBig);
+}
+
+// Group ids from the scanned flags: designated slots -> Gr + their rank, the rest -> their rank
+// among the rest; gslot[id] = slot (so gslot[Gr + j] lists the designated slots by bucket).
+__global__ void SplitIdsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
+                               const uint32_t* __restrict__ lvl, uint32_t min_samples, const uint64_t* __restrict__ fscan,
+                               const uint64_t* __restrict__ ftotal, uint32_t G, uint32_t* __restrict__ newid, uint32_t* __restrict__ gslot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap || slots[i] == 0) return;
+  const uint32_t t = SplitThreshold(lvl, min_samples);
+  const uint32_t nd = SplitNd(ftotal), Gr = G - nd;
+  const uint64_t f = fscan[i];
+  const uint32_t d_rank = static_cast<uint32_t>(f >> 32), o_rank = static_cast<uint32_t>(f);
+  const bool des = scnt[i] >= t && d_rank < kSplitMaxBig;
+  const uint32_t id = des ? Gr + d_rank : o_rank - min(d_rank, kSplitMaxBig);
+  newid[i] = id;
+  gslot[id] = i;
+}
+
+__device__ __forceinline__ uint32_t SplitHashPos(uint32_t s) { return (s * 0x9E3779B1u) >> 20; }
+static_assert(kSplitHash == 4096, "SplitHashPos yields 12 bits");
+
+// The block's LDS map designated slot -> bucket 1 + j, from gslot[Gr + j] (j < nd).
+__device__ __forceinline__ void SplitBuildMap(uint32_t* hk, uint16_t* hv, const uint32_t* __restrict__ gslot, uint32_t Gr, uint32_t nd) {
+  for (int i = threadIdx.x; i < kSplitHash; i += kSplitBlock) hk[i] = kSplitEmpty;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nd; j += kSplitBlock) {
+    const uint32_t x = gslot[Gr + j];
+    uint32_t h = SplitHashPos(x);
+    while (atomicCAS(&hk[h], kSplitEmpty, x) != kSplitEmpty) h = (h + 1) & (kSplitHash - 1);
+    hv[h] = static_cast<uint16_t>(j + 1);
+  }
+  __syncthreads();
+}
+
+// Bucket of a staged record: 0 = rest, 1 + j = designated, nd + 1 = no group.
+__device__ __forceinline__ uint32_t SplitLookup(const uint32_t* hk, const uint16_t* hv, uint32_t x, uint32_t cap, uint32_t nd) {
+  if (x >= cap) return nd + 1;
+  uint32_t h = SplitHashPos(x);
+  for (;;) {
+    const uint32_t k = hk[h];
+    if (k == x) return hv[h];
+    if (k == kSplitEmpty) return 0;
+    h = (h + 1) & (kSplitHash - 1);
+  }
+}
+
+// Bucket counts of one tile -> hist[b * ntiles + tile] (bucket-major, as the radix passes).
+// The rest bucket, a large share of every wave, is counted in registers and added once per wave.
+__global__ void __launch_bounds__(kSplitBlock) SplitHistKernel(const uint32_t* __restrict__ slot, uint64_t n, uint32_t cap,
+                                                               const uint32_t* __restrict__ gslot, const uint64_t* __restrict__ ftotal,
+                                                               uint32_t G, uint32_t* __restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t hk[kSplitHash];
+  __shared__ uint16_t hv[kSplitHash];
+  __shared__ uint32_t h[kSplitBuckets];
+  const uint32_t nd = SplitNd(ftotal), Gr = G - nd, nb = nd + 2;
+  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) h[b] = 0;
+  SplitBuildMap(hk, hv, gslot, Gr, nd);
+  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
+  const uint64_t r0 = static_cast<uint64_t>(tile) * kSplitTile;
+  const uint64_t r1 = min(r0 + kSplitTile, n);
+  uint32_t rest = 0;
+  constexpr int U = 8;
+  for (uint64_t r = r0 + threadIdx.x; r < r1; r += static_cast<uint64_t>(kSplitBlock) * U) {
+    uint32_t sv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = r + static_cast<uint64_t>(u) * kSplitBlock;
+      sv[u] = i < r1 ? slot[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r + static_cast<uint64_t>(u) * kSplitBlock >= r1) continue;
+      const uint32_t b = SplitLookup(hk, hv, sv[u], cap, nd);
+      if (b == 0) ++rest;
+      else atomicAdd(&h[b], 1u);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) rest += __shfl_xor(rest, o, 64);
+  if ((threadIdx.x & 63) == 0 && rest) atomicAdd(&h[0], rest);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) hist[static_cast<uint64_t>(b) * ntiles + tile] = h[b];
+}
+
+// tot[b] = bucket b's count over all tiles (0 past the live buckets, so one fixed-size scan
+// of tot gives the bucket bases).
+__global__ void __launch_bounds__(kRsScanBlock) SplitTotalKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                                 const uint64_t* __restrict__ ftotal, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s[kRsScanBlock];
+  const uint32_t b = blockIdx.x;
+  if (b >= SplitNd(ftotal) + 2) {
+    if (threadIdx.x == 0) tot[b] = 0;
+    return;
+  }
+  const uint32_t* row = hist + static_cast<uint64_t>(b) * ntiles;
+  uint32_t t = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += kRsScanBlock) t += row[i];
+  s[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[b] = s[0];
+}
+
+// Block b: exclusive scan of bucket b's tile counts plus the bucket base (RsScanKernel's
+// shape, with the base given).
+__global__ void __launch_bounds__(kRsScanBlock) SplitScanKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                                const uint64_t* __restrict__ ftotal, const uint32_t* __restrict__ base) {
+  constexpr int kWaves = kRsScanBlock / 64;
+  constexpr int kU = 4;
+  __shared__ uint32_t s_w[kWaves];
+  const int t = threadIdx.x;
+  const uint32_t d = blockIdx.x;
+  if (d >= SplitNd(ftotal) + 2) return;
+  const int lane = t & 63, wid = t >> 6;
+  uint32_t* row = hist + static_cast<uint64_t>(d) * ntiles;
+  const uint32_t per = (ntiles + kWaves - 1) / kWaves;
+  const uint32_t q0 = min(ntiles, per * wid), q1 = min(ntiles, q0 + per);
+  uint32_t tot = 0;
+  for (uint32_t i = q0 + lane; i < q1; i += 64) tot += row[i];
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) s_w[wid] = tot;
+  __syncthreads();
+  uint32_t run = base[d];
+  for (int w = 0; w < wid; ++w) run += s_w[w];
+  for (uint32_t i0 = q0; i0 < q1; i0 += 64 * kU) {
+    uint32_t c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + u * 64 + lane;
+      c[u] = i < q1 ? row[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      uint32_t incl = c[u];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t i = i0 + u * 64 + lane;
+      if (i < q1) row[i] = run + incl - c[u];
+      run += __shfl(incl, 63, 64);
+    }
+  }
+}
+
+// In-place exclusive scan of a[0..n) (n <= kSplitBuckets) by one block; a[n] = the total.
+__device__ __forceinline__ void SplitBlockScan(uint32_t* a, uint32_t n, uint32_t* s_w) {
+  constexpr int kPer = kSplitBuckets / kSplitBlock;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t i0 = threadIdx.x * kPer;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    v[k] = i0 + k < n ? a[i0 + k] : 0u;
+    sum += v[k];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (int w = 0; w < wid; ++w) run += s_w[w];
+  if (threadIdx.x == kSplitBlock - 1) a[n] = run + sum;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (i0 + k < n) a[i0 + k] = run;
+    run += v[k];
+  }
+}
+
+// The scatter, kSplitSub records at a time: ranks per bucket (LDS atomics; the rest bucket's
+// once per wave), the sub-tile reordered by bucket in LDS, then written out in bucket runs
+// (consecutive threads -> consecutive addresses), so a wave's stores touch few lines.  Rest
+// records (their slot, values) go to the sort's input region [0, n_rest); the others' values go
+// straight to their final position.  Order inside a bucket is arrival order, like the staging's.
+__global__ void __launch_bounds__(kSplitBlock) SplitScatterKernel(const uint32_t* __restrict__ slot, ConstValPtrs vin, int nvals, uint64_t n,
+                                                                  uint32_t cap, const uint32_t* __restrict__ gslot,
+                                                                  const uint64_t* __restrict__ ftotal, uint32_t G,
+                                                                  const uint32_t* __restrict__ offs, uint32_t ntiles,
+                                                                  uint32_t* __restrict__ rkey, ValPtrs vrest, ValPtrs vout) {
+  __shared__ uint32_t hk[kSplitHash];
+  __shared__ uint16_t hv[kSplitHash];
+  __shared__ uint32_t cur[kSplitBuckets];
+  __shared__ uint32_t lst[kSplitBuckets + 1];
+  __shared__ uint64_t s_val[kSplitSub];
+  __shared__ uint32_t s_key[kSplitSub];
+  __shared__ uint16_t s_bkt[kSplitSub];
+  __shared__ uint32_t s_w[kSplitBlock / 64];
+  const uint32_t nd = SplitNd(ftotal), Gr = G - nd, nb = nd + 2;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
+  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) cur[b] = offs[static_cast<uint64_t>(b) * ntiles + tile];
+  SplitBuildMap(hk, hv, gslot, Gr, nd);
+  const uint64_t r0 = static_cast<uint64_t>(tile) * kSplitTile;
+  const uint64_t r1 = min(r0 + kSplitTile, n);
+  for (uint64_t sb = r0; sb < r1; sb += kSplitSub) {
+    uint32_t sv[kSplitItems], bk[kSplitItems], rk[kSplitItems];
+    uint64_t v0[kSplitItems];
+#pragma unroll
+    for (int u = 0; u < kSplitItems; ++u) {
+      const uint64_t i = sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x;
+      sv[u] = i < r1 ? slot[i] : 0u;
+      v0[u] = (nvals > 0 && i < r1) ? vin.p[0][i] : 0ULL;
+    }
+    for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) lst[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kSplitItems; ++u) {
+      const bool valid = sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x < r1;
+      bk[u] = valid ? SplitLookup(hk, hv, sv[u], cap, nd) : 0xFFFFu;
+      const bool rest = bk[u] == 0;
+      const unsigned long long m = __ballot(rest);
+      rk[u] = 0;
+      if (m) {
+        const int leader = __ffsll(static_cast<long long>(m)) - 1;
+        uint32_t wb = 0;
+        if (lane == leader) wb = atomicAdd(&lst[0], static_cast<uint32_t>(__popcll(m)));
+        wb = __shfl(wb, leader, 64);
+        rk[u] = wb + static_cast<uint32_t>(__popcll(m & lanemask_lt));
+      }
+      if (valid && !rest) rk[u] = atomicAdd(&lst[bk[u]], 1u);
+    }
+    __syncthreads();
+    SplitBlockScan(lst, nb, s_w);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kSplitItems; ++u) {
+      if (bk[u] == 0xFFFFu) continue;
+      const uint32_t p = lst[bk[u]] + rk[u];
+      s_val[p] = v0[u];
+      s_bkt[p] = static_cast<uint16_t>(bk[u]);
+      s_key[p] = sv[u];
+    }
+    __syncthreads();
+    const uint32_t tn = lst[nb];
+    for (uint32_t j = threadIdx.x; j < tn; j += kSplitBlock) {
+      const uint32_t b = s_bkt[j];
+      const uint32_t dst = cur[b] + (j - lst[b]);
+      if (b == 0) {
+        rkey[dst] = s_key[j];
+        if (nvals > 0) vrest.p[0][dst] = s_val[j];
+      } else if (nvals > 0) {
+        vout.p[0][dst] = s_val[j];
+      }
+    }
+    for (int v = 1; v < nvals; ++v) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSplitItems; ++u) {
+        if (bk[u] == 0xFFFFu) continue;
+        s_val[lst[bk[u]] + rk[u]] = vin.p[v][sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x];
+      }
+      __syncthreads();
+      for (uint32_t j = threadIdx.x; j < tn; j += kSplitBlock) {
+        const uint32_t b = s_bkt[j];
+        const uint32_t dst = cur[b] + (j - lst[b]);
+        if (b == 0) vrest.p[v][dst] = s_val[j];
+        else vout.p[v][dst] = s_val[j];
+      }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) cur[b] += lst[b + 1] - lst[b];
+    __syncthreads();
+  }
+}
+
+// gstart of the designated groups (and gstart[G]) from the bucket bases: gstart[Gr + j] =
+// base[1 + j] for j in [0, nd].
+__global__ void SplitGstartKernel(const uint32_t* __restrict__ base, const uint64_t* __restrict__ ftotal, uint32_t G,
+                                  uint32_t* __restrict__ gstart) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nd = SplitNd(ftotal);
+  if (j <= nd) gstart[G - nd + j] = base[1 + j];
+}
+
 int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* vals,
                        uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals) {
   for (int b = 0; b < 2; ++b) {
@@ -1999,11 +2395,49 @@ int32_t AggFinalizeTable(Agg* a) {
   void* scan_tmp = ws.scan.p;
   PXG_RETURN_IF_ERROR(ws.rank.Ensure(static_cast<size_t>(a->cap) * 4 + 16));
   PXG_RETURN_IF_ERROR(ws.gslot.Ensure(static_cast<size_t>(ngroups) * 4));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "slot_flags", SlotFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                             a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>()));
-  PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
-  PXG_RETURN_IF_ERROR(Launch(ctx, "slot_gslot", SlotGslotKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                             a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<const uint32_t>(), ws.gslot.as<uint32_t>()));
+  // Large aggregations split the designated (sampled-large) groups out of the staging in one
+  // pass and radix-sort only the rest (SplitSampleKernel above).  PXG_SPLIT_MIN_ROWS /
+  // PXG_SPLIT_EST (tests) set the staged-row threshold and the designation estimate.
+  const uint64_t split_min_rows = [] {
+    const char* e = std::getenv("PXG_SPLIT_MIN_ROWS");
+    return e ? static_cast<uint64_t>(std::atoll(e)) : ~uint64_t(0);  // opt-in until it measures faster
+  }();
+  const uint32_t split_min_samples = [] {
+    const char* e = std::getenv("PXG_SPLIT_EST");
+    const uint64_t est = e ? static_cast<uint64_t>(std::atoll(e)) : kSplitMinRows;
+    return static_cast<uint32_t>(std::max<uint64_t>(1, est / kSplitStride));
+  }();
+  const bool split = n >= split_min_rows && ngroups >= 2;
+  uint64_t* d_ftotal = nullptr;
+  if (!split) {
+    PXG_RETURN_IF_ERROR(Launch(ctx, "slot_flags", SlotFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                               a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "slot_gslot", SlotGslotKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                               a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<const uint32_t>(), ws.gslot.as<uint32_t>()));
+  } else {
+    PXG_RETURN_IF_ERROR(ws.split_cnt.Ensure(static_cast<size_t>(a->cap) * 4 + 32 * 4));
+    PXG_RETURN_IF_ERROR(ws.split_flags.Ensure((static_cast<size_t>(a->cap) + 2) * 8));
+    uint64_t* flags = ws.split_flags.as<uint64_t>();
+    d_ftotal = flags + a->cap;
+    uint32_t* lvl = ws.split_cnt.as<uint32_t>() + a->cap;
+    PXG_HIP(hipMemsetAsync(ws.split_cnt.p, 0, static_cast<size_t>(a->cap) * 4 + 32 * 4, ctx->stream));
+    const uint64_t nsamp = (n + kSplitStride - 1) / kSplitStride;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_sample", SplitSampleKernel, dim3(GridFor(static_cast<int64_t>(nsamp), 256 * kSamplePerThread, 1 << 30)),
+                               dim3(256), 0, a->st_slot.as<const uint32_t>(), n, a->cap, ws.split_cnt.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitLevelsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                               ws.split_cnt.as<const uint32_t>(), a->cap, lvl));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                               a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
+                               static_cast<const uint32_t*>(lvl), split_min_samples, flags));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, flags, flags, a->cap, d_ftotal, scan_tmp));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitIdsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
+                               a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
+                               static_cast<const uint32_t*>(lvl), split_min_samples, static_cast<const uint64_t*>(flags), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.rank.as<uint32_t>(),
+                               ws.gslot.as<uint32_t>()));
+    // d_ngroups (the device's own group count, checked at the end) from the occupied total.
+    PXG_HIP(hipMemcpyAsync(d_ngroups, d_ftotal, 4, hipMemcpyDeviceToDevice, ctx->stream));
+  }
 
   // Group keys out of the arena, on side stream 2 while the radix sort runs on the main
   // stream (ConvertAggHashMapToRowBatch group columns, agg_node.cc:303-349).  String payloads
@@ -2070,15 +2504,70 @@ int32_t AggFinalizeTable(Agg* a) {
   }
   for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
   const uint32_t* kin = nullptr;
-  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, a->n_vals,
-                                       n, kbuf, vbuf, ws.rs, &kin, &vin));
-  PXG_RETURN_IF_ERROR(IssueKeys());
-  const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
-  // 3. Group starts (first index of every id).
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
-  PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                             skeys, n, ngroups, ws.gstart.as<uint32_t>()));
+  if (!split) {
+    PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, a->n_vals,
+                                         n, kbuf, vbuf, ws.rs, &kin, &vin));
+    PXG_RETURN_IF_ERROR(IssueKeys());
+    const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
+    // 3. Group starts (first index of every id).
+    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+                               skeys, n, ngroups, ws.gstart.as<uint32_t>()));
+  } else {
+    // 2'. The split: bucket counts per tile, bucket bases, tile offsets, one scatter; then the
+    //     radix sort of the rest records only.  The rest records' input goes to buffer 1 and the
+    //     designated records straight to the buffer the sort ends in (its pass count comes from
+    //     G, an upper bound of the rest ids), at [n_rest, n): the two never overlap.
+    int nbits = 1;
+    while ((uint64_t(1) << nbits) < static_cast<uint64_t>(ngroups) + 1) ++nbits;
+    const int passes = (nbits + kRadixBits - 1) / kRadixBits;
+    const int fin = (passes - 1) & 1;
+    const uint32_t ntiles = static_cast<uint32_t>((n + kSplitTile - 1) / kSplitTile);
+    PXG_RETURN_IF_ERROR(ws.split_hist.Ensure(static_cast<size_t>(kSplitBuckets) * ntiles * 4));
+    PXG_RETURN_IF_ERROR(ws.split_tot.Ensure(static_cast<size_t>(2 * kSplitBuckets + 2) * 4));
+    uint32_t* tot = ws.split_tot.as<uint32_t>();
+    uint32_t* base = tot + kSplitBuckets + 1;
+    uint32_t* hist = ws.split_hist.as<uint32_t>();
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_hist", SplitHistKernel, dim3(ntiles), dim3(kSplitBlock), 0, a->st_slot.as<const uint32_t>(), n,
+                               a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups, hist, ntiles));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scan", SplitTotalKernel, dim3(kSplitBuckets), dim3(kRsScanBlock), 0,
+                               static_cast<const uint32_t*>(hist), ntiles, static_cast<const uint64_t*>(d_ftotal), tot));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, tot, base, kSplitBuckets, base + kSplitBuckets, scan_tmp));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scan", SplitScanKernel, dim3(kSplitBuckets), dim3(kRsScanBlock), 0, hist, ntiles,
+                               static_cast<const uint64_t*>(d_ftotal), static_cast<const uint32_t*>(base)));
+    // n_rest (= base[1]) and the designated count to the host; the scatter runs meanwhile.
+    uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
+    PXG_HIP(hipMemcpyAsync(pin + 104, base + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipMemcpyAsync(pin + 112, d_ftotal, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipEventRecord(ctx->ev_split, ctx->stream));
+    ValPtrs vrest = vbuf[1], vout = vbuf[fin];
+    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scatter", SplitScatterKernel, dim3(ntiles), dim3(kSplitBlock), 0, a->st_slot.as<const uint32_t>(),
+                               vin, a->n_vals, n, a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups,
+                               static_cast<const uint32_t*>(hist), ntiles, kbuf[1], vrest, vout));
+    PXG_RETURN_IF_ERROR(IssueKeys());
+    clk.Mark("finalize: issue split");
+    PXG_HIP(hipEventSynchronize(ctx->ev_split));
+    clk.Mark("finalize: split wait");
+    uint32_t n_rest = 0;
+    uint64_t ft = 0;
+    std::memcpy(&n_rest, pin + 104, 4);
+    std::memcpy(&ft, pin + 112, 8);
+    const uint32_t nd = std::min<uint32_t>(static_cast<uint32_t>(ft >> 32), kSplitMaxBig);
+    const uint32_t Gr = ngroups - nd;
+    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vout.p[v];
+    if (n_rest > 0) {
+      ConstValPtrs rin;
+      for (int v = 0; v < kMaxVals; ++v) rin.p[v] = vrest.p[v];
+      // the rest records carry their slots: the first pass maps them to rest ids (< Gr)
+      PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], ws.rank.as<const uint32_t>(), a->cap, ngroups, rin, a->n_vals, n_rest, kbuf, vbuf,
+                                           ws.rs, &kin, &vin));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n_rest), 256, 1 << 30)), dim3(256), 0,
+                                 kin, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
+    }
+    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", SplitGstartKernel, dim3((kSplitMaxBig + 256) / 256), dim3(256), 0,
+                               static_cast<const uint32_t*>(base), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
+  }
   // 3. UDA reductions (chunk partials, then per-group combine).
   const ConstValPtrs cv = vin;
   UdaOut uo;

@@ -148,6 +148,7 @@ struct Ctx {
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   hipEvent_t ev_meta = nullptr;  // finalize: the big-group metadata readback has landed
   hipEvent_t ev_chain = nullptr; // finalize: the digest boundary chains are done (side stream)
+  hipEvent_t ev_split = nullptr; // finalize: the staging split's bucket totals have landed (pinned)
   bool profiling = false;
   std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;
@@ -155,7 +156,8 @@ struct Ctx {
   std::vector<hipEvent_t> free_events;
   int num_cus = 256;
   // Pinned scratch for counters read back by the host (async D2H, no staging copy):
-  // [0, 64) consume publish, [64, 128) finalize class counts, [128, 256) finalize totals,
+  // [0, 64) consume publish, [64, 104) finalize class counts, [104, 128) finalize split
+  // totals, [128, 256) finalize totals,
   // [kPinnedOps, kPinnedBytes) standalone Filter / Map per-chunk counts.
   void* pinned = nullptr;
   static constexpr size_t kPinnedOps = 4096, kPinnedBytes = 65536;

@@ -325,7 +325,8 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
       hipEventCreateWithFlags(&c->impl.ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_join2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_meta, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->impl.ev_chain, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->impl.ev_chain, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_split, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SetError(PXG_INTERNAL, "side stream / event creation failed");
   }
@@ -355,6 +356,7 @@ extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   hipEventDestroy(ctx->impl.ev_join2);
   hipEventDestroy(ctx->impl.ev_meta);
   hipEventDestroy(ctx->impl.ev_chain);
+  hipEventDestroy(ctx->impl.ev_split);
   hipStreamDestroy(ctx->impl.side2);
   hipStreamDestroy(ctx->impl.stream);
   delete ctx;
