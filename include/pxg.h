@@ -413,6 +413,11 @@ int32_t pxg_table_append_http_events(pxg_table* t, uint64_t seed, int64_t row_be
  * ------------------------------------------------------------------------------------- */
 int32_t pxg_digest_chains(pxg_ctx* ctx, const int64_t* d_w, int32_t n, int32_t wave, uint32_t* d_starts,
                           int32_t cap, int32_t* d_nc);
+/* Diagnostics (tests).  The merged digest of one group (the multi-GPU exchange's owner side,
+ * tdigest batch add restated from math_sketches.h:38 / oracle/tdigest.h merge_batch): n items in
+ * part order, d_vals = raw values (arg_type bits) or centroid means (double bits), d_wt = part
+ * << 48 | weight (weight 0: a raw value); the 7 quantiles to d_out7.  Synchronises. */
+int32_t pxg_digest_merge(pxg_ctx* ctx, const uint64_t* d_vals, const uint64_t* d_wt, int64_t n, int32_t arg_type, double* d_out7);
 
 #ifdef __cplusplus
 }

@@ -1609,6 +1609,41 @@ extern "C" void oracle_tdigest_quantiles(const double* vals, int64_t n, double* 
   for (int k = 0; k < 7; ++k) out7[k] = d.quantile(kQs[k]);
 }
 
+extern "C" void oracle_tdigest_centroids(const double* vals, int64_t n, double* means, double* weights, int64_t cap, int64_t* nc) {
+  TDigest d = TDigest::FromValuesOnce(std::vector<double>(vals, vals + n), 1000);
+  const auto& cs = d.processed();
+  *nc = static_cast<int64_t>(cs.size()) <= cap ? static_cast<int64_t>(cs.size()) : -1;
+  if (*nc < 0) return;
+  for (size_t i = 0; i < cs.size(); ++i) {
+    means[i] = cs[i].mean;
+    weights[i] = cs[i].weight;
+  }
+}
+
+extern "C" void oracle_tdigest_batch_quantiles(int32_t nparts, const int32_t* kind, const int64_t* counts, const double* data,
+                                               const double* weights, double* out7) {
+  std::vector<TDigest> parts;
+  parts.reserve(static_cast<size_t>(nparts));
+  int64_t at = 0;
+  for (int32_t p = 0; p < nparts; ++p) {
+    const int64_t c = counts[p];
+    if (kind[p] == 0) {
+      parts.push_back(TDigest::Unprocessed(std::vector<double>(data + at, data + at + c), 1000));
+    } else {
+      std::vector<Centroid> cs;
+      for (int64_t i = 0; i < c; ++i) cs.emplace_back(data[at + i], weights[at + i]);
+      parts.push_back(TDigest::FromCentroids(cs, 1000));
+    }
+    at += c;
+  }
+  std::vector<const TDigest*> batch;
+  for (const auto& d : parts) batch.push_back(&d);
+  TDigest out(1000);
+  out.merge_batch(batch);
+  static const double qs[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
+  for (int i = 0; i < 7; ++i) out7[i] = out.quantile(qs[i]);
+}
+
 extern "C" void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb, double* out7) {
   TDigest d1(1000), d2(1000);
   for (int64_t i = 0; i < na; ++i) d1.add(a[i]);

@@ -74,6 +74,14 @@ void oracle_free(uint8_t* p);
 // QuantilesUDA on a value sequence (math_sketches.h:36-54): out[7] = p01,p10,p25,p50,p75,p90,p99.
 void oracle_tdigest_quantiles(const double* vals, int64_t n, double* out7);
 // Two digests built from a and b, then merged (QuantilesUDA::Merge), then the quantiles.
+/* The single-pass digest of n values (TDigest::FromValuesOnce): centroid means / weights into
+ * means / weights (capacity cap), their count into *nc (-1 if cap is too small). */
+void oracle_tdigest_centroids(const double* vals, int64_t n, double* means, double* weights, int64_t cap, int64_t* nc);
+/* quantiles() x7 of a digest built as TDigest::merge_batch over nparts contributions, part i
+ * being kind[i] == 0: counts[i] raw values (unprocessed), == 1: counts[i] centroids (means in
+ * data, weights in weights), all concatenated in part order. */
+void oracle_tdigest_batch_quantiles(int32_t nparts, const int32_t* kind, const int64_t* counts, const double* data,
+                                    const double* weights, double* out7);
 void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb,
                                     double* out7);
 // The JSON string QuantilesUDA::Finalize would produce (rapidjson Writer bytes, json_double.h).

@@ -78,6 +78,47 @@ class TDigest {
     return QuantileProcessed(q);
   }
 
+  // The digest one rank ships for a group of more than 8 * delta values (pxg export v2,
+  // DESIGN.md §5): every value added unprocessed and ONE process() over them, i.e. the same
+  // single-pass digest the device emulates for one group on one node.
+  static TDigest FromValuesOnce(const std::vector<double>& v, double compression = 1000) {
+    TDigest d = Unprocessed(v, compression);
+    d.Process();
+    return d;
+  }
+  // A digest holding `v` as unprocessed centroids of weight 1 (NaN skipped, as add() does):
+  // a rank's raw contribution of <= 8 * delta values.
+  static TDigest Unprocessed(const std::vector<double>& v, double compression = 1000) {
+    TDigest d(compression);
+    for (double x : v)
+      if (!std::isnan(x)) {
+        d.unprocessed_.emplace_back(x, 1.0);
+        d.unprocessed_weight_ += 1.0;
+      }
+    return d;
+  }
+  // A digest whose processed centroids are `cs` (sorted by mean), as the shipping rank's
+  // process() left them: min/max are the first / last centroid means.
+  static TDigest FromCentroids(const std::vector<Centroid>& cs, double compression = 1000) {
+    TDigest d(compression);
+    d.processed_ = cs;
+    for (const auto& c : cs) d.processed_weight_ += c.weight;
+    if (!cs.empty()) {
+      d.min_ = cs.front().mean;
+      d.max_ = cs.back().mean;
+    }
+    d.UpdateCumulative();
+    return d;
+  }
+  // add(first, last) of the merging digest: a whole batch of digests merged at once (one k-way
+  // merge of their processed centroids, their unprocessed ones appended, process when dirty).
+  void merge_batch(const std::vector<const TDigest*>& batch) {
+    MergeProcessed(batch);
+    MergeUnprocessed(batch);
+    ProcessIfNecessary();
+    UpdateCumulative();
+  }
+
   const std::vector<Centroid>& processed() const { return processed_; }
   double processed_weight() const { return processed_weight_; }
   double min() const { return min_; }

@@ -85,7 +85,7 @@ EXPORTED = [
     "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial", "pxg_agg_import_partials",
-    "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains",
+    "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains", "pxg_digest_merge",
     "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_destroy", "pxg_agg_alltoall",
 ]
 
@@ -159,6 +159,7 @@ def load() -> C.CDLL:
         "pxg_datagen_http_events": (i32, [C.c_uint64, i64, i64, i64, i32, p(ColumnOut)]),
         "pxg_table_append_http_events": (i32, [vp, C.c_uint64, i64, i64, i64]),
         "pxg_digest_chains": (i32, [vp, vp, i32, i32, vp, i32, vp]),
+        "pxg_digest_merge": (i32, [vp, vp, vp, i64, i32, vp]),
         "pxg_comm_unique_id": (i32, [vp, i32]),
         "pxg_comm_init": (i32, [vp, i32, i32, vp, i32, p(vp)]),
         "pxg_comm_destroy": (i32, [vp]),

@@ -52,8 +52,20 @@ struct AggPlanDev {
   DevProgram vals2[kMaxVals];
 };
 
+// Probe records (consume fast path, all-STRING keys, <= 2 keys): per table slot kRecWords
+// words = [the published slot word, the key lengths (16 bits per key), key 0's kRecKeyWords
+// words, key 1's ...], tail-masked and zero-padded, 128-byte aligned.  Written by publication
+// (and rebuilt after a rehash); a probe that meets a published (arena) slot word compares its
+// keys against the record at the same position with 16-byte loads of one line instead of the
+// arena / representative row.  Word 0 equal to the slot word the probe saw
+// is what makes a record valid: records are cleared at reset and rebuilt after growth.
+constexpr int kRecWords = 16;
+constexpr int kRecKeyWords = 6;  // = kFastStrWords: STRING keys of <= 48 bytes
+constexpr int kRecMaxKeys = 2;
+
 struct AggTableDev {
   unsigned long long* slots;
+  const uint64_t* prec;  // probe records (null: off)
   uint32_t mask;
   uint32_t limit;                 // inserts beyond this are deferred (table kept <= 50% full)
   unsigned int* counters;         // [0] groups in the table (flushed per tile), [2] deferred rows

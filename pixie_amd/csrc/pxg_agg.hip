@@ -454,10 +454,48 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
   return eq;
 }
 
+// Key compare against the probe record at the probed position (pxg_agg.h): 1 equal, 0 not,
+// -1 when the record does not hold this slot word (never published: imported / spilled groups).
+// One 16-byte load for the header and one per chunk of used key words, all issued at once and
+// all in the record's 128-byte line; unused words are zero on both sides, so whole chunks compare.
+template <int NK>
+__device__ __forceinline__ int RecordEqual(const uint64_t* __restrict__ rec, unsigned long long w, const FastKeys<NK>& k) {
+  static_assert(NK <= kRecMaxKeys && 2 + NK * kRecKeyWords <= kRecWords, "record layout");
+  constexpr int kChunks = (2 + NK * kRecKeyWords + 1) / 2;
+  const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(rec);
+  uint32_t nw[NK];
+#pragma unroll
+  for (int i = 0; i < NK; ++i) nw[i] = (k.len[i] + 7) >> 3;
+  uint64_t c[2 * kChunks];
+#pragma unroll
+  for (int ci = 0; ci < kChunks; ++ci) {
+    bool need = ci == 0;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+      const int lo = 2 + kRecKeyWords * i;
+      need = need || (2 * ci + 1 >= lo && 2 * ci < lo + static_cast<int>(nw[i]));
+    }
+    ulonglong2 v = make_ulonglong2(0, 0);
+    if (need) v = r2[ci];
+    c[2 * ci] = v.x;
+    c[2 * ci + 1] = v.y;
+  }
+  if (c[0] != w) return -1;
+  uint64_t lens = 0;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) lens |= static_cast<uint64_t>(k.len[i]) << (16 * i);
+  bool eq = c[1] == lens;
+#pragma unroll
+  for (int i = 0; i < NK; ++i)
+#pragma unroll
+    for (int j = 0; j < kRecKeyWords; ++j) eq = eq && c[2 + kRecKeyWords * i + j] == k.w[i][j];
+  return eq ? 1 : 0;
+}
+
 // TAGONLY: timing-only diagnostic (PXG_DIAG_CONSUME=1): a tag match is taken as the group without
 // the representative compare, which prices that compare (tools/consume_diag.py; wrong groups on
 // a tag collision, never followed by a checked finalize).
-template <int NK, bool S = false, bool TAGONLY = false>
+template <int NK, bool S = false, bool TAGONLY = false, bool REC = false>
 __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                                      const KeyCols<NK>* __restrict__ s_kc, uint32_t n_lds_chunks,
                                                      const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
@@ -496,7 +534,9 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
       const uint32_t ref = static_cast<uint32_t>(w);
       bool eq;
       if (w & kKindArena) {
-        eq = FastKeysEqualArena<NK, S>(plan, keys, tab.arena + ref);
+        int r = -1;
+        if constexpr (REC) r = RecordEqual<NK>(tab.prec + static_cast<uint64_t>(pos) * kRecWords, w, keys);
+        eq = r >= 0 ? r == 1 : FastKeysEqualArena<NK, S>(plan, keys, tab.arena + ref);
       } else {
         const uint32_t c = ref >> kChunkShift;
         const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK, S>(plan, chunks[c]);
@@ -527,7 +567,9 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
 // of probing the global table; a row with a STRING key longer than kHcStrWords words leaves a
 // hole there and takes the table path (a staging record whose slot the generic list kernel
 // fills in, like any deferred row), so the two paths hold disjoint key sets.
-template <int NK, int MODE, bool PAIRS = false, bool HC = false>
+// REC: published slots compare against the probe records (all-STRING keys, <= 2 keys; the table
+// passes prec).
+template <int NK, int MODE, bool PAIRS = false, bool HC = false, bool REC = false>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
@@ -738,7 +780,8 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          slot = FastFindOrInsert<NK, S, (MODE & 3) == 1>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
+          slot = FastFindOrInsert<NK, S, (MODE & 3) == 1, REC && S && NK <= kRecMaxKeys>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab,
+                                                                                          &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -785,9 +828,45 @@ __global__ void AggPublishSizesKernel(const AggPlanDev* __restrict__ plan, const
   sizes[i] = s;
 }
 
+// The probe record of a published group (all-STRING keys): its slot word, the lengths, the key
+// words tail-masked and zero-padded (word 0 = 0, i.e. no record, when a key is too long).
+__device__ __forceinline__ void WriteProbeRecord(const AggPlanDev* __restrict__ plan, const KeySet& k, unsigned long long word,
+                                                 uint64_t* __restrict__ rec) {
+  uint64_t r[kRecWords];
+#pragma unroll
+  for (int t = 0; t < kRecWords; ++t) r[t] = 0;
+  r[0] = word;
+#pragma unroll
+  for (int i = 0; i < kRecMaxKeys; ++i) {
+    if (i >= plan->n_keys) break;
+    const uint32_t len = static_cast<uint32_t>(k.v[i].b);
+    if (len > 8u * kRecKeyWords) r[0] = 0;
+    r[1] |= static_cast<uint64_t>(len & 0xFFFF) << (16 * i);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(k.v[i].a);
+#pragma unroll
+    for (int j = 0; j < kRecKeyWords; ++j)
+      if (8u * j < len && len <= 8u * kRecKeyWords) r[2 + kRecKeyWords * i + j] = LoadWordU(src + 8 * j) & TailMask(len - 8u * j);
+  }
+  ulonglong2* d = reinterpret_cast<ulonglong2*>(rec);
+#pragma unroll
+  for (int t = 0; t < kRecWords / 2; ++t) d[t] = make_ulonglong2(r[2 * t], r[2 * t + 1]);
+}
+
+// Probe records of every published slot (after a rehash moved the slots).
+__global__ void RecordsFromArenaKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ slots, uint32_t cap,
+                                       const uint64_t* __restrict__ arena, uint64_t* __restrict__ prec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const unsigned long long w = slots[i];
+  if (!(w & kKindArena)) return;
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(w), k);
+  WriteProbeRecord(plan, k, w, prec + static_cast<uint64_t>(i) * kRecWords);
+}
+
 __global__ void AggPublishWriteKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                       unsigned long long* __restrict__ slots, uint32_t cap, const uint64_t* __restrict__ offs,
-                                      uint64_t base, uint64_t* __restrict__ arena) {
+                                      uint64_t base, uint64_t* __restrict__ arena, uint64_t* __restrict__ prec) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   const unsigned long long w = slots[i];
@@ -797,7 +876,9 @@ __global__ void AggPublishWriteKernel(const AggPlanDev* __restrict__ plan, const
   LoadKeysRow(plan, chunks[ref >> kChunkShift], static_cast<int64_t>(ref & (kChunkRows - 1)), k);
   const uint64_t at = base + (offs[i] & ((uint64_t(1) << kPublishCountShift) - 1));
   WriteKeyRecord(plan, k, arena + at);
-  slots[i] = MakeSlotWord(static_cast<uint32_t>(w >> 33), kKindArena, static_cast<uint32_t>(at));
+  const unsigned long long nw = MakeSlotWord(static_cast<uint32_t>(w >> 33), kKindArena, static_cast<uint32_t>(at));
+  slots[i] = nw;
+  if (prec) WriteProbeRecord(plan, k, nw, prec + static_cast<uint64_t>(i) * kRecWords);
 }
 
 __global__ void AggRehashKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ old_slots,
@@ -847,6 +928,7 @@ static AggTableDev TableDev(Agg* a, int defer_buf) {
   t.deferred = a->deferred[defer_buf].as<uint32_t>();
   t.deferred_pos = a->deferred_pos[defer_buf].as<uint32_t>();
   t.arena = a->arena.as<uint64_t>();
+  t.prec = a->rec_ok && a->rec_cap == a->cap ? a->prec.as<const uint64_t>() : nullptr;
   return t;
 }
 
@@ -869,6 +951,36 @@ int32_t Agg::EnsureTable(uint32_t want) {
   cap = want;
   PXG_RETURN_IF_ERROR(slots.Alloc(static_cast<size_t>(cap) * 8));
   PXG_HIP(hipMemsetAsync(slots.p, 0, static_cast<size_t>(cap) * 8, ctx->stream));
+  return PXG_OK;
+}
+
+// Probe records sized with the table (rec_ok plans only; at most kRecMaxCap slots).  Fresh
+// buffers are cleared: a record is valid only while its word 0 equals its slot's word.
+constexpr uint32_t kRecMaxCap = uint32_t(1) << 22;
+int32_t Agg::EnsureRecords() {
+  if (!rec_ok || cap > kRecMaxCap) {
+    rec_cap = 0;
+    return PXG_OK;
+  }
+  if (rec_cap == cap) return PXG_OK;
+  prec.Free();
+  PXG_RETURN_IF_ERROR(prec.Alloc(static_cast<size_t>(cap) * kRecWords * 8));
+  PXG_HIP(hipMemsetAsync(prec.p, 0, static_cast<size_t>(cap) * kRecWords * 8, ctx->stream));
+  rec_cap = cap;
+  rec_dirty = false;
+  return PXG_OK;
+}
+
+// After a rehash the slots moved: clear the records and write one per published slot again.
+int32_t Agg::RebuildRecords() {
+  if (!rec_ok || rec_cap == 0) return PXG_OK;
+  PXG_RETURN_IF_ERROR(EnsureRecords());
+  if (rec_cap != cap) return PXG_OK;
+  PXG_HIP(hipMemsetAsync(prec.p, 0, static_cast<size_t>(cap) * kRecWords * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "agg_records", RecordsFromArenaKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                             d_plan.as<const AggPlanDev>(), slots.as<const unsigned long long>(), cap, arena.as<const uint64_t>(),
+                             prec.as<uint64_t>()));
+  rec_dirty = true;
   return PXG_OK;
 }
 
@@ -927,7 +1039,7 @@ int32_t Agg::Grow(uint32_t new_cap) {
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   slots = std::move(ns);
   cap = new_cap;
-  return PXG_OK;
+  return RebuildRecords();
 }
 
 // Publish every kind-0 slot into the arena; reads back the group count, the deferred count
@@ -967,7 +1079,9 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
     PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + kArenaSlack, arena_words * 8, ctx->stream));
     PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
                                d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
-                               static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>()));
+                               static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>(),
+                               rec_ok && rec_cap == cap ? prec.as<uint64_t>() : nullptr));
+    if (rec_ok && rec_cap == cap) rec_dirty = true;
     arena_words += words;
   }
   // The device insert counter is exact (every successful insert CAS is counted).
@@ -1061,21 +1175,28 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   PXG_RETURN_IF_ERROR(deferred_pos[0].Ensure(static_cast<size_t>(rows) * 4 + 16));
   clk.Mark("consume: staging ensure");
   // The tile ranges of a repeated consume (same table, same rows) are already on the device.
-  const size_t rbytes = ranges.size() * sizeof(TileRange);
-  if (rbytes != last_ranges.size() || std::memcmp(last_ranges.data(), ranges.data(), rbytes) != 0) {
-    PXG_RETURN_IF_ERROR(d_ranges.Ensure(rbytes));
-    PXG_HIP(hipMemcpyAsync(d_ranges.p, ranges.data(), rbytes, hipMemcpyHostToDevice, ctx->stream));
-    PXG_HIP(hipStreamSynchronize(ctx->stream));  // `ranges` is pageable and goes out of scope
-    last_ranges.assign(reinterpret_cast<const uint8_t*>(ranges.data()), reinterpret_cast<const uint8_t*>(ranges.data()) + rbytes);
-  }
-  PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
+  auto upload = [&](DevBuf& dr, std::vector<uint8_t>& cache, const std::vector<TileRange>& rs) -> int32_t {
+    const size_t rbytes = rs.size() * sizeof(TileRange);
+    if (rbytes != cache.size() || std::memcmp(cache.data(), rs.data(), rbytes) != 0) {
+      PXG_RETURN_IF_ERROR(dr.Ensure(rbytes));
+      PXG_HIP(hipMemcpyAsync(dr.p, rs.data(), rbytes, hipMemcpyHostToDevice, ctx->stream));
+      PXG_HIP(hipStreamSynchronize(ctx->stream));  // `rs` is pageable and goes out of scope
+      cache.assign(reinterpret_cast<const uint8_t*>(rs.data()), reinterpret_cast<const uint8_t*>(rs.data()) + rbytes);
+    }
+    return PXG_OK;
+  };
   static const int64_t bpc = [] {  // workgroups per CU of the grid (experiments: PXG_CONSUME_BPC)
     const char* e = std::getenv("PXG_CONSUME_BPC");
     const int64_t v = e ? std::atoll(e) : 0;
     return v > 0 ? v : 8;
   }();
+  // Probe records (pxg_agg.h): a fresh run on a large range consumes a short prefix first, whose
+  // publication writes the records of (nearly) every hot group; the rest of the range then
+  // compares against records instead of representative rows.  PXG_NO_PREC=1 turns them off.
+  const bool rec = rec_ok && !hc_active && diag == 0 && fast_nk > 0 && fast_nk <= kRecMaxKeys && all_str && !EnvFlag("PXG_NO_PREC");
+  if (rec) PXG_RETURN_IF_ERROR(EnsureRecords());
   using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t);
-  auto pick = [&]() -> KernFn {
+  auto pick = [&](bool with_rec) -> KernFn {
     KernFn kern = AggConsumeKernel;
     switch (fast_nk * 4 + (diag & 3)) {
 #define PXG_FAST_CASE(nk)                                           \
@@ -1106,8 +1227,12 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     if (fast_nk == 0 || (diag & 3) != 0) return kern;
     if (all_str) {  // all-STRING keys: the specialised production kernels (PXG_PAIRS=1: 16-byte filter loads)
       switch (fast_nk) {
-        case 1: kern = pairs ? AggConsumeFastKernel<1, 4, true> : AggConsumeFastKernel<1, 4>; break;
-        case 2: kern = pairs ? AggConsumeFastKernel<2, 4, true> : AggConsumeFastKernel<2, 4>; break;
+        case 1:
+          kern = with_rec ? AggConsumeFastKernel<1, 4, false, false, true> : (pairs ? AggConsumeFastKernel<1, 4, true> : AggConsumeFastKernel<1, 4>);
+          break;
+        case 2:
+          kern = with_rec ? AggConsumeFastKernel<2, 4, false, false, true> : (pairs ? AggConsumeFastKernel<2, 4, true> : AggConsumeFastKernel<2, 4>);
+          break;
         case 3: kern = pairs ? AggConsumeFastKernel<3, 4, true> : AggConsumeFastKernel<3, 4>; break;
         case 4: kern = pairs ? AggConsumeFastKernel<4, 4, true> : AggConsumeFastKernel<4, 4>; break;
         default: break;
@@ -1115,38 +1240,55 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     }
     return kern;
   };
-  const TileRange* d_rg = d_ranges.as<const TileRange>();
-  {
-    const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(ctx->num_cus) * bpc));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume", pick(), dim3(grid), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
-                               t->d_chunks.as<const DevChunk>(), d_rg, static_cast<int>(ranges.size()), ntiles, TableDev(this, 0),
+  // One launch over `rs` (nt tiles), its publication, and the retry rounds of deferred rows.
+  auto run = [&](DevBuf& dr, std::vector<uint8_t>& cache, const std::vector<TileRange>& rs, int64_t nt, KernFn kern,
+                 const char* name) -> int32_t {
+    PXG_RETURN_IF_ERROR(upload(dr, cache, rs));
+    PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));  // deferred count
+    const int grid = static_cast<int>(std::min<int64_t>(nt, static_cast<int64_t>(ctx->num_cus) * bpc));
+    PXG_RETURN_IF_ERROR(Launch(ctx, name, kern, dim3(grid), dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(),
+                               t->d_chunks.as<const DevChunk>(), dr.as<const TileRange>(), static_cast<int>(rs.size()), nt, TableDev(this, 0),
                                StageDevOf(this), static_cast<uint32_t>(t->chunks.size())));
-  }
-  clk.Mark("consume: launch");
-  uint32_t n_def = 0;
-  PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
-  clk.Mark("consume: kernel + publish");
-  int buf = 0;
-  for (int round = 0; n_def > 0; ++round) {
-    // Rows are deferred by a full table / overlong probe, or (fast path) by a long string key.
-    // Grow unless this is the first retry and the table still has room for every deferred row.
-    // Growth is sized by groups, not rows: deferred rows mostly repeat groups, so the table
-    // grows geometrically (x4 per round, from at least 4x the groups it holds) and the retry
-    // defers again while it is still too small; 4 * (groups + deferred rows) caps it.
-    const uint64_t want = static_cast<uint64_t>(inserted) + n_def;
-    if (round > 0 || fast_nk == 0 || want > static_cast<uint64_t>(cap) * 3 / 8) {
-      const uint64_t geo = std::max<uint64_t>(static_cast<uint64_t>(cap) * 4, static_cast<uint64_t>(inserted) * 4);
-      PXG_RETURN_IF_ERROR(Grow(NextPow2(std::min<uint64_t>(geo, 4 * want))));
-    }
-    PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
-    PXG_RETURN_IF_ERROR(deferred_pos[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
-    PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume_list", AggConsumeListKernel, dim3(GridFor(n_def, kConsumeBlock, ctx->num_cus * 8)),
-                               dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(),
-                               deferred[buf].as<const uint32_t>(), deferred_pos[buf].as<const uint32_t>(), n_def,
-                               TableDev(this, 1 - buf), StageDevOf(this)));
+    clk.Mark("consume: launch");
+    uint32_t n_def = 0;
     PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
-    buf = 1 - buf;
+    clk.Mark("consume: kernel + publish");
+    int buf = 0;
+    for (int round = 0; n_def > 0; ++round) {
+      // Rows are deferred by a full table / overlong probe, or (fast path) by a long string key.
+      // Grow unless this is the first retry and the table still has room for every deferred row.
+      // Growth is sized by groups, not rows: deferred rows mostly repeat groups, so the table
+      // grows geometrically (x4 per round, from at least 4x the groups it holds) and the retry
+      // defers again while it is still too small; 4 * (groups + deferred rows) caps it.
+      const uint64_t want = static_cast<uint64_t>(inserted) + n_def;
+      if (round > 0 || fast_nk == 0 || want > static_cast<uint64_t>(cap) * 3 / 8) {
+        const uint64_t geo = std::max<uint64_t>(static_cast<uint64_t>(cap) * 4, static_cast<uint64_t>(inserted) * 4);
+        PXG_RETURN_IF_ERROR(Grow(NextPow2(std::min<uint64_t>(geo, 4 * want))));
+      }
+      PXG_RETURN_IF_ERROR(deferred[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
+      PXG_RETURN_IF_ERROR(deferred_pos[1 - buf].Ensure(static_cast<size_t>(n_def) * 4 + 16));
+      PXG_HIP(hipMemsetAsync(counters.as<uint8_t>() + 8, 0, 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "agg_consume_list", AggConsumeListKernel, dim3(GridFor(n_def, kConsumeBlock, ctx->num_cus * 8)),
+                                 dim3(kConsumeBlock), 0, d_plan.as<const AggPlanDev>(), t->d_chunks.as<const DevChunk>(),
+                                 deferred[buf].as<const uint32_t>(), deferred_pos[buf].as<const uint32_t>(), n_def,
+                                 TableDev(this, 1 - buf), StageDevOf(this)));
+      PXG_RETURN_IF_ERROR(PublishNew(t, &n_def));
+      buf = 1 - buf;
+    }
+    return PXG_OK;
+  };
+  // The prefix: ~1/32 of the range (1M..16M rows) in 8192-row tiles, so its launch is one short
+  // round of workgroups.
+  const int64_t pre_rows = (std::min<int64_t>(int64_t(1) << 24, std::max<int64_t>(int64_t(1) << 20, rows / 32)) / kSubRows) * kSubRows;
+  if (rec && inserted == 0 && rows >= 8 * pre_rows) {
+    std::vector<TileRange> pre, rest;
+    const int64_t nt_pre = make_ranges(begin, begin + pre_rows, kSubRows, &pre);
+    const int64_t nt_rest = make_ranges(begin + pre_rows, end, tile_rows, &rest);
+    PXG_RETURN_IF_ERROR(run(d_ranges_pre, last_ranges_pre, pre, nt_pre, pick(false), "agg_consume_prefix"));
+    PXG_RETURN_IF_ERROR(EnsureRecords());  // the prefix may have grown the table
+    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, rest, nt_rest, pick(rec_cap == cap), "agg_consume"));
+  } else {
+    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(rec && rec_cap == cap), "agg_consume"));
   }
   // Keep the table at most ~37% full for the next consume.
   if (inserted > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(static_cast<uint64_t>(inserted) * 4)));
@@ -1351,6 +1493,11 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   for (auto& pf : pool_fix) pf.first->pool = a.d_pool.as<uint8_t>() + pf.second;
   PXG_RETURN_IF_ERROR(a.d_plan.Alloc(sizeof(AggPlanDev)));
   a.fast_nk = FastPathKeys(a.hplan);
+  {
+    bool all_str = a.fast_nk > 0;
+    for (int k = 0; k < a.n_keys; ++k) all_str = all_str && a.key_types[k] == PXG_STRING;
+    a.rec_ok = all_str && a.fast_nk <= kRecMaxKeys;
+  }
   // High-cardinality mode: fast-path keys, integer SUM / MEAN / MINSUM and integer MIN / MAX (LDS
   // integer atomics: order-independent, so the partition tables give deterministic results),
   // at most kHcMaxVals value streams and 4 accumulated UDAs.
@@ -1462,6 +1609,10 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
     PXG_RETURN_IF_ERROR(a.slots.Alloc(static_cast<size_t>(a.cap) * 8));
   }
   PXG_HIP(hipMemsetAsync(a.slots.p, 0, static_cast<size_t>(a.cap) * 8, a.ctx->stream));
+  if (a.rec_dirty && a.rec_cap == a.cap) {  // a record is valid only for a slot word of its own run
+    PXG_HIP(hipMemsetAsync(a.prec.p, 0, static_cast<size_t>(a.cap) * kRecWords * 8, a.ctx->stream));
+    a.rec_dirty = false;
+  }
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));  // stream-ordered before the next consume
   PXG_HIP(hipMemsetAsync(a.hc_maxlen.p, 0, sizeof(a.hc_maxlen_h), a.ctx->stream));
   std::memset(a.hc_maxlen_h, 0, sizeof(a.hc_maxlen_h));

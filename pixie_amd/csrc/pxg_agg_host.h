@@ -50,13 +50,21 @@ struct Agg {
 
   // Global open-addressing table.
   DevBuf slots;
+  // Probe records (pxg_agg.h kRecWords per slot), allocated with the table when the plan
+  // qualifies (rec_ok: consume fast path, all-STRING keys, <= kRecMaxKeys); rec_dirty: written
+  // since the last clear.
+  DevBuf prec;
+  bool rec_ok = false, rec_dirty = false;
+  uint32_t rec_cap = 0;
+  int32_t EnsureRecords();
+  int32_t RebuildRecords();
   uint32_t cap = 0;
   uint32_t min_cap = 1024;  // the capacity the creation hint asked for (reset never shrinks below)
   DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor;
                     // u32 @32 import inserts, @36 import error flags
   DevBuf deferred[2], deferred_pos[2];
-  DevBuf d_ranges;
-  std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
+  DevBuf d_ranges, d_ranges_pre;
+  std::vector<uint8_t> last_ranges, last_ranges_pre;  // host copies of what d_ranges / d_ranges_pre hold
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint32_t last_big_sort_groups = 0;  // pxg_agg_stats.big_sort_groups

@@ -1263,6 +1263,260 @@ __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restric
 }
 
 // ---------------------------------------------------------------------------------------
+// Merged digests (multi-GPU exchange).  An owner rank receives, per group, one
+// contribution from every rank that holds rows of it: the raw values when that rank held at
+// most 8 * delta of them (unprocessed), else the centroid list of its single-pass digest
+// (processed).  The group's digest is tdigest's batch add (add(first, last), the multi-digest
+// form of TDigest::merge, math_sketches.h:38): one k-way merge of the processed lists by mean,
+// the raw values appended unprocessed, then -- since raw values are present or the merged list
+// passes 2 * delta centroids -- one process(): sorted raw values merged in front of equal
+// means, and the greedy pass with the q-scale limits over the total weight.  Restated against
+// oracle/tdigest.h merge_batch (tests/test_digest_merge.py).
+//
+// Items of a group (contiguous after the finalize's grouping, in part order): value = the raw
+// value (the UDA's argument type) or the centroid mean (double bits); wt = part << 48 | weight
+// (weight 0 marks a raw value).  One 512-thread workgroup per merged group:
+//   A. part segments;  B. raw runs sorted in LDS (NaN dropped, as add() drops it) and every run
+//   copied to scratch as (sort key, weight);  C. pairwise stable merge rounds (left run first:
+//   raw runs are listed first, so raw values precede equal centroid means, as inplace_merge
+//   puts the unprocessed range first);  D/E. the greedy pass by one thread over LDS windows;
+//   F/G. min / max as the merge tracks them, tdigest quantile() x7.
+// ---------------------------------------------------------------------------------------
+constexpr int kMergeThreads = 512;
+constexpr int kMergeRawMax = kMergeThreads * kMsIpt;  // 8192: the largest raw run (8 * delta = 8000)
+constexpr int kMergeOutCap = 4096;
+constexpr int kMergeWin = 2048;
+constexpr int kXParts = 64;
+constexpr int kWtPartShift = 48;
+constexpr uint64_t kWtMask = (uint64_t(1) << kWtPartShift) - 1;
+constexpr int64_t kMaxProcessed = 2000;  // 2 * ceil(delta): a merged list above this is processed
+
+__device__ __forceinline__ int64_t MergePathSplit(const uint64_t* __restrict__ A, int64_t na, const uint64_t* __restrict__ B, int64_t nb,
+                                                  int64_t d) {
+  int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (!(B[d - 1 - mid] < A[mid])) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(kMergeThreads) DigestMergeKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ nlist_p,
+                                                                   const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
+                                                                   const uint64_t* __restrict__ wt, int arg_type, uint64_t* __restrict__ mk0,
+                                                                   uint64_t* __restrict__ mw0, uint64_t* __restrict__ mk1,
+                                                                   uint64_t* __restrict__ mw1, double* __restrict__ out,
+                                                                   unsigned int* __restrict__ err) {
+  __shared__ uint64_t s_keys[PaddedLen(kMergeRawMax)];  // raw-run sort; then the greedy windows
+  __shared__ double s_mean[kMergeOutCap];
+  __shared__ int64_t s_start[kMergeOutCap];
+  __shared__ int64_t s_seg[kXParts];
+  __shared__ int64_t s_run[kXParts + 1];
+  __shared__ int64_t s_cnt[2];
+  __shared__ uint64_t s_wred[kMergeThreads / 64];
+  __shared__ int s_nruns, s_nc;
+  __shared__ int64_t s_cursor, s_ncent, s_nraw;
+  __shared__ double s_mn, s_mx;
+  if (blockIdx.x >= *nlist_p) return;
+  const uint32_t g = list[blockIdx.x];
+  const int64_t s = gstart[g], e = gstart[g + 1];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  // A. first item of every part present
+  for (int p = t; p < kXParts; p += kMergeThreads) s_seg[p] = -1;
+  __syncthreads();
+  for (int64_t i = s + t; i < e; i += kMergeThreads) {
+    const uint64_t p = wt[i] >> kWtPartShift;
+    if (i == s || (wt[i - 1] >> kWtPartShift) != p) s_seg[p & (kXParts - 1)] = i;
+  }
+  if (t == 0) {
+    s_cursor = s;
+    s_nruns = 0;
+    s_ncent = 0;
+    s_nraw = 0;
+    s_mn = kDblMax;
+    s_mx = kDblMin;
+  }
+  __syncthreads();
+  // B. raw parts first (each sorted in LDS, NaN dropped), then centroid parts, into (mk0, mw0).
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int p = 0; p < kXParts; ++p) {
+      const int64_t lo = s_seg[p];
+      if (lo < 0) continue;
+      int64_t hi = e;
+      for (int q = p + 1; q < kXParts; ++q)
+        if (s_seg[q] >= 0) {
+          hi = s_seg[q];
+          break;
+        }
+      const bool raw = (wt[lo] & kWtMask) == 0;
+      if (raw != (pass == 0)) continue;
+      const int64_t n = hi - lo;
+      const int64_t at = s_cursor;
+      if (raw) {
+        if (n > kMergeRawMax) {
+          if (t == 0) atomicOr(err, 4u);
+          continue;
+        }
+        int P = 16;
+        while (P < n) P <<= 1;
+        for (int i = t; i < P; i += kMergeThreads) s_keys[PadIdx(i)] = i < n ? QKey(vals[lo + i], arg_type) : ~0ULL;
+        if (t < 2) s_cnt[t] = 0;
+        __syncthreads();
+        MergeSortLds<false>(s_keys, P, t);
+        // NaN keys sort below -inf (negative NaN) and above +inf: count them, keep the rest
+        for (int i = t; i < n; i += kMergeThreads) {
+          const uint64_t k = s_keys[PadIdx(i)];
+          if (k < kNegInfKey) atomicAdd(reinterpret_cast<unsigned long long*>(&s_cnt[0]), 1ULL);
+          else if (k > kPosInfKey) atomicAdd(reinterpret_cast<unsigned long long*>(&s_cnt[1]), 1ULL);
+        }
+        __syncthreads();
+        const int64_t lead = s_cnt[0], keep = n - s_cnt[0] - s_cnt[1];
+        for (int64_t i = t; i < keep; i += kMergeThreads) {
+          mk0[at + i] = s_keys[PadIdx(static_cast<int>(lead + i))];
+          mw0[at + i] = 1;
+        }
+        __syncthreads();
+        if (t == 0 && keep > 0) {
+          s_run[s_nruns++] = at;
+          s_cursor = at + keep;
+          s_nraw += keep;
+        }
+      } else {
+        for (int64_t i = t; i < n; i += kMergeThreads) {
+          mk0[at + i] = SortKeyF(vals[lo + i]);
+          mw0[at + i] = wt[lo + i] & kWtMask;
+        }
+        if (t == 0) {
+          s_run[s_nruns++] = at;
+          s_cursor = at + n;
+          s_ncent += n;
+          s_mn = StdMin(s_mn, AsF(vals[lo]));
+          s_mx = StdMax(s_mx, AsF(vals[hi - 1]));
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) s_run[s_nruns] = s_cursor;
+  __syncthreads();
+  const int64_t end = s_cursor;
+  // C. pairwise stable merge rounds
+  uint64_t *ks = mk0, *ws = mw0, *kd = mk1, *wd = mw1;
+  int R = s_nruns;
+  while (R > 1) {
+    for (int j = 0; 2 * j < R; ++j) {
+      const int64_t a0 = s_run[2 * j], a1 = s_run[2 * j + 1];
+      const int64_t b1 = 2 * j + 1 < R ? s_run[2 * j + 2] : a1;
+      const int64_t na = a1 - a0, nb = b1 - a1, len = na + nb;
+      for (int64_t d0 = 0; d0 < len; d0 += static_cast<int64_t>(kMergeThreads) * kMsIpt) {
+        const int64_t d = d0 + static_cast<int64_t>(t) * kMsIpt;
+        if (d >= len) continue;
+        int64_t ia = MergePathSplit(ks + a0, na, ks + a1, nb, d), ib = d - ia;
+        const int cnt = len - d < kMsIpt ? static_cast<int>(len - d) : kMsIpt;
+        for (int k = 0; k < cnt; ++k) {
+          const bool takeA = ib >= nb || (ia < na && !(ks[a1 + ib] < ks[a0 + ia]));
+          const int64_t src = takeA ? a0 + ia : a1 + ib;
+          kd[a0 + d + k] = ks[src];
+          wd[a0 + d + k] = ws[src];
+          if (takeA) ++ia;
+          else ++ib;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      const int R2 = (R + 1) / 2;
+      for (int j = 0; j < R2; ++j) s_run[j] = s_run[2 * j];
+      s_run[R2] = end;
+    }
+    __syncthreads();
+    R = (R + 1) / 2;
+    uint64_t* x = ks;
+    ks = kd;
+    kd = x;
+    x = ws;
+    ws = wd;
+    wd = x;
+  }
+  // D. total weight (integral)
+  uint64_t wsum = 0;
+  for (int64_t i = s + t; i < end; i += kMergeThreads) wsum += ws[i];
+  wsum = WaveSumU64(wsum);
+  if (lane == 0) s_wred[wid] = wsum;
+  __syncthreads();
+  uint64_t Wt = 0;
+  for (int w = 0; w < kMergeThreads / 64; ++w) Wt += s_wred[w];
+  const bool do_process = s_nraw > 0 || s_ncent > kMaxProcessed;
+  // E. the greedy pass (or, unprocessed, the merged list itself), one thread, LDS windows
+  const double W = static_cast<double>(Wt);
+  double w_so_far = 0, w_limit = 0, cm = 0, cw = 0;
+  int nc = 0;
+  bool ovf = false;
+  uint64_t* s_w = s_keys + kMergeWin;
+  for (int64_t w0 = s; w0 < end; w0 += kMergeWin) {
+    const int64_t wn = end - w0 < kMergeWin ? end - w0 : kMergeWin;
+    for (int64_t i = t; i < wn; i += kMergeThreads) {
+      s_keys[i] = ks[w0 + i];
+      s_w[i] = ws[w0 + i];
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int64_t i = 0; i < wn; ++i) {
+        const double x = QVal(s_keys[i]);
+        const double xw = static_cast<double>(s_w[i]);
+        if (!do_process || (w0 == s && i == 0)) {  // a new centroid per item / the first one
+          if (nc > 0 && nc <= kMergeOutCap) s_mean[nc - 1] = cm;
+          if (nc < kMergeOutCap) s_start[nc] = static_cast<int64_t>(w_so_far);
+          else ovf = true;
+          ++nc;
+          cm = x;
+          cw = xw;
+          w_so_far += xw;
+          if (do_process) w_limit = W * IntegratedQ(1.0);
+          continue;
+        }
+        const double projected = w_so_far + xw;
+        if (projected <= w_limit) {
+          w_so_far = projected;
+          cw += xw;  // Centroid::add
+          cm += xw * (x - cm) / cw;
+        } else {
+          const double k1 = IntegratedLocation(w_so_far / W);
+          w_limit = W * IntegratedQ(k1 + 1.0);
+          if (nc <= kMergeOutCap) s_mean[nc - 1] = cm;
+          if (nc < kMergeOutCap) s_start[nc] = static_cast<int64_t>(w_so_far);
+          else ovf = true;
+          ++nc;
+          w_so_far += xw;
+          cm = x;
+          cw = xw;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (nc > 0 && nc <= kMergeOutCap) s_mean[nc - 1] = cm;
+    if (ovf) atomicOr(err, 8u);
+    s_nc = ovf ? 0 : nc;
+    if (do_process && nc > 0 && !ovf) {
+      s_mn = StdMin(s_mn, s_mean[0]);
+      s_mx = StdMax(s_mx, s_mean[nc - 1]);
+    }
+  }
+  __syncthreads();
+  // G. quantile() x7
+  if (t < 7) {
+    const int64_t ncv = s_nc;
+    out[static_cast<uint64_t>(g) * 7 + t] =
+        DigestQuantileMM(kQuantileQ[t], ncv, static_cast<int64_t>(Wt), [&](int64_t j) -> int64_t { return s_start[j]; },
+                         [&](int64_t j) -> double { return s_mean[j]; }, s_mn, s_mx);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Big groups by selection.  A digest reads at most 4 centroid means per quantile, each the
 // mean of a known range of sorted ranks (the chain depends on W only), so a big group is never
 // sorted.  Its values are binned by splitters taken from a sorted sample (BigSample), the bins
@@ -3043,6 +3297,28 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
     }
   }
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  return PXG_OK;
+}
+
+// Diagnostics: one merged digest (DigestMergeKernel) over n items already in part order
+// (tests/test_digest_merge.py compares it with oracle/tdigest.h merge_batch).
+extern "C" int32_t pxg_digest_merge(pxg_ctx* ctx, const uint64_t* d_vals, const uint64_t* d_wt, int64_t n, int32_t arg_type, double* d_out7) {
+  if (!ctx || !d_vals || !d_wt || !d_out7 || n <= 0 || n >= (int64_t(1) << 31)) return SetError(PXG_INVALID_ARGUMENT, "bad pxg_digest_merge arguments");
+  Ctx* c = &ctx->impl;
+  DevBuf scratch;
+  PXG_RETURN_IF_ERROR(scratch.Alloc(static_cast<size_t>(n) * 32 + 64));
+  uint64_t* k0 = scratch.as<uint64_t>();
+  uint32_t* meta = reinterpret_cast<uint32_t*>(k0 + 4 * n);
+  const uint32_t hmeta[4] = {0u, 1u, 0u, static_cast<uint32_t>(n)};  // list {0}, count 1, gstart {0, n}
+  PXG_HIP(hipMemcpyAsync(meta, hmeta, sizeof(hmeta), hipMemcpyHostToDevice, c->stream));
+  PXG_HIP(hipMemsetAsync(meta + 4, 0, 4, c->stream));
+  PXG_RETURN_IF_ERROR(Launch(c, "digest_merge", DigestMergeKernel, dim3(1), dim3(kMergeThreads), 0, static_cast<const uint32_t*>(meta),
+                             static_cast<const uint32_t*>(meta + 1), static_cast<const uint32_t*>(meta + 2), d_vals, d_wt, arg_type, k0, k0 + n,
+                             k0 + 2 * n, k0 + 3 * n, d_out7, meta + 4));
+  uint32_t errv = 0;
+  PXG_HIP(hipMemcpyAsync(&errv, meta + 4, 4, hipMemcpyDeviceToHost, c->stream));
+  PXG_HIP(hipStreamSynchronize(c->stream));
+  if (errv) return SetError(PXG_INTERNAL, "merged digest overflow (flags %u)", errv);
   return PXG_OK;
 }
 

@@ -193,7 +193,9 @@ inline int32_t LaunchOn(Ctx* ctx, hipStream_t stream, const char* name, void (*k
                         size_t shmem, Args&&... args) {
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return PXG_OK;
   hipEvent_t s0 = nullptr, s1 = nullptr;
-  const bool timed = ctx->profiling && (ctx->profile_only.empty() || ctx->profile_only == name);
+  // profile_only selects the launches whose name starts with it ("agg_consume" also times
+  // "agg_consume_prefix", the probe-record prefix launch).
+  const bool timed = ctx->profiling && (ctx->profile_only.empty() || std::strncmp(name, ctx->profile_only.c_str(), ctx->profile_only.size()) == 0);
   if (timed) {
     s0 = ctx->GetEvent();
     s1 = ctx->GetEvent();

@@ -100,6 +100,40 @@ __device__ double DigestQuantile(double q, int64_t nc, int64_t W, StartF start, 
   return WeightedAverage(mean(nc - 1), z1, mx, z2);
 }
 
+// tdigest::quantile() of a processed digest whose min_ / max_ are given explicitly (a merged
+// digest: the merge tracks them from the merged lists' ends, not from its own first / last
+// centroid), same interpolation as DigestQuantile.
+template <typename StartF, typename MeanF>
+__device__ double DigestQuantileMM(double q, int64_t nc, int64_t W, StartF start, MeanF mean, double mn, double mx) {
+  if (nc <= 0) return __longlong_as_double(0x7FF8000000000000LL);
+  if (nc == 1) return mean(0);
+  const double Wd = static_cast<double>(W);
+  const double index = q * Wd;
+  auto weight = [&](int64_t j) -> double {
+    return static_cast<double>((j + 1 < nc ? start(j + 1) : W) - start(j));
+  };
+  auto cum = [&](int64_t j) -> double {
+    return j < nc ? static_cast<double>(start(j)) + weight(j) / 2.0 : Wd;
+  };
+  const double w0 = weight(0);
+  if (index <= w0 / 2.0) return mn + 2.0 * index / w0 * (mean(0) - mn);
+  int64_t lo = 0, hi = nc;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cum(mid) < index) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < nc) {
+    const double z1 = index - cum(lo - 1);
+    const double z2 = cum(lo) - index;
+    return WeightedAverage(mean(lo - 1), z2, mean(lo), z1);
+  }
+  const double wl = weight(nc - 1);
+  const double z1 = index - Wd - wl / 2.0;
+  const double z2 = wl / 2 - z1;
+  return WeightedAverage(mean(nc - 1), z1, mx, z2);
+}
+
 // Singleton digest (W <= kSingletonMaxW): centroid j = value j.
 template <typename ValF>
 __device__ __forceinline__ double SingletonQuantile(double q, int64_t W, ValF val) {

@@ -56,6 +56,10 @@ def load():
     lib.oracle_tdigest_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
     lib.oracle_tdigest_merge_quantiles.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64,
                                                    C.POINTER(C.c_double)]
+    lib.oracle_tdigest_centroids.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                             C.c_int64, C.POINTER(C.c_int64)]
+    lib.oracle_tdigest_batch_quantiles.argtypes = [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.oracle_quantiles_json.argtypes = [C.POINTER(C.c_double), C.c_int64, C.c_char_p, C.c_int32]
     lib.oracle_quantiles_json.restype = C.c_int32
     lib.oracle_pluck_float64.argtypes = [C.c_char_p, C.c_char_p]
@@ -199,6 +203,47 @@ def tdigest_merge_quantiles(a_vals, b_vals) -> List[float]:
     out = (C.c_double * 7)()
     lib.oracle_tdigest_merge_quantiles(a.ctypes.data_as(C.POINTER(C.c_double)), len(a),
                                        b.ctypes.data_as(C.POINTER(C.c_double)), len(b), out)
+    return list(out)
+
+
+def tdigest_centroids(vals, cap: int = 8192):
+    """TDigest::FromValuesOnce(vals): the single-pass digest a rank ships (means, weights)."""
+    lib = load()
+    a = np.ascontiguousarray(np.asarray(vals, dtype=np.float64))
+    m = np.zeros(cap, np.float64)
+    w = np.zeros(cap, np.float64)
+    nc = C.c_int64()
+    lib.oracle_tdigest_centroids(a.ctypes.data_as(C.POINTER(C.c_double)), len(a), m.ctypes.data_as(C.POINTER(C.c_double)),
+                                 w.ctypes.data_as(C.POINTER(C.c_double)), cap, C.byref(nc))
+    assert nc.value >= 0
+    return m[:nc.value].copy(), w[:nc.value].copy()
+
+
+def tdigest_batch_quantiles(parts) -> List[float]:
+    """TDigest::merge_batch over parts = [("raw", values) | ("centroids", (means, weights))], then
+    quantile() x7."""
+    lib = load()
+    kinds, counts, data, weights = [], [], [], []
+    for kind, payload in parts:
+        if kind == "raw":
+            v = np.asarray(payload, np.float64)
+            kinds.append(0)
+            counts.append(len(v))
+            data.append(v)
+            weights.append(np.zeros(len(v)))
+        else:
+            m, w = payload
+            kinds.append(1)
+            counts.append(len(m))
+            data.append(np.asarray(m, np.float64))
+            weights.append(np.asarray(w, np.float64))
+    k = np.asarray(kinds, np.int32)
+    c = np.asarray(counts, np.int64)
+    d = np.ascontiguousarray(np.concatenate(data) if data else np.zeros(0))
+    w = np.ascontiguousarray(np.concatenate(weights) if weights else np.zeros(0))
+    out = (C.c_double * 7)()
+    lib.oracle_tdigest_batch_quantiles(len(k), k.ctypes.data_as(C.POINTER(C.c_int32)), c.ctypes.data_as(C.POINTER(C.c_int64)),
+                                       d.ctypes.data_as(C.POINTER(C.c_double)), w.ctypes.data_as(C.POINTER(C.c_double)), out)
     return list(out)
 
 

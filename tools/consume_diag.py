@@ -28,8 +28,9 @@ def child(rows, steps):
         agg.reset(); agg.consume(t)
     ctx.sync(); ctx.set_profiling(False)
     n, ms = ctx.kernel_stats("agg_consume")
-    print(json.dumps({"mode": os.environ.get("PXG_DIAG_CONSUME", "0"), "launches_per_step": n / steps,
-                      "consume_ms_per_step": ms / steps,
+    n0, ms0 = ctx.kernel_stats("agg_consume_prefix")  # the probe-record prefix launch, when it runs
+    print(json.dumps({"mode": os.environ.get("PXG_DIAG_CONSUME", "0"), "launches_per_step": (n + n0) / steps,
+                      "consume_ms_per_step": (ms + ms0) / steps, "prefix_ms_per_step": ms0 / steps,
                       "ms_per_launch": ms / max(n, 1)}), flush=True)
 
 
