@@ -1036,6 +1036,7 @@ int32_t Agg::Grow(uint32_t new_cap) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "stage_remap", StageRemapKernel, dim3(GridFor(static_cast<int64_t>(st_n), 256, 1 << 30)), dim3(256), 0,
                                st_slot.as<uint32_t>(), st_n, remap.as<const uint32_t>()));
   }
+  PXG_RETURN_IF_ERROR(MaccFollowGrow(this, slots.as<const unsigned long long>(), cap, remap.as<const uint32_t>(), new_cap));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   slots = std::move(ns);
   cap = new_cap;
@@ -1492,6 +1493,33 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   if (!pool.empty()) PXG_HIP(hipMemcpy(a.d_pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
   for (auto& pf : pool_fix) pf.first->pool = a.d_pool.as<uint8_t>() + pf.second;
   PXG_RETURN_IF_ERROR(a.d_plan.Alloc(sizeof(AggPlanDev)));
+  // Exchange states (pxg_xchg.hip): Serialize() sizes of every non-quantile UDA
+  // (math_ops.h:583-772: count / sum / min / max 8 bytes, MeanInfo 16).
+  {
+    a.hplan_x = a.hplan;
+    bool ok = !a.windowed && !a.emit_states && a.n_keys > 0;
+    int32_t so = 0, mw = 0;
+    for (int u = 0; u < a.n_udas; ++u) {
+      const int k = a.uda_kind[u];
+      a.hplan_x.state_off[u] = 0;
+      a.macc_off[u] = -1;
+      if (k == PXG_UDA_QUANTILES) {
+        if (a.x_qval >= 0 && a.x_qval != a.uda_val[u]) ok = false;
+        a.x_qval = a.uda_val[u];
+        continue;
+      }
+      if (k == PXG_UDA_MINSUM || k == PXG_UDA_MEAN_MERGE) ok = false;
+      a.hplan_x.state_off[u] = so;
+      so += k == PXG_UDA_MEAN ? 16 : 8;
+      a.macc_off[u] = mw;
+      mw += k == PXG_UDA_MEAN ? 2 : 1;
+    }
+    a.hplan_x.state_rec = so;
+    a.hplan_x.emit_states = 0;
+    a.macc_words = mw + 1;  // + the flags word
+    a.x_ok = ok;
+    PXG_RETURN_IF_ERROR(a.d_plan_x.Alloc(sizeof(AggPlanDev)));
+  }
   a.fast_nk = FastPathKeys(a.hplan);
   {
     bool all_str = a.fast_nk > 0;
@@ -1531,6 +1559,7 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   }
   a.hint_groups = spec->expected_groups;
   PXG_HIP(hipMemcpy(a.d_plan.p, &a.hplan, sizeof(AggPlanDev), hipMemcpyHostToDevice));
+  PXG_HIP(hipMemcpy(a.d_plan_x.p, &a.hplan_x, sizeof(AggPlanDev), hipMemcpyHostToDevice));
   PXG_RETURN_IF_ERROR(a.counters.Alloc(64));
   PXG_HIP(hipMemsetAsync(a.counters.p, 0, 64, a.ctx->stream));
   PXG_RETURN_IF_ERROR(a.hc_maxlen.Alloc(sizeof(a.hc_maxlen_h)));
@@ -1564,6 +1593,7 @@ extern "C" int32_t pxg_agg_consume(pxg_agg* agg, pxg_table* table, int64_t begin
   PXG_RETURN_IF_ERROR(t.FlushStage());
   if (begin < 0 || end > t.nrows || begin > end) return SetError(PXG_INVALID_ARGUMENT, "row range [%lld,%lld) outside table of %lld rows", (long long)begin, (long long)end, (long long)t.nrows);
   if (t.ctx != agg->impl.ctx) return SetError(PXG_INVALID_ARGUMENT, "table and agg belong to different contexts");
+  if (agg->impl.merged) return SetError(PXG_FAILED_PRECONDITION, "this aggregation holds merged partial states; reset it before consuming rows");
   agg->impl.res.ready = false;
   agg->impl.state_version++;
   return agg->impl.ConsumeRange(&t, begin, end);
@@ -1619,6 +1649,10 @@ extern "C" int32_t pxg_agg_reset(pxg_agg* agg) {
   a.st_n = 0;
   a.hc_n = 0;
   a.hc_active = false;
+  a.merged = false;    // accumulators are re-initialised by the next merged import
+  a.macc_cap = 0;
+  a.x_parts_seen = 0;
+  a.xc.valid = false;
   a.arena_words = 0;
   a.inserted = 0;
   a.state_version++;

@@ -48,6 +48,30 @@ struct Agg {
   DevBuf d_plan;
   DevBuf d_pool;
 
+  // Multi-GPU exchange of partial states (pxg_xchg.hip).  hplan_x: the plan with
+  // every non-quantile UDA's Serialize() state laid out per group (GroupCombine writes them in
+  // export mode); x_ok: the plan can exchange states (no windowing / partial-emit / MINSUM /
+  // MEAN_MERGE, all quantile UDAs on one value stream x_qval, -1: none).
+  AggPlanDev hplan_x;
+  DevBuf d_plan_x;
+  bool x_ok = false;
+  int32_t x_qval = -1;
+  bool export_x = false;       // finalize runs for an export: states + centroid lists, below
+  const uint64_t* x_vals = nullptr;  // after an export finalize: the grouped quantile stream
+  uint32_t x_nbig = 0;               // ... and its big groups (ws.big / ws.xcent / ws.xcnt)
+  // Owner side: imported states merged per slot (macc: macc_words u64 per slot at macc_off[u],
+  // plus a flags word) and quantile items staged with a weight stream (st_wt: part << 48 |
+  // weight, 0 = raw value).  merged: this run holds imported states (consume refused).
+  bool merged = false;
+  DevBuf macc, st_wt;
+  uint32_t macc_cap = 0;
+  int32_t macc_words = 0;
+  int32_t macc_off[kMaxUdas] = {0};
+  int32_t x_parts_seen = 0;   // part index of the next imported part (weights carry it)
+  int32_t EnsureMacc();
+  int32_t FinalizeMerged();
+  const uint64_t* x_wts = nullptr;  // after a merged finalize: the grouped item weights
+
   // Global open-addressing table.
   DevBuf slots;
   // Probe records (pxg_agg.h kRecWords per slot), allocated with the table when the plan
@@ -111,6 +135,8 @@ struct Agg {
     int32_t n_parts = 0;
     uint64_t version = 0;
     DevBuf part_of, words, slist, grank, koff, rdigit, rlist, starts, hist, scan, scan2, desc, remap;
+    bool v2 = false;  // the cache describes an exchange-v2 (partial states) export
+    uint64_t G = 0;   // v2: groups of the export finalize
     std::vector<uint64_t> g_start, r_start, k_start;  // per part (+ total): groups, rows, key words
   } xc;
 
@@ -128,6 +154,9 @@ struct Agg {
     // staging split (pxg_finalize.hip): sampled slot counts, flag scan, bucket x tile counts,
     // bucket totals / bases
     DevBuf split_cnt, split_flags, split_hist, split_tot;
+    // export mode: per-group states, centroid lists of the big groups (kXCentCap per big group)
+    // and their counts; owner side: merged digests' scratch, digest group list
+    DevBuf xstates, xcent, xcnt, mrg, dlist;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);
@@ -142,12 +171,22 @@ struct Agg {
   int32_t ExportPartial(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
   int32_t ImportPartial(const void* src, int64_t nbytes);
   int32_t ImportPartials(const void* src, int32_t n, const int64_t* offs, const int64_t* sizes);
+  // Exchange v2 (partial UDA states, pxg_partial.hip).
+  int32_t ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
+  int32_t ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* offs, const int64_t* sizes, const void* hdrs);
 };
 
 // Finalize stages (pxg_finalize.hip): the table path, then (high-cardinality mode) the
 // partition records appended after its groups (pxg_hc.hip).
 int32_t AggFinalizeImpl(Agg* agg);
 int32_t AggFinalizeTable(Agg* agg);
+// Merged digests of the groups listed in dlist (count on the device, at most cap_list) into
+// every quantile UDA's output (pxg_finalize.hip; synchronises and checks its flags).
+int32_t LaunchDigestMerge(Agg* a, const uint32_t* dlist, const uint32_t* dcount, uint32_t cap_list);
+// Exchange v2 helpers (pxg_partial.hip): is the plan exchanging states; the accumulators of a
+// merged aggregation following a table growth.
+bool ExchangeV2(const Agg& a);
+int32_t MaccFollowGrow(Agg* a, const unsigned long long* old_slots, uint32_t old_cap, const uint32_t* remap, uint32_t new_cap);
 
 // Groups the hint (or the last run) must reach before a qualifying plan stages partition
 // records (PXG_HC_MIN_GROUPS overrides; tests use it at small sizes, 0 disables).

@@ -1262,6 +1262,67 @@ __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restric
               PreChainAt(chain_starts, chain_nc, blockIdx.x, static_cast<int64_t>(G.n)), out + static_cast<uint64_t>(G.g) * 7, err, sh);
 }
 
+// Exchange export: the complete single-pass digest of a big group (what one rank ships for a
+// group of more than 8 * delta values, oracle TDigest::FromValuesOnce): NaN trimmed, centroid
+// boundaries from the precomputed chain (or the sequential one), every centroid's mean and
+// weight -- the reference's incremental mean for centroids of <= kSeqMean values, sum / count
+// above, as BlockDigest.  xcnt[b] = the centroid count, or -1 when the group ships its values.
+constexpr int kXCentCap = kChainCap;
+constexpr int64_t kXRawMax = 8000;  // 8 * delta
+__global__ void __launch_bounds__(256) CentroidListKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ ngroups_p,
+                                                          const uint64_t* __restrict__ keysA, const uint64_t* __restrict__ keysB,
+                                                          uint32_t* __restrict__ starts_all, const uint32_t* __restrict__ chain_starts,
+                                                          const int32_t* __restrict__ chain_nc, uint64_t* __restrict__ xcent,
+                                                          int32_t* __restrict__ xcnt) {
+  __shared__ int64_t s_meta[3];
+  if (blockIdx.x >= *ngroups_p) return;
+  const BigGroup G = groups[blockIdx.x];
+  const uint64_t* k = ((G.passes & 1) ? keysB : keysA) + G.off;
+  const int64_t n = static_cast<int64_t>(G.n);
+  const int t = threadIdx.x;
+  auto keyat = [&](int64_t i) -> uint64_t { return k[i]; };
+  if (t == 0) {
+    const int64_t lead = LowerBoundKey(keyat, n, kNegInfKey);
+    const int64_t tail = LowerBoundKey(keyat, n, kPosInfKey + 1);
+    s_meta[0] = lead;
+    s_meta[1] = tail - lead;
+    s_meta[2] = -1;
+  }
+  __syncthreads();
+  const int64_t lead = s_meta[0], W = s_meta[1];
+  if (W <= kXRawMax) {
+    if (t == 0) xcnt[blockIdx.x] = -1;
+    return;
+  }
+  uint32_t* starts_buf = starts_all + static_cast<uint64_t>(blockIdx.x) * kBigCentroids;
+  const PreChain pre = PreChainAt(chain_starts, chain_nc, blockIdx.x, n);
+  const bool use_pre = pre.starts != nullptr && pre.W == W && pre.nc >= 0;
+  const uint32_t* starts = use_pre ? pre.starts : starts_buf;
+  if (t == 0) s_meta[2] = use_pre ? pre.nc : DigestBoundaries(W, starts_buf, kXCentCap);
+  __syncthreads();
+  const int64_t nc = s_meta[2];
+  if (nc < 0 || nc > kXCentCap) {
+    if (t == 0) xcnt[blockIdx.x] = -2;  // cannot happen for delta = 1000 (<= ~1600 centroids)
+    return;
+  }
+  auto val = [&](int64_t j) -> double { return QVal(k[lead + j]); };
+  uint64_t* out = xcent + static_cast<uint64_t>(blockIdx.x) * kXCentCap * 2;
+  for (int64_t j = t; j < nc; j += blockDim.x) {
+    const int64_t s = starts[j], e = j + 1 < nc ? starts[j + 1] : W;
+    double m;
+    if (e - s <= kSeqMean) {
+      m = CentroidMean(val, s, e);
+    } else {
+      double acc = 0;
+      for (int64_t x = s; x < e; ++x) acc += val(x);
+      m = acc / static_cast<double>(e - s);
+    }
+    out[2 * j] = FBits(m);
+    out[2 * j + 1] = static_cast<uint64_t>(e - s);
+  }
+  if (t == 0) xcnt[blockIdx.x] = static_cast<int32_t>(nc);
+}
+
 // ---------------------------------------------------------------------------------------
 // Merged digests (multi-GPU exchange).  An owner rank receives, per group, one
 // contribution from every rank that holds rows of it: the raw values when that rank held at
@@ -2623,6 +2684,9 @@ int32_t AggFinalizeTable(Agg* a) {
     return PXG_OK;
   }
   if (n >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
+  // Streams the grouping moves: the plan's value streams, plus (owner of a merged exchange) the
+  // imported items' weights after them.
+  const int nvs = a->n_vals + (a->merged ? 1 : 0);
   PXG_RETURN_IF_ERROR(ws.meta.Ensure(64));
   uint8_t* meta = ws.meta.as<uint8_t>();
   uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta + 8);
@@ -2745,7 +2809,7 @@ int32_t AggFinalizeTable(Agg* a) {
   //    left as it is (slots), so finalize can run again and export still works.
   for (int b = 0; b < 2; ++b) {
     PXG_RETURN_IF_ERROR(ws.skey[b].Ensure(n * 4 + 16));
-    for (int v = 0; v < a->n_vals; ++v) PXG_RETURN_IF_ERROR(ws.sval[b][v].Ensure(n * 8 + 16));
+    for (int v = 0; v < nvs; ++v) PXG_RETURN_IF_ERROR(ws.sval[b][v].Ensure(n * 8 + 16));
   }
   PXG_RETURN_IF_ERROR(ws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(n, a->cap) + 1)) + 64));
   scan_tmp = ws.scan.p;
@@ -2754,14 +2818,15 @@ int32_t AggFinalizeTable(Agg* a) {
   ValPtrs vbuf[2];
   for (int b = 0; b < 2; ++b) {
     kbuf[b] = ws.skey[b].as<uint32_t>();
-    for (int v = 0; v < kMaxVals; ++v) vbuf[b].p[v] = v < a->n_vals ? ws.sval[b][v].as<uint64_t>() : nullptr;
+    for (int v = 0; v < kMaxVals; ++v) vbuf[b].p[v] = v < nvs ? ws.sval[b][v].as<uint64_t>() : nullptr;
   }
   for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
+  if (a->merged) vin.p[a->n_vals] = a->st_wt.as<const uint64_t>();  // the imported items' weights ride along
   const uint32_t* kin = nullptr;
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
   if (!split) {
-    PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, a->n_vals,
+    PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, nvs,
                                          n, kbuf, vbuf, ws.rs, &kin, &vin));
     PXG_RETURN_IF_ERROR(IssueKeys());
     const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
@@ -2797,7 +2862,7 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_HIP(hipEventRecord(ctx->ev_split, ctx->stream));
     ValPtrs vrest = vbuf[1], vout = vbuf[fin];
     PXG_RETURN_IF_ERROR(Launch(ctx, "split_scatter", SplitScatterKernel, dim3(ntiles), dim3(kSplitBlock), 0, a->st_slot.as<const uint32_t>(),
-                               vin, a->n_vals, n, a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups,
+                               vin, nvs, n, a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups,
                                static_cast<const uint32_t*>(hist), ntiles, kbuf[1], vrest, vout));
     PXG_RETURN_IF_ERROR(IssueKeys());
     clk.Mark("finalize: issue split");
@@ -2814,7 +2879,7 @@ int32_t AggFinalizeTable(Agg* a) {
       ConstValPtrs rin;
       for (int v = 0; v < kMaxVals; ++v) rin.p[v] = vrest.p[v];
       // the rest records carry their slots: the first pass maps them to rest ids (< Gr)
-      PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], ws.rank.as<const uint32_t>(), a->cap, ngroups, rin, a->n_vals, n_rest, kbuf, vbuf,
+      PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], ws.rank.as<const uint32_t>(), a->cap, ngroups, rin, nvs, n_rest, kbuf, vbuf,
                                            ws.rs, &kin, &vin));
       PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n_rest), 256, 1 << 30)), dim3(256), 0,
                                  kin, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
@@ -2858,12 +2923,17 @@ int32_t AggFinalizeTable(Agg* a) {
     }
   }
   uint8_t* states = nullptr;
+  const AggPlanDev* cplan = a->d_plan.as<const AggPlanDev>();
   if (a->emit_states && a->state_rec > 0) {
     PXG_RETURN_IF_ERROR(R.states.Ensure(static_cast<size_t>(ngroups) * a->state_rec + 16));
     states = R.states.as<uint8_t>();
+  } else if (a->export_x && a->hplan_x.state_rec > 0) {  // exchange export: every group's Serialize() states
+    PXG_RETURN_IF_ERROR(ws.xstates.Ensure(static_cast<size_t>(ngroups) * a->hplan_x.state_rec + 16));
+    states = ws.xstates.as<uint8_t>();
+    cplan = a->d_plan_x.as<const AggPlanDev>();
   }
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                             a->d_plan.as<const AggPlanDev>(), gstart, static_cast<const uint32_t*>(cbase), ngroups,
+                             cplan, gstart, static_cast<const uint32_t*>(cbase), ngroups,
                              ws.partial.as<const uint64_t>(), max_chunks, uo, states));
   return PXG_OK;
   };
@@ -2894,9 +2964,17 @@ int32_t AggFinalizeTable(Agg* a) {
                                    dst->as<uint64_t>(), w, pass));
       std::swap(src, dst);
     }
-    return LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+                                 static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
+                                 ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err));
+    if (!a->export_x) return PXG_OK;
+    // Exchange export: each big group's whole single-pass centroid list (those of > 8 * delta
+    // values ship it instead of their values).
+    PXG_RETURN_IF_ERROR(ws.xcent.Ensure(static_cast<size_t>(n_big_groups) * kXCentCap * 16 + 16));
+    PXG_RETURN_IF_ERROR(ws.xcnt.Ensure(static_cast<size_t>(n_big_groups) * 4 + 16));
+    return LaunchOn(ctx, st, "quant_big_digest", CentroidListKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
                     static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
-                    ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err);
+                    ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, ws.xcent.as<uint64_t>(), ws.xcnt.as<int32_t>());
   };
   // Selection path, first half (needs the sorted values and the chunk list only): sample,
   // splitters, bin counts.
@@ -3027,7 +3105,7 @@ int32_t AggFinalizeTable(Agg* a) {
     big_max = hm[5];
     n_bchunks = hm[4];
     // PXG_BIG_SORT=1 forces the full sort path for every big group (tests compare the two).
-    big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT");
+    big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT") && !a->export_x;
     if (big_select) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
       PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8));
@@ -3120,6 +3198,9 @@ int32_t AggFinalizeTable(Agg* a) {
     err = pin32[kMaxKeys];
   }
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
+  a->x_vals = a->x_qval >= 0 ? cv.p[a->x_qval] : nullptr;
+  a->x_wts = a->merged ? cv.p[a->n_vals] : nullptr;
+  a->x_nbig = n_big_groups;
   if (g_dev != ngroups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, ngroups);
   for (int k = 0; k < a->n_keys; ++k)
     if (a->key_types[k] == PXG_STRING) R.key_data_len[k] = totals[k];
@@ -3297,6 +3378,28 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
     }
   }
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  return PXG_OK;
+}
+
+int32_t pxg::LaunchDigestMerge(Agg* a, const uint32_t* dlist, const uint32_t* dcount, uint32_t cap_list) {
+  Ctx* ctx = a->ctx;
+  if (!a->x_vals || !a->x_wts || cap_list == 0) return PXG_OK;
+  const uint64_t n = a->st_n;
+  Agg::FinalizeWs& ws = a->ws;
+  PXG_RETURN_IF_ERROR(ws.mrg.Ensure(n * 32 + 64));
+  uint64_t* k0 = ws.mrg.as<uint64_t>();
+  uint32_t* d_err = reinterpret_cast<uint32_t*>(ws.meta.as<uint8_t>() + 16);
+  PXG_HIP(hipMemsetAsync(d_err, 0, 4, ctx->stream));
+  for (int u = 0; u < a->n_udas; ++u) {
+    if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "digest_merge", DigestMergeKernel, dim3(cap_list), dim3(kMergeThreads), 0, dlist, dcount,
+                               ws.gstart.as<const uint32_t>(), a->x_vals, a->x_wts, a->uda_arg_type[u], k0, k0 + n, k0 + 2 * n, k0 + 3 * n,
+                               a->res.uda_out[u].as<double>(), d_err));
+  }
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 120);
+  PXG_HIP(hipMemcpyAsync(pin, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  if (*pin) return SetError(PXG_INTERNAL, "merged digest overflow (flags %u)", *pin);
   return PXG_OK;
 }
 

@@ -701,6 +701,7 @@ int32_t Agg::SpillHc() {
 }
 
 int32_t AggFinalizeImpl(Agg* a) {
+  if (a->merged) return a->FinalizeMerged();  // imported partial states (pxg_partial.hip)
   PXG_RETURN_IF_ERROR(AggFinalizeTable(a));  // the table path (high-cardinality mode: rows with long keys)
   if (!a->hc_active) return PXG_OK;
   return a->FinalizeHc();

@@ -23,6 +23,7 @@
 #include "pxg_agg_host.h"
 #include "pxg_keys.h"
 #include "pxg_scan.h"
+#include "pxg_tdigest.h"
 
 namespace pxg {
 
@@ -42,6 +43,34 @@ struct PartHeader {
   uint64_t reserved[2];
 };
 static_assert(sizeof(PartHeader) == 64, "PartHeader is 64 bytes");
+
+// Exchange v2 part header (partial states; layout below, XLayoutOf).
+constexpr uint32_t kXMagic = 0x58475850u;  // "PXGX"
+constexpr uint32_t kXVersion = 2;
+constexpr int kXCentCapH = 2048;  // = kXCentCap (pxg_finalize.hip)
+constexpr uint64_t kXFlagDigest = 1;
+constexpr int kXWtShift = 48;
+
+struct XHeader {
+  uint32_t magic;
+  uint32_t version;
+  uint32_t n_keys;
+  uint32_t state_rec;
+  uint64_t n_groups;
+  uint64_t n_items;
+  uint64_t key_words;
+  uint64_t plan_sig;
+  uint64_t has_q;
+  uint64_t reserved;
+};
+static_assert(sizeof(XHeader) == 64, "XHeader is 64 bytes");
+
+static bool IsXPart(const void* hdr_host) {
+  uint32_t m = 0;
+  std::memcpy(&m, hdr_host, 4);
+  return m == kXMagic;
+}
+
 
 static inline uint64_t Align8(uint64_t x) { return (x + 7) & ~uint64_t(7); }
 
@@ -442,6 +471,16 @@ int32_t Agg::ImportPartials(const void* src, int32_t n, const int64_t* offs, con
     PXG_HIP(hipMemcpyAsync(&H[i], base8 + offs[i], sizeof(PartHeader), hipMemcpyDeviceToHost, ctx->stream));
   }
   PXG_HIP(hipStreamSynchronize(ctx->stream));
+  // Exchange v2 parts (partial states) have their own header and merge.
+  int nx = 0;
+  for (int i = 0; i < n; ++i) nx += IsXPart(&H[i]) ? 1 : 0;
+  if (nx == n) {
+    std::vector<XHeader> XH(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) std::memcpy(&XH[i], &H[i], sizeof(XHeader));
+    return ImportPartialsV2(base8, n, offs, sizes, XH.data());
+  }
+  if (nx > 0) return SetError(PXG_INVALID_ARGUMENT, "row parts and partial-state parts cannot be imported together");
+  if (merged) return SetError(PXG_FAILED_PRECONDITION, "row parts cannot join an aggregation that merged partial states");
   uint64_t tot_groups = 0, tot_rows = 0, tot_words = 0;
   std::vector<PartLayout> L(static_cast<size_t>(n));
   for (int i = 0; i < n; ++i) {
@@ -524,6 +563,539 @@ int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
   return ImportPartials(src, 1, &off, &nbytes);
 }
 
+// ---------------------------------------------------------------------------------------
+// Exchange v2: partial UDA states (partial_op_mgr.cc:69-83, math_ops.h:590-609,
+// math_sketches.h:38).  Per group a part carries the group's key record, its Serialize() state
+// record (count / sum / min / max 8 bytes, MeanInfo {size, sum} 16 bytes; hplan_x), and its
+// quantile contribution: the raw values when this rank holds <= 8 * delta of them (kept
+// bit-exact: a group of <= 8000 values anywhere is <= 8000 on every rank), else the centroid
+// list of its single-pass digest (<= 2 * delta centroids; CentroidListKernel).  The owner merges
+// states into per-slot accumulators and digests with DigestMergeKernel (pxg_finalize.hip).
+//
+// Part layout (8-byte aligned sections):
+//   XHeader (64 B) | koff u64[G] | keys u64[KW] | states u8[G * state_rec] | gid u32[I] (pad) |
+//   vals u64[I] | wts u64[I]   (wts: centroid weight, 0 for a raw value)
+// ---------------------------------------------------------------------------------------
+
+
+struct XLayout {
+  uint64_t koff, keys, states, gid, vals, wts, bytes;
+};
+static XLayout XLayoutOf(uint64_t ng, uint64_t ni, uint64_t kw, uint64_t srec) {
+  XLayout L;
+  L.koff = sizeof(XHeader);
+  L.keys = L.koff + ng * 8;
+  L.states = L.keys + kw * 8;
+  L.gid = L.states + Align8(ng * srec);
+  L.vals = L.gid + Align8(ni * 4);
+  L.wts = L.vals + ni * 8;
+  L.bytes = L.wts + ni * 8;
+  return L;
+}
+
+static uint64_t XPlanSig(const Agg& a) {
+  uint64_t h = PlanSig(a) ^ 0x9E3779B97F4A7C15ULL;
+  for (int u = 0; u < a.n_udas; ++u) h = (h ^ static_cast<uint64_t>(a.uda_kind[u] * 31 + a.uda_arg_type[u])) * 1099511628211ULL;
+  return h;
+}
+
+__global__ void XBigIndexKernel(const uint32_t* __restrict__ big_g, uint32_t nbig, int32_t* __restrict__ xbig) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nbig) xbig[big_g[b]] = static_cast<int32_t>(b);
+}
+
+// Per dense group: its part, key-record words and item count.
+__global__ void XGroupPartKernel(const AggPlanDev* __restrict__ plan, const unsigned long long* __restrict__ slots,
+                                 const uint32_t* __restrict__ gslot, uint32_t G, const uint64_t* __restrict__ arena, uint32_t n_parts,
+                                 const uint32_t* __restrict__ gstart, const int32_t* __restrict__ xbig, const int32_t* __restrict__ xcnt,
+                                 int has_q, uint8_t* __restrict__ gpart, uint64_t* __restrict__ kw, uint64_t* __restrict__ ic) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  KeySet k;
+  LoadKeysArena(plan, arena + static_cast<uint32_t>(slots[gslot[g]]), k);
+  gpart[g] = static_cast<uint8_t>(PartOfHash(HashKeys(plan, k), n_parts));
+  kw[g] = KeyRecordWords(plan, k);
+  uint64_t items = 0;
+  if (has_q) {
+    const int32_t b = xbig ? xbig[g] : -1;
+    const int32_t nc = b >= 0 ? xcnt[b] : -1;
+    items = nc > 0 ? static_cast<uint64_t>(nc) : (nc == 0 ? 1 : gstart[g + 1] - gstart[g]);
+  }
+  ic[g] = items;
+}
+
+struct XDst {
+  uint8_t* base;
+  const uint64_t* poff;    // [n_parts] byte offset of each part
+  const uint64_t* layout;  // [n_parts][6] koff, keys, states, gid, vals, wts
+  const uint64_t* nitems;  // [n_parts]
+};
+
+// One wave per listed group (part order): key record, state record, items.
+__global__ void XWriteGroupsKernel(const uint32_t* __restrict__ glist, uint64_t ng, const uint8_t* __restrict__ gpart,
+                                   const uint64_t* __restrict__ gstarts, const uint64_t* __restrict__ koff_j, const uint64_t* __restrict__ ioff_j,
+                                   const unsigned long long* __restrict__ slots, const uint32_t* __restrict__ gslot,
+                                   const uint64_t* __restrict__ arena, const AggPlanDev* __restrict__ plan, const uint8_t* __restrict__ states,
+                                   uint32_t srec, const uint32_t* __restrict__ gstart, const uint64_t* __restrict__ vals,
+                                   const int32_t* __restrict__ xbig, const int32_t* __restrict__ xcnt, const uint64_t* __restrict__ xcent,
+                                   int has_q, XDst dst) {
+  const uint64_t j = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (j >= ng) return;
+  const uint32_t g = glist[j];
+  const uint32_t p = gpart[g];
+  const uint64_t local = j - gstarts[p];
+  uint8_t* part = dst.base + dst.poff[p];
+  const uint64_t* L = dst.layout + 6 * p;
+  const uint64_t k0 = koff_j[gstarts[p]], i0 = ioff_j[gstarts[p]];
+  const uint64_t krel = koff_j[j] - k0, irel = ioff_j[j] - i0;
+  const uint64_t* rec = arena + static_cast<uint32_t>(slots[gslot[g]]);
+  const uint64_t nkw = koff_j[j + 1] - koff_j[j];
+  if (lane == 0) reinterpret_cast<uint64_t*>(part + L[0])[local] = krel;
+  for (uint64_t w = lane; w < nkw; w += 64) reinterpret_cast<uint64_t*>(part + L[1])[krel + w] = rec[w];
+  for (uint32_t b = lane; b < srec; b += 64) part[L[2] + local * srec + b] = states[static_cast<uint64_t>(g) * srec + b];
+  if (!has_q) return;
+  uint32_t* gid = reinterpret_cast<uint32_t*>(part + L[3]) + irel;
+  uint64_t* ov = reinterpret_cast<uint64_t*>(part + L[4]) + irel;
+  uint64_t* ow = reinterpret_cast<uint64_t*>(part + L[5]) + irel;
+  const uint64_t ni = ioff_j[j + 1] - ioff_j[j];
+  const int32_t b = xbig ? xbig[g] : -1;
+  const int32_t nc = b >= 0 ? xcnt[b] : -1;
+  for (uint64_t i = lane; i < ni; i += 64) {
+    gid[i] = static_cast<uint32_t>(local);
+    if (nc > 0) {
+      const uint64_t* c = xcent + (static_cast<uint64_t>(b) * kXCentCapH + i) * 2;
+      ov[i] = c[0];
+      ow[i] = c[1];
+    } else if (nc == 0) {  // every value NaN: one NaN stands for the group (add() skips it)
+      ov[i] = 0x7FF8000000000000ULL;
+      ow[i] = 0;
+    } else {
+      ov[i] = vals[gstart[g] + i];
+      ow[i] = 0;
+    }
+  }
+}
+
+// Owner side: per-slot state accumulators (macc_words u64 per slot: each UDA's words at its
+// offset, then a flags word), initialised to every UDA's identity.
+struct UdaOutX {
+  uint64_t* p[kMaxUdas];
+};
+
+struct XAccPlan {
+  int32_t n_udas, words;
+  int32_t kind[kMaxUdas], at[kMaxUdas], off[kMaxUdas], soff[kMaxUdas];
+  int64_t init[kMaxUdas];
+};
+
+__device__ __forceinline__ uint64_t XAccInit(int kind, int at) {
+  if (kind == PXG_UDA_MIN) return at == PXG_FLOAT64 ? static_cast<uint64_t>(OrderedFromDouble(FBits(kDblMax))) : static_cast<uint64_t>(INT64_MAX);
+  if (kind == PXG_UDA_MAX) return at == PXG_FLOAT64 ? static_cast<uint64_t>(OrderedFromDouble(FBits(kDblMin))) : static_cast<uint64_t>(INT64_MIN);
+  return 0;
+}
+
+__global__ void XAccInitKernel(XAccPlan xp, uint64_t* __restrict__ macc, uint32_t cap) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  uint64_t* r = macc + i * xp.words;
+  for (int w = 0; w < xp.words; ++w) r[w] = 0;
+  for (int u = 0; u < xp.n_udas; ++u)
+    if (xp.off[u] >= 0) r[xp.off[u]] = XAccInit(xp.kind[u], xp.at[u]);
+}
+
+__global__ void XAccRemapKernel(XAccPlan xp, const unsigned long long* __restrict__ old_slots, uint32_t old_cap,
+                                const uint32_t* __restrict__ remap, const uint64_t* __restrict__ src, uint64_t* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap || old_slots[i] == 0) return;
+  const uint64_t* a = src + static_cast<uint64_t>(i) * xp.words;
+  uint64_t* b = dst + static_cast<uint64_t>(remap[i]) * xp.words;
+  for (int w = 0; w < xp.words; ++w) b[w] = a[w];
+}
+
+// Merge one part's state records into the accumulators (UDA Merge, math_ops.h:590-593 count,
+// 633 sum, 668-672 mean, 710-714 min, 747 max).  INT64 sums wrap as the reference's do; float
+// sums and mean sums are added in arrival order (within the 1e-6 bar).
+__global__ void XImportStatesKernel(XAccPlan xp, const uint8_t* __restrict__ states, uint32_t srec, uint64_t ng,
+                                    const uint32_t* __restrict__ remap, uint64_t* __restrict__ macc) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const uint32_t slot = remap[g];
+  if (slot == kDeferredSlot) return;
+  uint64_t* r = macc + static_cast<uint64_t>(slot) * xp.words;
+  const uint8_t* st = states + g * srec;
+  for (int u = 0; u < xp.n_udas; ++u) {
+    const int o = xp.off[u];
+    if (o < 0) continue;
+    uint64_t v0, v1 = 0;
+    __builtin_memcpy(&v0, st + xp.soff[u], 8);
+    switch (xp.kind[u]) {
+      case PXG_UDA_COUNT: atomicAdd(reinterpret_cast<unsigned long long*>(r + o), static_cast<unsigned long long>(v0)); break;
+      case PXG_UDA_SUM:
+        if (xp.at[u] == PXG_FLOAT64) atomicAdd(reinterpret_cast<double*>(r + o), AsF(v0));
+        else atomicAdd(reinterpret_cast<unsigned long long*>(r + o), static_cast<unsigned long long>(v0));
+        break;
+      case PXG_UDA_MEAN:  // MeanInfo {uint64 size; double sum}
+        __builtin_memcpy(&v1, st + xp.soff[u] + 8, 8);
+        atomicAdd(reinterpret_cast<unsigned long long*>(r + o), static_cast<unsigned long long>(v0));
+        atomicAdd(reinterpret_cast<double*>(r + o + 1), AsF(v1));
+        break;
+      case PXG_UDA_MIN:
+        atomicMin(reinterpret_cast<long long*>(r + o), xp.at[u] == PXG_FLOAT64 ? OrderedFromDouble(v0) : static_cast<long long>(v0));
+        break;
+      case PXG_UDA_MAX:
+        atomicMax(reinterpret_cast<long long*>(r + o), xp.at[u] == PXG_FLOAT64 ? OrderedFromDouble(v0) : static_cast<long long>(v0));
+        break;
+      default: break;
+    }
+  }
+}
+
+// Items of one part -> staging weights (part index on top) and digest flags of their slots.
+__global__ void XImportItemsKernel(const uint64_t* __restrict__ wts, const uint32_t* __restrict__ gid, uint64_t ni,
+                                   const uint32_t* __restrict__ remap, uint64_t part, uint64_t* __restrict__ st_wt, uint64_t* __restrict__ macc,
+                                   int32_t words) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= ni) return;
+  const uint64_t w = wts[i];
+  st_wt[i] = (part << kXWtShift) | w;
+  if (w != 0) {
+    const uint32_t slot = remap[gid[i]];
+    if (slot != kDeferredSlot) atomicOr(reinterpret_cast<unsigned long long*>(macc + static_cast<uint64_t>(slot) * words + words - 1),
+                                        static_cast<unsigned long long>(kXFlagDigest));
+  }
+}
+
+// Plans without quantiles stage one placeholder item per imported group (so the grouping and
+// the key output run as for any aggregation; every output is then taken from the accumulators).
+__global__ void XPlaceholderKernel(const uint32_t* __restrict__ remap, uint64_t ng, uint32_t* __restrict__ st_slot,
+                                   uint64_t* __restrict__ st_wt) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  st_slot[g] = remap[g];
+  st_wt[g] = 0;
+}
+
+// Merged finalize: every non-quantile output from the accumulators of the group's slot, and the
+// list of groups whose quantiles need the merged digest.
+__global__ void XFinalizeStatesKernel(XAccPlan xp, const uint32_t* __restrict__ gslot, uint32_t G, const uint64_t* __restrict__ macc,
+                                      UdaOutX out, uint32_t* __restrict__ dlist, uint32_t* __restrict__ dcount) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint64_t* r = macc + static_cast<uint64_t>(gslot[g]) * xp.words;
+  for (int u = 0; u < xp.n_udas; ++u) {
+    const int o = xp.off[u];
+    if (o < 0) continue;
+    uint64_t v = r[o];
+    switch (xp.kind[u]) {
+      case PXG_UDA_MEAN: v = FBits(AsF(r[o + 1]) / static_cast<double>(r[o])); break;
+      case PXG_UDA_MIN:
+      case PXG_UDA_MAX:
+        if (xp.at[u] == PXG_FLOAT64) v = DoubleFromOrdered(static_cast<int64_t>(v));
+        break;
+      default: break;
+    }
+    out.p[u][g] = v;
+  }
+  if (dlist && (r[xp.words - 1] & kXFlagDigest)) dlist[atomicAdd(dcount, 1u)] = g;
+}
+static XAccPlan XAccPlanOf(const Agg& a) {
+  XAccPlan xp;
+  std::memset(&xp, 0, sizeof(xp));
+  xp.n_udas = a.n_udas;
+  xp.words = a.macc_words;
+  for (int u = 0; u < a.n_udas; ++u) {
+    xp.kind[u] = a.uda_kind[u];
+    xp.at[u] = a.uda_arg_type[u];
+    xp.off[u] = a.macc_off[u];
+    xp.soff[u] = a.hplan_x.state_off[u];
+    xp.init[u] = a.uda_init[u];
+  }
+  return xp;
+}
+
+bool ExchangeV2(const Agg& a) { return a.x_ok && !EnvFlag("PXG_XCHG_V1"); }
+
+// Accumulators sized with the table (a fresh table: identities everywhere).
+int32_t Agg::EnsureMacc() {
+  if (macc_cap == cap) return PXG_OK;
+  if (macc_cap != 0) return SetError(PXG_INTERNAL, "state accumulators out of step with the table");
+  PXG_RETURN_IF_ERROR(macc.Ensure(static_cast<size_t>(cap) * macc_words * 8 + 64));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "import_states", XAccInitKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0, XAccPlanOf(*this),
+                             macc.as<uint64_t>(), cap));
+  macc_cap = cap;
+  return PXG_OK;
+}
+
+// Grow() of a merged aggregation: its accumulator rows follow their slots.
+int32_t MaccFollowGrow(Agg* a, const unsigned long long* old_slots, uint32_t old_cap, const uint32_t* remap, uint32_t new_cap) {
+  if (!a->merged || a->macc_cap != old_cap) return PXG_OK;
+  DevBuf nm;
+  PXG_RETURN_IF_ERROR(nm.Alloc(static_cast<size_t>(new_cap) * a->macc_words * 8 + 64));
+  const XAccPlan xp = XAccPlanOf(*a);
+  PXG_RETURN_IF_ERROR(Launch(a->ctx, "import_states", XAccInitKernel, dim3(GridFor(new_cap, 256, 1 << 30)), dim3(256), 0, xp,
+                             nm.as<uint64_t>(), new_cap));
+  PXG_RETURN_IF_ERROR(Launch(a->ctx, "import_states", XAccRemapKernel, dim3(GridFor(old_cap, 256, 1 << 30)), dim3(256), 0, xp, old_slots,
+                             old_cap, remap, a->macc.as<const uint64_t>(), nm.as<uint64_t>()));
+  PXG_HIP(hipStreamSynchronize(a->ctx->stream));
+  a->macc = std::move(nm);
+  a->macc_cap = new_cap;
+  return PXG_OK;
+}
+
+__global__ void XGatherU64Kernel(const uint32_t* __restrict__ idx, uint64_t n, const uint64_t* __restrict__ src, uint64_t* __restrict__ dst) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+// Part boundaries of the group / key-word / item scans (one readback).
+__global__ void XPartBoundsKernel(const uint64_t* __restrict__ gstarts, int n_parts, const uint64_t* __restrict__ koff_j,
+                                  const uint64_t* __restrict__ ioff_j, uint64_t* __restrict__ out) {
+  const int p = threadIdx.x;
+  if (p > n_parts) return;
+  const uint64_t j = gstarts[p];
+  out[p] = j;
+  out[n_parts + 1 + p] = koff_j[j];
+  out[2 * (n_parts + 1) + p] = ioff_j[j];
+}
+
+int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes) {
+  ExportCache& X = xc;
+  if (merged) return SetError(PXG_FAILED_PRECONDITION, "an aggregation that merged imported states cannot be exported again");
+  const bool has_q = x_qval >= 0;
+  const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
+  if (!(X.valid && X.v2 && X.n_parts == n_parts && X.version == state_version)) {
+    X.valid = false;
+    // 1. The local finalize in export mode: grouping, per-group states, big groups' centroid lists.
+    export_x = true;
+    const int32_t rc = AggFinalizeTable(this);
+    export_x = false;
+    res.ready = false;
+    if (rc != PXG_OK) return rc;
+    const uint64_t G = static_cast<uint64_t>(res.n_groups);
+    X.G = G;
+    PXG_RETURN_IF_ERROR(X.part_of.Ensure(G + 16));
+    PXG_RETURN_IF_ERROR(X.koff.Ensure((2 * G + 2) * 8 + 64));   // kw, then koff_j
+    PXG_RETURN_IF_ERROR(X.words.Ensure((2 * G + 2) * 8 + 64));  // ic, then ioff_j
+    PXG_RETURN_IF_ERROR(X.slist.Ensure(G * 4 + 16));            // glist
+    PXG_RETURN_IF_ERROR(X.grank.Ensure(G * 4 + 16));            // xbig
+    PXG_RETURN_IF_ERROR(X.starts.Ensure(4 * (kPartBuckets + 1) * 8 + 64));
+    uint64_t* gstarts = X.starts.as<uint64_t>();
+    uint64_t* bounds = gstarts + kPartBuckets + 1;
+    int32_t* xbig = nullptr;
+    if (has_q && x_nbig > 0 && G > 0) {
+      xbig = reinterpret_cast<int32_t*>(X.grank.p);
+      PXG_HIP(hipMemsetAsync(xbig, 0xFF, G * 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XBigIndexKernel, dim3(GridFor(x_nbig, 256, 1 << 30)), dim3(256), 0,
+                                 ws.lists.as<const uint32_t>() + 3 * G, x_nbig, xbig));
+    }
+    uint64_t* kw = X.koff.as<uint64_t>();
+    uint64_t* koff_j = kw + G + 1;
+    uint64_t* ic = X.words.as<uint64_t>();
+    uint64_t* ioff_j = ic + G + 1;
+    if (G > 0)
+      PXG_RETURN_IF_ERROR(Launch(ctx, "export_slot_part", XGroupPartKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                                 d_plan.as<const AggPlanDev>(), slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(),
+                                 static_cast<uint32_t>(G), arena.as<const uint64_t>(), static_cast<uint32_t>(n_parts),
+                                 ws.gstart.as<const uint32_t>(), static_cast<const int32_t*>(xbig),
+                                 static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), has_q ? 1 : 0, X.part_of.as<uint8_t>(), kw, ic));
+    PXG_RETURN_IF_ERROR(Partition(ctx, X.part_of.as<const uint8_t>(), G, X.slist.as<uint32_t>(), gstarts, &X.hist, &X.scan));
+    PXG_RETURN_IF_ERROR(X.scan2.Ensure(ScanScratchBytes(static_cast<int64_t>(G) + 1) + 64));
+    if (G > 0) {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XGatherU64Kernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                                 X.slist.as<const uint32_t>(), G, static_cast<const uint64_t*>(kw), koff_j));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XGatherU64Kernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                                 X.slist.as<const uint32_t>(), G, static_cast<const uint64_t*>(ic), ioff_j));
+    }
+    PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, koff_j, koff_j, static_cast<int64_t>(G), koff_j + G, X.scan2.p));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, ioff_j, ioff_j, static_cast<int64_t>(G), ioff_j + G, X.scan2.p));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XPartBoundsKernel, dim3(1), dim3(kPartBuckets + 1), 0,
+                               static_cast<const uint64_t*>(gstarts), n_parts, static_cast<const uint64_t*>(koff_j),
+                               static_cast<const uint64_t*>(ioff_j), bounds));
+    std::vector<uint64_t> hb(3 * (n_parts + 1));
+    PXG_HIP(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+    X.g_start.assign(hb.begin(), hb.begin() + n_parts + 1);
+    X.k_start.assign(hb.begin() + n_parts + 1, hb.begin() + 2 * (n_parts + 1));
+    X.r_start.assign(hb.begin() + 2 * (n_parts + 1), hb.end());
+    X.n_parts = n_parts;
+    X.version = state_version;
+    X.v2 = true;
+    X.valid = true;
+  }
+  std::vector<XHeader> hdr(n_parts);
+  std::vector<uint64_t> poff(n_parts), lay(6 * n_parts), nit(n_parts);
+  uint64_t off = 0;
+  const uint64_t sig = XPlanSig(*this);
+  for (int p = 0; p < n_parts; ++p) {
+    const uint64_t ng = X.g_start[p + 1] - X.g_start[p];
+    const uint64_t ni = X.r_start[p + 1] - X.r_start[p];
+    const uint64_t kwp = X.k_start[p + 1] - X.k_start[p];
+    const XLayout L = XLayoutOf(ng, ni, kwp, srec);
+    XHeader& H = hdr[p];
+    std::memset(&H, 0, sizeof(H));
+    H.magic = kXMagic;
+    H.version = kXVersion;
+    H.n_keys = static_cast<uint32_t>(n_keys);
+    H.state_rec = srec;
+    H.n_groups = ng;
+    H.n_items = ni;
+    H.key_words = kwp;
+    H.plan_sig = sig;
+    H.has_q = has_q ? 1 : 0;
+    poff[p] = off;
+    const uint64_t l6[6] = {L.koff, L.keys, L.states, L.gid, L.vals, L.wts};
+    for (int k = 0; k < 6; ++k) lay[6 * p + k] = l6[k];
+    nit[p] = ni;
+    part_offsets[p] = static_cast<int64_t>(off);
+    part_bytes[p] = static_cast<int64_t>(L.bytes);
+    off += Align8(L.bytes);
+  }
+  if (dst == nullptr) return PXG_OK;
+  if (static_cast<uint64_t>(dst_capacity) < off)
+    return SetError(PXG_INVALID_ARGUMENT, "export buffer holds %lld bytes; %llu needed", (long long)dst_capacity, (unsigned long long)off);
+  std::vector<uint64_t> desc;
+  desc.insert(desc.end(), poff.begin(), poff.end());
+  desc.insert(desc.end(), lay.begin(), lay.end());
+  desc.insert(desc.end(), nit.begin(), nit.end());
+  PXG_RETURN_IF_ERROR(X.desc.Ensure(desc.size() * 8 + 64));
+  PXG_HIP(hipMemcpyAsync(X.desc.p, desc.data(), desc.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  uint8_t* base = static_cast<uint8_t*>(dst);
+  for (int p = 0; p < n_parts; ++p) PXG_HIP(hipMemcpyAsync(base + poff[p], &hdr[p], sizeof(XHeader), hipMemcpyHostToDevice, ctx->stream));
+  XDst D;
+  D.base = base;
+  D.poff = X.desc.as<const uint64_t>();
+  D.layout = D.poff + n_parts;
+  D.nitems = D.layout + 6 * n_parts;
+  const uint64_t G = X.G;
+  if (G > 0) {
+    const bool has_big = has_q && x_nbig > 0;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", XWriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(G) * 64, 256, 1 << 30)),
+                               dim3(256), 0, X.slist.as<const uint32_t>(), G, X.part_of.as<const uint8_t>(), X.starts.as<const uint64_t>(),
+                               static_cast<const uint64_t*>(X.koff.as<uint64_t>() + G + 1), static_cast<const uint64_t*>(X.words.as<uint64_t>() + G + 1),
+                               slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(), arena.as<const uint64_t>(),
+                               d_plan.as<const AggPlanDev>(), ws.xstates.as<const uint8_t>(), srec, ws.gstart.as<const uint32_t>(), x_vals,
+                               has_big ? static_cast<const int32_t*>(reinterpret_cast<int32_t*>(X.grank.p)) : nullptr,
+                               static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), static_cast<const uint64_t*>(ws.xcent.as<uint64_t>()),
+                               has_q ? 1 : 0, D));
+  }
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+
+int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* offs, const int64_t* sizes, const void* hdrs) {
+  const XHeader* H = static_cast<const XHeader*>(hdrs);
+  if (!x_ok) return SetError(PXG_UNIMPLEMENTED, "this aggregation's UDAs cannot merge exchanged states");
+  if (!merged && (st_n > 0 || inserted > 0 || hc_active))
+    return SetError(PXG_FAILED_PRECONDITION, "exchanged states merge into an aggregation without consumed rows (reset it first)");
+  const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
+  const bool has_q = x_qval >= 0;
+  uint64_t tot_groups = 0, tot_items = 0, tot_words = 0;
+  std::vector<XLayout> L(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) {
+    const XHeader& h = H[i];
+    if (h.version != kXVersion || h.plan_sig != XPlanSig(*this) || h.n_keys != static_cast<uint32_t>(n_keys) || h.state_rec != srec ||
+        h.has_q != (has_q ? 1u : 0u))
+      return SetError(PXG_INVALID_ARGUMENT, "partial-state buffer was exported by an aggregation with a different plan");
+    L[i] = XLayoutOf(h.n_groups, h.n_items, h.key_words, srec);
+    if (static_cast<uint64_t>(sizes[i]) < L[i].bytes)
+      return SetError(PXG_INVALID_ARGUMENT, "partial buffer truncated: %lld of %llu bytes", (long long)sizes[i], (unsigned long long)L[i].bytes);
+    tot_groups += h.n_groups;
+    tot_items += has_q ? h.n_items : h.n_groups;
+    tot_words += h.key_words;
+  }
+  merged = true;
+  state_version++;
+  res.ready = false;
+  if (tot_groups == 0) return PXG_OK;
+  const uint64_t abase = arena_words;
+  if (abase + tot_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  PXG_RETURN_IF_ERROR(arena.Reserve((abase + tot_words) * 8 + kArenaSlack, abase * 8, ctx->stream));
+  uint64_t want = 4 * (inserted + tot_groups);
+  if (want > cap) {
+    uint64_t c = cap;
+    while (c < want) c <<= 1;
+    if (c > (uint64_t(1) << 31)) return SetError(PXG_RESOURCE_UNAVAILABLE, "group table would exceed 2^31 slots");
+    PXG_RETURN_IF_ERROR(Grow(static_cast<uint32_t>(c)));
+  }
+  PXG_RETURN_IF_ERROR(EnsureMacc());
+  PXG_RETURN_IF_ERROR(xc.remap.Ensure(tot_groups * 4 + 16));
+  PXG_RETURN_IF_ERROR(EnsureStage(st_n + tot_items));
+  PXG_RETURN_IF_ERROR(st_wt.Reserve((st_n + tot_items) * 8 + 16, st_n * 8, ctx->stream));
+  uint8_t* meta = counters.as<uint8_t>();
+  unsigned int* d_ins = reinterpret_cast<unsigned int*>(meta + 32);
+  unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 36);
+  PXG_HIP(hipMemsetAsync(meta + 32, 0, 8, ctx->stream));
+  const XAccPlan xp = XAccPlanOf(*this);
+  uint64_t kw = abase, g0 = 0, r0 = st_n;
+  for (int i = 0; i < n; ++i) {
+    const XHeader& h = H[i];
+    const uint8_t* p = base8 + offs[i];
+    if (h.n_groups == 0) continue;
+    uint32_t* remap = xc.remap.as<uint32_t>() + g0;
+    PXG_HIP(hipMemcpyAsync(arena.as<uint64_t>() + kw, p + L[i].keys, h.key_words * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "import_keys", ImportKeysKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)), dim3(256), 0,
+                               d_plan.as<const AggPlanDev>(), slots.as<unsigned long long>(), cap - 1, arena.as<const uint64_t>(), kw,
+                               reinterpret_cast<const uint64_t*>(p + L[i].koff), h.n_groups, remap, d_ins, d_err));
+    if (srec > 0)
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_states", XImportStatesKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)),
+                                 dim3(256), 0, xp, p + L[i].states, srec, h.n_groups, static_cast<const uint32_t*>(remap), macc.as<uint64_t>()));
+    const uint64_t part = static_cast<uint64_t>(x_parts_seen++ & 63);
+    if (has_q && h.n_items > 0) {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", ImportRowsKernel, dim3(GridFor(static_cast<int64_t>(h.n_items), 256, 1 << 30)), dim3(256), 0,
+                                 reinterpret_cast<const uint32_t*>(p + L[i].gid), h.n_items, h.n_groups, static_cast<const uint32_t*>(remap),
+                                 st_slot.as<uint32_t>() + r0, d_err));
+      PXG_HIP(hipMemcpyAsync(st_val[x_qval].as<uint64_t>() + r0, p + L[i].vals, h.n_items * 8, hipMemcpyDeviceToDevice, ctx->stream));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XImportItemsKernel, dim3(GridFor(static_cast<int64_t>(h.n_items), 256, 1 << 30)), dim3(256), 0,
+                                 reinterpret_cast<const uint64_t*>(p + L[i].wts), reinterpret_cast<const uint32_t*>(p + L[i].gid), h.n_items,
+                                 static_cast<const uint32_t*>(remap), part, st_wt.as<uint64_t>() + r0, macc.as<uint64_t>(), macc_words));
+      r0 += h.n_items;
+    } else if (!has_q) {
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XPlaceholderKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)), dim3(256), 0,
+                                 static_cast<const uint32_t*>(remap), h.n_groups, st_slot.as<uint32_t>() + r0, st_wt.as<uint64_t>() + r0));
+      r0 += h.n_groups;
+    }
+    kw += h.key_words;
+    g0 += h.n_groups;
+  }
+  arena_words = kw;
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 240);
+  PXG_HIP(hipMemcpyAsync(pin, meta + 32, 8, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  const uint32_t r_ins = pin[0], r_err = pin[1];
+  if (r_err & 1u) return SetError(PXG_INTERNAL, "group table full during partial import");
+  if (r_err & 2u) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has an item whose group index is out of range");
+  inserted += r_ins;
+  st_n = r0;
+  uint64_t* pin64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(ctx->pinned) + 248);
+  *pin64 = st_n;
+  PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(counters.as<uint8_t>() + 16, pin64, 8, hipMemcpyHostToDevice, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
+// Finalize of a merged aggregation: the ordinary finalize over the imported items (grouping, key
+// output, and the quantiles of groups that arrived as raw values only), then every non-quantile
+// output from the accumulators and the merged digests of the groups that received centroids.
+int32_t Agg::FinalizeMerged() {
+  PXG_RETURN_IF_ERROR(AggFinalizeTable(this));
+  const uint32_t G = static_cast<uint32_t>(res.n_groups);
+  if (G == 0) return PXG_OK;
+  UdaOutX uo;
+  for (int u = 0; u < kMaxUdas; ++u) uo.p[u] = u < n_udas ? res.uda_out[u].as<uint64_t>() : nullptr;
+  const bool has_q = x_qval >= 0;
+  PXG_RETURN_IF_ERROR(ws.dlist.Ensure(static_cast<size_t>(G) * 4 + 64));
+  uint32_t* dcount = ws.dlist.as<uint32_t>() + G;
+  PXG_HIP(hipMemsetAsync(dcount, 0, 4, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "merged_states", XFinalizeStatesKernel, dim3(GridFor(G, 256, 1 << 30)), dim3(256), 0, XAccPlanOf(*this),
+                             ws.gslot.as<const uint32_t>(), G, macc.as<const uint64_t>(), uo, has_q ? ws.dlist.as<uint32_t>() : nullptr,
+                             dcount));
+  if (has_q) PXG_RETURN_IF_ERROR(LaunchDigestMerge(this, ws.dlist.as<const uint32_t>(), dcount, G));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  return PXG_OK;
+}
+
 }  // namespace pxg
 
 using namespace pxg;
@@ -533,6 +1105,7 @@ extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* d
   if (!agg || !part_offsets || !part_bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   if (n_parts < 1 || n_parts > kMaxParts) return SetError(PXG_INVALID_ARGUMENT, "n_parts must be in [1, %d]", kMaxParts);
   PXG_RETURN_IF_ERROR(agg->impl.SpillHc());
+  if (ExchangeV2(agg->impl)) return agg->impl.ExportPartialV2(n_parts, dst, dst_capacity, part_offsets, part_bytes);
   return agg->impl.ExportPartial(n_parts, dst, dst_capacity, part_offsets, part_bytes);
 }
 
