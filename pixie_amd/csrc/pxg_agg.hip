@@ -291,7 +291,9 @@ __device__ __forceinline__ void LoadKeyHeads(const AggPlanDev* __restrict__ plan
     } else {
       h.o0[i] = 0;
       const Val v = LoadCol(col, t, r);
-      h.a[i] = v.a;
+      // A computed fixed-width key (kShapeColOpConst over an 8-byte integer column, e.g.
+      // bin(time_, 10 s) = t - t % b, math_ops.h:512-527) is applied to the loaded value.
+      h.a[i] = plan->keys[i].shape == kShapeCol ? v.a : ApplyShape(&plan->keys[i], v.a);
       h.b[i] = v.b;
       h.len[i] = 0;
     }
@@ -439,7 +441,8 @@ __device__ __forceinline__ bool FastKeysEqualRow(const AggPlanDev* __restrict__ 
       c.offsets = nullptr;
       c.data = nullptr;
       const Val v = LoadCol(c, t, r);
-      eq = eq && v.a == x.w[i][0] && (t != PXG_UINT128 || v.b == x.w[i][1]);
+      const uint64_t a = plan->keys[i].shape == kShapeCol ? v.a : ApplyShape(&plan->keys[i], v.a);
+      eq = eq && a == x.w[i][0] && (t != PXG_UINT128 || v.b == x.w[i][1]);
     }
   }
   if (!eq) return false;
@@ -1353,9 +1356,14 @@ static bool UdaSupported(int kind, int arg) {
 static int32_t FastPathKeys(const AggPlanDev& p) {
   if (p.n_keys < 1 || p.n_keys > kMaxKeys) return 0;
   for (int k = 0; k < p.n_keys; ++k) {
-    if (p.keys[k].shape != kShapeCol) return 0;
     const int t = p.key_types[k];
     if (t < PXG_BOOLEAN || t > PXG_TIME64NS) return 0;
+    if (p.keys[k].shape == kShapeCol) continue;
+    // col op const over an 8-byte integer column giving an 8-byte integer (bin(), arithmetic):
+    // the kernel loads the column at its own width and applies the shape.
+    const int ct = p.col_types[p.keys[k].col];
+    const bool int8 = (ct == PXG_INT64 || ct == PXG_TIME64NS) && (t == PXG_INT64 || t == PXG_TIME64NS);
+    if (p.keys[k].shape != kShapeColOpConst || !int8 || p.keys[k].conv != 0) return 0;
   }
   auto fixed_shape = [&](const DevProgram& q) {
     if (q.shape != kShapeCol && q.shape != kShapeColOpConst) return false;

@@ -571,8 +571,41 @@ int32_t Agg::FinalizeHc() {
 // Spill: partition records -> table state (arena keys, slots, staging records), so export /
 // import (which work on the table state) see every group.
 // ---------------------------------------------------------------------------------------
+// Pass 1: each live record's compact arena record (pxg_keys.h layout) in its fixed-size arena
+// slot.  A separate launch from the inserts: a thread that meets another record's slot word reads
+// that record's key bytes, which are only guaranteed visible (across XCDs, whose L2s are not
+// coherent with relaxed atomics) after the kernel that wrote them has ended.
+__global__ void __launch_bounds__(256) HcSpillArenaKernel(HcAggPlan hp, const uint64_t* __restrict__ rec, uint64_t rcap, uint64_t n,
+                                                          int32_t rec_words, uint64_t abase, uint64_t* __restrict__ arena) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t lens = rec[i];
+  if (lens == kHcHole) return;
+  uint64_t* ar = arena + abase + i * static_cast<uint64_t>(rec_words);
+  int wo = 0;
+  for (int k = 0; k < hp.nk; ++k) {
+    const int t = hp.ktype[k];
+    const uint64_t* kw = rec + static_cast<uint64_t>(hp.koff[k]) * rcap + i;
+    if (t == PXG_STRING) {
+      const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
+      ar[wo] = len;
+      const int nw = static_cast<int>((len + 7) >> 3);
+      for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j * rcap];
+      wo += 1 + nw;
+    } else if (t == PXG_UINT128) {
+      ar[wo] = kw[0];
+      ar[wo + 1] = kw[rcap];
+      wo += 2;
+    } else {
+      ar[wo] = kw[0];
+      wo += 1;
+    }
+  }
+}
+
+// Pass 2: find-or-insert every live record's arena record, and its staging record.
 __global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restrict__ plan, HcAggPlan hp, const uint64_t* __restrict__ rec,
-                                                     uint64_t rcap, uint64_t n, int32_t rec_words, uint64_t abase, uint64_t* __restrict__ arena,
+                                                     uint64_t rcap, uint64_t n, int32_t rec_words, uint64_t abase, const uint64_t* __restrict__ arena,
                                                      unsigned long long* __restrict__ slots, uint32_t mask, uint32_t* __restrict__ st_slot,
                                                      StageDev stg, int nv, unsigned int* __restrict__ counters) {
   __shared__ unsigned int s_ins;
@@ -583,28 +616,8 @@ __global__ void __launch_bounds__(256) HcSpillKernel(const AggPlanDev* __restric
   const bool live = lens != kHcHole;
   uint32_t slot = kDeferredSlot;
   if (live) {
-    // Compact arena record (pxg_keys.h layout) in this record's fixed-size arena slot.
     const uint64_t at = abase + i * static_cast<uint64_t>(rec_words);
-    uint64_t* ar = arena + at;
-    int wo = 0;
-    for (int k = 0; k < hp.nk; ++k) {
-      const int t = hp.ktype[k];
-      const uint64_t* kw = rec + static_cast<uint64_t>(hp.koff[k]) * rcap + i;
-      if (t == PXG_STRING) {
-        const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
-        ar[wo] = len;
-        const int nw = static_cast<int>((len + 7) >> 3);
-        for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j * rcap];
-        wo += 1 + nw;
-      } else if (t == PXG_UINT128) {
-        ar[wo] = kw[0];
-        ar[wo + 1] = kw[rcap];
-        wo += 2;
-      } else {
-        ar[wo] = kw[0];
-        wo += 1;
-      }
-    }
+    const uint64_t* ar = arena + at;
     KeySet mine;
     LoadKeysArena(plan, ar, mine);
     const uint64_t h = HashKeys(plan, mine);
@@ -682,9 +695,12 @@ int32_t Agg::SpillHc() {
   std::memset(&stg, 0, sizeof(stg));
   for (int v = 0; v < n_vals; ++v) stg.vals[v] = st_val[v].as<uint64_t>();
   stg.cursor = reinterpret_cast<unsigned long long*>(cb + 16);
-  PXG_RETURN_IF_ERROR(Launch(ctx, "hc_spill", HcSpillKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
+  const dim3 grid(GridFor(static_cast<int64_t>(n), 256, 1 << 30));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "hc_spill_arena", HcSpillArenaKernel, grid, dim3(256), 0, hp, hc_rec.as<const uint64_t>(), hc_cap, n,
+                             rec_words, abase, arena.as<uint64_t>()));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "hc_spill", HcSpillKernel, grid, dim3(256), 0,
                              d_plan.as<const AggPlanDev>(), hp, hc_rec.as<const uint64_t>(), hc_cap, n, rec_words, abase,
-                             arena.as<uint64_t>(), slots.as<unsigned long long>(), cap - 1,
+                             arena.as<const uint64_t>(), slots.as<unsigned long long>(), cap - 1,
                              st_slot.as<uint32_t>(), stg, n_vals, counters.as<unsigned int>()));
   arena_words = abase + n * rec_words;
   uint8_t* pin = static_cast<uint8_t*>(ctx->pinned) + 224;
