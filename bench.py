@@ -110,6 +110,9 @@ def alg_bytes_of(table, n):
     return 8 * n + 8 * n + table.device_bytes(P.HE["service"]) + table.device_bytes(P.HE["req_path"])
 
 
+PMC_STEPS = 3
+
+
 def pmc_child(rows):
     """The workload the PMC leg profiles: the C2 consume (reset + consume, the timed step's
     dominant kernel) over `rows` device-generated rows, 3 launches."""
@@ -120,7 +123,7 @@ def pmc_child(rows):
     t = Table(ctx, P.HTTP_TYPES)
     t.append_http_events(SEED, 0, rows, N_PAIR_KEYS)
     a = plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
-    for _ in range(3):
+    for _ in range(PMC_STEPS):
         a.reset()
         a.consume(t)
     ctx.sync()
@@ -151,10 +154,12 @@ def pmc_leg(n):
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=200)
             if r.returncode != 0:
                 return {"error": f"rocprofv3 --pmc {counter} exited {r.returncode}"}
-            res[counter], res[counter + "_launches"] = ps.counter_avg(out, r"AggConsume(Fast)?Kernel", counter)
+            res[counter], res[counter + "_launches"] = ps.counter_per_step(out, r"AggConsume(Fast)?Kernel", counter, PMC_STEPS)
+        # per consume step (prefix + main launch when the probe-record prefix runs)
         return {"hbm_bytes_per_launch": (2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024,
                 "hbm_read_bytes_per_launch": 2 * res["FETCH_SIZE"] * 1024, "hbm_write_bytes_per_launch": res["WRITE_SIZE"] * 1024,
-                "launches": [res["FETCH_SIZE_launches"], res["WRITE_SIZE_launches"]], "rows": n,
+                "launches": [res["FETCH_SIZE_launches"], res["WRITE_SIZE_launches"]], "steps": PMC_STEPS, "rows": n,
+                "per": "consume step (every agg_consume / agg_consume_prefix launch of one consume summed)",
                 "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build (bench.py --pmc-child), "
                           "FETCH_SIZE x2 (gfx950), KiB -> bytes"}
     except Exception as e:  # the legs must never break the bench line

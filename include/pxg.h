@@ -203,7 +203,8 @@ int64_t pxg_table_num_rows(const pxg_table* t);
 int32_t pxg_table_num_chunks(const pxg_table* t);
 /* Device bytes of the table's column data in Arrow layout (values, offsets, payload). */
 int64_t pxg_table_device_bytes(const pxg_table* t, int32_t col);
-/* Copy rows [begin, end) of column col back to host (test / sink path). */
+/* Copy rows [begin, end) of column col back to host (sink path): buffers from the pinned
+ * result pool, released with pxg_result_free (also on error, nothing is left allocated). */
 int32_t pxg_table_fetch(pxg_table* t, int32_t col, int64_t begin, int64_t end,
                         pxg_column_out* out);
 /* Time-range cursor support (Table::FindRowIDFromTimeFirstGreaterThanOrEqual / ...GreaterThan,
@@ -293,6 +294,12 @@ int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
 /* pxg_agg_result with skip[c] != 0 leaving value column c without buffers (type and length
  * set; the caller reads it another way, e.g. pxg_agg_quantile_lanes). */
 int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip);
+/* The finalized result as device column views into the agg's own result buffers (no copy),
+ * for a device consumer (the engine's agg -> equijoin hand-off): valid until the agg's next
+ * consume / finalize / destroy.  *bytes = the Arrow payload bytes (RowBatch::NumBytes).
+ * UNIMPLEMENTED for results rendered on the host (QUANTILES, emit_states) and for the one
+ * synthetic row of a group-less agg over no rows; the caller then uses pxg_agg_result. */
+int32_t pxg_agg_result_device(pxg_agg* agg, pxg_column_view* cols, int32_t n_cols, int64_t* bytes);
 /* The quantile lanes a post-aggregate pluck_float64 reads (MapNode over the AggNode output,
  * math_sketches.h:40-54 + the pluck UDF): for every group, the lanes set in lane_mask (bit k =
  * p01,p10,p25,p50,p75,p90,p99[k]) packed in lane order into host_out (popcount(mask) doubles

@@ -3287,6 +3287,45 @@ extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t la
   return PXG_OK;
 }
 
+extern "C" int32_t pxg_agg_result_device(pxg_agg* agg, pxg_column_view* cols, int32_t n_cols, int64_t* bytes) {
+  if (!agg || !cols || !bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Agg& a = agg->impl;
+  if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
+  if (n_cols != a.n_keys + a.n_udas) return SetError(PXG_INVALID_ARGUMENT, "expected %d result columns", a.n_keys + a.n_udas);
+  if (a.emit_states) return SetError(PXG_UNIMPLEMENTED, "serialized states are assembled on the host");
+  for (int u = 0; u < a.n_udas; ++u) {
+    if (a.uda_kind[u] == PXG_UDA_QUANTILES) return SetError(PXG_UNIMPLEMENTED, "quantiles are rendered on the host");
+    if (TypeWidth(a.uda_out_type[u]) != 8) return SetError(PXG_UNIMPLEMENTED, "UDA %d has no 8-byte device column", u);
+  }
+  const int64_t G = a.res.n_groups;
+  if (a.n_keys == 0 && G == 0) return SetError(PXG_UNIMPLEMENTED, "the synthetic row of an empty group-less agg is built on the host");
+  int64_t b = 0;
+  for (int k = 0; k < a.n_keys; ++k) {
+    pxg_column_view& v = cols[k];
+    std::memset(&v, 0, sizeof(v));
+    v.type = a.key_types[k];
+    v.length = G;
+    if (v.type == PXG_STRING) {
+      v.offsets = a.res.key_offsets[k].as<const int32_t>();
+      v.data = a.res.key_data[k].as<const uint8_t>();
+      b += a.res.key_data_len[k];
+    } else {
+      v.values = a.res.key_fixed[k].p;
+      b += static_cast<int64_t>(TypeWidth(v.type)) * G;
+    }
+  }
+  for (int u = 0; u < a.n_udas; ++u) {
+    pxg_column_view& v = cols[a.n_keys + u];
+    std::memset(&v, 0, sizeof(v));
+    v.type = a.uda_out_type[u];
+    v.length = G;
+    v.values = a.res.uda_out[u].p;
+    b += 8 * G;
+  }
+  *bytes = b;
+  return PXG_OK;
+}
+
 extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip) {
   if (!agg || !cols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   Agg& a = agg->impl;

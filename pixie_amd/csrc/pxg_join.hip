@@ -276,13 +276,23 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
   const DevChunk* bch = B.d_chunks.as<const DevChunk>();
   const DevChunk* pch = P.d_chunks.as<const DevChunk>();
   const int gcap = ctx->num_cus * 8;
-  DevBuf slots, rank, meta, bslot, brefs, kstart, probed;
+  DevBuf slots, rank, meta, bslot, brefs, kstart, probed, key_of, cnt, off, ucnt, uoff, pref, bref;
   RadixWs rws;
-  PXG_RETURN_IF_ERROR(slots.Alloc(static_cast<size_t>(cap) * 8));
-  PXG_RETURN_IF_ERROR(rank.Alloc(static_cast<size_t>(cap) * 4 + 16));
-  PXG_RETURN_IF_ERROR(meta.Alloc(64));
-  PXG_RETURN_IF_ERROR(bslot.Alloc(nb * 4 + 16));
-  PXG_RETURN_IF_ERROR(brefs.Alloc(nb * 8 + 16));
+  // Temporaries come from the ctx buffer pool and go back to it (a hipFree synchronises the
+  // device; C5's join paid ~3 ms of them).
+  struct PoolBack {
+    Ctx* ctx;
+    std::vector<DevBuf*> bufs;
+    ~PoolBack() {
+      for (DevBuf* b : bufs) PoolRelease(ctx, *b);
+    }
+  } back{ctx, {&slots, &rank, &meta, &bslot, &brefs, &kstart, &probed, &key_of, &cnt, &off, &ucnt, &uoff, &pref, &bref, &rws.key[0],
+               &rws.key[1], &rws.val[0], &rws.val[1], &rws.scan, &rws.rs.hist, &rws.rs.ghist}};
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, slots, static_cast<size_t>(cap) * 8));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, rank, static_cast<size_t>(cap) * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, meta, 64));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, bslot, nb * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, brefs, nb * 8 + 16));
   PXG_RETURN_IF_ERROR(rws.scan.Ensure(ScanScratchBytes(static_cast<int64_t>(std::max<uint64_t>(np, cap) + 1)) + 64));
   uint32_t* d_meta = meta.as<uint32_t>();  // [0] overflow, [1] G, [2] probe output rows, [3] build output rows
   PXG_HIP(hipMemsetAsync(slots.p, 0, static_cast<size_t>(cap) * 8, ctx->stream));
@@ -300,8 +310,8 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   if (hmeta[0]) return SetError(PXG_INTERNAL, "join build table overflow (%u rows)", hmeta[0]);
   const uint32_t G = hmeta[1];
-  PXG_RETURN_IF_ERROR(kstart.Alloc((static_cast<size_t>(G) + 1) * 4 + 16));
-  PXG_RETURN_IF_ERROR(probed.Alloc(static_cast<size_t>(G) * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, kstart, (static_cast<size_t>(G) + 1) * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, probed, static_cast<size_t>(G) * 4 + 16));
   PXG_HIP(hipMemsetAsync(probed.p, 0, static_cast<size_t>(G) * 4 + 16, ctx->stream));
   JoinTableDev tab;
   tab.slots = slots.as<unsigned long long>();
@@ -319,19 +329,17 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
     tab.sorted_refs = svals;
   }
   // 2. Probe: counts, scan, (probe ref, build ref) pairs.
-  DevBuf key_of, cnt, off;
-  PXG_RETURN_IF_ERROR(key_of.Alloc(np * 4 + 16));
-  PXG_RETURN_IF_ERROR(cnt.Alloc(np * 4 + 16));
-  PXG_RETURN_IF_ERROR(off.Alloc(np * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, key_of, np * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, cnt, np * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, off, np * 4 + 16));
   for (size_t c = 0; c < P.chunks.size(); ++c)
     PXG_RETURN_IF_ERROR(Launch(ctx, "join_probe_count", JoinProbeCountKernel, dim3(GridFor64(P.chunks[c]->nrows, 256, gcap)), dim3(256), 0,
                                pk, pch, static_cast<uint32_t>(c), bk, bch, tab, sp.emit_unmatched_probe, key_of.as<uint32_t>(),
                                cnt.as<uint32_t>()));
   if (np > 0) PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cnt.as<const uint32_t>(), off.as<uint32_t>(), static_cast<int64_t>(np), d_meta + 2, rws.scan.p));
-  DevBuf ucnt, uoff;
   if (sp.emit_unmatched_build && G > 0) {
-    PXG_RETURN_IF_ERROR(ucnt.Alloc(static_cast<size_t>(G) * 4 + 16));
-    PXG_RETURN_IF_ERROR(uoff.Alloc(static_cast<size_t>(G) * 4 + 16));
+    PXG_RETURN_IF_ERROR(PoolAlloc(ctx, ucnt, static_cast<size_t>(G) * 4 + 16));
+    PXG_RETURN_IF_ERROR(PoolAlloc(ctx, uoff, static_cast<size_t>(G) * 4 + 16));
     PXG_RETURN_IF_ERROR(Launch(ctx, "join_unprobed_count", JoinUnprobedCountKernel, dim3(GridFor64(G, 256, 1 << 30)), dim3(256), 0, tab, G,
                                ucnt.as<uint32_t>()));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ucnt.as<const uint32_t>(), uoff.as<uint32_t>(), G, d_meta + 3, rws.scan.p));
@@ -343,9 +351,8 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
   const uint64_t n_out = static_cast<uint64_t>(n_probe_out) + n_build_out;
   if (n_out >= kNullRef) return SetError(PXG_UNIMPLEMENTED, "join output exceeds 2^32 - 1 rows");
   if (probe_rows) *probe_rows = n_probe_out;
-  DevBuf pref, bref;
-  PXG_RETURN_IF_ERROR(pref.Alloc(n_out * 4 + 16));
-  PXG_RETURN_IF_ERROR(bref.Alloc(n_out * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, pref, n_out * 4 + 16));
+  PXG_RETURN_IF_ERROR(PoolAlloc(ctx, bref, n_out * 4 + 16));
   for (size_t c = 0; c < P.chunks.size() && n_probe_out > 0; ++c)
     PXG_RETURN_IF_ERROR(Launch(ctx, "join_probe_write", JoinProbeWriteKernel, dim3(GridFor64(P.chunks[c]->nrows, 256, gcap)), dim3(256), 0,
                                pch, static_cast<uint32_t>(c), tab, key_of.as<const uint32_t>(), off.as<const uint32_t>(),
@@ -361,9 +368,35 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
   for (int i = 0; i < sp.n_out; ++i) otypes[i] = sp.out_side[i] == 0 ? P.types[sp.out_col[i]] : B.types[sp.out_col[i]];
   PXG_RETURN_IF_ERROR(NewTable(ctx, sp.n_out, otypes.data(), out));
   if (n_out == 0) return PXG_OK;
+  // Output columns in pooled buffers: string lengths and their scans first, every payload size
+  // read back with one synchronisation, then the gathers.  A result that fits one chunk adopts
+  // the buffers as its chunk (no copy); a larger one is appended chunk by chunk.
   std::vector<DevBuf> bufs(3 * static_cast<size_t>(sp.n_out));
+  struct PoolBackVec {
+    Ctx* ctx;
+    std::vector<DevBuf>& v;
+    ~PoolBackVec() {
+      for (DevBuf& b : v) PoolRelease(ctx, b);
+    }
+  } back_out{ctx, bufs};
   std::vector<pxg_column_view> views(sp.n_out);
-  DevBuf lens;
+  uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps);
+  if (static_cast<size_t>(sp.n_out) * 4 > Ctx::kPinnedBytes - Ctx::kPinnedOps) return SetError(PXG_UNIMPLEMENTED, "too many join outputs");
+  int n_str = 0;
+  for (int i = 0; i < sp.n_out; ++i) {
+    if (otypes[i] != PXG_STRING) continue;
+    const bool probe_side = sp.out_side[i] == 0;
+    DevBuf& o = bufs[3 * i + 1];
+    PXG_RETURN_IF_ERROR(PoolAlloc(ctx, o, (n_out + 1) * 4 + 16));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "join_gather", JoinStringLenKernel, dim3(GridFor64(n_out, 256, gcap)), dim3(256), 0, probe_side ? pch : bch,
+                               sp.out_col[i], probe_side ? pref.as<const uint32_t>() : bref.as<const uint32_t>(), n_out, o.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, o.as<const uint32_t>(), o.as<uint32_t>(), static_cast<int64_t>(n_out), o.as<uint32_t>() + n_out,
+                                         scratch));
+    PXG_HIP(hipMemcpyAsync(pin + i, o.as<uint32_t>() + n_out, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ++n_str;
+  }
+  if (n_str > 0) PXG_HIP(hipStreamSynchronize(ctx->stream));
+  bool one_chunk = static_cast<int64_t>(n_out) <= kChunkRows;
   for (int i = 0; i < sp.n_out; ++i) {
     const bool probe_side = sp.out_side[i] == 0;
     const DevChunk* ch = probe_side ? pch : bch;
@@ -377,15 +410,9 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
     if (t == PXG_STRING) {
       DevBuf& o = bufs[3 * i + 1];
       DevBuf& d = bufs[3 * i + 2];
-      PXG_RETURN_IF_ERROR(o.Alloc((n_out + 1) * 4 + 16));
-      PXG_RETURN_IF_ERROR(Launch(ctx, "join_gather", JoinStringLenKernel, dim3(GridFor64(n_out, 256, gcap)), dim3(256), 0, ch, col, ref, n_out,
-                                 o.as<uint32_t>()));
-      PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, o.as<const uint32_t>(), o.as<uint32_t>(), static_cast<int64_t>(n_out), o.as<uint32_t>() + n_out,
-                                           scratch));
-      uint32_t bytes = 0;
-      PXG_HIP(hipMemcpyAsync(&bytes, o.as<uint32_t>() + n_out, 4, hipMemcpyDeviceToHost, ctx->stream));
-      PXG_HIP(hipStreamSynchronize(ctx->stream));
-      PXG_RETURN_IF_ERROR(d.Alloc(static_cast<size_t>(bytes) + 16));
+      const uint32_t bytes = pin[i];
+      one_chunk = one_chunk && bytes < (uint32_t(1) << 31) - 64;
+      PXG_RETURN_IF_ERROR(PoolAlloc(ctx, d, static_cast<size_t>(bytes) + 16));
       PXG_RETURN_IF_ERROR(Launch(ctx, "join_gather", JoinStringCopyKernel, dim3(GridFor64(n_out, 256, gcap)), dim3(256), 0, ch, col, ref, n_out,
                                  o.as<const uint32_t>(), d.as<uint8_t>()));
       v.offsets = o.as<const int32_t>();
@@ -393,16 +420,38 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
     } else {
       const int w = TypeWidth(t);
       DevBuf& val = bufs[3 * i];
-      PXG_RETURN_IF_ERROR(val.Alloc(n_out * w + 16));
+      PXG_RETURN_IF_ERROR(PoolAlloc(ctx, val, n_out * w + 16));
       PXG_RETURN_IF_ERROR(Launch(ctx, "join_gather", JoinGatherFixedKernel, dim3(GridFor64(n_out, 256, gcap)), dim3(256), 0, ch, col, w, ref,
                                  n_out, val.as<uint8_t>()));
       v.values = val.p;
     }
   }
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
-  const int32_t rc = (*out)->impl.AppendRows(views.data(), static_cast<int64_t>(n_out), hipMemcpyDeviceToDevice);
+  Table& ot = (*out)->impl;
+  if (one_chunk) {
+    auto c = std::make_unique<Chunk>();
+    c->row_base = 0;
+    c->nrows = static_cast<int64_t>(n_out);
+    c->rows_cap = c->nrows;
+    c->sealed = true;
+    c->cols.resize(static_cast<size_t>(sp.n_out));
+    for (int i = 0; i < sp.n_out; ++i) {
+      ChunkCol& cc = c->cols[i];
+      if (otypes[i] == PXG_STRING) {
+        cc.offsets = std::move(bufs[3 * i + 1]);
+        cc.data = std::move(bufs[3 * i + 2]);
+        cc.data_len = pin[i];
+      } else {
+        cc.values = std::move(bufs[3 * i]);
+      }
+    }
+    ot.chunks.push_back(std::move(c));
+    ot.nrows = static_cast<int64_t>(n_out);
+    ot.version++;
+    return PXG_OK;  // contents complete in stream order (consumers on the ctx stream need no sync)
+  }
+  const int32_t rc = ot.AppendRows(views.data(), static_cast<int64_t>(n_out), hipMemcpyDeviceToDevice);
   if (rc != PXG_OK) return rc;
-  PXG_RETURN_IF_ERROR((*out)->impl.FlushStage());
+  PXG_RETURN_IF_ERROR(ot.FlushStage());
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   return PXG_OK;
 }

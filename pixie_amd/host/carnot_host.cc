@@ -204,6 +204,11 @@ struct RowBatch {
   std::vector<HostColumn> cols;
   int64_t num_rows = 0;
   bool eow = false, eos = false;
+  // A device-resident batch (the agg -> equijoin hand-off): `cols` is empty and `dev` holds one
+  // device column view per output column, valid while the batch is being sent.  Only sent to
+  // nodes whose AcceptsDeviceBatch() is true.
+  const pxg_column_view* dev = nullptr;
+  int64_t dev_bytes = 0;
 };
 
 using RowDescriptor = std::vector<int32_t>;  // column types (schema::RowDescriptor)
@@ -749,6 +754,7 @@ struct ExecNodeStats {
 
 static int64_t RowBatchNumBytes(const RowBatch& rb) {
   if (rb.num_rows == 0) return 0;
+  if (rb.dev) return rb.dev_bytes;
   int64_t b = 0;
   for (const HostColumn& c : rb.cols) {
     switch (c.type) {
@@ -792,6 +798,8 @@ class ExecNode {
   virtual bool ReadsColumnValue(size_t /*col*/) const { return true; }
   // Quantile lanes (bit k = kQuantileKeys[k]) this node plucks from input column col.
   virtual uint32_t PluckedLanes(size_t /*col*/) const { return 0x7Fu; }
+  // Whether this node takes device-resident batches (RowBatch::dev) from its parents.
+  virtual bool AcceptsDeviceBatch() const { return false; }
   const RowDescriptor& output_descriptor() const { return output_; }
   const std::vector<std::pair<ExecNode*, size_t>>& children() const { return children_; }
   virtual std::string DebugString() const = 0;
@@ -1370,6 +1378,29 @@ class GpuAggNode : public ExecNode {
       stats_.AddExtraMetric("groups", static_cast<double>(groups));
     }
     clk.Mark("agg finalize");
+    // Every consumer takes device batches (the agg -> equijoin hand-off): the result stays in HBM.
+    bool dev_ok = !children_.empty() && !emit_states;
+    for (auto& ch : children_) dev_ok = dev_ok && ch.first->AcceptsDeviceBatch();
+    if (dev_ok) {
+      std::vector<pxg_column_view> dv(keys.size() + udas.size());
+      int64_t bytes = 0;
+      const int32_t rc = pxg_agg_result_device(agg_, dv.data(), static_cast<int32_t>(dv.size()), &bytes);
+      if (rc == PXG_OK) {
+        RowBatch ob;
+        ob.num_rows = groups;
+        ob.eow = eow;
+        ob.eos = eos;
+        ob.dev = dv.data();
+        ob.dev_bytes = bytes;
+        clk.Mark("agg result (device views)");
+        Status st = SendRowBatchToChildren(s, ob);  // consumers copy in stream order
+        clk.Mark("children (device batch)");
+        PXC_RETURN_IF_ERROR(st);
+        PXG_CALL(pxg_agg_reset(agg_));
+        return Status::OK();
+      }
+      if (rc != PXG_UNIMPLEMENTED) return FromPxg(rc);
+    }
     std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
     // A quantiles column no consumer reads as a string (the pluck-only C2 shape) is not copied
     // out: only the plucked lanes and a per-group finiteness flag come back (pluck on the device).
@@ -1854,6 +1885,7 @@ class LimitNode : public ExecNode {
 // is sent when there is no output at all (equijoin_node.cc:447-459).
 class GpuEquijoinNode : public ExecNode {
  public:
+  bool AcceptsDeviceBatch() const override { return true; }
   std::string DebugString() const override {
     std::ostringstream os;
     os << "GpuEquijoinNode(type=" << type_ << ", probe=" << (probe_is_left_ ? "left" : "right") << ", rows_per_batch=" << rows_per_batch_
@@ -1918,10 +1950,14 @@ class GpuEquijoinNode : public ExecNode {
   Status ConsumeNextImpl(ExecState* s, const RowBatch& rb, size_t parent_index) override {
     if (parent_index > 1) return Err(PXG_INTERNAL, "join parent index %zu", parent_index);
     if (eos_[parent_index]) return Err(PXG_INTERNAL, "join input %zu after eos", parent_index);
-    if (rb.num_rows > 0) {
+    if (rb.num_rows > 0 && rb.dev) {
+      PXG_CALL(pxg_table_append_device(staged_[parent_index], rb.dev, rb.num_rows));  // HBM to HBM
+    } else if (rb.num_rows > 0) {
+      StageClock clk;
       std::vector<pxg_column_view> v;
       for (auto& c : rb.cols) v.push_back(c.View());
       PXG_CALL(pxg_table_append(staged_[parent_index], v.data(), rb.num_rows));
+      clk.Mark("join: stage input");
     }
     if (rb.eos) eos_[parent_index] = true;
     if (!(eos_[0] && eos_[1])) return Status::OK();
@@ -1945,7 +1981,9 @@ class GpuEquijoinNode : public ExecNode {
     sp.out_col = out_col_.data();
     pxg_table* out = nullptr;
     int64_t nprobe = 0;
+    StageClock clk;
     PXG_CALL(pxg_join(build, probe, &sp, &out, &nprobe));
+    clk.Mark("join: device join");
     std::unique_ptr<pxg_table, int32_t (*)(pxg_table*)> guard(out, pxg_table_destroy);
     const int64_t n = pxg_table_num_rows(out);
     std::vector<std::pair<int64_t, int64_t>> ranges;
@@ -1960,6 +1998,7 @@ class GpuEquijoinNode : public ExecNode {
       PXG_CALL(pxg_table_fetch(out, static_cast<int32_t>(c), 0, n, &o));
       full.push_back(FromOut(o));
     }
+    clk.Mark("join: output D2H");
     for (size_t r = 0; r < ranges.size(); ++r) {
       RowBatch ob;
       ob.num_rows = ranges[r].second - ranges[r].first;
@@ -1967,6 +2006,7 @@ class GpuEquijoinNode : public ExecNode {
       ob.eow = ob.eos = r + 1 == ranges.size();
       PXC_RETURN_IF_ERROR(SendRowBatchToChildren(s, ob));
     }
+    clk.Mark("join: output batches");
     return Status::OK();
   }
 
@@ -2893,15 +2933,33 @@ static size_t BatchBytes(const RowBatch& rb) {
   return b;
 }
 
-static void WriteBatch(Writer* w, const RowBatch& rb) {
-  w->put<int64_t>(rb.num_rows);
-  w->put<uint8_t>(rb.eow);
-  w->put<uint8_t>(rb.eos);
-  w->put<uint16_t>(0);
-  w->put<uint32_t>(static_cast<uint32_t>(rb.cols.size()));
+// Writes at a fixed position of a buffer sized up front (the parallel PXRB pass).
+struct SpanWriter {
+  uint8_t* p;
+  uint8_t* claim(size_t k) {
+    uint8_t* at = p;
+    p += k;
+    return at;
+  }
+  template <typename V>
+  void put(V v) {
+    std::memcpy(claim(sizeof(V)), &v, sizeof(V));
+  }
+  void bytes(const void* src, size_t k) {
+    if (k) std::memcpy(claim(k), src, k);
+  }
+};
+
+template <typename W>
+static void WriteBatch(W* w, const RowBatch& rb) {
+  w->template put<int64_t>(rb.num_rows);
+  w->template put<uint8_t>(rb.eow);
+  w->template put<uint8_t>(rb.eos);
+  w->template put<uint16_t>(0);
+  w->template put<uint32_t>(static_cast<uint32_t>(rb.cols.size()));
   const size_t n = static_cast<size_t>(rb.num_rows);
   for (auto& c : rb.cols) {
-    w->put<int32_t>(c.type);
+    w->template put<int32_t>(c.type);
     switch (c.type) {
       case B: w->bytes(c.values, n); break;
       case U: w->bytes(c.values, n * 16); break;
@@ -3153,11 +3211,45 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
+  // Large results: the batches are copied by several threads, each into its own byte range
+  // (a single thread copied C5's 195 MB result at ~15 GB/s).
+  struct Job {
+    const RowBatch* rb;
+    size_t at;
+  };
+  std::vector<Job> jobs;
   for (auto* sk : g.sinks_) {
     w.put<uint32_t>(static_cast<uint32_t>(sk->name.size()));
     w.bytes(sk->name.data(), sk->name.size());
     w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
-    for (auto& rb : sk->batches) WriteBatch(&w, rb);
+    for (auto& rb : sk->batches) {
+      const size_t b = BatchBytes(rb);
+      jobs.push_back({&rb, w.n});
+      w.claim(b);
+    }
+  }
+  const size_t nthreads = total < (size_t(8) << 20) ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+  if (nthreads <= 1) {
+    for (auto& j : jobs) {
+      SpanWriter sw{w.p + j.at};
+      WriteBatch(&sw, *j.rb);
+    }
+  } else {  // contiguous job ranges of ~equal bytes
+    std::vector<std::thread> th;
+    size_t j0 = 0;
+    for (size_t k = 0; k < nthreads && j0 < jobs.size(); ++k) {
+      const size_t goal = jobs[j0].at + (w.n - jobs[j0].at) / (nthreads - k);
+      size_t j1 = j0 + 1;
+      while (j1 < jobs.size() && jobs[j1].at < goal) ++j1;
+      th.emplace_back([&jobs, &w, j0, j1] {
+        for (size_t j = j0; j < j1; ++j) {
+          SpanWriter sw{w.p + jobs[j].at};
+          WriteBatch(&sw, *jobs[j].rb);
+        }
+      });
+      j0 = j1;
+    }
+    for (auto& t : th) t.join();
   }
   *out = w.release(out_len);
   if (grpc_out) {  // "PXGS": per GRPC sink, its destination source id and RowBatchData messages

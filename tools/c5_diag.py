@@ -22,7 +22,7 @@ for name, t in tabs.items():
     for b in t["batches"]:
         eng.append(name, b)
 pb = P.c5_plan().SerializeToString()
-eng.set_analyze(True)
+eng.set_analyze(os.environ.get("C5_ANALYZE", "1") == "1")
 names = ["agg_consume", "agg_consume_list", "agg_rehash", "stage_remap", "agg_publish_sizes", "agg_publish_write"]
 for q in range(4):
     ctx.sync()

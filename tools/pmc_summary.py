@@ -17,7 +17,7 @@ import os
 import re
 
 
-def counter_avg(d, kernel, counter):
+def counter_values(d, kernel, counter):
     vals = []
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path, newline="") as f:
@@ -26,7 +26,19 @@ def counter_avg(d, kernel, counter):
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} under {d}")
+    return vals
+
+
+def counter_avg(d, kernel, counter):
+    vals = counter_values(d, kernel, counter)
     return sum(vals) / len(vals), len(vals)
+
+
+def counter_per_step(d, kernel, counter, steps):
+    """Sum over every matching launch / steps: a step may launch the kernel more than once
+    (the consume's probe-record prefix launch + the rest of the range)."""
+    vals = counter_values(d, kernel, counter)
+    return sum(vals) / steps, len(vals)
 
 
 def main():
