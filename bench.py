@@ -453,7 +453,7 @@ def filter_map_leg(ctx, table, n, P, reps=5):
     kept_bytes = f.device_bytes(0) + f.device_bytes(1) + 8 * kept
     m.close()
     f.close()
-    names = ["filter_mask", "filter_gather", "str_gather", "scan_reduce", "scan_spine", "scan_downsweep", "map_eval", "map_rebase"]
+    names = ["filter_count", "filter_scan", "filter_write", "map_eval", "map_rebase"]
     ctx.sync()
     ctx.reset_stats()
     ctx.set_profiling(True)
@@ -467,13 +467,13 @@ def filter_map_leg(ctx, table, n, P, reps=5):
     wall = (time.perf_counter() - t0) / reps
     ctx.set_profiling(False)
     kms = {k: ctx.kernel_stats(k)[1] / reps for k in names if ctx.kernel_stats(k)[0]}
-    filt_ms = sum(v for k, v in kms.items() if k.startswith(("filter", "str_gather", "scan")))
+    filt_ms = sum(v for k, v in kms.items() if k.startswith("filter"))
     alg = 8 * n + 2 * kept_bytes
     return {"workload": "Filter(resp_status>=400; service, req_path, latency) -> Map(service, req_path, latency/1e6) "
                         "over the HBM table (pxg_filter + pxg_map, non-fused operators)",
             "rows": n, "kept_rows": kept, "ms_per_query_wall": wall * 1000.0, "rows_per_s": n / wall,
             "kernel_ms": {k: round(v, 4) for k, v in kms.items()},
-            "roofline": {"bound": "hbm", "kernels": "filter_mask + filter_gather + str_gather + scans",
+            "roofline": {"bound": "hbm", "kernels": "filter_count + filter_scan + filter_write",
                          "algorithmic_bytes": alg, "achieved": alg / (filt_ms / 1000.0) / 1e9 if filt_ms else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / (filt_ms / 1000.0) / 1e9 / HBM_PEAK_GBS if filt_ms else None}}

@@ -346,3 +346,52 @@ def test_standalone_filter_string_lengths(ctx):
     assert len(ref) == len(dev) == 1
     assert rows(ref[0]["cols"]) == rows(dev[0]["cols"])
     assert dev[0]["rows"] == int(keep.sum())
+
+
+@pytest.mark.gpu
+def test_standalone_filter_across_chunks_and_launches(ctx, monkeypatch):
+    """pxg_filter over a device-generated table of two chunks (2^24 + 300_001 rows), with one
+    chunk per launch (PXG_FILTER_BATCH=1) and with both in one launch: the selected rows of
+    resp_status >= 400 (service, req_path, latency, resp_status) equal numpy's filter of the
+    fetched input columns, in order, bit for bit; a range [begin, end) crossing the chunk
+    boundary keeps the same rows."""
+    from pixie_amd.compile import ExprCompiler
+    n = (1 << 24) + 300_001
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(20250117, 0, n, 10_000_000)
+    assert t.num_chunks == 2
+    comp = ExprCompiler(P.HTTP_TYPES)
+    pred = comp.compile(P.func("greaterThanEqual", [P.col(P.HE["resp_status"]), P.const(2, 400)], [2, 2]))
+    sel = [P.HE["service"], P.HE["req_path"], P.HE["latency"], P.HE["resp_status"]]
+    status = t.fetch(P.HE["resp_status"]).values
+    inp = {c: t.fetch(c) for c in sel}
+
+    def want(begin, end):
+        keep = np.flatnonzero(status[begin:end] >= 400) + begin
+        out = []
+        for c in sel:
+            col = inp[c]
+            if col.type == 5:
+                o = col.offsets.astype(np.int64)
+                lens = o[keep + 1] - o[keep]
+                starts = np.repeat(o[keep], lens)
+                within = np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens)
+                out.append((np.concatenate([[0], np.cumsum(lens)]), col.data[starts + within]))
+            else:
+                out.append(col.values[keep])
+        return keep.size, out
+
+    for batch, (begin, end) in [("1", (0, n)), ("8", (0, n)), ("1", ((1 << 24) - 77_777, n - 5))]:
+        monkeypatch.setenv("PXG_FILTER_BATCH", batch)
+        f = t.filter(pred, sel, begin, end)
+        m, exp = want(begin, end)
+        assert f.num_rows == m
+        for j, c in enumerate(sel):
+            got = f.fetch(j)
+            if got.type == 5:
+                assert np.array_equal(got.offsets.astype(np.int64), exp[j][0])
+                assert np.array_equal(got.data[:got.offsets[-1]], exp[j][1])
+            else:
+                assert np.array_equal(got.values, exp[j])
+        f.close()
+    t.close()
