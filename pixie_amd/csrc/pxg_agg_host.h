@@ -186,6 +186,7 @@ int32_t LaunchDigestMerge(Agg* a, const uint32_t* dlist, const uint32_t* dcount,
 // Exchange v2 helpers (pxg_partial.hip): is the plan exchanging states; the accumulators of a
 // merged aggregation following a table growth.
 bool ExchangeV2(const Agg& a);
+size_t XHeaderBytes();  // bytes of an exchange-v2 part header (the first bytes of every part)
 int32_t MaccFollowGrow(Agg* a, const unsigned long long* old_slots, uint32_t old_cap, const uint32_t* remap, uint32_t new_cap);
 
 // Groups the hint (or the last run) must reach before a qualifying plan stages partition

@@ -46,7 +46,7 @@ static_assert(sizeof(PartHeader) == 64, "PartHeader is 64 bytes");
 
 // Exchange v2 part header (partial states; layout below, XLayoutOf).
 constexpr uint32_t kXMagic = 0x58475850u;  // "PXGX"
-constexpr uint32_t kXVersion = 2;
+constexpr uint32_t kXVersion = 3;
 constexpr int kXCentCapH = 2048;  // = kXCentCap (pxg_finalize.hip)
 constexpr uint64_t kXFlagDigest = 1;
 constexpr int kXWtShift = 48;
@@ -61,7 +61,7 @@ struct XHeader {
   uint64_t key_words;
   uint64_t plan_sig;
   uint64_t has_q;
-  uint64_t reserved;
+  uint64_t item_words;  // words of the items region (raw value 1, centroid 2)
 };
 static_assert(sizeof(XHeader) == 64, "XHeader is 64 bytes");
 
@@ -578,18 +578,24 @@ int32_t Agg::ImportPartial(const void* src, int64_t nbytes) {
 // ---------------------------------------------------------------------------------------
 
 
+// Part layout: header, per group its key record offset (words), the key records, the state
+// records, per group its items' start (kXItemShift: item index, low 32 bits: word, bit 63: the
+// items are centroids) plus one end entry, then the items: a raw value is one word, a centroid
+// two (mean bits, weight).  Raw values (the common case, groups <= 8 * delta values) thus cost
+// 8 bytes each, as little as a shipped row value.
+constexpr int kXItemShift = 32;
+constexpr uint64_t kXCentFlag = uint64_t(1) << 63;
 struct XLayout {
-  uint64_t koff, keys, states, gid, vals, wts, bytes;
+  uint64_t koff, keys, states, gofs, items, bytes;
 };
-static XLayout XLayoutOf(uint64_t ng, uint64_t ni, uint64_t kw, uint64_t srec) {
+static XLayout XLayoutOf(uint64_t ng, uint64_t nw, uint64_t kw, uint64_t srec, bool has_q) {
   XLayout L;
   L.koff = sizeof(XHeader);
   L.keys = L.koff + ng * 8;
   L.states = L.keys + kw * 8;
-  L.gid = L.states + Align8(ng * srec);
-  L.vals = L.gid + Align8(ni * 4);
-  L.wts = L.vals + ni * 8;
-  L.bytes = L.wts + ni * 8;
+  L.gofs = L.states + Align8(ng * srec);
+  L.items = L.gofs + (has_q ? (ng + 1) * 8 : 0);
+  L.bytes = L.items + (has_q ? nw * 8 : 0);
   return L;
 }
 
@@ -615,19 +621,20 @@ __global__ void XGroupPartKernel(const AggPlanDev* __restrict__ plan, const unsi
   LoadKeysArena(plan, arena + static_cast<uint32_t>(slots[gslot[g]]), k);
   gpart[g] = static_cast<uint8_t>(PartOfHash(HashKeys(plan, k), n_parts));
   kw[g] = KeyRecordWords(plan, k);
-  uint64_t items = 0;
+  uint64_t items = 0, words = 0;
   if (has_q) {
     const int32_t b = xbig ? xbig[g] : -1;
     const int32_t nc = b >= 0 ? xcnt[b] : -1;
     items = nc > 0 ? static_cast<uint64_t>(nc) : (nc == 0 ? 1 : gstart[g + 1] - gstart[g]);
+    words = nc > 0 ? 2 * items : items;
   }
-  ic[g] = items;
+  ic[g] = (items << kXItemShift) | words;  // both fields scanned at once (no carry: words < 2^32)
 }
 
 struct XDst {
   uint8_t* base;
   const uint64_t* poff;    // [n_parts] byte offset of each part
-  const uint64_t* layout;  // [n_parts][6] koff, keys, states, gid, vals, wts
+  const uint64_t* layout;  // [n_parts][6] koff, keys, states, gofs, items, -
   const uint64_t* nitems;  // [n_parts]
 };
 
@@ -655,25 +662,22 @@ __global__ void XWriteGroupsKernel(const uint32_t* __restrict__ glist, uint64_t 
   for (uint64_t w = lane; w < nkw; w += 64) reinterpret_cast<uint64_t*>(part + L[1])[krel + w] = rec[w];
   for (uint32_t b = lane; b < srec; b += 64) part[L[2] + local * srec + b] = states[static_cast<uint64_t>(g) * srec + b];
   if (!has_q) return;
-  uint32_t* gid = reinterpret_cast<uint32_t*>(part + L[3]) + irel;
-  uint64_t* ov = reinterpret_cast<uint64_t*>(part + L[4]) + irel;
-  uint64_t* ow = reinterpret_cast<uint64_t*>(part + L[5]) + irel;
-  const uint64_t ni = ioff_j[j + 1] - ioff_j[j];
   const int32_t b = xbig ? xbig[g] : -1;
   const int32_t nc = b >= 0 ? xcnt[b] : -1;
-  for (uint64_t i = lane; i < ni; i += 64) {
-    gid[i] = static_cast<uint32_t>(local);
-    if (nc > 0) {
-      const uint64_t* c = xcent + (static_cast<uint64_t>(b) * kXCentCapH + i) * 2;
-      ov[i] = c[0];
-      ow[i] = c[1];
-    } else if (nc == 0) {  // every value NaN: one NaN stands for the group (add() skips it)
-      ov[i] = 0x7FF8000000000000ULL;
-      ow[i] = 0;
-    } else {
-      ov[i] = vals[gstart[g] + i];
-      ow[i] = 0;
-    }
+  uint64_t* gofs = reinterpret_cast<uint64_t*>(part + L[3]);
+  if (lane == 0) {
+    gofs[local] = irel | (nc > 0 ? kXCentFlag : 0);
+    if (j + 1 == gstarts[p + 1]) gofs[local + 1] = ioff_j[j + 1] - i0;  // the part's end entry
+  }
+  uint64_t* ov = reinterpret_cast<uint64_t*>(part + L[4]) + (irel & 0xFFFFFFFFu);
+  const uint64_t nw = (ioff_j[j + 1] - ioff_j[j]) & 0xFFFFFFFFu;
+  if (nc > 0) {  // the centroid list: (mean bits, weight) pairs
+    const uint64_t* c = xcent + static_cast<uint64_t>(b) * kXCentCapH * 2;
+    for (uint64_t w = lane; w < nw; w += 64) ov[w] = c[w];
+  } else if (nc == 0) {  // every value NaN: one NaN stands for the group (add() skips it)
+    if (lane == 0) ov[0] = 0x7FF8000000000000ULL;
+  } else {
+    for (uint64_t i = lane; i < nw; i += 64) ov[i] = vals[gstart[g] + i];
   }
 }
 
@@ -752,18 +756,37 @@ __global__ void XImportStatesKernel(XAccPlan xp, const uint8_t* __restrict__ sta
 }
 
 // Items of one part -> staging weights (part index on top) and digest flags of their slots.
-__global__ void XImportItemsKernel(const uint64_t* __restrict__ wts, const uint32_t* __restrict__ gid, uint64_t ni,
-                                   const uint32_t* __restrict__ remap, uint64_t part, uint64_t* __restrict__ st_wt, uint64_t* __restrict__ macc,
-                                   int32_t words) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= ni) return;
-  const uint64_t w = wts[i];
-  st_wt[i] = (part << kXWtShift) | w;
-  if (w != 0) {
-    const uint32_t slot = remap[gid[i]];
-    if (slot != kDeferredSlot) atomicOr(reinterpret_cast<unsigned long long*>(macc + static_cast<uint64_t>(slot) * words + words - 1),
-                                        static_cast<unsigned long long>(kXFlagDigest));
+// One wave per imported group: its items into staging records (slot, value, part << 48 | weight;
+// weight 0 = a raw value), and the digest flag of a slot that received centroids.
+__global__ void XImportItemsKernel(const uint64_t* __restrict__ gofs, const uint64_t* __restrict__ items, uint64_t ng, uint64_t ni,
+                                   uint64_t nw, const uint32_t* __restrict__ remap, uint64_t part, uint32_t* __restrict__ st_slot,
+                                   uint64_t* __restrict__ st_val, uint64_t* __restrict__ st_wt, uint64_t* __restrict__ macc, int32_t words,
+                                   unsigned int* __restrict__ err) {
+  const uint64_t g = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (g >= ng) return;
+  const uint64_t a = gofs[g], e = gofs[g + 1] & ~kXCentFlag;
+  const bool cent = (a & kXCentFlag) != 0;
+  const uint64_t i0 = (a & ~kXCentFlag) >> kXItemShift, i1 = e >> kXItemShift;
+  const uint64_t w0 = a & 0xFFFFFFFFu, w1 = e & 0xFFFFFFFFu;
+  if (i1 < i0 || i1 > ni || w1 < w0 || w1 > nw || (w1 - w0) != (cent ? 2 : 1) * (i1 - i0)) {
+    if (lane == 0) atomicOr(err, 2u);
+    return;
   }
+  const uint32_t slot = remap[g];
+  for (uint64_t i = lane; i < i1 - i0; i += 64) {
+    st_slot[i0 + i] = slot;
+    if (cent) {
+      st_val[i0 + i] = items[w0 + 2 * i];
+      st_wt[i0 + i] = (part << kXWtShift) | items[w0 + 2 * i + 1];
+    } else {
+      st_val[i0 + i] = items[w0 + i];
+      st_wt[i0 + i] = part << kXWtShift;
+    }
+  }
+  if (cent && lane == 0 && slot != kDeferredSlot)
+    atomicOr(reinterpret_cast<unsigned long long*>(macc + static_cast<uint64_t>(slot) * words + words - 1),
+             static_cast<unsigned long long>(kXFlagDigest));
 }
 
 // Plans without quantiles stage one placeholder item per imported group (so the grouping and
@@ -815,6 +838,7 @@ static XAccPlan XAccPlanOf(const Agg& a) {
 }
 
 bool ExchangeV2(const Agg& a) { return a.x_ok && !EnvFlag("PXG_XCHG_V1"); }
+size_t XHeaderBytes() { return sizeof(XHeader); }
 
 // Accumulators sized with the table (a fresh table: identities everywhere).
 int32_t Agg::EnsureMacc() {
@@ -872,6 +896,8 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
     res.ready = false;
     if (rc != PXG_OK) return rc;
     const uint64_t G = static_cast<uint64_t>(res.n_groups);
+    if (st_n + uint64_t(2) * kXCentCapH * x_nbig >= (uint64_t(1) << 32))
+      return SetError(PXG_UNIMPLEMENTED, "exchange parts hold fewer than 2^32 item words");
     X.G = G;
     PXG_RETURN_IF_ERROR(X.part_of.Ensure(G + 16));
     PXG_RETURN_IF_ERROR(X.koff.Ensure((2 * G + 2) * 8 + 64));   // kw, then koff_j
@@ -928,9 +954,10 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
   const uint64_t sig = XPlanSig(*this);
   for (int p = 0; p < n_parts; ++p) {
     const uint64_t ng = X.g_start[p + 1] - X.g_start[p];
-    const uint64_t ni = X.r_start[p + 1] - X.r_start[p];
+    const uint64_t ni = (X.r_start[p + 1] >> kXItemShift) - (X.r_start[p] >> kXItemShift);
+    const uint64_t nw = (X.r_start[p + 1] & 0xFFFFFFFFu) - (X.r_start[p] & 0xFFFFFFFFu);
     const uint64_t kwp = X.k_start[p + 1] - X.k_start[p];
-    const XLayout L = XLayoutOf(ng, ni, kwp, srec);
+    const XLayout L = XLayoutOf(ng, nw, kwp, srec, has_q);
     XHeader& H = hdr[p];
     std::memset(&H, 0, sizeof(H));
     H.magic = kXMagic;
@@ -942,8 +969,9 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
     H.key_words = kwp;
     H.plan_sig = sig;
     H.has_q = has_q ? 1 : 0;
+    H.item_words = nw;
     poff[p] = off;
-    const uint64_t l6[6] = {L.koff, L.keys, L.states, L.gid, L.vals, L.wts};
+    const uint64_t l6[6] = {L.koff, L.keys, L.states, L.gofs, L.items, 0};
     for (int k = 0; k < 6; ++k) lay[6 * p + k] = l6[k];
     nit[p] = ni;
     part_offsets[p] = static_cast<int64_t>(off);
@@ -997,7 +1025,7 @@ int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* of
     if (h.version != kXVersion || h.plan_sig != XPlanSig(*this) || h.n_keys != static_cast<uint32_t>(n_keys) || h.state_rec != srec ||
         h.has_q != (has_q ? 1u : 0u))
       return SetError(PXG_INVALID_ARGUMENT, "partial-state buffer was exported by an aggregation with a different plan");
-    L[i] = XLayoutOf(h.n_groups, h.n_items, h.key_words, srec);
+    L[i] = XLayoutOf(h.n_groups, h.item_words, h.key_words, srec, has_q);
     if (static_cast<uint64_t>(sizes[i]) < L[i].bytes)
       return SetError(PXG_INVALID_ARGUMENT, "partial buffer truncated: %lld of %llu bytes", (long long)sizes[i], (unsigned long long)L[i].bytes);
     tot_groups += h.n_groups;
@@ -1042,13 +1070,10 @@ int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* of
                                  dim3(256), 0, xp, p + L[i].states, srec, h.n_groups, static_cast<const uint32_t*>(remap), macc.as<uint64_t>()));
     const uint64_t part = static_cast<uint64_t>(x_parts_seen++ & 63);
     if (has_q && h.n_items > 0) {
-      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", ImportRowsKernel, dim3(GridFor(static_cast<int64_t>(h.n_items), 256, 1 << 30)), dim3(256), 0,
-                                 reinterpret_cast<const uint32_t*>(p + L[i].gid), h.n_items, h.n_groups, static_cast<const uint32_t*>(remap),
-                                 st_slot.as<uint32_t>() + r0, d_err));
-      PXG_HIP(hipMemcpyAsync(st_val[x_qval].as<uint64_t>() + r0, p + L[i].vals, h.n_items * 8, hipMemcpyDeviceToDevice, ctx->stream));
-      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XImportItemsKernel, dim3(GridFor(static_cast<int64_t>(h.n_items), 256, 1 << 30)), dim3(256), 0,
-                                 reinterpret_cast<const uint64_t*>(p + L[i].wts), reinterpret_cast<const uint32_t*>(p + L[i].gid), h.n_items,
-                                 static_cast<const uint32_t*>(remap), part, st_wt.as<uint64_t>() + r0, macc.as<uint64_t>(), macc_words));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XImportItemsKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups) * 64, 256, 1 << 30)),
+                                 dim3(256), 0, reinterpret_cast<const uint64_t*>(p + L[i].gofs), reinterpret_cast<const uint64_t*>(p + L[i].items),
+                                 h.n_groups, h.n_items, h.item_words, static_cast<const uint32_t*>(remap), part, st_slot.as<uint32_t>() + r0,
+                                 st_val[x_qval].as<uint64_t>() + r0, st_wt.as<uint64_t>() + r0, macc.as<uint64_t>(), macc_words, d_err));
       r0 += h.n_items;
     } else if (!has_q) {
       PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XPlaceholderKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)), dim3(256), 0,
@@ -1067,11 +1092,10 @@ int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* of
   if (r_err & 2u) return SetError(PXG_INVALID_ARGUMENT, "partial buffer has an item whose group index is out of range");
   inserted += r_ins;
   st_n = r0;
-  uint64_t* pin64 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(ctx->pinned) + 248);
-  *pin64 = st_n;
+  // The device insert count and staging cursor follow (stream-ordered memsets: no host buffer).
   PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.p), static_cast<int>(inserted), 1, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(counters.as<uint8_t>() + 16, pin64, 8, hipMemcpyHostToDevice, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.as<uint8_t>() + 16), static_cast<int>(st_n & 0xFFFFFFFFu), 1, ctx->stream));
+  PXG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(counters.as<uint8_t>() + 20), static_cast<int>(st_n >> 32), 1, ctx->stream));
   return PXG_OK;
 }
 

@@ -159,7 +159,7 @@ def test_two_processes_share_gpu0_exchange_matches_oracle(tmp_path, mode):
     assert rep["ok"], rep  # compare_agg also rejects a group finalized on two ranks (duplicates)
     for x in res:
         assert x["sent"] > 0 and x["recv"] > 0
-    print("exchange via", [x["via"] for x in res])
+    print("exchange via", [x["via"] for x in res], "bytes sent / received per rank", [(x["sent"], x["recv"]) for x in res])
     if mode == "rccl" and any(x["via"] != "rccl" for x in res):
         # RCCL refuses two ranks on one device ("invalid usage": duplicate GPU), so on a one-GPU
         # box the ranks exchanged over gloo; the result above is still checked, but the RCCL
