@@ -5,6 +5,7 @@
 #   bench  : bench.py default line (C2 + legs + n1 with parity) -> gpurun_out/bench.json
 #   prof   : rocprofv3 --kernel-trace --stats over the bench's timed C2 steps only
 #   n1prof : the same over the 1B-row n1 steps (no C2 legs)
+#   n1only : rocprofv3 stats of tools/n1_prof.py alone (every launch a 1B-row launch)
 #   pmc    : FETCH_SIZE / WRITE_SIZE passes over the consume kernel (C2) + summary JSON
 #   c3prof : rocprofv3 stats of the C3 leg
 #   diag   : tools/consume_diag.py timing modes (0 production, 2 filter only, 3 keys + hash)
@@ -20,7 +21,8 @@ step() {
     n1prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n1 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 $B --no-n1-parity --no-pmc --rows-per-gpu 1000000 > gpurun_out/prof_n1.log 2>&1 ;;
     pmc) timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --pmc-child 100000000 > gpurun_out/pmc_fetch.log 2>&1 &&
          timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --pmc-child 100000000 > gpurun_out/pmc_write.log 2>&1 &&
-         python3 tools/pmc_summary.py --rows 100000000 --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --out gpurun_out/pmc_agg_consume.json > gpurun_out/pmc_summary.log 2>&1 ;;
+         python3 tools/pmc_summary.py --steps 3 --rows 100000000 --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --out gpurun_out/pmc_agg_consume.json > gpurun_out/pmc_summary.log 2>&1 ;;
+    n1only) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n1only -o run --output-format csv -- python3 tools/n1_prof.py 3 > gpurun_out/prof_n1only.log 2>&1 ;;
     c3prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/c3_prof.py > gpurun_out/prof_c3.log 2>&1 ;;
     diag) timeout -k 10 300 python3 tools/consume_diag.py 0 2 3 > gpurun_out/diag.log 2>&1 ;;
     *) echo "unknown mode $1" >&2; return 2 ;;

@@ -49,9 +49,16 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--steps", type=int, default=0,
+                    help="consume steps in the run: report bytes per step (every matching launch of a step summed: the "
+                         "probe-record prefix launch + the main launch) instead of per launch")
     a = ap.parse_args()
-    fetch_kib, nf = counter_avg(a.fetch, a.kernel, "FETCH_SIZE")
-    write_kib, nw = counter_avg(a.write, a.kernel, "WRITE_SIZE")
+    if a.steps > 0:
+        fetch_kib, nf = counter_per_step(a.fetch, a.kernel, "FETCH_SIZE", a.steps)
+        write_kib, nw = counter_per_step(a.write, a.kernel, "WRITE_SIZE", a.steps)
+    else:
+        fetch_kib, nf = counter_avg(a.fetch, a.kernel, "FETCH_SIZE")
+        write_kib, nw = counter_avg(a.write, a.kernel, "WRITE_SIZE")
     res = {
         "kernel": a.name,
         "kernel_symbol": a.kernel,
@@ -59,6 +66,7 @@ def main():
         "fetch_size_kib_raw": fetch_kib,
         "write_size_kib": write_kib,
         "launches": [nf, nw],
+        "per": f"consume step ({a.steps} steps)" if a.steps > 0 else "launch",
         "hbm_read_bytes_per_launch": 2 * fetch_kib * 1024,
         "hbm_write_bytes_per_launch": write_kib * 1024,
         "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024,
