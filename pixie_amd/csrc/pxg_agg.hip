@@ -1283,8 +1283,21 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   };
   // The prefix: ~1/32 of the range (1M..16M rows) in 8192-row tiles, so its launch is one short
   // round of workgroups.
-  const int64_t pre_rows = (std::min<int64_t>(int64_t(1) << 24, std::max<int64_t>(int64_t(1) << 20, rows / 32)) / kSubRows) * kSubRows;
-  if (rec && inserted == 0 && rows >= 8 * pre_rows) {
+  static const int64_t pre_div = [] {  // experiments: PXG_PREFIX_DIV (range / prefix rows), PXG_PREFIX_MIN
+    const char* e = std::getenv("PXG_PREFIX_DIV");
+    return e && std::atoll(e) > 0 ? std::atoll(e) : 32;
+  }();
+  static const int64_t pre_min = [] {
+    const char* e = std::getenv("PXG_PREFIX_MIN");
+    return e && std::atoll(e) > 0 ? std::atoll(e) : (int64_t(1) << 20);
+  }();
+  const int64_t pre_rows = (std::min<int64_t>(int64_t(1) << 24, std::max<int64_t>(pre_min, rows / pre_div)) / kSubRows) * kSubRows;
+  // Below ~2^28 rows the prefix launch and its publication cost what the records save (C2,
+  // 100M rows: step 2.51 ms with records vs 2.48 without, tools/prefix_ab.sh); at 1B rows they
+  // save ~1.5 ms of consume.
+  const char* rme = std::getenv("PXG_PREFIX_MIN_ROWS");  // tests: the prefix path at small sizes
+  const int64_t rec_min_rows = rme && std::atoll(rme) > 0 ? std::atoll(rme) : (int64_t(1) << 28);
+  if (rec && inserted == 0 && rows >= std::max<int64_t>(8 * pre_rows, rec_min_rows)) {
     std::vector<TileRange> pre, rest;
     const int64_t nt_pre = make_ranges(begin, begin + pre_rows, kSubRows, &pre);
     const int64_t nt_rest = make_ranges(begin + pre_rows, end, tile_rows, &rest);
@@ -1292,7 +1305,8 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     PXG_RETURN_IF_ERROR(EnsureRecords());  // the prefix may have grown the table
     PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, rest, nt_rest, pick(rec_cap == cap), "agg_consume"));
   } else {
-    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(rec && rec_cap == cap), "agg_consume"));
+    // Records are compared only once some groups are published (a later consume of the run).
+    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(rec && rec_cap == cap && inserted > 0), "agg_consume"));
   }
   // Keep the table at most ~37% full for the next consume.
   if (inserted > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(static_cast<uint64_t>(inserted) * 4)));
