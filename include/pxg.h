@@ -294,6 +294,11 @@ int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
 /* pxg_agg_result with skip[c] != 0 leaving value column c without buffers (type and length
  * set; the caller reads it another way, e.g. pxg_agg_quantile_lanes). */
 int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip);
+/* pxg_agg_finalize + pxg_agg_result_skip in one call: the finalize issues each result column's
+ * device-to-host copy as soon as the column is produced (group keys while the quantile digests
+ * still run), so the copies overlap the finalize.  Same columns, buffers and release
+ * (pxg_result_free) as pxg_agg_result_skip. */
+int32_t pxg_agg_finalize_result(pxg_agg* agg, int64_t* n_groups, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip);
 /* The finalized result as device column views into the agg's own result buffers (no copy),
  * for a device consumer (the engine's agg -> equijoin hand-off): valid until the agg's next
  * consume / finalize / destroy.  *bytes = the Arrow payload bytes (RowBatch::NumBytes).

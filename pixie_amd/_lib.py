@@ -83,7 +83,7 @@ EXPORTED = [
     "pxg_ctx_reset_stats", "pxg_table_create", "pxg_table_destroy", "pxg_table_append",
     "pxg_table_append_device", "pxg_table_flush", "pxg_table_num_rows", "pxg_table_num_chunks",
     "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
-    "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_result_device", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
+    "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_result_device", "pxg_agg_finalize_result", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial", "pxg_agg_import_partials",
     "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains", "pxg_digest_merge",
     "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_destroy", "pxg_agg_alltoall",
@@ -145,6 +145,7 @@ def load() -> C.CDLL:
         "pxg_agg_result": (i32, [vp, p(ColumnOut), i32]),
         "pxg_agg_result_skip": (i32, [vp, p(ColumnOut), i32, C.c_void_p]),
         "pxg_agg_result_device": (i32, [vp, C.c_void_p, i32, C.c_void_p]),
+        "pxg_agg_finalize_result": (i32, [vp, C.c_void_p, p(ColumnOut), i32, C.c_void_p]),
         "pxg_agg_quantile_lanes": (i32, [vp, i32, C.c_uint32, C.c_void_p, C.c_void_p]),
         "pxg_result_free": (None, [p(ColumnOut), i32]),
         "pxg_host_alloc": (C.c_void_p, [C.c_int64]),

@@ -117,6 +117,15 @@ struct Agg {
   int32_t last_hc_pbits = 0;  // partition bits of the last finalize (pxg_agg_stats)
   int32_t last_hc_reruns = 0; // partition passes the last finalize reran (pxg_agg_stats)
   int32_t EnsureHc(uint64_t need);
+  // pxg_agg_finalize_result: result columns whose D2H copies the finalize issues as soon as
+  // they are produced (keys on side stream 2, non-quantile values after the combine), so they
+  // overlap the rest of the finalize.  cols has n_keys + n_udas entries; skip as in
+  // pxg_agg_result_skip.
+  struct EarlyResult {
+    bool want = false, keys = false, vals = false;
+    pxg_column_out* cols = nullptr;
+    const uint8_t* skip = nullptr;
+  } early;
   bool HcNext() const;     // would the next run after a reset be high-cardinality?
   int32_t FinalizeHc();
   // Moves staged partition records into the table state (export / import need it): every

@@ -2800,6 +2800,34 @@ int32_t AggFinalizeTable(Agg* a) {
                                      static_cast<const uint32_t*>(R.key_offsets[k].as<uint32_t>()), R.key_data[k].as<uint8_t>()));
       }
       keys_on_side2 = true;
+      // Early result: the key columns go to pooled pinned host blocks right behind their
+      // kernels (STRING payloads copied up to the arena bound; the exact length is set after
+      // the final synchronisation).
+      if (a->early.want && !a->export_x && !a->merged && !a->emit_states) {
+        bool ok = true;
+        for (int k = 0; k < a->n_keys && ok; ++k) {
+          pxg_column_out& o = a->early.cols[k];
+          std::memset(&o, 0, sizeof(o));
+          o.type = a->key_types[k];
+          o.length = ngroups;
+          if (o.type == PXG_STRING) {
+            o.offsets = static_cast<int32_t*>(ResultAlloc((static_cast<size_t>(ngroups) + 1) * 4));
+            o.data = static_cast<uint8_t*>(ResultAlloc(static_cast<size_t>(a->arena_words) * 8 + 16));
+            ok = o.offsets && o.data;
+            if (ok) {
+              PXG_HIP(hipMemcpyAsync(o.offsets, R.key_offsets[k].p, (static_cast<size_t>(ngroups) + 1) * 4, hipMemcpyDeviceToHost, ctx->side2));
+              if (a->arena_words > 0)
+                PXG_HIP(hipMemcpyAsync(o.data, R.key_data[k].p, static_cast<size_t>(a->arena_words) * 8, hipMemcpyDeviceToHost, ctx->side2));
+            }
+          } else {
+            const size_t w = o.type == PXG_BOOLEAN ? 1 : TypeWidth(o.type);
+            o.values = ResultAlloc(std::max<size_t>(static_cast<size_t>(ngroups) * w, 1));
+            ok = o.values != nullptr;
+            if (ok) PXG_HIP(hipMemcpyAsync(o.values, R.key_fixed[k].p, static_cast<size_t>(ngroups) * w, hipMemcpyDeviceToHost, ctx->side2));
+          }
+        }
+        a->early.keys = ok;
+      }
     }
   }
     return PXG_OK;
@@ -2935,6 +2963,21 @@ int32_t AggFinalizeTable(Agg* a) {
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                              cplan, gstart, static_cast<const uint32_t*>(cbase), ngroups,
                              ws.partial.as<const uint64_t>(), max_chunks, uo, states));
+  if (a->early.want && !states && !a->merged && !a->export_x) {  // early result: the combined values
+    bool ok = true;
+    for (int u = 0; u < a->n_udas && ok; ++u) {
+      if (a->uda_kind[u] == PXG_UDA_QUANTILES) continue;  // after the quantile kernels
+      pxg_column_out& o = a->early.cols[a->n_keys + u];
+      std::memset(&o, 0, sizeof(o));
+      o.type = a->uda_out_type[u];
+      o.length = ngroups;
+      if (a->early.skip && a->early.skip[a->n_keys + u]) continue;
+      o.values = ResultAlloc(std::max<size_t>(static_cast<size_t>(ngroups) * 8, 8));
+      ok = o.values != nullptr;
+      if (ok) PXG_HIP(hipMemcpyAsync(o.values, R.uda_out[u].p, static_cast<size_t>(ngroups) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    a->early.vals = ok;
+  }
   return PXG_OK;
   };
   if (!any_q) PXG_RETURN_IF_ERROR(RunReductions());
@@ -3284,6 +3327,57 @@ extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t la
   if (nsel) PXG_HIP(hipMemcpyAsync(host_out, d_out, G * nsel * 8, hipMemcpyDeviceToHost, a.ctx->stream));
   PXG_HIP(hipMemcpyAsync(host_finite, d_fin, G, hipMemcpyDeviceToHost, a.ctx->stream));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  return PXG_OK;
+}
+
+extern "C" int32_t pxg_agg_finalize_result(pxg_agg* agg, int64_t* n_groups, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip) {
+  if (!agg || !cols) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  Agg& a = agg->impl;
+  const int32_t n_val_cols = a.emit_states ? 1 : a.n_udas;
+  if (n_cols != a.n_keys + n_val_cols) return SetError(PXG_INVALID_ARGUMENT, "expected %d result columns", a.n_keys + n_val_cols);
+  for (int c = 0; c < n_cols; ++c) std::memset(&cols[c], 0, sizeof(cols[c]));
+  const bool early = !a.emit_states && !a.merged && !a.hc_active && a.n_keys > 0;
+  a.early.want = early;
+  a.early.keys = a.early.vals = false;
+  a.early.cols = cols;
+  a.early.skip = skip;
+  const int32_t rc = AggFinalizeImpl(&a);
+  const bool got = a.early.keys && a.early.vals;
+  a.early = Agg::EarlyResult();
+  // A run that switched to partitioned groups (or failed, or stopped before issuing every copy)
+  // drops what was copied early and takes the ordinary result path.
+  const bool usable = rc == PXG_OK && got && !a.hc_active && a.res.n_groups > 0;
+  if (!usable) {
+    (void)hipStreamSynchronize(a.ctx->stream);
+    pxg_result_free(cols, n_cols);
+    for (int c = 0; c < n_cols; ++c) std::memset(&cols[c], 0, sizeof(cols[c]));
+    if (rc != PXG_OK) return rc;
+    int64_t g = a.res.n_groups;
+    if (a.n_keys == 0 && g == 0) g = 1;
+    if (n_groups) *n_groups = g;
+    return pxg_agg_result_skip(agg, cols, n_cols, skip);
+  }
+  const int64_t G = a.res.n_groups;
+  for (int k = 0; k < a.n_keys; ++k)
+    if (a.key_types[k] == PXG_STRING) cols[k].data_len = a.res.key_data_len[k];
+  // Quantile columns not skipped: 7 doubles per group, after the quantile kernels.
+  bool q = false;
+  for (int u = 0; u < a.n_udas; ++u) {
+    pxg_column_out& o = cols[a.n_keys + u];
+    if (a.uda_kind[u] != PXG_UDA_QUANTILES) continue;
+    o.type = a.uda_out_type[u];
+    o.length = G;
+    if (skip && skip[a.n_keys + u]) continue;
+    o.values = ResultAlloc(static_cast<size_t>(G) * 56);
+    if (!o.values) {
+      pxg_result_free(cols, n_cols);
+      return SetError(PXG_RESOURCE_UNAVAILABLE, "host result allocation failed");
+    }
+    PXG_HIP(hipMemcpyAsync(o.values, a.res.uda_out[u].p, static_cast<size_t>(G) * 56, hipMemcpyDeviceToHost, a.ctx->stream));
+    q = true;
+  }
+  if (q) PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  if (n_groups) *n_groups = G;
   return PXG_OK;
 }
 

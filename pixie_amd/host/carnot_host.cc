@@ -14,6 +14,7 @@
 // math_sketches.h:40-54, and pluck_float64 of it, json_ops.h:131-153) is host-side output
 // formatting, as in the reference, where UDA Finalize runs on the host.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <cmath>
@@ -1370,7 +1371,32 @@ class GpuAggNode : public ExecNode {
   Status Emit(ExecState* s, bool eow, bool eos) {
     StageClock clk;
     int64_t groups = 0;
-    PXG_CALL(pxg_agg_finalize(agg_, &groups));
+    // Every consumer takes device batches (the agg -> equijoin hand-off): the result stays in HBM.
+    bool dev_ok = !children_.empty() && !emit_states;
+    for (auto& ch : children_) dev_ok = dev_ok && ch.first->AcceptsDeviceBatch();
+    std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
+    // A quantiles column no consumer reads as a string (the pluck-only C2 shape) is not copied
+    // out: only the plucked lanes and a per-group finiteness flag come back (pluck on the device).
+    std::vector<uint8_t> skip(out.size(), 0);
+    std::vector<uint32_t> lanes(out.size(), 0);
+    quantiles_raw_.clear();
+    quantile_lanes_.clear();
+    for (size_t c = keys.size(); c < out.size() && !emit_states; ++c) {
+      if (udas[c - keys.size()].kind != PXG_UDA_QUANTILES) continue;
+      bool observed = false;
+      for (auto& ch : children_) {
+        observed = observed || ch.first->ReadsColumnValue(c);
+        lanes[c] |= ch.first->PluckedLanes(c);
+      }
+      skip[c] = observed || !DevicePluck() ? 0 : 1;
+    }
+    bool fetched = false;
+    if (dev_ok) {
+      PXG_CALL(pxg_agg_finalize(agg_, &groups));
+    } else {  // finalize with the result copies overlapping it
+      PXG_CALL(pxg_agg_finalize_result(agg_, &groups, out.data(), static_cast<int32_t>(out.size()), skip.data()));
+      fetched = true;
+    }
     if (hints_) (*hints_)[HintKey()] = std::max<int64_t>(groups, 1);
     if (stats_.collect) {
       int64_t sel = 0;
@@ -1378,9 +1404,6 @@ class GpuAggNode : public ExecNode {
       stats_.AddExtraMetric("groups", static_cast<double>(groups));
     }
     clk.Mark("agg finalize");
-    // Every consumer takes device batches (the agg -> equijoin hand-off): the result stays in HBM.
-    bool dev_ok = !children_.empty() && !emit_states;
-    for (auto& ch : children_) dev_ok = dev_ok && ch.first->AcceptsDeviceBatch();
     if (dev_ok) {
       std::vector<pxg_column_view> dv(keys.size() + udas.size());
       int64_t bytes = 0;
@@ -1401,23 +1424,7 @@ class GpuAggNode : public ExecNode {
       }
       if (rc != PXG_UNIMPLEMENTED) return FromPxg(rc);
     }
-    std::vector<pxg_column_out> out(keys.size() + (emit_states ? 1 : udas.size()));
-    // A quantiles column no consumer reads as a string (the pluck-only C2 shape) is not copied
-    // out: only the plucked lanes and a per-group finiteness flag come back (pluck on the device).
-    std::vector<uint8_t> skip(out.size(), 0);
-    std::vector<uint32_t> lanes(out.size(), 0);
-    quantiles_raw_.clear();
-    quantile_lanes_.clear();
-    for (size_t c = keys.size(); c < out.size() && !emit_states; ++c) {
-      if (udas[c - keys.size()].kind != PXG_UDA_QUANTILES) continue;
-      bool observed = false;
-      for (auto& ch : children_) {
-        observed = observed || ch.first->ReadsColumnValue(c);
-        lanes[c] |= ch.first->PluckedLanes(c);
-      }
-      skip[c] = observed || !DevicePluck() ? 0 : 1;
-    }
-    PXG_CALL(pxg_agg_result_skip(agg_, out.data(), static_cast<int32_t>(out.size()), skip.data()));
+    if (!fetched) PXG_CALL(pxg_agg_result_skip(agg_, out.data(), static_cast<int32_t>(out.size()), skip.data()));
     const int64_t G = out.empty() ? 0 : out[0].length;
     for (size_t c = 0; c < out.size(); ++c) {
       if (!skip[c] || groups == 0) continue;
@@ -2879,6 +2886,18 @@ class ExecutionGraph {
 // PXRB serialisation of the sinks (layout of tests/oracle_client.py::parse_pxrb).  The buffer
 // is malloc'ed, sized up front and handed to the caller as is (pxc_free), so a result is
 // written once: no growth copies and no second copy-out.
+// PXRB STRING offsets relative to the column's first offset.
+static void RebaseOffsets(uint8_t* dst, const int32_t* src, size_t count, int32_t o0) {
+  if (o0 == 0) {
+    std::memcpy(dst, src, 4 * count);
+    return;
+  }
+  for (size_t i = 0; i < count; ++i) {
+    const int32_t v = src[i] - o0;
+    std::memcpy(dst + 4 * i, &v, 4);
+  }
+}
+
 struct Writer {
   uint8_t* p = nullptr;
   size_t n = 0, cap = 0;
@@ -2907,6 +2926,7 @@ struct Writer {
   void bytes(const void* src, size_t k) {
     if (k) std::memcpy(claim(k), src, k);
   }
+  void offsets(const int32_t* src, size_t count, int32_t o0) { RebaseOffsets(claim(4 * count), src, count, o0); }
   uint8_t* release(int64_t* len) {
     *len = static_cast<int64_t>(n);
     if (!p) p = static_cast<uint8_t*>(pxg_host_alloc(1));
@@ -2933,6 +2953,33 @@ static size_t BatchBytes(const RowBatch& rb) {
   return b;
 }
 
+// Writes the small header fields at once and records every column copy as a task, so the bulk
+// of a result is copied by several threads (a single 64K-group batch included).
+struct CopyTask {
+  uint8_t* dst;
+  const void* src;
+  size_t bytes;  // bytes to write
+  int32_t o0;    // offsets task: the first offset (src is int32_t[])
+  bool offs;
+};
+struct TaskWriter {
+  uint8_t* p;
+  std::vector<CopyTask>* tasks;
+  uint8_t* claim(size_t k) {
+    uint8_t* at = p;
+    p += k;
+    return at;
+  }
+  template <typename V>
+  void put(V v) {
+    std::memcpy(claim(sizeof(V)), &v, sizeof(V));
+  }
+  void bytes(const void* src, size_t k) {
+    if (k) tasks->push_back({claim(k), src, k, 0, false});
+  }
+  void offsets(const int32_t* src, size_t count, int32_t o0) { tasks->push_back({claim(4 * count), src, 4 * count, o0, true}); }
+};
+
 // Writes at a fixed position of a buffer sized up front (the parallel PXRB pass).
 struct SpanWriter {
   uint8_t* p;
@@ -2948,6 +2995,7 @@ struct SpanWriter {
   void bytes(const void* src, size_t k) {
     if (k) std::memcpy(claim(k), src, k);
   }
+  void offsets(const int32_t* src, size_t count, int32_t o0) { RebaseOffsets(claim(4 * count), src, count, o0); }
 };
 
 template <typename W>
@@ -2965,17 +3013,10 @@ static void WriteBatch(W* w, const RowBatch& rb) {
       case U: w->bytes(c.values, n * 16); break;
       case S: {
         const int32_t o0 = n ? c.offsets[0] : 0;
-        int32_t* dst = reinterpret_cast<int32_t*>(w->claim(4 * (n + 1)));
         if (!n) {
-          const int32_t z = 0;
-          std::memcpy(dst, &z, 4);
-        } else if (o0 == 0) {
-          std::memcpy(dst, c.offsets, 4 * (n + 1));
+          w->template put<int32_t>(0);
         } else {
-          for (size_t i = 0; i <= n; ++i) {
-            const int32_t v = c.offsets[i] - o0;
-            std::memcpy(dst + i, &v, 4);
-          }
+          w->offsets(c.offsets, n + 1, o0);
         }
         if (n) w->bytes(c.data + o0, static_cast<size_t>(c.offsets[n] - o0));
         break;
@@ -3211,44 +3252,49 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
-  // Large results: the batches are copied by several threads, each into its own byte range
-  // (a single thread copied C5's 195 MB result at ~15 GB/s).
-  struct Job {
-    const RowBatch* rb;
-    size_t at;
-  };
-  std::vector<Job> jobs;
+  // The headers are written here; every column copy becomes a task, and tasks are split into
+  // ~1 MB pieces shared by up to 8 threads for large results (a single thread copied C5's
+  // 195 MB result at ~15 GB/s), even when they are one batch.
+  std::vector<CopyTask> tasks;
   for (auto* sk : g.sinks_) {
     w.put<uint32_t>(static_cast<uint32_t>(sk->name.size()));
     w.bytes(sk->name.data(), sk->name.size());
     w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
     for (auto& rb : sk->batches) {
       const size_t b = BatchBytes(rb);
-      jobs.push_back({&rb, w.n});
+      TaskWriter tw{w.p + w.n, &tasks};
       w.claim(b);
+      WriteBatch(&tw, rb);
     }
   }
-  const size_t nthreads = total < (size_t(8) << 20) ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+  constexpr size_t kPiece = size_t(1) << 20;
+  std::vector<CopyTask> pieces;
+  for (const CopyTask& t : tasks) {
+    if (t.offs) {  // 4-byte elements: split on element boundaries
+      for (size_t at = 0; at < t.bytes; at += kPiece)
+        pieces.push_back({t.dst + at, static_cast<const int32_t*>(t.src) + at / 4, std::min(kPiece, t.bytes - at), t.o0, true});
+    } else {
+      for (size_t at = 0; at < t.bytes; at += kPiece)
+        pieces.push_back({t.dst + at, static_cast<const uint8_t*>(t.src) + at, std::min(kPiece, t.bytes - at), 0, false});
+    }
+  }
+  auto run_piece = [](const CopyTask& t) {
+    if (t.offs) RebaseOffsets(t.dst, static_cast<const int32_t*>(t.src), t.bytes / 4, t.o0);
+    else std::memcpy(t.dst, t.src, t.bytes);
+  };
+  // Threads pay from ~32 MB (C2's 4.8 MB result: 0.12 ms on one thread, 0.23 ms with four).
+  const size_t nthreads = total < (size_t(32) << 20)
+                              ? 1
+                              : std::min<size_t>({8, total >> 24, pieces.size(), std::max(1u, std::thread::hardware_concurrency())});
   if (nthreads <= 1) {
-    for (auto& j : jobs) {
-      SpanWriter sw{w.p + j.at};
-      WriteBatch(&sw, *j.rb);
-    }
-  } else {  // contiguous job ranges of ~equal bytes
+    for (const CopyTask& t : pieces) run_piece(t);
+  } else {
+    std::atomic<size_t> next{0};
     std::vector<std::thread> th;
-    size_t j0 = 0;
-    for (size_t k = 0; k < nthreads && j0 < jobs.size(); ++k) {
-      const size_t goal = jobs[j0].at + (w.n - jobs[j0].at) / (nthreads - k);
-      size_t j1 = j0 + 1;
-      while (j1 < jobs.size() && jobs[j1].at < goal) ++j1;
-      th.emplace_back([&jobs, &w, j0, j1] {
-        for (size_t j = j0; j < j1; ++j) {
-          SpanWriter sw{w.p + jobs[j].at};
-          WriteBatch(&sw, *jobs[j].rb);
-        }
+    for (size_t k = 0; k < nthreads; ++k)
+      th.emplace_back([&] {
+        for (size_t i = next.fetch_add(1); i < pieces.size(); i = next.fetch_add(1)) run_piece(pieces[i]);
       });
-      j0 = j1;
-    }
     for (auto& t : th) t.join();
   }
   *out = w.release(out_len);

@@ -57,3 +57,69 @@ def test_quantile_lanes_match_full_result(ctx):
     assert lib.pxg_agg_quantile_lanes(a.h, 0, 1, None, fin.ctypes.data_as(C.c_void_p)) != 0
     a.close()
     t.close()
+
+
+def _cols_bytes(outs, n, per_row=None):
+    """Every column of a pxg_column_out array as raw bytes (values / offsets / payload)."""
+    from pixie_amd.device import column_from_out
+    res = []
+    for j in range(n):
+        if not outs[j].values and not outs[j].offsets:
+            res.append((outs[j].type, None, None, None))
+            continue
+        c = column_from_out(outs[j], (per_row or {}).get(j, 1))
+        res.append((c.type, None if c.values is None else np.asarray(c.values).tobytes(),
+                    None if c.offsets is None else np.asarray(c.offsets).tobytes(),
+                    None if c.data is None else np.asarray(c.data)[:int(np.asarray(c.offsets)[-1])].tobytes() if c.offsets is not None else None))
+    return res
+
+
+@pytest.mark.parametrize("skip_q", [0, 1])
+def test_finalize_result_equals_finalize_then_result(ctx, skip_q):
+    """pxg_agg_finalize_result (result copies issued inside the finalize, overlapping it) gives
+    the same rows as pxg_agg_finalize followed by pxg_agg_result_skip (group order is the
+    table's, which differs run to run, so rows are compared by key); a skipped quantiles column
+    comes back typed and sized without buffers."""
+    from pixie_amd.device import column_from_out
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(20250117, 0, 3_000_000, 10_000_000)
+    q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
+    a = q.make_agg(ctx)
+    lib = ctx.lib
+    skip = (C.c_uint8 * 5)(0, 0, 0, 0, skip_q)
+
+    def rows_of(outs, G):
+        cols = [column_from_out(outs[j]).to_list() for j in range(4)]
+        qv = None
+        if not skip_q:
+            qv = column_from_out(outs[4], 7).values
+        out = {}
+        for g in range(G):
+            out[(cols[0][g], cols[1][g])] = (cols[2][g], cols[3][g], None if qv is None else tuple(qv[g]))
+        return out
+
+    a.consume(t)
+    ng = C.c_int64(0)
+    assert lib.pxg_agg_finalize(a.h, C.byref(ng)) == 0
+    ref = (_lib.ColumnOut * 5)()
+    assert lib.pxg_agg_result_skip(a.h, ref, 5, skip) == 0
+    want = rows_of(ref, ng.value)
+    lib.pxg_result_free(ref, 5)
+    a.reset()
+    a.consume(t)
+    got_o = (_lib.ColumnOut * 5)()
+    ng2 = C.c_int64(0)
+    assert lib.pxg_agg_finalize_result(a.h, C.byref(ng2), got_o, 5, skip) == 0
+    assert ng2.value == ng.value > 20_000
+    if skip_q:
+        assert got_o[4].length == ng.value and not got_o[4].values
+    got = rows_of(got_o, ng2.value)
+    lib.pxg_result_free(got_o, 5)
+    assert set(got) == set(want)
+    for k, (c, m, qq) in want.items():
+        gc, gm, gq = got[k]
+        assert gc == c and abs(gm - m) <= 1e-12 * abs(m), k
+        if qq is not None and c <= 8000:
+            assert gq == qq, k
+    a.close()
+    t.close()
