@@ -3252,48 +3252,71 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
-  // The headers are written here; every column copy becomes a task, and tasks are split into
-  // ~1 MB pieces shared by up to 8 threads for large results (a single thread copied C5's
-  // 195 MB result at ~15 GB/s), even when they are one batch.
-  std::vector<CopyTask> tasks;
+  // Large results are copied by up to 8 threads (a single thread copied C5's 195 MB result at
+  // ~15 GB/s; threads pay from ~32 MB, C2's 4.8 MB took 0.12 ms on one thread and 0.23 with
+  // four).  Many batches (C5: 2634): each thread writes a contiguous range of whole batches.
+  // Few large batches: the headers are written first and every column copy becomes ~1 MB
+  // pieces shared by the threads.
+  struct Job {
+    const RowBatch* rb;
+    size_t at;
+  };
+  std::vector<Job> jobs;
   for (auto* sk : g.sinks_) {
     w.put<uint32_t>(static_cast<uint32_t>(sk->name.size()));
     w.bytes(sk->name.data(), sk->name.size());
     w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
     for (auto& rb : sk->batches) {
-      const size_t b = BatchBytes(rb);
-      TaskWriter tw{w.p + w.n, &tasks};
-      w.claim(b);
-      WriteBatch(&tw, rb);
+      jobs.push_back({&rb, w.n});
+      w.claim(BatchBytes(rb));
     }
   }
-  constexpr size_t kPiece = size_t(1) << 20;
-  std::vector<CopyTask> pieces;
-  for (const CopyTask& t : tasks) {
-    if (t.offs) {  // 4-byte elements: split on element boundaries
-      for (size_t at = 0; at < t.bytes; at += kPiece)
-        pieces.push_back({t.dst + at, static_cast<const int32_t*>(t.src) + at / 4, std::min(kPiece, t.bytes - at), t.o0, true});
-    } else {
-      for (size_t at = 0; at < t.bytes; at += kPiece)
-        pieces.push_back({t.dst + at, static_cast<const uint8_t*>(t.src) + at, std::min(kPiece, t.bytes - at), 0, false});
-    }
-  }
-  auto run_piece = [](const CopyTask& t) {
-    if (t.offs) RebaseOffsets(t.dst, static_cast<const int32_t*>(t.src), t.bytes / 4, t.o0);
-    else std::memcpy(t.dst, t.src, t.bytes);
-  };
-  // Threads pay from ~32 MB (C2's 4.8 MB result: 0.12 ms on one thread, 0.23 ms with four).
-  const size_t nthreads = total < (size_t(32) << 20)
-                              ? 1
-                              : std::min<size_t>({8, total >> 24, pieces.size(), std::max(1u, std::thread::hardware_concurrency())});
+  const size_t nthreads = total < (size_t(32) << 20) ? 1 : std::min<size_t>({8, total >> 24, std::max(1u, std::thread::hardware_concurrency())});
   if (nthreads <= 1) {
-    for (const CopyTask& t : pieces) run_piece(t);
+    for (auto& j : jobs) {
+      SpanWriter sw{w.p + j.at};
+      WriteBatch(&sw, *j.rb);
+    }
+  } else if (jobs.size() >= 4 * nthreads) {
+    std::vector<std::thread> th;
+    size_t j0 = 0;
+    for (size_t k = 0; k < nthreads && j0 < jobs.size(); ++k) {  // contiguous ranges of ~equal bytes
+      const size_t goal = jobs[j0].at + (w.n - jobs[j0].at) / (nthreads - k);
+      size_t j1 = j0 + 1;
+      while (j1 < jobs.size() && jobs[j1].at < goal) ++j1;
+      th.emplace_back([&jobs, &w, j0, j1] {
+        for (size_t j = j0; j < j1; ++j) {
+          SpanWriter sw{w.p + jobs[j].at};
+          WriteBatch(&sw, *jobs[j].rb);
+        }
+      });
+      j0 = j1;
+    }
+    for (auto& t : th) t.join();
   } else {
+    std::vector<CopyTask> tasks;
+    for (auto& j : jobs) {
+      TaskWriter tw{w.p + j.at, &tasks};
+      WriteBatch(&tw, *j.rb);
+    }
+    constexpr size_t kPiece = size_t(1) << 20;
+    std::vector<CopyTask> pieces;
+    for (const CopyTask& t : tasks) {
+      for (size_t at = 0; at < t.bytes; at += kPiece) {
+        const size_t len = std::min(kPiece, t.bytes - at);
+        if (t.offs) pieces.push_back({t.dst + at, static_cast<const int32_t*>(t.src) + at / 4, len, t.o0, true});
+        else pieces.push_back({t.dst + at, static_cast<const uint8_t*>(t.src) + at, len, 0, false});
+      }
+    }
     std::atomic<size_t> next{0};
     std::vector<std::thread> th;
-    for (size_t k = 0; k < nthreads; ++k)
+    for (size_t k = 0; k < std::min(nthreads, pieces.size()); ++k)
       th.emplace_back([&] {
-        for (size_t i = next.fetch_add(1); i < pieces.size(); i = next.fetch_add(1)) run_piece(pieces[i]);
+        for (size_t i = next.fetch_add(1); i < pieces.size(); i = next.fetch_add(1)) {
+          const CopyTask& t = pieces[i];
+          if (t.offs) RebaseOffsets(t.dst, static_cast<const int32_t*>(t.src), t.bytes / 4, t.o0);
+          else std::memcpy(t.dst, t.src, t.bytes);
+        }
       });
     for (auto& t : th) t.join();
   }
