@@ -17,6 +17,7 @@ constexpr int kRadixItems = 12;
 constexpr int kRadixTile = kRadixBlock * kRadixItems;
 constexpr int kRadixBits = 8;
 constexpr int kRadixBuckets = 1 << kRadixBits;
+constexpr int kRsScanBlock = 256;
 
 struct ValPtrs {
   uint64_t* p[kMaxVals];
@@ -41,7 +42,9 @@ __device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restr
 // round trip while ~1000 tiles start at once.
 // ---------------------------------------------------------------------------------------
 
-// Tile digit counts of one pass -> hist[d * ntiles + tile].  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
+// Tile digit counts of one pass -> hist[tile * kRadixBuckets + d] (tile-major: one contiguous
+// 1 KB row per workgroup; the digit-major layout cost one partial-line write per digit and
+// tile, ~10M scattered writes per pass at 1B rows).  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
 // them instead of gathering again.
 __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
                                                             const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G, int shift,
@@ -83,12 +86,77 @@ __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __re
   uint32_t t = 0;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) t += h[w][threadIdx.x];
-  hist[static_cast<uint64_t>(threadIdx.x) * ntiles + tile] = t;
+  hist[static_cast<uint64_t>(tile) * kRadixBuckets + threadIdx.x] = t;
+  (void)ntiles;
+}
+
+// The tile offsets from the tile-major counts, in three coalesced kernels: per range of
+// kRsTilesPerPart tiles the digit sums (RsPart), per digit the exclusive scan of those sums and
+// the digit total (RsPartScan), per range the running offsets tile by tile plus the digit
+// base (RsDown, in place: hist[tile][d] becomes the output position of the tile's first d).
+constexpr uint32_t kRsTilesPerPart = 16;
+__global__ void __launch_bounds__(kRadixBuckets) RsPartKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                              uint32_t* __restrict__ part) {
+  const uint32_t w = blockIdx.x, d = threadIdx.x;
+  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
+  uint32_t s = 0;
+  for (uint32_t t = t0; t < t1; ++t) s += hist[static_cast<uint64_t>(t) * kRadixBuckets + d];
+  part[static_cast<uint64_t>(w) * kRadixBuckets + d] = s;
+}
+__global__ void __launch_bounds__(kRsScanBlock) RsPartScanKernel(uint32_t* __restrict__ part, uint32_t nparts,
+                                                                 uint32_t* __restrict__ ghist) {
+  constexpr int kWaves = kRsScanBlock / 64;
+  __shared__ uint32_t s_w[kWaves];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint32_t d = blockIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < nparts; i0 += kRsScanBlock) {
+    const uint32_t i = i0 + t;
+    const uint32_t c = i < nparts ? part[static_cast<uint64_t>(i) * kRadixBuckets + d] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int w = 0; w < wid; ++w) before += s_w[w];
+    uint32_t round = 0;
+    for (int w = 0; w < kWaves; ++w) round += s_w[w];
+    if (i < nparts) part[static_cast<uint64_t>(i) * kRadixBuckets + d] = before + incl - c;
+    carry += round;
+    __syncthreads();
+  }
+  if (t == 0) ghist[d] = carry;
+}
+__global__ void __launch_bounds__(kRadixBuckets) RsDownKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                              const uint32_t* __restrict__ part, const uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s[kRadixBuckets];
+  const uint32_t w = blockIdx.x, d = threadIdx.x;
+  // digit base: exclusive scan of the digit totals (Hillis-Steele over 256 values)
+  const uint32_t tot = ghist[d];
+  s[d] = tot;
+  __syncthreads();
+  for (int o = 1; o < kRadixBuckets; o <<= 1) {
+    const uint32_t x = d >= static_cast<uint32_t>(o) ? s[d - o] : 0u;
+    __syncthreads();
+    s[d] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[d] - tot + part[static_cast<uint64_t>(w) * kRadixBuckets + d];
+  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
+  for (uint32_t t = t0; t < t1; ++t) {
+    uint32_t* h = hist + static_cast<uint64_t>(t) * kRadixBuckets + d;
+    const uint32_t c = *h;
+    *h = run;
+    run += c;
+  }
 }
 
 // Block d: digit d's total over all tiles (the digit bases come from these; per-tile atomics
 // into 256 global totals were a contention point).
-constexpr int kRsScanBlock = 256;
 __global__ void __launch_bounds__(kRsScanBlock) RsTotalKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
                                                               uint32_t* __restrict__ ghist) {
   __shared__ uint32_t s[kRsScanBlock];
@@ -177,7 +245,8 @@ __global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* _
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
   const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);  // as in RsHistKernel
   for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
-  gofs[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * ntiles + tile];
+  gofs[threadIdx.x] = offs[static_cast<uint64_t>(tile) * kRadixBuckets + threadIdx.x];
+  (void)ntiles;
   WaveSync();
   const uint64_t tile0 = static_cast<uint64_t>(tile) * kRadixTile;
   const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
@@ -282,6 +351,8 @@ static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* 
   const uint32_t ntiles = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
   PXG_RETURN_IF_ERROR(ws.hist.Ensure(static_cast<size_t>(ntiles) * kRadixBuckets * 4));
   PXG_RETURN_IF_ERROR(ws.ghist.Ensure(static_cast<size_t>(kRsMaxPasses) * kRadixBuckets * 4));
+  const uint32_t nparts = (ntiles + kRsTilesPerPart - 1) / kRsTilesPerPart;
+  PXG_RETURN_IF_ERROR(ws.part.Ensure(static_cast<size_t>(nparts) * kRadixBuckets * 4));
   uint32_t* ghist = ws.ghist.as<uint32_t>();
   // With a rank map, the first histogram pass writes the dense keys into kbuf[1] (which the
   // first scatter does not write) and the scatters read those.
@@ -293,10 +364,12 @@ static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* 
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist", RsHistKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, n, gather ? rank : nullptr, cap,
                                G, shift0 + p * kRadixBits, ws.hist.as<uint32_t>(), ntiles, gather ? kbuf[1] : nullptr));
     if (gather) kin = kbuf[1];
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsTotalKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0,
-                               static_cast<const uint32_t*>(ws.hist.as<uint32_t>()), ntiles, gh));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsScanKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0, ws.hist.as<uint32_t>(), ntiles,
-                               static_cast<const uint32_t*>(gh)));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsPartKernel, dim3(nparts), dim3(kRadixBuckets), 0,
+                               static_cast<const uint32_t*>(ws.hist.as<uint32_t>()), ntiles, ws.part.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsPartScanKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0, ws.part.as<uint32_t>(),
+                               nparts, gh));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsDownKernel, dim3(nparts), dim3(kRadixBuckets), 0, ws.hist.as<uint32_t>(), ntiles,
+                               static_cast<const uint32_t*>(ws.part.as<uint32_t>()), static_cast<const uint32_t*>(gh)));
     PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RsScatterKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, kbuf[cur], vin, vbuf[cur],
                                nvals, n, shift0 + p * kRadixBits, ws.hist.as<const uint32_t>(), ntiles));
     kin = kbuf[cur];

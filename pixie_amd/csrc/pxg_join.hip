@@ -287,7 +287,7 @@ static int32_t JoinImpl(Table& B, Table& P, const pxg_join_spec& sp, pxg_table**
       for (DevBuf* b : bufs) PoolRelease(ctx, *b);
     }
   } back{ctx, {&slots, &rank, &meta, &bslot, &brefs, &kstart, &probed, &key_of, &cnt, &off, &ucnt, &uoff, &pref, &bref, &rws.key[0],
-               &rws.key[1], &rws.val[0], &rws.val[1], &rws.scan, &rws.rs.hist, &rws.rs.ghist}};
+               &rws.key[1], &rws.val[0], &rws.val[1], &rws.scan, &rws.rs.hist, &rws.rs.ghist, &rws.rs.part}};
   PXG_RETURN_IF_ERROR(PoolAlloc(ctx, slots, static_cast<size_t>(cap) * 8));
   PXG_RETURN_IF_ERROR(PoolAlloc(ctx, rank, static_cast<size_t>(cap) * 4 + 16));
   PXG_RETURN_IF_ERROR(PoolAlloc(ctx, meta, 64));

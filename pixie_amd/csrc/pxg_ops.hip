@@ -163,7 +163,6 @@ __global__ void __launch_bounds__(kOpsBlock) FilterCountKernel(const DevProgram*
                                                                const int32_t* __restrict__ types, const FDesc* __restrict__ fd,
                                                                unsigned long long* __restrict__ masks, uint32_t* __restrict__ fig, int64_t T) {
   const FBatch& fb = fd->fb;
-  const FSel& sel = fd->sel;
   __shared__ uint32_t s_cnt[1][kOpsBlock / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = fb.t_begin + blockIdx.x;

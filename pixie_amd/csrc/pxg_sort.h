@@ -7,7 +7,7 @@ namespace pxg {
 
 // Radix sort pass state: tile x digit counts / offsets and the global digit totals.
 struct RadixPassWs {
-  DevBuf hist, ghist;
+  DevBuf hist, ghist, part;  // hist: tile-major digit counts; part: per range of tiles
 };
 
 struct RadixWs {
