@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level par
 SEED = 20250117
 N_PAIR_KEYS = 10_000_000
 KERNELS = ["agg_consume", "agg_consume_prefix", "agg_records", "agg_publish_sizes", "agg_publish_write", "finalize_init", "slot_flags", "slot_gslot", "group_heads",
-           "radix_hist", "radix_scan", "radix_scatter",
+           "radix_hist_rank", "radix_hist", "radix_scan", "radix_scatter",
            "run_heads", "group_starts", "group_chunk_count", "chunk_reduce", "group_combine", "classify_groups",
            "digest_chain", "quant_tiny", "quant_small", "quant_mid", "big_setup", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
            "quant_sel_sample", "quant_sel_hist", "quant_sel_plan", "quant_sel_collect", "quant_sel_bin_sort", "quant_sel_digest",
