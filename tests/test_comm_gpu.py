@@ -39,12 +39,15 @@ _SELF = textwrap.dedent('''
     print("comm init", flush=True)
     comm = Comm(ctx, 0, 1, Comm.unique_id())
     print("exchange", flush=True)
-    a.reset()
-    a.consume(t)
-    sent, recv = a.alltoall(comm)
-    assert sent == recv and sent > 0
-    a.finalize()
-    merged = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
+    # the bench's step, three times in a row: reset -> consume -> alltoall -> finalize
+    for rep in range(3):
+        a.reset()
+        a.consume(t)
+        sent, recv = a.alltoall(comm)
+        assert sent == recv and sent > 0
+        a.finalize()
+        merged = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
+        assert len(merged) == len(local), (rep, len(merged), len(local))
     # Keys and counts are identical; the mean is a float sum whose order follows the
     # staging order, and consume places tiles in the staging in completion order (one atomic
     # per tile flush), so two consumes of the same table may differ in the last bits.
