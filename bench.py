@@ -38,7 +38,7 @@ KERNELS = ["agg_consume", "agg_consume_prefix", "agg_records", "agg_publish_size
            "digest_chain", "quant_tiny", "quant_small", "quant_mid", "big_setup", "quant_big_chunk_sort", "quant_big_merge", "quant_big_digest",
            "quant_sel_sample", "quant_sel_hist", "quant_sel_plan", "quant_sel_collect", "quant_sel_bin_sort", "quant_sel_digest",
            "key_extract", "key_string_copy", "scan_reduce", "scan_spine", "scan_downsweep",
-           "export_slot_part", "export_group_rank", "export_row_digit", "export_write_groups", "export_write_rows",
+           "export_slot_part", "export_group_rank", "export_row_digit", "export_centroids", "export_write_groups", "export_write_rows",
            "part_hist", "part_scatter", "part_starts", "import_keys", "import_rows",
            "hc_part_starts", "hc_agg", "hc_key_copy", "hc_spill",
            "split_sample", "split_ids", "split_hist", "split_scan", "split_scatter"]

@@ -747,9 +747,12 @@ constexpr uint32_t kTinyMax = 64;
 constexpr uint32_t kSmallMax = 1024;
 constexpr int kNumClasses = 4;
 
+// skip_flags (merged exchange): groups whose slot's flags word (macc, words per slot, last word)
+// has the digest flag get no class; their quantiles come from the merged digest instead.
 __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups,
                                                             uint32_t* __restrict__ lists, uint32_t* __restrict__ counts,
-                                                            uint32_t mid_max) {
+                                                            uint32_t mid_max, const uint64_t* __restrict__ skip_flags, int flag_words,
+                                                            const uint32_t* __restrict__ gslot) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
@@ -757,6 +760,7 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
   if (g < ngroups) {
     const uint32_t n = gstart[g + 1] - gstart[g];
     cls = n <= kTinyMax ? 0 : (n <= kSmallMax ? 1 : (n <= mid_max ? 2 : 3));
+    if (skip_flags && (skip_flags[static_cast<uint64_t>(gslot[g]) * flag_words + flag_words - 1] & 1ULL)) cls = -1;
   }
   // Block-aggregated list appends: wave leaders reserve within the block in LDS, then one
   // global atomic per class per block (the four class counters are hot addresses).
@@ -1363,7 +1367,10 @@ __global__ void __launch_bounds__(256) BigDigestKernel(const BigGroup* __restric
 // above, as BlockDigest.  xcnt[b] = the centroid count, or -1 when the group ships its values.
 constexpr int kXCentCap = kChainCap;
 constexpr int64_t kXRawMax = 8000;  // 8 * delta
-__global__ void __launch_bounds__(256) CentroidListKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ ngroups_p,
+// 1024 threads per group: one group of several million values otherwise kept four waves
+// streaming its large centroids alone (~1.2 ms of the export at 125M rows per rank).
+constexpr int kCentListBlock = 1024;
+__global__ void __launch_bounds__(kCentListBlock) CentroidListKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ ngroups_p,
                                                           const uint64_t* __restrict__ keysA, const uint64_t* __restrict__ keysB,
                                                           uint32_t* __restrict__ starts_all, const uint32_t* __restrict__ chain_starts,
                                                           const int32_t* __restrict__ chain_nc, uint64_t* __restrict__ xcent,
@@ -1401,18 +1408,27 @@ __global__ void __launch_bounds__(256) CentroidListKernel(const BigGroup* __rest
   }
   auto val = [&](int64_t j) -> double { return QVal(k[lead + j]); };
   uint64_t* out = xcent + static_cast<uint64_t>(blockIdx.x) * kXCentCap * 2;
+  // Small centroids: one thread each, incremental means (Centroid::add order).
   for (int64_t j = t; j < nc; j += blockDim.x) {
     const int64_t s = starts[j], e = j + 1 < nc ? starts[j + 1] : W;
-    double m;
-    if (e - s <= kSeqMean) {
-      m = CentroidMean(val, s, e);
-    } else {
-      double acc = 0;
-      for (int64_t x = s; x < e; ++x) acc += val(x);
-      m = acc / static_cast<double>(e - s);
-    }
-    out[2 * j] = FBits(m);
+    if (e - s > kSeqMean) continue;
+    out[2 * j] = FBits(CentroidMean(val, s, e));
     out[2 * j + 1] = static_cast<uint64_t>(e - s);
+  }
+  // Large centroids (thousands of values near the median of a multi-million-value group): one
+  // wave each, coalesced loads and a fixed shuffle tree (a thread per centroid summed them
+  // serially, ~2 ms per export at 125M rows per rank).
+  const int lane = t & 63, wid = t >> 6, nw = static_cast<int>(blockDim.x >> 6);
+  for (int64_t j = wid; j < nc; j += nw) {
+    const int64_t s = starts[j], e = j + 1 < nc ? starts[j + 1] : W;
+    if (e - s <= kSeqMean) continue;
+    double acc = 0;
+    for (int64_t x = s + lane; x < e; x += 64) acc += val(x);
+    acc = WaveSumF64(acc);
+    if (lane == 0) {
+      out[2 * j] = FBits(acc / static_cast<double>(e - s));
+      out[2 * j + 1] = static_cast<uint64_t>(e - s);
+    }
   }
   if (t == 0) xcnt[blockIdx.x] = static_cast<int32_t>(nc);
 }
@@ -3101,15 +3117,17 @@ int32_t AggFinalizeTable(Agg* a) {
                                    dst->as<uint64_t>(), w, pass));
       std::swap(src, dst);
     }
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
-                                 static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
-                                 ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err));
-    if (!a->export_x) return PXG_OK;
+    // An exchange export ships values / centroid lists, not quantiles: no digests there.
+    if (!a->export_x) {
+      return LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+                      static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
+                      ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err);
+    }
     // Exchange export: each big group's whole single-pass centroid list (those of > 8 * delta
     // values ship it instead of their values).
     PXG_RETURN_IF_ERROR(ws.xcent.Ensure(static_cast<size_t>(n_big_groups) * kXCentCap * 16 + 16));
     PXG_RETURN_IF_ERROR(ws.xcnt.Ensure(static_cast<size_t>(n_big_groups) * 4 + 16));
-    return LaunchOn(ctx, st, "quant_big_digest", CentroidListKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
+    return LaunchOn(ctx, st, "export_centroids", CentroidListKernel, dim3(n_big_groups), dim3(kCentListBlock), 0, ws.big.as<const BigGroup>(),
                     static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
                     ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, ws.xcent.as<uint64_t>(), ws.xcnt.as<int32_t>());
   };
@@ -3176,8 +3194,14 @@ int32_t AggFinalizeTable(Agg* a) {
   // 4. Quantile digests.
   if (any_q) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
+    // A merged exchange's groups that received centroid lists get their quantiles from the
+    // merged digest (FinalizeMerged): no class here, so the selection path never sees their
+    // centroid means as values (which made it fall back to the full sort).
+    const bool skip_merged = a->merged && a->macc_cap == a->cap;
     PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
-                               ngroups, ws.lists.as<uint32_t>(), d_cls, static_cast<uint32_t>(kMidMax)));
+                               ngroups, ws.lists.as<uint32_t>(), d_cls, static_cast<uint32_t>(kMidMax),
+                               skip_merged ? a->macc.as<const uint64_t>() : nullptr, a->macc_words,
+                               ws.gslot.as<const uint32_t>()));
     const uint32_t* lists = ws.lists.as<const uint32_t>();
     // Big-group metadata on the device; one readback of the class counts, the big-group chunk
     // total and the largest group (grid sizes and the merge-pass count).
@@ -3216,14 +3240,14 @@ int32_t AggFinalizeTable(Agg* a) {
     // The small digests follow the chains on the side stream (neither needs the other); the
     // reductions and the tiny digests run on the main stream meanwhile.
     const uint32_t small_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kTinyMax + 1) + 1));
-    for (int u = 0; u < a->n_udas; ++u) {
+    for (int u = 0; u < a->n_udas && !a->export_x; ++u) {  // (an export needs no quantiles)
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "quant_small", QuantSmallKernel, dim3((small_cap + kSmallWaves - 1) / kSmallWaves),
                                    dim3(256), 0, lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart,
                                    cv.p[a->uda_val[u]], a->uda_arg_type[u], R.uda_out[u].as<double>()));
     }
     PXG_RETURN_IF_ERROR(RunReductions());
-    for (int u = 0; u < a->n_udas; ++u) {
+    for (int u = 0; u < a->n_udas && !a->export_x; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
                                  static_cast<const uint32_t*>(d_cls), gstart, cv.p[a->uda_val[u]], a->uda_arg_type[u],
@@ -3273,7 +3297,7 @@ int32_t AggFinalizeTable(Agg* a) {
         PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(u) : BigSortPath(ctx->side2, u));
       }
       double* qo = R.uda_out[u].as<double>();
-      if (cls[2] > 0)
+      if (cls[2] > 0 && !a->export_x)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
                                    gstart, chain_starts, chain_nc, static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
     }
