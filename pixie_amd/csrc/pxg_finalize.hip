@@ -1052,7 +1052,10 @@ __device__ __forceinline__ PreChain PreChainAt(const uint32_t* starts_all, const
   return p;
 }
 
-template <typename KeyAt>
+// kStagePre: starts_buf is LDS; a precomputed chain is copied into it first (one coalesced
+// pass), so the quantile searches and centroid ranges read LDS instead of chains of dependent
+// global loads.
+template <bool kStagePre = false, typename KeyAt>
 __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_t max_c, PreChain pre, double* out7,
                             unsigned int* err, DigestShared& sh) {
   const int t = threadIdx.x;
@@ -1073,6 +1076,10 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_
   }
   const bool use_pre = pre.starts != nullptr && pre.W == W && pre.nc >= 0;
   const uint32_t* starts = use_pre ? pre.starts : starts_buf;
+  if (kStagePre && use_pre && pre.nc <= max_c) {  // the barrier below orders the copy
+    for (int64_t j = t; j < pre.nc; j += blockDim.x) starts_buf[j] = pre.starts[j];
+    starts = starts_buf;
+  }
   if (t == 0) {
     int64_t nc;
     if (use_pre) nc = pre.nc;
@@ -1127,9 +1134,31 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_
   __syncthreads();
 }
 
-// One workgroup per group with 1024 < n <= 4096: LDS bitonic sort + digest.
+// Boundary chains of every mid-class size W (kSingletonMaxW < W <= kMidMax).  A chain depends
+// on W alone (DigestBoundaries never reads a value), so the table is built once per context
+// (one wave per W, ~0.2 ms) and the mid digests index it by group size instead of waiting for
+// the per-finalize chain kernel.  A group whose NaN-trimmed size differs from its row count
+// builds its own chain in the digest (BlockDigest), as before.
+constexpr int kMidChainW0 = kSingletonMaxW + 1;
+constexpr int kMidChainN = kMidMax - kSingletonMaxW;
+__global__ void __launch_bounds__(256) MidChainTableKernel(uint32_t* __restrict__ starts, int32_t* __restrict__ nc) {
+  const int i = static_cast<int>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= kMidChainN) return;
+  const int64_t n = DigestBoundariesWave(static_cast<int64_t>(kMidChainW0 + i), starts + static_cast<uint64_t>(i) * kChainCap, kChainCap);
+  if ((threadIdx.x & 63) == 0) nc[i] = static_cast<int32_t>(n);
+}
+__device__ __forceinline__ PreChain MidPreChain(const uint32_t* tab, const int32_t* tab_nc, int64_t n) {
+  PreChain p;
+  const bool in = n >= kMidChainW0 && n < kMidChainW0 + kMidChainN;
+  p.starts = in ? tab + static_cast<uint64_t>(n - kMidChainW0) * kChainCap : nullptr;
+  p.nc = in ? tab_nc[n - kMidChainW0] : -1;
+  p.W = n;
+  return p;
+}
+
+// One workgroup per group with 1024 < n <= 4096: LDS merge sort + digest.
 __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
-                                                      const uint32_t* __restrict__ chain_starts, const int32_t* __restrict__ chain_nc,
+                                                      const uint32_t* __restrict__ mid_starts, const int32_t* __restrict__ mid_nc,
                                                       const uint32_t* __restrict__ nlist_p, const uint64_t* __restrict__ vals,
                                                       int arg_type, double* __restrict__ out, unsigned int* __restrict__ err) {
   __shared__ uint64_t keys[PaddedLen(kMidMax)];
@@ -1143,8 +1172,24 @@ __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict
   for (int i = threadIdx.x; i < P; i += blockDim.x) keys[PadIdx(i)] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
   __syncthreads();
   if (g_diag_quant != 2) BlockMergeSortLds(keys, P);
-  BlockDigest([&](int64_t i) -> uint64_t { return keys[PadIdx(static_cast<int>(i))]; }, n, starts, kMidCentroids,
-              PreChainAt(chain_starts, chain_nc, blockIdx.x, n), out + static_cast<uint64_t>(g) * 7, err, sh);
+  BlockDigest<true>([&](int64_t i) -> uint64_t { return keys[PadIdx(static_cast<int>(i))]; }, n, starts, kMidCentroids,
+              MidPreChain(mid_starts, mid_nc, n), out + static_cast<uint64_t>(g) * 7, err, sh);
+}
+
+// The mid-class chain table of a context, built on the ctx stream on first use (every reader
+// runs on that stream or after it).
+static constexpr size_t kMidChainStartBytes = static_cast<size_t>(kMidChainN) * kChainCap * 4;
+static int32_t EnsureMidChains(Ctx* ctx) {
+  if (ctx->mid_chains.p) return PXG_OK;
+  PXG_RETURN_IF_ERROR(ctx->mid_chains.Alloc(kMidChainStartBytes + static_cast<size_t>(kMidChainN) * 4));
+  const int32_t rc = Launch(ctx, "mid_chain_table", MidChainTableKernel, dim3((kMidChainN + 3) / 4), dim3(256), 0,
+                            ctx->mid_chains.as<uint32_t>(), reinterpret_cast<int32_t*>(ctx->mid_chains.as<uint8_t>() + kMidChainStartBytes));
+  if (rc != PXG_OK) ctx->mid_chains.Free();
+  return rc;
+}
+static const uint32_t* MidChainStarts(Ctx* ctx) { return ctx->mid_chains.as<const uint32_t>(); }
+static const int32_t* MidChainNc(Ctx* ctx) {
+  return reinterpret_cast<const int32_t*>(ctx->mid_chains.as<const uint8_t>() + kMidChainStartBytes);
 }
 
 // Big groups: chunk sort (one workgroup per 4096-element chunk) into sort keys.
@@ -1178,17 +1223,25 @@ struct BigGroup {
 };
 
 // Big-group metadata on the device (one block): per big group its offset, size and merge-pass
-// count, and its 4096-key chunks; meta gets the chunk total and the largest group.
+// count, and its 4096-key chunks; meta gets the chunk total and the largest group.  large_list
+// gets the indices of the groups above kSelLargeN values (any order) and large_cnt their count:
+// the 512-thread / 70 KB splitter launch runs only those, instead of one block per big group
+// that must find 70 KB of free LDS before it can exit.
 constexpr int kSetupBlock = 1024;
+constexpr uint64_t kSelLargeN = uint64_t(1) << 22;
 __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                               const uint32_t* __restrict__ gstart, BigGroup* __restrict__ groups,
-                                                              BigChunk* __restrict__ chunks, uint32_t* __restrict__ meta_out) {
+                                                              BigChunk* __restrict__ chunks, uint32_t* __restrict__ meta_out,
+                                                              uint32_t* __restrict__ large_list, uint32_t* __restrict__ large_cnt) {
   __shared__ uint32_t scan[kSetupBlock];
   __shared__ uint32_t s_off[kSetupBlock], s_n[kSetupBlock], s_pass[kSetupBlock];
-  __shared__ uint32_t s_max;
+  __shared__ uint32_t s_max, s_large;
   const uint32_t nbig = *count;
   const int t = threadIdx.x;
-  if (t == 0) s_max = 0;
+  if (t == 0) {
+    s_max = 0;
+    s_large = 0;
+  }
   uint32_t carry = 0;
   for (uint32_t b0 = 0; b0 < nbig; b0 += kSetupBlock) {
     const uint32_t i = b0 + t;
@@ -1221,6 +1274,7 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
       B.g = g;
       B.passes = passes;
       groups[i] = B;
+      if (n > kSelLargeN) large_list[atomicAdd(&s_large, 1u)] = i;
     }
     s_off[t] = off;
     s_n[t] = n;
@@ -1254,6 +1308,7 @@ __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __
   if (t == 0) {
     meta_out[0] = carry;  // total chunks
     meta_out[1] = s_max;  // largest big group
+    *large_cnt = s_large;
   }
 }
 
@@ -1753,15 +1808,84 @@ __device__ __forceinline__ int BinOfRank(const uint32_t* bs, uint32_t r) {
   return b;
 }
 
+// Guide table per group: kSelGuide equal-width buckets of the key range [lo, hi] = [S[1],
+// S[nb - 1]] (bucket i starts at lo + (i << sh), sh the smallest shift that leaves fewer than
+// kSelGuide buckets), entry i = SelBin of the bucket's start.  A key's bin then lies between
+// the entries of its bucket and its successor: a few splitter reads instead of a 12-step
+// search (bins are equi-depth, buckets equal-width; a bucket holds ~2 bins on average, ~6 at
+// the densest part of a lognormal).  The search result is SelBin's, bit for bit.
+constexpr int kSelGuideBits = 11;
+constexpr int kSelGuide = 1 << kSelGuideBits;
+constexpr int kSelGuideStride = kSelGuide + 2;  // u16 entries per group (kSelGuide + 1 used)
+
+__device__ __forceinline__ int SelGuideShift(uint64_t span) {
+  const int bits = span == 0 ? 0 : 64 - __clzll(static_cast<long long>(span));
+  return bits > kSelGuideBits ? bits - kSelGuideBits : 0;
+}
+__device__ __forceinline__ uint64_t SelGuideStart(uint64_t lo, int i, int sh) {
+  const uint64_t off = static_cast<uint64_t>(i) << sh;
+  if ((off >> sh) != static_cast<uint64_t>(i)) return ~0ULL;
+  const uint64_t v = lo + off;
+  return v < lo ? ~0ULL : v;
+}
+// Per-group constants of the guided search (S in LDS with S[0] = 0, nb >= 2).
+struct SelGuideK {
+  uint64_t lo, hi;
+  int sh, nb;
+};
+__device__ __forceinline__ SelGuideK SelGuideOf(const uint64_t* S, int nb) {
+  SelGuideK g;
+  g.lo = S[1];
+  g.hi = S[nb - 1];
+  g.sh = SelGuideShift(g.hi - g.lo);
+  g.nb = nb;
+  return g;
+}
+// Bracket [b, e] of a key's bin from the guide (b == e: decided).  Selects only: a branch
+// here made the compiler copy the callers' whole per-value arrays on every path.
+__device__ __forceinline__ void SelGuideBracket(const uint16_t* Gd, const SelGuideK& g, uint64_t key, int& b, int& e) {
+  const bool below = key < g.lo, above = key >= g.hi, ones = key == ~0ULL;
+  const int gi = (below || above) ? 0 : static_cast<int>((key - g.lo) >> g.sh);
+  const int gb = Gd[gi], ge = Gd[gi + 1];
+  const int fixed = ones ? kSelBins - 1 : below ? 0 : g.nb - 1;
+  const bool dec = below || above;  // (ones implies above)
+  b = dec ? fixed : gb;
+  e = dec ? fixed : ge;
+}
+// Last index in [b, e] whose splitter is <= key (S[b] <= key holds): binary lifting, the
+// rare wide brackets first, then three fixed steps.
+// Branch-free steps (the probe index is clamped to e, so every load is in range and no step
+// needs its own exec mask).
+__device__ __forceinline__ int SelGuideFinish(const uint64_t* S, uint64_t key, int b, int e) {
+  const int d = e - b;
+  if (d > 7) {
+    for (int step = 1 << (31 - __clz(d)); step >= 8; step >>= 1) {
+      const int m = min(b + step, e);
+      b = (b + step <= e && S[m] <= key) ? m : b;
+    }
+  }
+#pragma unroll
+  for (int step = 4; step >= 1; step >>= 1) {
+    const int m = min(b + step, e);
+    const uint64_t sm = S[m];
+    b = (b + step <= e && sm <= key) ? m : b;
+  }
+  return b;
+}
+
 // Splitters: 2 * nb keys at evenly spaced positions of the group, sorted; S[b] = every second
 // of them (b < nb), S[0] = 0, S[b >= nb] = ~0 (empty bins).  Two launches: groups sampling
 // <= 4096 keys (256 threads, 35 KB of LDS) and the few sampling 8192 (512 threads, 70 KB), so
 // the common case is not held to the large kernel's occupancy.
 template <int NS>
 __global__ void __launch_bounds__(NS / kMsIpt) BigSampleKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ nbig_p,
-                                                               const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl) {
-  if (blockIdx.x >= *nbig_p) return;
-  const BigGroup G = groups[blockIdx.x];
+                                                               const uint64_t* __restrict__ vals, int arg_type, uint64_t* __restrict__ spl,
+                                                               uint16_t* __restrict__ guide, const uint32_t* __restrict__ only,
+                                                               const uint32_t* __restrict__ only_cnt) {
+  // only != nullptr: block i serves big group only[i] (i < *only_cnt).
+  if (blockIdx.x >= (only ? *only_cnt : *nbig_p)) return;
+  const uint32_t bi = only ? only[blockIdx.x] : blockIdx.x;
+  const BigGroup G = groups[bi];
   const int nb = SelNb(G.n), ns = 2 * nb;
   if (ns > NS || (NS > kSelSample / 2 && ns <= kSelSample / 2)) return;  // the other launch's group
   __shared__ uint64_t keys[PaddedLen(NS)];
@@ -1782,49 +1906,65 @@ __global__ void __launch_bounds__(NS / kMsIpt) BigSampleKernel(const BigGroup* _
   }
   __syncthreads();
   BlockMergeSortLds(keys, ns);
-  uint64_t* S = spl + static_cast<uint64_t>(blockIdx.x) * kSelBins;
+  uint64_t* S = spl + static_cast<uint64_t>(bi) * kSelBins;
   for (int b = threadIdx.x; b < kSelBins; b += blockDim.x) S[b] = b == 0 ? 0ULL : b < nb ? keys[PadIdx(2 * b)] : ~0ULL;
+  auto Sk = [&](int b) -> uint64_t { return b == 0 ? 0ULL : keys[PadIdx(2 * b)]; };
+  const uint64_t lo = Sk(1), hi = Sk(nb - 1);
+  const int gsh = SelGuideShift(hi - lo);
+  uint16_t* Gd = guide + static_cast<uint64_t>(bi) * kSelGuideStride;
+  for (int i = threadIdx.x; i <= kSelGuide; i += blockDim.x) {
+    const uint64_t v = SelGuideStart(lo, i, gsh);
+    int b = 0;
+    for (int step = nb >> 1; step >= 1; step >>= 1)
+      if (Sk(b + step) <= v) b += step;
+    Gd[i] = static_cast<uint16_t>(b);
+  }
 }
 
 // Bin counts (and NaN count) per big group.  A workgroup takes cpb consecutive 4096-value
-// chunks (a group's chunks are consecutive; cpb = SelChunksPerBlock, up to 8 while the grid
-// still fills the chip): the splitters are loaded and the LDS counts flushed to the group's
-// global histogram once per group it meets, not once per chunk.
-// BigCollect (per-chunk range sums, latency-bound gathers) wants more blocks in flight than
-// BigHist (whose per-group flush is the cost it saves), hence the larger per-CU target.
+// chunks (a group's chunks are consecutive; cpb = SelChunksPerBlock): the splitters are loaded
+// and the LDS counts flushed to the group's global histogram once per group it meets, not once
+// per chunk.  Both BigHist and BigCollect load the next chunk while binning the current one,
+// so one resident round of blocks (3 per CU: LDS and VGPRs) keeps the memory system busy.
+// cpb is rounded up, so the grid never exceeds blocks_per_cu per CU (a second, partial round
+// of blocks would run alone on part of the chip).
 static uint32_t SelChunksPerBlock(uint32_t nchunks, int num_cus, uint32_t blocks_per_cu, uint32_t cap = 8) {
-  return std::max<uint32_t>(1, std::min<uint32_t>(cap, nchunks / (blocks_per_cu * static_cast<uint32_t>(num_cus))));
+  const uint32_t slots = blocks_per_cu * static_cast<uint32_t>(num_cus);
+  return std::max<uint32_t>(1, std::min<uint32_t>(cap, (nchunks + slots - 1) / slots));
 }
-// quant_sel_hist: every block flushes its LDS histogram (up to kSelBins device atomics) and loads
-// its group's splitters, so blocks take more chunks than the collect pass: up to 32 (1B rows:
-// 0.77 -> 0.60 ms average over the profiled launches, tools/n1_selhist_ab.sh; PXG_SEL_HIST_CPB
-// overrides).
+// quant_sel_hist's cap on chunks per block (PXG_SEL_HIST_CPB overrides; tools/n1_selhist_ab.sh).
 static uint32_t SelHistCap() {
   const char* e = std::getenv("PXG_SEL_HIST_CPB");
   const int v = e ? std::atoi(e) : 0;
-  return v > 0 ? static_cast<uint32_t>(v) : 32;
+  return v > 0 ? static_cast<uint32_t>(v) : 64;
 }
 __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                      const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
-                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ nan_cnt, uint32_t cpb) {
+                                                     const uint16_t* __restrict__ guide, uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ nan_cnt, uint32_t cpb) {
   const uint32_t nchunks = *nchunks_p;
   const uint32_t c0 = blockIdx.x * cpb;
   if (c0 >= nchunks) return;
   const uint32_t c1 = min(nchunks, c0 + cpb);
   __shared__ uint64_t S[kSelBins];
   __shared__ uint32_t h[kSelBins];
+  __shared__ uint16_t Gd[kSelGuide + 1];
   __shared__ uint32_t s_nan;
   constexpr int kPer = kMidMax / 256;
   uint32_t cur = 0xFFFFFFFFu;
-  int nb = 0;
-  for (uint32_t ci = c0; ci < c1; ++ci) {
-    const BigChunk c = chunks[ci];
-    uint64_t raw[kPer];
+  SelGuideK gk{0, 0, 0, 2};
+  // The next chunk's values are loaded while the current one is binned.
+  // Loads past a chunk's end re-read its last value (no exec-masked load branches; those
+  // lanes are not counted).
+  BigChunk c = chunks[c0];
+  uint64_t raw[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = k * 256 + threadIdx.x;
-      raw[k] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
-    }
+  for (int k = 0; k < kPer; ++k) raw[k] = vals[c.off + min(k * 256 + static_cast<int>(threadIdx.x), static_cast<int>(c.len) - 1)];
+  for (uint32_t ci = c0; ci < c1; ++ci) {
+    const BigChunk cn = ci + 1 < c1 ? chunks[ci + 1] : c;  // the last chunk re-reads itself
+    uint64_t rawn[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) rawn[k] = vals[cn.off + min(k * 256 + static_cast<int>(threadIdx.x), static_cast<int>(cn.len) - 1)];
     if (c.bidx != cur) {
       if (cur != 0xFFFFFFFFu) {  // flush the previous group's counts
         __syncthreads();
@@ -1835,30 +1975,39 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
         __syncthreads();
       }
       cur = c.bidx;
-      nb = SelNb(c.g_n);
+      const int nb = SelNb(c.g_n);
       const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
+      const uint16_t* Gg = guide + static_cast<uint64_t>(cur) * kSelGuideStride;
       for (int b = threadIdx.x; b < kSelBins; b += 256) {
         S[b] = b < nb ? Sg[b] : ~0ULL;
         h[b] = 0;
       }
+      for (int i = threadIdx.x; i <= kSelGuide; i += 256) Gd[i] = Gg[i];
       if (threadIdx.x == 0) s_nan = 0;
       __syncthreads();
+      gk = SelGuideOf(S, nb);
     }
-    // Every value's bin first (16 independent searches in flight), then the LDS counts: an
-    // atomic between two searches would order the next search's LDS reads behind it.
+    // Every value's bracket, then the lifting steps (16 independent searches in flight), then
+    // the LDS counts: an atomic between two searches would order the next one's reads behind it.
+    // (Keys are recomputed from raw rather than kept: 32 fewer VGPRs, one more wave per SIMD.)
     uint32_t nn = 0;
-    int bin[kPer];
+    int bin[kPer], bend[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint64_t key = QKey(raw[k], arg_type);
       const int i = k * 256 + threadIdx.x;
       nn += (i < static_cast<int>(c.len) && (key < kNegInfKey || key > kPosInfKey)) ? 1u : 0u;
-      bin[k] = SelBin(S, key, nb);
+      SelGuideBracket(Gd, gk, key, bin[k], bend[k]);
     }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) bin[k] = SelGuideFinish(S, QKey(raw[k], arg_type), bin[k], bend[k]);
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
       if (k * 256 + static_cast<int>(threadIdx.x) < static_cast<int>(c.len)) atomicAdd(&h[bin[k]], 1u);
     if (nn) atomicAdd(&s_nan, nn);
+    c = cn;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) raw[k] = rawn[k];
   }
   __syncthreads();
   uint32_t* H = hist + static_cast<uint64_t>(cur) * kSelBins;
@@ -1889,8 +2038,14 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
   const BigGroup G = groups[bi];
   const int64_t W = static_cast<int64_t>(G.n);
   const uint32_t* H = hist + static_cast<uint64_t>(bi) * kSelBins;
-  const uint32_t* starts = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
   const int32_t nc = chain_nc[bi];
+  // The chain staged in LDS for the recording pass's searches (ordered by the barriers below).
+  __shared__ uint32_t s_starts[kChainCap];
+  {
+    const uint32_t* gs = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
+    for (int j = t; j < nc; j += 256) s_starts[j] = gs[j];
+  }
+  const uint32_t* starts = s_starts;
   constexpr int kPer = kSelBins / 256;
   // exclusive scan of the bin counts
   uint32_t cnt[kPer], tot = 0;
@@ -2057,10 +2212,13 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
 // deterministic: wave w takes chunk positions [1024 w, 1024 (w + 1)) in 16 rounds, each
 // round's values of one range are summed by a fixed shuffle tree, rounds and waves in order.
 // A workgroup takes cpb consecutive chunks (as BigHistKernel); splitters and tags are reloaded
-// only when the group changes.
+// only when the group changes.  Gather slots are taken in two steps: LDS counters per gathered
+// bin, then one device atomic per bin and chunk reserves the bin's range — a device atomic per
+// value put its round trip in almost every 64-value round (~6% of values are gathered).
 __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                         const BigPlan* __restrict__ plans, const uint64_t* __restrict__ vals, int arg_type,
-                                                        const uint64_t* __restrict__ spl, const uint8_t* __restrict__ tag_all,
+                                                        const uint64_t* __restrict__ spl, const uint16_t* __restrict__ guide,
+                                                        const uint8_t* __restrict__ tag_all,
                                                         const uint32_t* __restrict__ cbase_all, uint32_t* __restrict__ cursor_all,
                                                         uint64_t* __restrict__ cand, double* __restrict__ partial, uint32_t cpb) {
   const uint32_t nchunks = *nchunks_p;
@@ -2069,72 +2227,106 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
   const uint32_t c1 = min(nchunks, c0 + cpb);
   __shared__ uint64_t S[kSelBins];
   __shared__ uint8_t tg[kSelBins];
+  __shared__ uint16_t Gd[kSelGuide + 1];
   __shared__ double acc[4][kSelMaxRanges];
+  __shared__ uint8_t cix[kSelBins];              // gathered bin -> its index in P.coll
+  __shared__ uint16_t s_coll[kSelMaxColl];
+  __shared__ uint32_t lcnt[kSelMaxColl], lbase[kSelMaxColl];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   constexpr int kRounds = kMidMax / 256;
   uint32_t cur = 0xFFFFFFFFu;
   int nb = kSelBins;
+  bool fresh = false;
+  SelGuideK gk{0, 0, 0, 2};
+  for (int k = t; k < kSelMaxColl; k += 256) lcnt[k] = 0;  // (the loop's first barrier orders it)
+  // (No next-chunk prefetch here: its 32 VGPRs cost a wave per SIMD and measured no faster.)
   for (uint32_t ci = c0; ci < c1; ++ci) {
     const BigChunk c = chunks[ci];
-    const BigPlan* P = plans + c.bidx;
-    if (P->fallback) continue;  // uniform
-    const int n_ranges = P->n_ranges;
     uint64_t raw[kRounds];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int i = wid * (kMidMax / 4) + r * 64 + lane;
-      raw[r] = i < static_cast<int>(c.len) ? vals[c.off + i] : 0ULL;
-    }
-    __syncthreads();  // the previous chunk's acc / S / tg readers are done
-    if (c.bidx != cur) {
-      cur = c.bidx;
-      nb = SelNb(c.g_n);
-      const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
-      const uint8_t* Tg = tag_all + static_cast<uint64_t>(cur) * kSelBins;
-      for (int b = t; b < kSelBins; b += 256) {
-        S[b] = b < nb ? Sg[b] : ~0ULL;
-        tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
+    for (int r = 0; r < kRounds; ++r) raw[r] = vals[c.off + min(wid * (kMidMax / 4) + r * 64 + lane, static_cast<int>(c.len) - 1)];
+    const BigPlan* P = plans + c.bidx;
+    if (!P->fallback) {  // uniform
+      const int n_ranges = P->n_ranges, n_coll = P->n_coll;
+      __syncthreads();  // the previous chunk's acc / S / tg / lbase readers are done
+      if (c.bidx != cur) {
+        cur = c.bidx;
+        nb = SelNb(c.g_n);
+        const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
+        const uint8_t* Tg = tag_all + static_cast<uint64_t>(cur) * kSelBins;
+        const uint16_t* Gg = guide + static_cast<uint64_t>(cur) * kSelGuideStride;
+        for (int b = t; b < kSelBins; b += 256) {
+          S[b] = b < nb ? Sg[b] : ~0ULL;
+          tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
+        }
+        for (int i = t; i <= kSelGuide; i += 256) Gd[i] = Gg[i];
+        for (int k = t; k < n_coll; k += 256) {
+          const int b = P->coll[k];
+          s_coll[k] = static_cast<uint16_t>(b);
+          cix[b] = static_cast<uint8_t>(k);
+        }
+        fresh = true;
       }
-    }
-    if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
-    __syncthreads();
-    const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
-    uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
-    uint64_t* cg = cand + c.g_off;
-    // Bins of the whole chunk first (independent searches in flight), then the gathers and
-    // the inside-range sums.
-    int bins[kRounds];
+      if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
+      __syncthreads();
+      if (fresh) {
+        gk = SelGuideOf(S, nb);
+        fresh = false;
+      }
+      const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
+      uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
+      uint64_t* cg = cand + c.g_off;
+      uint32_t ls[kRounds];  // gathered: (index in P.coll) << 16 | slot in this chunk's run
+      // Bins of the whole chunk first (independent searches in flight), then the gathers and
+      // the inside-range sums.
+      int bins[kRounds], bend[kRounds];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) bins[r] = SelBin(S, QKey(raw[r], arg_type), nb);
+      for (int r = 0; r < kRounds; ++r) SelGuideBracket(Gd, gk, QKey(raw[r], arg_type), bins[r], bend[r]);
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int i = wid * (kMidMax / 4) + r * 64 + lane;
-      int u = -1;
-      double v = 0.0;
-      if (i < static_cast<int>(c.len)) {
-        const uint64_t key = QKey(raw[r], arg_type);
-        const int b = bins[r];
-        const uint8_t tag = tg[b];
-        if (tag == kTagColl) {
-          const uint32_t slot = atomicAdd(&cc[b], 1u);
-          cg[cb[b] + slot] = key;
-        } else if (tag != 0) {
-          u = tag - 1;
-          v = QVal(key);
+      for (int r = 0; r < kRounds; ++r) bins[r] = SelGuideFinish(S, QKey(raw[r], arg_type), bins[r], bend[r]);
+#pragma unroll
+      for (int r = 0; r < kRounds; ++r) {
+        const int i = wid * (kMidMax / 4) + r * 64 + lane;
+        int u = -1;
+        double v = 0.0;
+        ls[r] = ~0u;
+        if (i < static_cast<int>(c.len)) {
+          const uint64_t key = QKey(raw[r], arg_type);
+          const int b = bins[r];
+          const uint8_t tag = tg[b];
+          if (tag == kTagColl) {
+            const uint32_t ix = cix[b];
+            ls[r] = (ix << 16) | atomicAdd(&lcnt[ix], 1u);
+          } else if (tag != 0) {
+            u = tag - 1;
+            v = QVal(key);
+          }
+        }
+        unsigned long long pend = __ballot(u >= 0);
+        while (pend) {
+          const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
+          const bool mine = u == uu;
+          const double sm = WaveSumF64(mine ? v : 0.0);
+          if (lane == 0) acc[wid][uu] += sm;
+          pend &= ~__ballot(mine);
         }
       }
-      unsigned long long pend = __ballot(u >= 0);
-      while (pend) {
-        const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
-        const bool mine = u == uu;
-        const double sm = WaveSumF64(mine ? v : 0.0);
-        if (lane == 0) acc[wid][uu] += sm;
-        pend &= ~__ballot(mine);
+      __syncthreads();
+      for (int k = t; k < n_coll; k += 256) {  // reserve each gathered bin's run of this chunk
+        const uint32_t cnt = lcnt[k];
+        if (cnt) {
+          const int b = s_coll[k];
+          lbase[k] = cb[b] + atomicAdd(&cc[b], cnt);
+          lcnt[k] = 0;
+        }
       }
+      for (int u = t; u < n_ranges; u += 256)
+        partial[static_cast<uint64_t>(ci) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kRounds; ++r)
+        if (ls[r] != ~0u) cg[lbase[ls[r] >> 16] + (ls[r] & 0xFFFFu)] = QKey(raw[r], arg_type);
     }
-    __syncthreads();
-    for (int u = t; u < n_ranges; u += 256)
-      partial[static_cast<uint64_t>(ci) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
   }
 }
 
@@ -2220,6 +2412,7 @@ __global__ void __launch_bounds__(256) BigSelDigestKernel(const BigGroup* __rest
   __shared__ BigPlan P;
   __shared__ double mean_u[kSelMaxRanges];
   __shared__ double red[4];
+  __shared__ uint32_t s_starts[kChainCap];  // the chain, staged for the quantile searches
   const int t = threadIdx.x;
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(plans + bi);
@@ -2229,15 +2422,25 @@ __global__ void __launch_bounds__(256) BigSelDigestKernel(const BigGroup* __rest
   __syncthreads();
   const BigGroup G = groups[bi];
   const int64_t W = static_cast<int64_t>(G.n);
-  const uint32_t* starts = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
+  {
+    const uint32_t* gs = chain_starts + static_cast<uint64_t>(bi) * kChainCap;
+    for (int j = t; j < P.nc; j += 256) s_starts[j] = gs[j];  // (ordered by the barriers below)
+  }
+  const uint32_t* starts = s_starts;
   const uint32_t* bs = bstart_all + static_cast<uint64_t>(bi) * (kSelBins + 1);
   const uint32_t* cb = cbase_all + static_cast<uint64_t>(bi) * kSelBins;
   const uint64_t* cg = cand + G.off;
-  auto rank_val = [&](int64_t r) -> double {
-    const int b = BinOfRank(bs, static_cast<uint32_t>(r));
-    return QVal(cg[cb[b] + (static_cast<uint32_t>(r) - bs[b])]);
-  };
-  if (t < P.n_ranges && P.re[t] - P.rs[t] <= static_cast<uint32_t>(kSeqMean)) mean_u[t] = CentroidMean(rank_val, P.rs[t], P.re[t]);
+  if (t < P.n_ranges && P.re[t] - P.rs[t] <= static_cast<uint32_t>(kSeqMean)) {
+    // CentroidMean reads ranks in increasing order: one bin search, then walk the bins.
+    int cur_b = -1;
+    auto rank_val_seq = [&](int64_t r) -> double {
+      const uint32_t rr = static_cast<uint32_t>(r);
+      if (cur_b < 0) cur_b = BinOfRank(bs, rr);
+      while (bs[cur_b + 1] <= rr) ++cur_b;
+      return QVal(cg[cb[cur_b] + (rr - bs[cur_b])]);
+    };
+    mean_u[t] = CentroidMean(rank_val_seq, P.rs[t], P.re[t]);
+  }
   for (int u = 0; u < P.n_ranges; ++u) {  // uniform: large ranges, block sums
     const uint32_t s = P.rs[u], e = P.re[u];
     if (e - s <= static_cast<uint32_t>(kSeqMean)) continue;
@@ -3138,17 +3341,22 @@ int32_t AggFinalizeTable(Agg* a) {
     const int at = a->uda_arg_type[u];
     const uint64_t nb = n_big_groups;
     PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4 + 16, ctx->side2));
+    uint16_t* guide = reinterpret_cast<uint16_t*>(ws.sel_spl.as<uint64_t>() + nb * kSelBins);
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(n_big_groups),
                                  dim3(kSelSample / 2 / kMsIpt), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
-                                 vals, at, ws.sel_spl.as<uint64_t>()));
-    if (big_max > (uint64_t(1) << 22))
-      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_big_groups),
+                                 vals, at, ws.sel_spl.as<uint64_t>(), guide, nullptr, nullptr));
+    if (big_max > kSelLargeN) {  // only the groups BigSetup listed (<= n / 2^22 of them)
+      const uint64_t bcap = n / (kMidMax + 1) + 1;  // as big_cap below
+      const uint32_t* lcnt = reinterpret_cast<const uint32_t*>(ws.big.as<const uint8_t>() + bcap * sizeof(BigGroup));
+      const uint32_t n_large = static_cast<uint32_t>(std::min<uint64_t>(nb, n / (kSelLargeN + 1) + 1));
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_large),
                                    dim3(kSelSampleThreads), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
-                                   vals, at, ws.sel_spl.as<uint64_t>()));
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 2, SelHistCap());
+                                   vals, at, ws.sel_spl.as<uint64_t>(), guide, lcnt + 4, lcnt));
+    }
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, SelHistCap());
     return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
-                    ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);
+                    static_cast<const uint16_t*>(guide), ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);
   };
   // Second half, after the chains: plan, gather + inside sums, bin sorts, digests.
   auto BigSelectBack = [&](int u) -> int32_t {
@@ -3166,10 +3374,11 @@ int32_t AggFinalizeTable(Agg* a) {
                                  static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), ws.sel_bstart.as<uint32_t>(),
                                  ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback, lists,
                                  list_cap, list_cnt));
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 8);
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, 64);  // 3 resident per CU (LDS)
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                                  ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
-                                 vals, at, ws.sel_spl.as<const uint64_t>(), ws.sel_tag.as<const uint8_t>(),
+                                 vals, at, ws.sel_spl.as<const uint64_t>(),
+                                 reinterpret_cast<const uint16_t*>(ws.sel_spl.as<const uint64_t>() + nb * kSelBins), ws.sel_tag.as<const uint8_t>(),
                                  ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>(), cpb));
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel,
                                  dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0,
@@ -3207,12 +3416,14 @@ int32_t AggFinalizeTable(Agg* a) {
     // total and the largest group (grid sizes and the merge-pass count).
     const uint64_t big_cap = n / (kMidMax + 1) + 1;  // groups of > kMidMax rows
     const uint64_t chunk_cap = n / kMidMax + big_cap + 1;
-    PXG_RETURN_IF_ERROR(ws.big.Ensure(big_cap * sizeof(BigGroup)));
+    PXG_RETURN_IF_ERROR(ws.big.Ensure(big_cap * sizeof(BigGroup) + 16 + big_cap * 4));
+    uint32_t* large_cnt = reinterpret_cast<uint32_t*>(ws.big.as<uint8_t>() + big_cap * sizeof(BigGroup));
+    uint32_t* large_list = large_cnt + 4;
     PXG_RETURN_IF_ERROR(ws.bchunks.Ensure(chunk_cap * sizeof(BigChunk)));
     uint32_t* d_bigmeta = reinterpret_cast<uint32_t*>(meta + 48);
     PXG_RETURN_IF_ERROR(Launch(ctx, "big_setup", BigSetupKernel, dim3(1), dim3(kSetupBlock), 0, lists + 3 * static_cast<uint64_t>(ngroups),
                                static_cast<const uint32_t*>(d_cls + 3), gstart, ws.big.as<BigGroup>(), ws.bchunks.as<BigChunk>(),
-                               d_bigmeta));
+                               d_bigmeta, large_list, large_cnt));
     // Class counts + big-group metadata to pinned memory right away; the host waits on this
     // event only, while the digests below keep the GPU busy.
     uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
@@ -3221,9 +3432,9 @@ int32_t AggFinalizeTable(Agg* a) {
     // Kernels whose work lists are counted on the device launch right away with upper-bound
     // grids (blocks past the device count exit); the host reads the counts back only after
     // them, so the tiny / small digests and the boundary chains run while it waits.
-    const uint32_t mid_cap = static_cast<uint32_t>(std::min<uint64_t>(ngroups, n / (kSmallMax + 1) + 1));
     const uint32_t big_cap32 = static_cast<uint32_t>(std::min<uint64_t>(ngroups, big_cap));
-    const uint32_t n_chain_cap = mid_cap + big_cap32;
+    const uint32_t n_chain_cap = big_cap32;  // mid groups read the per-context table
+    PXG_RETURN_IF_ERROR(EnsureMidChains(ctx));
     PXG_RETURN_IF_ERROR(ws.chain_nc.Ensure(static_cast<size_t>(n_chain_cap) * 4));
     PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain_cap) * kChainCap * 4));
     const uint32_t* chain_starts = ws.chain_starts.as<const uint32_t>();
@@ -3233,7 +3444,7 @@ int32_t AggFinalizeTable(Agg* a) {
     guard.side = true;
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "digest_chain", DigestChainKernel, dim3((n_chain_cap + kChainWaves - 1) / kChainWaves),
                                  dim3(64 * kChainWaves), 0,
-                                 lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), mid_cap,
+                                 lists + 2 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 2), 0u,
                                  lists + 3 * static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 3), gstart,
                                  ws.chain_starts.as<uint32_t>(), ws.chain_nc.as<int32_t>()));
     PXG_HIP(hipEventRecord(ctx->ev_chain, ctx->side));
@@ -3261,15 +3472,15 @@ int32_t AggFinalizeTable(Agg* a) {
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3];
     n_big_groups = n_big;
-    chain_starts_big = chain_starts + static_cast<uint64_t>(mid_cap) * kChainCap;
-    chain_nc_big = chain_nc + mid_cap;
+    chain_starts_big = chain_starts;
+    chain_nc_big = chain_nc;
     big_max = hm[5];
     n_bchunks = hm[4];
     // PXG_BIG_SORT=1 forces the full sort path for every big group (tests compare the two).
     big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT") && !a->export_x;
     if (big_select) {
       PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
-      PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8));
+      PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * kSelGuideStride * 2));
       PXG_RETURN_IF_ERROR(ws.sel_cnt.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * 4 + 16));
       PXG_RETURN_IF_ERROR(ws.sel_list.Ensure(static_cast<size_t>(n_big) * kSelMaxColl * kSelLists * 4 + 16));
       PXG_RETURN_IF_ERROR(ws.sel_bstart.Ensure(static_cast<size_t>(n_big) * (kSelBins + 1) * 4));
@@ -3291,7 +3502,6 @@ int32_t AggFinalizeTable(Agg* a) {
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
       if (big_select) PXG_RETURN_IF_ERROR(BigSelectFront(u));
-      PXG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_chain, 0));  // mid digests read the chains
       if (n_big > 0) {
         PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_chain, 0));
         PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(u) : BigSortPath(ctx->side2, u));
@@ -3299,7 +3509,8 @@ int32_t AggFinalizeTable(Agg* a) {
       double* qo = R.uda_out[u].as<double>();
       if (cls[2] > 0 && !a->export_x)
         PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
-                                   gstart, chain_starts, chain_nc, static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
+                                   gstart, MidChainStarts(ctx), MidChainNc(ctx), static_cast<const uint32_t*>(d_cls + 2), vals, at, qo,
+                                   d_err));
     }
   }
   if (guard.side) PXG_RETURN_IF_ERROR(JoinSide(ctx));  // the small digests

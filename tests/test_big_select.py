@@ -66,6 +66,9 @@ def _groups(fallback):
         ("grid", np.round(rng.lognormal(4, 1, 90_000), 1)),     # many ties
         ("m2000", rng.normal(0, 1, 2000)),
         ("t10", rng.normal(0, 1, 10)),
+        # a dense spike inside a huge range: most splitters share a few guide buckets (the
+        # guided bin search's wide-bracket steps)
+        ("spike", np.concatenate([rng.normal(100, 1e-6, 40_000), rng.uniform(-1e9, 1e9, 300)])),
     ]
     if fallback == "dup":
         spec.append(("dup", np.full(20_000, 7.25)))                          # one value
