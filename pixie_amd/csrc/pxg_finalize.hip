@@ -2115,8 +2115,6 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
           P.rj[u] = j;
           P.rs[u] = s;
           P.re[u] = e;
-          P.rbs[u] = static_cast<uint32_t>(BinOfRank(bs, s));
-          P.rbe[u] = static_cast<uint32_t>(BinOfRank(bs, e - 1));
         }
       }
       P.need_u[i] = u;
@@ -2124,6 +2122,11 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
     P.n_ranges = nr;
     P.nc = nc;
     P.fallback = 0;
+  }
+  __syncthreads();
+  if (t < P.n_ranges) {  // the ranges' end bins, one thread per range (12-step LDS searches)
+    P.rbs[t] = static_cast<uint32_t>(BinOfRank(bs, P.rs[t]));
+    P.rbe[t] = static_cast<uint32_t>(BinOfRank(bs, P.re[t] - 1));
   }
   __syncthreads();
   // Tags: the end bins of every range (every bin of a small range) are gathered; the bins
