@@ -737,6 +737,12 @@ __device__ __forceinline__ uint64_t QKey(uint64_t raw, int arg_type) {
   return SortKeyF(bits);
 }
 __device__ __forceinline__ double QVal(uint64_t key) { return AsF(FromSortKeyF(key)); }
+// QKey with the argument type fixed at compile time (the selection passes: no int64 conversion
+// computed and discarded per value).
+template <bool kF64>
+__device__ __forceinline__ uint64_t QKeyT(uint64_t raw) {
+  return SortKeyF(kF64 ? raw : FBits(static_cast<double>(static_cast<int64_t>(raw))));
+}
 
 constexpr uint64_t kNegInfKey = 0x000FFFFFFFFFFFFFULL;  // SortKeyF(-inf) = ~0xFFF0... = 0x000F...F
 constexpr uint64_t kPosInfKey = 0xFFF0000000000000ULL;  // SortKeyF(+inf) = 0x7FF0... ^ 0x8000...
@@ -1944,6 +1950,7 @@ static uint32_t SelHistCap() {
   const int v = e ? std::atoi(e) : 0;
   return v > 0 ? static_cast<uint32_t>(v) : 64;
 }
+template <bool kF64>
 __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                      const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
                                                      const uint16_t* __restrict__ guide, uint32_t* __restrict__ hist,
@@ -2000,13 +2007,13 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
     int bin[kPer], bend[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-      const uint64_t key = QKey(raw[k], arg_type);
+      const uint64_t key = QKeyT<kF64>(raw[k]);
       const int i = k * 256 + threadIdx.x;
       nn += (i < static_cast<int>(c.len) && (key < kNegInfKey || key > kPosInfKey)) ? 1u : 0u;
       SelGuideBracket(Gd, gk, key, bin[k], bend[k]);
     }
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) bin[k] = SelGuideFinish(S, QKey(raw[k], arg_type), bin[k], bend[k]);
+    for (int k = 0; k < kPer; ++k) bin[k] = SelGuideFinish(S, QKeyT<kF64>(raw[k]), bin[k], bend[k]);
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
       if (k * 256 + static_cast<int>(threadIdx.x) < static_cast<int>(c.len)) atomicAdd(&h[bin[k]], 1u);
@@ -2224,6 +2231,7 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
 // only when the group changes.  Gather slots are taken in two steps: LDS counters per gathered
 // bin, then one device atomic per bin and chunk reserves the bin's range — a device atomic per
 // value put its round trip in almost every 64-value round (~6% of values are gathered).
+template <bool kF64>
 __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                         const BigPlan* __restrict__ plans, const uint64_t* __restrict__ vals, int arg_type,
                                                         const uint64_t* __restrict__ spl, const uint16_t* __restrict__ guide,
@@ -2290,9 +2298,9 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
       // the inside-range sums.
       int bins[kRounds], bend[kRounds];
 #pragma unroll
-      for (int r = 0; r < kRounds; ++r) SelGuideBracket(Gd, gk, QKey(raw[r], arg_type), bins[r], bend[r]);
+      for (int r = 0; r < kRounds; ++r) SelGuideBracket(Gd, gk, QKeyT<kF64>(raw[r]), bins[r], bend[r]);
 #pragma unroll
-      for (int r = 0; r < kRounds; ++r) bins[r] = SelGuideFinish(S, QKey(raw[r], arg_type), bins[r], bend[r]);
+      for (int r = 0; r < kRounds; ++r) bins[r] = SelGuideFinish(S, QKeyT<kF64>(raw[r]), bins[r], bend[r]);
 #pragma unroll
       for (int r = 0; r < kRounds; ++r) {
         const int i = wid * (kMidMax / 4) + r * 64 + lane;
@@ -2300,7 +2308,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
         double v = 0.0;
         ls[r] = ~0u;
         if (i < static_cast<int>(c.len)) {
-          const uint64_t key = QKey(raw[r], arg_type);
+          const uint64_t key = QKeyT<kF64>(raw[r]);
           const int b = bins[r];
           const uint8_t tag = tg[b];
           if (tag == kTagColl) {
@@ -2334,7 +2342,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < kRounds; ++r)
-        if (ls[r] != ~0u) cg[lbase[ls[r] >> 16] + (ls[r] & 0xFFFFu)] = QKey(raw[r], arg_type);
+        if (ls[r] != ~0u) cg[lbase[ls[r] >> 16] + (ls[r] & 0xFFFFu)] = QKeyT<kF64>(raw[r]);
     }
   }
 }
@@ -3363,7 +3371,8 @@ int32_t AggFinalizeTable(Agg* a) {
                                    vals, at, ws.sel_spl.as<uint64_t>(), guide, lcnt + 4, lcnt));
     }
     const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, SelHistCap());
-    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", BigHistKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
+    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", at == PXG_FLOAT64 ? BigHistKernel<true> : BigHistKernel<false>,
+                    dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
                     static_cast<const uint16_t*>(guide), ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);
   };
@@ -3384,7 +3393,8 @@ int32_t AggFinalizeTable(Agg* a) {
                                  ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback, lists,
                                  list_cap, list_cnt));
     const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, 64);  // 3 resident per CU (LDS)
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", BigCollectKernel, dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", at == PXG_FLOAT64 ? BigCollectKernel<true> : BigCollectKernel<false>,
+                                 dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                                  ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
                                  vals, at, ws.sel_spl.as<const uint64_t>(),
                                  reinterpret_cast<const uint16_t*>(ws.sel_spl.as<const uint64_t>() + nb * kSelBins), ws.sel_tag.as<const uint8_t>(),

@@ -219,3 +219,41 @@ def test_selection_serves_multi_million_groups(ctx):
             else:
                 rank = lambda x: (np.searchsorted(sv, x, "left") + np.searchsorted(sv, x, "right")) / (2.0 * len(sv))  # noqa: E731
                 assert abs(rank(d) - rank(ref[j])) <= parity.rank_bound(parity.QS[j], len(sv)), (k, name, d, ref[j])
+
+
+def test_selection_path_int64_values_match_sort_path(ctx):
+    """INT64 quantile arguments (the selection passes are compiled per argument type): the
+    selection path against the full sort path on the same integer values."""
+    rng = np.random.default_rng(31)
+    spec = [("i9000", np.round(rng.lognormal(8, 1, 9000))), ("i60000", np.round(rng.lognormal(6, 2, 60_000))),
+            ("neg30000", rng.integers(-10**12, 10**12, 30_000).astype(np.float64)), ("i500", np.arange(500.0))]
+    keys = sum(([k] * len(v) for k, v in spec), [])
+    vals = np.concatenate([v for _, v in spec]).astype(np.int64)
+    perm = rng.permutation(len(keys))
+    keys = [keys[i] for i in perm]
+    vals = vals[perm]
+    plan = P.linear_plan([P.source_op("t", [5, 2], ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("quantiles", [P.col(1)], [2]), P.agg_expr("count", [P.col(1)], [2], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": [5, 2], "batches": [[Column.from_values(5, keys), Column(2, values=vals)]]}}
+    res = {}
+    for force in (False, True):
+        old = os.environ.pop("PXG_BIG_SORT", None)
+        if force:
+            os.environ["PXG_BIG_SORT"] = "1"
+        try:
+            out = run_plan(ctx, plan, tables)
+        finally:
+            os.environ.pop("PXG_BIG_SORT", None)
+            if old is not None:
+                os.environ["PXG_BIG_SORT"] = old
+        res[force] = {r[0]: (json.loads(r[1]), r[2]) for r in rows(out[0]["cols"])}
+    for k, v in spec:
+        (qa, ca), (qb, cb) = res[False][k], res[True][k]
+        assert ca == cb == len(v)
+        for name in NAMES:
+            a, b = qa[name], qb[name]
+            if len(v) <= 10_000:
+                assert a == b, (k, name, a, b)
+            else:
+                assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
