@@ -69,8 +69,10 @@ def parse():
                     help="N>1 data path: nccl = libpxg's RCCL communicator over xGMI (pxg_agg_alltoall); "
                          "gloo = torch.distributed all_to_all on the host (CPU rehearsal). The control plane is gloo.")
     ap.add_argument("--share-gpu0", action="store_true",
-                    help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; RCCL allows it)")
-    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"),
+                    help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; pair it with --backend gloo, since RCCL "
+                         "refuses two ranks on one GPU)")
+    ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)  # tests only: N>1 protocol on CPU
+    ap.add_argument("--pmc-file",default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"),
                     help="committed PMC summary used for roofline.traffic only when the live PMC leg cannot run")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live PMC leg (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this build's consume)")
@@ -194,26 +196,29 @@ def main():
     if args.cpu_shard_child:
         cpu_shard_child(*args.cpu_shard_child)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # No external launcher: start the N ranks here (fresh interpreters; this process never
+        # touches the GPU) and pass rank 0's JSON line through.
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"[bench] refusing to run: WORLD_SIZE={world} but --gpus {args.gpus} (launch one rank per GPU with "
+              f"--gpus equal to the world size, or run `bench.py --gpus N` alone and it starts the N ranks itself)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
-    if args.share_gpu0:
-        local_rank = 0
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        # Control plane only (the unique id, barriers, the max over ranks) on gloo; the data path
-        # is libpxg's own RCCL communicator (backend "nccl"), so torch never opens an NCCL group.
-        dist.init_process_group("gloo", init_method="env://")
+        return multi_main(args, rank, world, local_rank)
+    import torch
 
     from pixie_amd import plans as P
     from pixie_amd.device import Ctx, Table, datagen_http_events
     from pixie_amd.host_engine import Engine, plan_agg
-    from pixie_amd.dist import exchange_partials
 
-    n = args.rows_per_gpu or (100_000_000 if world == 1 else 125_000_000)
-    row0 = rank * n
+    n = args.rows_per_gpu or 100_000_000
+    row0 = 0
     # The table lives in the C++ engine's HBM-resident table store; the timed step runs the
     # libpxg ABI on that device table, and the engine leg runs the whole plan over it.
     engine = Engine(local_rank)
@@ -228,37 +233,17 @@ def main():
     else:
         table.append_http_events(SEED, row0, n, N_PAIR_KEYS)
     assert engine.num_rows("http_events") == n
-    log(rank, f"[bench] {'host-generated + uploaded' if args.host_gen else 'device-generated'} {n} rows/rank "
+    log(rank, f"[bench] {'host-generated + uploaded' if args.host_gen else 'device-generated'} {n} rows "
               f"in {time.time() - t0:.1f}s ({table.num_chunks} chunks)")
     alg_bytes = alg_bytes_of(table, n)
 
     # The engine's own lowering of the C2 plan (the drop-in path's fused Filter/Map/Agg), driven
     # directly on the HBM-resident table so the timed step is exactly the device hot path.
     agg = plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
-    exch = {"bytes_sent": 0, "bytes_recv": 0, "via": None}
-    # N > 1: libpxg's own RCCL communicator (pxg_comm_init / pxg_agg_alltoall, one rank per
-    # GPU over xGMI); torch.distributed only carries the unique id.  A gloo run (CPU rehearsal)
-    # exchanges through torch.distributed instead.
-    comm = None
-    if world > 1 and args.backend == "nccl":
-        # every rank is on this node (--nnodes=1): RCCL's bootstrap socket stays on loopback
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        from pixie_amd.device import Comm
-        obj = [Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = Comm(ctx, rank, world, obj[0])
 
     def step():
         agg.reset()
         agg.consume(table)
-        if world > 1:
-            if comm is not None:
-                s, r = agg.alltoall(comm)
-                exch["via"] = "pxg_agg_alltoall (RCCL grouped send/recv on the ctx stream)"
-            else:
-                s, r = exchange_partials(agg)
-                exch["via"] = "torch.distributed all_to_all_single (" + args.backend + ")"
-            exch["bytes_sent"], exch["bytes_recv"] = s, r
         return agg.finalize()
 
     for _ in range(args.warmup):
@@ -266,20 +251,9 @@ def main():
     ctx.sync()
     # Per-kernel breakdown from one untimed, fully event-bracketed pass (the event records
     # themselves cost time, so the timed region brackets agg_consume only).
-    ctx.reset_stats()
-    ctx.set_profiling(True)
-    step()
-    ctx.sync()
-    ctx.set_profiling(False)
-    kernel_ms = {}
-    for name in KERNELS:
-        l, ms = ctx.kernel_stats(name)
-        if l:
-            kernel_ms[name] = round(ms, 4)
+    kernel_ms = profiled_kernels(ctx, step)
     ctx.reset_stats()
     ctx.set_profiling(True, only="agg_consume")
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize()
     ctx.sync()
     t_start = time.perf_counter()
@@ -287,24 +261,19 @@ def main():
         ngroups = step()
     ctx.sync()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     elapsed = time.perf_counter() - t_start
     ctx.set_profiling(False)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     launches, cons_ms, pre_ms = consume_stats(ctx)
     ms_per_step = elapsed * 1000.0 / args.steps
     selected = agg.rows_selected()
-    total_rows = n * world
+    world = 1
+    total_rows = n
     value = total_rows * args.steps / elapsed
     # The consume kernel's time per step (both launches when the prefix runs): the algorithmic
     # bytes of one step are read by the two launches together.
     avg_launch_ms = cons_ms / args.steps
     achieved = alg_bytes / (avg_launch_ms / 1000.0) / 1e9 if launches else None
-    dev_result = agg.result() if (world == 1 and rank == 0 and not args.no_cpu_baseline) else None
+    dev_result = agg.result() if not args.no_cpu_baseline else None
     traffic = pmc_traffic(args, n)
 
     # Engine leg (N=1): the unmodified binary C2 plan through pxc_execute_plan over the stored
@@ -346,12 +315,10 @@ def main():
         c1 = c1_leg(args, P)
 
     cpu, par = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         cpu, par = oracle_leg(args, n, row0, dev_result)
         if cpu is not None and args.cpu_procs > 0:
             cpu["parallel"] = cpu_parallel_leg(args, n, row0)
-    elif world > 1:
-        par = {"skipped": "N>1: shard-exchange parity is tests/test_scale_parity.py (8-way) and tests/test_partial.py"}
 
     # North-star leg (N=1): the same step over 1B rows on one GPU.
     n1 = None
@@ -393,11 +360,10 @@ def main():
                 "workload": "C2: Filter(resp_status>=400) -> Map(latency_ms=latency/1e6) -> BlockingAgg by (service, req_path): "
                             "count, mean, quantiles -> pluck p50/p99",
                 "rows_per_gpu": n, "total_rows": total_rows, "groups": ngroups, "selected_rows_per_gpu": selected,
-                "parallelism": f"dp{world} (row shards, partial UDA states exchanged by key hash)" if world > 1 else "single GPU",
+                "parallelism": "single GPU",
                 "algorithmic_bytes_per_row": alg_bytes / n,
                 "kernel_ms_per_step": kernel_ms,
-                "step_rate_gbs_algorithmic": alg_bytes * world / (ms_per_step / 1000.0) / 1e9,
-                "exchange_bytes_per_rank": exch if world > 1 else None,
+                "step_rate_gbs_algorithmic": alg_bytes / (ms_per_step / 1000.0) / 1e9,
             },
             "roofline": {
                 "bound": "hbm",
@@ -425,14 +391,262 @@ def main():
             "n1": n1,
         }
         print(json.dumps(line), flush=True)
-    if comm is not None:
-        comm.close()
-    if world > 1 or args.n1_rows <= 0:
+    if args.n1_rows <= 0:
         agg.close()
     table.close()
     ctx.close()
     engine.close()
-    if world > 1:
+
+
+def profiled_kernels(ctx, step):
+    """kernel -> summed ms of one untimed step with every library launch event-bracketed."""
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    step()
+    ctx.sync()
+    ctx.set_profiling(False)
+    out = {}
+    for name in KERNELS + ["gather_rebase"]:
+        l, ms = ctx.kernel_stats(name)
+        if l:
+            out[name] = round(ms, 4)
+    return out
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` with no external launcher: start N rank processes of this script
+    (fresh interpreters, env RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1), wait for
+    them, and return the worst exit code.  This process never initialises the GPU.  Rank 0
+    inherits stdout, so its JSON line is the only one printed; the other ranks' stdout is
+    discarded.  A rank that fails takes the others down with it."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    n = args.gpus
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    print(f"[bench] starting {n} ranks (one process per GPU, rendezvous 127.0.0.1:{port})", file=sys.stderr, flush=True)
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
+    codes = [None] * n
+    failed = False
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                c = p.poll()
+                if c is not None:
+                    codes[r] = c
+                    if c != 0 and not failed:
+                        failed = True
+                        print(f"[bench] rank {r} exited {c}: stopping the other ranks", file=sys.stderr, flush=True)
+                        for q in procs:
+                            if q.poll() is None:
+                                try:
+                                    os.killpg(q.pid, signal.SIGTERM)
+                                except ProcessLookupError:
+                                    pass
+        time.sleep(0.05)
+    return max((c if c > 0 else 1 if c != 0 else 0) for c in codes)
+
+
+class DeviceRank:
+    """One rank of the N > 1 bench (BASELINE configs[3], C4): its contiguous row shard
+    [rank * n, (rank + 1) * n) generated in HBM, the engine's C2 lowering, libpxg's own RCCL
+    communicator (backend nccl) or torch.distributed gloo (CPU-hosted rehearsal)."""
+
+    def __init__(self, args, rank, world, local_rank):
+        import torch
+        from pixie_amd import plans as P
+        from pixie_amd.device import Ctx, Table
+        from pixie_amd.host_engine import Engine, plan_agg
+        torch.cuda.set_device(local_rank)
+        self.torch = torch
+        self.rank, self.world, self.backend = rank, world, args.backend
+        self.n = args.rows_per_gpu or 125_000_000
+        self.engine = Engine(local_rank)
+        self.ctx = Ctx(local_rank, handle=self.engine.ctx_handle())
+        self.engine.create_table("http_events", P.HTTP_TYPES, P.HTTP_NAMES)
+        self.table = Table(self.ctx, P.HTTP_TYPES, handle=self.engine.device_table("http_events"), owned=False)
+        t0 = time.time()
+        self.table.append_http_events(SEED, rank * self.n, self.n, N_PAIR_KEYS)
+        log(rank, f"[bench] device-generated {self.n} rows/rank in {time.time() - t0:.1f}s ({self.table.num_chunks} chunks)")
+        self.alg_bytes = alg_bytes_of(self.table, self.n)
+        self.agg = plan_agg(self.ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)
+        self.comm = None
+        self.parts = None
+        self.exch = {"bytes_sent": 0, "bytes_recv": 0, "via": None, "gather": None}
+        if args.backend == "nccl":
+            import torch.distributed as dist
+            from pixie_amd.device import Comm
+            # every rank is on this node (--nnodes=1): RCCL's bootstrap socket stays on loopback
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            obj = [Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            self.comm = Comm(self.ctx, rank, world, obj[0])
+
+    def step(self):
+        """reset -> consume -> exchange partial states by key hash -> finalize -> gather the
+        final rows on rank 0.  Returns the gathered groups on rank 0 (0 elsewhere)."""
+        a = self.agg
+        a.reset()
+        a.consume(self.table)
+        if self.comm is not None:
+            s, r = a.alltoall(self.comm)
+            a.finalize()
+            g = a.gather(self.comm, 0)
+            self.exch.update(via="pxg_agg_alltoall (RCCL grouped send/recv on the ctx stream)",
+                             gather="pxg_agg_gather (RCCL send/recv of the result columns to rank 0)")
+        else:
+            from pixie_amd.dist import exchange_partials, gather_results
+            s, r = exchange_partials(a)
+            a.finalize()
+            self.parts = gather_results(a.result())
+            g = sum(len(p[0]) for p in self.parts) if self.parts else 0
+            self.exch.update(via=f"torch.distributed all_to_all_single ({self.backend})",
+                             gather="torch.distributed gather_object of the host result columns")
+        self.exch["bytes_sent"], self.exch["bytes_recv"] = s, r
+        return g
+
+    def sync(self):
+        self.ctx.sync()
+        self.torch.cuda.synchronize()
+
+    def profile(self):
+        return profiled_kernels(self.ctx, self.step)
+
+    def start_timing(self):
+        self.ctx.reset_stats()
+        self.ctx.set_profiling(True, only="agg_consume")
+
+    def consume_ms(self):
+        self.ctx.set_profiling(False)
+        return consume_stats(self.ctx)
+
+    def selected(self):
+        return self.agg.rows_selected()
+
+    def result(self):
+        """Rank 0: the whole gathered result (service, req_path, count, mean, quantiles)."""
+        if self.comm is not None:
+            return self.agg.result()
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import parity
+        return parity.concat_columns(self.parts)
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        self.agg.close()
+        self.table.close()
+        self.ctx.close()
+        self.engine.close()
+
+
+def multi_main(args, rank, world, local_rank):
+    """N > 1 (BASELINE configs[3] "C4": 1B rows over 8 GPUs = 125M rows per rank):
+    one process per GPU, row shards, partial UDA states exchanged by hash(key) with one
+    all-to-all(v), local finalize, final rows gathered to rank 0 -- all inside the timed step.
+    Control plane (unique id, barriers, max over ranks) on torch.distributed gloo.  After the
+    timed region rank 0 checks the gathered result of the last step against the generator's
+    ground truth over all world * n rows (tests/parity.py::check_c2_against_truth: group set and
+    counts bit-exact, means 1e-6, quantiles 4 ULP / rank bound)."""
+    import torch.distributed as dist
+    if args.share_gpu0:
+        local_rank = 0
+    # gloo's connection banner goes to the C-level stdout; keep stdout for the one JSON line.
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", init_method="env://")
+        dist.barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    runner = None
+    try:
+        if args.standin:
+            # TEST ONLY (tests/test_bench_launch.py): the launcher / rendezvous / timing / gather /
+            # parity protocol on CPU, with a numpy + oracle stand-in for the device step.
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            from bench_standin import StandinRank
+            runner = StandinRank(args, rank, world, SEED, N_PAIR_KEYS)
+        else:
+            runner = DeviceRank(args, rank, world, local_rank)
+        n = runner.n
+        for _ in range(args.warmup):
+            runner.step()
+        runner.sync()
+        kernel_ms = runner.profile()
+        runner.start_timing()
+        dist.barrier()
+        runner.sync()
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            ngroups = runner.step()
+        runner.sync()
+        dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        launches, cons_ms, pre_ms = runner.consume_ms()
+        import torch
+        tt = torch.tensor([elapsed, cons_ms / args.steps], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, avg_launch_ms = float(tt[0]), float(tt[1])
+        ms_per_step = elapsed * 1000.0 / args.steps
+        total_rows = n * world
+        value = total_rows * args.steps / elapsed
+        alg_bytes = runner.alg_bytes
+        achieved = alg_bytes / (avg_launch_ms / 1000.0) / 1e9 if launches and avg_launch_ms > 0 else None
+        par = None
+        if rank == 0:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            try:
+                import parity
+                par = parity.check_c2_against_truth(runner.result(), SEED, 0, total_rows, threads=16)
+                par["scope"] = (f"the rank-0 gathered result of the last timed step against the generator's ground truth over "
+                                f"all {total_rows} rows of the {world} shards")
+            except Exception as e:  # the legs must never break the bench line
+                import traceback
+                traceback.print_exc()
+                par = {"ok": False, "error": f"N>1 parity failed: {e}"}
+        if rank == 0:
+            line = {
+                "metric": "rows/sec + achieved HBM GB/s, http_events filter+group-by agg, 1/2/4/8 MI355X",
+                "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "int64/f64",
+                "data": ("STAND-IN (test of the launcher protocol; numpy + oracle step, not the product)" if args.standin else
+                         "synthetic http_events (counter-based splitmix64, seed 20250117; SURVEY.md §8d spec), generated in HBM"),
+                "config": {
+                    "workload": "C4: per-rank Filter(resp_status>=400) -> Map(latency_ms=latency/1e6) -> partial BlockingAgg by "
+                                "(service, req_path): count, mean, quantiles; partial states exchanged by hash(key) % N; "
+                                "finalize; final rows gathered on rank 0",
+                    "rows_per_gpu": n, "total_rows": total_rows, "groups": ngroups, "selected_rows_per_gpu": runner.selected(),
+                    "parallelism": f"dp{world} (row shards, partial UDA states exchanged by key hash, rows gathered on rank 0)",
+                    "algorithmic_bytes_per_row": alg_bytes / n if n else None,
+                    "kernel_ms_per_step_rank0": kernel_ms,
+                    "step_rate_gbs_algorithmic": alg_bytes * world / (ms_per_step / 1000.0) / 1e9,
+                    "exchange_bytes_per_rank": runner.exch, "backend": args.backend, "share_gpu0": bool(args.share_gpu0),
+                },
+                "roofline": {
+                    "bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                    "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_launch_ms if launches else None,
+                    "per": "one rank's consume step (the slowest rank's event-timed consume)",
+                },
+                "cpu_baseline": None,
+                "parity": par,
+            }
+            print(json.dumps(line), flush=True)
+        dist.barrier()
+    finally:
+        if runner is not None:
+            runner.close()
         dist.destroy_process_group()
 
 

@@ -370,6 +370,13 @@ int32_t pxg_comm_destroy(pxg_comm* comm);
  * import what arrived.  Afterwards every group lives on exactly one rank; finalize locally.
  * Collective.  bytes_sent / bytes_recv (optional) receive this rank's traffic. */
 int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes_sent, int64_t* bytes_recv);
+/* Gather every rank's finalized result rows on `root` (the final rows to one
+ * rank, as Kelvin's GRPCSink streams them to the query broker, grpc_sink_node.cc:305-330).  Call
+ * after pxg_agg_alltoall + pxg_agg_finalize on every rank (collective).  On the root the result
+ * (pxg_agg_result and friends) becomes the concatenation of all ranks' rows, its own first, then
+ * the others by rank; *n_groups receives the total (0 on the other ranks, whose results are left
+ * as they were).  Group-less aggregates are UNIMPLEMENTED (they merge, they do not concatenate). */
+int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, int64_t* n_groups);
 
 /* ---------------------------------------------------------------------------------------
  * Equijoin (EquijoinNode, src/carnot/exec/equijoin_node.cc:53-470).  A hash table is built on

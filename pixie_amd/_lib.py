@@ -86,7 +86,7 @@ EXPORTED = [
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_result_device", "pxg_agg_finalize_result", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial", "pxg_agg_import_partials",
     "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains", "pxg_digest_merge",
-    "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_destroy", "pxg_agg_alltoall",
+    "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_destroy", "pxg_agg_alltoall", "pxg_agg_gather",
 ]
 
 _lib = None
@@ -166,6 +166,7 @@ def load() -> C.CDLL:
         "pxg_comm_init": (i32, [vp, i32, i32, vp, i32, p(vp)]),
         "pxg_comm_destroy": (i32, [vp]),
         "pxg_agg_alltoall": (i32, [vp, vp, p(i64), p(i64)]),
+        "pxg_agg_gather": (i32, [vp, vp, i32, p(i64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

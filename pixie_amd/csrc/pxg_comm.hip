@@ -191,3 +191,214 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   if (bytes_recv) *bytes_recv = rtotal;
   return PXG_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// pxg_agg_gather: the finalized rows of every rank to one rank (the Kelvin
+// result stream that the reference's GRPCSink sends to the query broker, grpc_sink_node.cc:305-330).
+// After pxg_agg_alltoall + pxg_agg_finalize every group lives on exactly one rank, so the global
+// result is the row-wise concatenation of the ranks' results: the root's own rows first (left in
+// place), then the other ranks' rows in rank order.  Per rank one 8-word header {groups, STRING
+// key payload bytes} travels first; the root waits for the headers once (it sizes its buffers
+// from them), the senders never wait.  STRING key offsets arrive relative to their rank's payload
+// and are rebased on the device.
+// ---------------------------------------------------------------------------------------------
+namespace pxg {
+
+constexpr int kGatherHdr = 1 + kMaxKeys;  // int64 words: groups, then key_data_len per key
+
+// out[base_g[r] + 1 + j] = tmp[base_t[r] + 1 + j] - tmp[base_t[r]] + base_b[r] for the non-root
+// ranks r (slot 0 = the root keeps its offsets in place); out[G] = the total payload.
+__global__ void GatherRebaseKernel(const int32_t* __restrict__ tmp, const int64_t* __restrict__ bases, int32_t nr,
+                                   int32_t* __restrict__ out) {
+  // bases: [nr] group base, [nr] tmp base, [nr] byte base, [nr] groups (ranks in concatenation
+  // order, slot 0 = the root).
+  const int64_t* gb = bases;
+  const int64_t* tb = bases + nr;
+  const int64_t* bb = bases + 2 * nr;
+  const int64_t* gn = bases + 3 * nr;
+  for (int r = 1; r < nr; ++r) {
+    const int32_t t0 = tmp[tb[r]];
+    for (int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < gn[r]; j += static_cast<int64_t>(gridDim.x) * blockDim.x)
+      out[gb[r] + 1 + j] = static_cast<int32_t>(tmp[tb[r] + 1 + j] - t0 + bb[r]);
+  }
+}
+
+}  // namespace pxg
+
+extern "C" int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, int64_t* n_groups) {
+  if (!agg || !comm) return SetError(PXG_INVALID_ARGUMENT, "bad pxg_agg_gather arguments");
+  Comm& C = comm->impl;
+  Agg& a = agg->impl;
+  Ctx* ctx = a.ctx;
+  if (ctx != C.ctx) return SetError(PXG_INVALID_ARGUMENT, "aggregation and communicator belong to different contexts");
+  const int32_t n = C.nranks;
+  if (root < 0 || root >= n) return SetError(PXG_INVALID_ARGUMENT, "root %d of %d ranks", root, n);
+  if (!a.res.ready) return SetError(PXG_FAILED_PRECONDITION, "pxg_agg_finalize has not run since the last consume");
+  if (a.n_keys == 0) return SetError(PXG_UNIMPLEMENTED, "a group-less aggregate is merged, not gathered");
+  AggResult& R = a.res;
+  const bool me_root = C.rank == root;
+  // Per column: bytes of this rank's part (STRING keys: offsets then payload).
+  auto fixed_w = [&](int k) { return static_cast<int64_t>(TypeWidth(a.key_types[k])); };
+  const int64_t val_per = 8;
+  auto val_bytes = [&](int u, int64_t G) -> int64_t {
+    if (a.emit_states) return G * a.state_rec;
+    return G * (a.uda_kind[u] == PXG_UDA_QUANTILES ? 7 * val_per : val_per);
+  };
+  const int n_vcols = a.emit_states ? 1 : a.n_udas;
+  DevBuf* vbuf[kMaxUdas];
+  for (int u = 0; u < n_vcols; ++u) vbuf[u] = a.emit_states ? &R.states : &R.uda_out[u];
+  // 1. Headers: every rank's {groups, key payload bytes} to the root.
+  int64_t* pin = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps);
+  if (static_cast<size_t>(n + 1) * kGatherHdr * 8 > Ctx::kPinnedBytes - Ctx::kPinnedOps) return SetError(PXG_UNIMPLEMENTED, "%d ranks", n);
+  PXG_RETURN_IF_ERROR(C.counts.Ensure(static_cast<size_t>(n + 1) * kGatherHdr * 8 + 64));
+  int64_t* d_hdr = C.counts.as<int64_t>();  // [0] mine, [1 + r] rank r's (root)
+  // The stream may still be writing pinned scratch of an earlier call (the finalize's readbacks
+  // are synchronous, so it is idle here); write this rank's header.
+  pin[0] = R.n_groups;
+  for (int k = 0; k < kMaxKeys; ++k) pin[1 + k] = k < a.n_keys && a.key_types[k] == PXG_STRING ? R.key_data_len[k] : 0;
+  std::vector<int64_t> hdr(static_cast<size_t>(n) * kGatherHdr, 0);
+  if (!me_root) {
+    PXG_HIP(hipMemcpyAsync(d_hdr, pin, kGatherHdr * 8, hipMemcpyHostToDevice, ctx->stream));
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    PXG_NCCL(ncclSend(d_hdr, kGatherHdr, ncclInt64, root, C.nccl, ctx->stream));
+    PXG_RETURN_IF_ERROR(grp.End());
+  } else {
+    std::copy(pin, pin + kGatherHdr, hdr.begin() + static_cast<size_t>(root) * kGatherHdr);
+    if (n > 1) {
+      NcclGroup grp;
+      PXG_RETURN_IF_ERROR(grp.Start());
+      for (int r = 0; r < n; ++r)
+        if (r != root) PXG_NCCL(ncclRecv(d_hdr + static_cast<size_t>(1 + r) * kGatherHdr, kGatherHdr, ncclInt64, r, C.nccl, ctx->stream));
+      PXG_RETURN_IF_ERROR(grp.End());
+      PXG_HIP(hipMemcpyAsync(pin + kGatherHdr, d_hdr + kGatherHdr, static_cast<size_t>(n) * kGatherHdr * 8, hipMemcpyDeviceToHost, ctx->stream));
+      PXG_HIP(hipStreamSynchronize(ctx->stream));
+      for (int r = 0; r < n; ++r)
+        if (r != root) std::copy(pin + (1 + r) * kGatherHdr, pin + (2 + r) * kGatherHdr, hdr.begin() + static_cast<size_t>(r) * kGatherHdr);
+    }
+  }
+  // 2. Senders: every column to the root, in column order (zero-length columns skipped on both
+  //    sides by the same rule).
+  if (!me_root) {
+    const int64_t G = R.n_groups;
+    if (G > 0) {
+      NcclGroup grp;
+      PXG_RETURN_IF_ERROR(grp.Start());
+      for (int k = 0; k < a.n_keys; ++k) {
+        if (a.key_types[k] == PXG_STRING) {
+          PXG_NCCL(ncclSend(R.key_offsets[k].p, static_cast<size_t>(G + 1), ncclInt32, root, C.nccl, ctx->stream));
+          if (R.key_data_len[k] > 0) PXG_NCCL(ncclSend(R.key_data[k].p, static_cast<size_t>(R.key_data_len[k]), ncclUint8, root, C.nccl, ctx->stream));
+        } else {
+          PXG_NCCL(ncclSend(R.key_fixed[k].p, static_cast<size_t>(G * fixed_w(k)), ncclUint8, root, C.nccl, ctx->stream));
+        }
+      }
+      for (int u = 0; u < n_vcols; ++u) {
+        const int64_t b = val_bytes(u, G);
+        if (b > 0) PXG_NCCL(ncclSend(vbuf[u]->p, static_cast<size_t>(b), ncclUint8, root, C.nccl, ctx->stream));
+      }
+      PXG_RETURN_IF_ERROR(grp.End());
+    }
+    // The rows now belong to the root's result; this rank keeps its (already sent) copy until
+    // the next finalize.  The sends are stream-ordered before any later write of these buffers.
+    if (n_groups) *n_groups = 0;
+    return PXG_OK;
+  }
+  // 3. Root: concatenation order = the root, then the other ranks by rank.
+  std::vector<int> order{root};
+  for (int r = 0; r < n; ++r)
+    if (r != root) order.push_back(r);
+  const int nr = static_cast<int>(order.size());
+  std::vector<int64_t> gbase(nr), tbase(nr), gcnt(nr);
+  std::vector<std::vector<int64_t>> bbase(a.n_keys, std::vector<int64_t>(nr, 0));
+  int64_t Gt = 0, Tt = 0;
+  std::vector<int64_t> btot(a.n_keys, 0);
+  for (int i = 0; i < nr; ++i) {
+    const int64_t* h = hdr.data() + static_cast<size_t>(order[i]) * kGatherHdr;
+    if (h[0] < 0) return SetError(PXG_INTERNAL, "rank %d announced %lld groups", order[i], static_cast<long long>(h[0]));
+    gbase[i] = Gt;
+    gcnt[i] = h[0];
+    tbase[i] = Tt;
+    Gt += h[0];
+    Tt += h[0] + 1;
+    for (int k = 0; k < a.n_keys; ++k) {
+      bbase[k][i] = btot[k];
+      btot[k] += h[1 + k];
+    }
+  }
+  for (int k = 0; k < a.n_keys; ++k)
+    if (btot[k] >= (int64_t(1) << 31)) return SetError(PXG_UNIMPLEMENTED, "gathered key payload of %lld bytes needs 64-bit offsets", static_cast<long long>(btot[k]));
+  const int64_t G0 = R.n_groups;  // the root's own rows stay at the front of its buffers
+  for (int k = 0; k < a.n_keys; ++k) {
+    if (a.key_types[k] == PXG_STRING) {
+      PXG_RETURN_IF_ERROR(R.key_offsets[k].Reserve(static_cast<size_t>(Gt + 1) * 4 + 16, static_cast<size_t>(G0 + 1) * 4, ctx->stream));
+      PXG_RETURN_IF_ERROR(R.key_data[k].Reserve(static_cast<size_t>(btot[k]) + 16, static_cast<size_t>(R.key_data_len[k]), ctx->stream));
+    } else {
+      PXG_RETURN_IF_ERROR(R.key_fixed[k].Reserve(static_cast<size_t>(Gt * fixed_w(k)) + 16, static_cast<size_t>(G0 * fixed_w(k)), ctx->stream));
+    }
+  }
+  for (int u = 0; u < n_vcols; ++u)
+    PXG_RETURN_IF_ERROR(vbuf[u]->Reserve(static_cast<size_t>(val_bytes(u, Gt)) + 16, static_cast<size_t>(val_bytes(u, G0)), ctx->stream));
+  // Other ranks' STRING offsets land in scratch (C.recv), rebased below.
+  bool any_str = false;
+  for (int k = 0; k < a.n_keys; ++k) any_str |= a.key_types[k] == PXG_STRING;
+  const size_t tmp_words = static_cast<size_t>(Tt);
+  if (any_str) PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(a.n_keys) * tmp_words * 4 + static_cast<size_t>(4 * nr) * 8 + 128));
+  int32_t* tmp = C.recv.as<int32_t>();
+  if (Gt > G0) {
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    for (int i = 1; i < nr; ++i) {
+      const int64_t G = gcnt[i];
+      if (G == 0) continue;
+      const int src = order[i];
+      for (int k = 0; k < a.n_keys; ++k) {
+        if (a.key_types[k] == PXG_STRING) {
+          PXG_NCCL(ncclRecv(tmp + static_cast<size_t>(k) * tmp_words + tbase[i], static_cast<size_t>(G + 1), ncclInt32, src, C.nccl, ctx->stream));
+          const int64_t len = hdr[static_cast<size_t>(src) * kGatherHdr + 1 + k];
+          if (len > 0) PXG_NCCL(ncclRecv(R.key_data[k].as<uint8_t>() + bbase[k][i], static_cast<size_t>(len), ncclUint8, src, C.nccl, ctx->stream));
+        } else {
+          PXG_NCCL(ncclRecv(R.key_fixed[k].as<uint8_t>() + gbase[i] * fixed_w(k), static_cast<size_t>(G * fixed_w(k)), ncclUint8, src, C.nccl, ctx->stream));
+        }
+      }
+      for (int u = 0; u < n_vcols; ++u) {
+        const int64_t b = val_bytes(u, G);
+        if (b > 0) PXG_NCCL(ncclRecv(vbuf[u]->as<uint8_t>() + val_bytes(u, gbase[i]), static_cast<size_t>(b), ncclUint8, src, C.nccl, ctx->stream));
+      }
+    }
+    PXG_RETURN_IF_ERROR(grp.End());
+    if (any_str) {
+      int64_t* d_bases = reinterpret_cast<int64_t*>(tmp + static_cast<size_t>(a.n_keys) * tmp_words + 16);
+      d_bases = reinterpret_cast<int64_t*>((reinterpret_cast<uintptr_t>(d_bases) + 7) & ~uintptr_t(7));
+      for (int k = 0; k < a.n_keys; ++k) {
+        if (a.key_types[k] != PXG_STRING) continue;
+        // Host table of bases, staged through pinned memory one key at a time (stream-ordered).
+        int64_t* hb = pin + kGatherHdr * (n + 1);
+        if (static_cast<size_t>(kGatherHdr * (n + 1) + 4 * nr + 1) * 8 > Ctx::kPinnedBytes - Ctx::kPinnedOps)
+          return SetError(PXG_UNIMPLEMENTED, "%d ranks", n);
+        for (int i = 0; i < nr; ++i) {
+          hb[i] = gbase[i];
+          hb[nr + i] = tbase[i] + static_cast<int64_t>(k) * static_cast<int64_t>(tmp_words);
+          hb[2 * nr + i] = bbase[k][i];
+          hb[3 * nr + i] = gcnt[i];
+        }
+        PXG_HIP(hipMemcpyAsync(d_bases, hb, static_cast<size_t>(4 * nr) * 8, hipMemcpyHostToDevice, ctx->stream));
+        PXG_RETURN_IF_ERROR(Launch(ctx, "gather_rebase", GatherRebaseKernel, dim3(GridFor(Gt, 256, 1024)), dim3(256), 0,
+                                   static_cast<const int32_t*>(tmp), static_cast<const int64_t*>(d_bases), nr, R.key_offsets[k].as<int32_t>()));
+        // The pinned base table is reused by the next key: wait for this copy first.
+        PXG_HIP(hipStreamSynchronize(ctx->stream));
+      }
+    }
+  }
+  for (int k = 0; k < a.n_keys; ++k)
+    if (a.key_types[k] == PXG_STRING) {
+      if (G0 == 0) {
+        // The root had no rows: its offsets start at 0 (the other ranks' rows follow).
+        PXG_HIP(hipMemsetAsync(R.key_offsets[k].p, 0, 4, ctx->stream));
+      }
+      R.key_data_len[k] = btot[k];
+    }
+  R.n_groups = Gt;
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  if (n_groups) *n_groups = Gt;
+  return PXG_OK;
+}

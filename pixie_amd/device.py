@@ -350,6 +350,14 @@ class Agg:
         check(self.lib.pxg_agg_alltoall(self.h, comm.h, C.byref(s), C.byref(r)))
         return int(s.value), int(r.value)
 
+    def gather(self, comm: "Comm", root: int = 0) -> int:
+        """Every rank's finalized rows to `root` over RCCL (pxg_agg_gather; after alltoall +
+        finalize on every rank).  Collective.  Returns the gathered groups on the root, 0 elsewhere;
+        the root's result() is then the whole result."""
+        g = C.c_int64()
+        check(self.lib.pxg_agg_gather(self.h, comm.h, root, C.byref(g)))
+        return int(g.value)
+
     def close(self) -> None:
         if self.h and getattr(self.ctx, "h", None):
             self.lib.pxg_agg_destroy(self.h)

@@ -45,7 +45,9 @@ _SELF = textwrap.dedent('''
         a.consume(t)
         sent, recv = a.alltoall(comm)
         assert sent == recv and sent > 0
-        a.finalize()
+        g = a.finalize()
+        # world of one: the gather to rank 0 leaves the result as it is
+        assert a.gather(comm, 0) == g
         merged = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
         assert len(merged) == len(local), (rep, len(merged), len(local))
     # Keys and counts are identical; the mean is a float sum whose order follows the
