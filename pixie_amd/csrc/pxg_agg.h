@@ -84,6 +84,13 @@ constexpr int kHcStrWords = 3;  // STRING keys of <= 24 bytes ride in the record
 constexpr int kHcMaxVals = 4;
 constexpr int kHcMaxStride = 16;  // record streams the partition sort moves (kMaxVals)
 constexpr uint64_t kHcHole = ~0ULL;
+constexpr int kHcTableEntries = 1024;  // LDS table entries per partition (pxg_hc.hip kHcTable)
+// Dynamic LDS of one hc_agg workgroup: per table entry an 8-byte {tag, record}, 8 bytes per
+// accumulator and per MEAN high word (the exact 128-bit sum), and a 4-byte count.
+inline size_t HcAggLdsBytes(int n_acc, int n_wide) { return static_cast<size_t>(kHcTableEntries) * (8 + 8 * (n_acc + n_wide) + 4); }
+// What hc_agg may declare: gfx950 gives one workgroup up to 160 KiB of LDS; a margin is left for
+// the kernel's static LDS.
+inline size_t HcMaxDynLds() { return static_cast<size_t>(144) << 10; }
 
 struct HcStageDev {
   uint64_t* rec;

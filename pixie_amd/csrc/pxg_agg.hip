@@ -1553,21 +1553,23 @@ extern "C" int32_t pxg_agg_create(pxg_ctx* ctx, const pxg_agg_spec* spec, pxg_ag
   // at most kHcMaxVals value streams and 4 accumulated UDAs.
   {
     bool ok = a.fast_nk > 0 && !a.windowed && !a.emit_states && a.n_vals <= kHcMaxVals && kMaxVals >= kHcMaxStride;
-    int acc = 0;
+    int acc = 0, wide = 0;  // wide: MEAN accumulators, which also keep a high-word LDS array
     for (int u = 0; u < a.n_udas && ok; ++u) {
       const int k = a.uda_kind[u], at = a.uda_arg_type[u];
       const bool int_arg = at == PXG_INT64 || at == PXG_BOOLEAN;
       switch (k) {
         case PXG_UDA_COUNT: break;
         case PXG_UDA_SUM:
-        case PXG_UDA_MEAN: ok = int_arg; ++acc; break;
+        case PXG_UDA_MEAN: ok = int_arg; ++acc; wide += k == PXG_UDA_MEAN; break;
         case PXG_UDA_MINSUM: ++acc; break;
         case PXG_UDA_MIN:
         case PXG_UDA_MAX: ok = at == PXG_INT64 || at == PXG_TIME64NS; ++acc; break;
         default: ok = false;
       }
     }
-    a.hc_ok = ok && acc <= 4;
+    // LDS of one hc_agg workgroup: kHcTable x (8 B entry + 8 B per accumulator and per MEAN high
+    // word + 4 B count), within HcMaxDynLds (4 MEANs: 77,824 B; gfx950 allows 160 KiB per workgroup).
+    a.hc_ok = ok && acc <= 4 && HcAggLdsBytes(acc, wide) <= HcMaxDynLds();
     int32_t w = 1;
     for (int k = 0; k < a.n_keys; ++k) {
       const int t = a.key_types[k];

@@ -492,7 +492,9 @@ int32_t Agg::FinalizeHc() {
     out.kscr = w.hc_kscr.as<uint64_t>();
   }
   out.g0 = g0;
-  const size_t lds = static_cast<size_t>(kHcTable) * (8 + 8 * (hp.nacc + hp.nhi) + 4);
+  static_assert(kHcTable == kHcTableEntries, "LDS budget and table size disagree");
+  const size_t lds = HcAggLdsBytes(hp.nacc, hp.nhi);
+  if (lds > HcMaxDynLds()) return SetError(PXG_INTERNAL, "hc_agg needs %zu bytes of LDS", lds);
   uint32_t* meta = w.hc_meta.as<uint32_t>();
   uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 192);
   // The first pass aims at ~2^kHcGroupsLog2 groups per partition (a half-full LDS table) from

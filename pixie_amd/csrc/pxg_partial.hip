@@ -50,6 +50,7 @@ constexpr uint32_t kXVersion = 3;
 constexpr int kXCentCapH = 2048;  // = kXCentCap (pxg_finalize.hip)
 constexpr uint64_t kXFlagDigest = 1;
 constexpr int kXWtShift = 48;
+constexpr int kXMaxParts = 64;  // parts one merged run may import (pxg_finalize.hip kXParts)
 
 struct XHeader {
   uint32_t magic;
@@ -896,8 +897,10 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
     res.ready = false;
     if (rc != PXG_OK) return rc;
     const uint64_t G = static_cast<uint64_t>(res.n_groups);
-    if (st_n + uint64_t(2) * kXCentCapH * x_nbig >= (uint64_t(1) << 32))
-      return SetError(PXG_UNIMPLEMENTED, "exchange parts hold fewer than 2^32 item words");
+    // Items and item words both stay below 2^31: the group offset word keeps the item index in
+    // bits 32..62 and the centroid flag in bit 63 (kXCentFlag).
+    if (st_n + uint64_t(2) * kXCentCapH * x_nbig >= (uint64_t(1) << 31))
+      return SetError(PXG_UNIMPLEMENTED, "exchange parts hold fewer than 2^31 items and item words");
     X.G = G;
     PXG_RETURN_IF_ERROR(X.part_of.Ensure(G + 16));
     PXG_RETURN_IF_ERROR(X.koff.Ensure((2 * G + 2) * 8 + 64));   // kw, then koff_j
@@ -1032,6 +1035,13 @@ int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* of
     tot_items += has_q ? h.n_items : h.n_groups;
     tot_words += h.key_words;
   }
+  // The merged digest tells the parts apart by the part index in the weights' top bits, and
+  // DigestMergeKernel keeps one segment per part for at most kXMaxParts parts per merged run.
+  int32_t parts_here = 0;
+  for (int i = 0; i < n; ++i) parts_here += H[i].n_groups > 0 ? 1 : 0;
+  if (has_q && x_parts_seen + parts_here > kXMaxParts)
+    return SetError(PXG_UNIMPLEMENTED, "a merged aggregation takes at most %d imported parts (%d so far, %d more)", kXMaxParts, x_parts_seen,
+                    parts_here);
   merged = true;
   state_version++;
   res.ready = false;
@@ -1068,7 +1078,7 @@ int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* of
     if (srec > 0)
       PXG_RETURN_IF_ERROR(Launch(ctx, "import_states", XImportStatesKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups), 256, 1 << 30)),
                                  dim3(256), 0, xp, p + L[i].states, srec, h.n_groups, static_cast<const uint32_t*>(remap), macc.as<uint64_t>()));
-    const uint64_t part = static_cast<uint64_t>(x_parts_seen++ & 63);
+    const uint64_t part = static_cast<uint64_t>(x_parts_seen++);  // < kXMaxParts (checked above)
     if (has_q && h.n_items > 0) {
       PXG_RETURN_IF_ERROR(Launch(ctx, "import_rows", XImportItemsKernel, dim3(GridFor(static_cast<int64_t>(h.n_groups) * 64, 256, 1 << 30)),
                                  dim3(256), 0, reinterpret_cast<const uint64_t*>(p + L[i].gofs), reinterpret_cast<const uint64_t*>(p + L[i].items),

@@ -334,3 +334,36 @@ def test_every_key_long_leaves_no_partition_groups(ctx, hc_env):
     if off is not None:
         assert list(off)[-1] == sum(len(s) for s in cols[0].to_list())
     assert rows_match(rows(cols), rows(ref), ordered=False, tol_ulp=0)
+
+
+@pytest.mark.parametrize("kinds", [["mean", "mean", "mean", "mean"], ["mean", "mean", "mean", "sum"]])
+def test_four_accumulators_with_wide_means_fit_lds(ctx, hc_env, kinds):
+    """The widest high-cardinality plans: 4 INT64 MEANs (each with a 128-bit LDS sum: 77,824 B of
+    LDS per hc_agg workgroup) and 3 MEANs + 1 SUM run partitioned and match the oracle."""
+    rng = np.random.default_rng(11)
+    n = 80_000
+    types = [2, 2, 2, 2]
+    batch = [Column.from_values(2, rng.integers(0, 9000, n).tolist())] + \
+            [Column.from_values(2, rng.integers(-(1 << 50), 1 << 50, n).tolist()) for _ in range(3)]
+    tables = {"t": {"types": types, "batches": [batch]}}
+    plan = P.linear_plan([P.source_op("t", types, [f"c{i}" for i in range(4)], list(range(4))),
+                          P.agg_op([0], [P.agg_expr(k, [P.col(1 + (i % 3))], [2], fid=i) for i, k in enumerate(kinds)]),
+                          P.sink_op("out")])
+    R = _by_key(oc.execute_plan(plan, tables)["out"][0]["cols"], 1)
+    t = Table(ctx, types)
+    t.append(batch)
+    q = LinearQuery(plan, types, expected_groups=10_000)
+    a = q.make_agg(ctx)
+    a.consume(t)
+    assert a.info()["hc_mode"] == 1
+    a.finalize()
+    D = _by_key(q.emit(a.result()), 1)
+    assert set(R) == set(D)
+    for k in R:
+        for kind, x, y in zip(kinds, R[k], D[k]):
+            if kind == "sum":
+                assert x == y, k
+            else:
+                assert abs(x - y) <= 1e-9 * abs(x) + 1e-12, (k, x, y)
+    a.close()
+    t.close()

@@ -9,6 +9,7 @@
 #   pmc    : FETCH_SIZE / WRITE_SIZE passes over the consume kernel (C2) + summary JSON
 #   c3prof : rocprofv3 stats of the C3 leg
 #   diag   : tools/consume_diag.py timing modes (0 production, 2 filter only, 3 keys + hash)
+#   multi2 : bench.py --gpus 2 --share-gpu0 --backend gloo (the N>1 line, both ranks on GPU 0)
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 B="--no-cpu-baseline --no-engine-leg"
@@ -25,6 +26,7 @@ step() {
     n1only) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n1only -o run --output-format csv -- python3 tools/n1_prof.py 3 > gpurun_out/prof_n1only.log 2>&1 ;;
     c3prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/c3_prof.py > gpurun_out/prof_c3.log 2>&1 ;;
     diag) timeout -k 10 300 python3 tools/consume_diag.py 0 2 3 > gpurun_out/diag.log 2>&1 ;;
+    multi2) timeout -k 10 400 python3 -u bench.py --gpus 2 --share-gpu0 --backend gloo --steps 3 --warmup 1 > gpurun_out/bench_multi2.json 2> gpurun_out/bench_multi2.err ;;
     *) echo "unknown mode $1" >&2; return 2 ;;
   esac
 }
