@@ -166,8 +166,6 @@ struct Agg {
     // export mode: per-group states, centroid lists of the big groups (kXCentCap per big group)
     // and their counts; owner side: merged digests' scratch, digest group list
     DevBuf xstates, xcent, xcnt, mrg, dlist;
-    // counting placement (pxg_place.hip): per-slot counts, then starts / cursors
-    DevBuf place_cnt;
   } ws;
 
   int32_t EnsureTable(uint32_t new_cap);

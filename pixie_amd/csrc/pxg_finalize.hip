@@ -6,7 +6,6 @@
 
 #include "pxg_agg_host.h"
 #include "pxg_keys.h"
-#include "pxg_place.h"
 #include "pxg_scan.h"
 #include "pxg_sort.h"
 #include "pxg_tdigest.h"
@@ -3002,12 +3001,6 @@ struct SideJoinGuard {
   }
 };
 
-// Grouping by counting placement instead of the radix sort (PXG_PLACE=0 / 1 overrides).
-static bool PlaceGrouping() {
-  const char* e = std::getenv("PXG_PLACE");
-  return e ? (e[0] != 0 && e[0] != '0') : false;
-}
-
 int32_t AggFinalizeTable(Agg* a) {
   Ctx* ctx = a->ctx;
   SideJoinGuard guard{ctx};
@@ -3190,21 +3183,7 @@ int32_t AggFinalizeTable(Agg* a) {
   const uint32_t* kin = nullptr;
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
-  // Grouping by counting placement (pxg_place.hip) unless a merged / export finalize needs each
-  // part's items in order inside their group (then the stable radix sort).
-  const bool place = !split && !a->merged && !a->export_x && PlaceGrouping();
-  if (place) {
-    PlaceVals pv;
-    PlaceOut po;
-    for (int v = 0; v < kMaxVals; ++v) {
-      pv.p[v] = vin.p[v];
-      po.p[v] = vbuf[0].p[v];
-    }
-    PXG_RETURN_IF_ERROR(PlaceBySlot(ctx, a->st_slot.as<const uint32_t>(), n, a->cap, a->slots.as<const unsigned long long>(),
-                                    ws.rank.as<const uint32_t>(), ngroups, pv, nvs, po, ws.gstart.as<uint32_t>(), ws.place_cnt, scan_tmp));
-    PXG_RETURN_IF_ERROR(IssueKeys());
-    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[0].p[v];
-  } else if (!split) {
+  if (!split) {
     PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, nvs,
                                          n, kbuf, vbuf, ws.rs, &kin, &vin));
     PXG_RETURN_IF_ERROR(IssueKeys());
