@@ -65,7 +65,7 @@ constexpr int kRecMaxKeys = 2;
 
 struct AggTableDev {
   unsigned long long* slots;
-  const uint64_t* prec;  // probe records (null: off)
+  uint64_t* prec;  // probe records (null: off); row-record consumes also write them
   uint32_t mask;
   uint32_t limit;                 // inserts beyond this are deferred (table kept <= 50% full)
   unsigned int* counters;         // [0] groups in the table (flushed per tile), [2] deferred rows

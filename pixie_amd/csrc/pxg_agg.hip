@@ -495,10 +495,38 @@ __device__ __forceinline__ int RecordEqual(const uint64_t* __restrict__ rec, uns
   return eq ? 1 : 0;
 }
 
+// In-launch probe record of a group whose slot still holds its row word (RROW consumes): written
+// by the inserting lane and by a lane that confirmed the group against its representative row,
+// from the key in its registers.  Words 1..15 first, then (after their stores are acknowledged)
+// word 0 = the slot word, so a line that shows the slot word already holds the key; a reader
+// that sees a stale line (its L1 / L2 copy from before, or another XCD's copy not written back
+// yet) sees word 0 != the slot word and compares against the representative row instead.  Only
+// a record that EQUALS the probe key is trusted (a record is never taken as proof of inequality
+// in-launch), so a line caught mid-write can cost a slow compare but never a wrong group.
+template <int NK>
+__device__ __forceinline__ void WriteRowRecord(uint64_t* __restrict__ rec, unsigned long long w, const FastKeys<NK>& k) {
+  uint64_t lens = 0;
+#pragma unroll
+  for (int i = 0; i < NK; ++i) lens |= static_cast<uint64_t>(k.len[i]) << (16 * i);
+  uint64_t r[kRecWords];
+#pragma unroll
+  for (int t = 0; t < kRecWords; ++t) r[t] = 0;
+#pragma unroll
+  for (int i = 0; i < NK; ++i)
+#pragma unroll
+    for (int j = 0; j < kRecKeyWords; ++j) r[2 + kRecKeyWords * i + j] = k.w[i][j];
+  rec[1] = lens;
+  ulonglong2* d = reinterpret_cast<ulonglong2*>(rec);
+#pragma unroll
+  for (int t = 1; t < kRecWords / 2; ++t) d[t] = make_ulonglong2(r[2 * t], r[2 * t + 1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  rec[0] = w;
+}
+
 // TAGONLY: timing-only diagnostic (PXG_DIAG_CONSUME=1): a tag match is taken as the group without
 // the representative compare, which prices that compare (tools/consume_diag.py; wrong groups on
 // a tag collision, never followed by a checked finalize).
-template <int NK, bool S = false, bool TAGONLY = false, bool REC = false>
+template <int NK, bool S = false, bool TAGONLY = false, bool REC = false, bool RROW = false>
 __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                                      const KeyCols<NK>* __restrict__ s_kc, uint32_t n_lds_chunks,
                                                      const FastKeys<NK>& keys, uint64_t h, uint32_t rowref,
@@ -527,6 +555,7 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
       if (__hip_atomic_compare_exchange_strong(&tab.slots[pos], &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)) {
         atomicAdd(s_ins, 1u);
+        if constexpr (RROW) WriteRowRecord<NK>(tab.prec + static_cast<uint64_t>(pos) * kRecWords, desired, keys);
         return pos;
       }
       w = expected;  // lost the race: the winner's word decides below
@@ -541,9 +570,17 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
         if constexpr (REC) r = RecordEqual<NK>(tab.prec + static_cast<uint64_t>(pos) * kRecWords, w, keys);
         eq = r >= 0 ? r == 1 : FastKeysEqualArena<NK, S>(plan, keys, tab.arena + ref);
       } else {
-        const uint32_t c = ref >> kChunkShift;
-        const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK, S>(plan, chunks[c]);
-        eq = FastKeysEqualRow<NK, S>(plan, kc, static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
+        int r = -1;
+        if constexpr (RROW) r = RecordEqual<NK>(tab.prec + static_cast<uint64_t>(pos) * kRecWords, w, keys);
+        if (r == 1) {
+          eq = true;  // the in-launch record equals this key (see WriteRowRecord)
+        } else {
+          const uint32_t c = ref >> kChunkShift;
+          const KeyCols<NK> kc = c < n_lds_chunks ? s_kc[c] : KeyColsOf<NK, S>(plan, chunks[c]);
+          eq = FastKeysEqualRow<NK, S>(plan, kc, static_cast<int64_t>(ref & (kChunkRows - 1)), keys);
+          if constexpr (RROW)
+            if (eq && r < 0) WriteRowRecord<NK>(tab.prec + static_cast<uint64_t>(pos) * kRecWords, w, keys);
+        }
       }
       if (eq) return pos;
     }
@@ -572,7 +609,7 @@ __device__ __forceinline__ uint32_t FastFindOrInsert(const AggPlanDev* __restric
 // fills in, like any deferred row), so the two paths hold disjoint key sets.
 // REC: published slots compare against the probe records (all-STRING keys, <= 2 keys; the table
 // passes prec).
-template <int NK, int MODE, bool PAIRS = false, bool HC = false, bool REC = false>
+template <int NK, int MODE, bool PAIRS = false, bool HC = false, bool REC = false, bool RROW = false>
 __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggPlanDev* __restrict__ plan,
                                                                       const DevChunk* __restrict__ chunks,
                                                                       const TileRange* __restrict__ ranges, int nranges,
@@ -783,8 +820,8 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
             stg.slot[pos] = static_cast<uint32_t>(h);
             continue;
           }
-          slot = FastFindOrInsert<NK, S, (MODE & 3) == 1, REC && S && NK <= kRecMaxKeys>(plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab,
-                                                                                          &s_ins);
+          slot = FastFindOrInsert<NK, S, (MODE & 3) == 1, REC && S && NK <= kRecMaxKeys, RROW && S && NK <= kRecMaxKeys>(
+              plan, chunks, s_kc, n_lds_chunks, k, h, rowref, tab, &s_ins);
         }
         const unsigned long long dm = __ballot(slot == kDeferredSlot);
         if (dm) {
@@ -931,7 +968,7 @@ static AggTableDev TableDev(Agg* a, int defer_buf) {
   t.deferred = a->deferred[defer_buf].as<uint32_t>();
   t.deferred_pos = a->deferred_pos[defer_buf].as<uint32_t>();
   t.arena = a->arena.as<uint64_t>();
-  t.prec = a->rec_ok && a->rec_cap == a->cap ? a->prec.as<const uint64_t>() : nullptr;
+  t.prec = a->rec_ok && a->rec_cap == a->cap ? a->prec.as<uint64_t>() : nullptr;
   return t;
 }
 
@@ -1104,6 +1141,12 @@ static int32_t CheckTableTypes(const Agg& a, const Table& t) {
   return PXG_OK;
 }
 
+// Probe records written inside the consume launch (PXG_REC_ROW=1; off while measured).
+static bool RowRecords() {
+  const char* e = std::getenv("PXG_REC_ROW");
+  return e ? (e[0] != 0 && e[0] != '0') : false;
+}
+
 int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   HostClock clk;
   PXG_RETURN_IF_ERROR(CheckTableTypes(*this, *t));
@@ -1200,7 +1243,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   const bool rec = rec_ok && !hc_active && diag == 0 && fast_nk > 0 && fast_nk <= kRecMaxKeys && all_str && !EnvFlag("PXG_NO_PREC");
   if (rec) PXG_RETURN_IF_ERROR(EnsureRecords());
   using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t);
-  auto pick = [&](bool with_rec) -> KernFn {
+  auto pick = [&](bool with_rec, bool with_rrow = false) -> KernFn {
     KernFn kern = AggConsumeKernel;
     switch (fast_nk * 4 + (diag & 3)) {
 #define PXG_FAST_CASE(nk)                                           \
@@ -1232,10 +1275,14 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     if (all_str) {  // all-STRING keys: the specialised production kernels (PXG_PAIRS=1: 16-byte filter loads)
       switch (fast_nk) {
         case 1:
-          kern = with_rec ? AggConsumeFastKernel<1, 4, false, false, true> : (pairs ? AggConsumeFastKernel<1, 4, true> : AggConsumeFastKernel<1, 4>);
+          kern = with_rrow  ? AggConsumeFastKernel<1, 4, false, false, true, true>
+                 : with_rec ? AggConsumeFastKernel<1, 4, false, false, true>
+                            : (pairs ? AggConsumeFastKernel<1, 4, true> : AggConsumeFastKernel<1, 4>);
           break;
         case 2:
-          kern = with_rec ? AggConsumeFastKernel<2, 4, false, false, true> : (pairs ? AggConsumeFastKernel<2, 4, true> : AggConsumeFastKernel<2, 4>);
+          kern = with_rrow  ? AggConsumeFastKernel<2, 4, false, false, true, true>
+                 : with_rec ? AggConsumeFastKernel<2, 4, false, false, true>
+                            : (pairs ? AggConsumeFastKernel<2, 4, true> : AggConsumeFastKernel<2, 4>);
           break;
         case 3: kern = pairs ? AggConsumeFastKernel<3, 4, true> : AggConsumeFastKernel<3, 4>; break;
         case 4: kern = pairs ? AggConsumeFastKernel<4, 4, true> : AggConsumeFastKernel<4, 4>; break;
@@ -1297,7 +1344,13 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   // save ~1.5 ms of consume.
   const char* rme = std::getenv("PXG_PREFIX_MIN_ROWS");  // tests: the prefix path at small sizes
   const int64_t rec_min_rows = rme && std::atoll(rme) > 0 ? std::atoll(rme) : (int64_t(1) << 28);
-  if (rec && inserted == 0 && rows >= std::max<int64_t>(8 * pre_rows, rec_min_rows)) {
+  // In-launch row records (WriteRowRecord): the records build up inside the one launch, so no
+  // prefix launch is needed (PXG_REC_ROW=0 / 1 overrides).
+  const bool rrow = rec && rec_cap == cap && RowRecords();
+  if (rrow) {
+    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(true, true), "agg_consume"));
+    rec_dirty = true;
+  } else if (rec && inserted == 0 && rows >= std::max<int64_t>(8 * pre_rows, rec_min_rows)) {
     std::vector<TileRange> pre, rest;
     const int64_t nt_pre = make_ranges(begin, begin + pre_rows, kSubRows, &pre);
     const int64_t nt_rest = make_ranges(begin + pre_rows, end, tile_rows, &rest);
