@@ -1141,12 +1141,6 @@ static int32_t CheckTableTypes(const Agg& a, const Table& t) {
   return PXG_OK;
 }
 
-// Probe records written inside the consume launch (PXG_REC_ROW=1; off while measured).
-static bool RowRecords() {
-  const char* e = std::getenv("PXG_REC_ROW");
-  return e ? (e[0] != 0 && e[0] != '0') : false;
-}
-
 int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
   HostClock clk;
   PXG_RETURN_IF_ERROR(CheckTableTypes(*this, *t));
@@ -1237,9 +1231,7 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     const int64_t v = e ? std::atoll(e) : 0;
     return v > 0 ? v : 8;
   }();
-  // Probe records (pxg_agg.h): a fresh run on a large range consumes a short prefix first, whose
-  // publication writes the records of (nearly) every hot group; the rest of the range then
-  // compares against records instead of representative rows.  PXG_NO_PREC=1 turns them off.
+  // Probe records (pxg_agg.h) for all-STRING keys; PXG_NO_PREC=1 turns them off (tests compare).
   const bool rec = rec_ok && !hc_active && diag == 0 && fast_nk > 0 && fast_nk <= kRecMaxKeys && all_str && !EnvFlag("PXG_NO_PREC");
   if (rec) PXG_RETURN_IF_ERROR(EnsureRecords());
   using KernFn = void (*)(const AggPlanDev*, const DevChunk*, const TileRange*, int, int64_t, AggTableDev, StageDev, uint32_t);
@@ -1328,38 +1320,16 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     }
     return PXG_OK;
   };
-  // The prefix: ~1/32 of the range (1M..16M rows) in 8192-row tiles, so its launch is one short
-  // round of workgroups.
-  static const int64_t pre_div = [] {  // experiments: PXG_PREFIX_DIV (range / prefix rows), PXG_PREFIX_MIN
-    const char* e = std::getenv("PXG_PREFIX_DIV");
-    return e && std::atoll(e) > 0 ? std::atoll(e) : 32;
-  }();
-  static const int64_t pre_min = [] {
-    const char* e = std::getenv("PXG_PREFIX_MIN");
-    return e && std::atoll(e) > 0 ? std::atoll(e) : (int64_t(1) << 20);
-  }();
-  const int64_t pre_rows = (std::min<int64_t>(int64_t(1) << 24, std::max<int64_t>(pre_min, rows / pre_div)) / kSubRows) * kSubRows;
-  // Below ~2^28 rows the prefix launch and its publication cost what the records save (C2,
-  // 100M rows: step 2.51 ms with records vs 2.48 without, tools/prefix_ab.sh); at 1B rows they
-  // save ~1.5 ms of consume.
-  const char* rme = std::getenv("PXG_PREFIX_MIN_ROWS");  // tests: the prefix path at small sizes
-  const int64_t rec_min_rows = rme && std::atoll(rme) > 0 ? std::atoll(rme) : (int64_t(1) << 28);
-  // In-launch row records (WriteRowRecord): the records build up inside the one launch, so no
-  // prefix launch is needed (PXG_REC_ROW=0 / 1 overrides).
-  const bool rrow = rec && rec_cap == cap && RowRecords();
-  if (rrow) {
+  // Probe records build up inside the launch (WriteRowRecord): the inserting lane writes its
+  // group's record, lanes that confirm a group against its representative row write it where
+  // their XCD had none, and published groups of earlier consumes keep their publication records.
+  // (Round 4 published the hot groups with a separate prefix launch over ~1/32 of the range
+  // first: 0.43 ms at 1B rows, break-even at 100M; the in-launch records replaced it.)
+  if (rec && rec_cap == cap) {
     PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(true, true), "agg_consume"));
     rec_dirty = true;
-  } else if (rec && inserted == 0 && rows >= std::max<int64_t>(8 * pre_rows, rec_min_rows)) {
-    std::vector<TileRange> pre, rest;
-    const int64_t nt_pre = make_ranges(begin, begin + pre_rows, kSubRows, &pre);
-    const int64_t nt_rest = make_ranges(begin + pre_rows, end, tile_rows, &rest);
-    PXG_RETURN_IF_ERROR(run(d_ranges_pre, last_ranges_pre, pre, nt_pre, pick(false), "agg_consume_prefix"));
-    PXG_RETURN_IF_ERROR(EnsureRecords());  // the prefix may have grown the table
-    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, rest, nt_rest, pick(rec_cap == cap), "agg_consume"));
   } else {
-    // Records are compared only once some groups are published (a later consume of the run).
-    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(rec && rec_cap == cap && inserted > 0), "agg_consume"));
+    PXG_RETURN_IF_ERROR(run(d_ranges, last_ranges, ranges, ntiles, pick(false), "agg_consume"));
   }
   // Keep the table at most ~37% full for the next consume.
   if (inserted > static_cast<uint64_t>(cap) * 3 / 8) PXG_RETURN_IF_ERROR(Grow(NextPow2(static_cast<uint64_t>(inserted) * 4)));

@@ -87,8 +87,8 @@ struct Agg {
   DevBuf counters;  // u32 [0] groups in the table (fill guard) [2] deferred rows ; u64 @16 staging cursor;
                     // u32 @32 import inserts, @36 import error flags
   DevBuf deferred[2], deferred_pos[2];
-  DevBuf d_ranges, d_ranges_pre;
-  std::vector<uint8_t> last_ranges, last_ranges_pre;  // host copies of what d_ranges / d_ranges_pre hold
+  DevBuf d_ranges;
+  std::vector<uint8_t> last_ranges;  // host copy of what d_ranges holds
   DevBuf arena;
   uint64_t arena_words = 0;  // used (host mirror after publish)
   uint32_t last_big_sort_groups = 0;  // pxg_agg_stats.big_sort_groups

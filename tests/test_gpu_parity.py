@@ -398,12 +398,11 @@ def test_standalone_filter_across_chunks_and_launches(ctx, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_probe_record_prefix_matches_plain_consume(ctx, monkeypatch):
-    """The probe-record path (a prefix launch publishes the hot groups, the rest of the range
-    compares against 128-byte records) gives the same groups, counts, means and quantiles as the
-    plain consume, here forced at 12M rows (PXG_PREFIX_MIN_ROWS; by default it starts at 2^28)
-    and with a second consume into the same run (records of published groups, new groups
-    inserted beside them)."""
+def test_probe_records_match_plain_consume(ctx, monkeypatch):
+    """The probe-record path (records written inside the consume launch by inserting and
+    confirming lanes, WriteRowRecord; published groups' records from publication) gives the same
+    groups, counts, means and quantiles as the plain consume (PXG_NO_PREC=1), with a second
+    consume into the same run (records of published groups, new groups inserted beside them)."""
     from pixie_amd.pipeline import LinearQuery
     t = Table(ctx, P.HTTP_TYPES)
     t.append_http_events(20250117, 0, 12_000_000, 10_000_000)
@@ -411,10 +410,8 @@ def test_probe_record_prefix_matches_plain_consume(ctx, monkeypatch):
     t2.append_http_events(20250117, 12_000_000, 3_000_000, 10_000_000)
     q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
 
-    def run(prefix):
-        if prefix:
-            monkeypatch.setenv("PXG_PREFIX_MIN_ROWS", "1")
-        else:
+    def run(records):
+        if not records:
             monkeypatch.setenv("PXG_NO_PREC", "1")
         a = q.make_agg(ctx)
         a.consume(t)
@@ -422,7 +419,6 @@ def test_probe_record_prefix_matches_plain_consume(ctx, monkeypatch):
         a.finalize()
         out = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
         a.close()
-        monkeypatch.delenv("PXG_PREFIX_MIN_ROWS", raising=False)
         monkeypatch.delenv("PXG_NO_PREC", raising=False)
         return out
 

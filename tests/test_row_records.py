@@ -1,4 +1,4 @@
-"""In-launch probe records (PXG_REC_ROW=1, pixie_amd/csrc/pxg_agg.hip WriteRowRecord): the consume
+"""In-launch probe records (pixie_amd/csrc/pxg_agg.hip WriteRowRecord; PXG_NO_PREC=1 turns records off): the consume
 writes a group's probe record as soon as its inserting lane (or a lane that confirmed the group
 against its representative row) has the key in registers, and later probes trust a record only
 when it equals their key.  Checked against the CPU restatement on single consumes, on several
@@ -27,7 +27,6 @@ def _check(dev, cols_list):
 
 @pytest.mark.parametrize("expected_groups", [65536, 16])
 def test_row_records_single_consume_matches_oracle(ctx, monkeypatch, expected_groups):
-    monkeypatch.setenv("PXG_REC_ROW", "1")
     cols = datagen_http_events(SEED, 0, 3_000_000, threads=8)
     t = Table(ctx, P.HTTP_TYPES)
     t.append(cols)
@@ -45,7 +44,6 @@ def test_row_records_single_consume_matches_oracle(ctx, monkeypatch, expected_gr
 def test_row_records_across_consumes_of_two_tables(ctx, monkeypatch):
     """Rows of table B probe groups published from table A (arena records) and groups B inserts
     itself (in-launch records); the same row references name different keys in A and B."""
-    monkeypatch.setenv("PXG_REC_ROW", "1")
     ca = datagen_http_events(SEED, 0, 1_500_000, threads=8)
     cb = datagen_http_events(SEED + 1, 5_000_000, 1_500_000, threads=8)
     ta, tb = Table(ctx, P.HTTP_TYPES), Table(ctx, P.HTTP_TYPES)
@@ -68,7 +66,10 @@ def test_row_records_same_result_as_without(ctx, monkeypatch):
     t.append_http_events(SEED, 0, 20_000_000, 10_000_000)
     out = []
     for on in ("0", "1"):
-        monkeypatch.setenv("PXG_REC_ROW", on)
+        if on == "0":
+            monkeypatch.setenv("PXG_NO_PREC", "1")
+        else:
+            monkeypatch.delenv("PXG_NO_PREC", raising=False)
         q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
         a = q.make_agg(ctx)
         a.consume(t)
