@@ -163,6 +163,7 @@ struct Agg {
     // staging split (pxg_finalize.hip): sampled slot counts, flag scan, bucket x tile counts,
     // bucket totals / bases
     DevBuf split_cnt, split_flags, split_hist, split_tot;
+    DevBuf fs_keys;  // fused split: dense ids of the staged records (first pass)
     // export mode: per-group states, centroid lists of the big groups (kXCentCap per big group)
     // and their counts; owner side: merged digests' scratch, digest group list
     DevBuf xstates, xcent, xcnt, mrg, dlist;

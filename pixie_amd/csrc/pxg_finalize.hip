@@ -2633,12 +2633,12 @@ __global__ void SplitLevelsKernel(const uint32_t* __restrict__ scnt, uint32_t ca
   if (threadIdx.x < 32 && s_l[threadIdx.x]) atomicAdd(&lvl[threadIdx.x], s_l[threadIdx.x]);
 }
 
-__device__ __forceinline__ uint32_t SplitThreshold(const uint32_t* __restrict__ lvl, uint32_t min_samples) {
+__device__ __forceinline__ uint32_t SplitThreshold(const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big) {
   uint32_t above = 0;  // slots with a count >= 2^(l + 1)
   int L = 32;
   for (int l = 31; l >= 0; --l) {
     above += lvl[l];
-    if (above > kSplitMaxBig) break;
+    if (above > max_big) break;
     L = l;
   }
   const uint32_t p = L >= 32 ? 0xFFFFFFFFu : (1u << L);
@@ -2647,32 +2647,32 @@ __device__ __forceinline__ uint32_t SplitThreshold(const uint32_t* __restrict__ 
 
 // flags[slot] = designated << 32 | occupied (one u64 scan gives both ranks).
 __global__ void SplitFlagsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
-                                 const uint32_t* __restrict__ lvl, uint32_t min_samples, uint64_t* __restrict__ flags) {
+                                 const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big, uint64_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
-  const uint32_t t = SplitThreshold(lvl, min_samples);
+  const uint32_t t = SplitThreshold(lvl, min_samples, max_big);
   const bool occ = slots[i] != 0;
   const bool des = occ && scnt[i] >= t;
   flags[i] = (static_cast<uint64_t>(des) << 32) | static_cast<uint64_t>(occ);
 }
 
-__device__ __forceinline__ uint32_t SplitNd(const uint64_t* __restrict__ ftotal) {
-  return min(static_cast<uint32_t>(*ftotal >> 32), kSplitMaxBig);
+__device__ __forceinline__ uint32_t SplitNd(const uint64_t* __restrict__ ftotal, uint32_t max_big = kSplitMaxBig) {
+  return min(static_cast<uint32_t>(*ftotal >> 32), max_big);
 }
 
 // Group ids from the scanned flags: designated slots -> Gr + their rank, the rest -> their rank
 // among the rest; gslot[id] = slot (so gslot[Gr + j] lists the designated slots by bucket).
 __global__ void SplitIdsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
-                               const uint32_t* __restrict__ lvl, uint32_t min_samples, const uint64_t* __restrict__ fscan,
+                               const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big, const uint64_t* __restrict__ fscan,
                                const uint64_t* __restrict__ ftotal, uint32_t G, uint32_t* __restrict__ newid, uint32_t* __restrict__ gslot) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap || slots[i] == 0) return;
-  const uint32_t t = SplitThreshold(lvl, min_samples);
-  const uint32_t nd = SplitNd(ftotal), Gr = G - nd;
+  const uint32_t t = SplitThreshold(lvl, min_samples, max_big);
+  const uint32_t nd = SplitNd(ftotal, max_big), Gr = G - nd;
   const uint64_t f = fscan[i];
   const uint32_t d_rank = static_cast<uint32_t>(f >> 32), o_rank = static_cast<uint32_t>(f);
-  const bool des = scnt[i] >= t && d_rank < kSplitMaxBig;
-  const uint32_t id = des ? Gr + d_rank : o_rank - min(d_rank, kSplitMaxBig);
+  const bool des = scnt[i] >= t && d_rank < max_big;
+  const uint32_t id = des ? Gr + d_rank : o_rank - min(d_rank, max_big);
   newid[i] = id;
   gslot[id] = i;
 }
@@ -2942,6 +2942,304 @@ __global__ void SplitGstartKernel(const uint32_t* __restrict__ base, const uint6
   if (j <= nd) gstart[G - nd + j] = base[1 + j];
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused split (large aggregations): the staging split folded into the radix sort's first pass.
+// The largest groups by a sample (at most kFsMaxU, "designated" as in the split above) get one
+// bucket each in a 10-bit first pass whose other 256 buckets are the low digit of the remaining
+// ("rest") groups' ids: one stable pass leaves every designated group contiguous and final, and
+// the rest records sorted by their low digit, so only the rest records (~30 % at the north_star
+// size) go through the remaining pass(es).  Final layout [rest by id | designated by id | no
+// group], the same as the split's.
+// ---------------------------------------------------------------------------------------
+constexpr int kFsBits = 10;
+constexpr int kFsBuckets = 1 << kFsBits;          // 1024
+constexpr int kFsRest = kRadixBuckets;            // buckets [0, 256): the rest's low digit
+constexpr uint32_t kFsMaxU = kFsBuckets - kFsRest - 1;  // designated buckets; the last one: no group
+constexpr int kFsBlock = 256;
+constexpr int kFsItems = 12;
+constexpr int kFsTile = kFsBlock * kFsItems;      // 3072 records
+static_assert(kFsBuckets % kFsBlock == 0, "buckets per thread");
+
+__device__ __forceinline__ uint32_t FsBucket(uint32_t id, uint32_t Gr, uint32_t G, uint32_t nd) {
+  return id < Gr ? (id & (kFsRest - 1)) : (id < G ? kFsRest + (id - Gr) : kFsRest + nd);
+}
+
+// Tile bucket counts -> hist[tile * kFsBuckets + b] (tile-major); the dense ids (newid[slot], G
+// for a record without a group) to dense_out for the scatter.
+template <int kHistTiles>
+__global__ void __launch_bounds__(kFsBlock) FsHistKernel(const uint32_t* __restrict__ slot, uint64_t n, const uint32_t* __restrict__ newid,
+                                                         uint32_t cap, uint32_t G, const uint64_t* __restrict__ ftotal,
+                                                         uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ dense_out) {
+  constexpr int kWaves = kFsBlock / 64;
+  __shared__ uint32_t h[kWaves][kFsBuckets];
+  const int wid = threadIdx.x >> 6;
+  const uint32_t nd = SplitNd(ftotal, kFsMaxU), Gr = G - nd;
+  const uint32_t tile0 = XcdRemap(blockIdx.x, gridDim.x) * kHistTiles;
+  const uint64_t base = static_cast<uint64_t>(tile0) * kFsTile;
+  const uint32_t rem = static_cast<uint32_t>(min(n - min(n, base), static_cast<uint64_t>(kHistTiles) * kFsTile));
+  const uint32_t* kp = slot + base;
+  uint32_t kk[kHistTiles][kFsItems];
+#pragma unroll
+  for (int j = 0; j < kHistTiles; ++j)
+#pragma unroll
+    for (int k = 0; k < kFsItems; ++k) {
+      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
+      kk[j][k] = i < rem ? kp[i] : 0u;
+    }
+#pragma unroll
+  for (int j = 0; j < kHistTiles; ++j)
+#pragma unroll
+    for (int k = 0; k < kFsItems; ++k) {
+      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
+      if (i < rem) {
+        kk[j][k] = kk[j][k] < cap ? newid[kk[j][k]] : G;
+        dense_out[base + i] = kk[j][k];
+      }
+    }
+#pragma unroll
+  for (int j = 0; j < kHistTiles; ++j) {
+    if (tile0 + j >= ntiles) break;  // uniform
+    for (int w = 0; w < kWaves; ++w)
+      for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) h[w][d] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kFsItems; ++k) {
+      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
+      if (i < rem) atomicAdd(&h[wid][FsBucket(kk[j][k], Gr, G, nd)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) t += h[w][d];
+      hist[static_cast<uint64_t>(tile0 + j) * kFsBuckets + d] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// Tile offsets of NB-bucket tile-major counts (the RsPart / RsPartScan / RsDown scheme for any
+// bucket count): per 16-tile range the bucket sums; per bucket the scan of the range sums and
+// the bucket total; the bucket bases (exclusive scan of the totals, base[NB] = the total); per
+// range the running offsets, in place.
+template <int NB>
+__global__ void __launch_bounds__(256) XPartKernel(const uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ part) {
+  const uint32_t w = blockIdx.x;
+  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
+  for (int d = threadIdx.x; d < NB; d += 256) {
+    uint32_t s = 0;
+    for (uint32_t t = t0; t < t1; ++t) s += hist[static_cast<uint64_t>(t) * NB + d];
+    part[static_cast<uint64_t>(w) * NB + d] = s;
+  }
+}
+template <int NB>
+__global__ void __launch_bounds__(kRsScanBlock) XPartScanKernel(uint32_t* __restrict__ part, uint32_t nparts, uint32_t* __restrict__ tot) {
+  constexpr int kWaves = kRsScanBlock / 64;
+  __shared__ uint32_t s_w[kWaves];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint32_t d = blockIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < nparts; i0 += kRsScanBlock) {
+    const uint32_t i = i0 + t;
+    const uint32_t c = i < nparts ? part[static_cast<uint64_t>(i) * NB + d] : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int w = 0; w < wid; ++w) before += s_w[w];
+    uint32_t round = 0;
+    for (int w = 0; w < kWaves; ++w) round += s_w[w];
+    if (i < nparts) part[static_cast<uint64_t>(i) * NB + d] = before + incl - c;
+    carry += round;
+    __syncthreads();
+  }
+  if (t == 0) tot[d] = carry;
+}
+template <int NB>
+__global__ void __launch_bounds__(256) XBaseKernel(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
+  constexpr int kPer = NB / 256;
+  __shared__ uint32_t s_w[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    v[k] = tot[threadIdx.x * kPer + k];
+    sum += v[k];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (int w = 0; w < wid; ++w) run += s_w[w];
+  if (threadIdx.x == 255) base[NB] = run + sum;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    base[threadIdx.x * kPer + k] = run;
+    run += v[k];
+  }
+}
+template <int NB>
+__global__ void __launch_bounds__(256) XDownKernel(uint32_t* __restrict__ hist, uint32_t ntiles, const uint32_t* __restrict__ part,
+                                                   const uint32_t* __restrict__ base) {
+  const uint32_t w = blockIdx.x;
+  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
+  for (int d = threadIdx.x; d < NB; d += 256) {
+    uint32_t run = base[d] + part[static_cast<uint64_t>(w) * NB + d];
+    for (uint32_t t = t0; t < t1; ++t) {
+      uint32_t* h = hist + static_cast<uint64_t>(t) * NB + d;
+      const uint32_t c = *h;
+      *h = run;
+      run += c;
+    }
+  }
+}
+
+// The fused first pass (RsScatterKernel's scheme with 1024 buckets: 10-ballot wave ranks, the
+// tile reordered by bucket in LDS, bucket runs written out).  Rest records (key and values) go to
+// the rest sort's input [0, n_rest); designated records' values straight to their final position
+// in vfin; records without a group are not written (nothing reads past gstart[G]).
+__global__ void __launch_bounds__(kFsBlock) FsScatterKernel(const uint32_t* __restrict__ kin, uint64_t n, uint32_t G,
+                                                            const uint64_t* __restrict__ ftotal, ConstValPtrs vin, int nvals,
+                                                            const uint32_t* __restrict__ offs, uint32_t* __restrict__ kout, ValPtrs vrest,
+                                                            ValPtrs vfin) {
+  constexpr int kWaves = kFsBlock / 64;
+  constexpr int kPerWave = kFsTile / kWaves;
+  constexpr int kPerThr = kFsBuckets / kFsBlock;
+  __shared__ uint32_t whist[kWaves][kFsBuckets];
+  __shared__ uint32_t dstart[kFsBuckets];
+  __shared__ uint32_t gofs[kFsBuckets];
+  __shared__ uint64_t s_buf[kFsTile];
+  __shared__ uint16_t s_dig[kFsTile];
+  __shared__ uint32_t s_w[kWaves];
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
+  const uint32_t nd = SplitNd(ftotal, kFsMaxU), Gr = G - nd;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
+  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
+  for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) {
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) whist[w][d] = 0;
+    gofs[d] = offs[static_cast<uint64_t>(tile) * kFsBuckets + d];
+  }
+  __syncthreads();
+  const uint64_t tile0 = static_cast<uint64_t>(tile) * kFsTile;
+  const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
+  const int tn = static_cast<int>(min(static_cast<uint64_t>(kFsTile), n - tile0));
+  uint32_t part[kFsItems], keys[kFsItems], dig[kFsItems];
+  uint64_t v0[kFsItems];
+#pragma unroll
+  for (int k = 0; k < kFsItems; ++k) {
+    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
+    keys[k] = i < n ? kin[i] : 0u;
+    v0[k] = (nvals > 0 && i < n) ? vin.p[0][i] : 0ULL;
+  }
+#pragma unroll
+  for (int k = 0; k < kFsItems; ++k) {
+    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
+    const bool valid = i < n;
+    const uint32_t d = FsBucket(keys[k], Gr, G, nd);
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kFsBits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(valid && bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t r = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
+    const uint32_t pre = valid ? whist[wid][d] : 0u;
+    WaveSync();
+    if (valid && r == 0) whist[wid][d] = pre + static_cast<uint32_t>(__popcll(peers));
+    WaveSync();
+    part[k] = pre + r;
+    dig[k] = d;
+  }
+  __syncthreads();
+  {
+    // Bucket starts inside the tile: thread t owns buckets [t * kPerThr, (t + 1) * kPerThr).
+    uint32_t tot[kPerThr], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPerThr; ++q) {
+      const int d = threadIdx.x * kPerThr + q;
+      tot[q] = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) tot[q] += whist[w][d];
+      sum += tot[q];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wid; ++w) run += s_w[w];
+#pragma unroll
+    for (int q = 0; q < kPerThr; ++q) {
+      const int d = threadIdx.x * kPerThr + q;
+      dstart[d] = run;
+      uint32_t acc = run;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {  // in place: whist[w][d] becomes the start of (w, d)
+        const uint32_t c = whist[w][d];
+        whist[w][d] = acc;
+        acc += c;
+      }
+      run += tot[q];
+    }
+  }
+  __syncthreads();
+  uint32_t lpos[kFsItems];
+#pragma unroll
+  for (int k = 0; k < kFsItems; ++k) {
+    lpos[k] = whist[wid][dig[k]] + part[k];
+    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) {
+      s_key[lpos[k]] = keys[k];
+      s_dig[lpos[k]] = static_cast<uint16_t>(dig[k]);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < tn; j += kFsBlock) {
+    const uint32_t d = s_dig[j];
+    if (d < static_cast<uint32_t>(kFsRest)) kout[gofs[d] + (j - dstart[d])] = s_key[j];
+  }
+  const uint32_t d_none = kFsRest + nd;
+  for (int v = 0; v < nvals; ++v) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kFsItems; ++k) {
+      const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
+      if (i < n) s_buf[lpos[k]] = v == 0 ? v0[k] : vin.p[v][i];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < tn; j += kFsBlock) {
+      const uint32_t d = s_dig[j];
+      const uint32_t dst = gofs[d] + (j - dstart[d]);
+      if (d < static_cast<uint32_t>(kFsRest)) vrest.p[v][dst] = s_buf[j];
+      else if (d < d_none) vfin.p[v][dst] = s_buf[j];
+    }
+  }
+}
+
+// gstart of the designated groups and gstart[G]: gstart[Gr + j] = base[kFsRest + j], j <= nd.
+__global__ void FsGstartKernel(const uint32_t* __restrict__ base, const uint64_t* __restrict__ ftotal, uint32_t G,
+                               uint32_t* __restrict__ gstart) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nd = SplitNd(ftotal, kFsMaxU);
+  if (j <= nd) gstart[G - nd + j] = base[kFsRest + j];
+}
+
 int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* vals,
                        uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals) {
   for (int b = 0; b < 2; ++b) {
@@ -3001,6 +3299,15 @@ struct SideJoinGuard {
   }
 };
 
+// Fused split for large aggregations (PXG_FSPLIT=0 / 1 overrides the size rule).
+constexpr uint64_t kFsMinStaged = uint64_t(1) << 22;
+constexpr uint32_t kFsMinRows = 4096;  // designate a group whose sampled estimate reaches this
+static bool FusedSplitOn(uint64_t n) {
+  const char* e = std::getenv("PXG_FSPLIT");
+  if (e && e[0]) return e[0] != '0';
+  return n >= kFsMinStaged;
+}
+
 int32_t AggFinalizeTable(Agg* a) {
   Ctx* ctx = a->ctx;
   SideJoinGuard guard{ctx};
@@ -3056,8 +3363,15 @@ int32_t AggFinalizeTable(Agg* a) {
     return static_cast<uint32_t>(std::max<uint64_t>(1, est / kSplitStride));
   }();
   const bool split = n >= split_min_rows && ngroups >= 2;
+  // Fused split (FsHistKernel above): large aggregations whose radix sort needs more than one
+  // pass (PXG_FSPLIT=0 / 1 overrides).
+  int gbits = 1;
+  while ((uint64_t(1) << gbits) < static_cast<uint64_t>(ngroups) + 1) ++gbits;
+  const bool fsplit = !split && gbits > kRadixBits && FusedSplitOn(n);
+  const uint32_t max_big = fsplit ? kFsMaxU : kSplitMaxBig;
+  const uint32_t min_samples = fsplit ? std::max<uint32_t>(1, kFsMinRows / kSplitStride) : split_min_samples;
   uint64_t* d_ftotal = nullptr;
-  if (!split) {
+  if (!split && !fsplit) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "slot_flags", SlotFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
                                a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>()));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
@@ -3077,11 +3391,11 @@ int32_t AggFinalizeTable(Agg* a) {
                                ws.split_cnt.as<const uint32_t>(), a->cap, lvl));
     PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
                                a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
-                               static_cast<const uint32_t*>(lvl), split_min_samples, flags));
+                               static_cast<const uint32_t*>(lvl), min_samples, max_big, flags));
     PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, flags, flags, a->cap, d_ftotal, scan_tmp));
     PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitIdsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
                                a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
-                               static_cast<const uint32_t*>(lvl), split_min_samples, static_cast<const uint64_t*>(flags), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.rank.as<uint32_t>(),
+                               static_cast<const uint32_t*>(lvl), min_samples, max_big, static_cast<const uint64_t*>(flags), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.rank.as<uint32_t>(),
                                ws.gslot.as<uint32_t>()));
     // d_ngroups (the device's own group count, checked at the end) from the occupied total.
     PXG_HIP(hipMemcpyAsync(d_ngroups, d_ftotal, 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -3183,7 +3497,64 @@ int32_t AggFinalizeTable(Agg* a) {
   const uint32_t* kin = nullptr;
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
-  if (!split) {
+  if (fsplit) {
+    // 2''. The fused split: one 10-bit pass (designated groups final, rest records by their low
+    //      digit), then the rest records' remaining pass(es) by the higher digits.  The pass
+    //      count of the rest comes from G (an upper bound of the rest ids), so the buffer the
+    //      rest sort ends in is known before the rest count comes back.
+    const int p2 = (gbits - kRadixBits + kRadixBits - 1) / kRadixBits;
+    const int fin = p2 == 0 ? 1 : (p2 - 1) & 1;
+    const uint32_t ntiles = static_cast<uint32_t>((n + kFsTile - 1) / kFsTile);
+    const uint32_t nparts = (ntiles + kRsTilesPerPart - 1) / kRsTilesPerPart;
+    PXG_RETURN_IF_ERROR(ws.split_hist.Ensure(static_cast<size_t>(ntiles) * kFsBuckets * 4));
+    PXG_RETURN_IF_ERROR(ws.rs.part.Ensure(static_cast<size_t>(nparts) * kFsBuckets * 4));
+    PXG_RETURN_IF_ERROR(ws.split_tot.Ensure(static_cast<size_t>(2 * kFsBuckets + 2) * 4));
+    PXG_RETURN_IF_ERROR(ws.fs_keys.Ensure(n * 4 + 16));
+    uint32_t* hist = ws.split_hist.as<uint32_t>();
+    uint32_t* tot = ws.split_tot.as<uint32_t>();
+    uint32_t* base = tot + kFsBuckets;
+    const int ht = ntiles >= 16384 ? 4 : 1;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist_rank", ht == 4 ? FsHistKernel<4> : FsHistKernel<1>, dim3((ntiles + ht - 1) / ht),
+                               dim3(kFsBlock), 0, a->st_slot.as<const uint32_t>(), n, ws.rank.as<const uint32_t>(), a->cap, ngroups,
+                               static_cast<const uint64_t*>(d_ftotal), hist, ntiles, ws.fs_keys.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XPartKernel<kFsBuckets>, dim3(nparts), dim3(256), 0, static_cast<const uint32_t*>(hist), ntiles,
+                               ws.rs.part.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XPartScanKernel<kFsBuckets>, dim3(kFsBuckets), dim3(kRsScanBlock), 0, ws.rs.part.as<uint32_t>(),
+                               nparts, tot));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XBaseKernel<kFsBuckets>, dim3(1), dim3(256), 0, static_cast<const uint32_t*>(tot), base));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XDownKernel<kFsBuckets>, dim3(nparts), dim3(256), 0, hist, ntiles,
+                               static_cast<const uint32_t*>(ws.rs.part.as<uint32_t>()), static_cast<const uint32_t*>(base)));
+    // n_rest (= base[kFsRest]) and the designated count to the host; the scatter runs meanwhile.
+    uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
+    PXG_HIP(hipMemcpyAsync(pin + 104, base + kFsRest, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipMemcpyAsync(pin + 112, d_ftotal, 8, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipEventRecord(ctx->ev_split, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", FsScatterKernel, dim3(ntiles), dim3(kFsBlock), 0, static_cast<const uint32_t*>(ws.fs_keys.as<uint32_t>()),
+                               n, ngroups, static_cast<const uint64_t*>(d_ftotal), vin, nvs, static_cast<const uint32_t*>(hist), kbuf[1], vbuf[1],
+                               vbuf[fin]));
+    PXG_RETURN_IF_ERROR(IssueKeys());
+    PXG_HIP(hipEventSynchronize(ctx->ev_split));
+    uint32_t n_rest = 0;
+    uint64_t ft = 0;
+    std::memcpy(&n_rest, pin + 104, 4);
+    std::memcpy(&ft, pin + 112, 8);
+    const uint32_t nd = std::min<uint32_t>(static_cast<uint32_t>(ft >> 32), kFsMaxU);
+    const uint32_t Gr = ngroups - nd;
+    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[fin].p[v];
+    if (n_rest > 0) {
+      const uint32_t* rkeys = kbuf[1];
+      if (p2 > 0) {
+        ConstValPtrs rin, rout;
+        for (int v = 0; v < kMaxVals; ++v) rin.p[v] = vbuf[1].p[v];
+        PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], nullptr, 0, Gr, rin, nvs, n_rest, kbuf, vbuf, ws.rs, &rkeys, &rout, kRadixBits,
+                                             p2 * kRadixBits));
+      }
+      PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n_rest), 256, 1 << 30)), dim3(256), 0,
+                                 rkeys, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
+    }
+    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", FsGstartKernel, dim3((kFsMaxU + 256) / 256), dim3(256), 0, static_cast<const uint32_t*>(base),
+                               static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
+  } else if (!split) {
     PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, nvs,
                                          n, kbuf, vbuf, ws.rs, &kin, &vin));
     PXG_RETURN_IF_ERROR(IssueKeys());
