@@ -2951,8 +2951,8 @@ __global__ void SplitGstartKernel(const uint32_t* __restrict__ base, const uint6
 // size) go through the remaining pass(es).  Final layout [rest by id | designated by id | no
 // group], the same as the split's.
 // ---------------------------------------------------------------------------------------
-constexpr int kFsBits = 10;
-constexpr int kFsBuckets = 1 << kFsBits;          // 1024
+constexpr int kFsBits = 9;
+constexpr int kFsBuckets = 1 << kFsBits;          // 512
 constexpr int kFsRest = kRadixBuckets;            // buckets [0, 256): the rest's low digit
 constexpr uint32_t kFsMaxU = kFsBuckets - kFsRest - 1;  // designated buckets; the last one: no group
 constexpr int kFsBlock = 256;
