@@ -2945,11 +2945,13 @@ __global__ void SplitGstartKernel(const uint32_t* __restrict__ base, const uint6
 // ---------------------------------------------------------------------------------------
 // Fused split (large aggregations): the staging split folded into the radix sort's first pass.
 // The largest groups by a sample (at most kFsMaxU, "designated" as in the split above) get one
-// bucket each in a 10-bit first pass whose other 256 buckets are the low digit of the remaining
+// bucket each in a 9-bit first pass whose other 256 buckets are the low digit of the remaining
 // ("rest") groups' ids: one stable pass leaves every designated group contiguous and final, and
 // the rest records sorted by their low digit, so only the rest records (~30 % at the north_star
 // size) go through the remaining pass(es).  Final layout [rest by id | designated by id | no
-// group], the same as the split's.
+// group], the same as the split's.  A 10-bit pass (767 designated groups, 73 % of the records at
+// 1B rows) measured slower: ~1000 partial-line runs per 3072-record tile outran the L2's write
+// combining (scatter 1.11 ms vs 0.83 ms with 512 buckets).
 // ---------------------------------------------------------------------------------------
 constexpr int kFsBits = 9;
 constexpr int kFsBuckets = 1 << kFsBits;          // 512
@@ -3300,7 +3302,9 @@ struct SideJoinGuard {
 };
 
 // Fused split for large aggregations (PXG_FSPLIT=0 / 1 overrides the size rule).
-constexpr uint64_t kFsMinStaged = uint64_t(1) << 22;
+// Measured (rocprof, same box): 1B rows (120M staged) finalize span 5.00 -> 4.84 ms; at C2 (12M
+// staged) the extra sample / designation launches cost what the shorter rest pass saves.
+constexpr uint64_t kFsMinStaged = uint64_t(1) << 25;
 constexpr uint32_t kFsMinRows = 4096;  // designate a group whose sampled estimate reaches this
 static bool FusedSplitOn(uint64_t n) {
   const char* e = std::getenv("PXG_FSPLIT");
