@@ -253,20 +253,25 @@ __global__ void __launch_bounds__(kOpsBlock) FilterCountKernel(const DevProgram*
 constexpr int kFScanPer = 16;
 static_assert(kOpsBlock * kFScanPer * kOpsTileRows >= kChunkRows, "a part's tiles must fit one scan workgroup");
 __global__ void __launch_bounds__(kOpsBlock) FilterScanKernel(const FDesc* __restrict__ fd, int part0, int nq, uint32_t* __restrict__ fig,
-                                                              int64_t T, uint32_t* __restrict__ totals) {
+                                                              int64_t T, uint32_t* __restrict__ totals, uint32_t* __restrict__ maxes) {
   __shared__ uint32_t s_part[kOpsBlock];
+  __shared__ uint32_t s_max[kOpsBlock / 64];
   const FPart& pt = fd->fb.part[blockIdx.x];
   const int q = blockIdx.y;
   uint32_t* f = fig + q * T + pt.tile0;
   const int nt = pt.ntiles;
   const int i0 = threadIdx.x * kFScanPer;
   uint32_t v[kFScanPer];
-  uint32_t sum = 0;
+  uint32_t sum = 0, mx = 0;
 #pragma unroll
   for (int j = 0; j < kFScanPer; ++j) {
     v[j] = i0 + j < nt ? f[i0 + j] : 0u;
     sum += v[j];
+    mx = max(mx, v[j]);
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, o, 64)));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = mx;
   s_part[threadIdx.x] = sum;
   __syncthreads();
   for (int o = 1; o < kOpsBlock; o <<= 1) {  // inclusive Hillis-Steele scan of the partials
@@ -282,6 +287,7 @@ __global__ void __launch_bounds__(kOpsBlock) FilterScanKernel(const FDesc* __res
     run += v[j];
   }
   if (threadIdx.x == kOpsBlock - 1) totals[(part0 + blockIdx.x) * nq + q] = s_part[kOpsBlock - 1];
+  if (threadIdx.x == 0 && q == 0) maxes[part0 + blockIdx.x] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
 }
 
 // Decoupled look-back status words (one per tile and STRING column): bits 62-63 the state
@@ -296,9 +302,15 @@ constexpr uint64_t kLbAgg = uint64_t(1) << 62, kLbIncl = uint64_t(2) << 62, kLbV
 // finds its byte base by decoupled look-back over the preceding tiles of its chunk (tiles are
 // taken in launch order from a counter, so every tile it waits for is already running), then a
 // block scan per round of 256 ranks places each payload and writes the end offsets.
+// The first kFLdsStr STRING columns keep every selected row's {start, length} in dynamic LDS
+// (lds_cap entries per column: the largest tile count of the call, from the scan) between the
+// byte count and the payload copy, so the offsets are read once.
+constexpr int kFLdsStr = 2;
 __global__ void __launch_bounds__(kOpsBlock) FilterWriteKernel(const DevChunk* __restrict__ chunks, const FDesc* __restrict__ fd,
                                                                const unsigned long long* __restrict__ masks, const uint32_t* __restrict__ fig,
-                                                               int64_t T, unsigned int* __restrict__ tile_ctr, uint64_t* __restrict__ lb) {
+                                                               int64_t T, unsigned int* __restrict__ tile_ctr, uint64_t* __restrict__ lb,
+                                                               uint32_t lds_cap) {
+  extern __shared__ uint32_t s_dyn[];  // [kFLdsStr][lds_cap] starts, then [kFLdsStr][lds_cap] lengths
   __shared__ uint32_t s_pre[kOpsMasksPerTile];
   __shared__ uint16_t s_row[kOpsTileRows];
   __shared__ uint32_t s_wave[kOpsBlock / 64];
@@ -345,10 +357,20 @@ __global__ void __launch_bounds__(kOpsBlock) FilterWriteKernel(const DevChunk* _
   for (int c = 0; c < sel.n; ++c) {
     if (sel.width[c] != 0) continue;
     const int32_t* off = ch.cols[sel.col[c]].offsets + row0;
+    const int si = sel.sidx[c];
+    uint32_t* s_st = s_dyn + static_cast<uint32_t>(si) * lds_cap;
+    uint32_t* s_ln = s_dyn + static_cast<uint32_t>(kFLdsStr + si) * lds_cap;
+    const bool keep = si < kFLdsStr && tile_sel <= lds_cap;
     uint32_t bytes = 0;
     for (uint32_t i = threadIdx.x; i < tile_sel; i += kOpsBlock) {
       const uint32_t r = s_row[i];
-      bytes += static_cast<uint32_t>(off[r + 1] - off[r]);
+      const int32_t a = off[r];
+      const uint32_t len = static_cast<uint32_t>(off[r + 1] - a);
+      bytes += len;
+      if (keep) {
+        s_st[i] = static_cast<uint32_t>(a);
+        s_ln[i] = len;
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o, 64);
@@ -417,15 +439,24 @@ __global__ void __launch_bounds__(kOpsBlock) FilterWriteKernel(const DevChunk* _
     int32_t* doff = out.off[c] + base + 1;
     uint8_t* ddata = out.data[c];
     uint32_t carry = static_cast<uint32_t>(s_base[sel.sidx[c]]);
+    const int si = sel.sidx[c];
+    const uint32_t* s_st = s_dyn + static_cast<uint32_t>(si) * lds_cap;
+    const uint32_t* s_ln = s_dyn + static_cast<uint32_t>(kFLdsStr + si) * lds_cap;
+    const bool kept = si < kFLdsStr && tile_sel <= lds_cap;
     for (uint32_t r0 = 0; r0 < tile_sel; r0 += kOpsBlock) {  // block-uniform rounds
       const uint32_t i = r0 + threadIdx.x;
       const bool on = i < tile_sel;
       int32_t a = 0;
       uint32_t len = 0;
       if (on) {
-        const uint32_t r = s_row[i];
-        a = off[r];
-        len = static_cast<uint32_t>(off[r + 1] - a);
+        if (kept) {
+          a = static_cast<int32_t>(s_st[i]);
+          len = s_ln[i];
+        } else {
+          const uint32_t r = s_row[i];
+          a = off[r];
+          len = static_cast<uint32_t>(off[r + 1] - a);
+        }
       }
       uint32_t x = len;  // inclusive wave scan, then the waves before this one
 #pragma unroll
@@ -514,7 +545,7 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
   const size_t pin_cap = (Ctx::kPinnedBytes - Ctx::kPinnedOps) / 4;
   // pinned: [0, P) selected rows, then per (part, STRING column) the input byte range (2 words)
   // and the output bytes (2 words, the look-back's u64 inclusive prefix)
-  if (parts.size() * (1 + 4 * static_cast<size_t>(fs.n_str)) + 2 > pin_cap) return SetError(PXG_UNIMPLEMENTED, "filter over %zu chunks", parts.size());
+  if (parts.size() * (2 + 4 * static_cast<size_t>(fs.n_str)) + 2 > pin_cap) return SetError(PXG_UNIMPLEMENTED, "filter over %zu chunks", parts.size());
   uint32_t* pin = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps);
   pxg_table* ot = nullptr;
   PXG_RETURN_IF_ERROR(NewTable(ctx, static_cast<int32_t>(otypes.size()), otypes.data(), &ot));
@@ -531,9 +562,10 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
   const bool fast = shape == kShapeCol || shape == kShapeColOpConst;
   OpsWorkspace& w = ctx->ops;
   PXG_RETURN_IF_ERROR(w.masks.Ensure(static_cast<size_t>(T) * kOpsMasksPerTile * 8 + 64));
-  PXG_RETURN_IF_ERROR(w.tiles.Ensure(static_cast<size_t>(T) * nq * 4 + parts.size() * nq * 4 + 64));
+  PXG_RETURN_IF_ERROR(w.tiles.Ensure(static_cast<size_t>(T) * nq * 4 + parts.size() * (nq + 1) * 4 + 64));
   uint32_t* fig = w.tiles.as<uint32_t>();
   uint32_t* totals = fig + T * nq;
+  uint32_t* maxes = totals + parts.size() * nq;  // the largest tile count of each part
   // Chunks per launch (tests: PXG_FILTER_BATCH=1..8 forces launch boundaries at small sizes).
   const char* fbe = std::getenv("PXG_FILTER_BATCH");
   const size_t nbatch = fbe && std::atoi(fbe) >= 1 && std::atoi(fbe) <= kFBatch ? static_cast<size_t>(std::atoi(fbe)) : kFBatch;
@@ -561,12 +593,13 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
                                dim3(static_cast<unsigned>(batch_tiles(fb))), dim3(kOpsBlock), 0, d_prog, t.d_chunks.as<const DevChunk>(),
                                d_types, d_desc, w.masks.as<unsigned long long>(), fig, T));
     PXG_RETURN_IF_ERROR(Launch(ctx, "filter_scan", FilterScanKernel, dim3(static_cast<unsigned>(fb.n), static_cast<unsigned>(nq)), dim3(kOpsBlock),
-                               0, d_desc, static_cast<int>(b0), nq, fig, T, totals));
+                               0, d_desc, static_cast<int>(b0), nq, fig, T, totals, maxes));
   }
-  PXG_HIP(hipMemcpyAsync(pin, totals, parts.size() * nq * 4, hipMemcpyDeviceToHost, ctx->stream));
+  // totals then maxes (adjacent on the device)
+  PXG_HIP(hipMemcpyAsync(pin, totals, parts.size() * (nq + 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
   // Each STRING column's input byte range of each part: the worst-case output payload (the write
   // pass finds the exact size by look-back, read back at the end).
-  int32_t* pin_rng = reinterpret_cast<int32_t*>(pin + parts.size());
+  int32_t* pin_rng = reinterpret_cast<int32_t*>(pin + parts.size() * (nq + 1));
   for (size_t i = 0; i < parts.size(); ++i)
     for (int sidx = 0, s2 = 0; s2 < n_select; ++s2) {
       if (fs.width[s2] != 0) continue;
@@ -633,6 +666,9 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
     o.nrows += m;
     o.chunks.push_back(std::move(oc));
   }
+  uint32_t max_sel = 0;
+  for (size_t i = 0; i < parts.size(); ++i) max_sel = std::max(max_sel, pin[parts.size() * nq + i]);
+  const size_t lds_bytes = fs.n_str > 0 ? static_cast<size_t>(2 * kFLdsStr) * max_sel * 4 : 0;
   uint64_t* lb = nullptr;
   unsigned int* tile_ctr = nullptr;
   if (n_select > 0) {
@@ -649,9 +685,9 @@ static int32_t FilterImpl(Table& t, const pxg_program& pred, int32_t n_select, c
     std::memset(&desc.fo, 0, sizeof(desc.fo));
     for (int i = 0; i < fb.n; ++i) desc.fo.out[i] = outs[b0 + i];
     PXG_RETURN_IF_ERROR(Launch(ctx, "filter_desc", FDescCopyKernel, dim3(1), dim3(256), 0, desc, w.gsrc.as<uint64_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_write", FilterWriteKernel, dim3(static_cast<unsigned>(batch_tiles(fb))), dim3(kOpsBlock), 0,
+    PXG_RETURN_IF_ERROR(Launch(ctx, "filter_write", FilterWriteKernel, dim3(static_cast<unsigned>(batch_tiles(fb))), dim3(kOpsBlock), lds_bytes,
                                t.d_chunks.as<const DevChunk>(), d_desc, static_cast<const unsigned long long*>(w.masks.as<unsigned long long>()),
-                               static_cast<const uint32_t*>(fig), T, tile_ctr + b0 / nbatch, lb));
+                               static_cast<const uint32_t*>(fig), T, tile_ctr + b0 / nbatch, lb, max_sel));
   }
   if (fs.n_str > 0 && n_select > 0) {  // exact payload sizes: each part's last inclusive prefix
     uint64_t* pin_out = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(pin_rng + 2 * parts.size() * fs.n_str) + 7) & ~uintptr_t(7));

@@ -9,6 +9,7 @@
 #   pmc    : FETCH_SIZE / WRITE_SIZE passes over the consume kernel (C2) + summary JSON
 #   c3prof : rocprofv3 stats of the C3 leg
 #   diag   : tools/consume_diag.py timing modes (0 production, 2 filter only, 3 keys + hash)
+#   filterpmc: the Filter -> Map leg alone + FETCH_SIZE / WRITE_SIZE passes of its filter kernels
 #   multi2 : bench.py --gpus 2 --share-gpu0 --backend gloo (the N>1 line, both ranks on GPU 0)
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -26,6 +27,11 @@ step() {
     n1only) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n1only -o run --output-format csv -- python3 tools/n1_prof.py 3 > gpurun_out/prof_n1only.log 2>&1 ;;
     c3prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 tools/c3_prof.py > gpurun_out/prof_c3.log 2>&1 ;;
     diag) timeout -k 10 300 python3 tools/consume_diag.py 0 2 3 > gpurun_out/diag.log 2>&1 ;;
+    filterpmc) timeout -k 10 200 python3 tools/ops_bench.py > gpurun_out/ops_bench.json 2> gpurun_out/ops_bench.err &&
+         timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fpmc_fetch -o run --output-format csv -- python3 tools/ops_bench.py > gpurun_out/fpmc_fetch.log 2>&1 &&
+         timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/fpmc_write -o run --output-format csv -- python3 tools/ops_bench.py > gpurun_out/fpmc_write.log 2>&1 &&
+         python3 tools/pmc_summary.py --kernel FilterWriteKernel --name filter_write --rows 100000000 --fetch gpurun_out/fpmc_fetch --write gpurun_out/fpmc_write --out gpurun_out/fpmc_write.json > /dev/null 2>&1 &&
+         python3 tools/pmc_summary.py --kernel FilterCountKernel --name filter_count --rows 100000000 --fetch gpurun_out/fpmc_fetch --write gpurun_out/fpmc_write --out gpurun_out/fpmc_count.json > /dev/null 2>&1 ;;
     multi2) timeout -k 10 400 python3 -u bench.py --gpus 2 --share-gpu0 --backend gloo --steps 3 --warmup 1 > gpurun_out/bench_multi2.json 2> gpurun_out/bench_multi2.err ;;
     *) echo "unknown mode $1" >&2; return 2 ;;
   esac
