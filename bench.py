@@ -683,6 +683,9 @@ def filter_map_leg(ctx, table, n, P, reps=5):
     kms = {k: ctx.kernel_stats(k)[1] / reps for k in names if ctx.kernel_stats(k)[0]}
     filt_ms = sum(v for k, v in kms.items() if k.startswith("filter"))
     alg = 8 * n + 2 * kept_bytes
+    # SURVEY.md §8d's definition (the one agg_consume is priced by): every referenced input column
+    # once in Arrow layout, plus the kept rows written.
+    cols_bytes = 8 * n + table.device_bytes(P.HE["service"]) + table.device_bytes(P.HE["req_path"]) + 8 * n + kept_bytes
     return {"workload": "Filter(resp_status>=400; service, req_path, latency) -> Map(service, req_path, latency/1e6) "
                         "over the HBM table (pxg_filter + pxg_map, non-fused operators)",
             "rows": n, "kept_rows": kept, "ms_per_query_wall": wall * 1000.0, "rows_per_s": n / wall,
@@ -690,7 +693,13 @@ def filter_map_leg(ctx, table, n, P, reps=5):
             "roofline": {"bound": "hbm", "kernels": "filter_count + filter_scan + filter_write",
                          "algorithmic_bytes": alg, "achieved": alg / (filt_ms / 1000.0) / 1e9 if filt_ms else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alg / (filt_ms / 1000.0) / 1e9 / HBM_PEAK_GBS if filt_ms else None}}
+                         "frac": alg / (filt_ms / 1000.0) / 1e9 / HBM_PEAK_GBS if filt_ms else None,
+                         "algorithmic_bytes_input_columns": cols_bytes,
+                         "frac_input_columns": cols_bytes / (filt_ms / 1000.0) / 1e9 / HBM_PEAK_GBS if filt_ms else None,
+                         "bytes_note": "frac counts the predicate column and the kept rows read + written once; a 12%-selective "
+                                       "gather touches most 128-byte lines of every gathered column, so the measured traffic "
+                                       "(profiles/r05_filter_pmc.json) is ~2.5x that; frac_input_columns uses SURVEY.md §8d's "
+                                       "definition (every referenced input column once + the output), as agg_consume does"}}
 
 
 def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
