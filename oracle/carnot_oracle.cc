@@ -1644,6 +1644,38 @@ extern "C" void oracle_tdigest_batch_quantiles(int32_t nparts, const int32_t* ki
   for (int i = 0; i < 7; ++i) out7[i] = out.quantile(qs[i]);
 }
 
+// As oracle_tdigest_batch_quantiles, with every centroid-list part carrying its rank's true
+// min / max (mins[p], maxs[p]) into the merged digest (math_sketches.h:38 merge; the carried
+// reading).
+extern "C" void oracle_tdigest_batch_quantiles_mm(int32_t nparts, const int32_t* kind, const int64_t* counts, const double* data,
+                                                  const double* weights, const double* mins, const double* maxs, double* out7) {
+  std::vector<TDigest> parts;
+  parts.reserve(static_cast<size_t>(nparts));
+  int64_t at = 0;
+  double lo = std::numeric_limits<double>::infinity(), hi = -std::numeric_limits<double>::infinity();
+  for (int32_t p = 0; p < nparts; ++p) {
+    const int64_t c = counts[p];
+    if (kind[p] == 0) {
+      parts.push_back(TDigest::Unprocessed(std::vector<double>(data + at, data + at + c), 1000));
+    } else {
+      std::vector<Centroid> cs;
+      for (int64_t i = 0; i < c; ++i) cs.emplace_back(data[at + i], weights[at + i]);
+      parts.push_back(TDigest::FromCentroids(cs, 1000, mins[p], maxs[p]));
+      if (c > 0) {
+        lo = std::min(lo, mins[p]);
+        hi = std::max(hi, maxs[p]);
+      }
+    }
+    at += c;
+  }
+  std::vector<const TDigest*> batch;
+  for (const auto& d : parts) batch.push_back(&d);
+  TDigest out(1000);
+  out.merge_batch(batch);
+  out.carry_extremes(lo, hi);
+  for (int i = 0; i < 7; ++i) out7[i] = out.quantile(kQs[i]);
+}
+
 extern "C" void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb, double* out7) {
   TDigest d1(1000), d2(1000);
   for (int64_t i = 0; i < na; ++i) d1.add(a[i]);

@@ -82,6 +82,9 @@ void oracle_tdigest_centroids(const double* vals, int64_t n, double* means, doub
  * data, weights in weights), all concatenated in part order. */
 void oracle_tdigest_batch_quantiles(int32_t nparts, const int32_t* kind, const int64_t* counts, const double* data,
                                     const double* weights, double* out7);
+/* The same, with centroid-list part i carrying its rank's true extremes mins[i] / maxs[i]. */
+void oracle_tdigest_batch_quantiles_mm(int32_t nparts, const int32_t* kind, const int64_t* counts, const double* data,
+                                       const double* weights, const double* mins, const double* maxs, double* out7);
 void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb,
                                     double* out7);
 // The JSON string QuantilesUDA::Finalize would produce (rapidjson Writer bytes, json_double.h).

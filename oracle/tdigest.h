@@ -110,6 +110,25 @@ class TDigest {
     d.UpdateCumulative();
     return d;
   }
+  // The same list carrying the shipping rank's true extremes (the min / max of the values it
+  // added, as the incremental digest on that rank tracks them).  The published merge
+  // (MergeProcessed below) never reads another digest's min_ / max_, and the 7 quantiles read the
+  // merged min_ / max_ only when the first / last centroid holds >= 2% of the weight (W <= 50 for
+  // delta = 1000): tests/test_digest_minmax.py checks both forms agree bit for bit.
+  static TDigest FromCentroids(const std::vector<Centroid>& cs, double compression, double true_min, double true_max) {
+    TDigest d = FromCentroids(cs, compression);
+    if (!cs.empty()) {
+      d.min_ = std::min(d.min_, true_min);
+      d.max_ = std::max(d.max_, true_max);
+    }
+    return d;
+  }
+  // A merged digest whose min_ / max_ are then set to the given extremes (the "carried" reading
+  // of merge(&other)): min_ = min(min_, lo), max_ = max(max_, hi).
+  void carry_extremes(double lo, double hi) {
+    min_ = std::min(min_, lo);
+    max_ = std::max(max_, hi);
+  }
   // add(first, last) of the merging digest: a whole batch of digests merged at once (one k-way
   // merge of their processed centroids, their unprocessed ones appended, process when dirty).
   void merge_batch(const std::vector<const TDigest*>& batch) {

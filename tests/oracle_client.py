@@ -60,6 +60,9 @@ def load():
                                              C.c_int64, C.POINTER(C.c_int64)]
     lib.oracle_tdigest_batch_quantiles.argtypes = [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double),
                                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.oracle_tdigest_batch_quantiles_mm.argtypes = [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                                      C.POINTER(C.c_double)]
     lib.oracle_quantiles_json.argtypes = [C.POINTER(C.c_double), C.c_int64, C.c_char_p, C.c_int32]
     lib.oracle_quantiles_json.restype = C.c_int32
     lib.oracle_pluck_float64.argtypes = [C.c_char_p, C.c_char_p]
@@ -219,9 +222,10 @@ def tdigest_centroids(vals, cap: int = 8192):
     return m[:nc.value].copy(), w[:nc.value].copy()
 
 
-def tdigest_batch_quantiles(parts) -> List[float]:
+def tdigest_batch_quantiles(parts, extremes=None) -> List[float]:
     """TDigest::merge_batch over parts = [("raw", values) | ("centroids", (means, weights))], then
-    quantile() x7."""
+    quantile() x7.  extremes: per part (true_min, true_max) carried with a centroid list into the
+    merged digest (oracle_tdigest_batch_quantiles_mm), None = min / max from the centroid means."""
     lib = load()
     kinds, counts, data, weights = [], [], [], []
     for kind, payload in parts:
@@ -242,6 +246,13 @@ def tdigest_batch_quantiles(parts) -> List[float]:
     d = np.ascontiguousarray(np.concatenate(data) if data else np.zeros(0))
     w = np.ascontiguousarray(np.concatenate(weights) if weights else np.zeros(0))
     out = (C.c_double * 7)()
+    if extremes is not None:
+        lo = np.ascontiguousarray([e[0] if e else np.inf for e in extremes], np.float64)
+        hi = np.ascontiguousarray([e[1] if e else -np.inf for e in extremes], np.float64)
+        lib.oracle_tdigest_batch_quantiles_mm(len(k), k.ctypes.data_as(C.POINTER(C.c_int32)), c.ctypes.data_as(C.POINTER(C.c_int64)),
+                                              d.ctypes.data_as(C.POINTER(C.c_double)), w.ctypes.data_as(C.POINTER(C.c_double)),
+                                              lo.ctypes.data_as(C.POINTER(C.c_double)), hi.ctypes.data_as(C.POINTER(C.c_double)), out)
+        return list(out)
     lib.oracle_tdigest_batch_quantiles(len(k), k.ctypes.data_as(C.POINTER(C.c_int32)), c.ctypes.data_as(C.POINTER(C.c_int64)),
                                        d.ctypes.data_as(C.POINTER(C.c_double)), w.ctypes.data_as(C.POINTER(C.c_double)), out)
     return list(out)

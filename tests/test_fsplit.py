@@ -1,5 +1,5 @@
 """The fused split (pixie_amd/csrc/pxg_finalize.hip FsHistKernel / FsScatterKernel): the largest
-groups by a sample get their own bucket in a 10-bit first radix pass, the rest records are
+groups by a sample get their own bucket in a 9-bit first radix pass, the rest records are
 sorted by their low digit in the same pass and by the higher digits after it.  Both this and the
 plain radix sort are stable sorts of the same staging, so the grouped value streams -- and every
 result, means and big-group quantiles included -- are bit-identical between them (forced on and
@@ -49,7 +49,7 @@ def test_fused_split_bit_identical_to_radix(ctx, monkeypatch, rows):
 
 
 def test_fused_split_every_group_designated_or_rest(ctx, monkeypatch):
-    """1024 groups (group by req_path): up to 767 designated, the rest needs one more pass."""
+    """1024 groups (group by req_path): up to 255 designated, the rest needs one more pass."""
     cols = datagen_http_events(SEED, 0, 2_000_000, threads=8)
     types = P.HTTP_TYPES
     plan = P.linear_plan([P.source_op("http_events", types, P.HTTP_NAMES, list(range(len(types)))),
