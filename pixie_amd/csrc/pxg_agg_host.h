@@ -183,6 +183,11 @@ struct Agg {
   int32_t ImportPartials(const void* src, int32_t n, const int64_t* offs, const int64_t* sizes);
   // Exchange v2 (partial UDA states, pxg_partial.hip).
   int32_t ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
+  int32_t ExportGroupV2(int32_t n_parts);
+  int32_t CheckExportFinalize(const uint8_t* meta_copy) const;
+  // pxg_agg_alltoall's export: parts laid out on the device (no host wait); per part its aligned
+  // bytes to seg_dev[p] and its header to hdr_dev + 64 p.
+  int32_t ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, uint8_t* hdr_dev);
   int32_t ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* offs, const int64_t* sizes, const void* hdrs);
 };
 

@@ -8,10 +8,12 @@
 // pxg_partial.hip), exchange per peer one record of {part bytes, part header} (grouped
 // ncclSend / ncclRecv), exchange the parts (all-to-all(v) as grouped ncclSend / ncclRecv of
 // bytes), merge what arrived (ImportPartialsV2 with the received headers).  Every RCCL call is
-// enqueued on the ctx stream.  Host waits per call: the export's sizes, the export's write, the
-// {bytes, header} records, the import's insert count and error flags (4; plus one when the merge
-// accumulators or the group table must grow).  A high-cardinality run first moves its partition
-// records into the table (SpillHc).
+// enqueued on the ctx stream.  The v2 parts are laid out on the device, so the host waits twice
+// per call (AlltoallV2): once for every size and header after the {bytes, header} records have
+// crossed, once for the import's insert count and error flags (plus the export finalize's
+// class-count wait when the plan has quantiles, and one more when the merge accumulators or the
+// group table must grow).  A high-cardinality run first moves its partition records into the
+// table (SpillHc).
 #include <cstddef>
 #include <rccl/rccl.h>
 
@@ -92,6 +94,89 @@ extern "C" int32_t pxg_comm_destroy(pxg_comm* comm) {
   return PXG_OK;
 }
 
+namespace pxg {
+
+// Exchange v2 (partial states, pxg_partial.hip): the parts are laid out and written on the device
+// (ExportPartialDev), so the host first learns any size after the {bytes, header} records have
+// crossed: one wait for every size and header (plus the export finalize's deferred checks),
+// then the parts, then the import's one wait.  (An export finalize over quantiles also waits
+// once inside, for its class counts.)
+static int32_t AlltoallV2(pxg_agg* agg, Comm& C, int64_t* bytes_sent, int64_t* bytes_recv) {
+  Agg& a = agg->impl;
+  Ctx* ctx = a.ctx;
+  const int32_t n = C.nranks;
+  const size_t hb = XHeaderBytes();
+  // counts: [n] own part bytes, [n] received bytes, [n * hb] received headers, [n * hb] own headers
+  PXG_RETURN_IF_ERROR(C.counts.Ensure(static_cast<size_t>(n) * (16 + 2 * hb) + 64));
+  int64_t* d_send_cnt = C.counts.as<int64_t>();
+  int64_t* d_recv_cnt = d_send_cnt + n;
+  uint8_t* d_recv_hdr = reinterpret_cast<uint8_t*>(d_recv_cnt + n);
+  uint8_t* d_send_hdr = d_recv_hdr + static_cast<size_t>(n) * hb;
+  uint8_t* pin8 = static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps;
+  const size_t back = static_cast<size_t>(n) * (16 + hb);
+  if (back + 64 > Ctx::kPinnedBytes - Ctx::kPinnedOps) return SetError(PXG_UNIMPLEMENTED, "%d ranks", n);
+  PXG_RETURN_IF_ERROR(a.ExportPartialDev(n, &C.send, d_send_cnt, d_send_hdr));
+  {
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    for (int p = 0; p < n; ++p) {
+      PXG_NCCL(ncclSend(d_send_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+      PXG_NCCL(ncclRecv(d_recv_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+      PXG_NCCL(ncclSend(d_send_hdr + p * hb, hb, ncclUint8, p, C.nccl, ctx->stream));
+      PXG_NCCL(ncclRecv(d_recv_hdr + p * hb, hb, ncclUint8, p, C.nccl, ctx->stream));
+    }
+    PXG_RETURN_IF_ERROR(grp.End());
+  }
+  // The one wait before the parts move: own sizes, received sizes and headers, finalize checks.
+  PXG_HIP(hipMemcpyAsync(pin8, d_send_cnt, back, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipMemcpyAsync(pin8 + back, a.ws.meta.p, 24, hipMemcpyDeviceToHost, ctx->stream));
+  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  PXG_RETURN_IF_ERROR(a.CheckExportFinalize(pin8 + back));
+  const int64_t* pin = reinterpret_cast<const int64_t*>(pin8);
+  std::vector<int64_t> seg(pin, pin + n), rs(pin + n, pin + 2 * n);
+  std::vector<uint8_t> rhdr(pin8 + 16 * n, pin8 + 16 * n + n * hb);
+  int64_t total = 0, rtotal = 0;
+  for (int p = 0; p < n; ++p) {
+    if (seg[p] < 0 || rs[p] < 0) return SetError(PXG_INTERNAL, "part sizes %lld / %lld", static_cast<long long>(seg[p]), static_cast<long long>(rs[p]));
+    total += seg[p];
+    rtotal += rs[p];
+  }
+  if (static_cast<uint64_t>(total) > C.send.bytes) return SetError(PXG_INTERNAL, "export wrote %lld bytes past its bound", static_cast<long long>(total));
+  PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(rtotal) + 64));
+  {
+    NcclGroup grp;
+    PXG_RETURN_IF_ERROR(grp.Start());
+    int64_t so = 0, ro = 0;
+    for (int p = 0; p < n; ++p) {
+      if (seg[p] > 0) PXG_NCCL(ncclSend(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), ncclUint8, p, C.nccl, ctx->stream));
+      if (rs[p] > 0) PXG_NCCL(ncclRecv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), ncclUint8, p, C.nccl, ctx->stream));
+      so += seg[p];
+      ro += rs[p];
+    }
+    PXG_RETURN_IF_ERROR(grp.End());
+  }
+  // Every group this rank exported now lives on its owner (as in the v1 path below).
+  PXG_RETURN_IF_ERROR(pxg_agg_reset(agg));
+  std::vector<int64_t> poffs, psizes;
+  std::vector<uint8_t> phdr;
+  int64_t at = 0;
+  for (int p = 0; p < n; ++p) {
+    if (rs[p] > 0) {
+      poffs.push_back(at);
+      psizes.push_back(rs[p]);
+      phdr.insert(phdr.end(), rhdr.begin() + p * hb, rhdr.begin() + (p + 1) * hb);
+    }
+    at += rs[p];
+  }
+  if (!poffs.empty())
+    PXG_RETURN_IF_ERROR(a.ImportPartialsV2(C.recv.as<const uint8_t>(), static_cast<int32_t>(poffs.size()), poffs.data(), psizes.data(), phdr.data()));
+  if (bytes_sent) *bytes_sent = total;
+  if (bytes_recv) *bytes_recv = rtotal;
+  return PXG_OK;
+}
+
+}  // namespace pxg
+
 extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes_sent, int64_t* bytes_recv) {
   if (!agg || !comm) return SetError(PXG_INVALID_ARGUMENT, "bad pxg_agg_alltoall arguments");
   Comm& C = comm->impl;
@@ -99,10 +184,11 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   Ctx* ctx = a.ctx;
   if (ctx != C.ctx) return SetError(PXG_INVALID_ARGUMENT, "aggregation and communicator belong to different contexts");
   const int32_t n = C.nranks;
-  // 1. Sizes of the n parts, then the parts themselves.
-  std::vector<int64_t> offs(n), bytes(n), seg(n);
   PXG_RETURN_IF_ERROR(a.SpillHc());
-  const bool v2 = ExchangeV2(a);
+  if (ExchangeV2(a)) return AlltoallV2(agg, C, bytes_sent, bytes_recv);
+  // Exchange v1 (PXG_XCHG_V1=1, row parts): sizes of the n parts, then the parts themselves.
+  std::vector<int64_t> offs(n), bytes(n), seg(n);
+  const bool v2 = false;
   auto do_export = [&](void* dst, int64_t cap) {
     return v2 ? a.ExportPartialV2(n, dst, cap, offs.data(), bytes.data()) : a.ExportPartial(n, dst, cap, offs.data(), bytes.data());
   };

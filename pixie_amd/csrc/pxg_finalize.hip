@@ -3405,6 +3405,7 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_HIP(hipMemcpyAsync(d_ngroups, d_ftotal, 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
 
+  clk.Mark("finalize: dense ids");
   // Group keys out of the arena, on side stream 2 while the radix sort runs on the main
   // stream (ConvertAggHashMapToRowBatch group columns, agg_node.cc:303-349).  String payloads
   // are sized by the arena (an upper bound), so no count comes back to the host first.  Side
@@ -3463,15 +3464,15 @@ int32_t AggFinalizeTable(Agg* a) {
             o.data = static_cast<uint8_t*>(ResultAlloc(static_cast<size_t>(a->arena_words) * 8 + 16));
             ok = o.offsets && o.data;
             if (ok) {
-              PXG_HIP(hipMemcpyAsync(o.offsets, R.key_offsets[k].p, (static_cast<size_t>(ngroups) + 1) * 4, hipMemcpyDeviceToHost, ctx->side2));
+              PXG_RETURN_IF_ERROR(CopyD2H(ctx, ctx->side2, o.offsets, R.key_offsets[k].p, (static_cast<size_t>(ngroups) + 1) * 4));
               if (a->arena_words > 0)
-                PXG_HIP(hipMemcpyAsync(o.data, R.key_data[k].p, static_cast<size_t>(a->arena_words) * 8, hipMemcpyDeviceToHost, ctx->side2));
+                PXG_RETURN_IF_ERROR(CopyD2H(ctx, ctx->side2, o.data, R.key_data[k].p, static_cast<size_t>(a->arena_words) * 8));
             }
           } else {
             const size_t w = o.type == PXG_BOOLEAN ? 1 : TypeWidth(o.type);
             o.values = ResultAlloc(std::max<size_t>(static_cast<size_t>(ngroups) * w, 1));
             ok = o.values != nullptr;
-            if (ok) PXG_HIP(hipMemcpyAsync(o.values, R.key_fixed[k].p, static_cast<size_t>(ngroups) * w, hipMemcpyDeviceToHost, ctx->side2));
+            if (ok) PXG_RETURN_IF_ERROR(CopyD2H(ctx, ctx->side2, o.values, R.key_fixed[k].p, static_cast<size_t>(ngroups) * w));
           }
         }
         a->early.keys = ok;
@@ -3620,6 +3621,7 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", SplitGstartKernel, dim3((kSplitMaxBig + 256) / 256), dim3(256), 0,
                                static_cast<const uint32_t*>(base), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
   }
+  clk.Mark("finalize: grouping issued");
   // 3. UDA reductions (chunk partials, then per-group combine).
   const ConstValPtrs cv = vin;
   UdaOut uo;
@@ -3641,8 +3643,10 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_RETURN_IF_ERROR(Launch(ctx, "group_chunk_count", GroupChunkCountKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
                                ngroups, cbase));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
+    clk.Mark("finalize: red chunk scan");
     PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 2 * 8));
     PXG_RETURN_IF_ERROR(ws.cgroup.Ensure(max_chunks * 4 + 16));
+    clk.Mark("finalize: red ensure");
     PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(static_cast<unsigned>((max_chunks + 255) / 256)), dim3(256), 0,
                                static_cast<const uint32_t*>(cbase), ngroups, ws.cgroup.as<uint32_t>(), static_cast<uint32_t>(max_chunks)));
     if (n < 32 * static_cast<uint64_t>(ngroups)) {  // groups average < 32 rows: a thread per chunk
@@ -3668,6 +3672,7 @@ int32_t AggFinalizeTable(Agg* a) {
   PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
                              cplan, gstart, static_cast<const uint32_t*>(cbase), ngroups,
                              ws.partial.as<const uint64_t>(), max_chunks, uo, states));
+  clk.Mark("finalize: red kernels");
   if (a->early.want && !states && !a->merged && !a->export_x) {  // early result: the combined values
     bool ok = true;
     for (int u = 0; u < a->n_udas && ok; ++u) {
@@ -3679,7 +3684,7 @@ int32_t AggFinalizeTable(Agg* a) {
       if (a->early.skip && a->early.skip[a->n_keys + u]) continue;
       o.values = ResultAlloc(std::max<size_t>(static_cast<size_t>(ngroups) * 8, 8));
       ok = o.values != nullptr;
-      if (ok) PXG_HIP(hipMemcpyAsync(o.values, R.uda_out[u].p, static_cast<size_t>(ngroups) * 8, hipMemcpyDeviceToHost, ctx->stream));
+      if (ok) PXG_RETURN_IF_ERROR(CopyD2H(ctx, ctx->stream, o.values, R.uda_out[u].p, static_cast<size_t>(ngroups) * 8));
     }
     a->early.vals = ok;
   }
@@ -3820,6 +3825,7 @@ int32_t AggFinalizeTable(Agg* a) {
                                d_bigmeta, large_list, large_cnt));
     // Class counts + big-group metadata to pinned memory right away; the host waits on this
     // event only, while the digests below keep the GPU busy.
+    clk.Mark("finalize: classes issued");
     uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
     PXG_HIP(hipMemcpyAsync(pin + 64, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
     PXG_HIP(hipEventRecord(ctx->ev_meta, ctx->stream));
@@ -3829,6 +3835,7 @@ int32_t AggFinalizeTable(Agg* a) {
     const uint32_t big_cap32 = static_cast<uint32_t>(std::min<uint64_t>(ngroups, big_cap));
     const uint32_t n_chain_cap = big_cap32;  // mid groups read the per-context table
     PXG_RETURN_IF_ERROR(EnsureMidChains(ctx));
+    clk.Mark("finalize: mid chains ready");
     PXG_RETURN_IF_ERROR(ws.chain_nc.Ensure(static_cast<size_t>(n_chain_cap) * 4));
     PXG_RETURN_IF_ERROR(ws.chain_starts.Ensure(static_cast<size_t>(n_chain_cap) * kChainCap * 4));
     const uint32_t* chain_starts = ws.chain_starts.as<const uint32_t>();
@@ -3851,7 +3858,9 @@ int32_t AggFinalizeTable(Agg* a) {
                                    dim3(256), 0, lists + static_cast<uint64_t>(ngroups), static_cast<const uint32_t*>(d_cls + 1), gstart,
                                    cv.p[a->uda_val[u]], a->uda_arg_type[u], R.uda_out[u].as<double>()));
     }
+    clk.Mark("finalize: chains + small issued");
     PXG_RETURN_IF_ERROR(RunReductions());
+    clk.Mark("finalize: reductions issued");
     for (int u = 0; u < a->n_udas && !a->export_x; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
@@ -3911,6 +3920,17 @@ int32_t AggFinalizeTable(Agg* a) {
   guard.side = false;
   if (keys_on_side2 || n_big_groups > 0) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
   guard.side2 = false;
+  if (a->export_x) {
+    // An export reads neither the string-key totals nor the result columns: its caller checks
+    // the error flag and the device group count (ws.meta) with the readback it waits for anyway
+    // (Agg::CheckExportFinalize), so the export finalize ends without a host wait of its own.
+    a->x_vals = a->x_qval >= 0 ? cv.p[a->x_qval] : nullptr;
+    a->x_wts = nullptr;
+    a->x_nbig = n_big_groups;
+    a->last_big_sort_groups = n_big_groups;
+    R.ready = true;
+    return PXG_OK;
+  }
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;
@@ -4047,8 +4067,8 @@ extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t la
   uint8_t* d_fin = reinterpret_cast<uint8_t*>(d_out + G * nsel);
   PXG_RETURN_IF_ERROR(Launch(a.ctx, "quant_lanes", QuantLanesKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
                              a.res.uda_out[uda].as<const double>(), G, lane_mask, nsel, d_out, d_fin));
-  if (nsel) PXG_HIP(hipMemcpyAsync(host_out, d_out, G * nsel * 8, hipMemcpyDeviceToHost, a.ctx->stream));
-  PXG_HIP(hipMemcpyAsync(host_finite, d_fin, G, hipMemcpyDeviceToHost, a.ctx->stream));
+  if (nsel) PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, host_out, d_out, G * nsel * 8));
+  PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, host_finite, d_fin, G));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
   return PXG_OK;
 }
@@ -4096,7 +4116,7 @@ extern "C" int32_t pxg_agg_finalize_result(pxg_agg* agg, int64_t* n_groups, pxg_
       pxg_result_free(cols, n_cols);
       return SetError(PXG_RESOURCE_UNAVAILABLE, "host result allocation failed");
     }
-    PXG_HIP(hipMemcpyAsync(o.values, a.res.uda_out[u].p, static_cast<size_t>(G) * 56, hipMemcpyDeviceToHost, a.ctx->stream));
+    PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.values, a.res.uda_out[u].p, static_cast<size_t>(G) * 56));
     q = true;
   }
   if (q) PXG_HIP(hipStreamSynchronize(a.ctx->stream));
@@ -4169,8 +4189,8 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
       o.data = static_cast<uint8_t*>(ResultAlloc(a.res.key_data_len[k] + 16));
       o.data_len = a.res.key_data_len[k];
       if (G > 0) {
-        PXG_HIP(hipMemcpyAsync(o.offsets, a.res.key_offsets[k].p, (G + 1) * 4, hipMemcpyDeviceToHost, a.ctx->stream));
-        PXG_HIP(hipMemcpyAsync(o.data, a.res.key_data[k].p, o.data_len, hipMemcpyDeviceToHost, a.ctx->stream));
+        PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.offsets, a.res.key_offsets[k].p, (G + 1) * 4));
+        PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.data, a.res.key_data[k].p, o.data_len));
       } else {
         o.offsets[0] = 0;
       }
@@ -4179,9 +4199,9 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
       o.values = ResultAlloc(std::max<size_t>(rows * w, 1));
       if (G > 0) {
         if (o.type == PXG_BOOLEAN) {
-          PXG_HIP(hipMemcpyAsync(o.values, a.res.key_fixed[k].p, G, hipMemcpyDeviceToHost, a.ctx->stream));
+          PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.values, a.res.key_fixed[k].p, G));
         } else {
-          PXG_HIP(hipMemcpyAsync(o.values, a.res.key_fixed[k].p, G * w, hipMemcpyDeviceToHost, a.ctx->stream));
+          PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.values, a.res.key_fixed[k].p, G * w));
         }
       }
     }
@@ -4196,7 +4216,7 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
     o.data_len = rows * rec;
     for (int64_t g = 0; g <= rows; ++g) o.offsets[g] = static_cast<int32_t>(g * rec);
     if (!synth) {
-      if (G > 0 && rec > 0) PXG_HIP(hipMemcpyAsync(o.data, a.res.states.p, G * rec, hipMemcpyDeviceToHost, a.ctx->stream));
+      if (G > 0 && rec > 0) PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.data, a.res.states.p, G * rec));
     } else {
       // Initial states serialized (no-groups agg over zero rows): Mean {0, 0.0}, the rest as
       // their initial value.
@@ -4222,7 +4242,7 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
     const size_t per = q ? 56 : 8;
     o.values = ResultAlloc(std::max<size_t>(rows * per, 8));
     if (!synth) {
-      PXG_HIP(hipMemcpyAsync(o.values, a.res.uda_out[u].p, G * per, hipMemcpyDeviceToHost, a.ctx->stream));
+      PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.values, a.res.uda_out[u].p, G * per));
       continue;
     }
     // Initial UDA states finalized (AggNode no-groups emit over zero rows, agg_node.cc:182-207).

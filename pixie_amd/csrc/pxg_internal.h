@@ -314,6 +314,10 @@ int32_t NewTable(Ctx* ctx, int32_t ncols, const int32_t* types, pxg_table** out)
 // pool blocks, reused across results.
 void* ResultAlloc(size_t n);
 void ResultFree(void* p);
+// Device -> host copy on `stream` (stream-ordered): into a block of the pinned result pool (up
+// to kCopyKernelMaxBytes) by a copy kernel, otherwise hipMemcpyAsync.
+constexpr size_t kCopyKernelMaxBytes = size_t(8) << 20;
+int32_t CopyD2H(Ctx* ctx, hipStream_t stream, void* host, const void* dev, size_t n);
 }
 
 struct pxg_ctx {

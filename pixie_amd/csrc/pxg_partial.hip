@@ -73,7 +73,7 @@ static bool IsXPart(const void* hdr_host) {
 }
 
 
-static inline uint64_t Align8(uint64_t x) { return (x + 7) & ~uint64_t(7); }
+__host__ __device__ static inline uint64_t Align8(uint64_t x) { return (x + 7) & ~uint64_t(7); }
 
 struct PartLayout {
   uint64_t koff, keys, gid, vals, bytes;
@@ -589,7 +589,7 @@ constexpr uint64_t kXCentFlag = uint64_t(1) << 63;
 struct XLayout {
   uint64_t koff, keys, states, gofs, items, bytes;
 };
-static XLayout XLayoutOf(uint64_t ng, uint64_t nw, uint64_t kw, uint64_t srec, bool has_q) {
+__host__ __device__ static XLayout XLayoutOf(uint64_t ng, uint64_t nw, uint64_t kw, uint64_t srec, bool has_q) {
   XLayout L;
   L.koff = sizeof(XHeader);
   L.keys = L.koff + ng * 8;
@@ -883,13 +883,27 @@ __global__ void XPartBoundsKernel(const uint64_t* __restrict__ gstarts, int n_pa
   out[2 * (n_parts + 1) + p] = ioff_j[j];
 }
 
-int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes) {
+// The export finalize's deferred checks (AggFinalizeTable ends an export without a host wait):
+// `m` holds a host copy of ws.meta's first 24 bytes, taken after the stream passed the export.
+int32_t Agg::CheckExportFinalize(const uint8_t* m) const {
+  uint32_t g_dev = 0, err = 0;
+  std::memcpy(&g_dev, m + 8, 4);
+  std::memcpy(&err, m + 16, 4);
+  if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
+  if (g_dev != static_cast<uint32_t>(res.n_groups))
+    return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, static_cast<uint32_t>(res.n_groups));
+  return PXG_OK;
+}
+
+// Export grouping (no host wait; the finalize waits once for its class counts when the plan has
+// quantiles): the local finalize in export mode, each group's part, key-record words and items,
+// the groups in part order, and per part (+ total) the group / key-word / item starts at
+// xc.starts + kPartBuckets + 1 (device).
+int32_t Agg::ExportGroupV2(int32_t n_parts) {
   ExportCache& X = xc;
-  if (merged) return SetError(PXG_FAILED_PRECONDITION, "an aggregation that merged imported states cannot be exported again");
+  X.valid = false;
   const bool has_q = x_qval >= 0;
-  const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
-  if (!(X.valid && X.v2 && X.n_parts == n_parts && X.version == state_version)) {
-    X.valid = false;
+  {
     // 1. The local finalize in export mode: grouping, per-group states, big groups' centroid lists.
     export_x = true;
     const int32_t rc = AggFinalizeTable(this);
@@ -940,12 +954,27 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
     PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XPartBoundsKernel, dim3(1), dim3(kPartBuckets + 1), 0,
                                static_cast<const uint64_t*>(gstarts), n_parts, static_cast<const uint64_t*>(koff_j),
                                static_cast<const uint64_t*>(ioff_j), bounds));
-    std::vector<uint64_t> hb(3 * (n_parts + 1));
-    PXG_HIP(hipMemcpyAsync(hb.data(), bounds, hb.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  return PXG_OK;
+}
+
+int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes) {
+  ExportCache& X = xc;
+  if (merged) return SetError(PXG_FAILED_PRECONDITION, "an aggregation that merged imported states cannot be exported again");
+  const bool has_q = x_qval >= 0;
+  const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
+  if (!(X.valid && X.v2 && X.n_parts == n_parts && X.version == state_version)) {
+    PXG_RETURN_IF_ERROR(ExportGroupV2(n_parts));
+    const uint64_t* bounds = X.starts.as<const uint64_t>() + kPartBuckets + 1;
+    // Part bounds and the finalize's deferred checks in one readback.
+    std::vector<uint64_t> hb(3 * (n_parts + 1) + 3);
+    PXG_HIP(hipMemcpyAsync(hb.data(), bounds, 3 * (n_parts + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    PXG_HIP(hipMemcpyAsync(hb.data() + 3 * (n_parts + 1), ws.meta.p, 24, hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));
+    PXG_RETURN_IF_ERROR(CheckExportFinalize(reinterpret_cast<const uint8_t*>(hb.data() + 3 * (n_parts + 1))));
     X.g_start.assign(hb.begin(), hb.begin() + n_parts + 1);
     X.k_start.assign(hb.begin() + n_parts + 1, hb.begin() + 2 * (n_parts + 1));
-    X.r_start.assign(hb.begin() + 2 * (n_parts + 1), hb.end());
+    X.r_start.assign(hb.begin() + 2 * (n_parts + 1), hb.begin() + 3 * (n_parts + 1));
     X.n_parts = n_parts;
     X.version = state_version;
     X.v2 = true;
@@ -1013,6 +1042,105 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
   return PXG_OK;
 }
 
+
+// The layout ExportPartialV2 computes on the host, on the device: one thread walks the parts
+// (<= kPartBuckets) from the device bounds, writes the descriptor XWriteGroupsKernel reads, each
+// part's header (into the part and into hdr_out), and each part's aligned byte count.
+struct XHdrConst {
+  uint32_t n_keys, srec;
+  uint64_t plan_sig;
+  int32_t has_q;
+};
+__global__ void XLayoutDevKernel(const uint64_t* __restrict__ bounds, int32_t n_parts, XHdrConst hc, uint8_t* __restrict__ base,
+                                 uint64_t* __restrict__ desc, int64_t* __restrict__ seg_out, uint8_t* __restrict__ hdr_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t* g_start = bounds;
+  const uint64_t* k_start = bounds + n_parts + 1;
+  const uint64_t* r_start = bounds + 2 * (n_parts + 1);
+  uint64_t* poff = desc;
+  uint64_t* lay = desc + n_parts;
+  uint64_t* nit = lay + 6 * n_parts;
+  uint64_t off = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    const uint64_t ng = g_start[p + 1] - g_start[p];
+    const uint64_t ni = (r_start[p + 1] >> kXItemShift) - (r_start[p] >> kXItemShift);
+    const uint64_t nw = (r_start[p + 1] & 0xFFFFFFFFu) - (r_start[p] & 0xFFFFFFFFu);
+    const uint64_t kwp = k_start[p + 1] - k_start[p];
+    const XLayout L = XLayoutOf(ng, nw, kwp, hc.srec, hc.has_q != 0);
+    XHeader H;
+    __builtin_memset(&H, 0, sizeof(H));
+    H.magic = kXMagic;
+    H.version = kXVersion;
+    H.n_keys = hc.n_keys;
+    H.state_rec = hc.srec;
+    H.n_groups = ng;
+    H.n_items = ni;
+    H.key_words = kwp;
+    H.plan_sig = hc.plan_sig;
+    H.has_q = hc.has_q ? 1 : 0;
+    H.item_words = nw;
+    poff[p] = off;
+    lay[6 * p + 0] = L.koff;
+    lay[6 * p + 1] = L.keys;
+    lay[6 * p + 2] = L.states;
+    lay[6 * p + 3] = L.gofs;
+    lay[6 * p + 4] = L.items;
+    lay[6 * p + 5] = 0;
+    nit[p] = ni;
+    const uint64_t* hw = reinterpret_cast<const uint64_t*>(&H);
+    uint64_t* d0 = reinterpret_cast<uint64_t*>(base + off);
+    uint64_t* d1 = reinterpret_cast<uint64_t*>(hdr_out + 64 * static_cast<uint64_t>(p));
+    for (int w = 0; w < 8; ++w) {
+      d0[w] = hw[w];
+      d1[w] = hw[w];
+    }
+    const uint64_t seg = Align8(L.bytes);
+    seg_out[p] = static_cast<int64_t>(seg);
+    off += seg;
+  }
+}
+
+int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, uint8_t* hdr_dev) {
+  if (merged) return SetError(PXG_FAILED_PRECONDITION, "an aggregation that merged imported states cannot be exported again");
+  if (n_parts < 1 || n_parts > kPartBuckets) return SetError(PXG_INVALID_ARGUMENT, "%d parts", n_parts);
+  ExportCache& X = xc;
+  const bool has_q = x_qval >= 0;
+  const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
+  PXG_RETURN_IF_ERROR(ExportGroupV2(n_parts));
+  const uint64_t G = X.G;
+  // Host bound of the parts' total: headers, per-group offsets / states / item offsets, every
+  // group's key record (<= the arena), items (raw values <= staged rows, <= 2 * kXCentCapH words
+  // per centroid list), alignment.
+  const uint64_t bound = static_cast<uint64_t>(n_parts) * (sizeof(XHeader) + 32) + G * (24 + Align8(srec)) + 8 * arena_words +
+                         8 * (st_n + uint64_t(2) * kXCentCapH * x_nbig) + 64;
+  PXG_RETURN_IF_ERROR(send->Ensure(bound));
+  PXG_RETURN_IF_ERROR(X.desc.Ensure(static_cast<size_t>(8 * n_parts) * 8 + 64));
+  XHdrConst hc;
+  hc.n_keys = static_cast<uint32_t>(n_keys);
+  hc.srec = srec;
+  hc.plan_sig = XPlanSig(*this);
+  hc.has_q = has_q ? 1 : 0;
+  PXG_RETURN_IF_ERROR(Launch(ctx, "export_layout", XLayoutDevKernel, dim3(1), dim3(64), 0,
+                             X.starts.as<const uint64_t>() + kPartBuckets + 1, n_parts, hc, send->as<uint8_t>(), X.desc.as<uint64_t>(),
+                             seg_dev, hdr_dev));
+  XDst D;
+  D.base = send->as<uint8_t>();
+  D.poff = X.desc.as<const uint64_t>();
+  D.layout = D.poff + n_parts;
+  D.nitems = D.layout + 6 * n_parts;
+  if (G > 0) {
+    const bool has_big = has_q && x_nbig > 0;
+    PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", XWriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(G) * 64, 256, 1 << 30)),
+                               dim3(256), 0, X.slist.as<const uint32_t>(), G, X.part_of.as<const uint8_t>(), X.starts.as<const uint64_t>(),
+                               static_cast<const uint64_t*>(X.koff.as<uint64_t>() + G + 1), static_cast<const uint64_t*>(X.words.as<uint64_t>() + G + 1),
+                               slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(), arena.as<const uint64_t>(),
+                               d_plan.as<const AggPlanDev>(), ws.xstates.as<const uint8_t>(), srec, ws.gstart.as<const uint32_t>(), x_vals,
+                               has_big ? static_cast<const int32_t*>(reinterpret_cast<int32_t*>(X.grank.p)) : nullptr,
+                               static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), static_cast<const uint64_t*>(ws.xcent.as<uint64_t>()),
+                               has_q ? 1 : 0, D));
+  }
+  return PXG_OK;
+}
 
 int32_t Agg::ImportPartialsV2(const uint8_t* base8, int32_t n, const int64_t* offs, const int64_t* sizes, const void* hdrs) {
   const XHeader* H = static_cast<const XHeader*>(hdrs);

@@ -300,6 +300,18 @@ extern "C" int32_t pxg_device_count(int32_t* count) {
   return PXG_OK;
 }
 
+// Side stream 2 carries the finalize's critical chain (the big groups' selection path, which
+// waits on the sort and on nothing the other streams produce later): at the highest stream
+// priority its kernels take CUs first and the small / mid digests fill in around them.
+// PXG_SIDE2_PRIO=0: default priority (A/B).
+static hipError_t CreateSide2(hipStream_t* s) {
+  const char* e = std::getenv("PXG_SIDE2_PRIO");
+  if (e && std::atoi(e) == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
   if (!out) return SetError(PXG_INVALID_ARGUMENT, "out is null");
   int n = 0;
@@ -321,7 +333,7 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
   if (hipStreamCreateWithFlags(&c->impl.side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->impl.side2, hipStreamNonBlocking) != hipSuccess ||
+      CreateSide2(&c->impl.side2) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_join2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_meta, hipEventDisableTiming) != hipSuccess ||
@@ -670,11 +682,59 @@ void* ResultAlloc(size_t n) {
     p = fl.back();
     fl.pop_back();
     g_pin_kept -= c;
-  } else if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
-    return std::malloc(n);
+  } else {
+    HostClock clk;
+    if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return std::malloc(n);
+    if (HostClock::On()) {
+      char what[64];
+      std::snprintf(what, sizeof(what), "pinned alloc %zu KiB", c >> 10);
+      clk.Mark(what);
+    }
   }
   g_pin_live[p] = c;
   return p;
+}
+
+// Is [p, p + n) inside one live block of the pinned pool?
+static bool PinnedPoolHolds(const void* p, size_t n) {
+  std::lock_guard<std::mutex> lock(g_pin_mu);
+  auto it = g_pin_live.upper_bound(const_cast<void*>(p));
+  if (it == g_pin_live.begin()) return false;
+  --it;
+  const uint8_t* b = static_cast<const uint8_t*>(it->first);
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  return q >= b && q + n <= b + it->second;
+}
+
+// Device -> pinned-pool host copy by a kernel storing into the mapped host block (16-byte vector
+// stores, then the byte tail).
+__global__ void CopyToHostKernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n) {
+  const size_t tid = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+  size_t done = 0;
+  if (aligned) {
+    const size_t n16 = n >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (size_t i = tid; i < n16; i += stride) d4[i] = s4[i];
+    done = n16 << 4;
+  }
+  for (size_t i = done + tid; i < n; i += stride) dst[i] = src[i];
+}
+
+int32_t CopyD2H(Ctx* ctx, hipStream_t stream, void* host, const void* dev, size_t n) {
+  if (n == 0) return PXG_OK;
+  // Result-sized copies into the pinned pool go by kernel: a hipMemcpyAsync into a recycled pool
+  // block was measured to block the issuing thread for ~7-10 ms once (the second query of an
+  // engine), a kernel launch never blocks it.  Large copies keep the DMA engines.
+  if (n <= kCopyKernelMaxBytes && PinnedPoolHolds(host, n)) {
+    const int grid = static_cast<int>(std::min<size_t>(1024, std::max<size_t>(1, (n + 16 * 256 - 1) / (16 * 256))));
+    return LaunchOn(ctx, stream, "copy_to_host", CopyToHostKernel, dim3(grid), dim3(256), 0, static_cast<uint8_t*>(host),
+                    static_cast<const uint8_t*>(dev), n);
+  }
+  PXG_HIP(hipMemcpyAsync(host, dev, n, hipMemcpyDeviceToHost, stream));
+  return PXG_OK;
 }
 
 void ResultFree(void* p) {
