@@ -1226,10 +1226,13 @@ int32_t Agg::ConsumeRange(Table* t, int64_t begin, int64_t end) {
     }
     return PXG_OK;
   };
-  static const int64_t bpc = [] {  // workgroups per CU of the grid (experiments: PXG_CONSUME_BPC)
+  // Workgroups per CU of the grid (PXG_CONSUME_BPC: experiments).  4 (round 5, tools/
+  // consume_diag.py sweep on one box): C2 1.287 ms (8: 1.310, 6: 1.463, 3: 1.371), 1B rows
+  // 10.70 ms (8: 10.80).
+  static const int64_t bpc = [] {
     const char* e = std::getenv("PXG_CONSUME_BPC");
     const int64_t v = e ? std::atoll(e) : 0;
-    return v > 0 ? v : 8;
+    return v > 0 ? v : 4;
   }();
   // Probe records (pxg_agg.h) for all-STRING keys; PXG_NO_PREC=1 turns them off (tests compare).
   const bool rec = rec_ok && !hc_active && diag == 0 && fast_nk > 0 && fast_nk <= kRecMaxKeys && all_str && !EnvFlag("PXG_NO_PREC");

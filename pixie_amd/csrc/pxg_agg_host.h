@@ -8,6 +8,8 @@
 
 namespace pxg {
 
+struct HcExport;  // pxg_hc.hip
+
 struct AggResult {
   int64_t n_groups = 0;
   bool ready = false;
@@ -57,6 +59,8 @@ struct Agg {
   bool x_ok = false;
   int32_t x_qval = -1;
   bool export_x = false;       // finalize runs for an export: states + centroid lists, below
+  bool x_check_pending = false;  // an export finalize left its checks to CheckExportFinalize
+  uint32_t x_check_groups = 0;   // ... and the group count the device must agree with
   const uint64_t* x_vals = nullptr;  // after an export finalize: the grouped quantile stream
   uint32_t x_nbig = 0;               // ... and its big groups (ws.big / ws.xcent / ws.xcnt)
   // Owner side: imported states merged per slot (macc: macc_words u64 per slot at macc_off[u],
@@ -127,7 +131,10 @@ struct Agg {
     const uint8_t* skip = nullptr;
   } early;
   bool HcNext() const;     // would the next run after a reset be high-cardinality?
-  int32_t FinalizeHc();
+  int32_t FinalizeHc(struct HcExport* ex = nullptr);
+  // Export of a high-cardinality run (pxg_hc.hip): partition groups' states after the table
+  // groups' (states from g_table on), their key records as arena scratch named by eslots.
+  int32_t ExportHcGroups(uint32_t g_table, DevBuf* states, DevBuf* eslots, uint32_t* n_hc, uint64_t* key_words);
   // Moves staged partition records into the table state (export / import need it): every
   // record's key goes to the arena and finds or inserts its group, its values become a staging
   // record.  No-op outside high-cardinality mode; afterwards the run continues on the table.
@@ -147,6 +154,14 @@ struct Agg {
     bool v2 = false;  // the cache describes an exchange-v2 (partial states) export
     uint64_t G = 0;   // v2: groups of the export finalize
     std::vector<uint64_t> g_start, r_start, k_start;  // per part (+ total): groups, rows, key words
+    // v2 group naming of the last export grouping: group g's key record at arena + (uint32_t)
+    // e_slots[e_gslot[g]] (the table's slots / dense ids, or, for a high-cardinality run, eslots
+    // with the partition groups' scratch records and an identity egslot); hc_key_words: the
+    // scratch's words past arena_words.
+    DevBuf eslots, egslot;
+    const unsigned long long* e_slots = nullptr;
+    const uint32_t* e_gslot = nullptr;
+    uint64_t hc_key_words = 0;
   } xc;
 
   // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).
@@ -156,7 +171,7 @@ struct Agg {
     DevBuf keysA, keysB, bstarts, big, bchunks;
     DevBuf chain_list, chain_nc, chain_starts;
     // big groups by selection (pxg_finalize.hip)
-    DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list;
+    DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list, sel_bin;
     RadixPassWs rs;
     // high-cardinality finalize
     DevBuf hc_k[2], hc_v[2], hc_starts, hc_kscr, hc_meta;
@@ -184,7 +199,7 @@ struct Agg {
   // Exchange v2 (partial UDA states, pxg_partial.hip).
   int32_t ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, int64_t* part_offsets, int64_t* part_bytes);
   int32_t ExportGroupV2(int32_t n_parts);
-  int32_t CheckExportFinalize(const uint8_t* meta_copy) const;
+  int32_t CheckExportFinalize(const uint8_t* meta_copy);
   // pxg_agg_alltoall's export: parts laid out on the device (no host wait); per part its aligned
   // bytes to seg_dev[p] and its header to hdr_dev + 64 p.
   int32_t ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, uint8_t* hdr_dev);

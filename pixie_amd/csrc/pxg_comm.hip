@@ -12,8 +12,8 @@
 // per call (AlltoallV2): once for every size and header after the {bytes, header} records have
 // crossed, once for the import's insert count and error flags (plus the export finalize's
 // class-count wait when the plan has quantiles, and one more when the merge accumulators or the
-// group table must grow).  A high-cardinality run first moves its partition records into the
-// table (SpillHc).
+// group table must grow).  A high-cardinality run exports its partition groups as states
+// straight from the partition pass (no spill; only the v1 row parts still spill).
 #include <cstddef>
 #include <rccl/rccl.h>
 
@@ -184,8 +184,10 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   Ctx* ctx = a.ctx;
   if (ctx != C.ctx) return SetError(PXG_INVALID_ARGUMENT, "aggregation and communicator belong to different contexts");
   const int32_t n = C.nranks;
-  PXG_RETURN_IF_ERROR(a.SpillHc());
+  // v2 exports a high-cardinality run's partition groups directly (ExportGroupV2); the v1 row
+  // parts are cut from the table state, so that path first spills the partition records.
   if (ExchangeV2(a)) return AlltoallV2(agg, C, bytes_sent, bytes_recv);
+  PXG_RETURN_IF_ERROR(a.SpillHc());
   // Exchange v1 (PXG_XCHG_V1=1, row parts): sizes of the n parts, then the parts themselves.
   std::vector<int64_t> offs(n), bytes(n), seg(n);
   const bool v2 = false;

@@ -12,417 +12,6 @@
 
 namespace pxg {
 
-constexpr int kRadixBlock = 256;
-constexpr int kRadixItems = 12;
-constexpr int kRadixTile = kRadixBlock * kRadixItems;
-constexpr int kRadixBits = 8;
-constexpr int kRadixBuckets = 1 << kRadixBits;
-constexpr int kRsScanBlock = 256;
-
-struct ValPtrs {
-  uint64_t* p[kMaxVals];
-};
-struct ConstValPtrs {
-  const uint64_t* p[kMaxVals];
-};
-
-// Sort key of a staged record.  Pass 0 reads table slots and maps them through `rank` (slot ->
-// dense group id; kDeferredSlot / empty -> G, which sorts last); later passes read dense ids.
-__device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G) {
-  if (!rank) return k;
-  return k < cap ? rank[k] : G;
-}
-
-
-// ---------------------------------------------------------------------------------------
-// Stable LSD radix sort, 8-bit digits, four kernels per pass: tile digit counts (RsHist),
-// digit totals (RsTotal), tile offsets (RsScan: one workgroup per digit scans that digit's
-// tile counts and adds the digit's base), and the scatter (RsScatter).  No tile ever waits on another: a decoupled look-back (one-sweep) was
-// measured slower here, its inclusive prefixes advancing only a few tiles per device-scope
-// round trip while ~1000 tiles start at once.
-// ---------------------------------------------------------------------------------------
-
-// Tile digit counts of one pass -> hist[tile * kRadixBuckets + d] (tile-major: one contiguous
-// 1 KB row per workgroup; the digit-major layout cost one partial-line write per digit and
-// tile, ~10M scattered writes per pass at 1B rows).  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
-// them instead of gathering again.
-// A workgroup counts kHistTiles consecutive tiles: all their keys (and, in the first pass, their
-// rank gathers) are in flight at once, then each tile's counts are taken in turn.  Four tiles
-// per workgroup at >= 16K tiles (1B rows: the rank-gathering pass 0.59 -> 0.51 ms); one below,
-// where four would leave too few workgroups (C2: 0.057 -> 0.085 ms).
-template <int kHistTiles>
-__global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __restrict__ keys, uint64_t n,
-                                                            const uint32_t* __restrict__ rank, uint32_t cap, uint32_t G, int shift,
-                                                            uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ dense_out) {
-  // One LDS histogram per wave, plain LDS atomics (a hot digit serialises only within its wave;
-  // the 8-ballot match of WaveHistAdd cost more ALU than the conflicts it saved here).
-  constexpr int kWaves = kRadixBlock / 64;
-  __shared__ uint32_t h[kWaves][kRadixBuckets];
-  const int wid = threadIdx.x >> 6;
-  const uint32_t tile0 = XcdRemap(blockIdx.x, gridDim.x) * kHistTiles;
-  // 32-bit positions relative to the workgroup's first record (n < 2^32).
-  const uint64_t base = static_cast<uint64_t>(tile0) * kRadixTile;
-  const uint32_t rem = static_cast<uint32_t>(min(n - min(n, base), static_cast<uint64_t>(kHistTiles) * kRadixTile));
-  const uint32_t* kp = keys + base;
-  uint32_t kk[kHistTiles][kRadixItems];
-#pragma unroll
-  for (int j = 0; j < kHistTiles; ++j)
-#pragma unroll
-    for (int k = 0; k < kRadixItems; ++k) {
-      const uint32_t i = j * kRadixTile + k * kRadixBlock + threadIdx.x;
-      kk[j][k] = i < rem ? kp[i] : 0u;
-    }
-  if (rank) {
-#pragma unroll
-    for (int j = 0; j < kHistTiles; ++j)
-#pragma unroll
-      for (int k = 0; k < kRadixItems; ++k) {
-        const uint32_t i = j * kRadixTile + k * kRadixBlock + threadIdx.x;
-        if (i < rem) kk[j][k] = DenseKey(kk[j][k], rank, cap, G);
-      }
-    uint32_t* dp = dense_out + base;
-#pragma unroll
-    for (int j = 0; j < kHistTiles; ++j)
-#pragma unroll
-      for (int k = 0; k < kRadixItems; ++k) {
-        const uint32_t i = j * kRadixTile + k * kRadixBlock + threadIdx.x;
-        if (i < rem) dp[i] = kk[j][k];
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < kHistTiles; ++j) {
-    if (tile0 + j >= ntiles) break;  // uniform
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) h[w][threadIdx.x] = 0;  // kRadixBlock == kRadixBuckets
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kRadixItems; ++k) {
-      const uint32_t i = j * kRadixTile + k * kRadixBlock + threadIdx.x;
-      if (i < rem) atomicAdd(&h[wid][(kk[j][k] >> shift) & (kRadixBuckets - 1)], 1u);
-    }
-    __syncthreads();
-    uint32_t t = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) t += h[w][threadIdx.x];
-    hist[static_cast<uint64_t>(tile0 + j) * kRadixBuckets + threadIdx.x] = t;
-    __syncthreads();
-  }
-}
-
-// The tile offsets from the tile-major counts, in three coalesced kernels: per range of
-// kRsTilesPerPart tiles the digit sums (RsPart), per digit the exclusive scan of those sums and
-// the digit total (RsPartScan), per range the running offsets tile by tile plus the digit
-// base (RsDown, in place: hist[tile][d] becomes the output position of the tile's first d).
-constexpr uint32_t kRsTilesPerPart = 16;
-__global__ void __launch_bounds__(kRadixBuckets) RsPartKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                              uint32_t* __restrict__ part) {
-  const uint32_t w = blockIdx.x, d = threadIdx.x;
-  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
-  uint32_t s = 0;
-  for (uint32_t t = t0; t < t1; ++t) s += hist[static_cast<uint64_t>(t) * kRadixBuckets + d];
-  part[static_cast<uint64_t>(w) * kRadixBuckets + d] = s;
-}
-__global__ void __launch_bounds__(kRsScanBlock) RsPartScanKernel(uint32_t* __restrict__ part, uint32_t nparts,
-                                                                 uint32_t* __restrict__ ghist) {
-  constexpr int kWaves = kRsScanBlock / 64;
-  __shared__ uint32_t s_w[kWaves];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const uint32_t d = blockIdx.x;
-  uint32_t carry = 0;
-  for (uint32_t i0 = 0; i0 < nparts; i0 += kRsScanBlock) {
-    const uint32_t i = i0 + t;
-    const uint32_t c = i < nparts ? part[static_cast<uint64_t>(i) * kRadixBuckets + d] : 0u;
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t before = carry;
-    for (int w = 0; w < wid; ++w) before += s_w[w];
-    uint32_t round = 0;
-    for (int w = 0; w < kWaves; ++w) round += s_w[w];
-    if (i < nparts) part[static_cast<uint64_t>(i) * kRadixBuckets + d] = before + incl - c;
-    carry += round;
-    __syncthreads();
-  }
-  if (t == 0) ghist[d] = carry;
-}
-__global__ void __launch_bounds__(kRadixBuckets) RsDownKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                              const uint32_t* __restrict__ part, const uint32_t* __restrict__ ghist) {
-  __shared__ uint32_t s[kRadixBuckets];
-  const uint32_t w = blockIdx.x, d = threadIdx.x;
-  // digit base: exclusive scan of the digit totals (Hillis-Steele over 256 values)
-  const uint32_t tot = ghist[d];
-  s[d] = tot;
-  __syncthreads();
-  for (int o = 1; o < kRadixBuckets; o <<= 1) {
-    const uint32_t x = d >= static_cast<uint32_t>(o) ? s[d - o] : 0u;
-    __syncthreads();
-    s[d] += x;
-    __syncthreads();
-  }
-  uint32_t run = s[d] - tot + part[static_cast<uint64_t>(w) * kRadixBuckets + d];
-  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
-  for (uint32_t t = t0; t < t1; ++t) {
-    uint32_t* h = hist + static_cast<uint64_t>(t) * kRadixBuckets + d;
-    const uint32_t c = *h;
-    *h = run;
-    run += c;
-  }
-}
-
-// Block d: digit d's total over all tiles (the digit bases come from these; per-tile atomics
-// into 256 global totals were a contention point).
-__global__ void __launch_bounds__(kRsScanBlock) RsTotalKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                              uint32_t* __restrict__ ghist) {
-  __shared__ uint32_t s[kRsScanBlock];
-  const uint32_t* row = hist + static_cast<uint64_t>(blockIdx.x) * ntiles;
-  uint32_t tot = 0;
-  for (uint32_t i = threadIdx.x; i < ntiles; i += kRsScanBlock) tot += row[i];
-  s[threadIdx.x] = tot;
-  __syncthreads();
-  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
-    if (static_cast<int>(threadIdx.x) < o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) ghist[blockIdx.x] = s[0];
-}
-
-// Block d: exclusive scan of digit d's tile counts, plus the digit's global base.  Each wave
-// scans a contiguous quarter of the row with coalesced loads (4 x 64 counts per step, a wave
-// prefix by shuffles); the quarters' totals are combined through LDS first.
-__global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                             const uint32_t* __restrict__ ghist) {
-  constexpr int kWaves = kRsScanBlock / 64;
-  constexpr int kU = 4;
-  __shared__ uint32_t s[kRsScanBlock];
-  __shared__ uint32_t s_w[kWaves];
-  const int t = threadIdx.x, d = blockIdx.x;
-  const int lane = t & 63, wid = t >> 6;
-  // the digit base: sum of the totals of digits < d
-  s[t] = t < d ? ghist[t] : 0u;
-  __syncthreads();
-  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
-    if (t < o) s[t] += s[t + o];
-    __syncthreads();
-  }
-  const uint32_t carry = s[0];
-  uint32_t* row = hist + static_cast<uint64_t>(d) * ntiles;
-  const uint32_t per = (ntiles + kWaves - 1) / kWaves;
-  const uint32_t q0 = min(ntiles, per * wid), q1 = min(ntiles, q0 + per);
-  uint32_t tot = 0;
-  for (uint32_t i = q0 + lane; i < q1; i += 64) tot += row[i];
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  if (lane == 0) s_w[wid] = tot;
-  __syncthreads();
-  uint32_t run = carry;
-  for (int w = 0; w < wid; ++w) run += s_w[w];
-  for (uint32_t i0 = q0; i0 < q1; i0 += 64 * kU) {
-    uint32_t c[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t i = i0 + u * 64 + lane;
-      c[u] = i < q1 ? row[i] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      uint32_t incl = c[u];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      const uint32_t i = i0 + u * 64 + lane;
-      if (i < q1) row[i] = run + incl - c[u];
-      run += __shfl(incl, 63, 64);
-    }
-  }
-}
-
-// One pass.  Wave w of a block owns the contiguous quarter [w * kPerWave, (w + 1) * kPerWave)
-// of the tile, in (k, lane) order, so a wave's running per-digit counts live in its own LDS
-// slice and need no block barrier inside the item loop: ranks within a wave come from an
-// 8-ballot match of the digit bits.  The tile is then reordered by digit in LDS and written
-// out in digit runs (consecutive threads -> consecutive addresses) instead of one scattered
-// store per item.  The first value stream is loaded up front so its latency overlaps the
-// ranking.
-__global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
-                                                               ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n, int shift,
-                                                               const uint32_t* __restrict__ offs, uint32_t ntiles) {
-  constexpr int kWaves = kRadixBlock / 64;
-  constexpr int kPerWave = kRadixTile / kWaves;
-  __shared__ uint32_t whist[kWaves][kRadixBuckets];
-  __shared__ uint32_t dstart[kRadixBuckets];
-  __shared__ uint32_t gofs[kRadixBuckets];
-  __shared__ uint64_t s_buf[kRadixTile];
-  __shared__ uint8_t s_dig[kRadixTile];
-  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
-  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);  // as in RsHistKernel
-  for (int d = lane; d < kRadixBuckets; d += 64) whist[wid][d] = 0;
-  gofs[threadIdx.x] = offs[static_cast<uint64_t>(tile) * kRadixBuckets + threadIdx.x];
-  (void)ntiles;
-  WaveSync();
-  const uint64_t tile0 = static_cast<uint64_t>(tile) * kRadixTile;
-  const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
-  const int tn = static_cast<int>(min(static_cast<uint64_t>(kRadixTile), n - tile0));
-  uint32_t part[kRadixItems], keys[kRadixItems], dig[kRadixItems];
-  uint64_t v0[kRadixItems];
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-    keys[k] = i < n ? kin[i] : 0u;
-    v0[k] = (nvals > 0 && i < n) ? vin.p[0][i] : 0ULL;
-  }
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-    const bool valid = i < n;
-    const uint32_t d = (keys[k] >> shift) & (kRadixBuckets - 1);
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < kRadixBits; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(valid && bit);
-      peers &= bit ? m : ~m;
-    }
-    const uint32_t r = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
-    const uint32_t pre = valid ? whist[wid][d] : 0u;
-    WaveSync();
-    if (valid && r == 0) whist[wid][d] = pre + static_cast<uint32_t>(__popcll(peers));
-    WaveSync();
-    part[k] = pre + r;
-    dig[k] = d;
-  }
-  __syncthreads();
-  {
-    const int d = threadIdx.x;  // kRadixBlock == kRadixBuckets
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) tot += whist[w][d];
-    dstart[d] = tot;
-    __syncthreads();
-    for (int o = 1; o < kRadixBuckets; o <<= 1) {
-      const uint32_t x = d >= o ? dstart[d - o] : 0u;
-      __syncthreads();
-      dstart[d] += x;
-      __syncthreads();
-    }
-    const uint32_t start = dstart[d] - tot;
-    __syncthreads();
-    dstart[d] = start;
-    uint32_t acc = start;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {  // in place: whist[w][d] becomes the start of (w, d)
-      const uint32_t c = whist[w][d];
-      whist[w][d] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-  uint32_t lpos[kRadixItems];
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    lpos[k] = whist[wid][dig[k]] + part[k];
-    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) {
-      s_key[lpos[k]] = keys[k];
-      s_dig[lpos[k]] = static_cast<uint8_t>(dig[k]);
-    }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
-    const uint32_t d = s_dig[j];
-    kout[gofs[d] + (j - dstart[d])] = s_key[j];
-  }
-  for (int v = 0; v < nvals; ++v) {
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kRadixItems; ++k) {
-      const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-      if (i < n) s_buf[lpos[k]] = v == 0 ? v0[k] : vin.p[v][i];
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < tn; j += kRadixBlock) {
-      const uint32_t d = s_dig[j];
-      vout.p[v][gofs[d] + (j - dstart[d])] = s_buf[j];
-    }
-  }
-}
-
-// Sorts n records (dense key = DenseKey(keys[i]), values vin[0..nvals)) stably by dense key
-// into kbuf[0/1] / vbuf[0/1] (ping-pong); *skeys / *svals name the sorted streams.
-constexpr int kRsMaxPasses = 4;
-// shift0 / fixed_bits (partition sorts, pxg_hc.hip): sort by bits [shift0, shift0 + fixed_bits)
-// of the raw keys instead (no rank map).
-static int32_t RadixSortStreams(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, ConstValPtrs vin,
-                                int nvals, uint64_t n, uint32_t* kbuf[2], ValPtrs vbuf[2], RadixPassWs& ws, const uint32_t** skeys,
-                                ConstValPtrs* svals, int shift0 = 0, int fixed_bits = 0) {
-  if (n == 0 || n >= (uint64_t(1) << 32)) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %llu records", static_cast<unsigned long long>(n));
-  int nbits = 1;
-  while ((uint64_t(1) << nbits) < static_cast<uint64_t>(G) + 1) ++nbits;
-  if (fixed_bits > 0) nbits = fixed_bits;
-  const int passes = (nbits + kRadixBits - 1) / kRadixBits;
-  if (passes > kRsMaxPasses) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %u keys", G);
-  const uint32_t ntiles = static_cast<uint32_t>((n + kRadixTile - 1) / kRadixTile);
-  PXG_RETURN_IF_ERROR(ws.hist.Ensure(static_cast<size_t>(ntiles) * kRadixBuckets * 4));
-  PXG_RETURN_IF_ERROR(ws.ghist.Ensure(static_cast<size_t>(kRsMaxPasses) * kRadixBuckets * 4));
-  const uint32_t nparts = (ntiles + kRsTilesPerPart - 1) / kRsTilesPerPart;
-  PXG_RETURN_IF_ERROR(ws.part.Ensure(static_cast<size_t>(nparts) * kRadixBuckets * 4));
-  uint32_t* ghist = ws.ghist.as<uint32_t>();
-  // With a rank map, the first histogram pass writes the dense keys into kbuf[1] (which the
-  // first scatter does not write) and the scatters read those.
-  const uint32_t* kin = keys;
-  for (int p = 0; p < passes; ++p) {
-    const int cur = p & 1;
-    const bool gather = p == 0 && rank != nullptr;
-    uint32_t* gh = ghist + p * kRadixBuckets;
-    const int ht = ntiles >= 16384 ? 4 : 1;
-    PXG_RETURN_IF_ERROR(Launch(ctx, gather ? "radix_hist_rank" : "radix_hist", ht == 4 ? RsHistKernel<4> : RsHistKernel<1>,
-                               dim3((ntiles + ht - 1) / ht), dim3(kRadixBlock), 0, kin, n, gather ? rank : nullptr, cap,
-                               G, shift0 + p * kRadixBits, ws.hist.as<uint32_t>(), ntiles, gather ? kbuf[1] : nullptr));
-    if (gather) kin = kbuf[1];
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsPartKernel, dim3(nparts), dim3(kRadixBuckets), 0,
-                               static_cast<const uint32_t*>(ws.hist.as<uint32_t>()), ntiles, ws.part.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsPartScanKernel, dim3(kRadixBuckets), dim3(kRsScanBlock), 0, ws.part.as<uint32_t>(),
-                               nparts, gh));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", RsDownKernel, dim3(nparts), dim3(kRadixBuckets), 0, ws.hist.as<uint32_t>(), ntiles,
-                               static_cast<const uint32_t*>(ws.part.as<uint32_t>()), static_cast<const uint32_t*>(gh)));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", RsScatterKernel, dim3(ntiles), dim3(kRadixBlock), 0, kin, kbuf[cur], vin, vbuf[cur],
-                               nvals, n, shift0 + p * kRadixBits, ws.hist.as<const uint32_t>(), ntiles));
-    kin = kbuf[cur];
-    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[cur].p[v];
-  }
-  *skeys = kin;
-  *svals = vin;
-  return PXG_OK;
-}
-
-// Dense group ids of the table's occupied slots, in slot order (rank = exclusive scan of the
-// occupancy flags); gslot[rank] = slot.
-__global__ void SlotFlagsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, uint32_t* __restrict__ flags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap) flags[i] = slots[i] != 0 ? 1u : 0u;
-}
-__global__ void SlotGslotKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ rank,
-                                uint32_t* __restrict__ gslot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap && slots[i] != 0) gslot[rank[i]] = i;
-}
-
-// Group starts straight from the sorted dense ids: the first index of every id (ids are dense,
-// so no scan is needed); gstart[G] = the number of records with a valid group.
-__global__ void GroupHeadsKernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t G, uint32_t* __restrict__ gstart) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = keys[i];
-  if (i == 0 || keys[i - 1] != k) gstart[k < G ? k : G] = static_cast<uint32_t>(i);
-  if (i == n - 1 && k < G) gstart[G] = static_cast<uint32_t>(n);
-}
-
 // ---------------------------------------------------------------------------------------
 // Per-group UDA reductions, two levels: one wave per chunk of <= kRedChunk rows of a group
 // writes a partial state; one thread per group combines its chunks in order.  Balanced for
@@ -509,14 +98,22 @@ __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __res
       n = WaveSumU64(n);
       if (lane == 0) partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
     } else if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
-      if (at == PXG_FLOAT64) {
-        double acc = 0;
-        for (uint32_t i = s + lane; i < e; i += 64) acc += AsF(v[i]);
-        r = FBits(WaveSumF64(acc));
-      } else if (kind == PXG_UDA_MEAN) {
-        double acc = 0;
-        for (uint32_t i = s + lane; i < e; i += 64) acc += static_cast<double>(static_cast<int64_t>(v[i]));
-        r = FBits(WaveSumF64(acc));
+      if (at == PXG_FLOAT64 || kind == PXG_UDA_MEAN) {
+        // Four loads in flight per lane (a dependent one-load loop left the pass latency-bound:
+        // ~3 TB/s over the 1B-row staging), four partial sums added in a fixed order.
+        const bool f64 = at == PXG_FLOAT64;
+        auto dv = [f64](uint64_t x) { return f64 ? AsF(x) : static_cast<double>(static_cast<int64_t>(x)); };
+        double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        uint32_t i = s + lane;
+        for (; i + 192 < e; i += 256) {
+          const uint64_t x0 = v[i], x1 = v[i + 64], x2 = v[i + 128], x3 = v[i + 192];
+          a0 += dv(x0);
+          a1 += dv(x1);
+          a2 += dv(x2);
+          a3 += dv(x3);
+        }
+        for (; i < e; i += 64) a0 += dv(v[i]);
+        r = FBits(WaveSumF64((a0 + a1) + (a2 + a3)));
       } else {
         uint64_t acc = 0;
         for (uint32_t i = s + lane; i < e; i += 64) acc += v[i];
@@ -751,13 +348,29 @@ constexpr uint64_t kPosInfKey = 0xFFF0000000000000ULL;  // SortKeyF(+inf) = 0x7F
 // 2 mid (<= 4096, one workgroup, LDS), 3 big (chunk sort + merge in HBM).
 constexpr uint32_t kTinyMax = 64;
 constexpr uint32_t kSmallMax = 1024;
+// Size classes: 0 tiny (<= 64), 1 small (<= 1024), 2 mid (<= 2048), 3 big (> mid_max), and the
+// larger mid classes 4 (<= 4096), 5 (<= 8192), 6 (<= 16384; empty while kMidClassMax is 8192):
+// one LDS-sort workgroup per group, sized per class (QuantMidKernel<kMaxN>).  Counters of classes 0-3 at meta + 32, of 4-6 at
+// meta + 64; lists[c * G ..] per class.
 constexpr int kNumClasses = 4;
+constexpr int kNumMidSub = 3;
+constexpr int kAllClasses = kNumClasses + kNumMidSub;
+// Groups above take the selection path (export: 4096).  8192: an LDS sort of a 4K-8K-value
+// group costs half of its selection path (tools/quant_class_bench.py: 15M values in 6000-value
+// groups 0.40 vs ~0.80 ms); at 8K-16K the two cost about the same and the 1024-thread sort ran
+// on the critical stream (1B rows: 0.77 ms), so those groups stay on the selection path.
+constexpr uint32_t kMidClassMax = 8192;
+__device__ __forceinline__ int SizeClass(uint32_t n, uint32_t mid_max) {
+  if (n > mid_max) return 3;
+  return n <= kTinyMax ? 0 : n <= kSmallMax ? 1 : n <= 2048 ? 2 : n <= 4096 ? 4 : n <= 8192 ? 5 : 6;
+}
 
 // skip_flags (merged exchange): groups whose slot's flags word (macc, words per slot, last word)
 // has the digest flag get no class; their quantiles come from the merged digest instead.
 __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __restrict__ gstart, uint32_t ngroups,
                                                             uint32_t* __restrict__ lists, uint32_t* __restrict__ counts,
-                                                            uint32_t mid_max, const uint64_t* __restrict__ skip_flags, int flag_words,
+                                                            uint32_t* __restrict__ counts_mid, uint32_t mid_max,
+                                                            const uint64_t* __restrict__ skip_flags, int flag_words,
                                                             const uint32_t* __restrict__ gslot) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -765,18 +378,18 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
   int cls = -1;
   if (g < ngroups) {
     const uint32_t n = gstart[g + 1] - gstart[g];
-    cls = n <= kTinyMax ? 0 : (n <= kSmallMax ? 1 : (n <= mid_max ? 2 : 3));
+    cls = SizeClass(n, mid_max);
     if (skip_flags && (skip_flags[static_cast<uint64_t>(gslot[g]) * flag_words + flag_words - 1] & 1ULL)) cls = -1;
   }
   // Block-aggregated list appends: wave leaders reserve within the block in LDS, then one
-  // global atomic per class per block (the four class counters are hot addresses).
-  __shared__ uint32_t s_cnt[kNumClasses], s_base[kNumClasses];
-  if (threadIdx.x < kNumClasses) s_cnt[threadIdx.x] = 0;
+  // global atomic per class per block (the class counters are hot addresses).
+  __shared__ uint32_t s_cnt[kAllClasses], s_base[kAllClasses];
+  if (threadIdx.x < kAllClasses) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t wofs[kNumClasses];
-  unsigned long long wm[kNumClasses];
+  uint32_t wofs[kAllClasses];
+  unsigned long long wm[kAllClasses];
 #pragma unroll
-  for (int c = 0; c < kNumClasses; ++c) {
+  for (int c = 0; c < kAllClasses; ++c) {
     wm[c] = __ballot(cls == c);
     const int leader = wm[c] ? __ffsll(static_cast<long long>(wm[c])) - 1 : 0;
     uint32_t o = 0;
@@ -784,10 +397,13 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
     wofs[c] = __shfl(o, leader, 64);
   }
   __syncthreads();
-  if (threadIdx.x < kNumClasses) s_base[threadIdx.x] = s_cnt[threadIdx.x] ? atomicAdd(&counts[threadIdx.x], s_cnt[threadIdx.x]) : 0u;
+  if (threadIdx.x < kAllClasses) {
+    uint32_t* ctr = threadIdx.x < kNumClasses ? &counts[threadIdx.x] : &counts_mid[threadIdx.x - kNumClasses];
+    s_base[threadIdx.x] = s_cnt[threadIdx.x] ? atomicAdd(ctr, s_cnt[threadIdx.x]) : 0u;
+  }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < kNumClasses; ++c)
+  for (int c = 0; c < kAllClasses; ++c)
     if (cls == c) lists[static_cast<uint64_t>(c) * ngroups + s_base[c] + wofs[c] + __popcll(wm[c] & lanemask_lt)] = g;
 }
 
@@ -1008,9 +624,6 @@ __device__ __forceinline__ int64_t LowerBoundKey(Acc a, int64_t n, uint64_t key)
 // of DigestQuantile lists them (its control flow depends on positions only, never on means),
 // then each is computed — the reference's incremental mean for centroids of <= kSeqMean
 // values (every centroid while W <= ~10000), sum/count cooperatively for larger ones.
-// Timing-only diagnosis (PXG_DIAG_QUANT): 1 skips the centroid-boundary chain, 2 skips the
-// mid-group LDS sort.  Results are garbage when set; never set outside tools/.
-__device__ int g_diag_quant = 0;
 
 constexpr int kNeed = 7 * 4;
 constexpr int64_t kSeqMean = 16;
@@ -1019,7 +632,7 @@ struct DigestShared {
   int64_t meta[4];
   int32_t need[kNeed];
   double mean[kNeed];
-  double red[4];
+  double red[16];  // per-wave partial sums (workgroups of up to 1024 threads)
 };
 
 // Centroid boundaries precomputed by DigestChainKernel for a group assumed NaN-free (W = n);
@@ -1089,7 +702,7 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_
   if (t == 0) {
     int64_t nc;
     if (use_pre) nc = pre.nc;
-    else nc = g_diag_quant == 1 ? (starts_buf[0] = 0, 1) : DigestBoundaries(W, starts_buf, max_c);
+    else nc = DigestBoundaries(W, starts_buf, max_c);
     if (nc < 0) atomicExch(err, 1u);
     sh.meta[2] = nc < 0 ? 0 : nc;
   }
@@ -1146,7 +759,7 @@ __device__ void BlockDigest(KeyAt keyat, int64_t n, uint32_t* starts_buf, int64_
 // the per-finalize chain kernel.  A group whose NaN-trimmed size differs from its row count
 // builds its own chain in the digest (BlockDigest), as before.
 constexpr int kMidChainW0 = kSingletonMaxW + 1;
-constexpr int kMidChainN = kMidMax - kSingletonMaxW;
+constexpr int kMidChainN = static_cast<int>(kMidClassMax) - kSingletonMaxW;
 __global__ void __launch_bounds__(256) MidChainTableKernel(uint32_t* __restrict__ starts, int32_t* __restrict__ nc) {
   const int i = static_cast<int>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (i >= kMidChainN) return;
@@ -1162,12 +775,17 @@ __device__ __forceinline__ PreChain MidPreChain(const uint32_t* tab, const int32
   return p;
 }
 
-// One workgroup per group with 1024 < n <= 4096: LDS merge sort + digest.
-__global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
-                                                      const uint32_t* __restrict__ mid_starts, const int32_t* __restrict__ mid_nc,
-                                                      const uint32_t* __restrict__ nlist_p, const uint64_t* __restrict__ vals,
-                                                      int arg_type, double* __restrict__ out, unsigned int* __restrict__ err) {
-  __shared__ uint64_t keys[PaddedLen(kMidMax)];
+// One workgroup per group of a mid class (1024 < n <= 16384): LDS merge sort + digest, one
+// launch per class, each workgroup sized to its class (kMaxN / 16 threads, kMaxN keys in LDS): a
+// 256-thread workgroup left half its threads idle through the sort of a <= 2048-value group, and
+// groups of 4K-16K values cost the selection path (sample, chain, plan, bin sorts per group)
+// about twice what one LDS sort does (tools/quant_class_bench.py).
+template <int kMaxN>
+__global__ void __launch_bounds__(kMaxN / kMsIpt) QuantMidKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ gstart,
+                                                                 const uint32_t* __restrict__ mid_starts, const int32_t* __restrict__ mid_nc,
+                                                                 const uint32_t* __restrict__ nlist_p, const uint64_t* __restrict__ vals,
+                                                                 int arg_type, double* __restrict__ out, unsigned int* __restrict__ err) {
+  __shared__ uint64_t keys[PaddedLen(kMaxN)];
   __shared__ uint32_t starts[kMidCentroids];
   __shared__ DigestShared sh;
   if (blockIdx.x >= *nlist_p) return;
@@ -1177,7 +795,7 @@ __global__ void __launch_bounds__(256) QuantMidKernel(const uint32_t* __restrict
   while (P < static_cast<int>(n)) P <<= 1;
   for (int i = threadIdx.x; i < P; i += blockDim.x) keys[PadIdx(i)] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
   __syncthreads();
-  if (g_diag_quant != 2) BlockMergeSortLds(keys, P);
+  BlockMergeSortLds(keys, P);
   BlockDigest<true>([&](int64_t i) -> uint64_t { return keys[PadIdx(static_cast<int>(i))]; }, n, starts, kMidCentroids,
               MidPreChain(mid_starts, mid_nc, n), out + static_cast<uint64_t>(g) * 7, err, sh);
 }
@@ -1774,10 +1392,18 @@ constexpr uint32_t kSelCollCap = kSelHugeThreads * kMsIpt;  // 16384
 constexpr int kSelLists = 3;  // gathered bins: <= 1024 values (wave), <= 4096 (256 threads), larger (1024 threads)
 
 // Bins actually used by a group of n values (the rest hold splitter ~0 and stay empty): <= 2048
-// values per bin on average, so a gathered bin beyond kSelCollCap is a ~1e-6 event per bin;
-// small big groups keep the small sample and the short splitter loads.
+// values per bin on average, so a gathered bin beyond kSelCollCap is a ~1e-6 event per bin.
+// Groups under 16K values use ~16-32 values per bin (128..1024 bins): their sample (2 nb keys)
+// and its sort stay a small fraction of the group (at 1B rows 1,872 of the 2,692 big groups hold
+// 4K-16K values; a 2048-key sample of a 5000-value group cost almost a sort of the group).
+// The largest groups use 2048 bins too (a 4096-key sample): the 8192-key sample of a > 4M-value
+// group took one 512-thread workgroup ~0.2 ms on the critical path at 1B rows, more than its
+// larger bins cost the bin sorts.
 __device__ __forceinline__ int SelNb(uint64_t n) {
-  return n > (uint64_t(1) << 22) ? kSelBins : n > (uint64_t(1) << 21) ? kSelBins / 2 : kSelBins / 4;
+  if (n > (uint64_t(1) << 21)) return kSelBins / 2;
+  int nb = kSelBins / 4;
+  while (nb > 128 && static_cast<uint64_t>(nb) * 16 > n) nb >>= 1;
+  return nb;
 }
 constexpr uint8_t kTagColl = 0x80;
 
@@ -1944,17 +1570,14 @@ static uint32_t SelChunksPerBlock(uint32_t nchunks, int num_cus, uint32_t blocks
   const uint32_t slots = blocks_per_cu * static_cast<uint32_t>(num_cus);
   return std::max<uint32_t>(1, std::min<uint32_t>(cap, (nchunks + slots - 1) / slots));
 }
-// quant_sel_hist's cap on chunks per block (PXG_SEL_HIST_CPB overrides; tools/n1_selhist_ab.sh).
-static uint32_t SelHistCap() {
-  const char* e = std::getenv("PXG_SEL_HIST_CPB");
-  const int v = e ? std::atoi(e) : 0;
-  return v > 0 ? static_cast<uint32_t>(v) : 64;
-}
+// quant_sel_hist's cap on chunks per block (64: measured in round 3 against 8 / 16 / 32, fewer
+// histogram flushes per group).
+constexpr uint32_t kSelHistCap = 64;
 template <bool kF64>
 __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                      const uint64_t* __restrict__ vals, int arg_type, const uint64_t* __restrict__ spl,
                                                      const uint16_t* __restrict__ guide, uint32_t* __restrict__ hist,
-                                                     uint32_t* __restrict__ nan_cnt, uint32_t cpb) {
+                                                     uint32_t* __restrict__ nan_cnt, uint32_t cpb, uint16_t* __restrict__ bin_out) {
   const uint32_t nchunks = *nchunks_p;
   const uint32_t c0 = blockIdx.x * cpb;
   if (c0 >= nchunks) return;
@@ -2014,6 +1637,10 @@ __global__ void __launch_bounds__(256) BigHistKernel(const BigChunk* __restrict_
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) bin[k] = SelGuideFinish(S, QKeyT<kF64>(raw[k]), bin[k], bend[k]);
+    // Each value's bin, for BigCollect (which then needs neither the splitters nor the search).
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (k * 256 + static_cast<int>(threadIdx.x) < static_cast<int>(c.len)) bin_out[c.off + k * 256 + threadIdx.x] = static_cast<uint16_t>(bin[k]);
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
       if (k * 256 + static_cast<int>(threadIdx.x) < static_cast<int>(c.len)) atomicAdd(&h[bin[k]], 1u);
@@ -2234,17 +1861,14 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
 template <bool kF64>
 __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restrict__ chunks, const uint32_t* __restrict__ nchunks_p,
                                                         const BigPlan* __restrict__ plans, const uint64_t* __restrict__ vals, int arg_type,
-                                                        const uint64_t* __restrict__ spl, const uint16_t* __restrict__ guide,
-                                                        const uint8_t* __restrict__ tag_all,
+                                                        const uint16_t* __restrict__ bin_in, const uint8_t* __restrict__ tag_all,
                                                         const uint32_t* __restrict__ cbase_all, uint32_t* __restrict__ cursor_all,
                                                         uint64_t* __restrict__ cand, double* __restrict__ partial, uint32_t cpb) {
   const uint32_t nchunks = *nchunks_p;
   const uint32_t c0 = blockIdx.x * cpb;
   if (c0 >= nchunks) return;
   const uint32_t c1 = min(nchunks, c0 + cpb);
-  __shared__ uint64_t S[kSelBins];
   __shared__ uint8_t tg[kSelBins];
-  __shared__ uint16_t Gd[kSelGuide + 1];
   __shared__ double acc[4][kSelMaxRanges];
   __shared__ uint8_t cix[kSelBins];              // gathered bin -> its index in P.coll
   __shared__ uint16_t s_coll[kSelMaxColl];
@@ -2252,55 +1876,38 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   constexpr int kRounds = kMidMax / 256;
   uint32_t cur = 0xFFFFFFFFu;
-  int nb = kSelBins;
-  bool fresh = false;
-  SelGuideK gk{0, 0, 0, 2};
   for (int k = t; k < kSelMaxColl; k += 256) lcnt[k] = 0;  // (the loop's first barrier orders it)
   // (No next-chunk prefetch here: its 32 VGPRs cost a wave per SIMD and measured no faster.)
   for (uint32_t ci = c0; ci < c1; ++ci) {
     const BigChunk c = chunks[ci];
     uint64_t raw[kRounds];
+    int bins[kRounds];  // from BigHist (bin_in: the same search over the same splitters)
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) raw[r] = vals[c.off + min(wid * (kMidMax / 4) + r * 64 + lane, static_cast<int>(c.len) - 1)];
+    for (int r = 0; r < kRounds; ++r) {
+      const int i = min(wid * (kMidMax / 4) + r * 64 + lane, static_cast<int>(c.len) - 1);
+      raw[r] = vals[c.off + i];
+      bins[r] = bin_in[c.off + i];
+    }
     const BigPlan* P = plans + c.bidx;
     if (!P->fallback) {  // uniform
       const int n_ranges = P->n_ranges, n_coll = P->n_coll;
-      __syncthreads();  // the previous chunk's acc / S / tg / lbase readers are done
+      __syncthreads();  // the previous chunk's acc / tg / lbase readers are done
       if (c.bidx != cur) {
         cur = c.bidx;
-        nb = SelNb(c.g_n);
-        const uint64_t* Sg = spl + static_cast<uint64_t>(cur) * kSelBins;
         const uint8_t* Tg = tag_all + static_cast<uint64_t>(cur) * kSelBins;
-        const uint16_t* Gg = guide + static_cast<uint64_t>(cur) * kSelGuideStride;
-        for (int b = t; b < kSelBins; b += 256) {
-          S[b] = b < nb ? Sg[b] : ~0ULL;
-          tg[b] = b < nb ? Tg[b] : Tg[kSelBins - 1];
-        }
-        for (int i = t; i <= kSelGuide; i += 256) Gd[i] = Gg[i];
+        for (int b = t; b < kSelBins; b += 256) tg[b] = Tg[b];
         for (int k = t; k < n_coll; k += 256) {
           const int b = P->coll[k];
           s_coll[k] = static_cast<uint16_t>(b);
           cix[b] = static_cast<uint8_t>(k);
         }
-        fresh = true;
       }
       if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
       __syncthreads();
-      if (fresh) {
-        gk = SelGuideOf(S, nb);
-        fresh = false;
-      }
       const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
       uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
       uint64_t* cg = cand + c.g_off;
       uint32_t ls[kRounds];  // gathered: (index in P.coll) << 16 | slot in this chunk's run
-      // Bins of the whole chunk first (independent searches in flight), then the gathers and
-      // the inside-range sums.
-      int bins[kRounds], bend[kRounds];
-#pragma unroll
-      for (int r = 0; r < kRounds; ++r) SelGuideBracket(Gd, gk, QKeyT<kF64>(raw[r]), bins[r], bend[r]);
-#pragma unroll
-      for (int r = 0; r < kRounds; ++r) bins[r] = SelGuideFinish(S, QKeyT<kF64>(raw[r]), bins[r], bend[r]);
 #pragma unroll
       for (int r = 0; r < kRounds; ++r) {
         const int i = wid * (kMidMax / 4) + r * 64 + lane;
@@ -2543,751 +2150,10 @@ __global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
     *reinterpret_cast<uint32_t*>(meta + 16) = 0;
     *reinterpret_cast<uint32_t*>(meta + 20) = 0;
     for (int c = 0; c < kNumClasses; ++c) reinterpret_cast<uint32_t*>(meta + 32)[c] = 0;
+    for (int c = 0; c < kNumMidSub; ++c) reinterpret_cast<uint32_t*>(meta + 64)[c] = 0;
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Staging split (large aggregations).  Finalize only needs each group's records contiguous
-// (every reduction and digest below works on a group's range; the quantile kernels sort the
-// values they read).  The LSD radix sort gets that with two full passes over all records at
-// ~65K groups.  Here the groups a sample says are large ("designated", at most kSplitMaxBig)
-// are partitioned out of the staging in ONE counting pass, each into its own contiguous range,
-// and only the remaining records go through the radix sort: at the north_star size the
-// designated groups hold ~80 % of the records.  (The work replaced is agg_node.cc:273-349's
-// flush + per-group finalize; how records get grouped is this implementation's choice.)
-//
-// Group ids: the rest groups take [0, Gr) and the designated ones [Gr, G), both in slot order;
-// buckets: 0 = rest, 1 + j = designated group Gr + j, nd + 1 = records without a group.  The
-// final layout is [rest records sorted by id | designated records by id | no group], so gstart
-// stays monotone and every kernel after the grouping is unchanged.  A group the sample misses
-// goes through the sort; one it over-estimates is classified by its true count: the sample
-// decides the cost, never the result.
-// ---------------------------------------------------------------------------------------
-constexpr uint32_t kSplitStride = 128;    // every 128th staged record is sampled
-constexpr uint32_t kSplitMinRows = 8192;  // designate a group whose sampled estimate reaches this
-constexpr uint32_t kSplitMaxBig = 2046;   // rest + designated + no-group buckets <= kSplitBuckets
-constexpr int kSplitBuckets = 2048;
-constexpr int kSplitHash = 4096;          // LDS map designated slot -> bucket (<= 50 % full)
-constexpr uint32_t kSplitEmpty = 0xFFFFFFFFu;
-constexpr int kSplitBlock = 256;
-constexpr uint32_t kSplitTile = 32768;    // records per tile of the split's (bucket x tile) counts
-constexpr int kSplitItems = 8;            // scatter: records per thread per sub-tile
-constexpr int kSplitSub = kSplitBlock * kSplitItems;
-constexpr int kSampleTable = 4096;
-constexpr int kSamplePerThread = 16;
-
-// Sampled per-slot counts: each block aggregates 4096 samples in an LDS table, then adds its
-// distinct slots' counts to scnt (one global atomic per distinct slot per block, so a hot
-// group sees one per block, not one per sample).  A slot that finds no LDS entry within 32
-// probes is dropped: such a block met thousands of distinct cold slots, none of them large.
-__global__ void __launch_bounds__(256) SplitSampleKernel(const uint32_t* __restrict__ slot, uint64_t n, uint32_t cap,
-                                                         uint32_t* __restrict__ scnt) {
-  __shared__ uint32_t s_key[kSampleTable];
-  __shared__ uint32_t s_cnt[kSampleTable];
-  for (int i = threadIdx.x; i < kSampleTable; i += 256) {
-    s_key[i] = 0xFFFFFFFFu;
-    s_cnt[i] = 0;
-  }
-  __syncthreads();
-  const uint64_t j0 = static_cast<uint64_t>(blockIdx.x) * 256 * kSamplePerThread;
-  uint32_t sv[kSamplePerThread];
-#pragma unroll
-  for (int k = 0; k < kSamplePerThread; ++k) {
-    const uint64_t r = (j0 + static_cast<uint64_t>(k) * 256 + threadIdx.x) * kSplitStride;
-    sv[k] = r < n ? slot[r] : 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (int k = 0; k < kSamplePerThread; ++k) {
-    const uint32_t x = sv[k];
-    if (x >= cap) continue;
-    uint32_t h = (x * 0x9E3779B1u) >> 20;
-    for (int p = 0; p < 32; ++p) {
-      uint32_t cur = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (cur == 0xFFFFFFFFu) {
-        cur = atomicCAS(&s_key[h], 0xFFFFFFFFu, x);
-        if (cur == 0xFFFFFFFFu) cur = x;
-      }
-      if (cur == x) {
-        atomicAdd(&s_cnt[h], 1u);
-        break;
-      }
-      h = (h + 1) & (kSampleTable - 1);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kSampleTable; i += 256)
-    if (s_cnt[i]) atomicAdd(&scnt[s_key[i]], s_cnt[i]);
-}
-
-// lvl[l] = occupied slots whose sample count has floor(log2) == l: the designation threshold
-// is raised by powers of two until at most kSplitMaxBig slots reach it, so the cap keeps the
-// largest groups rather than the first ones in slot order.
-__global__ void SplitLevelsKernel(const uint32_t* __restrict__ scnt, uint32_t cap, uint32_t* __restrict__ lvl) {
-  __shared__ uint32_t s_l[32];
-  if (threadIdx.x < 32) s_l[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = i < cap ? scnt[i] : 0u;
-  if (c) atomicAdd(&s_l[31 - __clz(c)], 1u);
-  __syncthreads();
-  if (threadIdx.x < 32 && s_l[threadIdx.x]) atomicAdd(&lvl[threadIdx.x], s_l[threadIdx.x]);
-}
-
-__device__ __forceinline__ uint32_t SplitThreshold(const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big) {
-  uint32_t above = 0;  // slots with a count >= 2^(l + 1)
-  int L = 32;
-  for (int l = 31; l >= 0; --l) {
-    above += lvl[l];
-    if (above > max_big) break;
-    L = l;
-  }
-  const uint32_t p = L >= 32 ? 0xFFFFFFFFu : (1u << L);
-  return max(min_samples, p);
-}
-
-// flags[slot] = designated << 32 | occupied (one u64 scan gives both ranks).
-__global__ void SplitFlagsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
-                                 const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big, uint64_t* __restrict__ flags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap) return;
-  const uint32_t t = SplitThreshold(lvl, min_samples, max_big);
-  const bool occ = slots[i] != 0;
-  const bool des = occ && scnt[i] >= t;
-  flags[i] = (static_cast<uint64_t>(des) << 32) | static_cast<uint64_t>(occ);
-}
-
-__device__ __forceinline__ uint32_t SplitNd(const uint64_t* __restrict__ ftotal, uint32_t max_big = kSplitMaxBig) {
-  return min(static_cast<uint32_t>(*ftotal >> 32), max_big);
-}
-
-// Group ids from the scanned flags: designated slots -> Gr + their rank, the rest -> their rank
-// among the rest; gslot[id] = slot (so gslot[Gr + j] lists the designated slots by bucket).
-__global__ void SplitIdsKernel(const unsigned long long* __restrict__ slots, uint32_t cap, const uint32_t* __restrict__ scnt,
-                               const uint32_t* __restrict__ lvl, uint32_t min_samples, uint32_t max_big, const uint64_t* __restrict__ fscan,
-                               const uint64_t* __restrict__ ftotal, uint32_t G, uint32_t* __restrict__ newid, uint32_t* __restrict__ gslot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap || slots[i] == 0) return;
-  const uint32_t t = SplitThreshold(lvl, min_samples, max_big);
-  const uint32_t nd = SplitNd(ftotal, max_big), Gr = G - nd;
-  const uint64_t f = fscan[i];
-  const uint32_t d_rank = static_cast<uint32_t>(f >> 32), o_rank = static_cast<uint32_t>(f);
-  const bool des = scnt[i] >= t && d_rank < max_big;
-  const uint32_t id = des ? Gr + d_rank : o_rank - min(d_rank, max_big);
-  newid[i] = id;
-  gslot[id] = i;
-}
-
-__device__ __forceinline__ uint32_t SplitHashPos(uint32_t s) { return (s * 0x9E3779B1u) >> 20; }
-static_assert(kSplitHash == 4096, "SplitHashPos yields 12 bits");
-
-// The block's LDS map designated slot -> bucket 1 + j, from gslot[Gr + j] (j < nd).
-__device__ __forceinline__ void SplitBuildMap(uint32_t* hk, uint16_t* hv, const uint32_t* __restrict__ gslot, uint32_t Gr, uint32_t nd) {
-  for (int i = threadIdx.x; i < kSplitHash; i += kSplitBlock) hk[i] = kSplitEmpty;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nd; j += kSplitBlock) {
-    const uint32_t x = gslot[Gr + j];
-    uint32_t h = SplitHashPos(x);
-    while (atomicCAS(&hk[h], kSplitEmpty, x) != kSplitEmpty) h = (h + 1) & (kSplitHash - 1);
-    hv[h] = static_cast<uint16_t>(j + 1);
-  }
-  __syncthreads();
-}
-
-// Bucket of a staged record: 0 = rest, 1 + j = designated, nd + 1 = no group.
-__device__ __forceinline__ uint32_t SplitLookup(const uint32_t* hk, const uint16_t* hv, uint32_t x, uint32_t cap, uint32_t nd) {
-  if (x >= cap) return nd + 1;
-  uint32_t h = SplitHashPos(x);
-  for (;;) {
-    const uint32_t k = hk[h];
-    if (k == x) return hv[h];
-    if (k == kSplitEmpty) return 0;
-    h = (h + 1) & (kSplitHash - 1);
-  }
-}
-
-// Bucket counts of one tile -> hist[b * ntiles + tile] (bucket-major, as the radix passes).
-// The rest bucket, a large share of every wave, is counted in registers and added once per wave.
-__global__ void __launch_bounds__(kSplitBlock) SplitHistKernel(const uint32_t* __restrict__ slot, uint64_t n, uint32_t cap,
-                                                               const uint32_t* __restrict__ gslot, const uint64_t* __restrict__ ftotal,
-                                                               uint32_t G, uint32_t* __restrict__ hist, uint32_t ntiles) {
-  __shared__ uint32_t hk[kSplitHash];
-  __shared__ uint16_t hv[kSplitHash];
-  __shared__ uint32_t h[kSplitBuckets];
-  const uint32_t nd = SplitNd(ftotal), Gr = G - nd, nb = nd + 2;
-  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) h[b] = 0;
-  SplitBuildMap(hk, hv, gslot, Gr, nd);
-  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
-  const uint64_t r0 = static_cast<uint64_t>(tile) * kSplitTile;
-  const uint64_t r1 = min(r0 + kSplitTile, n);
-  uint32_t rest = 0;
-  constexpr int U = 8;
-  for (uint64_t r = r0 + threadIdx.x; r < r1; r += static_cast<uint64_t>(kSplitBlock) * U) {
-    uint32_t sv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = r + static_cast<uint64_t>(u) * kSplitBlock;
-      sv[u] = i < r1 ? slot[i] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (r + static_cast<uint64_t>(u) * kSplitBlock >= r1) continue;
-      const uint32_t b = SplitLookup(hk, hv, sv[u], cap, nd);
-      if (b == 0) ++rest;
-      else atomicAdd(&h[b], 1u);
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) rest += __shfl_xor(rest, o, 64);
-  if ((threadIdx.x & 63) == 0 && rest) atomicAdd(&h[0], rest);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) hist[static_cast<uint64_t>(b) * ntiles + tile] = h[b];
-}
-
-// tot[b] = bucket b's count over all tiles (0 past the live buckets, so one fixed-size scan
-// of tot gives the bucket bases).
-__global__ void __launch_bounds__(kRsScanBlock) SplitTotalKernel(const uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                                 const uint64_t* __restrict__ ftotal, uint32_t* __restrict__ tot) {
-  __shared__ uint32_t s[kRsScanBlock];
-  const uint32_t b = blockIdx.x;
-  if (b >= SplitNd(ftotal) + 2) {
-    if (threadIdx.x == 0) tot[b] = 0;
-    return;
-  }
-  const uint32_t* row = hist + static_cast<uint64_t>(b) * ntiles;
-  uint32_t t = 0;
-  for (uint32_t i = threadIdx.x; i < ntiles; i += kRsScanBlock) t += row[i];
-  s[threadIdx.x] = t;
-  __syncthreads();
-  for (int o = kRsScanBlock / 2; o > 0; o >>= 1) {
-    if (static_cast<int>(threadIdx.x) < o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) tot[b] = s[0];
-}
-
-// Block b: exclusive scan of bucket b's tile counts plus the bucket base (RsScanKernel's
-// shape, with the base given).
-__global__ void __launch_bounds__(kRsScanBlock) SplitScanKernel(uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                                const uint64_t* __restrict__ ftotal, const uint32_t* __restrict__ base) {
-  constexpr int kWaves = kRsScanBlock / 64;
-  constexpr int kU = 4;
-  __shared__ uint32_t s_w[kWaves];
-  const int t = threadIdx.x;
-  const uint32_t d = blockIdx.x;
-  if (d >= SplitNd(ftotal) + 2) return;
-  const int lane = t & 63, wid = t >> 6;
-  uint32_t* row = hist + static_cast<uint64_t>(d) * ntiles;
-  const uint32_t per = (ntiles + kWaves - 1) / kWaves;
-  const uint32_t q0 = min(ntiles, per * wid), q1 = min(ntiles, q0 + per);
-  uint32_t tot = 0;
-  for (uint32_t i = q0 + lane; i < q1; i += 64) tot += row[i];
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  if (lane == 0) s_w[wid] = tot;
-  __syncthreads();
-  uint32_t run = base[d];
-  for (int w = 0; w < wid; ++w) run += s_w[w];
-  for (uint32_t i0 = q0; i0 < q1; i0 += 64 * kU) {
-    uint32_t c[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t i = i0 + u * 64 + lane;
-      c[u] = i < q1 ? row[i] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      uint32_t incl = c[u];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      const uint32_t i = i0 + u * 64 + lane;
-      if (i < q1) row[i] = run + incl - c[u];
-      run += __shfl(incl, 63, 64);
-    }
-  }
-}
-
-// In-place exclusive scan of a[0..n) (n <= kSplitBuckets) by one block; a[n] = the total.
-__device__ __forceinline__ void SplitBlockScan(uint32_t* a, uint32_t n, uint32_t* s_w) {
-  constexpr int kPer = kSplitBuckets / kSplitBlock;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t i0 = threadIdx.x * kPer;
-  uint32_t v[kPer], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    v[k] = i0 + k < n ? a[i0 + k] : 0u;
-    sum += v[k];
-  }
-  uint32_t incl = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) s_w[wid] = incl;
-  __syncthreads();
-  uint32_t run = incl - sum;
-  for (int w = 0; w < wid; ++w) run += s_w[w];
-  if (threadIdx.x == kSplitBlock - 1) a[n] = run + sum;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    if (i0 + k < n) a[i0 + k] = run;
-    run += v[k];
-  }
-}
-
-// The scatter, kSplitSub records at a time: ranks per bucket (LDS atomics; the rest bucket's
-// once per wave), the sub-tile reordered by bucket in LDS, then written out in bucket runs
-// (consecutive threads -> consecutive addresses), so a wave's stores touch few lines.  Rest
-// records (their slot, values) go to the sort's input region [0, n_rest); the others' values go
-// straight to their final position.  Order inside a bucket is arrival order, like the staging's.
-__global__ void __launch_bounds__(kSplitBlock) SplitScatterKernel(const uint32_t* __restrict__ slot, ConstValPtrs vin, int nvals, uint64_t n,
-                                                                  uint32_t cap, const uint32_t* __restrict__ gslot,
-                                                                  const uint64_t* __restrict__ ftotal, uint32_t G,
-                                                                  const uint32_t* __restrict__ offs, uint32_t ntiles,
-                                                                  uint32_t* __restrict__ rkey, ValPtrs vrest, ValPtrs vout) {
-  __shared__ uint32_t hk[kSplitHash];
-  __shared__ uint16_t hv[kSplitHash];
-  __shared__ uint32_t cur[kSplitBuckets];
-  __shared__ uint32_t lst[kSplitBuckets + 1];
-  __shared__ uint64_t s_val[kSplitSub];
-  __shared__ uint32_t s_key[kSplitSub];
-  __shared__ uint16_t s_bkt[kSplitSub];
-  __shared__ uint32_t s_w[kSplitBlock / 64];
-  const uint32_t nd = SplitNd(ftotal), Gr = G - nd, nb = nd + 2;
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
-  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
-  for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) cur[b] = offs[static_cast<uint64_t>(b) * ntiles + tile];
-  SplitBuildMap(hk, hv, gslot, Gr, nd);
-  const uint64_t r0 = static_cast<uint64_t>(tile) * kSplitTile;
-  const uint64_t r1 = min(r0 + kSplitTile, n);
-  for (uint64_t sb = r0; sb < r1; sb += kSplitSub) {
-    uint32_t sv[kSplitItems], bk[kSplitItems], rk[kSplitItems];
-    uint64_t v0[kSplitItems];
-#pragma unroll
-    for (int u = 0; u < kSplitItems; ++u) {
-      const uint64_t i = sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x;
-      sv[u] = i < r1 ? slot[i] : 0u;
-      v0[u] = (nvals > 0 && i < r1) ? vin.p[0][i] : 0ULL;
-    }
-    for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) lst[b] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kSplitItems; ++u) {
-      const bool valid = sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x < r1;
-      bk[u] = valid ? SplitLookup(hk, hv, sv[u], cap, nd) : 0xFFFFu;
-      const bool rest = bk[u] == 0;
-      const unsigned long long m = __ballot(rest);
-      rk[u] = 0;
-      if (m) {
-        const int leader = __ffsll(static_cast<long long>(m)) - 1;
-        uint32_t wb = 0;
-        if (lane == leader) wb = atomicAdd(&lst[0], static_cast<uint32_t>(__popcll(m)));
-        wb = __shfl(wb, leader, 64);
-        rk[u] = wb + static_cast<uint32_t>(__popcll(m & lanemask_lt));
-      }
-      if (valid && !rest) rk[u] = atomicAdd(&lst[bk[u]], 1u);
-    }
-    __syncthreads();
-    SplitBlockScan(lst, nb, s_w);
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kSplitItems; ++u) {
-      if (bk[u] == 0xFFFFu) continue;
-      const uint32_t p = lst[bk[u]] + rk[u];
-      s_val[p] = v0[u];
-      s_bkt[p] = static_cast<uint16_t>(bk[u]);
-      s_key[p] = sv[u];
-    }
-    __syncthreads();
-    const uint32_t tn = lst[nb];
-    for (uint32_t j = threadIdx.x; j < tn; j += kSplitBlock) {
-      const uint32_t b = s_bkt[j];
-      const uint32_t dst = cur[b] + (j - lst[b]);
-      if (b == 0) {
-        rkey[dst] = s_key[j];
-        if (nvals > 0) vrest.p[0][dst] = s_val[j];
-      } else if (nvals > 0) {
-        vout.p[0][dst] = s_val[j];
-      }
-    }
-    for (int v = 1; v < nvals; ++v) {
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < kSplitItems; ++u) {
-        if (bk[u] == 0xFFFFu) continue;
-        s_val[lst[bk[u]] + rk[u]] = vin.p[v][sb + static_cast<uint64_t>(u) * kSplitBlock + threadIdx.x];
-      }
-      __syncthreads();
-      for (uint32_t j = threadIdx.x; j < tn; j += kSplitBlock) {
-        const uint32_t b = s_bkt[j];
-        const uint32_t dst = cur[b] + (j - lst[b]);
-        if (b == 0) vrest.p[v][dst] = s_val[j];
-        else vout.p[v][dst] = s_val[j];
-      }
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += kSplitBlock) cur[b] += lst[b + 1] - lst[b];
-    __syncthreads();
-  }
-}
-
-// gstart of the designated groups (and gstart[G]) from the bucket bases: gstart[Gr + j] =
-// base[1 + j] for j in [0, nd].
-__global__ void SplitGstartKernel(const uint32_t* __restrict__ base, const uint64_t* __restrict__ ftotal, uint32_t G,
-                                  uint32_t* __restrict__ gstart) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nd = SplitNd(ftotal);
-  if (j <= nd) gstart[G - nd + j] = base[1 + j];
-}
-
-// ---------------------------------------------------------------------------------------
-// Fused split (large aggregations): the staging split folded into the radix sort's first pass.
-// The largest groups by a sample (at most kFsMaxU, "designated" as in the split above) get one
-// bucket each in a 9-bit first pass whose other 256 buckets are the low digit of the remaining
-// ("rest") groups' ids: one stable pass leaves every designated group contiguous and final, and
-// the rest records sorted by their low digit, so only the rest records (~30 % at the north_star
-// size) go through the remaining pass(es).  Final layout [rest by id | designated by id | no
-// group], the same as the split's.  A 10-bit pass (767 designated groups, 73 % of the records at
-// 1B rows) measured slower: ~1000 partial-line runs per 3072-record tile outran the L2's write
-// combining (scatter 1.11 ms vs 0.83 ms with 512 buckets).
-// ---------------------------------------------------------------------------------------
-constexpr int kFsBits = 9;
-constexpr int kFsBuckets = 1 << kFsBits;          // 512
-constexpr int kFsRest = kRadixBuckets;            // buckets [0, 256): the rest's low digit
-constexpr uint32_t kFsMaxU = kFsBuckets - kFsRest - 1;  // designated buckets; the last one: no group
-constexpr int kFsBlock = 256;
-constexpr int kFsItems = 12;
-constexpr int kFsTile = kFsBlock * kFsItems;      // 3072 records
-static_assert(kFsBuckets % kFsBlock == 0, "buckets per thread");
-
-__device__ __forceinline__ uint32_t FsBucket(uint32_t id, uint32_t Gr, uint32_t G, uint32_t nd) {
-  return id < Gr ? (id & (kFsRest - 1)) : (id < G ? kFsRest + (id - Gr) : kFsRest + nd);
-}
-
-// Tile bucket counts -> hist[tile * kFsBuckets + b] (tile-major); the dense ids (newid[slot], G
-// for a record without a group) to dense_out for the scatter.
-template <int kHistTiles>
-__global__ void __launch_bounds__(kFsBlock) FsHistKernel(const uint32_t* __restrict__ slot, uint64_t n, const uint32_t* __restrict__ newid,
-                                                         uint32_t cap, uint32_t G, const uint64_t* __restrict__ ftotal,
-                                                         uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ dense_out) {
-  constexpr int kWaves = kFsBlock / 64;
-  __shared__ uint32_t h[kWaves][kFsBuckets];
-  const int wid = threadIdx.x >> 6;
-  const uint32_t nd = SplitNd(ftotal, kFsMaxU), Gr = G - nd;
-  const uint32_t tile0 = XcdRemap(blockIdx.x, gridDim.x) * kHistTiles;
-  const uint64_t base = static_cast<uint64_t>(tile0) * kFsTile;
-  const uint32_t rem = static_cast<uint32_t>(min(n - min(n, base), static_cast<uint64_t>(kHistTiles) * kFsTile));
-  const uint32_t* kp = slot + base;
-  uint32_t kk[kHistTiles][kFsItems];
-#pragma unroll
-  for (int j = 0; j < kHistTiles; ++j)
-#pragma unroll
-    for (int k = 0; k < kFsItems; ++k) {
-      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
-      kk[j][k] = i < rem ? kp[i] : 0u;
-    }
-#pragma unroll
-  for (int j = 0; j < kHistTiles; ++j)
-#pragma unroll
-    for (int k = 0; k < kFsItems; ++k) {
-      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
-      if (i < rem) {
-        kk[j][k] = kk[j][k] < cap ? newid[kk[j][k]] : G;
-        dense_out[base + i] = kk[j][k];
-      }
-    }
-#pragma unroll
-  for (int j = 0; j < kHistTiles; ++j) {
-    if (tile0 + j >= ntiles) break;  // uniform
-    for (int w = 0; w < kWaves; ++w)
-      for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) h[w][d] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kFsItems; ++k) {
-      const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
-      if (i < rem) atomicAdd(&h[wid][FsBucket(kk[j][k], Gr, G, nd)], 1u);
-    }
-    __syncthreads();
-    for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) {
-      uint32_t t = 0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) t += h[w][d];
-      hist[static_cast<uint64_t>(tile0 + j) * kFsBuckets + d] = t;
-    }
-    __syncthreads();
-  }
-}
-
-// Tile offsets of NB-bucket tile-major counts (the RsPart / RsPartScan / RsDown scheme for any
-// bucket count): per 16-tile range the bucket sums; per bucket the scan of the range sums and
-// the bucket total; the bucket bases (exclusive scan of the totals, base[NB] = the total); per
-// range the running offsets, in place.
-template <int NB>
-__global__ void __launch_bounds__(256) XPartKernel(const uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ part) {
-  const uint32_t w = blockIdx.x;
-  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
-  for (int d = threadIdx.x; d < NB; d += 256) {
-    uint32_t s = 0;
-    for (uint32_t t = t0; t < t1; ++t) s += hist[static_cast<uint64_t>(t) * NB + d];
-    part[static_cast<uint64_t>(w) * NB + d] = s;
-  }
-}
-template <int NB>
-__global__ void __launch_bounds__(kRsScanBlock) XPartScanKernel(uint32_t* __restrict__ part, uint32_t nparts, uint32_t* __restrict__ tot) {
-  constexpr int kWaves = kRsScanBlock / 64;
-  __shared__ uint32_t s_w[kWaves];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const uint32_t d = blockIdx.x;
-  uint32_t carry = 0;
-  for (uint32_t i0 = 0; i0 < nparts; i0 += kRsScanBlock) {
-    const uint32_t i = i0 + t;
-    const uint32_t c = i < nparts ? part[static_cast<uint64_t>(i) * NB + d] : 0u;
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t before = carry;
-    for (int w = 0; w < wid; ++w) before += s_w[w];
-    uint32_t round = 0;
-    for (int w = 0; w < kWaves; ++w) round += s_w[w];
-    if (i < nparts) part[static_cast<uint64_t>(i) * NB + d] = before + incl - c;
-    carry += round;
-    __syncthreads();
-  }
-  if (t == 0) tot[d] = carry;
-}
-template <int NB>
-__global__ void __launch_bounds__(256) XBaseKernel(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
-  constexpr int kPer = NB / 256;
-  __shared__ uint32_t s_w[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t v[kPer], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    v[k] = tot[threadIdx.x * kPer + k];
-    sum += v[k];
-  }
-  uint32_t incl = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) s_w[wid] = incl;
-  __syncthreads();
-  uint32_t run = incl - sum;
-  for (int w = 0; w < wid; ++w) run += s_w[w];
-  if (threadIdx.x == 255) base[NB] = run + sum;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    base[threadIdx.x * kPer + k] = run;
-    run += v[k];
-  }
-}
-template <int NB>
-__global__ void __launch_bounds__(256) XDownKernel(uint32_t* __restrict__ hist, uint32_t ntiles, const uint32_t* __restrict__ part,
-                                                   const uint32_t* __restrict__ base) {
-  const uint32_t w = blockIdx.x;
-  const uint32_t t0 = w * kRsTilesPerPart, t1 = min(ntiles, t0 + kRsTilesPerPart);
-  for (int d = threadIdx.x; d < NB; d += 256) {
-    uint32_t run = base[d] + part[static_cast<uint64_t>(w) * NB + d];
-    for (uint32_t t = t0; t < t1; ++t) {
-      uint32_t* h = hist + static_cast<uint64_t>(t) * NB + d;
-      const uint32_t c = *h;
-      *h = run;
-      run += c;
-    }
-  }
-}
-
-// The fused first pass (RsScatterKernel's scheme with 1024 buckets: 10-ballot wave ranks, the
-// tile reordered by bucket in LDS, bucket runs written out).  Rest records (key and values) go to
-// the rest sort's input [0, n_rest); designated records' values straight to their final position
-// in vfin; records without a group are not written (nothing reads past gstart[G]).
-__global__ void __launch_bounds__(kFsBlock) FsScatterKernel(const uint32_t* __restrict__ kin, uint64_t n, uint32_t G,
-                                                            const uint64_t* __restrict__ ftotal, ConstValPtrs vin, int nvals,
-                                                            const uint32_t* __restrict__ offs, uint32_t* __restrict__ kout, ValPtrs vrest,
-                                                            ValPtrs vfin) {
-  constexpr int kWaves = kFsBlock / 64;
-  constexpr int kPerWave = kFsTile / kWaves;
-  constexpr int kPerThr = kFsBuckets / kFsBlock;
-  __shared__ uint32_t whist[kWaves][kFsBuckets];
-  __shared__ uint32_t dstart[kFsBuckets];
-  __shared__ uint32_t gofs[kFsBuckets];
-  __shared__ uint64_t s_buf[kFsTile];
-  __shared__ uint16_t s_dig[kFsTile];
-  __shared__ uint32_t s_w[kWaves];
-  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_buf);
-  const uint32_t nd = SplitNd(ftotal, kFsMaxU), Gr = G - nd;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned long long lanemask_lt = (1ULL << lane) - 1;
-  const uint32_t tile = XcdRemap(blockIdx.x, gridDim.x);
-  for (int d = threadIdx.x; d < kFsBuckets; d += kFsBlock) {
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) whist[w][d] = 0;
-    gofs[d] = offs[static_cast<uint64_t>(tile) * kFsBuckets + d];
-  }
-  __syncthreads();
-  const uint64_t tile0 = static_cast<uint64_t>(tile) * kFsTile;
-  const uint64_t wbase = tile0 + static_cast<uint64_t>(wid) * kPerWave;
-  const int tn = static_cast<int>(min(static_cast<uint64_t>(kFsTile), n - tile0));
-  uint32_t part[kFsItems], keys[kFsItems], dig[kFsItems];
-  uint64_t v0[kFsItems];
-#pragma unroll
-  for (int k = 0; k < kFsItems; ++k) {
-    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-    keys[k] = i < n ? kin[i] : 0u;
-    v0[k] = (nvals > 0 && i < n) ? vin.p[0][i] : 0ULL;
-  }
-#pragma unroll
-  for (int k = 0; k < kFsItems; ++k) {
-    const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-    const bool valid = i < n;
-    const uint32_t d = FsBucket(keys[k], Gr, G, nd);
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < kFsBits; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(valid && bit);
-      peers &= bit ? m : ~m;
-    }
-    const uint32_t r = static_cast<uint32_t>(__popcll(peers & lanemask_lt));
-    const uint32_t pre = valid ? whist[wid][d] : 0u;
-    WaveSync();
-    if (valid && r == 0) whist[wid][d] = pre + static_cast<uint32_t>(__popcll(peers));
-    WaveSync();
-    part[k] = pre + r;
-    dig[k] = d;
-  }
-  __syncthreads();
-  {
-    // Bucket starts inside the tile: thread t owns buckets [t * kPerThr, (t + 1) * kPerThr).
-    uint32_t tot[kPerThr], sum = 0;
-#pragma unroll
-    for (int q = 0; q < kPerThr; ++q) {
-      const int d = threadIdx.x * kPerThr + q;
-      tot[q] = 0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) tot[q] += whist[w][d];
-      sum += tot[q];
-    }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t run = incl - sum;
-    for (int w = 0; w < wid; ++w) run += s_w[w];
-#pragma unroll
-    for (int q = 0; q < kPerThr; ++q) {
-      const int d = threadIdx.x * kPerThr + q;
-      dstart[d] = run;
-      uint32_t acc = run;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) {  // in place: whist[w][d] becomes the start of (w, d)
-        const uint32_t c = whist[w][d];
-        whist[w][d] = acc;
-        acc += c;
-      }
-      run += tot[q];
-    }
-  }
-  __syncthreads();
-  uint32_t lpos[kFsItems];
-#pragma unroll
-  for (int k = 0; k < kFsItems; ++k) {
-    lpos[k] = whist[wid][dig[k]] + part[k];
-    if (wbase + static_cast<uint64_t>(k) * 64 + lane < n) {
-      s_key[lpos[k]] = keys[k];
-      s_dig[lpos[k]] = static_cast<uint16_t>(dig[k]);
-    }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < tn; j += kFsBlock) {
-    const uint32_t d = s_dig[j];
-    if (d < static_cast<uint32_t>(kFsRest)) kout[gofs[d] + (j - dstart[d])] = s_key[j];
-  }
-  const uint32_t d_none = kFsRest + nd;
-  for (int v = 0; v < nvals; ++v) {
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kFsItems; ++k) {
-      const uint64_t i = wbase + static_cast<uint64_t>(k) * 64 + lane;
-      if (i < n) s_buf[lpos[k]] = v == 0 ? v0[k] : vin.p[v][i];
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < tn; j += kFsBlock) {
-      const uint32_t d = s_dig[j];
-      const uint32_t dst = gofs[d] + (j - dstart[d]);
-      if (d < static_cast<uint32_t>(kFsRest)) vrest.p[v][dst] = s_buf[j];
-      else if (d < d_none) vfin.p[v][dst] = s_buf[j];
-    }
-  }
-}
-
-// gstart of the designated groups and gstart[G]: gstart[Gr + j] = base[kFsRest + j], j <= nd.
-__global__ void FsGstartKernel(const uint32_t* __restrict__ base, const uint64_t* __restrict__ ftotal, uint32_t G,
-                               uint32_t* __restrict__ gstart) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nd = SplitNd(ftotal, kFsMaxU);
-  if (j <= nd) gstart[G - nd + j] = base[kFsRest + j];
-}
-
-int32_t RadixSortPairs(Ctx* ctx, const uint32_t* keys, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* vals,
-                       uint64_t n, RadixWs& ws, const uint32_t** skeys, const uint64_t** svals) {
-  for (int b = 0; b < 2; ++b) {
-    PXG_RETURN_IF_ERROR(ws.key[b].Ensure(n * 4 + 16));
-    PXG_RETURN_IF_ERROR(ws.val[b].Ensure(n * 8 + 16));
-  }
-  ConstValPtrs vin;
-  uint32_t* kbuf[2];
-  ValPtrs vbuf[2];
-  for (int v = 0; v < kMaxVals; ++v) {
-    vin.p[v] = nullptr;
-    vbuf[0].p[v] = vbuf[1].p[v] = nullptr;
-  }
-  vin.p[0] = vals;
-  for (int b = 0; b < 2; ++b) {
-    kbuf[b] = ws.key[b].as<uint32_t>();
-    vbuf[b].p[0] = ws.val[b].as<uint64_t>();
-  }
-  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, rank, cap, G, vin, 1, n, kbuf, vbuf, ws.rs, skeys, &vin));
-  *svals = vin.p[0];
-  return PXG_OK;
-}
-
-int32_t RadixSortBits(Ctx* ctx, const uint32_t* keys, int shift0, int nbits, const uint64_t* const* vals, int nvals, uint64_t n,
-                      DevBuf kb[2], DevBuf vb[2], RadixPassWs& ws, const uint32_t** skeys, const uint64_t** svals) {
-  if (nvals < 1 || nvals > kMaxVals) return SetError(PXG_INVALID_ARGUMENT, "radix sort of %d streams", nvals);
-  for (int b = 0; b < 2; ++b) {
-    PXG_RETURN_IF_ERROR(kb[b].Ensure(n * 4 + 16));
-    PXG_RETURN_IF_ERROR(vb[b].Ensure(n * 8 * nvals + 16));
-  }
-  ConstValPtrs vin;
-  uint32_t* kbuf[2];
-  ValPtrs vbuf[2];
-  for (int v = 0; v < kMaxVals; ++v) {
-    vin.p[v] = v < nvals ? vals[v] : nullptr;
-    for (int b = 0; b < 2; ++b) vbuf[b].p[v] = v < nvals ? vb[b].as<uint64_t>() + v * n : nullptr;
-  }
-  for (int b = 0; b < 2; ++b) kbuf[b] = kb[b].as<uint32_t>();
-  PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, keys, nullptr, 0, 0, vin, nvals, n, kbuf, vbuf, ws, skeys, &vin, shift0, nbits));
-  *svals = vin.p[0];  // stream v at *svals + v * n
-  return PXG_OK;
-}
-
-int32_t GroupStarts(Ctx* ctx, const uint32_t* skeys, uint64_t n, uint32_t G, uint32_t* gstart) {
-  return Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0, skeys, n, G, gstart);
-}
 
 // Side streams forked by finalize are joined back into the main stream on every exit path, so
 // an early error return never leaves side-stream kernels running on workspace buffers that a
@@ -3301,16 +2167,6 @@ struct SideJoinGuard {
   }
 };
 
-// Fused split for large aggregations (PXG_FSPLIT=0 / 1 overrides the size rule).
-// Measured (rocprof, same box): 1B rows (120M staged) finalize span 5.00 -> 4.84 ms; at C2 (12M
-// staged) the extra sample / designation launches cost what the shorter rest pass saves.
-constexpr uint64_t kFsMinStaged = uint64_t(1) << 25;
-constexpr uint32_t kFsMinRows = 4096;  // designate a group whose sampled estimate reaches this
-static bool FusedSplitOn(uint64_t n) {
-  const char* e = std::getenv("PXG_FSPLIT");
-  if (e && e[0]) return e[0] != '0';
-  return n >= kFsMinStaged;
-}
 
 int32_t AggFinalizeTable(Agg* a) {
   Ctx* ctx = a->ctx;
@@ -3325,21 +2181,16 @@ int32_t AggFinalizeTable(Agg* a) {
     return PXG_OK;
   }
   if (n >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "more than 2^32 staged rows in one aggregation");
-  // Streams the grouping moves: the plan's value streams, plus (owner of a merged exchange) the
-  // imported items' weights after them.
-  const int nvs = a->n_vals + (a->merged ? 1 : 0);
-  PXG_RETURN_IF_ERROR(ws.meta.Ensure(64));
+  // Streams the grouping moves: the plan's value streams.  The owner of a merged exchange moves
+  // only the quantile stream (the items; every other output comes from the merged accumulators,
+  // FinalizeMerged) and the items' weights: cv.p[x_qval] and cv.p[n_vals] after the grouping.
+  const bool mq = a->merged && a->x_qval >= 0;
+  const int nvs = a->merged ? (mq ? 2 : 1) : a->n_vals;
+  PXG_RETURN_IF_ERROR(ws.meta.Ensure(96));
   uint8_t* meta = ws.meta.as<uint8_t>();
   uint32_t* d_ngroups = reinterpret_cast<uint32_t*>(meta + 8);
   unsigned int* d_err = reinterpret_cast<unsigned int*>(meta + 16);
   uint32_t* d_cls = reinterpret_cast<uint32_t*>(meta + 32);
-  {
-    static const int diag = [] {
-      const char* e = std::getenv("PXG_DIAG_QUANT");
-      return e ? std::atoi(e) : 0;
-    }();
-    if (diag) PXG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_quant), &diag, sizeof(int)));
-  }
   PXG_RETURN_IF_ERROR(Launch(ctx, "finalize_init", FinalizeInitKernel, dim3(1), dim3(64), 0, meta, n));
 
   // 1. Dense group ids: rank of every occupied table slot (slot order).
@@ -3354,55 +2205,19 @@ int32_t AggFinalizeTable(Agg* a) {
   void* scan_tmp = ws.scan.p;
   PXG_RETURN_IF_ERROR(ws.rank.Ensure(static_cast<size_t>(a->cap) * 4 + 16));
   PXG_RETURN_IF_ERROR(ws.gslot.Ensure(static_cast<size_t>(ngroups) * 4));
-  // Large aggregations split the designated (sampled-large) groups out of the staging in one
-  // pass and radix-sort only the rest (SplitSampleKernel above).  PXG_SPLIT_MIN_ROWS /
-  // PXG_SPLIT_EST (tests) set the staged-row threshold and the designation estimate.
-  const uint64_t split_min_rows = [] {
-    const char* e = std::getenv("PXG_SPLIT_MIN_ROWS");
-    return e ? static_cast<uint64_t>(std::atoll(e)) : ~uint64_t(0);  // opt-in until it measures faster
-  }();
-  const uint32_t split_min_samples = [] {
-    const char* e = std::getenv("PXG_SPLIT_EST");
-    const uint64_t est = e ? static_cast<uint64_t>(std::atoll(e)) : kSplitMinRows;
-    return static_cast<uint32_t>(std::max<uint64_t>(1, est / kSplitStride));
-  }();
-  const bool split = n >= split_min_rows && ngroups >= 2;
-  // Fused split (FsHistKernel above): large aggregations whose radix sort needs more than one
-  // pass (PXG_FSPLIT=0 / 1 overrides).
+  // Fused split (pxg_group.hip): large aggregations whose radix sort needs more than one pass
+  // (PXG_FSPLIT=0 / 1: tests force it off / on).
   int gbits = 1;
   while ((uint64_t(1) << gbits) < static_cast<uint64_t>(ngroups) + 1) ++gbits;
-  const bool fsplit = !split && gbits > kRadixBits && FusedSplitOn(n);
-  const uint32_t max_big = fsplit ? kFsMaxU : kSplitMaxBig;
-  const uint32_t min_samples = fsplit ? std::max<uint32_t>(1, kFsMinRows / kSplitStride) : split_min_samples;
+  const bool fsplit = gbits > kRadixBits && FusedSplitOn(n);
   uint64_t* d_ftotal = nullptr;
-  if (!split && !fsplit) {
-    PXG_RETURN_IF_ERROR(Launch(ctx, "slot_flags", SlotFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                               a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, ws.rank.as<const uint32_t>(), ws.rank.as<uint32_t>(), a->cap, d_ngroups, scan_tmp));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "slot_gslot", SlotGslotKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                               a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<const uint32_t>(), ws.gslot.as<uint32_t>()));
+  if (!fsplit) {
+    PXG_RETURN_IF_ERROR(DenseIdsBySlot(ctx, a->slots.as<const unsigned long long>(), a->cap, ws.rank.as<uint32_t>(), ws.gslot.as<uint32_t>(),
+                                       d_ngroups, scan_tmp));
   } else {
-    PXG_RETURN_IF_ERROR(ws.split_cnt.Ensure(static_cast<size_t>(a->cap) * 4 + 32 * 4));
-    PXG_RETURN_IF_ERROR(ws.split_flags.Ensure((static_cast<size_t>(a->cap) + 2) * 8));
-    uint64_t* flags = ws.split_flags.as<uint64_t>();
-    d_ftotal = flags + a->cap;
-    uint32_t* lvl = ws.split_cnt.as<uint32_t>() + a->cap;
-    PXG_HIP(hipMemsetAsync(ws.split_cnt.p, 0, static_cast<size_t>(a->cap) * 4 + 32 * 4, ctx->stream));
-    const uint64_t nsamp = (n + kSplitStride - 1) / kSplitStride;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_sample", SplitSampleKernel, dim3(GridFor(static_cast<int64_t>(nsamp), 256 * kSamplePerThread, 1 << 30)),
-                               dim3(256), 0, a->st_slot.as<const uint32_t>(), n, a->cap, ws.split_cnt.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitLevelsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                               ws.split_cnt.as<const uint32_t>(), a->cap, lvl));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitFlagsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                               a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
-                               static_cast<const uint32_t*>(lvl), min_samples, max_big, flags));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU64(ctx, flags, flags, a->cap, d_ftotal, scan_tmp));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_ids", SplitIdsKernel, dim3(GridFor(a->cap, 256, 1 << 30)), dim3(256), 0,
-                               a->slots.as<const unsigned long long>(), a->cap, ws.split_cnt.as<const uint32_t>(),
-                               static_cast<const uint32_t*>(lvl), min_samples, max_big, static_cast<const uint64_t*>(flags), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.rank.as<uint32_t>(),
-                               ws.gslot.as<uint32_t>()));
-    // d_ngroups (the device's own group count, checked at the end) from the occupied total.
-    PXG_HIP(hipMemcpyAsync(d_ngroups, d_ftotal, 4, hipMemcpyDeviceToDevice, ctx->stream));
+    PXG_RETURN_IF_ERROR(DesignateLargeGroups(ctx, a->slots.as<const unsigned long long>(), a->cap, a->st_slot.as<const uint32_t>(), n,
+                                             ngroups, ws.split_cnt, ws.split_flags, ws.rank.as<uint32_t>(), ws.gslot.as<uint32_t>(),
+                                             d_ngroups, scan_tmp, &d_ftotal));
   }
 
   clk.Mark("finalize: dense ids");
@@ -3497,46 +2312,26 @@ int32_t AggFinalizeTable(Agg* a) {
     kbuf[b] = ws.skey[b].as<uint32_t>();
     for (int v = 0; v < kMaxVals; ++v) vbuf[b].p[v] = v < nvs ? ws.sval[b][v].as<uint64_t>() : nullptr;
   }
-  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals ? a->st_val[v].as<const uint64_t>() : nullptr;
-  if (a->merged) vin.p[a->n_vals] = a->st_wt.as<const uint64_t>();  // the imported items' weights ride along
+  for (int v = 0; v < kMaxVals; ++v) vin.p[v] = v < a->n_vals && !a->merged ? a->st_val[v].as<const uint64_t>() : nullptr;
+  if (a->merged) {  // [quantile items,] weights
+    if (mq) vin.p[0] = a->st_val[a->x_qval].as<const uint64_t>();
+    vin.p[mq ? 1 : 0] = a->st_wt.as<const uint64_t>();
+  }
   const uint32_t* kin = nullptr;
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
   if (fsplit) {
-    // 2''. The fused split: one 10-bit pass (designated groups final, rest records by their low
+    // 2''. The fused split: one 9-bit pass (designated groups final, rest records by their low
     //      digit), then the rest records' remaining pass(es) by the higher digits.  The pass
     //      count of the rest comes from G (an upper bound of the rest ids), so the buffer the
     //      rest sort ends in is known before the rest count comes back.
     const int p2 = (gbits - kRadixBits + kRadixBits - 1) / kRadixBits;
     const int fin = p2 == 0 ? 1 : (p2 - 1) & 1;
-    const uint32_t ntiles = static_cast<uint32_t>((n + kFsTile - 1) / kFsTile);
-    const uint32_t nparts = (ntiles + kRsTilesPerPart - 1) / kRsTilesPerPart;
-    PXG_RETURN_IF_ERROR(ws.split_hist.Ensure(static_cast<size_t>(ntiles) * kFsBuckets * 4));
-    PXG_RETURN_IF_ERROR(ws.rs.part.Ensure(static_cast<size_t>(nparts) * kFsBuckets * 4));
-    PXG_RETURN_IF_ERROR(ws.split_tot.Ensure(static_cast<size_t>(2 * kFsBuckets + 2) * 4));
-    PXG_RETURN_IF_ERROR(ws.fs_keys.Ensure(n * 4 + 16));
-    uint32_t* hist = ws.split_hist.as<uint32_t>();
-    uint32_t* tot = ws.split_tot.as<uint32_t>();
-    uint32_t* base = tot + kFsBuckets;
-    const int ht = ntiles >= 16384 ? 4 : 1;
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_hist_rank", ht == 4 ? FsHistKernel<4> : FsHistKernel<1>, dim3((ntiles + ht - 1) / ht),
-                               dim3(kFsBlock), 0, a->st_slot.as<const uint32_t>(), n, ws.rank.as<const uint32_t>(), a->cap, ngroups,
-                               static_cast<const uint64_t*>(d_ftotal), hist, ntiles, ws.fs_keys.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XPartKernel<kFsBuckets>, dim3(nparts), dim3(256), 0, static_cast<const uint32_t*>(hist), ntiles,
-                               ws.rs.part.as<uint32_t>()));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XPartScanKernel<kFsBuckets>, dim3(kFsBuckets), dim3(kRsScanBlock), 0, ws.rs.part.as<uint32_t>(),
-                               nparts, tot));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XBaseKernel<kFsBuckets>, dim3(1), dim3(256), 0, static_cast<const uint32_t*>(tot), base));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scan", XDownKernel<kFsBuckets>, dim3(nparts), dim3(256), 0, hist, ntiles,
-                               static_cast<const uint32_t*>(ws.rs.part.as<uint32_t>()), static_cast<const uint32_t*>(base)));
-    // n_rest (= base[kFsRest]) and the designated count to the host; the scatter runs meanwhile.
+    const uint32_t* base = nullptr;
+    PXG_RETURN_IF_ERROR(FusedSplitPass(ctx, a->st_slot.as<const uint32_t>(), n, ws.rank.as<const uint32_t>(), a->cap, ngroups,
+                                       static_cast<const uint64_t*>(d_ftotal), vin, nvs, ws.split_hist, ws.split_tot, ws.fs_keys, ws.rs,
+                                       kbuf[1], vbuf[1], vbuf[fin], &base));
     uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
-    PXG_HIP(hipMemcpyAsync(pin + 104, base + kFsRest, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipMemcpyAsync(pin + 112, d_ftotal, 8, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipEventRecord(ctx->ev_split, ctx->stream));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "radix_scatter", FsScatterKernel, dim3(ntiles), dim3(kFsBlock), 0, static_cast<const uint32_t*>(ws.fs_keys.as<uint32_t>()),
-                               n, ngroups, static_cast<const uint64_t*>(d_ftotal), vin, nvs, static_cast<const uint32_t*>(hist), kbuf[1], vbuf[1],
-                               vbuf[fin]));
     PXG_RETURN_IF_ERROR(IssueKeys());
     PXG_HIP(hipEventSynchronize(ctx->ev_split));
     uint32_t n_rest = 0;
@@ -3554,74 +2349,24 @@ int32_t AggFinalizeTable(Agg* a) {
         PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], nullptr, 0, Gr, rin, nvs, n_rest, kbuf, vbuf, ws.rs, &rkeys, &rout, kRadixBits,
                                              p2 * kRadixBits));
       }
-      PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n_rest), 256, 1 << 30)), dim3(256), 0,
-                                 rkeys, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
+      PXG_RETURN_IF_ERROR(GroupStarts(ctx, rkeys, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
     }
-    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", FsGstartKernel, dim3((kFsMaxU + 256) / 256), dim3(256), 0, static_cast<const uint32_t*>(base),
-                               static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
-  } else if (!split) {
+    PXG_RETURN_IF_ERROR(FusedSplitGstart(ctx, base, static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
+  } else {
     PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, a->st_slot.as<const uint32_t>(), ws.rank.as<const uint32_t>(), a->cap, ngroups, vin, nvs,
                                          n, kbuf, vbuf, ws.rs, &kin, &vin));
     PXG_RETURN_IF_ERROR(IssueKeys());
     const uint32_t* skeys = kin;  // sorted dense ids; vin = the values in the same order
     // 3. Group starts (first index of every id).
-    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n), 256, 1 << 30)), dim3(256), 0,
-                               skeys, n, ngroups, ws.gstart.as<uint32_t>()));
-  } else {
-    // 2'. The split: bucket counts per tile, bucket bases, tile offsets, one scatter; then the
-    //     radix sort of the rest records only.  The rest records' input goes to buffer 1 and the
-    //     designated records straight to the buffer the sort ends in (its pass count comes from
-    //     G, an upper bound of the rest ids), at [n_rest, n): the two never overlap.
-    int nbits = 1;
-    while ((uint64_t(1) << nbits) < static_cast<uint64_t>(ngroups) + 1) ++nbits;
-    const int passes = (nbits + kRadixBits - 1) / kRadixBits;
-    const int fin = (passes - 1) & 1;
-    const uint32_t ntiles = static_cast<uint32_t>((n + kSplitTile - 1) / kSplitTile);
-    PXG_RETURN_IF_ERROR(ws.split_hist.Ensure(static_cast<size_t>(kSplitBuckets) * ntiles * 4));
-    PXG_RETURN_IF_ERROR(ws.split_tot.Ensure(static_cast<size_t>(2 * kSplitBuckets + 2) * 4));
-    uint32_t* tot = ws.split_tot.as<uint32_t>();
-    uint32_t* base = tot + kSplitBuckets + 1;
-    uint32_t* hist = ws.split_hist.as<uint32_t>();
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_hist", SplitHistKernel, dim3(ntiles), dim3(kSplitBlock), 0, a->st_slot.as<const uint32_t>(), n,
-                               a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups, hist, ntiles));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scan", SplitTotalKernel, dim3(kSplitBuckets), dim3(kRsScanBlock), 0,
-                               static_cast<const uint32_t*>(hist), ntiles, static_cast<const uint64_t*>(d_ftotal), tot));
-    PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, tot, base, kSplitBuckets, base + kSplitBuckets, scan_tmp));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scan", SplitScanKernel, dim3(kSplitBuckets), dim3(kRsScanBlock), 0, hist, ntiles,
-                               static_cast<const uint64_t*>(d_ftotal), static_cast<const uint32_t*>(base)));
-    // n_rest (= base[1]) and the designated count to the host; the scatter runs meanwhile.
-    uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
-    PXG_HIP(hipMemcpyAsync(pin + 104, base + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipMemcpyAsync(pin + 112, d_ftotal, 8, hipMemcpyDeviceToHost, ctx->stream));
-    PXG_HIP(hipEventRecord(ctx->ev_split, ctx->stream));
-    ValPtrs vrest = vbuf[1], vout = vbuf[fin];
-    PXG_RETURN_IF_ERROR(Launch(ctx, "split_scatter", SplitScatterKernel, dim3(ntiles), dim3(kSplitBlock), 0, a->st_slot.as<const uint32_t>(),
-                               vin, nvs, n, a->cap, ws.gslot.as<const uint32_t>(), static_cast<const uint64_t*>(d_ftotal), ngroups,
-                               static_cast<const uint32_t*>(hist), ntiles, kbuf[1], vrest, vout));
-    PXG_RETURN_IF_ERROR(IssueKeys());
-    clk.Mark("finalize: issue split");
-    PXG_HIP(hipEventSynchronize(ctx->ev_split));
-    clk.Mark("finalize: split wait");
-    uint32_t n_rest = 0;
-    uint64_t ft = 0;
-    std::memcpy(&n_rest, pin + 104, 4);
-    std::memcpy(&ft, pin + 112, 8);
-    const uint32_t nd = std::min<uint32_t>(static_cast<uint32_t>(ft >> 32), kSplitMaxBig);
-    const uint32_t Gr = ngroups - nd;
-    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vout.p[v];
-    if (n_rest > 0) {
-      ConstValPtrs rin;
-      for (int v = 0; v < kMaxVals; ++v) rin.p[v] = vrest.p[v];
-      // the rest records carry their slots: the first pass maps them to rest ids (< Gr)
-      PXG_RETURN_IF_ERROR(RadixSortStreams(ctx, kbuf[1], ws.rank.as<const uint32_t>(), a->cap, ngroups, rin, nvs, n_rest, kbuf, vbuf,
-                                           ws.rs, &kin, &vin));
-      PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", GroupHeadsKernel, dim3(GridFor(static_cast<int64_t>(n_rest), 256, 1 << 30)), dim3(256), 0,
-                                 kin, static_cast<uint64_t>(n_rest), Gr, ws.gstart.as<uint32_t>()));
-    }
-    PXG_RETURN_IF_ERROR(Launch(ctx, "group_heads", SplitGstartKernel, dim3((kSplitMaxBig + 256) / 256), dim3(256), 0,
-                               static_cast<const uint32_t*>(base), static_cast<const uint64_t*>(d_ftotal), ngroups, ws.gstart.as<uint32_t>()));
+    PXG_RETURN_IF_ERROR(GroupStarts(ctx, skeys, n, ngroups, ws.gstart.as<uint32_t>()));
   }
   clk.Mark("finalize: grouping issued");
+  if (a->merged) {  // back to stream numbering: the quantile stream at x_qval, the weights at n_vals
+    const ConstValPtrs sorted = vin;
+    for (int v = 0; v < kMaxVals; ++v) vin.p[v] = nullptr;
+    if (mq) vin.p[a->x_qval] = sorted.p[0];
+    vin.p[a->n_vals] = sorted.p[mq ? 1 : 0];
+  }
   // 3. UDA reductions (chunk partials, then per-group combine).
   const ConstValPtrs cv = vin;
   UdaOut uo;
@@ -3630,7 +2375,7 @@ int32_t AggFinalizeTable(Agg* a) {
   for (int u = 0; u < a->n_udas; ++u) {
     const bool q = a->uda_kind[u] == PXG_UDA_QUANTILES;
     any_q |= q;
-    any_red |= !q && a->uda_kind[u] != PXG_UDA_COUNT;
+    any_red |= !q && a->uda_kind[u] != PXG_UDA_COUNT && !a->merged;  // (merged: from the accumulators)
     PXG_RETURN_IF_ERROR(R.uda_out[u].Ensure(static_cast<size_t>(ngroups) * (q ? 7 * 8 : 8)));
     uo.p[u] = R.uda_out[u].as<uint64_t>();
   }
@@ -3669,9 +2414,10 @@ int32_t AggFinalizeTable(Agg* a) {
     states = ws.xstates.as<uint8_t>();
     cplan = a->d_plan_x.as<const AggPlanDev>();
   }
-  PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
-                             cplan, gstart, static_cast<const uint32_t*>(cbase), ngroups,
-                             ws.partial.as<const uint64_t>(), max_chunks, uo, states));
+  if (!a->merged)  // (a merged run's outputs come from its accumulators: XFinalizeStatesKernel)
+    PXG_RETURN_IF_ERROR(Launch(ctx, "group_combine", GroupCombineKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0,
+                               cplan, gstart, static_cast<const uint32_t*>(cbase), ngroups,
+                               ws.partial.as<const uint64_t>(), max_chunks, uo, states));
   clk.Mark("finalize: red kernels");
   if (a->early.want && !states && !a->merged && !a->export_x) {  // early result: the combined values
     bool ok = true;
@@ -3742,19 +2488,12 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(n_big_groups),
                                  dim3(kSelSample / 2 / kMsIpt), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
                                  vals, at, ws.sel_spl.as<uint64_t>(), guide, nullptr, nullptr));
-    if (big_max > kSelLargeN) {  // only the groups BigSetup listed (<= n / 2^22 of them)
-      const uint64_t bcap = n / (kMidMax + 1) + 1;  // as big_cap below
-      const uint32_t* lcnt = reinterpret_cast<const uint32_t*>(ws.big.as<const uint8_t>() + bcap * sizeof(BigGroup));
-      const uint32_t n_large = static_cast<uint32_t>(std::min<uint64_t>(nb, n / (kSelLargeN + 1) + 1));
-      PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_large),
-                                   dim3(kSelSampleThreads), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
-                                   vals, at, ws.sel_spl.as<uint64_t>(), guide, lcnt + 4, lcnt));
-    }
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, SelHistCap());
+    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, kSelHistCap);
     return LaunchOn(ctx, ctx->side2, "quant_sel_hist", at == PXG_FLOAT64 ? BigHistKernel<true> : BigHistKernel<false>,
                     dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                     ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
-                    static_cast<const uint16_t*>(guide), ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb);
+                    static_cast<const uint16_t*>(guide), ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb,
+                    ws.sel_bin.as<uint16_t>());
   };
   // Second half, after the chains: plan, gather + inside sums, bin sorts, digests.
   auto BigSelectBack = [&](int u) -> int32_t {
@@ -3776,8 +2515,7 @@ int32_t AggFinalizeTable(Agg* a) {
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", at == PXG_FLOAT64 ? BigCollectKernel<true> : BigCollectKernel<false>,
                                  dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
                                  ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
-                                 vals, at, ws.sel_spl.as<const uint64_t>(),
-                                 reinterpret_cast<const uint16_t*>(ws.sel_spl.as<const uint64_t>() + nb * kSelBins), ws.sel_tag.as<const uint8_t>(),
+                                 vals, at, ws.sel_bin.as<const uint16_t>(), ws.sel_tag.as<const uint8_t>(),
                                  ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>(), cpb));
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel,
                                  dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0,
@@ -3801,13 +2539,14 @@ int32_t AggFinalizeTable(Agg* a) {
   bool big_select = false;
   // 4. Quantile digests.
   if (any_q) {
-    PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kNumClasses * 4));
+    PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kAllClasses * 4));
     // A merged exchange's groups that received centroid lists get their quantiles from the
     // merged digest (FinalizeMerged): no class here, so the selection path never sees their
     // centroid means as values (which made it fall back to the full sort).
     const bool skip_merged = a->merged && a->macc_cap == a->cap;
     PXG_RETURN_IF_ERROR(Launch(ctx, "classify_groups", ClassifyGroupsKernel, dim3(GridFor(ngroups, 256, 1 << 30)), dim3(256), 0, gstart,
-                               ngroups, ws.lists.as<uint32_t>(), d_cls, static_cast<uint32_t>(kMidMax),
+                               ngroups, ws.lists.as<uint32_t>(), d_cls, reinterpret_cast<uint32_t*>(meta + 64),
+                               a->export_x ? static_cast<uint32_t>(kMidMax) : kMidClassMax,
                                skip_merged ? a->macc.as<const uint64_t>() : nullptr, a->macc_words,
                                ws.gslot.as<const uint32_t>()));
     const uint32_t* lists = ws.lists.as<const uint32_t>();
@@ -3828,6 +2567,7 @@ int32_t AggFinalizeTable(Agg* a) {
     clk.Mark("finalize: classes issued");
     uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
     PXG_HIP(hipMemcpyAsync(pin + 64, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
+    PXG_HIP(hipMemcpyAsync(pin + 88, meta + 64, 4 * kNumMidSub, hipMemcpyDeviceToHost, ctx->stream));  // mid classes 4-6
     PXG_HIP(hipEventRecord(ctx->ev_meta, ctx->stream));
     // Kernels whose work lists are counted on the device launch right away with upper-bound
     // grids (blocks past the device count exit); the host reads the counts back only after
@@ -3867,11 +2607,12 @@ int32_t AggFinalizeTable(Agg* a) {
                                  static_cast<const uint32_t*>(d_cls), gstart, cv.p[a->uda_val[u]], a->uda_arg_type[u],
                                  R.uda_out[u].as<double>()));
     }
-    uint32_t hm[6];
+    uint32_t hm[6], hmid[kNumMidSub];
     clk.Mark("finalize: issue to meta");
     PXG_HIP(hipEventSynchronize(ctx->ev_meta));
     clk.Mark("finalize: meta wait");
     std::memcpy(hm, pin + 64, 24);
+    std::memcpy(hmid, pin + 88, 4 * kNumMidSub);
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3];
     n_big_groups = n_big;
@@ -3891,6 +2632,7 @@ int32_t AggFinalizeTable(Agg* a) {
       PXG_RETURN_IF_ERROR(ws.sel_cbase.Ensure(static_cast<size_t>(n_big) * kSelBins * 4));
       PXG_RETURN_IF_ERROR(ws.sel_plan.Ensure(static_cast<size_t>(n_big) * sizeof(BigPlan)));
       PXG_RETURN_IF_ERROR(ws.sel_partial.Ensure(static_cast<size_t>(n_bchunks) * kSelMaxRanges * 8 + 16));
+      PXG_RETURN_IF_ERROR(ws.sel_bin.Ensure(n * 2 + 16));  // per staged value its bin (BigHist -> BigCollect)
     }
     // Big groups on side stream 2, overlapping the mid digests and the key output on the main
     // stream: the selection path's sample + bin counts start right after the metadata readback,
@@ -3910,10 +2652,21 @@ int32_t AggFinalizeTable(Agg* a) {
         PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(u) : BigSortPath(ctx->side2, u));
       }
       double* qo = R.uda_out[u].as<double>();
-      if (cls[2] > 0 && !a->export_x)
-        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel, dim3(cls[2]), dim3(256), 0, lists + 2 * static_cast<uint64_t>(ngroups),
-                                   gstart, MidChainStarts(ctx), MidChainNc(ctx), static_cast<const uint32_t*>(d_cls + 2), vals, at, qo,
-                                   d_err));
+      if (!a->export_x) {  // the mid classes, one launch each (largest first: the longest workgroups)
+        const uint32_t* cnt_mid = reinterpret_cast<const uint32_t*>(meta + 64);
+        if (hmid[1] > 0)
+          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel<8192>, dim3(hmid[1]), dim3(8192 / kMsIpt), 0,
+                                     lists + 5 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
+                                     cnt_mid + 1, vals, at, qo, d_err));
+        if (hmid[0] > 0)
+          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel<4096>, dim3(hmid[0]), dim3(4096 / kMsIpt), 0,
+                                     lists + 4 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
+                                     cnt_mid, vals, at, qo, d_err));
+        if (cls[2] > 0)  // on the side stream, behind the small digests (it idles from there on)
+          PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "quant_mid", QuantMidKernel<2048>, dim3(cls[2]), dim3(2048 / kMsIpt), 0,
+                                       lists + 2 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
+                                       static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
+      }
     }
   }
   if (guard.side) PXG_RETURN_IF_ERROR(JoinSide(ctx));  // the small digests
@@ -3928,6 +2681,8 @@ int32_t AggFinalizeTable(Agg* a) {
     a->x_wts = nullptr;
     a->x_nbig = n_big_groups;
     a->last_big_sort_groups = n_big_groups;
+    a->x_check_pending = true;
+    a->x_check_groups = ngroups;
     R.ready = true;
     return PXG_OK;
   }
@@ -3951,29 +2706,6 @@ int32_t AggFinalizeTable(Agg* a) {
   g_dev = pin32[kMaxKeys + 1];
   const uint32_t n_fallback = big_select ? pin32[kMaxKeys + 2] : 0;
   a->last_big_sort_groups = big_select ? n_fallback : n_big_groups;
-  if (big_select && EnvFlag("PXG_DIAG_SEL")) {  // selection-path shape (tools/; one extra sync)
-    std::vector<BigPlan> plans(n_big_groups);
-    std::vector<uint32_t> hh(static_cast<size_t>(n_big_groups) * kSelBins);
-    std::vector<BigGroup> gg(n_big_groups);
-    PXG_HIP(hipMemcpy(plans.data(), ws.sel_plan.p, plans.size() * sizeof(BigPlan), hipMemcpyDeviceToHost));
-    PXG_HIP(hipMemcpy(hh.data(), ws.sel_cnt.p, hh.size() * 4, hipMemcpyDeviceToHost));
-    PXG_HIP(hipMemcpy(gg.data(), ws.big.p, gg.size() * sizeof(BigGroup), hipMemcpyDeviceToHost));
-    uint64_t coll = 0, cand = 0, big_bins = 0, maxbin = 0, rows = 0;
-    for (uint32_t i = 0; i < n_big_groups; ++i) {
-      rows += gg[i].n;
-      if (plans[i].fallback) continue;
-      coll += plans[i].n_coll;
-      for (int c = 0; c < plans[i].n_coll && c < kSelMaxColl; ++c) {
-        const uint32_t h = hh[static_cast<size_t>(i) * kSelBins + plans[i].coll[c]];
-        cand += h;
-        big_bins += h > static_cast<uint32_t>(kWaveSortMax) ? 1 : 0;
-        maxbin = std::max<uint64_t>(maxbin, h);
-      }
-    }
-    std::fprintf(stderr, "[pxg sel] big groups %u (%llu rows), chunks %u, fallback %u, gathered bins %llu (%llu values, %llu > %d, max %llu)\n",
-                 n_big_groups, (unsigned long long)rows, n_bchunks, n_fallback, (unsigned long long)coll, (unsigned long long)cand,
-                 (unsigned long long)big_bins, kWaveSortMax, (unsigned long long)maxbin);
-  }
   if (big_select && n_fallback > 0) {
     // Some big group could not be served by selection (NaN values, heavy duplicates): the full
     // sort path recomputes every big group's quantiles (the chains are long done).

@@ -54,10 +54,21 @@ struct HcAggPlan {
 
 struct HcOut {
   uint64_t* uda[kMaxUdas];
+  uint8_t* states;           // export: each group's Serialize() states (srec bytes) instead of uda[]
+  int32_t srec, soff[kMaxUdas];
   uint64_t* kfix[kMaxKeys];  // fixed-width keys (UINT128: 2 words per group, BOOLEAN: bytes)
   uint32_t* klen[kMaxKeys];  // STRING: lengths, turned into offsets by the scan
   uint64_t* kscr;            // the representative's key words, kwords per group (STRING keys), or null
   uint32_t g0;               // groups the table path already wrote
+};
+
+// FinalizeHc in export mode (ExportHcGroups): per partition group its Serialize() states at
+// states + g * state_rec and its key words in the scratch (word j at kscr[j * plan.n + g]).
+struct HcExport {
+  uint8_t* states = nullptr;
+  uint32_t groups = 0;
+  const uint64_t* kscr = nullptr;
+  HcAggPlan plan{};
 };
 
 // starts[p] = first sorted record of partition p (p in [0, P]); partition = key >> shift.
@@ -83,6 +94,7 @@ __device__ __forceinline__ void HcEmitKeys(const HcAggPlan& hp, const HcOut& out
 #pragma unroll
     for (int j = 0; j < KW; ++j) out.kscr[static_cast<uint64_t>(j) * hp.n + l] = w[j];
   }
+  if (out.states) return;  // export: the key words are all it needs
 #pragma unroll
   for (int k = 0; k < kMaxKeys; ++k) {
     if (k >= hp.nk) break;
@@ -120,6 +132,29 @@ __device__ __forceinline__ double WideToDouble(int64_t hi, uint64_t lo) {
 // accumulates the same values in a double; both agree to rounding, and neither wraps).
 __device__ __forceinline__ void HcEmitVals(const HcAggPlan& hp, const HcOut& out, uint32_t g, uint32_t cnt, const unsigned long long* s_acc,
                                            int slot) {
+  if (out.states) {  // export: Serialize() states (math_ops.h:583-772; MeanInfo {size, sum})
+    uint8_t* st = out.states + static_cast<uint64_t>(g) * out.srec;
+    for (int u = 0; u < hp.n_udas; ++u) {
+      const int a = hp.uda_acc[u];
+      const unsigned long long acc = a >= 0 ? s_acc[a * kHcTable + slot] : 0ULL;
+      uint64_t v0 = acc, v1 = 0;
+      switch (hp.uda_kind[u]) {
+        case PXG_UDA_COUNT: v0 = cnt; break;
+        case PXG_UDA_MEAN: {
+          const int hi = a >= 0 ? hp.acc_hi[a] : -1;
+          const int64_t h = hi >= 0 ? static_cast<int64_t>(s_acc[hi * kHcTable + slot]) : (static_cast<int64_t>(acc) >> 63);
+          v0 = cnt;
+          v1 = FBits(WideToDouble(h, acc));
+          break;
+        }
+        case PXG_UDA_SUM: v0 = acc + static_cast<uint64_t>(hp.uda_init[u]); break;
+        default: break;  // MIN / MAX (integer)
+      }
+      __builtin_memcpy(st + out.soff[u], &v0, 8);
+      if (hp.uda_kind[u] == PXG_UDA_MEAN) __builtin_memcpy(st + out.soff[u] + 8, &v1, 8);
+    }
+    return;
+  }
   for (int u = 0; u < hp.n_udas; ++u) {
     const int a = hp.uda_acc[u];
     const unsigned long long acc = a >= 0 ? s_acc[a * kHcTable + slot] : 0ULL;
@@ -444,13 +479,14 @@ static HcAggPlan MakeHcPlan(const Agg& a, bool compact = false, int32_t* src = n
   return hp;
 }
 
-int32_t Agg::FinalizeHc() {
+int32_t Agg::FinalizeHc(HcExport* ex) {
   AggResult& R = res;
   const uint64_t n = hc_n;
-  const uint32_t g0 = static_cast<uint32_t>(R.n_groups);
-  R.ready = false;
+  const uint32_t g0 = ex ? 0u : static_cast<uint32_t>(R.n_groups);
+  if (ex) ex->groups = 0;
+  if (!ex) R.ready = false;
   if (n == 0) {
-    R.ready = true;
+    if (!ex) R.ready = true;
     return PXG_OK;
   }
   int32_t src[kHcMaxStride];
@@ -464,8 +500,8 @@ int32_t Agg::FinalizeHc() {
   // Result buffers for up to n more groups, keeping the table path's g0 groups.
   const uint64_t cap_g = static_cast<uint64_t>(g0) + n;
   uint64_t dbase[kMaxKeys] = {0};
-  for (int u = 0; u < n_udas; ++u) PXG_RETURN_IF_ERROR(R.uda_out[u].Reserve(cap_g * 8, static_cast<size_t>(g0) * 8, ctx->stream));
-  for (int k = 0; k < n_keys; ++k) {
+  for (int u = 0; u < n_udas && !ex; ++u) PXG_RETURN_IF_ERROR(R.uda_out[u].Reserve(cap_g * 8, static_cast<size_t>(g0) * 8, ctx->stream));
+  for (int k = 0; k < n_keys && !ex; ++k) {
     const int t = key_types[k];
     if (t == PXG_STRING) {
       dbase[k] = static_cast<uint64_t>(R.key_data_len[k]);
@@ -480,14 +516,20 @@ int32_t Agg::FinalizeHc() {
     if (dbase[k] + n * 8 * kHcStrWords >= (uint64_t(1) << 31)) return SetError(PXG_UNIMPLEMENTED, "string key column over 2 GiB");
   HcOut out;
   std::memset(&out, 0, sizeof(out));
-  for (int u = 0; u < n_udas; ++u) out.uda[u] = R.uda_out[u].as<uint64_t>();
-  for (int k = 0; k < n_keys; ++k) {
-    if (key_types[k] == PXG_STRING) out.klen[k] = R.key_offsets[k].as<uint32_t>();
-    else out.kfix[k] = R.key_fixed[k].as<uint64_t>();
+  if (ex) {
+    out.states = ex->states;
+    out.srec = hplan_x.state_rec;
+    for (int u = 0; u < n_udas; ++u) out.soff[u] = hplan_x.state_off[u];
+  } else {
+    for (int u = 0; u < n_udas; ++u) out.uda[u] = R.uda_out[u].as<uint64_t>();
+    for (int k = 0; k < n_keys; ++k) {
+      if (key_types[k] == PXG_STRING) out.klen[k] = R.key_offsets[k].as<uint32_t>();
+      else out.kfix[k] = R.key_fixed[k].as<uint64_t>();
+    }
   }
   bool any_str_key = false;
   for (int k = 0; k < n_keys; ++k) any_str_key = any_str_key || key_types[k] == PXG_STRING;
-  if (any_str_key) {
+  if (any_str_key || ex) {  // (an export rebuilds every group's key record from the scratch)
     PXG_RETURN_IF_ERROR(w.hc_kscr.Ensure(n * static_cast<uint64_t>(hp.kwords) * 8 + 16));
     out.kscr = w.hc_kscr.as<uint64_t>();
   }
@@ -533,6 +575,12 @@ int32_t Agg::FinalizeHc() {
     ++last_hc_reruns;
   }
   last_hc_pbits = pbits;
+  if (ex) {
+    ex->groups = G;
+    ex->kscr = out.kscr;
+    ex->plan = hp;
+    return PXG_OK;
+  }
   // String keys: lengths -> offsets (scan), then the bytes.
   bool any_str = false;
   HcKeyCopy kc;
@@ -715,6 +763,65 @@ int32_t Agg::SpillHc() {
   if (err) return SetError(PXG_INTERNAL, "group table full while spilling partition records");
   inserted = groups;
   state_version++;
+  return PXG_OK;
+}
+
+// Export of a high-cardinality run without the spill: the partition groups are aggregated as in
+// FinalizeHc (states instead of results), and each group's key record is rebuilt from the key
+// scratch into the arena past its live words; eslots[g_table + l] names it (arena word offset,
+// as a table slot word would).  The export then treats table groups and partition groups alike.
+__global__ void __launch_bounds__(256) HcGroupArenaKernel(HcAggPlan hp, const uint64_t* __restrict__ kscr, uint32_t G, int32_t rec_words,
+                                                          uint64_t abase, uint64_t* __restrict__ arena, unsigned long long* __restrict__ eslots) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= G) return;
+  const uint64_t n = hp.n;
+  const uint64_t lens = kscr[l];
+  const uint64_t at = abase + static_cast<uint64_t>(l) * rec_words;
+  uint64_t* ar = arena + at;
+  int wo = 0;
+  for (int k = 0; k < hp.nk; ++k) {
+    const int t = hp.ktype[k];
+    const uint64_t* kw = kscr + static_cast<uint64_t>(hp.koff[k]) * n + l;
+    if (t == PXG_STRING) {
+      const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
+      ar[wo] = len;
+      const int nw = static_cast<int>((len + 7) >> 3);
+      for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j * n];
+      wo += 1 + nw;
+    } else if (t == PXG_UINT128) {
+      ar[wo] = kw[0];
+      ar[wo + 1] = kw[n];
+      wo += 2;
+    } else {
+      ar[wo] = kw[0];
+      wo += 1;
+    }
+  }
+  eslots[l] = at;
+}
+
+int32_t Agg::ExportHcGroups(uint32_t g_table, DevBuf* states, DevBuf* eslots, uint32_t* n_hc, uint64_t* key_words) {
+  *n_hc = 0;
+  *key_words = 0;
+  if (!hc_active || hc_n == 0) return PXG_OK;
+  const uint64_t srec = static_cast<uint64_t>(hplan_x.state_rec);
+  PXG_RETURN_IF_ERROR(states->Reserve((static_cast<uint64_t>(g_table) + hc_n) * srec + 16, static_cast<uint64_t>(g_table) * srec, ctx->stream));
+  HcExport ex;
+  ex.states = states->as<uint8_t>() + static_cast<uint64_t>(g_table) * srec;
+  PXG_RETURN_IF_ERROR(FinalizeHc(&ex));
+  const uint32_t G = ex.groups;
+  if (G == 0) return PXG_OK;
+  int32_t rec_words = 0;
+  for (int k = 0; k < n_keys; ++k) rec_words += key_types[k] == PXG_STRING ? 1 + kHcStrWords : hc_layout.kw[k];
+  const uint64_t abase = arena_words;
+  if (abase + static_cast<uint64_t>(G) * rec_words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
+  // Scratch past the live words: arena_words is not advanced (the records serve this export only).
+  PXG_RETURN_IF_ERROR(arena.Reserve((abase + static_cast<uint64_t>(G) * rec_words) * 8 + kArenaSlack, abase * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(eslots->Reserve((static_cast<uint64_t>(g_table) + G) * 8 + 16, static_cast<uint64_t>(g_table) * 8, ctx->stream));
+  PXG_RETURN_IF_ERROR(Launch(ctx, "hc_export_keys", HcGroupArenaKernel, dim3(GridFor(G, 256, 1 << 30)), dim3(256), 0, ex.plan, ex.kscr, G, rec_words,
+                             abase, arena.as<uint64_t>(), eslots->as<unsigned long long>() + g_table));
+  *n_hc = G;
+  *key_words = static_cast<uint64_t>(G) * rec_words;
   return PXG_OK;
 }
 

@@ -190,20 +190,12 @@ struct HostClock {
   }
 };
 
-// Timing-only diagnosis (PXG_DIAG_SERIAL=1, tools/): every kernel launches on the main stream,
-// in issue order, so a kernel trace shows each kernel's duration without the side streams'
-// kernels sharing the chip.  Never set outside tools/.
-inline bool DiagSerial() {
-  static const bool on = std::getenv("PXG_DIAG_SERIAL") != nullptr;
-  return on;
-}
 
 // Launch helper: optional event bracketing on the launch stream (stats resolved lazily).
 template <typename... KArgs, typename... Args>
 inline int32_t LaunchOn(Ctx* ctx, hipStream_t stream, const char* name, void (*kernel)(KArgs...), dim3 grid, dim3 block,
                         size_t shmem, Args&&... args) {
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return PXG_OK;
-  if (DiagSerial()) stream = ctx->stream;
   hipEvent_t s0 = nullptr, s1 = nullptr;
   // profile_only selects the launches whose name starts with it ("agg_consume" also times
   // "agg_consume_prefix", the probe-record prefix launch).

@@ -885,14 +885,23 @@ __global__ void XPartBoundsKernel(const uint64_t* __restrict__ gstarts, int n_pa
 
 // The export finalize's deferred checks (AggFinalizeTable ends an export without a host wait):
 // `m` holds a host copy of ws.meta's first 24 bytes, taken after the stream passed the export.
-int32_t Agg::CheckExportFinalize(const uint8_t* m) const {
+int32_t Agg::CheckExportFinalize(const uint8_t* m) {
+  if (!x_check_pending) return PXG_OK;  // (the finalize returned before its kernels: nothing staged)
+  x_check_pending = false;
   uint32_t g_dev = 0, err = 0;
   std::memcpy(&g_dev, m + 8, 4);
   std::memcpy(&err, m + 16, 4);
   if (err) return SetError(PXG_INTERNAL, "t-digest centroid capacity exceeded");
-  if (g_dev != static_cast<uint32_t>(res.n_groups))
-    return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, static_cast<uint32_t>(res.n_groups));
+  if (g_dev != x_check_groups) return SetError(PXG_INTERNAL, "group table holds %u groups, host mirror says %u", g_dev, x_check_groups);
   return PXG_OK;
+}
+
+// eslots[g] = the table slot word of table group g (its arena record offset in the low word).
+__global__ void XTableSlotsKernel(const unsigned long long* __restrict__ slots, const uint32_t* __restrict__ gslot, uint32_t G,
+                                  unsigned long long* __restrict__ eslots, uint32_t* __restrict__ egslot, uint32_t Gt) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < G) eslots[g] = slots[gslot[g]];
+  if (g < Gt) egslot[g] = g;
 }
 
 // Export grouping (no host wait; the finalize waits once for its class counts when the plan has
@@ -905,12 +914,36 @@ int32_t Agg::ExportGroupV2(int32_t n_parts) {
   const bool has_q = x_qval >= 0;
   {
     // 1. The local finalize in export mode: grouping, per-group states, big groups' centroid lists.
+    PXG_RETURN_IF_ERROR(ws.meta.Ensure(64));  // read back by the callers even when nothing was staged
+    x_check_pending = false;
     export_x = true;
     const int32_t rc = AggFinalizeTable(this);
     export_x = false;
     res.ready = false;
     if (rc != PXG_OK) return rc;
-    const uint64_t G = static_cast<uint64_t>(res.n_groups);
+    const uint64_t Gtab = static_cast<uint64_t>(res.n_groups);
+    // A high-cardinality run exports its partition groups beside the table groups (no spill):
+    // aggregated to states by the partition pass, key records rebuilt as arena scratch.
+    X.e_slots = slots.as<const unsigned long long>();
+    X.e_gslot = ws.gslot.as<const uint32_t>();
+    X.hc_key_words = 0;
+    uint64_t G = Gtab;
+    if (hc_active) {
+      uint32_t n_hc = 0;
+      PXG_RETURN_IF_ERROR(ExportHcGroups(static_cast<uint32_t>(Gtab), &ws.xstates, &X.eslots, &n_hc, &X.hc_key_words));
+      G = Gtab + n_hc;
+      if (G >= (uint64_t(1) << 32)) return SetError(PXG_UNIMPLEMENTED, "export of 2^32 groups");
+      // (ExportHcGroups already sized eslots when it wrote partition groups; otherwise there is
+      // nothing in it to keep.)
+      PXG_RETURN_IF_ERROR(X.eslots.Reserve(G * 8 + 16, 0, ctx->stream));
+      PXG_RETURN_IF_ERROR(X.egslot.Ensure(G * 4 + 16));
+      if (G > 0)
+        PXG_RETURN_IF_ERROR(Launch(ctx, "export_group_rank", XTableSlotsKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                                   slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(), static_cast<uint32_t>(Gtab),
+                                   X.eslots.as<unsigned long long>(), X.egslot.as<uint32_t>(), static_cast<uint32_t>(G)));
+      X.e_slots = X.eslots.as<const unsigned long long>();
+      X.e_gslot = X.egslot.as<const uint32_t>();
+    }
     // Items and item words both stay below 2^31: the group offset word keeps the item index in
     // bits 32..62 and the centroid flag in bit 63 (kXCentFlag).
     if (st_n + uint64_t(2) * kXCentCapH * x_nbig >= (uint64_t(1) << 31))
@@ -937,7 +970,7 @@ int32_t Agg::ExportGroupV2(int32_t n_parts) {
     uint64_t* ioff_j = ic + G + 1;
     if (G > 0)
       PXG_RETURN_IF_ERROR(Launch(ctx, "export_slot_part", XGroupPartKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
-                                 d_plan.as<const AggPlanDev>(), slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(),
+                                 d_plan.as<const AggPlanDev>(), X.e_slots, X.e_gslot,
                                  static_cast<uint32_t>(G), arena.as<const uint64_t>(), static_cast<uint32_t>(n_parts),
                                  ws.gstart.as<const uint32_t>(), static_cast<const int32_t*>(xbig),
                                  static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), has_q ? 1 : 0, X.part_of.as<uint8_t>(), kw, ic));
@@ -1032,7 +1065,7 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
     PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", XWriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(G) * 64, 256, 1 << 30)),
                                dim3(256), 0, X.slist.as<const uint32_t>(), G, X.part_of.as<const uint8_t>(), X.starts.as<const uint64_t>(),
                                static_cast<const uint64_t*>(X.koff.as<uint64_t>() + G + 1), static_cast<const uint64_t*>(X.words.as<uint64_t>() + G + 1),
-                               slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(), arena.as<const uint64_t>(),
+                               X.e_slots, X.e_gslot, arena.as<const uint64_t>(),
                                d_plan.as<const AggPlanDev>(), ws.xstates.as<const uint8_t>(), srec, ws.gstart.as<const uint32_t>(), x_vals,
                                has_big ? static_cast<const int32_t*>(reinterpret_cast<int32_t*>(X.grank.p)) : nullptr,
                                static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), static_cast<const uint64_t*>(ws.xcent.as<uint64_t>()),
@@ -1111,7 +1144,7 @@ int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, u
   // Host bound of the parts' total: headers, per-group offsets / states / item offsets, every
   // group's key record (<= the arena), items (raw values <= staged rows, <= 2 * kXCentCapH words
   // per centroid list), alignment.
-  const uint64_t bound = static_cast<uint64_t>(n_parts) * (sizeof(XHeader) + 32) + G * (24 + Align8(srec)) + 8 * arena_words +
+  const uint64_t bound = static_cast<uint64_t>(n_parts) * (sizeof(XHeader) + 32) + G * (24 + Align8(srec)) + 8 * (arena_words + X.hc_key_words) +
                          8 * (st_n + uint64_t(2) * kXCentCapH * x_nbig) + 64;
   PXG_RETURN_IF_ERROR(send->Ensure(bound));
   PXG_RETURN_IF_ERROR(X.desc.Ensure(static_cast<size_t>(8 * n_parts) * 8 + 64));
@@ -1133,7 +1166,7 @@ int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, u
     PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", XWriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(G) * 64, 256, 1 << 30)),
                                dim3(256), 0, X.slist.as<const uint32_t>(), G, X.part_of.as<const uint8_t>(), X.starts.as<const uint64_t>(),
                                static_cast<const uint64_t*>(X.koff.as<uint64_t>() + G + 1), static_cast<const uint64_t*>(X.words.as<uint64_t>() + G + 1),
-                               slots.as<const unsigned long long>(), ws.gslot.as<const uint32_t>(), arena.as<const uint64_t>(),
+                               X.e_slots, X.e_gslot, arena.as<const uint64_t>(),
                                d_plan.as<const AggPlanDev>(), ws.xstates.as<const uint8_t>(), srec, ws.gstart.as<const uint32_t>(), x_vals,
                                has_big ? static_cast<const int32_t*>(reinterpret_cast<int32_t*>(X.grank.p)) : nullptr,
                                static_cast<const int32_t*>(ws.xcnt.as<int32_t>()), static_cast<const uint64_t*>(ws.xcent.as<uint64_t>()),
@@ -1266,8 +1299,8 @@ extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* d
                                           int64_t* part_bytes) {
   if (!agg || !part_offsets || !part_bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   if (n_parts < 1 || n_parts > kMaxParts) return SetError(PXG_INVALID_ARGUMENT, "n_parts must be in [1, %d]", kMaxParts);
-  PXG_RETURN_IF_ERROR(agg->impl.SpillHc());
   if (ExchangeV2(agg->impl)) return agg->impl.ExportPartialV2(n_parts, dst, dst_capacity, part_offsets, part_bytes);
+  PXG_RETURN_IF_ERROR(agg->impl.SpillHc());  // v1 row parts are cut from the table state
   return agg->impl.ExportPartial(n_parts, dst, dst_capacity, part_offsets, part_bytes);
 }
 

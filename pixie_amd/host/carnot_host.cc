@@ -3252,9 +3252,9 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
   w.put<uint32_t>(static_cast<uint32_t>(g.sinks_.size()));
-  // Large results are copied by up to 8 threads (a single thread copied C5's 195 MB result at
-  // ~15 GB/s; threads pay from ~32 MB, C2's 4.8 MB took 0.12 ms on one thread and 0.23 with
-  // four).  Many batches (C5: 2634): each thread writes a contiguous range of whole batches.
+  // Large results are copied by up to 16 threads, one per 8 MB (a single thread copied C5's
+  // 195 MB result at ~15 GB/s, 8 threads at ~65 GB/s; threads pay from ~32 MB, C2's 4.8 MB took
+  // 0.12 ms on one thread and 0.23 with four).  Many batches (C5: 2634): each thread writes a contiguous range of whole batches.
   // Few large batches: the headers are written first and every column copy becomes ~1 MB
   // pieces shared by the threads.
   struct Job {
@@ -3271,7 +3271,7 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
       w.claim(BatchBytes(rb));
     }
   }
-  const size_t nthreads = total < (size_t(32) << 20) ? 1 : std::min<size_t>({8, total >> 24, std::max(1u, std::thread::hardware_concurrency())});
+  const size_t nthreads = total < (size_t(32) << 20) ? 1 : std::min<size_t>({16, total >> 23, std::max(1u, std::thread::hardware_concurrency())});
   if (nthreads <= 1) {
     for (auto& j : jobs) {
       SpanWriter sw{w.p + j.at};

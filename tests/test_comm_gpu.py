@@ -81,6 +81,50 @@ def test_alltoall_single_rank_is_identity(tmp_path):
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
 
 
+_SELF_HC = textwrap.dedent('''
+    import os, sys
+    os.environ["PXG_HC_MIN_GROUPS"] = "1"
+    sys.path.insert(0, {repo!r})
+    from pixie_amd import plans as P
+    from pixie_amd.device import Comm, Ctx, Table
+    from pixie_amd.pipeline import LinearQuery
+    ctx = Ctx(0)
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events({seed}, 0, 1_000_000, 300_000)
+    q = LinearQuery(P.c3_plan(), P.HTTP_TYPES, expected_groups=100_000)
+    a = q.make_agg(ctx)
+    a.consume(t)
+    assert a.info()["hc_mode"] == 1
+    a.finalize()
+    local = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
+    comm = Comm(ctx, 0, 1, Comm.unique_id())
+    for rep in range(2):
+        a.reset()
+        a.consume(t)
+        assert a.info()["hc_mode"] == 1
+        sent, recv = a.alltoall(comm)  # partition groups exported as states, no spill
+        assert sent == recv and sent > 0
+        g = a.finalize()
+        merged = sorted(map(tuple, zip(*[c.to_list() for c in a.result()])))
+        assert g == len(local) == len(merged), (rep, g, len(local), len(merged))
+        for x, y in zip(local, merged):
+            assert x[:3] == y[:3] and x[4] == y[4], (x, y)
+            assert abs(x[3] - y[3]) <= 1e-12 * abs(x[3]), (x, y)
+    comm.close()
+    print("ok", sent, flush=True)
+''')
+
+
+def test_alltoall_single_rank_high_cardinality(tmp_path):
+    """World of one over a high-cardinality run (C3 plan, partition records): the exchange sends
+    the partition pass's groups as states (ExportHcGroups) and the merged result equals the
+    local one (keys, counts, sums exact; means 1e-12)."""
+    script = tmp_path / "self_hc.py"
+    script.write_text(_SELF_HC.format(repo=REPO, seed=SEED))
+    r = subprocess.run([sys.executable, str(script)], env=dict(os.environ, **_ENV), timeout=120, capture_output=True, text=True)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
 _RANK = textwrap.dedent('''
     import json, os, sys
     sys.path.insert(0, {repo!r})

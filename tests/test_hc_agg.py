@@ -173,9 +173,10 @@ def test_empty_selection_and_multiple_consumes(ctx, hc_env):
         x.close()
 
 
-def test_export_spills_partition_records_to_the_table(ctx, hc_env):
-    """export_partial on a high-cardinality run first moves the records into the table state;
-    the parts merged on 4 importers equal the single-agg result."""
+def test_export_partition_groups_without_spill(ctx, hc_env):
+    """export_partial on a high-cardinality run sends the partition pass's groups as states (no
+    spill into the table: the run stays in partition mode); the parts merged on 4 importers
+    equal the single-agg result."""
     import torch
     from pixie_amd.dist import segments
     tables, cols = _http(300_000, 100_000)
@@ -191,7 +192,7 @@ def test_export_spills_partition_records_to_the_table(ctx, hc_env):
         a.consume(t)
         assert a.info()["hc_mode"] == 1
         offs, nb = a.export_partial(parts)
-        assert a.info()["hc_mode"] == 0
+        assert a.info()["hc_mode"] == 1
         buf = torch.empty(max(sum(segments(offs, nb)), 8), dtype=torch.uint8, device="cuda")
         a.export_partial(parts, buf)
         tabs.append(t)
@@ -209,6 +210,61 @@ def test_export_spills_partition_records_to_the_table(ctx, hc_env):
         d.close()
     _check_c3(ref, out)
     for x in aggs + tabs:
+        x.close()
+
+
+def test_export_mixes_table_and_partition_groups(ctx, hc_env):
+    """A run whose long keys took the table path exports both halves: table groups (states from
+    the export finalize) and partition groups (states from the partition pass) share the parts,
+    and 3 importers merging 2 shards each reproduce the oracle."""
+    import torch
+    from pixie_amd.dist import segments
+    rng = np.random.default_rng(5)
+    n = 90_000
+    short = [f"s{i:05d}" for i in range(4000)]
+    long_ = ["L" * 25 + f"{i:04d}" for i in range(400)]
+    pool = short + long_
+    k1 = [pool[i] for i in rng.integers(0, len(pool), n)]
+    k2 = [("q" * int(l)) for l in rng.integers(0, 8, n)]
+    v = rng.integers(-1000, 1000, n)
+    types = [5, 5, 2]
+    plan = P.linear_plan([P.source_op("t", types, ["k", "k2", "v"], [0, 1, 2]),
+                          P.agg_op([0, 1], [P.agg_expr("count", [P.col(2)], [2]), P.agg_expr("sum", [P.col(2)], [2], fid=1),
+                                            P.agg_expr("min", [P.col(2)], [2], fid=2), P.agg_expr("max", [P.col(2)], [2], fid=3),
+                                            P.agg_expr("mean", [P.col(2)], [2], fid=4)]),
+                          P.sink_op("out")])
+    cols = [Column.from_values(5, k1), Column.from_values(5, k2), Column.from_values(2, v.tolist())]
+    tables = {"t": {"types": types, "batches": [cols], "names": ["k", "k2", "v"]}}
+    ref = _by_key(oc.execute_plan(plan, tables)["out"][0]["cols"], 2)
+    q = LinearQuery(plan, types, expected_groups=30_000)
+    parts, bufs, keep = 3, [], []
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        t = Table(ctx, types)
+        t.append([c.slice(lo, hi) for c in cols])
+        a = q.make_agg(ctx)
+        a.consume(t)
+        assert a.info()["hc_mode"] == 1
+        offs, nb = a.export_partial(parts)
+        buf = torch.empty(max(sum(segments(offs, nb)), 8), dtype=torch.uint8, device="cuda")
+        a.export_partial(parts, buf)
+        bufs.append((buf, offs, nb))
+        keep += [a, t]
+    out = {}
+    for p in range(parts):
+        d = q.make_agg(ctx)
+        for buf, offs, nb in bufs:
+            d.import_partial(buf[offs[p]:offs[p] + nb[p]])
+        d.finalize()
+        part = _by_key(q.emit(d.result()), 2)
+        assert not (set(part) & set(out))
+        out.update(part)
+        d.close()
+    assert len(ref) > 10_000 and set(ref) == set(out)
+    assert any(len(k[0]) > 24 for k in ref)
+    for k in ref:
+        assert ref[k][:4] == out[k][:4], k
+        assert abs(ref[k][4] - out[k][4]) <= 1e-9 * abs(ref[k][4]) + 1e-12, k
+    for x in keep:
         x.close()
 
 

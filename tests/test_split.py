@@ -1,9 +1,8 @@
-"""The finalize staging split (pxg_finalize.hip, SplitSampleKernel ..): groups a sample says are
-large are partitioned out of the staging in one counting pass and only the rest is radix-sorted.
-The split decides cost only, never results, so every case here is checked against the oracle
-and against the same aggregation finalized without the split (PXG_SPLIT_MIN_ROWS above n).
-Forced at small sizes with PXG_SPLIT_MIN_ROWS=0; PXG_SPLIT_EST sets the designation estimate
-(1: every sampled group, which also overflows the 4094 designated buckets)."""
+"""The large-group designation of the fused split (pxg_finalize.hip SplitSampleKernel ..
+FsHistKernel): groups a sample says are large get their own bucket in the sort's first pass and
+only the rest go through the remaining pass.  The designation decides cost only, never results,
+so every case here is checked against the oracle and against the same aggregation finalized with
+the plain radix sort (PXG_FSPLIT=0; PXG_FSPLIT=1 forces the fused split at small sizes)."""
 import json
 import math
 
@@ -25,23 +24,18 @@ def _by_key(cols, nkeys):
     return {t[:nkeys]: t[nkeys:] for t in rows(cols)}
 
 
-def _run(ctx, plan, tables, monkeypatch, split, est=None):
-    monkeypatch.setenv("PXG_SPLIT_MIN_ROWS", "0" if split else str(1 << 40))
-    if est is None:
-        monkeypatch.delenv("PXG_SPLIT_EST", raising=False)
-    else:
-        monkeypatch.setenv("PXG_SPLIT_EST", str(est))
+def _run(ctx, plan, tables, monkeypatch, split):
+    monkeypatch.setenv("PXG_FSPLIT", "1" if split else "0")
     return run_plan(ctx, plan, tables)
 
 
-@pytest.mark.parametrize("est", [None, 256, 1])
-def test_c2_split_matches_oracle_and_unsplit(ctx, monkeypatch, est):
+def test_c2_split_matches_oracle_and_unsplit(ctx, monkeypatch):
     n = 400_000
     cols = datagen_http_events(20250117, 0, n, threads=8)
     tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [cols], "names": P.HTTP_NAMES}}
     plan = P.c2_plan(with_pluck=False)
     R = _by_key(oc.execute_plan(plan, tables)["output"][0]["cols"], 2)
-    S = _by_key(_run(ctx, plan, tables, monkeypatch, True, est)[0]["cols"], 2)
+    S = _by_key(_run(ctx, plan, tables, monkeypatch, True)[0]["cols"], 2)
     U = _by_key(_run(ctx, plan, tables, monkeypatch, False)[0]["cols"], 2)
     assert set(R) == set(S) == set(U)
     sel = cols[5].values >= 400
@@ -72,11 +66,11 @@ def test_c2_split_matches_oracle_and_unsplit(ctx, monkeypatch, est):
 
 
 def test_designated_overflow_and_integer_udas(ctx, monkeypatch):
-    """~9000 groups of ~150 rows with every sampled group designated: more than the 4094
-    designated buckets, so the overflow goes through the sort; count / sum / min / max exact,
-    mean to 1e-12 against the unsplit run."""
+    """600 groups of ~5000 rows, every one large enough to be designated: more than the 255
+    designated buckets, so the overflow goes through the rest sort; count / sum / min / max
+    exact, mean to 1e-12 against the unsplit run."""
     rng = np.random.default_rng(77)
-    g = rng.integers(0, 9000, 1_400_000)
+    g = rng.integers(0, 600, 3_000_000)
     v = rng.integers(-(1 << 40), 1 << 40, len(g))
     types = [2, 2]
     plan = P.linear_plan([P.source_op("t", types, ["g", "v"], [0, 1]),
@@ -85,9 +79,9 @@ def test_designated_overflow_and_integer_udas(ctx, monkeypatch):
                                          P.agg_expr("mean", [P.col(1)], [2], fid=4)]),
                           P.sink_op("out")])
     tables = {"t": {"types": types, "batches": [[Column.from_values(2, g.tolist()), Column.from_values(2, v.tolist())]]}}
-    S = _by_key(_run(ctx, plan, tables, monkeypatch, True, 1)[0]["cols"], 1)
+    S = _by_key(_run(ctx, plan, tables, monkeypatch, True)[0]["cols"], 1)
     U = _by_key(_run(ctx, plan, tables, monkeypatch, False)[0]["cols"], 1)
-    assert set(S) == set(U) and len(S) == 9000
+    assert set(S) == set(U) and len(S) == 600
     for k in S:
         assert S[k][:4] == U[k][:4], k
         assert abs(S[k][4] - U[k][4]) <= 1e-12 * abs(U[k][4]) + 1e-9, k
