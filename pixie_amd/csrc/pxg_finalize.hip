@@ -2662,10 +2662,10 @@ int32_t AggFinalizeTable(Agg* a) {
           PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel<4096>, dim3(hmid[0]), dim3(4096 / kMsIpt), 0,
                                      lists + 4 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
                                      cnt_mid, vals, at, qo, d_err));
-        if (cls[2] > 0)  // on the side stream, behind the small digests (it idles from there on)
-          PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side, "quant_mid", QuantMidKernel<2048>, dim3(cls[2]), dim3(2048 / kMsIpt), 0,
-                                       lists + 2 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
-                                       static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
+        if (cls[2] > 0)
+          PXG_RETURN_IF_ERROR(Launch(ctx, "quant_mid", QuantMidKernel<2048>, dim3(cls[2]), dim3(2048 / kMsIpt), 0,
+                                     lists + 2 * static_cast<uint64_t>(ngroups), gstart, MidChainStarts(ctx), MidChainNc(ctx),
+                                     static_cast<const uint32_t*>(d_cls + 2), vals, at, qo, d_err));
       }
     }
   }
