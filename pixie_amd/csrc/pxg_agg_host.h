@@ -169,6 +169,13 @@ struct Agg {
     DevBuf skey[2], sval[2][kMaxVals], rank;
     DevBuf hist, scan, scan2, cgroup, flags, gidx, meta, gstart, gslot, cbase, partial, lists;
     DevBuf keysA, keysB, bstarts, big, bchunks;
+    // the designated big groups' own selection set (pxg_finalize.hip, started right after the
+    // fused split's first pass): group / chunk lists, their list of ids and group starts,
+    // counts (meta), chains, selection workspace
+    struct EarlyBig {
+      DevBuf big, chunks, ids, egs, meta, chain_starts, chain_nc;
+      DevBuf spl, cnt, list, bstart, tag, cbase, plan, partial;
+    } early;
     DevBuf chain_list, chain_nc, chain_starts;
     // big groups by selection (pxg_finalize.hip)
     DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list, sel_bin;

@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
                                                             uint32_t* __restrict__ lists, uint32_t* __restrict__ counts,
                                                             uint32_t* __restrict__ counts_mid, uint32_t mid_max,
                                                             const uint64_t* __restrict__ skip_flags, int flag_words,
-                                                            const uint32_t* __restrict__ gslot) {
+                                                            const uint32_t* __restrict__ gslot, uint32_t early_from) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const unsigned long long lanemask_lt = (1ULL << lane) - 1;
@@ -379,6 +379,7 @@ __global__ void __launch_bounds__(256) ClassifyGroupsKernel(const uint32_t* __re
   if (g < ngroups) {
     const uint32_t n = gstart[g + 1] - gstart[g];
     cls = SizeClass(n, mid_max);
+    if (cls == 3 && g >= early_from) cls = -1;  // a designated big group: the early set serves it
     if (skip_flags && (skip_flags[static_cast<uint64_t>(gslot[g]) * flag_words + flag_words - 1] & 1ULL)) cls = -1;
   }
   // Block-aggregated list appends: wave leaders reserve within the block in LDS, then one
@@ -1384,7 +1385,6 @@ __global__ void __launch_bounds__(kMergeThreads) DigestMergeKernel(const uint32_
 constexpr int kSelBins = 4096;
 constexpr int kSelBinBits = 12;
 constexpr int kSelSample = 8192;  // two samples per bin
-constexpr int kSelSampleThreads = kSelSample / kMsIpt;
 constexpr int kSelMaxRanges = kNeed;
 constexpr int kSelMaxColl = 256;
 constexpr int kSelHugeThreads = 1024;
@@ -2158,6 +2158,57 @@ __global__ void FinalizeInitKernel(uint8_t* meta, uint64_t n) {
 // Side streams forked by finalize are joined back into the main stream on every exit path, so
 // an early error return never leaves side-stream kernels running on workspace buffers that a
 // later reset / Ensure could free or reallocate.
+// One set of big groups for the selection / sort paths: its group and chunk lists (device, with
+// their device counts), host upper bounds for the grids, its chains and selection workspace.
+// Finalize runs two: the designated groups of a fused split (early, from the first pass) and
+// the other big groups (after the classification).
+struct BigSet {
+  BigGroup* big = nullptr;
+  BigChunk* chunks = nullptr;
+  const uint32_t* d_count = nullptr;  // groups in the set
+  const uint32_t* d_meta = nullptr;   // [0] chunks, [1] largest group (BigSetupKernel)
+  uint32_t n_big = 0, n_chunks = 0;   // host bounds of both (grids; exact after the meta readback)
+  uint64_t big_max = 0;               // largest group (host; the sort path's merge-pass count)
+  const uint32_t* chain_starts = nullptr;
+  const int32_t* chain_nc = nullptr;
+  DevBuf *spl = nullptr, *cnt = nullptr, *list = nullptr, *bstart = nullptr, *tag = nullptr, *cbase = nullptr, *plan = nullptr,
+         *partial = nullptr;
+};
+
+// The early set: the designated groups of a fused split (ids [Gr, G)) above mid_max values.
+// dstarts = the designated groups' starts (FusedSplitDesignatedStarts, j <= nd); they are
+// copied to egs[0, nd] so the early set reads its own group starts (the rest's group-start pass
+// writes gstart[Gr] concurrently).  One workgroup: nd <= kFsMaxU < 256.
+__global__ void __launch_bounds__(256) DesignatedBigListKernel(const uint32_t* __restrict__ dstarts, const uint64_t* __restrict__ ftotal,
+                                                               uint32_t G, uint32_t mid_max, uint32_t* __restrict__ egs,
+                                                               uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+  __shared__ uint32_t s[kFsMaxU + 1];
+  __shared__ uint32_t s_w[4];
+  const uint32_t nd = min(static_cast<uint32_t>(*ftotal >> 32), kFsMaxU);
+  const uint32_t t = threadIdx.x;
+  if (t <= nd) {
+    s[t] = dstarts[t];
+    egs[t] = s[t];
+  }
+  __syncthreads();
+  // ascending id order: a ballot per wave, then the waves in order
+  const bool big = t < nd && s[t + 1] - s[t] > mid_max;
+  const unsigned long long m = __ballot(big);
+  if ((t & 63) == 0) s_w[t >> 6] = __popcll(m);
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) before += s_w[w];
+  if (big) list[before + __popcll(m & ((1ULL << (t & 63)) - 1))] = G - nd + t;
+  if (t == 0) *count = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// The early big set runs whenever a fused split designated groups (PXG_EARLY_BIG=0: tests turn
+// it off to compare).
+static bool EarlyBigOn() {
+  const char* e = std::getenv("PXG_EARLY_BIG");
+  return !(e && e[0] == '0');
+}
+
 struct SideJoinGuard {
   Ctx* ctx;
   bool side = false, side2 = false;
@@ -2320,6 +2371,13 @@ int32_t AggFinalizeTable(Agg* a) {
   const uint32_t* kin = nullptr;
   PXG_RETURN_IF_ERROR(ws.gstart.Ensure((static_cast<size_t>(ngroups) + 1) * 4));
   const uint32_t* gstart = ws.gstart.as<const uint32_t>();
+  // The early big set (fused split only): the designated groups are final as soon as the split's
+  // scatter has run, so their big ones start the selection path on side stream 2 while the rest
+  // sort runs on the main stream (issued after the rest sort's launches, below).
+  bool early_on = false;
+  uint32_t early_gr = 0xFFFFFFFFu, early_nd = 0;
+  uint64_t early_rows = 0;
+  const uint32_t* early_dstarts = nullptr;
   if (fsplit) {
     // 2''. The fused split: one 9-bit pass (designated groups final, rest records by their low
     //      digit), then the rest records' remaining pass(es) by the higher digits.  The pass
@@ -2341,6 +2399,16 @@ int32_t AggFinalizeTable(Agg* a) {
     const uint32_t nd = std::min<uint32_t>(static_cast<uint32_t>(ft >> 32), kFsMaxU);
     const uint32_t Gr = ngroups - nd;
     for (int v = 0; v < kMaxVals; ++v) vin.p[v] = vbuf[fin].p[v];
+    bool plan_q = false;
+    for (int u = 0; u < a->n_udas; ++u) plan_q |= a->uda_kind[u] == PXG_UDA_QUANTILES;
+    if (plan_q && nd > 0 && !a->export_x && !a->merged && !EnvFlag("PXG_BIG_SORT") && EarlyBigOn()) {
+      early_on = true;
+      early_gr = Gr;
+      early_nd = nd;
+      early_rows = n - n_rest;
+      early_dstarts = FusedSplitDesignatedStarts(base);
+      PXG_HIP(hipEventRecord(ctx->ev_early, ctx->stream));  // right behind the split's scatter
+    }
     if (n_rest > 0) {
       const uint32_t* rkeys = kbuf[1];
       if (p2 > 0) {
@@ -2437,106 +2505,158 @@ int32_t AggFinalizeTable(Agg* a) {
   return PXG_OK;
   };
   if (!any_q) PXG_RETURN_IF_ERROR(RunReductions());
-  uint32_t n_big_groups = 0, n_bchunks = 0;
-  uint64_t big_max = 0;
-  const uint32_t* chain_starts_big = nullptr;
-  const int32_t* chain_nc_big = nullptr;
-  uint32_t* d_bigmeta = reinterpret_cast<uint32_t*>(meta + 48);
+  uint32_t n_big_groups = 0;  // the late set's groups (host, after the meta readback)
   unsigned int* d_fallback = reinterpret_cast<unsigned int*>(meta + 20);
-  // Full sort path of the big groups for quantile UDA u on stream st: chunk sort, merge
-  // passes, digests.  Runs after the boundary chains (st must be ordered after them).
-  auto BigSortPath = [&](hipStream_t st, int u) -> int32_t {
+  // Full sort path of a set's big groups for quantile UDA u on stream st: chunk sort, merge
+  // passes, digests.  Runs after the set's boundary chains (st must be ordered after them).
+  auto BigSortPath = [&](const BigSet& S, hipStream_t st, int u) -> int32_t {
     const uint64_t* vals = cv.p[a->uda_val[u]];
     const int at = a->uda_arg_type[u];
     PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
     PXG_RETURN_IF_ERROR(ws.keysB.Ensure(n * 8));
-    PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(n_big_groups) * kBigCentroids * 4));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_chunk_sort", BigChunkSortKernel, dim3(n_bchunks), dim3(256), 0,
-                                 ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at,
-                                 ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(S.n_big) * kBigCentroids * 4));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_chunk_sort", BigChunkSortKernel, dim3(S.n_chunks), dim3(256), 0,
+                                 static_cast<const BigChunk*>(S.chunks), S.d_meta, vals, at, ws.keysA.as<uint64_t>()));
     DevBuf* src = &ws.keysA;
     DevBuf* dst = &ws.keysB;
     uint32_t pass = 0;
-    for (uint64_t w = kMidMax; w < big_max; w *= 2, ++pass) {
-      PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_merge", BigMergeTileKernel, dim3(n_bchunks), dim3(256), 0,
-                                   ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), src->as<const uint64_t>(),
-                                   dst->as<uint64_t>(), w, pass));
+    for (uint64_t w = kMidMax; w < S.big_max; w *= 2, ++pass) {
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_big_merge", BigMergeTileKernel, dim3(S.n_chunks), dim3(256), 0,
+                                   static_cast<const BigChunk*>(S.chunks), S.d_meta, src->as<const uint64_t>(), dst->as<uint64_t>(), w, pass));
       std::swap(src, dst);
     }
     // An exchange export ships values / centroid lists, not quantiles: no digests there.
     if (!a->export_x) {
-      return LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
-                      static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
-                      ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, R.uda_out[u].as<double>(), d_err);
+      return LaunchOn(ctx, st, "quant_big_digest", BigDigestKernel, dim3(S.n_big), dim3(256), 0, static_cast<const BigGroup*>(S.big),
+                      S.d_count, ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(), S.chain_starts,
+                      S.chain_nc, R.uda_out[u].as<double>(), d_err);
     }
     // Exchange export: each big group's whole single-pass centroid list (those of > 8 * delta
     // values ship it instead of their values).
-    PXG_RETURN_IF_ERROR(ws.xcent.Ensure(static_cast<size_t>(n_big_groups) * kXCentCap * 16 + 16));
-    PXG_RETURN_IF_ERROR(ws.xcnt.Ensure(static_cast<size_t>(n_big_groups) * 4 + 16));
-    return LaunchOn(ctx, st, "export_centroids", CentroidListKernel, dim3(n_big_groups), dim3(kCentListBlock), 0, ws.big.as<const BigGroup>(),
-                    static_cast<const uint32_t*>(d_cls + 3), ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(),
-                    ws.bstarts.as<uint32_t>(), chain_starts_big, chain_nc_big, ws.xcent.as<uint64_t>(), ws.xcnt.as<int32_t>());
+    PXG_RETURN_IF_ERROR(ws.xcent.Ensure(static_cast<size_t>(S.n_big) * kXCentCap * 16 + 16));
+    PXG_RETURN_IF_ERROR(ws.xcnt.Ensure(static_cast<size_t>(S.n_big) * 4 + 16));
+    return LaunchOn(ctx, st, "export_centroids", CentroidListKernel, dim3(S.n_big), dim3(kCentListBlock), 0, static_cast<const BigGroup*>(S.big),
+                    S.d_count, ws.keysA.as<const uint64_t>(), ws.keysB.as<const uint64_t>(), ws.bstarts.as<uint32_t>(), S.chain_starts,
+                    S.chain_nc, ws.xcent.as<uint64_t>(), ws.xcnt.as<int32_t>());
+  };
+  // Selection workspace of a set (grown to its host bounds).
+  auto EnsureSel = [&](const BigSet& S) -> int32_t {
+    const size_t nb = S.n_big;
+    PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
+    PXG_RETURN_IF_ERROR(S.spl->Ensure(nb * kSelBins * 8 + nb * kSelGuideStride * 2 + 16));
+    PXG_RETURN_IF_ERROR(S.cnt->Ensure(nb * kSelBins * 8 + nb * 4 + 16));
+    PXG_RETURN_IF_ERROR(S.list->Ensure(nb * kSelMaxColl * kSelLists * 4 + 16));
+    PXG_RETURN_IF_ERROR(S.bstart->Ensure(nb * (kSelBins + 1) * 4 + 16));
+    PXG_RETURN_IF_ERROR(S.tag->Ensure(nb * kSelBins + 16));
+    PXG_RETURN_IF_ERROR(S.cbase->Ensure(nb * kSelBins * 4 + 16));
+    PXG_RETURN_IF_ERROR(S.plan->Ensure(nb * sizeof(BigPlan) + 16));
+    PXG_RETURN_IF_ERROR(S.partial->Ensure(static_cast<size_t>(S.n_chunks) * kSelMaxRanges * 8 + 16));
+    return ws.sel_bin.Ensure(n * 2 + 16);  // per staged value its bin (BigHist -> BigCollect; sets are disjoint)
   };
   // Selection path, first half (needs the sorted values and the chunk list only): sample,
   // splitters, bin counts.
-  auto BigSelectFront = [&](int u) -> int32_t {
+  auto BigSelectFront = [&](const BigSet& S, hipStream_t st, int u) -> int32_t {
     const uint64_t* vals = cv.p[a->uda_val[u]];
     const int at = a->uda_arg_type[u];
-    const uint64_t nb = n_big_groups;
-    PXG_HIP(hipMemsetAsync(ws.sel_cnt.p, 0, nb * kSelBins * 8 + nb * 4 + 16, ctx->side2));
-    uint16_t* guide = reinterpret_cast<uint16_t*>(ws.sel_spl.as<uint64_t>() + nb * kSelBins);
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(n_big_groups),
-                                 dim3(kSelSample / 2 / kMsIpt), 0, ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3),
-                                 vals, at, ws.sel_spl.as<uint64_t>(), guide, nullptr, nullptr));
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, kSelHistCap);
-    return LaunchOn(ctx, ctx->side2, "quant_sel_hist", at == PXG_FLOAT64 ? BigHistKernel<true> : BigHistKernel<false>,
-                    dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
-                    ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), vals, at, ws.sel_spl.as<const uint64_t>(),
-                    static_cast<const uint16_t*>(guide), ws.sel_cnt.as<uint32_t>(), ws.sel_cnt.as<uint32_t>() + 2 * nb * kSelBins, cpb,
+    const uint64_t nb = S.n_big;
+    PXG_HIP(hipMemsetAsync(S.cnt->p, 0, nb * kSelBins * 8 + nb * 4 + 16, st));
+    uint16_t* guide = reinterpret_cast<uint16_t*>(S.spl->as<uint64_t>() + nb * kSelBins);
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(S.n_big), dim3(kSelSample / 2 / kMsIpt), 0,
+                                 static_cast<const BigGroup*>(S.big), S.d_count, vals, at, S.spl->as<uint64_t>(), guide, nullptr, nullptr));
+    const uint32_t cpb = SelChunksPerBlock(S.n_chunks, ctx->num_cus, 3, kSelHistCap);
+    return LaunchOn(ctx, st, "quant_sel_hist", at == PXG_FLOAT64 ? BigHistKernel<true> : BigHistKernel<false>, dim3((S.n_chunks + cpb - 1) / cpb),
+                    dim3(256), 0, static_cast<const BigChunk*>(S.chunks), S.d_meta, vals, at, S.spl->as<const uint64_t>(),
+                    static_cast<const uint16_t*>(guide), S.cnt->as<uint32_t>(), S.cnt->as<uint32_t>() + 2 * nb * kSelBins, cpb,
                     ws.sel_bin.as<uint16_t>());
   };
   // Second half, after the chains: plan, gather + inside sums, bin sorts, digests.
-  auto BigSelectBack = [&](int u) -> int32_t {
+  auto BigSelectBack = [&](const BigSet& S, hipStream_t st, int u) -> int32_t {
     const uint64_t* vals = cv.p[a->uda_val[u]];
     const int at = a->uda_arg_type[u];
-    const uint64_t nb = n_big_groups;
-    uint32_t* hist = ws.sel_cnt.as<uint32_t>();
+    const uint64_t nb = S.n_big;
+    uint32_t* hist = S.cnt->as<uint32_t>();
     uint32_t* cursor = hist + nb * kSelBins;
     uint32_t* nan_cnt = hist + 2 * nb * kSelBins;
     uint32_t* list_cnt = nan_cnt + nb;
     const uint32_t list_cap = static_cast<uint32_t>(nb * kSelMaxColl);
-    uint32_t* lists = ws.sel_list.as<uint32_t>();
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_plan", BigPlanKernel, dim3(n_big_groups), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(d_cls + 3), chain_starts_big, chain_nc_big,
-                                 static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), ws.sel_bstart.as<uint32_t>(),
-                                 ws.sel_tag.as<uint8_t>(), ws.sel_cbase.as<uint32_t>(), ws.sel_plan.as<BigPlan>(), d_fallback, lists,
-                                 list_cap, list_cnt));
-    const uint32_t cpb = SelChunksPerBlock(n_bchunks, ctx->num_cus, 3, 64);  // 3 resident per CU (LDS)
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_collect", at == PXG_FLOAT64 ? BigCollectKernel<true> : BigCollectKernel<false>,
-                                 dim3((n_bchunks + cpb - 1) / cpb), dim3(256), 0,
-                                 ws.bchunks.as<const BigChunk>(), static_cast<const uint32_t*>(d_bigmeta), ws.sel_plan.as<const BigPlan>(),
-                                 vals, at, ws.sel_bin.as<const uint16_t>(), ws.sel_tag.as<const uint8_t>(),
-                                 ws.sel_cbase.as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), ws.sel_partial.as<double>(), cpb));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortKernel,
-                                 dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists), static_cast<const uint32_t*>(list_cnt),
-                                 static_cast<const uint32_t*>(hist), ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortLargeKernel,
-                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(256), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists + list_cap),
-                                 static_cast<const uint32_t*>(list_cnt + 1), static_cast<const uint32_t*>(hist),
-                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
-    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_sel_bin_sort", BigBinSortHugeKernel,
-                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(kSelHugeThreads), 0,
-                                 ws.big.as<const BigGroup>(), static_cast<const uint32_t*>(lists + 2 * list_cap),
-                                 static_cast<const uint32_t*>(list_cnt + 2), static_cast<const uint32_t*>(hist),
-                                 ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<uint64_t>()));
-    return LaunchOn(ctx, ctx->side2, "quant_sel_digest", BigSelDigestKernel, dim3(n_big_groups), dim3(256), 0, ws.big.as<const BigGroup>(),
-                    static_cast<const uint32_t*>(d_cls + 3), ws.sel_plan.as<const BigPlan>(), chain_starts_big,
-                    ws.sel_bstart.as<const uint32_t>(), ws.sel_cbase.as<const uint32_t>(), ws.keysA.as<const uint64_t>(),
-                    ws.sel_partial.as<const double>(), R.uda_out[u].as<double>());
+    uint32_t* lists = S.list->as<uint32_t>();
+    const BigGroup* big = S.big;
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_plan", BigPlanKernel, dim3(S.n_big), dim3(256), 0, big, S.d_count, S.chain_starts,
+                                 S.chain_nc, static_cast<const uint32_t*>(hist), static_cast<const uint32_t*>(nan_cnt), S.bstart->as<uint32_t>(),
+                                 S.tag->as<uint8_t>(), S.cbase->as<uint32_t>(), S.plan->as<BigPlan>(), d_fallback, lists, list_cap, list_cnt));
+    const uint32_t cpb = SelChunksPerBlock(S.n_chunks, ctx->num_cus, 3, 64);  // 3 resident per CU (LDS)
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_collect", at == PXG_FLOAT64 ? BigCollectKernel<true> : BigCollectKernel<false>,
+                                 dim3((S.n_chunks + cpb - 1) / cpb), dim3(256), 0, static_cast<const BigChunk*>(S.chunks), S.d_meta,
+                                 S.plan->as<const BigPlan>(), vals, at, ws.sel_bin.as<const uint16_t>(), S.tag->as<const uint8_t>(),
+                                 S.cbase->as<const uint32_t>(), cursor, ws.keysA.as<uint64_t>(), S.partial->as<double>(), cpb));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_bin_sort", BigBinSortKernel,
+                                 dim3(std::min<uint32_t>(list_cap / 4 + 1, static_cast<uint32_t>(ctx->num_cus) * 4)), dim3(256), 0, big,
+                                 static_cast<const uint32_t*>(lists), static_cast<const uint32_t*>(list_cnt), static_cast<const uint32_t*>(hist),
+                                 S.cbase->as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_bin_sort", BigBinSortLargeKernel,
+                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(256), 0, big,
+                                 static_cast<const uint32_t*>(lists + list_cap), static_cast<const uint32_t*>(list_cnt + 1),
+                                 static_cast<const uint32_t*>(hist), S.cbase->as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_bin_sort", BigBinSortHugeKernel,
+                                 dim3(std::min<uint32_t>(list_cap, static_cast<uint32_t>(ctx->num_cus))), dim3(kSelHugeThreads), 0, big,
+                                 static_cast<const uint32_t*>(lists + 2 * list_cap), static_cast<const uint32_t*>(list_cnt + 2),
+                                 static_cast<const uint32_t*>(hist), S.cbase->as<const uint32_t>(), ws.keysA.as<uint64_t>()));
+    return LaunchOn(ctx, st, "quant_sel_digest", BigSelDigestKernel, dim3(S.n_big), dim3(256), 0, big, S.d_count, S.plan->as<const BigPlan>(),
+                    S.chain_starts, S.bstart->as<const uint32_t>(), S.cbase->as<const uint32_t>(), ws.keysA.as<const uint64_t>(),
+                    S.partial->as<const double>(), R.uda_out[u].as<double>());
   };
+  BigSet SE;  // the early set
+  if (early_on) {
+    Agg::FinalizeWs::EarlyBig& E = ws.early;
+    const uint32_t nd = early_nd;
+    const uint64_t chunk_cap = early_rows / kMidMax + nd + 1;
+    PXG_RETURN_IF_ERROR(E.meta.Ensure(16));
+    PXG_RETURN_IF_ERROR(E.ids.Ensure(static_cast<size_t>(nd) * 4 + 16));
+    PXG_RETURN_IF_ERROR(E.egs.Ensure(static_cast<size_t>(nd) * 4 + 16));
+    PXG_RETURN_IF_ERROR(E.big.Ensure(static_cast<size_t>(nd) * (sizeof(BigGroup) + 4) + 32));
+    PXG_RETURN_IF_ERROR(E.chunks.Ensure(chunk_cap * sizeof(BigChunk)));
+    PXG_RETURN_IF_ERROR(E.chain_starts.Ensure(static_cast<size_t>(nd) * kChainCap * 4));
+    PXG_RETURN_IF_ERROR(E.chain_nc.Ensure(static_cast<size_t>(nd) * 4));
+    uint32_t* em = E.meta.as<uint32_t>();  // [0] groups, [1] chunks, [2] largest group, [3] large groups
+    uint32_t* large_list = reinterpret_cast<uint32_t*>(E.big.as<uint8_t>() + static_cast<size_t>(nd) * sizeof(BigGroup));
+    SE.big = E.big.as<BigGroup>();
+    SE.chunks = E.chunks.as<BigChunk>();
+    SE.d_count = em;
+    SE.d_meta = em + 1;
+    SE.n_big = nd;
+    SE.n_chunks = static_cast<uint32_t>(chunk_cap);
+    SE.chain_starts = E.chain_starts.as<const uint32_t>();
+    SE.chain_nc = E.chain_nc.as<const int32_t>();
+    SE.spl = &E.spl;
+    SE.cnt = &E.cnt;
+    SE.list = &E.list;
+    SE.bstart = &E.bstart;
+    SE.tag = &E.tag;
+    SE.cbase = &E.cbase;
+    SE.plan = &E.plan;
+    SE.partial = &E.partial;
+    PXG_RETURN_IF_ERROR(EnsureSel(SE));
+    PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_early, 0));
+    guard.side2 = true;
+    PXG_HIP(hipMemsetAsync(em, 0, 16, ctx->side2));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "quant_early_list", DesignatedBigListKernel, dim3(1), dim3(256), 0, early_dstarts,
+                                 static_cast<const uint64_t*>(d_ftotal), ngroups, kMidClassMax, E.egs.as<uint32_t>(), E.ids.as<uint32_t>(), em));
+    const uint32_t* egs_by_id = E.egs.as<const uint32_t>() - early_gr;  // group starts indexed by group id (ids [Gr, G) only)
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "big_setup", BigSetupKernel, dim3(1), dim3(kSetupBlock), 0, E.ids.as<const uint32_t>(),
+                                 static_cast<const uint32_t*>(em), egs_by_id, SE.big, SE.chunks, em + 1, large_list, em + 3));
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, ctx->side2, "digest_chain", DigestChainKernel, dim3((nd + kChainWaves - 1) / kChainWaves),
+                                 dim3(64 * kChainWaves), 0, E.ids.as<const uint32_t>(), static_cast<const uint32_t*>(em), 0u,
+                                 E.ids.as<const uint32_t>(), static_cast<const uint32_t*>(em), egs_by_id, E.chain_starts.as<uint32_t>(),
+                                 E.chain_nc.as<int32_t>()));
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+      PXG_RETURN_IF_ERROR(BigSelectFront(SE, ctx->side2, u));
+      PXG_RETURN_IF_ERROR(BigSelectBack(SE, ctx->side2, u));
+    }
+    clk.Mark("finalize: early big set issued");
+  }
   bool big_select = false;
+  BigSet SL;  // the late set: class 3 of the classification
   // 4. Quantile digests.
   if (any_q) {
     PXG_RETURN_IF_ERROR(ws.lists.Ensure(static_cast<size_t>(ngroups) * kAllClasses * 4));
@@ -2548,7 +2668,7 @@ int32_t AggFinalizeTable(Agg* a) {
                                ngroups, ws.lists.as<uint32_t>(), d_cls, reinterpret_cast<uint32_t*>(meta + 64),
                                a->export_x ? static_cast<uint32_t>(kMidMax) : kMidClassMax,
                                skip_merged ? a->macc.as<const uint64_t>() : nullptr, a->macc_words,
-                               ws.gslot.as<const uint32_t>()));
+                               ws.gslot.as<const uint32_t>(), early_gr));
     const uint32_t* lists = ws.lists.as<const uint32_t>();
     // Big-group metadata on the device; one readback of the class counts, the big-group chunk
     // total and the largest group (grid sizes and the merge-pass count).
@@ -2616,40 +2736,45 @@ int32_t AggFinalizeTable(Agg* a) {
     uint32_t cls[kNumClasses] = {hm[0], hm[1], hm[2], hm[3]};
     const uint32_t n_big = cls[3];
     n_big_groups = n_big;
-    chain_starts_big = chain_starts;
-    chain_nc_big = chain_nc;
-    big_max = hm[5];
-    n_bchunks = hm[4];
+    SL.big = ws.big.as<BigGroup>();
+    SL.chunks = ws.bchunks.as<BigChunk>();
+    SL.d_count = d_cls + 3;
+    SL.d_meta = d_bigmeta;
+    SL.n_big = n_big;
+    SL.n_chunks = hm[4];
+    SL.big_max = hm[5];
+    SL.chain_starts = chain_starts;
+    SL.chain_nc = chain_nc;
+    SL.spl = &ws.sel_spl;
+    SL.cnt = &ws.sel_cnt;
+    SL.list = &ws.sel_list;
+    SL.bstart = &ws.sel_bstart;
+    SL.tag = &ws.sel_tag;
+    SL.cbase = &ws.sel_cbase;
+    SL.plan = &ws.sel_plan;
+    SL.partial = &ws.sel_partial;
     // PXG_BIG_SORT=1 forces the full sort path for every big group (tests compare the two).
     big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT") && !a->export_x;
-    if (big_select) {
-      PXG_RETURN_IF_ERROR(ws.keysA.Ensure(n * 8));
-      PXG_RETURN_IF_ERROR(ws.sel_spl.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * kSelGuideStride * 2));
-      PXG_RETURN_IF_ERROR(ws.sel_cnt.Ensure(static_cast<size_t>(n_big) * kSelBins * 8 + static_cast<size_t>(n_big) * 4 + 16));
-      PXG_RETURN_IF_ERROR(ws.sel_list.Ensure(static_cast<size_t>(n_big) * kSelMaxColl * kSelLists * 4 + 16));
-      PXG_RETURN_IF_ERROR(ws.sel_bstart.Ensure(static_cast<size_t>(n_big) * (kSelBins + 1) * 4));
-      PXG_RETURN_IF_ERROR(ws.sel_tag.Ensure(static_cast<size_t>(n_big) * kSelBins));
-      PXG_RETURN_IF_ERROR(ws.sel_cbase.Ensure(static_cast<size_t>(n_big) * kSelBins * 4));
-      PXG_RETURN_IF_ERROR(ws.sel_plan.Ensure(static_cast<size_t>(n_big) * sizeof(BigPlan)));
-      PXG_RETURN_IF_ERROR(ws.sel_partial.Ensure(static_cast<size_t>(n_bchunks) * kSelMaxRanges * 8 + 16));
-      PXG_RETURN_IF_ERROR(ws.sel_bin.Ensure(n * 2 + 16));  // per staged value its bin (BigHist -> BigCollect)
-    }
+    if (big_select) PXG_RETURN_IF_ERROR(EnsureSel(SL));
     // Big groups on side stream 2, overlapping the mid digests and the key output on the main
     // stream: the selection path's sample + bin counts start right after the metadata readback,
     // the rest waits for the boundary chains.  Every quantile UDA's big work runs in order on
     // side stream 2, so later UDAs reuse the workspace safely.
+    // With an early set on side stream 2, the late set takes the side stream (behind the small
+    // digests), so the two sets' latency-bound chains of launches run side by side.
+    hipStream_t lst = early_on ? ctx->side : ctx->side2;
     if (n_big > 0) {
-      PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_meta, 0));
-      guard.side2 = true;
+      PXG_HIP(hipStreamWaitEvent(lst, ctx->ev_meta, 0));
+      if (!early_on) guard.side2 = true;
     }
     for (int u = 0; u < a->n_udas; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
       const uint64_t* vals = cv.p[a->uda_val[u]];
       const int at = a->uda_arg_type[u];
-      if (big_select) PXG_RETURN_IF_ERROR(BigSelectFront(u));
+      if (big_select) PXG_RETURN_IF_ERROR(BigSelectFront(SL, lst, u));
       if (n_big > 0) {
-        PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_chain, 0));
-        PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(u) : BigSortPath(ctx->side2, u));
+        PXG_HIP(hipStreamWaitEvent(lst, ctx->ev_chain, 0));
+        PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(SL, lst, u) : BigSortPath(SL, lst, u));
       }
       double* qo = R.uda_out[u].as<double>();
       if (!a->export_x) {  // the mid classes, one launch each (largest first: the longest workgroups)
@@ -2671,7 +2796,7 @@ int32_t AggFinalizeTable(Agg* a) {
   }
   if (guard.side) PXG_RETURN_IF_ERROR(JoinSide(ctx));  // the small digests
   guard.side = false;
-  if (keys_on_side2 || n_big_groups > 0) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
+  if (keys_on_side2 || n_big_groups > 0 || early_on) PXG_RETURN_IF_ERROR(JoinSide2(ctx));
   guard.side2 = false;
   if (a->export_x) {
     // An export reads neither the string-key totals nor the result columns: its caller checks
@@ -2697,6 +2822,7 @@ int32_t AggFinalizeTable(Agg* a) {
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 1, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 2, d_fallback, 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (early_on) PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 3, ws.early.meta.p, 12, hipMemcpyDeviceToHost, ctx->stream));
   clk.Mark("finalize: issue rest");
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   clk.Mark("finalize: final wait");
@@ -2704,13 +2830,23 @@ int32_t AggFinalizeTable(Agg* a) {
     if (a->key_types[k] == PXG_STRING) totals[k] = pin32[k];
   err = pin32[kMaxKeys];
   g_dev = pin32[kMaxKeys + 1];
-  const uint32_t n_fallback = big_select ? pin32[kMaxKeys + 2] : 0;
-  a->last_big_sort_groups = big_select ? n_fallback : n_big_groups;
-  if (big_select && n_fallback > 0) {
+  const bool any_select = big_select || early_on;
+  const uint32_t n_fallback = any_select ? pin32[kMaxKeys + 2] : 0;
+  a->last_big_sort_groups = any_select ? n_fallback : n_big_groups;
+  if (any_select && n_fallback > 0) {
     // Some big group could not be served by selection (NaN values, heavy duplicates): the full
-    // sort path recomputes every big group's quantiles (the chains are long done).
-    for (int u = 0; u < a->n_udas; ++u)
-      if (a->uda_kind[u] == PXG_UDA_QUANTILES) PXG_RETURN_IF_ERROR(BigSortPath(ctx->stream, u));
+    // sort path recomputes every big group's quantiles, both sets (the chains are long done).
+    if (early_on) {
+      SE.n_big = pin32[kMaxKeys + 3];
+      SE.n_chunks = pin32[kMaxKeys + 4];
+      SE.big_max = pin32[kMaxKeys + 5];
+    }
+    PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(std::max(SE.n_big, SL.n_big)) * kBigCentroids * 4 + 16));
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+      if (SL.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SL, ctx->stream, u));
+      if (SE.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SE, ctx->stream, u));
+    }
     PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));
     err = pin32[kMaxKeys];

@@ -961,6 +961,8 @@ int32_t FusedSplitPass(Ctx* ctx, const uint32_t* st_slot, uint64_t n, const uint
   return PXG_OK;
 }
 
+const uint32_t* FusedSplitDesignatedStarts(const uint32_t* base) { return base + kFsRest; }
+
 int32_t FusedSplitGstart(Ctx* ctx, const uint32_t* base, const uint64_t* d_ftotal, uint32_t G, uint32_t* gstart) {
   return Launch(ctx, "group_heads", FsGstartKernel, dim3((kFsMaxU + 256) / 256), dim3(256), 0, base, d_ftotal, G, gstart);
 }

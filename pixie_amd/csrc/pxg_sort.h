@@ -68,6 +68,9 @@ int32_t DesignateLargeGroups(Ctx* ctx, const unsigned long long* slots, uint32_t
 int32_t FusedSplitPass(Ctx* ctx, const uint32_t* st_slot, uint64_t n, const uint32_t* rank, uint32_t cap, uint32_t G, const uint64_t* d_ftotal,
                        ConstValPtrs vin, int nvs, DevBuf& split_hist, DevBuf& split_tot, DevBuf& fs_keys, RadixPassWs& rs, uint32_t* kout_rest,
                        ValPtrs vrest, ValPtrs vfin, const uint32_t** base_out);
+// The designated groups' starts (device, j <= nd: group Gr + j starts at [j]; [nd] = n) out of
+// FusedSplitPass's *base_out; final as soon as FusedSplitPass's scatter has run.
+const uint32_t* FusedSplitDesignatedStarts(const uint32_t* base);
 // Step 3 (after the rest's group starts): gstart of the designated groups and gstart[G].
 int32_t FusedSplitGstart(Ctx* ctx, const uint32_t* base, const uint64_t* d_ftotal, uint32_t G, uint32_t* gstart);
 // Whether a finalize of n staged records takes the fused split (PXG_FSPLIT=0 / 1: tests force it).

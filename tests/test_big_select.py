@@ -258,3 +258,35 @@ def test_selection_path_int64_values_match_sort_path(ctx):
                 assert a == b, (k, name, a, b)
             else:
                 assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
+
+
+@pytest.mark.parametrize("fallback", [None, "nan"])
+def test_early_set_matches_late_set(ctx, monkeypatch, fallback):
+    """Fused split (forced on, > 256 groups): the designated big groups take the selection path
+    as their own early set, started before the rest sort finishes (PXG_EARLY_BIG; off, they are
+    class 3 of the classification).  Same values, same kernels: the same quantiles (big groups to
+    the last bits of their inside-bin sums), and a fallback group in either set hands both sets to
+    the sort path (identical)."""
+    keys, vals, sizes = _groups(fallback)
+    rng = np.random.default_rng(77)
+    small = {f"s{i}": rng.lognormal(1, 1, 100) for i in range(400)}
+    keys = keys + [k for k, v in small.items() for _ in v]
+    vals = np.concatenate([vals] + list(small.values()))
+    sizes.update({k: len(v) for k, v in small.items()})
+    monkeypatch.setenv("PXG_FSPLIT", "1")
+    monkeypatch.setenv("PXG_EARLY_BIG", "0")
+    late, info_l = _run_info(ctx, keys, vals, force_sort=False)
+    monkeypatch.setenv("PXG_EARLY_BIG", "1")
+    early, info_e = _run_info(ctx, keys, vals, force_sort=False)
+    assert set(late) == set(early) == set(sizes)
+    assert info_l["big_sort_groups"] == info_e["big_sort_groups"], (info_l, info_e)
+    if fallback:
+        assert info_e["big_sort_groups"] >= 1
+    for k, n in sizes.items():
+        assert late[k][1] == early[k][1] == n
+        for name in NAMES:
+            a, b = late[k][0][name], early[k][0][name]
+            if n <= 10_000 or fallback:
+                assert a == b or (a != a and b != b), (k, name, a, b)
+            else:  # (inside-bin sums: atomics, last bits run to run, as in the late set alone)
+                assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)

@@ -10,6 +10,7 @@
 #   c3prof : rocprofv3 stats of the C3 leg
 #   diag   : tools/consume_diag.py timing modes (0 production, 2 filter only, 3 keys + hash)
 #   filterpmc: the Filter -> Map leg alone + FETCH_SIZE / WRITE_SIZE passes of its filter kernels
+#   c5pmc  : FETCH_SIZE / WRITE_SIZE passes over the C5 query's consume kernel (tools/c5_timing.py)
 #   multi2 : bench.py --gpus 2 --share-gpu0 --backend gloo (the N>1 line, both ranks on GPU 0)
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -32,6 +33,9 @@ step() {
          timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/fpmc_write -o run --output-format csv -- python3 tools/ops_bench.py > gpurun_out/fpmc_write.log 2>&1 &&
          python3 tools/pmc_summary.py --kernel FilterWriteKernel --name filter_write --rows 100000000 --fetch gpurun_out/fpmc_fetch --write gpurun_out/fpmc_write --out gpurun_out/fpmc_write.json > /dev/null 2>&1 &&
          python3 tools/pmc_summary.py --kernel FilterCountKernel --name filter_count --rows 100000000 --fetch gpurun_out/fpmc_fetch --write gpurun_out/fpmc_write --out gpurun_out/fpmc_count.json > /dev/null 2>&1 ;;
+    c5pmc) timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/c5pmc_fetch -o run --output-format csv -- python3 tools/c5_timing.py 20000000 2 > gpurun_out/c5pmc_fetch.log 2>&1 &&
+         timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/c5pmc_write -o run --output-format csv -- python3 tools/c5_timing.py 20000000 2 > gpurun_out/c5pmc_write.log 2>&1 &&
+         python3 tools/pmc_summary.py --kernel AggConsumeFastKernel --name c5_agg_consume --rows 20000000 --fetch gpurun_out/c5pmc_fetch --write gpurun_out/c5pmc_write --out gpurun_out/c5pmc_consume.json > gpurun_out/c5pmc_summary.log 2>&1 ;;
     multi2) timeout -k 10 400 python3 -u bench.py --gpus 2 --share-gpu0 --backend gloo --steps 3 --warmup 1 > gpurun_out/bench_multi2.json 2> gpurun_out/bench_multi2.err ;;
     *) echo "unknown mode $1" >&2; return 2 ;;
   esac
