@@ -212,6 +212,18 @@ int32_t pxg_table_fetch(pxg_table* t, int32_t col, int64_t begin, int64_t end,
  * non-decreasing INT64/TIME64NS column col is >= value (strict = 0) or > value (strict = 1);
  * num_rows when there is none. */
 int32_t pxg_table_time_bound(pxg_table* t, int32_t col, int64_t value, int32_t strict, int64_t* row);
+/* Device result image (sink path; MemorySinkNode::ConsumeNextImpl,
+ * src/carnot/exec/memory_sink_node.cc:75-80, keeps the row batches an operator sends it): rows
+ * [starts[0], starts[n_batches]) of t as n_batches row batches (batch i = rows [starts[i],
+ * starts[i+1]); eow / eos on the last one as given) in the engine's PXRB batch layout, built in
+ * device memory; *bytes = its size.  Single-chunk tables (<= 2^24 rows): PXG_UNIMPLEMENTED
+ * otherwise, and the caller fetches the columns instead.  pxg_pxrb_copy moves the image into a
+ * host buffer of *bytes bytes (one DMA; waits); pxg_pxrb_destroy releases it. */
+typedef struct pxg_pxrb pxg_pxrb;
+int32_t pxg_table_pxrb_image(pxg_table* t, const int64_t* starts, int64_t n_batches, int32_t last_eow,
+                             int32_t last_eos, pxg_pxrb** out, int64_t* bytes);
+int32_t pxg_pxrb_copy(pxg_pxrb* img, void* dst);
+int32_t pxg_pxrb_destroy(pxg_pxrb* img);
 
 /* ---------------------------------------------------------------------------------------
  * Filter and Map over a device table (non-fused operator shapes).

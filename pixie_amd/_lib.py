@@ -82,7 +82,8 @@ EXPORTED = [
     "pxg_ctx_sync", "pxg_ctx_stream", "pxg_ctx_set_profiling", "pxg_ctx_profile_only", "pxg_ctx_kernel_stats",
     "pxg_ctx_reset_stats", "pxg_table_create", "pxg_table_destroy", "pxg_table_append",
     "pxg_table_append_device", "pxg_table_flush", "pxg_table_num_rows", "pxg_table_num_chunks",
-    "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
+    "pxg_table_device_bytes", "pxg_table_fetch", "pxg_table_time_bound", "pxg_table_pxrb_image",
+    "pxg_pxrb_copy", "pxg_pxrb_destroy", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_result_device", "pxg_agg_finalize_result", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial", "pxg_agg_import_partials",
     "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains", "pxg_digest_merge",
@@ -158,6 +159,9 @@ def load() -> C.CDLL:
         "pxg_agg_import_partials": (i32, [vp, vp, i32, p(i64), p(i64)]),
         "pxg_join": (i32, [vp, vp, p(JoinSpec), p(vp), p(i64)]),
         "pxg_table_time_bound": (i32, [vp, i32, i64, i32, p(i64)]),
+        "pxg_table_pxrb_image": (i32, [vp, p(i64), i64, i32, i32, p(vp), p(i64)]),
+        "pxg_pxrb_copy": (i32, [vp, vp]),
+        "pxg_pxrb_destroy": (i32, [vp]),
         "pxg_datagen_http_events": (i32, [C.c_uint64, i64, i64, i64, i32, p(ColumnOut)]),
         "pxg_table_append_http_events": (i32, [vp, C.c_uint64, i64, i64, i64]),
         "pxg_digest_chains": (i32, [vp, vp, i32, i32, vp, i32, vp]),

@@ -158,7 +158,8 @@ struct Ctx {
   int num_cus = 256;
   // Pinned scratch for counters read back by the host (async D2H, no staging copy):
   // [0, 64) consume publish, [64, 104) finalize class counts, [104, 128) finalize split
-  // totals, [128, 256) finalize totals,
+  // totals, [128, 256) finalize totals (HC / export phases reuse [192, 256)), [256, 264) the
+  // device result image's size (pxg_pxrb.hip),
   // [kPinnedOps, kPinnedBytes) standalone Filter / Map per-chunk counts.
   void* pinned = nullptr;
   static constexpr size_t kPinnedOps = 4096, kPinnedBytes = 65536;

@@ -210,6 +210,12 @@ struct RowBatch {
   // nodes whose AcceptsDeviceBatch() is true.
   const pxg_column_view* dev = nullptr;
   int64_t dev_bytes = 0;
+  // A device result image (the equijoin -> sink hand-off, pxg_table_pxrb_image): `cols` is
+  // empty and the image holds image_batches row batches (num_rows rows in all) already in the
+  // PXRB batch layout.  Only sent to nodes whose AcceptsResultImage() is true.
+  std::shared_ptr<pxg_pxrb> image;
+  int64_t image_batches = 0;
+  int64_t image_bytes = 0;
 };
 
 using RowDescriptor = std::vector<int32_t>;  // column types (schema::RowDescriptor)
@@ -801,6 +807,8 @@ class ExecNode {
   virtual uint32_t PluckedLanes(size_t /*col*/) const { return 0x7Fu; }
   // Whether this node takes device-resident batches (RowBatch::dev) from its parents.
   virtual bool AcceptsDeviceBatch() const { return false; }
+  // Whether this node takes device result images (RowBatch::image) from its parents.
+  virtual bool AcceptsResultImage() const { return false; }
   const RowDescriptor& output_descriptor() const { return output_; }
   const std::vector<std::pair<ExecNode*, size_t>>& children() const { return children_; }
   virtual std::string DebugString() const = 0;
@@ -1156,6 +1164,12 @@ static HostColumn RenderQuantilesJson(const double* d, int64_t G) {
 // one batch per eow, then ClearAggState (agg_node.cc:169-180).
 // Pluck-only quantile columns fetched as their plucked lanes (pxg_agg_quantile_lanes);
 // PXC_DEVICE_PLUCK=0 copies the 7 doubles per group and plucks on the host instead.
+// A test switch read at each use (tests flip it between queries of one process).
+static bool EnvOn(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] && e[0] != '0';
+}
+
 static bool DevicePluck() {
   static const bool on = [] {
     const char* e = std::getenv("PXC_DEVICE_PLUCK");
@@ -1997,6 +2011,30 @@ class GpuEquijoinNode : public ExecNode {
     for (int64_t b = 0; b < nprobe; b += rows_per_batch_) ranges.push_back({b, std::min(nprobe, b + rows_per_batch_)});
     for (int64_t b = nprobe; b < n; b += rows_per_batch_) ranges.push_back({b, std::min(n, b + rows_per_batch_)});
     if (ranges.empty()) return SendRowBatchToChildren(s, ZeroRowBatch(output_, true, true));
+    // Every consumer a result sink (C5's shape) and no per-batch stats wanted: the batches are
+    // laid out on the device as one PXRB image, moved to the result buffer by one DMA at
+    // serialisation (PXC_NO_RESULT_IMAGE=1: tests compare with the host path below).
+    bool image_ok = !s->collect_exec_stats && !children_.empty() && !EnvOn("PXC_NO_RESULT_IMAGE");
+    for (auto& ch : children_) image_ok = image_ok && ch.first->AcceptsResultImage();
+    if (image_ok) {
+      std::vector<int64_t> starts;
+      for (auto& r : ranges) starts.push_back(r.first);
+      starts.push_back(ranges.back().second);
+      pxg_pxrb* img = nullptr;
+      int64_t bytes = 0;
+      const int32_t rc = pxg_table_pxrb_image(out, starts.data(), static_cast<int64_t>(ranges.size()), 1, 1, &img, &bytes);
+      if (rc == PXG_OK) {
+        RowBatch ob;
+        ob.num_rows = n;
+        ob.eow = ob.eos = true;
+        ob.image = std::shared_ptr<pxg_pxrb>(img, [](pxg_pxrb* p) { pxg_pxrb_destroy(p); });
+        ob.image_batches = static_cast<int64_t>(ranges.size());
+        ob.image_bytes = bytes;
+        clk.Mark("join: result image");
+        return SendRowBatchToChildren(s, ob);
+      }
+      if (rc != PXG_UNIMPLEMENTED) return FromPxg(rc);
+    }
     // One device-to-host fetch per output column; the batches are slices of it (a fetch per
     // batch and column cost ~140 us each: 2634 batches of C5 took 370 ms).
     std::vector<HostColumn> full;
@@ -2039,6 +2077,9 @@ class SinkNode : public ExecNode {
     batches.push_back(rb);
     return Status::OK();
   }
+
+ public:
+  bool AcceptsResultImage() const override { return true; }
 };
 
 // GRPCSinkNode to another Carnot (grpc_sink_node.cc:276-330): every RowBatch, split above the
@@ -3245,9 +3286,14 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
   clk.Mark("execute (total)");
   Writer w;
   size_t total = 8;
+  size_t host_bytes = 0;  // bytes the host writes (device result images come by DMA)
   for (auto* sk : g.sinks_) {
     total += 8 + sk->name.size();
-    for (auto& rb : sk->batches) total += BatchBytes(rb);
+    for (auto& rb : sk->batches) {
+      const size_t b = rb.image ? static_cast<size_t>(rb.image_bytes) : BatchBytes(rb);
+      total += b;
+      if (!rb.image) host_bytes += b;
+    }
   }
   w.reserve(total);
   w.put<uint32_t>(0x42525850u);  // "PXRB"
@@ -3262,16 +3308,36 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
     size_t at;
   };
   std::vector<Job> jobs;
+  struct ImageJob {
+    pxg_pxrb* img;
+    size_t at;
+  };
+  std::vector<ImageJob> images;
   for (auto* sk : g.sinks_) {
     w.put<uint32_t>(static_cast<uint32_t>(sk->name.size()));
     w.bytes(sk->name.data(), sk->name.size());
-    w.put<uint32_t>(static_cast<uint32_t>(sk->batches.size()));
+    size_t nb = 0;
+    for (auto& rb : sk->batches) nb += rb.image ? static_cast<size_t>(rb.image_batches) : 1;
+    w.put<uint32_t>(static_cast<uint32_t>(nb));
     for (auto& rb : sk->batches) {
+      if (rb.image) {
+        images.push_back({rb.image.get(), w.n});
+        w.claim(static_cast<size_t>(rb.image_bytes));
+        continue;
+      }
       jobs.push_back({&rb, w.n});
       w.claim(BatchBytes(rb));
     }
   }
-  const size_t nthreads = total < (size_t(32) << 20) ? 1 : std::min<size_t>({16, total >> 23, std::max(1u, std::thread::hardware_concurrency())});
+  // The images' DMAs run while the host writes the other batches.
+  int32_t image_rc = PXG_OK;
+  std::thread image_copy;
+  if (!images.empty())
+    image_copy = std::thread([&] {
+      for (auto& im : images)
+        if (image_rc == PXG_OK) image_rc = pxg_pxrb_copy(im.img, w.p + im.at);
+    });
+  const size_t nthreads = host_bytes < (size_t(32) << 20) ? 1 : std::min<size_t>({16, host_bytes >> 23, std::max(1u, std::thread::hardware_concurrency())});
   if (nthreads <= 1) {
     for (auto& j : jobs) {
       SpanWriter sw{w.p + j.at};
@@ -3320,6 +3386,8 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
       });
     for (auto& t : th) t.join();
   }
+  if (image_copy.joinable()) image_copy.join();
+  if (image_rc != PXG_OK) return Fail(FromPxg(image_rc));
   *out = w.release(out_len);
   if (grpc_out) {  // "PXGS": per GRPC sink, its destination source id and RowBatchData messages
     Writer gw;
