@@ -176,6 +176,7 @@ struct Agg {
       DevBuf big, chunks, ids, egs, meta, chain_starts, chain_nc;
       DevBuf spl, cnt, list, bstart, tag, cbase, plan, partial;
     } early;
+    DevBuf fb_list, fb_meta;  // the fallback groups of both sets (full sort path)
     DevBuf chain_list, chain_nc, chain_starts;
     // big groups by selection (pxg_finalize.hip)
     DevBuf sel_spl, sel_cnt, sel_bstart, sel_tag, sel_cbase, sel_plan, sel_partial, sel_list, sel_bin;

@@ -2202,6 +2202,14 @@ __global__ void __launch_bounds__(256) DesignatedBigListKernel(const uint32_t* _
   if (t == 0) *count = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
+// The group ids of a set's big groups whose selection plan fell back (BigPlan::fallback).
+__global__ void FallbackListKernel(const BigGroup* __restrict__ groups, const uint32_t* __restrict__ count, const BigPlan* __restrict__ plans,
+                                   uint32_t* __restrict__ list, uint32_t* __restrict__ n_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *count) return;
+  if (plans[i].fallback) list[atomicAdd(n_out, 1u)] = groups[i].g;
+}
+
 // The early big set runs whenever a fused split designated groups (PXG_EARLY_BIG=0: tests turn
 // it off to compare).
 static bool EarlyBigOn() {
@@ -2834,18 +2842,58 @@ int32_t AggFinalizeTable(Agg* a) {
   const uint32_t n_fallback = any_select ? pin32[kMaxKeys + 2] : 0;
   a->last_big_sort_groups = any_select ? n_fallback : n_big_groups;
   if (any_select && n_fallback > 0) {
-    // Some big group could not be served by selection (NaN values, heavy duplicates): the full
-    // sort path recomputes every big group's quantiles, both sets (the chains are long done).
+    // Some big group could not be served by selection (NaN values, a gathered bin past its
+    // capacity: heavy ties).  With one quantile UDA the full sort path recomputes just those
+    // groups (both sets' flagged groups as one set: their list, BigSetup and chains, then the
+    // chunk sort / merges / digests); with several, every big group of both sets (the plans hold
+    // the last UDA's flags only).  The chains and the sets' work are long done.
     if (early_on) {
       SE.n_big = pin32[kMaxKeys + 3];
       SE.n_chunks = pin32[kMaxKeys + 4];
       SE.big_max = pin32[kMaxKeys + 5];
     }
-    PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(std::max(SE.n_big, SL.n_big)) * kBigCentroids * 4 + 16));
-    for (int u = 0; u < a->n_udas; ++u) {
-      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
-      if (SL.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SL, ctx->stream, u));
-      if (SE.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SE, ctx->stream, u));
+    int nq = 0;
+    for (int u = 0; u < a->n_udas; ++u) nq += a->uda_kind[u] == PXG_UDA_QUANTILES ? 1 : 0;
+    if (nq == 1) {
+      const uint32_t cap_fb = (big_select ? SL.n_big : 0) + (early_on ? SE.n_big : 0);
+      PXG_RETURN_IF_ERROR(ws.fb_list.Ensure(static_cast<size_t>(cap_fb) * 4 + 16));
+      PXG_RETURN_IF_ERROR(ws.fb_meta.Ensure(16));
+      uint32_t* fm = ws.fb_meta.as<uint32_t>();  // [0] groups, [1] chunks, [2] largest, [3] large groups
+      uint32_t* fl = ws.fb_list.as<uint32_t>();
+      PXG_HIP(hipMemsetAsync(fm, 0, 16, ctx->stream));
+      for (const BigSet* S : {&SL, &SE}) {
+        if (S->n_big == 0 || (S == &SL && !big_select)) continue;
+        PXG_RETURN_IF_ERROR(Launch(ctx, "quant_fallback_list", FallbackListKernel, dim3((S->n_big + 255) / 256), dim3(256), 0,
+                                   static_cast<const BigGroup*>(S->big), S->d_count, S->plan->as<const BigPlan>(), fl, fm));
+      }
+      // The subset in the late set's buffers (sized for every group above kMidMax values).
+      BigSet SF;
+      SF.big = ws.big.as<BigGroup>();
+      SF.chunks = ws.bchunks.as<BigChunk>();
+      SF.d_count = fm;
+      SF.d_meta = fm + 1;
+      SF.chain_starts = ws.chain_starts.as<const uint32_t>();
+      SF.chain_nc = ws.chain_nc.as<const int32_t>();
+      uint32_t* large_list = reinterpret_cast<uint32_t*>(ws.big.as<uint8_t>() + (n / (kMidMax + 1) + 1) * sizeof(BigGroup)) + 4;
+      PXG_RETURN_IF_ERROR(Launch(ctx, "big_setup", BigSetupKernel, dim3(1), dim3(kSetupBlock), 0, static_cast<const uint32_t*>(fl),
+                                 static_cast<const uint32_t*>(fm), gstart, SF.big, SF.chunks, fm + 1, large_list, fm + 3));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "digest_chain", DigestChainKernel, dim3((cap_fb + kChainWaves - 1) / kChainWaves), dim3(64 * kChainWaves), 0,
+                                 static_cast<const uint32_t*>(fl), static_cast<const uint32_t*>(fm), 0u, static_cast<const uint32_t*>(fl),
+                                 static_cast<const uint32_t*>(fm), gstart, ws.chain_starts.as<uint32_t>(), ws.chain_nc.as<int32_t>()));
+      PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 6, fm, 12, hipMemcpyDeviceToHost, ctx->stream));
+      PXG_HIP(hipStreamSynchronize(ctx->stream));
+      SF.n_big = pin32[kMaxKeys + 6];
+      SF.n_chunks = pin32[kMaxKeys + 7];
+      SF.big_max = pin32[kMaxKeys + 8];
+      for (int u = 0; u < a->n_udas; ++u)
+        if (a->uda_kind[u] == PXG_UDA_QUANTILES && SF.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SF, ctx->stream, u));
+    } else {
+      PXG_RETURN_IF_ERROR(ws.bstarts.Ensure(static_cast<size_t>(std::max(SE.n_big, SL.n_big)) * kBigCentroids * 4 + 16));
+      for (int u = 0; u < a->n_udas; ++u) {
+        if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+        if (SL.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SL, ctx->stream, u));
+        if (SE.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SE, ctx->stream, u));
+      }
     }
     PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));

@@ -53,6 +53,9 @@ def test_speculative_chain_matches_sequential(ctx):
     assert list(n1) == list(n0) == [-1, -1]
 
 
+FALLBACK_GROUPS = ("dup", "few", "nan")
+
+
 def _groups(fallback):
     rng = np.random.default_rng(11)
     spec = [
@@ -107,9 +110,9 @@ def _run(ctx, keys, vals, force_sort):
 
 @pytest.mark.parametrize("fallback", [None, "dup", "nan"])
 def test_selection_path_matches_sort_path(ctx, fallback):
-    """Without fallback groups the two paths differ only in big-centroid summation order; with
-    one (duplicates beyond a bin's capacity, NaN values) finalize hands every big group to the
-    sort path, so all results are identical."""
+    """The two paths differ only in big-centroid summation order; a fallback group (duplicates
+    beyond a bin's capacity, NaN values) is handed to the sort path on its own (one quantile
+    UDA), so its results are identical and the others' stay the selection path's."""
     keys, vals, sizes = _groups(fallback)
     _, _, sel = _run(ctx, keys, vals, force_sort=False)
     _, _, srt = _run(ctx, keys, vals, force_sort=True)
@@ -120,7 +123,7 @@ def test_selection_path_matches_sort_path(ctx, fallback):
         assert ca == cb == n
         for name in NAMES:
             a, b = qa[name], qb[name]
-            if n <= 10_000 or fallback:
+            if n <= 10_000 or k in FALLBACK_GROUPS:
                 assert a == b or (a != a and b != b), (k, name, a, b)
             else:
                 assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
@@ -265,8 +268,8 @@ def test_early_set_matches_late_set(ctx, monkeypatch, fallback):
     """Fused split (forced on, > 256 groups): the designated big groups take the selection path
     as their own early set, started before the rest sort finishes (PXG_EARLY_BIG; off, they are
     class 3 of the classification).  Same values, same kernels: the same quantiles (big groups to
-    the last bits of their inside-bin sums), and a fallback group in either set hands both sets to
-    the sort path (identical)."""
+    the last bits of their inside-bin sums), and a fallback group in either set goes to the sort
+    path on its own (identical)."""
     keys, vals, sizes = _groups(fallback)
     rng = np.random.default_rng(77)
     small = {f"s{i}": rng.lognormal(1, 1, 100) for i in range(400)}
@@ -286,7 +289,37 @@ def test_early_set_matches_late_set(ctx, monkeypatch, fallback):
         assert late[k][1] == early[k][1] == n
         for name in NAMES:
             a, b = late[k][0][name], early[k][0][name]
-            if n <= 10_000 or fallback:
+            if n <= 10_000 or k in FALLBACK_GROUPS:
                 assert a == b or (a != a and b != b), (k, name, a, b)
             else:  # (inside-bin sums: atomics, last bits run to run, as in the late set alone)
                 assert abs(a - b) <= 1e-12 * max(abs(a), abs(b)), (k, name, a, b)
+
+
+def test_two_quantile_udas_with_a_fallback_group_sort_every_big_group(ctx):
+    """Two quantile UDAs (over the value and its negation) and a fallback group: the selection
+    plans keep the last UDA's flags only, so finalize hands every big group to the sort path
+    and both UDAs' results equal the forced sort path's exactly."""
+    keys, vals, sizes = _groups("dup")
+    plan = P.linear_plan([P.source_op("t", [5, 4], ["k", "v"], [0, 1]),
+                          P.map_op([P.col(0), P.col(1), P.func("multiply", [P.col(1), P.const(4, -1.0)], [4, 4])], ["k", "v", "w"]),
+                          P.agg_op([0], [P.agg_expr("quantiles", [P.col(1)], [4]), P.agg_expr("quantiles", [P.col(2)], [4], fid=1)]),
+                          P.sink_op("out")])
+    tables = {"t": {"types": [5, 4], "batches": [[Column.from_values(5, keys), Column(4, values=vals)]]}}
+    out = {}
+    for force in (False, True):
+        old = os.environ.pop("PXG_BIG_SORT", None)
+        if force:
+            os.environ["PXG_BIG_SORT"] = "1"
+        try:
+            res = run_plan(ctx, plan, tables)
+        finally:
+            os.environ.pop("PXG_BIG_SORT", None)
+            if old is not None:
+                os.environ["PXG_BIG_SORT"] = old
+        out[force] = {r[0]: (json.loads(r[1]), json.loads(r[2])) for r in rows(res[0]["cols"])}
+    assert set(out[False]) == set(out[True]) == set(sizes)
+    for k in sizes:
+        for j in range(2):
+            for name in NAMES:
+                a, b = out[False][k][j][name], out[True][k][j][name]
+                assert a == b or (a != a and b != b), (k, j, name, a, b)
