@@ -924,6 +924,7 @@ def n1_leg(args, ctx, P, Table, plan_agg):
     step()
     ctx.sync()
     prof_step_ms = (time.perf_counter() - t_prof) * 1000.0
+    fallback_groups = [a.info()["big_sort_groups"]]  # big groups the selection path handed to the sort path
     ctx.set_profiling(False)
     kernel_ms = {}
     for name in KERNELS:
@@ -938,6 +939,7 @@ def n1_leg(args, ctx, P, Table, plan_agg):
         g = step()
     ctx.sync()
     el = time.perf_counter() - ts
+    fallback_groups.append(a.info()["big_sort_groups"])
     ctx.set_profiling(False)
     l, ms, pre = consume_stats(ctx)
     avg = ms / args.n1_steps
@@ -955,6 +957,7 @@ def n1_leg(args, ctx, P, Table, plan_agg):
         "algorithmic_bytes_per_row": alg / n, "generate_s": gen_s,
         "kernel_ms_per_step": kernel_ms, "profiled_step_ms": round(prof_step_ms, 3),
         "finalize_ms_per_step": round(el * 1000.0 / args.n1_steps - avg, 3),
+        "sort_fallback_groups": {"profiled_step": fallback_groups[0], "last_timed_step": fallback_groups[1]},
         "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n),
                      "traffic_source": "committed file (replaced by the live PMC leg when it runs)", "algorithmic_bytes_per_launch": alg,
