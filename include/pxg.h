@@ -304,7 +304,11 @@ int32_t pxg_agg_finalize(pxg_agg* agg, int64_t* n_groups);
  * group-major); the host node renders the JSON string (math_sketches.h:40-54). */
 int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols);
 /* pxg_agg_result with skip[c] != 0 leaving value column c without buffers (type and length
- * set; the caller reads it another way, e.g. pxg_agg_quantile_lanes). */
+ * set; the caller reads it another way, e.g. pxg_agg_quantile_lanes).  For a QUANTILES column,
+ * skip[c] = 0x80 | lane_mask returns its plucked lanes instead: values = the lanes as
+ * pxg_agg_quantile_lanes lays them out (lane-major, n_groups doubles per lane in mask order,
+ * pluck's 0.0 for a group with a non-finite quantile), data = the n_groups finiteness bytes
+ * (data_len = n_groups). */
 int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32_t n_cols, const uint8_t* skip);
 /* pxg_agg_finalize + pxg_agg_result_skip in one call: the finalize issues each result column's
  * device-to-host copy as soon as the column is produced (group keys while the quantile digests
@@ -318,11 +322,12 @@ int32_t pxg_agg_finalize_result(pxg_agg* agg, int64_t* n_groups, pxg_column_out*
  * synthetic row of a group-less agg over no rows; the caller then uses pxg_agg_result. */
 int32_t pxg_agg_result_device(pxg_agg* agg, pxg_column_view* cols, int32_t n_cols, int64_t* bytes);
 /* The quantile lanes a post-aggregate pluck_float64 reads (MapNode over the AggNode output,
- * math_sketches.h:40-54 + the pluck UDF): for every group, the lanes set in lane_mask (bit k =
- * p01,p10,p25,p50,p75,p90,p99[k]) packed in lane order into host_out (popcount(mask) doubles
- * per group), and host_finite[g] = 1 when all 7 quantiles of the group are finite (a NaN / inf
- * one truncates the reference's JSON, which pluck then fails to parse: 0.0 for every key).
- * Host buffers hold n_groups * popcount(mask) doubles / n_groups bytes. */
+ * math_sketches.h:40-54 + the pluck UDF): the lanes set in lane_mask (bit k =
+ * p01,p10,p25,p50,p75,p90,p99[k]), lane-major in lane order (the j-th selected lane of group g
+ * at host_out[j * n_groups + g]) with pluck's value: 0.0 for a group whose 7 quantiles are not
+ * all finite (a NaN / inf one truncates the reference's JSON, which pluck then fails to parse);
+ * host_finite[g] = 1 when they are.  Host buffers hold n_groups * popcount(mask) doubles /
+ * n_groups bytes. */
 int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t lane_mask, double* host_out, uint8_t* host_finite);
 void pxg_result_free(pxg_column_out* cols, int32_t n_cols);
 /* Host buffers for result hand-off (no reference counterpart: replaces the per-query malloc of

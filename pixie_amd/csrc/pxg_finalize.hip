@@ -2227,6 +2227,55 @@ struct SideJoinGuard {
 };
 
 
+// Selected quantile lanes, lane-major (lane j of group g at out[j * G + g]) with pluck_float64's
+// rule applied: 0.0 for a group whose 7 quantiles are not all finite (a NaN / inf one makes the
+// reference's JSON unparsable, so pluck yields 0.0 for every key); fin[g] = that flag.  Each lane
+// is then a ready FLOAT64 column for the post-aggregate map.
+__global__ void QuantLanesKernel(const double* __restrict__ q, uint64_t G, uint32_t mask, double* __restrict__ out,
+                                 uint8_t* __restrict__ fin) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  double v[7];
+  bool f = true;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    v[k] = q[g * 7 + k];
+    f = f && !isnan(v[k]) && !isinf(v[k]);
+  }
+  int o = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+    if ((mask >> k) & 1u) out[static_cast<uint64_t>(o++) * G + g] = f ? v[k] : 0.0;
+  fin[g] = f ? 1 : 0;
+}
+
+// A quantiles result column requested as its plucked lanes (skip[c] = kSkipLanes | lane mask,
+// pxg_agg_result_skip / pxg_agg_finalize_result): values = the lanes (QuantLanesKernel layout),
+// data = the G finiteness bytes.  Host blocks are taken once; a second call (the finalize's
+// sort-path fallback changed quantiles) rewrites them.  Stream-ordered, no wait.
+constexpr uint8_t kSkipLanes = 0x80;
+int32_t IssueLanes(Agg& a, int u, uint32_t mask, pxg_column_out& o) {
+  const uint64_t G = static_cast<uint64_t>(a.res.n_groups);
+  mask &= 0x7Fu;
+  const int nsel = __builtin_popcount(mask);
+  o.type = a.uda_out_type[u];
+  o.length = static_cast<int64_t>(G);
+  if (G == 0) return PXG_OK;
+  if (!o.data) {
+    o.values = ResultAlloc(std::max<size_t>(G * nsel * 8, 8));
+    o.data = static_cast<uint8_t*>(ResultAlloc(G + 16));
+    o.data_len = static_cast<int64_t>(G);
+    if (!o.values || !o.data) return SetError(PXG_RESOURCE_UNAVAILABLE, "host result allocation failed");
+  }
+  PXG_RETURN_IF_ERROR(a.res.lanes.Ensure(G * (8 * nsel + 1) + 16));
+  double* d_out = a.res.lanes.as<double>();
+  uint8_t* d_fin = reinterpret_cast<uint8_t*>(d_out + G * nsel);
+  PXG_RETURN_IF_ERROR(Launch(a.ctx, "quant_lanes", QuantLanesKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
+                             a.res.uda_out[u].as<const double>(), G, mask, d_out, d_fin));
+  if (nsel) PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, o.values, d_out, G * nsel * 8));
+  return CopyD2H(a.ctx, a.ctx->stream, o.data, d_fin, G);
+}
+
 int32_t AggFinalizeTable(Agg* a) {
   Ctx* ctx = a->ctx;
   SideJoinGuard guard{ctx};
@@ -2819,6 +2868,17 @@ int32_t AggFinalizeTable(Agg* a) {
     R.ready = true;
     return PXG_OK;
   }
+  // Early result: quantile columns asked for as plucked lanes, behind the digests, so their
+  // copies land within the synchronisation below.
+  auto IssueEarlyLanes = [&]() -> int32_t {
+    if (!a->early.want || !a->early.skip || a->merged) return PXG_OK;
+    for (int u = 0; u < a->n_udas; ++u) {
+      const uint8_t sk = a->early.skip[a->n_keys + u];
+      if (a->uda_kind[u] == PXG_UDA_QUANTILES && (sk & kSkipLanes)) PXG_RETURN_IF_ERROR(IssueLanes(*a, u, sk, a->early.cols[a->n_keys + u]));
+    }
+    return PXG_OK;
+  };
+  PXG_RETURN_IF_ERROR(IssueEarlyLanes());
   // One sync for the digest error flag and every string-key total.
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;
@@ -2895,6 +2955,7 @@ int32_t AggFinalizeTable(Agg* a) {
         if (SE.n_big > 0) PXG_RETURN_IF_ERROR(BigSortPath(SE, ctx->stream, u));
       }
     }
+    PXG_RETURN_IF_ERROR(IssueEarlyLanes());  // the recomputed groups' lanes
     PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     PXG_HIP(hipStreamSynchronize(ctx->stream));
     err = pin32[kMaxKeys];
@@ -2951,23 +3012,6 @@ extern "C" int32_t pxg_agg_result(pxg_agg* agg, pxg_column_out* cols, int32_t n_
   return pxg_agg_result_skip(agg, cols, n_cols, nullptr);
 }
 
-// Selected quantile lanes, packed, plus whether all 7 of a group's quantiles are finite (a NaN /
-// inf one makes the reference's JSON unparsable, so pluck_float64 yields 0.0 for every key).
-__global__ void QuantLanesKernel(const double* __restrict__ q, uint64_t G, uint32_t mask, int nsel, double* __restrict__ out,
-                                 uint8_t* __restrict__ fin) {
-  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  bool f = true;
-  int o = 0;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const double v = q[g * 7 + k];
-    f = f && !isnan(v) && !isinf(v);
-    if ((mask >> k) & 1u) out[g * nsel + o++] = v;
-  }
-  fin[g] = f ? 1 : 0;
-}
-
 extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t lane_mask, double* host_out, uint8_t* host_finite) {
   if (!agg || !host_finite || (lane_mask && !host_out)) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   Agg& a = agg->impl;
@@ -2982,7 +3026,7 @@ extern "C" int32_t pxg_agg_quantile_lanes(pxg_agg* agg, int32_t uda, uint32_t la
   double* d_out = a.res.lanes.as<double>();
   uint8_t* d_fin = reinterpret_cast<uint8_t*>(d_out + G * nsel);
   PXG_RETURN_IF_ERROR(Launch(a.ctx, "quant_lanes", QuantLanesKernel, dim3(GridFor(static_cast<int64_t>(G), 256, 1 << 30)), dim3(256), 0,
-                             a.res.uda_out[uda].as<const double>(), G, lane_mask, nsel, d_out, d_fin));
+                             a.res.uda_out[uda].as<const double>(), G, lane_mask, d_out, d_fin));
   if (nsel) PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, host_out, d_out, G * nsel * 8));
   PXG_RETURN_IF_ERROR(CopyD2H(a.ctx, a.ctx->stream, host_finite, d_fin, G));
   PXG_HIP(hipStreamSynchronize(a.ctx->stream));
@@ -3153,6 +3197,10 @@ extern "C" int32_t pxg_agg_result_skip(pxg_agg* agg, pxg_column_out* cols, int32
     pxg_column_out& o = cols[a.n_keys + u];
     o.type = a.uda_out_type[u];
     o.length = rows;
+    if (skip && (skip[a.n_keys + u] & kSkipLanes) && a.uda_kind[u] == PXG_UDA_QUANTILES && !synth) {
+      PXG_RETURN_IF_ERROR(IssueLanes(a, u, skip[a.n_keys + u], o));
+      continue;
+    }
     if (skip && skip[a.n_keys + u] && !synth) continue;  // left without buffers (the caller fetches it otherwise)
     const bool q = a.uda_kind[u] == PXG_UDA_QUANTILES;
     const size_t per = q ? 56 : 8;

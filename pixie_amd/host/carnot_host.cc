@@ -26,6 +26,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -33,6 +34,8 @@
 #include <thread>
 #include <tuple>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../include/pxcarnot.h"
 #include "../../include/pxg.h"
@@ -1402,7 +1405,8 @@ class GpuAggNode : public ExecNode {
         observed = observed || ch.first->ReadsColumnValue(c);
         lanes[c] |= ch.first->PluckedLanes(c);
       }
-      skip[c] = observed || !DevicePluck() ? 0 : 1;
+      // pluck-only: the column comes back as its plucked lanes (pxg.h, skip = 0x80 | lane mask)
+      skip[c] = observed || !DevicePluck() ? 0 : static_cast<uint8_t>(0x80u | (lanes[c] & 0x7Fu));
     }
     bool fetched = false;
     if (dev_ok) {
@@ -1442,15 +1446,13 @@ class GpuAggNode : public ExecNode {
     const int64_t G = out.empty() ? 0 : out[0].length;
     for (size_t c = 0; c < out.size(); ++c) {
       if (!skip[c] || groups == 0) continue;
-      QuantLanes ql;
+      QuantLanes ql;  // values = the lanes, data = the finiteness bytes (one owner for both)
       ql.mask = lanes[c] & 0x7Fu;
       ql.nsel = __builtin_popcount(ql.mask);
-      double* vals = nullptr;
-      ql.vals = PooledDoubleColumn(G * ql.nsel, &vals);
-      void* fb = pxg_host_alloc(G + 16);
-      if (!fb) return Err(PXG_RESOURCE_UNAVAILABLE, "host buffer of %lld bytes", (long long)G);
-      ql.finite = std::shared_ptr<void>(fb, [](void* q) { pxg_host_free(q); });
-      PXG_CALL(pxg_agg_quantile_lanes(agg_, static_cast<int32_t>(c - keys.size()), ql.mask, vals, static_cast<uint8_t*>(fb)));
+      ql.vals = FromOut(out[c]);
+      ql.vals.type = F;
+      ql.vals.data = nullptr;
+      ql.finite = std::shared_ptr<void>(ql.vals.owner, const_cast<uint8_t*>(out[c].data));
       quantile_lanes_[c] = ql;
     }
     clk.Mark("agg result D2H");
@@ -1458,8 +1460,8 @@ class GpuAggNode : public ExecNode {
     ob.num_rows = G;
     for (size_t c = 0; c < out.size(); ++c) {
       const bool q = !emit_states && c >= keys.size() && udas[c - keys.size()].kind == PXG_UDA_QUANTILES;
-      if (q && skip[c]) {  // G empty strings keep the batch's relation
-        pxg_result_free(&out[c], 1);
+      if (q && skip[c]) {  // G empty strings keep the batch's relation (the lanes are owned above)
+        if (groups == 0) pxg_result_free(&out[c], 1);
         ob.cols.push_back(EmptyStringColumn(out[c].length));
         continue;
       }
@@ -1488,7 +1490,7 @@ class GpuAggNode : public ExecNode {
   struct QuantLanes {
     uint32_t mask = 0;
     int nsel = 0;
-    HostColumn vals;               // G * nsel doubles, lanes in bit order
+    HostColumn vals;               // nsel lanes of G doubles (lane-major, in bit order)
     std::shared_ptr<void> finite;  // G bytes: all 7 quantiles finite
   };
   std::map<size_t, QuantLanes> quantile_lanes_;
@@ -1765,19 +1767,26 @@ class PostAggMapNode : public ExecNode {
     std::vector<HostColumn> env = rb.cols;
     finite_.clear();
     for (auto& pk : plucks_) {
-      double* v = nullptr;
-      HostColumn vc = PooledDoubleColumn(G, &v);
       auto it = agg_ ? agg_->quantiles_raw_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantiles_raw_.end()){};
       auto lt = agg_ ? agg_->quantile_lanes_.find(static_cast<size_t>(pk.first)) : decltype(agg_->quantile_lanes_.end()){};
       int qk = -1;
       for (int k = 0; k < 7; ++k)
         if (pk.second == kQuantileKeys[k]) qk = k;
-      if (agg_ && lt != agg_->quantile_lanes_.end()) {  // plucked on the device
+      if (agg_ && lt != agg_->quantile_lanes_.end()) {  // plucked on the device: the lane is the column
         const auto& ql = lt->second;
-        const double* d = static_cast<const double*>(ql.vals.values);
-        const uint8_t* fin = static_cast<const uint8_t*>(ql.finite.get());
         const int at = qk >= 0 && ((ql.mask >> qk) & 1u) ? __builtin_popcount(ql.mask & ((1u << qk) - 1)) : -1;
-        for (int64_t g = 0; g < G; ++g) v[g] = (at >= 0 && fin[g]) ? d[g * ql.nsel + at] : 0.0;
+        if (at >= 0) {
+          HostColumn lc = ql.vals;
+          lc.length = G;
+          lc.values = static_cast<const double*>(ql.vals.values) + static_cast<int64_t>(at) * G;
+          env.push_back(lc);
+          continue;
+        }
+      }
+      double* v = nullptr;
+      HostColumn vc = PooledDoubleColumn(G, &v);
+      if (agg_ && lt != agg_->quantile_lanes_.end()) {
+        for (int64_t g = 0; g < G; ++g) v[g] = 0.0;
       } else if (agg_ && it != agg_->quantiles_raw_.end()) {
         // A NaN / inf quantile truncates the reference's JSON (json_double.h), which rapidjson then
         // fails to parse: pluck_float64 returns 0.0 for every key of that group.  The per-group
@@ -3039,6 +3048,72 @@ struct SpanWriter {
   void offsets(const int32_t* src, size_t count, int32_t o0) { RebaseOffsets(claim(4 * count), src, count, o0); }
 };
 
+// Persistent copy workers for the PXRB pass: a result of a few MB (C2: 4.8 MB, 0.12 ms on one
+// thread) is split over threads that already exist, since starting threads per query cost more
+// than the copy.  Run(n, fn) calls fn(i) for i in [0, n) on the workers and the caller.
+class CopyPool {
+ public:
+  static CopyPool& Get() {
+    // Never destroyed (workers may outlive static teardown); a forked child, which has none of
+    // the parent's threads, makes its own.
+    static CopyPool* p = nullptr;
+    static pid_t owner = 0;
+    static std::mutex m;
+    std::lock_guard<std::mutex> lk(m);
+    if (!p || owner != getpid()) {
+      p = new CopyPool();
+      owner = getpid();
+    }
+    return *p;
+  }
+  size_t workers() const { return th_.size(); }
+  void Run(size_t n, const std::function<void(size_t)>& fn) {
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &fn;
+    n_ = n;
+    next_.store(0);
+    active_ = th_.size();
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    Work(fn, n);
+    lk.lock();
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  CopyPool() {
+    const size_t k = std::min<size_t>(7, std::max(1u, std::thread::hardware_concurrency()) - 1);
+    for (size_t i = 0; i < k; ++i)
+      th_.emplace_back([this] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return gen_ != seen; });
+          seen = gen_;
+          const std::function<void(size_t)>* fn = job_;
+          const size_t n = n_;
+          lk.unlock();
+          if (fn) Work(*fn, n);
+          lk.lock();
+          if (--active_ == 0) done_cv_.notify_all();
+        }
+      });
+    for (auto& t : th_) t.detach();
+  }
+  void Work(const std::function<void(size_t)>& fn, size_t n) {
+    for (size_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t n_ = 0, active_ = 0;
+  uint64_t gen_ = 0;
+  std::atomic<size_t> next_{0};
+};
+
 template <typename W>
 static void WriteBatch(W* w, const RowBatch& rb) {
   w->template put<int64_t>(rb.num_rows);
@@ -3337,35 +3412,38 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
       for (auto& im : images)
         if (image_rc == PXG_OK) image_rc = pxg_pxrb_copy(im.img, w.p + im.at);
     });
-  const size_t nthreads = host_bytes < (size_t(32) << 20) ? 1 : std::min<size_t>({16, host_bytes >> 23, std::max(1u, std::thread::hardware_concurrency())});
+  // Up to ~1 MB: one thread.  Larger: the persistent copy workers (CopyPool), by contiguous
+  // ranges of whole batches when there are many, else by ~256 KB pieces of the column copies.
+  CopyPool& pool = CopyPool::Get();
+  const size_t nthreads = host_bytes < (size_t(1) << 20) ? 1 : pool.workers() + 1;
   if (nthreads <= 1) {
     for (auto& j : jobs) {
       SpanWriter sw{w.p + j.at};
       WriteBatch(&sw, *j.rb);
     }
   } else if (jobs.size() >= 4 * nthreads) {
-    std::vector<std::thread> th;
-    size_t j0 = 0;
-    for (size_t k = 0; k < nthreads && j0 < jobs.size(); ++k) {  // contiguous ranges of ~equal bytes
-      const size_t goal = jobs[j0].at + (w.n - jobs[j0].at) / (nthreads - k);
+    const size_t nr = 4 * nthreads;  // contiguous ranges of ~equal bytes
+    std::vector<size_t> cut(1, 0);
+    for (size_t k = 0; k < nr && cut.back() < jobs.size(); ++k) {
+      const size_t j0 = cut.back();
+      const size_t goal = jobs[j0].at + (w.n - jobs[j0].at) / (nr - k);
       size_t j1 = j0 + 1;
       while (j1 < jobs.size() && jobs[j1].at < goal) ++j1;
-      th.emplace_back([&jobs, &w, j0, j1] {
-        for (size_t j = j0; j < j1; ++j) {
-          SpanWriter sw{w.p + jobs[j].at};
-          WriteBatch(&sw, *jobs[j].rb);
-        }
-      });
-      j0 = j1;
+      cut.push_back(j1);
     }
-    for (auto& t : th) t.join();
+    pool.Run(cut.size() - 1, [&](size_t r) {
+      for (size_t j = cut[r]; j < cut[r + 1]; ++j) {
+        SpanWriter sw{w.p + jobs[j].at};
+        WriteBatch(&sw, *jobs[j].rb);
+      }
+    });
   } else {
     std::vector<CopyTask> tasks;
     for (auto& j : jobs) {
       TaskWriter tw{w.p + j.at, &tasks};
       WriteBatch(&tw, *j.rb);
     }
-    constexpr size_t kPiece = size_t(1) << 20;
+    constexpr size_t kPiece = size_t(1) << 18;
     std::vector<CopyTask> pieces;
     for (const CopyTask& t : tasks) {
       for (size_t at = 0; at < t.bytes; at += kPiece) {
@@ -3374,17 +3452,11 @@ static int32_t ExecuteImpl(pxc_engine* engine, const uint8_t* plan, int64_t plan
         else pieces.push_back({t.dst + at, static_cast<const uint8_t*>(t.src) + at, len, 0, false});
       }
     }
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < std::min(nthreads, pieces.size()); ++k)
-      th.emplace_back([&] {
-        for (size_t i = next.fetch_add(1); i < pieces.size(); i = next.fetch_add(1)) {
-          const CopyTask& t = pieces[i];
-          if (t.offs) RebaseOffsets(t.dst, static_cast<const int32_t*>(t.src), t.bytes / 4, t.o0);
-          else std::memcpy(t.dst, t.src, t.bytes);
-        }
-      });
-    for (auto& t : th) t.join();
+    pool.Run(pieces.size(), [&](size_t i) {
+      const CopyTask& t = pieces[i];
+      if (t.offs) RebaseOffsets(t.dst, static_cast<const int32_t*>(t.src), t.bytes / 4, t.o0);
+      else std::memcpy(t.dst, t.src, t.bytes);
+    });
   }
   if (image_copy.joinable()) image_copy.join();
   if (image_rc != PXG_OK) return Fail(FromPxg(image_rc));

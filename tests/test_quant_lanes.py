@@ -1,6 +1,7 @@
 """pxg_agg_result_skip + pxg_agg_quantile_lanes (pluck on the device) against pxg_agg_result:
-the packed lanes equal the selected columns of the 7-double quantiles, the finiteness flag is
-set exactly when all 7 are finite, and a skipped column comes back without buffers."""
+the lane-major lanes equal the selected columns of the 7-double quantiles (0.0 for a group with a
+non-finite quantile, as pluck_float64 of its JSON), the finiteness flag is set exactly when all 7
+are finite, and a skipped column comes back without buffers."""
 import ctypes as C
 
 import numpy as np
@@ -42,10 +43,11 @@ def test_quantile_lanes_match_full_result(ctx):
         rc = lib.pxg_agg_quantile_lanes(a.h, 1, mask, out.ctypes.data_as(C.c_void_p), fin.ctypes.data_as(C.c_void_p))
         assert rc == 0
         sel = [k for k in range(7) if (mask >> k) & 1]
-        got = out[:G * nsel].reshape(G, nsel)
-        want = qv[:, sel]
-        assert np.array_equal(np.isnan(got), np.isnan(want)) and np.array_equal(got[~np.isnan(got)], want[~np.isnan(want)])
-        assert np.array_equal(fin.astype(bool), np.isfinite(qv).all(axis=1))
+        got = out[:G * nsel].reshape(nsel, G).T      # lane-major
+        finite = np.isfinite(qv).all(axis=1)
+        want = np.where(finite[:, None], qv[:, sel], 0.0)  # pluck_float64 of an unparsable JSON: 0.0
+        assert np.array_equal(got, want)
+        assert np.array_equal(fin.astype(bool), finite)
     assert (~np.isfinite(qv).all(axis=1)).sum() > 0
     # skip: the quantiles column comes back typed and sized, without buffers
     outs = (_lib.ColumnOut * 3)()
@@ -121,5 +123,38 @@ def test_finalize_result_equals_finalize_then_result(ctx, skip_q):
         assert gc == c and abs(gm - m) <= 1e-12 * abs(m), k
         if qq is not None and c <= 8000:
             assert gq == qq, k
+    a.close()
+    t.close()
+
+
+@pytest.mark.parametrize("via", ["result_skip", "finalize_result"])
+def test_lanes_result_mode_equals_quantile_lanes(ctx, via):
+    """skip[c] = 0x80 | mask returns the quantiles column as its plucked lanes (values) and the
+    finiteness bytes (data), identical to pxg_agg_quantile_lanes; through pxg_agg_finalize_result
+    the lanes are issued inside the finalize, before its last synchronisation."""
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events(20250117, 0, 3_000_000, 10_000_000)
+    q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
+    a = q.make_agg(ctx)
+    lib = ctx.lib
+    mask = 0b1001000  # p50, p99
+    a.consume(t)
+    ng = C.c_int64(0)
+    outs = (_lib.ColumnOut * 5)()
+    skip = (C.c_uint8 * 5)(0, 0, 0, 0, 0x80 | mask)
+    if via == "result_skip":
+        assert lib.pxg_agg_finalize(a.h, C.byref(ng)) == 0
+        assert lib.pxg_agg_result_skip(a.h, outs, 5, skip) == 0
+    else:
+        assert lib.pxg_agg_finalize_result(a.h, C.byref(ng), outs, 5, skip) == 0
+    G = ng.value
+    assert G > 20_000 and outs[4].length == G and outs[4].data_len == G
+    got = np.ctypeslib.as_array(C.cast(outs[4].values, C.POINTER(C.c_double)), shape=(2 * G,)).copy()
+    got_fin = np.ctypeslib.as_array(C.cast(outs[4].data, C.POINTER(C.c_uint8)), shape=(G,)).copy()
+    want = np.zeros(2 * G, dtype=np.float64)
+    fin = np.zeros(G, dtype=np.uint8)
+    assert lib.pxg_agg_quantile_lanes(a.h, 2, mask, want.ctypes.data_as(C.c_void_p), fin.ctypes.data_as(C.c_void_p)) == 0
+    assert np.array_equal(got, want) and np.array_equal(got_fin, fin)
+    lib.pxg_result_free(outs, 5)
     a.close()
     t.close()
