@@ -853,7 +853,7 @@ struct BigGroup {
 // the 512-thread / 70 KB splitter launch runs only those, instead of one block per big group
 // that must find 70 KB of free LDS before it can exit.
 constexpr int kSetupBlock = 1024;
-constexpr uint64_t kSelLargeN = uint64_t(1) << 22;
+constexpr uint64_t kSelLargeN = uint64_t(1) << 21;
 __global__ void __launch_bounds__(kSetupBlock) BigSetupKernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                               const uint32_t* __restrict__ gstart, BigGroup* __restrict__ groups,
                                                               BigChunk* __restrict__ chunks, uint32_t* __restrict__ meta_out,
@@ -1396,11 +1396,15 @@ constexpr int kSelLists = 3;  // gathered bins: <= 1024 values (wave), <= 4096 (
 // Groups under 16K values use ~16-32 values per bin (128..1024 bins): their sample (2 nb keys)
 // and its sort stay a small fraction of the group (at 1B rows 1,872 of the 2,692 big groups hold
 // 4K-16K values; a 2048-key sample of a 5000-value group cost almost a sort of the group).
-// The largest groups use 2048 bins too (a 4096-key sample): the 8192-key sample of a > 4M-value
-// group took one 512-thread workgroup ~0.2 ms on the critical path at 1B rows, more than its
-// larger bins cost the bin sorts.
+// Groups above kSelLargeN (2M) values use all 4096 bins (an 8192-key sample, the 512-thread
+// launch over BigSetup's list of them): with 2048 bins a 6.9M-value group averaged ~3.4K values
+// per bin, and a gathered bin holds a Gamma(2)-distributed multiple of that (the splitters are
+// every other sample), so one past kSelCollCap (4.9x the mean) sent the group to the sort path in
+// ~5% of 1B-row finalizes (tools/n1_fallback.py: 2 of 40).  At 4096 bins that is 9.7x the mean
+// (~1e-7 per bin).  Those groups are the designated ones of the fused split, whose selection
+// runs off the critical path (the early set).
 __device__ __forceinline__ int SelNb(uint64_t n) {
-  if (n > (uint64_t(1) << 21)) return kSelBins / 2;
+  if (n > kSelLargeN) return kSelBins;
   int nb = kSelBins / 4;
   while (nb > 128 && static_cast<uint64_t>(nb) * 16 > n) nb >>= 1;
   return nb;
@@ -2173,6 +2177,8 @@ struct BigSet {
   const int32_t* chain_nc = nullptr;
   DevBuf *spl = nullptr, *cnt = nullptr, *list = nullptr, *bstart = nullptr, *tag = nullptr, *cbase = nullptr, *plan = nullptr,
          *partial = nullptr;
+  const uint32_t* large_list = nullptr;  // set indices of the groups above kSelLargeN values (BigSetupKernel)
+  const uint32_t* large_cnt = nullptr;
 };
 
 // The early set: the designated groups of a fused split (ids [Gr, G)) above mid_max values.
@@ -2620,6 +2626,10 @@ int32_t AggFinalizeTable(Agg* a) {
     uint16_t* guide = reinterpret_cast<uint16_t*>(S.spl->as<uint64_t>() + nb * kSelBins);
     PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_sample", BigSampleKernel<kSelSample / 2>, dim3(S.n_big), dim3(kSelSample / 2 / kMsIpt), 0,
                                  static_cast<const BigGroup*>(S.big), S.d_count, vals, at, S.spl->as<uint64_t>(), guide, nullptr, nullptr));
+    const uint32_t n_large = static_cast<uint32_t>(std::min<uint64_t>(S.n_big, n / kSelLargeN + 1));  // groups above kSelLargeN: bound
+    PXG_RETURN_IF_ERROR(LaunchOn(ctx, st, "quant_sel_sample", BigSampleKernel<kSelSample>, dim3(n_large), dim3(kSelSample / kMsIpt), 0,
+                                 static_cast<const BigGroup*>(S.big), S.d_count, vals, at, S.spl->as<uint64_t>(), guide, S.large_list,
+                                 S.large_cnt));
     const uint32_t cpb = SelChunksPerBlock(S.n_chunks, ctx->num_cus, 3, kSelHistCap);
     return LaunchOn(ctx, st, "quant_sel_hist", at == PXG_FLOAT64 ? BigHistKernel<true> : BigHistKernel<false>, dim3((S.n_chunks + cpb - 1) / cpb),
                     dim3(256), 0, static_cast<const BigChunk*>(S.chunks), S.d_meta, vals, at, S.spl->as<const uint64_t>(),
@@ -2692,6 +2702,8 @@ int32_t AggFinalizeTable(Agg* a) {
     SE.cbase = &E.cbase;
     SE.plan = &E.plan;
     SE.partial = &E.partial;
+    SE.large_list = large_list;
+    SE.large_cnt = em + 3;
     PXG_RETURN_IF_ERROR(EnsureSel(SE));
     PXG_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_early, 0));
     guard.side2 = true;
@@ -2810,6 +2822,8 @@ int32_t AggFinalizeTable(Agg* a) {
     SL.cbase = &ws.sel_cbase;
     SL.plan = &ws.sel_plan;
     SL.partial = &ws.sel_partial;
+    SL.large_list = large_list;
+    SL.large_cnt = large_cnt;
     // PXG_BIG_SORT=1 forces the full sort path for every big group (tests compare the two).
     big_select = n_big > 0 && !EnvFlag("PXG_BIG_SORT") && !a->export_x;
     if (big_select) PXG_RETURN_IF_ERROR(EnsureSel(SL));
@@ -2824,15 +2838,21 @@ int32_t AggFinalizeTable(Agg* a) {
       PXG_HIP(hipStreamWaitEvent(lst, ctx->ev_meta, 0));
       if (!early_on) guard.side2 = true;
     }
-    for (int u = 0; u < a->n_udas; ++u) {
-      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
-      const uint64_t* vals = cv.p[a->uda_val[u]];
-      const int at = a->uda_arg_type[u];
+    // (Issuing the late set after the mid classes when an early set runs started QuantMid<8192>
+    // 0.12 ms sooner at 1B rows but only moved the LDS contention: span 3.96 -> 4.02 ms.)
+    auto IssueLate = [&](int u) -> int32_t {
       if (big_select) PXG_RETURN_IF_ERROR(BigSelectFront(SL, lst, u));
       if (n_big > 0) {
         PXG_HIP(hipStreamWaitEvent(lst, ctx->ev_chain, 0));
         PXG_RETURN_IF_ERROR(big_select ? BigSelectBack(SL, lst, u) : BigSortPath(SL, lst, u));
       }
+      return PXG_OK;
+    };
+    for (int u = 0; u < a->n_udas; ++u) {
+      if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
+      const uint64_t* vals = cv.p[a->uda_val[u]];
+      const int at = a->uda_arg_type[u];
+      PXG_RETURN_IF_ERROR(IssueLate(u));
       double* qo = R.uda_out[u].as<double>();
       if (!a->export_x) {  // the mid classes, one launch each (largest first: the longest workgroups)
         const uint32_t* cnt_mid = reinterpret_cast<const uint32_t*>(meta + 64);

@@ -2,8 +2,6 @@
 # own time limit and the steps are chained with &&.
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_quant_lanes.py tests/test_host_engine.py > gpurun_out/t.log 2>&1 &&
-timeout -k 10 300 python3 -u tools/engine_outlier.py 100000000 10 > gpurun_out/eo.json 2> gpurun_out/eo.log &&
-PXC_TIMING= PXG_TIMING= timeout -k 10 300 python3 -u tools/engine_outlier.py 100000000 10 > gpurun_out/eo_plain.json 2> gpurun_out/eo_plain.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_n1only -o run --output-format csv -- python3 tools/n1_prof.py 4 > gpurun_out/prof_n1only.log 2>&1 &&
 true
-rc=$?; tail -2 gpurun_out/t.log; cat gpurun_out/eo.json gpurun_out/eo_plain.json; exit $rc
+rc=$?; grep n1_prof gpurun_out/prof_n1only.log; exit $rc

@@ -21,7 +21,7 @@ t.flush()
 for name, mk in [("plan_agg", lambda: plan_agg(ctx, P.c2_plan(with_pluck=True), "http_events", P.HTTP_TYPES, expected_groups=65536)),
                  ("linear", lambda: LinearQuery(P.c2_plan(with_pluck=True), P.HTTP_TYPES, expected_groups=65536).make_agg(ctx))]:
     a = mk()
-    for i in range(3):
+    for i in range(int(os.environ.get("N1_STEPS", "3"))):
         ctx.sync()
         t0 = time.perf_counter()
         a.reset()
