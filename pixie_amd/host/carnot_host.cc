@@ -145,23 +145,6 @@ struct OwnedColumn {
   std::vector<uint8_t> data;
 };
 
-static HostColumn StringColumn(const std::vector<std::string>& vals) {
-  auto o = std::make_shared<OwnedColumn>();
-  o->offsets.push_back(0);
-  for (auto& s : vals) {
-    o->data.insert(o->data.end(), s.begin(), s.end());
-    o->offsets.push_back(static_cast<int32_t>(o->data.size()));
-  }
-  o->data.resize(o->data.size() + 16, 0);
-  HostColumn hc;
-  hc.type = PXG_STRING;
-  hc.length = static_cast<int64_t>(vals.size());
-  hc.offsets = o->offsets.data();
-  hc.data = o->data.data();
-  hc.owner = o;
-  return hc;
-}
-
 // G empty strings (one zeroed offsets array, no per-row std::string).
 static HostColumn EmptyStringColumn(int64_t n) {
   // n + 1 zero offsets and a zeroed 16-byte payload pad in one host-pool block.
@@ -192,17 +175,6 @@ static HostColumn PooledDoubleColumn(int64_t n, double** out) {
   return hc;
 }
 
-static HostColumn DoubleColumn(const std::vector<double>& vals) {
-  auto o = std::make_shared<OwnedColumn>();
-  o->values.resize(vals.size() * 8 + 8);
-  if (!vals.empty()) std::memcpy(o->values.data(), vals.data(), vals.size() * 8);
-  HostColumn hc;
-  hc.type = PXG_FLOAT64;
-  hc.length = static_cast<int64_t>(vals.size());
-  hc.values = o->values.data();
-  hc.owner = o;
-  return hc;
-}
 
 struct RowBatch {
   std::vector<HostColumn> cols;
