@@ -45,8 +45,40 @@ __global__ void ChunkGroupKernel(const uint32_t* __restrict__ cbase, uint32_t ng
   cgroup[c] = lo;
 }
 
-// Partial state per (uda, chunk): SUM/MINSUM/MEAN = sum (int64 bits or double bits),
-// MIN/MAX = order-preserving int64 of the extreme (NaN skipped), COUNT unused.
+// Floating-point sums in double-double (an error-free TwoSum per addition, the error words
+// summed beside): a group's sum is then its exact sum to ~2^-100 relative, rounded once at the
+// end, so it no longer depends on the order its values were staged in (that order is the
+// consume's tile completion order, which differs run to run; plain double sums differed in the
+// last bits).  The reference sums sequentially in double; both agree to its rounding.
+// Compiled with -ffp-contract=off (the transformations need unfused operations).
+struct DD {
+  double hi, lo;
+};
+__device__ __forceinline__ DD TwoSum(double a, double b) {
+  const double s = a + b;
+  const double bb = s - a;
+  return DD{s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ DD DDAdd(DD x, DD y) {
+  const DD s = TwoSum(x.hi, y.hi);
+  const double e = s.lo + (x.lo + y.lo);
+  const double h = s.hi + e;
+  return DD{h, e - (h - s.hi)};
+}
+__device__ __forceinline__ DD DDAddD(DD x, double b) { return DDAdd(x, DD{b, 0.0}); }
+__device__ __forceinline__ DD WaveSumDD(DD v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = DDAdd(v, DD{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)});
+  return v;
+}
+// The rounded sum (non-finite: the plain sum's inf / NaN, whose error words are meaningless).
+__device__ __forceinline__ double DDValue(DD v) { return isfinite(v.hi) ? v.hi + v.lo : v.hi; }
+// Partial rows per UDA: [u] the sum's high words (or the integer / extreme state), [n_udas + u]
+// MEAN_MERGE sizes, [2 n_udas + u] the sum's low words.
+constexpr int kPartialRows = 3;
+
+// Partial state per (uda, chunk): SUM/MINSUM/MEAN = sum (int64 bits, or a double-double: high
+// and low words), MIN/MAX = order-preserving int64 of the extreme (NaN skipped), COUNT unused.
 __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __restrict__ plan, const uint32_t* __restrict__ gstart,
                                                          const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ cgroup,
                                                          uint32_t ngroups, ConstValPtrs vals, uint64_t* __restrict__ partial,
@@ -67,32 +99,36 @@ __global__ void __launch_bounds__(256) ChunkReduceKernel(const AggPlanDev* __res
     uint64_t r = 0;
     if (kind == PXG_UDA_MEAN_MERGE) {  // MeanUDA::Merge: sizes into the second partial row
       const uint64_t* sz = vals.p[plan->uda_val2[u]];
-      double acc = 0;
+      DD acc{0.0, 0.0};
       uint64_t n = 0;
       for (uint32_t i = s + lane; i < e; i += 64) {
-        acc += AsF(v[i]);
+        acc = DDAddD(acc, AsF(v[i]));
         n += sz[i];
       }
-      r = FBits(WaveSumF64(acc));
+      acc = WaveSumDD(acc);
+      r = FBits(acc.hi);
       n = WaveSumU64(n);
-      if (lane == 0) partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
+      if (lane == 0) {
+        partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
+        partial[static_cast<uint64_t>(2 * plan->n_udas + u) * pstride + w] = FBits(acc.lo);
+      }
     } else if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
       if (at == PXG_FLOAT64 || kind == PXG_UDA_MEAN) {
         // Four loads in flight per lane (a dependent one-load loop left the pass latency-bound:
         // ~3 TB/s over the 1B-row staging), four partial sums added in a fixed order.
         const bool f64 = at == PXG_FLOAT64;
         auto dv = [f64](uint64_t x) { return f64 ? AsF(x) : static_cast<double>(static_cast<int64_t>(x)); };
-        double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        DD a0{0.0, 0.0}, a1{0.0, 0.0};
         uint32_t i = s + lane;
         for (; i + 192 < e; i += 256) {
           const uint64_t x0 = v[i], x1 = v[i + 64], x2 = v[i + 128], x3 = v[i + 192];
-          a0 += dv(x0);
-          a1 += dv(x1);
-          a2 += dv(x2);
-          a3 += dv(x3);
+          a0 = DDAdd(a0, TwoSum(dv(x0), dv(x1)));
+          a1 = DDAdd(a1, TwoSum(dv(x2), dv(x3)));
         }
-        for (; i < e; i += 64) a0 += dv(v[i]);
-        r = FBits(WaveSumF64((a0 + a1) + (a2 + a3)));
+        for (; i < e; i += 64) a0 = DDAddD(a0, dv(v[i]));
+        const DD t = WaveSumDD(DDAdd(a0, a1));
+        r = FBits(t.hi);
+        if (lane == 0) partial[static_cast<uint64_t>(2 * plan->n_udas + u) * pstride + w] = FBits(t.lo);
       } else {
         uint64_t acc = 0;
         for (uint32_t i = s + lane; i < e; i += 64) acc += v[i];
@@ -148,23 +184,22 @@ __global__ void __launch_bounds__(256) ChunkReduceThreadKernel(const AggPlanDev*
     uint64_t r = 0;
     if (kind == PXG_UDA_MEAN_MERGE) {
       const uint64_t* sz = vals.p[plan->uda_val2[u]];
-      double acc = 0;
+      DD acc{0.0, 0.0};
       uint64_t n = 0;
       for (uint32_t i = s; i < e; ++i) {
-        acc += AsF(v[i]);
+        acc = DDAddD(acc, AsF(v[i]));
         n += sz[i];
       }
-      r = FBits(acc);
+      r = FBits(acc.hi);
       partial[static_cast<uint64_t>(plan->n_udas + u) * pstride + w] = n;
+      partial[static_cast<uint64_t>(2 * plan->n_udas + u) * pstride + w] = FBits(acc.lo);
     } else if (kind == PXG_UDA_SUM || kind == PXG_UDA_MINSUM || kind == PXG_UDA_MEAN) {
-      if (at == PXG_FLOAT64) {
-        double acc = 0;
-        for (uint32_t i = s; i < e; ++i) acc += AsF(v[i]);
-        r = FBits(acc);
-      } else if (kind == PXG_UDA_MEAN) {
-        double acc = 0;
-        for (uint32_t i = s; i < e; ++i) acc += static_cast<double>(static_cast<int64_t>(v[i]));
-        r = FBits(acc);
+      if (at == PXG_FLOAT64 || kind == PXG_UDA_MEAN) {
+        const bool f64 = at == PXG_FLOAT64;
+        DD acc{0.0, 0.0};
+        for (uint32_t i = s; i < e; ++i) acc = DDAddD(acc, f64 ? AsF(v[i]) : static_cast<double>(static_cast<int64_t>(v[i])));
+        r = FBits(acc.hi);
+        partial[static_cast<uint64_t>(2 * plan->n_udas + u) * pstride + w] = FBits(acc.lo);
       } else {
         uint64_t acc = 0;
         for (uint32_t i = s; i < e; ++i) acc += v[i];
@@ -218,16 +253,17 @@ __device__ __forceinline__ void CombineGroup(const AggPlanDev* __restrict__ plan
     const int kind = plan->uda_kind[u];
     const int at = plan->uda_arg_type[u];
     const uint64_t* p = partial + static_cast<uint64_t>(u) * pstride;
+    const uint64_t* plo = partial + static_cast<uint64_t>(2 * plan->n_udas + u) * pstride;  // sums' low words
     uint64_t r = 0;
     switch (kind) {
       case PXG_UDA_COUNT: r = cnt; break;
       case PXG_UDA_SUM:
       case PXG_UDA_MINSUM:
         if (at == PXG_FLOAT64) {
-          double acc = 0;
-          for (uint32_t c = cs; c < c1; c += step) acc += AsF(p[c]);
-          if (WAVE) acc = WaveSumF64(acc);
-          r = FBits(acc);
+          DD acc{0.0, 0.0};
+          for (uint32_t c = cs; c < c1; c += step) acc = DDAdd(acc, DD{AsF(p[c]), AsF(plo[c])});
+          if (WAVE) acc = WaveSumDD(acc);
+          r = FBits(DDValue(acc));
         } else {
           uint64_t acc = 0;
           for (uint32_t c = cs; c < c1; c += step) acc += p[c];
@@ -236,9 +272,10 @@ __device__ __forceinline__ void CombineGroup(const AggPlanDev* __restrict__ plan
         }
         break;
       case PXG_UDA_MEAN: {
-        double acc = 0;
-        for (uint32_t c = cs; c < c1; c += step) acc += AsF(p[c]);
-        if (WAVE) acc = WaveSumF64(acc);
+        DD dd{0.0, 0.0};
+        for (uint32_t c = cs; c < c1; c += step) dd = DDAdd(dd, DD{AsF(p[c]), AsF(plo[c])});
+        if (WAVE) dd = WaveSumDD(dd);
+        const double acc = DDValue(dd);
         r = FBits(acc / static_cast<double>(cnt));
         if (states && writer) {  // MeanInfo {uint64 size; double count} (math_ops.h:621-624)
           uint64_t* st = reinterpret_cast<uint64_t*>(states + static_cast<uint64_t>(g) * plan->state_rec + plan->state_off[u]);
@@ -249,17 +286,17 @@ __device__ __forceinline__ void CombineGroup(const AggPlanDev* __restrict__ plan
       }
       case PXG_UDA_MEAN_MERGE: {
         const uint64_t* pn = partial + static_cast<uint64_t>(plan->n_udas + u) * pstride;
-        double acc = 0;
+        DD dd{0.0, 0.0};
         uint64_t n = 0;
         for (uint32_t c = cs; c < c1; c += step) {
-          acc += AsF(p[c]);
+          dd = DDAdd(dd, DD{AsF(p[c]), AsF(plo[c])});
           n += pn[c];
         }
         if (WAVE) {
-          acc = WaveSumF64(acc);
+          dd = WaveSumDD(dd);
           n = WaveSumU64(n);
         }
-        r = FBits(acc / static_cast<double>(n));
+        r = FBits(DDValue(dd) / static_cast<double>(n));
         break;
       }
       case PXG_UDA_MAX: {
@@ -1482,7 +1519,7 @@ int32_t AggFinalizeTable(Agg* a) {
                                ngroups, cbase));
     PXG_RETURN_IF_ERROR(ScanExclusiveU32(ctx, cbase, cbase, ngroups, cbase + ngroups, scan_tmp));
     clk.Mark("finalize: red chunk scan");
-    PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * 2 * 8));
+    PXG_RETURN_IF_ERROR(ws.partial.Ensure(max_chunks * a->n_udas * kPartialRows * 8));
     PXG_RETURN_IF_ERROR(ws.cgroup.Ensure(max_chunks * 4 + 16));
     clk.Mark("finalize: red ensure");
     PXG_RETURN_IF_ERROR(Launch(ctx, "chunk_group", ChunkGroupKernel, dim3(static_cast<unsigned>((max_chunks + 255) / 256)), dim3(256), 0,
