@@ -45,34 +45,6 @@ __global__ void ChunkGroupKernel(const uint32_t* __restrict__ cbase, uint32_t ng
   cgroup[c] = lo;
 }
 
-// Floating-point sums in double-double (an error-free TwoSum per addition, the error words
-// summed beside): a group's sum is then its exact sum to ~2^-100 relative, rounded once at the
-// end, so it no longer depends on the order its values were staged in (that order is the
-// consume's tile completion order, which differs run to run; plain double sums differed in the
-// last bits).  The reference sums sequentially in double; both agree to its rounding.
-// Compiled with -ffp-contract=off (the transformations need unfused operations).
-struct DD {
-  double hi, lo;
-};
-__device__ __forceinline__ DD TwoSum(double a, double b) {
-  const double s = a + b;
-  const double bb = s - a;
-  return DD{s, (a - (s - bb)) + (b - bb)};
-}
-__device__ __forceinline__ DD DDAdd(DD x, DD y) {
-  const DD s = TwoSum(x.hi, y.hi);
-  const double e = s.lo + (x.lo + y.lo);
-  const double h = s.hi + e;
-  return DD{h, e - (h - s.hi)};
-}
-__device__ __forceinline__ DD DDAddD(DD x, double b) { return DDAdd(x, DD{b, 0.0}); }
-__device__ __forceinline__ DD WaveSumDD(DD v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = DDAdd(v, DD{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)});
-  return v;
-}
-// The rounded sum (non-finite: the plain sum's inf / NaN, whose error words are meaningless).
-__device__ __forceinline__ double DDValue(DD v) { return isfinite(v.hi) ? v.hi + v.lo : v.hi; }
 // Partial rows per UDA: [u] the sum's high words (or the integer / extreme state), [n_udas + u]
 // MEAN_MERGE sizes, [2 n_udas + u] the sum's low words.
 constexpr int kPartialRows = 3;

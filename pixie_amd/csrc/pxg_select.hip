@@ -502,9 +502,9 @@ __global__ void __launch_bounds__(256) BigPlanKernel(const BigGroup* __restrict_
 }
 
 // Gather the values of the tagged bins into the group's candidate region (any order: the bins
-// are sorted next) and sum the values inside each large range per chunk.  Sums are
-// deterministic: wave w takes chunk positions [1024 w, 1024 (w + 1)) in 16 rounds, each
-// round's values of one range are summed by a fixed shuffle tree, rounds and waves in order.
+// are sorted next) and sum the values inside each large range per chunk, in double-double
+// (pxg_quant.h DD): the group's range sums are then exact to ~2^-100 and rounded once in
+// BigSelDigest, so they do not depend on the staging order of the group's values.
 // A workgroup takes cpb consecutive chunks (as BigHistKernel); splitters and tags are reloaded
 // only when the group changes.  Gather slots are taken in two steps: LDS counters per gathered
 // bin, then one device atomic per bin and chunk reserves the bin's range — a device atomic per
@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
   if (c0 >= nchunks) return;
   const uint32_t c1 = min(nchunks, c0 + cpb);
   __shared__ uint8_t tg[kSelBins];
-  __shared__ double acc[4][kSelMaxRanges];
+  __shared__ double acc[4][kSelMaxRanges], acc_lo[4][kSelMaxRanges];
   __shared__ uint8_t cix[kSelBins];              // gathered bin -> its index in P.coll
   __shared__ uint16_t s_coll[kSelMaxColl];
   __shared__ uint32_t lcnt[kSelMaxColl], lbase[kSelMaxColl];
@@ -553,7 +553,10 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
           cix[b] = static_cast<uint8_t>(k);
         }
       }
-      if (t < 4 * kSelMaxRanges) (&acc[0][0])[t] = 0.0;
+      if (t < 4 * kSelMaxRanges) {
+        (&acc[0][0])[t] = 0.0;
+        (&acc_lo[0][0])[t] = 0.0;
+      }
       __syncthreads();
       const uint32_t* cb = cbase_all + static_cast<uint64_t>(cur) * kSelBins;
       uint32_t* cc = cursor_all + static_cast<uint64_t>(cur) * kSelBins;
@@ -581,8 +584,12 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
         while (pend) {
           const int uu = __builtin_amdgcn_readlane(u, __ffsll(static_cast<long long>(pend)) - 1);
           const bool mine = u == uu;
-          const double sm = WaveSumF64(mine ? v : 0.0);
-          if (lane == 0) acc[wid][uu] += sm;
+          const DD sm = WaveSumDD(DD{mine ? v : 0.0, 0.0});
+          if (lane == 0) {
+            const DD x = DDAdd(DD{acc[wid][uu], acc_lo[wid][uu]}, sm);
+            acc[wid][uu] = x.hi;
+            acc_lo[wid][uu] = x.lo;
+          }
           pend &= ~__ballot(mine);
         }
       }
@@ -595,8 +602,12 @@ __global__ void __launch_bounds__(256) BigCollectKernel(const BigChunk* __restri
           lcnt[k] = 0;
         }
       }
-      for (int u = t; u < n_ranges; u += 256)
-        partial[static_cast<uint64_t>(ci) * kSelMaxRanges + u] = acc[0][u] + acc[1][u] + acc[2][u] + acc[3][u];
+      for (int u = t; u < n_ranges; u += 256) {  // per range and chunk: high word, then low word
+        DD x{acc[0][u], acc_lo[0][u]};
+        for (int w = 1; w < 4; ++w) x = DDAdd(x, DD{acc[w][u], acc_lo[w][u]});
+        partial[(static_cast<uint64_t>(ci) * kSelMaxRanges + u) * 2] = x.hi;
+        partial[(static_cast<uint64_t>(ci) * kSelMaxRanges + u) * 2 + 1] = x.lo;
+      }
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < kRounds; ++r)
@@ -686,7 +697,7 @@ __global__ void __launch_bounds__(256) BigSelDigestKernel(const BigGroup* __rest
   if (plans[bi].fallback) return;
   __shared__ BigPlan P;
   __shared__ double mean_u[kSelMaxRanges];
-  __shared__ double red[4];
+  __shared__ double red[4], red_lo[4];
   __shared__ uint32_t s_starts[kChainCap];  // the chain, staged for the quantile searches
   const int t = threadIdx.x;
   {
@@ -720,16 +731,26 @@ __global__ void __launch_bounds__(256) BigSelDigestKernel(const BigGroup* __rest
     const uint32_t s = P.rs[u], e = P.re[u];
     if (e - s <= static_cast<uint32_t>(kSeqMean)) continue;
     const uint32_t b0 = P.rbs[u], b1 = P.rbe[u];
-    double acc = 0;
+    DD acc{0.0, 0.0};  // the range's end bins (sorted candidates) and its chunks' inside sums
     const uint32_t e0 = min(e, bs[b0 + 1]);
-    for (uint32_t r = s + t; r < e0; r += 256) acc += QVal(cg[cb[b0] + (r - bs[b0])]);
+    for (uint32_t r = s + t; r < e0; r += 256) acc = DDAddD(acc, QVal(cg[cb[b0] + (r - bs[b0])]));
     if (b1 != b0)
-      for (uint32_t r = bs[b1] + t; r < e; r += 256) acc += QVal(cg[cb[b1] + (r - bs[b1])]);
-    for (uint32_t k = t; k < G.nch; k += 256) acc += partial[static_cast<uint64_t>(G.c0 + k) * kSelMaxRanges + u];
-    acc = WaveSumF64(acc);
-    if ((t & 63) == 0) red[t >> 6] = acc;
+      for (uint32_t r = bs[b1] + t; r < e; r += 256) acc = DDAddD(acc, QVal(cg[cb[b1] + (r - bs[b1])]));
+    for (uint32_t k = t; k < G.nch; k += 256) {
+      const uint64_t pi = (static_cast<uint64_t>(G.c0 + k) * kSelMaxRanges + u) * 2;
+      acc = DDAdd(acc, DD{partial[pi], partial[pi + 1]});
+    }
+    acc = WaveSumDD(acc);
+    if ((t & 63) == 0) {
+      red[t >> 6] = acc.hi;
+      red_lo[t >> 6] = acc.lo;
+    }
     __syncthreads();
-    if (t == 0) mean_u[u] = (red[0] + red[1] + red[2] + red[3]) / static_cast<double>(e - s);
+    if (t == 0) {
+      DD x{red[0], red_lo[0]};
+      for (int w = 1; w < 4; ++w) x = DDAdd(x, DD{red[w], red_lo[w]});
+      mean_u[u] = DDValue(x) / static_cast<double>(e - s);
+    }
     __syncthreads();
   }
   __syncthreads();
@@ -764,7 +785,7 @@ int32_t SelEnsure(const BigSet& S, uint64_t n, DevBuf& keysA, DevBuf& sel_bin) {
   PXG_RETURN_IF_ERROR(S.tag->Ensure(nb * kSelBins + 16));
   PXG_RETURN_IF_ERROR(S.cbase->Ensure(nb * kSelBins * 4 + 16));
   PXG_RETURN_IF_ERROR(S.plan->Ensure(nb * sizeof(BigPlan) + 16));
-  PXG_RETURN_IF_ERROR(S.partial->Ensure(static_cast<size_t>(S.n_chunks) * kSelMaxRanges * 8 + 16));
+  PXG_RETURN_IF_ERROR(S.partial->Ensure(static_cast<size_t>(S.n_chunks) * kSelMaxRanges * 16 + 16));  // (high, low) words
   return sel_bin.Ensure(n * 2 + 16);  // per staged value its bin (BigHist -> BigCollect; sets are disjoint)
 }
 

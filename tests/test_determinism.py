@@ -3,7 +3,9 @@ pxg_finalize.hip ChunkReduce / GroupCombine: double-double sums).  The staging o
 group's values is the consume's tile completion order, which differs between runs; plain double
 sums then differed in the last bits (the reference, one sequential loop, is deterministic).
 With the sums carried in double-double and rounded once, count, sum and mean are bit-identical
-across runs, and agree with an exact (math.fsum) restatement to the last bit."""
+across runs, and agree with an exact (math.fsum) restatement to the last bit.  The big groups'
+selection path sums the values inside its centroid ranges the same way, so their quantiles are
+bit-identical across runs as well."""
 import math
 
 import numpy as np
@@ -16,13 +18,15 @@ from pixie_amd.pipeline import LinearQuery
 pytestmark = pytest.mark.gpu
 
 
-def _rows(res, nk):
+def _rows(res, nk, widths):
     keys = [c.to_list() for c in res[:nk]]
-    vals = [np.asarray(c.values) for c in res[nk:]]
+    vals = [np.asarray(c.values).reshape(-1, w) for c, w in zip(res[nk:], widths)]
     return {tuple(k[g] for k in keys): tuple(v[g].tobytes() for v in vals) for g in range(len(keys[0]))}
 
 
-def test_c2_means_are_bit_identical_across_runs(ctx):
+def test_c2_results_are_bit_identical_across_runs(ctx):
+    """count, mean and all 7 quantiles of every group, big groups (selection path: its inside-bin
+    centroid sums are double-double too) included."""
     t = Table(ctx, P.HTTP_TYPES)
     t.append_http_events(20250117, 0, 20_000_000, 10_000_000)
     q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
@@ -33,7 +37,7 @@ def test_c2_means_are_bit_identical_across_runs(ctx):
         a.consume(t)
         a.finalize()
         r = a.result()
-        runs.append(_rows(r[:4], 2))  # keys, count, mean (the quantiles column aside)
+        runs.append(_rows(r, 2, [1, 1, 7]))  # keys; count, mean, quantiles
     assert len(runs[0]) > 20_000
     assert runs[0] == runs[1] == runs[2]
     a.close()
