@@ -504,3 +504,22 @@ def test_engine_device_pluck_nan_quantiles_and_unplucked_keys(engine):
         for a, b in zip(r[2:], d[2:]):
             assert a == b or ulp_diff(a, b) <= 4, (r, d)
     assert all(d[4] == 0.0 for d in dev)  # "p42" is not a key of the JSON
+
+
+@pytest.mark.gpu
+def test_join_output_past_one_chunk_takes_the_host_path(engine):
+    """A join output of more than 2^24 rows spans two device chunks: the result image refuses
+    it (PXG_UNIMPLEMENTED) and the join fetches the columns instead; the batches are intact."""
+    import numpy as np
+    n = (1 << 24) + 1000
+    probe = {"types": [2, 2], "batches": [[Column(2, values=np.ones(n, dtype=np.int64)), Column(2, values=np.arange(n, dtype=np.int64))]]}
+    build = {"types": [2, 2], "batches": [[Column.from_values(2, [1]), Column.from_values(2, [7])]]}
+    plan = P.dag_plan([(1, P.source_op("l", [2, 2], ["k", "v"], [0, 1]), []),
+                       (2, P.source_op("r", [2, 2], ["k", "w"], [0, 1]), []),
+                       (3, P.join_op(P.JOIN_INNER, [(0, 0)], [(0, 1), (1, 1)], names=["time_", "w"], rows_per_batch=1 << 20), [1, 2]),
+                       (4, P.sink_op("out"), [3])])
+    out = engine.execute(plan, {"l": probe, "r": build})["out"]
+    assert sum(b["rows"] for b in out) == n
+    assert out[-1]["eos"] and not out[0]["eos"]
+    v = np.concatenate([np.asarray(b["cols"][0].values) for b in out])
+    assert np.array_equal(v, np.arange(n)) and set(np.asarray(out[0]["cols"][1].values).tolist()) == {7}
