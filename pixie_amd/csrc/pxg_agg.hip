@@ -24,6 +24,9 @@ constexpr int kGenericTile = 4096;   // rows per workgroup tile of the generic k
 constexpr int kConsumeTile = 16384;
 constexpr int kConsumeTileMax = 32768;
 constexpr int kSelCap = 16384;       // selected rows collected before phase 2 runs (LDS)
+// (The fast kernel runs 4 waves per SIMD, limited by both LDS (34.9 KB per workgroup) and
+// VGPRs (~125).  Forcing 5 -- a 12288-row selection buffer and amdgpu_waves_per_eu(5) --
+// spilled 32-93 VGPRs to scratch: C2 consume 1.30 -> 2.09 ms.)
 constexpr int kSubRows = 8192;       // rows per phase-1 sub-batch (32 per thread in flight)
 
 struct TileRange {
