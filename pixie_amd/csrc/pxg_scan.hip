@@ -48,31 +48,49 @@ __global__ void __launch_bounds__(kScanBlock) ScanReduceKernel(const T* __restri
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-// Scan a tile: each thread owns kScanItems consecutive items (strided load through LDS-free
-// sequential per-thread ranges keeps order simple).
+// Scan a tile: each thread owns kScanItems consecutive items. The tile goes through LDS so that
+// the global loads and stores stay coalesced (a wave touches 64 consecutive elements per
+// instruction, not 64 elements kScanItems apart); row j of the tile sits at j + j / kScanItems,
+// which keeps a thread's consecutive items off each other's banks. In-place (in == out) is fine:
+// a block reads its whole tile before it writes any of it.
 template <typename T>
 __global__ void __launch_bounds__(kScanBlock) ScanDownsweepKernel(const T* __restrict__ in, T* __restrict__ out, int64_t n,
                                                                   const T* __restrict__ block_base, T* __restrict__ total) {
+  constexpr int kPad = kScanItems + 1;
   __shared__ T lds[kScanBlock / 64];
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile + static_cast<int64_t>(threadIdx.x) * kScanItems;
+  __shared__ T tile[kScanBlock * kPad];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * kScanBlock + t;
+    const int64_t i = base + j;
+    tile[j + j / kScanItems] = i < n ? in[i] : T(0);
+  }
+  __syncthreads();
   T vals[kScanItems];
   T acc = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    int64_t i = base + k;
-    vals[k] = i < n ? in[i] : T(0);
+    vals[k] = tile[t * kPad + k];
     acc += vals[k];
   }
   T tot;
-  T prefix = BlockExclusiveScan(acc, lds, &tot);
+  T prefix = BlockExclusiveScan(acc, lds, &tot);  // its barriers also order the tile reads above
   T run = prefix + (block_base ? block_base[blockIdx.x] : T(0));
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    int64_t i = base + k;
-    if (i < n) out[i] = run;
+    tile[t * kPad + k] = run;
     run += vals[k];
   }
-  if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) *total = run;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * kScanBlock + t;
+    const int64_t i = base + j;
+    if (i < n) out[i] = tile[j + j / kScanItems];
+  }
+  if (total && blockIdx.x == gridDim.x - 1 && t == kScanBlock - 1) *total = run;
 }
 
 size_t ScanScratchBytes(int64_t n) {
