@@ -907,11 +907,19 @@ __global__ void RecordsFromArenaKernel(const AggPlanDev* __restrict__ plan, cons
   WriteProbeRecord(plan, k, w, prec + static_cast<uint64_t>(i) * kRecWords);
 }
 
+// total != null: the speculative launch (issued before the host has read the scanned total).
+// It writes nothing unless the new records fit the arena as reserved (arena_bytes, with the
+// slack) and keep 32-bit offsets; every thread reads the same total, so the whole grid agrees.
 __global__ void AggPublishWriteKernel(const AggPlanDev* __restrict__ plan, const DevChunk* __restrict__ chunks,
                                       unsigned long long* __restrict__ slots, uint32_t cap, const uint64_t* __restrict__ offs,
-                                      uint64_t base, uint64_t* __restrict__ arena, uint64_t* __restrict__ prec) {
+                                      uint64_t base, uint64_t* __restrict__ arena, uint64_t* __restrict__ prec,
+                                      const uint64_t* __restrict__ total, uint64_t arena_bytes) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
+  if (total) {
+    const uint64_t words = *total & ((uint64_t(1) << kPublishCountShift) - 1);
+    if ((base + words) * 8 + kArenaSlack > arena_bytes || base + words >= (uint64_t(1) << 32)) return;
+  }
   const unsigned long long w = slots[i];
   if (w == 0 || (w & kKindArena)) return;
   const uint32_t ref = static_cast<uint32_t>(w);
@@ -1103,7 +1111,22 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   PXG_HIP(hipMemcpyAsync(pin, total, 8, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipMemcpyAsync(pin + 8, counters.p, 56, hipMemcpyDeviceToHost, ctx->stream));
   if (hc_active) PXG_HIP(hipMemcpyAsync(pin + 64, hc_maxlen.p, sizeof(hc_maxlen_h), hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipStreamSynchronize(ctx->stream));
+  uint64_t* rec_p = rec_ok && rec_cap == cap ? prec.as<uint64_t>() : nullptr;
+  // With an arena already reserved, the write goes out before the read-back is waited on, and
+  // the host waits only for the read-back: the write runs during the host's round trip (the C2
+  // trace had the stream idle ~33 us here). It skips itself when the records do not fit; the host
+  // then reserves and launches it again below.
+  const uint64_t spec_bytes = arena.p ? arena.bytes : 0;
+  if (spec_bytes) {
+    PXG_HIP(hipEventRecord(ctx->ev_pub, ctx->stream));
+    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                               d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
+                               static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>(), rec_p,
+                               static_cast<const uint64_t*>(total), spec_bytes));
+    PXG_HIP(hipEventSynchronize(ctx->ev_pub));
+  } else {
+    PXG_HIP(hipStreamSynchronize(ctx->stream));
+  }
   uint8_t c[56];
   uint64_t tot = 0;
   std::memcpy(&tot, pin, 8);
@@ -1118,14 +1141,18 @@ int32_t Agg::PublishNew(Table* t, uint32_t* n_deferred) {
   uint32_t dev_groups = 0;  // exact: every successful insert CAS is counted (per-tile flushes)
   std::memcpy(&dev_groups, c, 4);
   if (n_new > 0) {
-    // Slot words hold 32-bit arena offsets: refuse before any record is written.
+    // Slot words hold 32-bit arena offsets: refuse before any record is written (the
+    // speculative launch checks the same bound on the device).
     if (arena_words + words >= (uint64_t(1) << 32)) return SetError(PXG_RESOURCE_UNAVAILABLE, "key arena exceeds 32 GiB");
-    PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + kArenaSlack, arena_words * 8, ctx->stream));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
-                               d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
-                               static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>(),
-                               rec_ok && rec_cap == cap ? prec.as<uint64_t>() : nullptr));
-    if (rec_ok && rec_cap == cap) rec_dirty = true;
+    const bool written = spec_bytes && (arena_words + words) * 8 + kArenaSlack <= spec_bytes;
+    if (!written) {
+      PXG_RETURN_IF_ERROR(arena.Reserve((arena_words + words) * 8 + kArenaSlack, arena_words * 8, ctx->stream));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "agg_publish_write", AggPublishWriteKernel, dim3(GridFor(cap, 256, 1 << 30)), dim3(256), 0,
+                                 d_plan.as<const AggPlanDev>(), chunks, slots.as<unsigned long long>(), cap,
+                                 static_cast<const uint64_t*>(sizes), arena_words, arena.as<uint64_t>(), rec_p,
+                                 static_cast<const uint64_t*>(nullptr), uint64_t(0)));
+    }
+    if (rec_p) rec_dirty = true;
     arena_words += words;
   }
   // The device insert counter is exact (every successful insert CAS is counted).

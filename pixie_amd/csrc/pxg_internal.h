@@ -150,6 +150,7 @@ struct Ctx {
   hipEvent_t ev_chain = nullptr; // finalize: the digest boundary chains are done (side stream)
   hipEvent_t ev_split = nullptr; // finalize: the staging split's bucket totals have landed (pinned)
   hipEvent_t ev_early = nullptr; // finalize: the fused split's designated groups are final (main stream)
+  hipEvent_t ev_pub = nullptr;   // consume: the publish read-back is on the host (main stream)
   bool profiling = false;
   std::string profile_only;  // non-empty: only launches of this kernel name are timed
   std::map<std::string, KernelStat> stats;

@@ -339,7 +339,8 @@ extern "C" int32_t pxg_ctx_create(int32_t device, pxg_ctx** out) {
       hipEventCreateWithFlags(&c->impl.ev_meta, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_chain, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->impl.ev_split, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->impl.ev_early, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->impl.ev_early, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->impl.ev_pub, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SetError(PXG_INTERNAL, "side stream / event creation failed");
   }
@@ -371,6 +372,7 @@ extern "C" int32_t pxg_ctx_destroy(pxg_ctx* ctx) {
   hipEventDestroy(ctx->impl.ev_chain);
   hipEventDestroy(ctx->impl.ev_split);
   hipEventDestroy(ctx->impl.ev_early);
+  hipEventDestroy(ctx->impl.ev_pub);
   hipStreamDestroy(ctx->impl.side2);
   hipStreamDestroy(ctx->impl.stream);
   delete ctx;
