@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--backend", default="nccl",
                     help="N>1 data path: nccl = libpxg's RCCL communicator over xGMI (pxg_agg_alltoall); "
                          "gloo = torch.distributed all_to_all on the host (CPU rehearsal). The control plane is gloo.")
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="N>1 launcher: wall-clock limit in seconds after which every rank still running is killed and the "
+                         "launcher exits non-zero (0 = none)")
     ap.add_argument("--share-gpu0", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; pair it with --backend gloo, since RCCL "
                          "refuses two ranks on one GPU)")
@@ -429,28 +432,52 @@ def launch_ranks(args):
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
     print(f"[bench] starting {n} ranks (one process per GPU, rendezvous 127.0.0.1:{port})", file=sys.stderr, flush=True)
     procs = []
+
+    def stop_all(sig=signal.SIGTERM):
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    os.killpg(q.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    # A Ctrl-C / kill of the launcher takes the ranks (each in its own session) with it.
+    def on_signal(signum, _frame):
+        print(f"[bench] launcher got signal {signum}: stopping the ranks", file=sys.stderr, flush=True)
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old_handlers = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGINT, signal.SIGTERM)}
     for r in range(n):
         env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
     codes = [None] * n
     failed = False
-    while any(c is None for c in codes):
-        for r, p in enumerate(procs):
-            if codes[r] is None:
-                c = p.poll()
-                if c is not None:
-                    codes[r] = c
-                    if c != 0 and not failed:
-                        failed = True
-                        print(f"[bench] rank {r} exited {c}: stopping the other ranks", file=sys.stderr, flush=True)
-                        for q in procs:
-                            if q.poll() is None:
-                                try:
-                                    os.killpg(q.pid, signal.SIGTERM)
-                                except ProcessLookupError:
-                                    pass
-        time.sleep(0.05)
+    deadline = time.time() + args.rank_timeout if args.rank_timeout > 0 else None
+    try:
+        while any(c is None for c in codes):
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    c = p.poll()
+                    if c is not None:
+                        codes[r] = c
+                        if c != 0 and not failed:
+                            failed = True
+                            print(f"[bench] rank {r} exited {c}: stopping the other ranks", file=sys.stderr, flush=True)
+                            stop_all()
+            if deadline is not None and time.time() > deadline and any(c is None for c in codes):
+                print(f"[bench] ranks still running after --rank-timeout {args.rank_timeout}s: killing them", file=sys.stderr, flush=True)
+                stop_all(signal.SIGKILL)
+                for r, p in enumerate(procs):
+                    if codes[r] is None:
+                        p.wait()
+                        codes[r] = 124
+                break
+            time.sleep(0.05)
+    finally:
+        for sg, h in old_handlers.items():
+            signal.signal(sg, h)
     return max((c if c > 0 else 1 if c != 0 else 0) for c in codes)
 
 
@@ -491,10 +518,16 @@ class DeviceRank:
 
     def step(self):
         """reset -> consume -> exchange partial states by key hash -> finalize -> gather the
-        final rows on rank 0.  Returns the gathered groups on rank 0 (0 elsewhere)."""
+        final rows on rank 0.  Returns the gathered groups on rank 0 (0 elsewhere).  Both
+        backends run libpxg's exchange (pxg_agg_alltoall: device part layout, {bytes, header}
+        records, import) and pxg_agg_gather (device rebase of the STRING offsets); backend gloo
+        moves the bytes through a host communicator (pxg_comm_init_host over torch gloo) instead
+        of RCCL."""
         a = self.agg
         a.reset()
         a.consume(self.table)
+        # rows this rank selected (read before the exchange: the import resets the staging)
+        self.selected_rows = a.rows_selected()
         if self.comm is not None:
             s, r = a.alltoall(self.comm)
             a.finalize()
@@ -502,13 +535,13 @@ class DeviceRank:
             self.exch.update(via="pxg_agg_alltoall (RCCL grouped send/recv on the ctx stream)",
                              gather="pxg_agg_gather (RCCL send/recv of the result columns to rank 0)")
         else:
-            from pixie_amd.dist import exchange_partials, gather_results
+            from pixie_amd.dist import exchange_partials, gather_device_results
             s, r = exchange_partials(a)
             a.finalize()
-            self.parts = gather_results(a.result())
-            g = sum(len(p[0]) for p in self.parts) if self.parts else 0
-            self.exch.update(via=f"torch.distributed all_to_all_single ({self.backend})",
-                             gather="torch.distributed gather_object of the host result columns")
+            g = gather_device_results(a)
+            self.exch.update(via=f"pxg_agg_alltoall over a host communicator (pxg_comm_init_host; bytes over torch.distributed "
+                                 f"{self.backend}, same device export / import code as RCCL)",
+                             gather="pxg_agg_gather over the host communicator (device rebase of the STRING offsets)")
         self.exch["bytes_sent"], self.exch["bytes_recv"] = s, r
         return g
 
@@ -528,19 +561,18 @@ class DeviceRank:
         return consume_stats(self.ctx)
 
     def selected(self):
-        return self.agg.rows_selected()
+        return self.selected_rows
 
     def result(self):
         """Rank 0: the whole gathered result (service, req_path, count, mean, quantiles)."""
-        if self.comm is not None:
-            return self.agg.result()
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import parity
-        return parity.concat_columns(self.parts)
+        return self.agg.result()
 
     def close(self):
         if self.comm is not None:
             self.comm.close()
+        else:
+            from pixie_amd.dist import close_host_comms
+            close_host_comms()
         self.agg.close()
         self.table.close()
         self.ctx.close()
@@ -597,12 +629,20 @@ def multi_main(args, rank, world, local_rank):
         tt = torch.tensor([elapsed, cons_ms / args.steps], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, avg_launch_ms = float(tt[0]), float(tt[1])
+        sel = torch.tensor([runner.selected()], dtype=torch.int64)
+        dist.all_reduce(sel, op=dist.ReduceOp.SUM)
+        selected_total = int(sel[0])
         ms_per_step = elapsed * 1000.0 / args.steps
         total_rows = n * world
         value = total_rows * args.steps / elapsed
         alg_bytes = runner.alg_bytes
         achieved = alg_bytes / (avg_launch_ms / 1000.0) / 1e9 if launches and avg_launch_ms > 0 else None
         par = None
+        pmc = None
+        if rank == 0 and not args.standin and not args.no_pmc:
+            # rank 0's consume (its shard = rows [0, n), the same consume as the timed one) under
+            # two rocprofv3 --pmc passes in a child process; the other ranks wait at the barrier
+            pmc = pmc_leg(n)
         if rank == 0:
             sys.path.insert(0, os.path.join(REPO, "tests"))
             try:
@@ -627,6 +667,7 @@ def multi_main(args, rank, world, local_rank):
                                 "(service, req_path): count, mean, quantiles; partial states exchanged by hash(key) % N; "
                                 "finalize; final rows gathered on rank 0",
                     "rows_per_gpu": n, "total_rows": total_rows, "groups": ngroups, "selected_rows_per_gpu": runner.selected(),
+                    "selected_rows_all_ranks": selected_total,
                     "parallelism": f"dp{world} (row shards, partial UDA states exchanged by key hash, rows gathered on rank 0)",
                     "algorithmic_bytes_per_row": alg_bytes / n if n else None,
                     "kernel_ms_per_step_rank0": kernel_ms,
@@ -635,9 +676,12 @@ def multi_main(args, rank, world, local_rank):
                 },
                 "roofline": {
                     "bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                    "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                    "traffic_detail": pmc,
                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_launch_ms if launches else None,
-                    "per": "one rank's consume step (the slowest rank's event-timed consume)",
+                    "per": "one rank's consume step (the slowest rank's event-timed consume); traffic: rank 0's consume of "
+                           "its shard under rocprofv3 --pmc after the timed region",
                 },
                 "cpu_baseline": None,
                 "parity": par,

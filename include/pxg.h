@@ -370,6 +370,14 @@ int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes);
  * part_bytes[i] bytes: e.g. what one all-to-all received from every rank) in one pass. */
 int32_t pxg_agg_import_partials(pxg_agg* agg, const void* src, int32_t n_parts,
                                 const int64_t* part_offsets, const int64_t* part_bytes);
+/* The export pxg_agg_alltoall sends: the same parts, laid out on the device (sizes, headers and
+ * offsets computed by a device kernel, no host sizing pass) into a device buffer owned by the
+ * aggregation (valid until its next export or destroy).  *parts receives that buffer; the parts
+ * lie back to back, part i part_bytes[i] bytes (already 8-byte aligned); headers (optional,
+ * n_parts * 64 bytes) receives each part's header, the first 64 bytes of the part.  The bytes
+ * equal pxg_agg_export_partial's.  Exchange-v2 aggregations only (FAILED_PRECONDITION else). */
+int32_t pxg_agg_export_partial_dev(pxg_agg* agg, int32_t n_parts, void** parts, int64_t* part_bytes,
+                                   uint8_t* headers);
 
 /* ---------------------------------------------------------------------------------------
  * Intra-node exchange over RCCL / xGMI (the PEM-partial -> Kelvin-finalize hop,
@@ -382,9 +390,33 @@ int32_t pxg_comm_unique_id(uint8_t* id_out, int32_t id_bytes);
 /* Communicator of `nranks` ranks over ctx's device; collective (every rank calls it). */
 int32_t pxg_comm_init(pxg_ctx* ctx, int32_t rank, int32_t nranks, const uint8_t* id, int32_t id_bytes, pxg_comm** out);
 int32_t pxg_comm_destroy(pxg_comm* comm);
+/* A host transport behind the same communicator interface, for ranks that cannot open an RCCL
+ * communicator (several ranks sharing one GPU, CPU-hosted process groups such as gloo): the
+ * caller supplies only the byte mover.  pxg_agg_alltoall and pxg_agg_gather then run exactly the
+ * device code of the RCCL path (device part layout, {bytes, header} records, import with the
+ * received headers, gather rebase); the bytes travel through pinned host memory instead of xGMI.
+ *
+ * Each grouped exchange calls `fn` once with n_ops point-to-point transfers between host buffers:
+ * op.send != 0 sends op.bytes from op.buf to rank op.peer, else receives op.bytes from op.peer
+ * into op.buf.  The k-th op of a rank to a peer matches that peer's k-th op from the rank, as
+ * grouped ncclSend / ncclRecv pairs do.  Transfers of a rank to itself and zero-byte transfers
+ * are done inside libpxg and never passed.  fn returns 0 on success; anything else fails the
+ * call with PXG_INTERNAL (the peers then see their own transport fail or time out).  fn runs on
+ * the calling thread, inside the libpxg call. */
+typedef struct {
+  int32_t peer;
+  int32_t send;
+  void* buf;
+  int64_t bytes;
+} pxg_xfer;
+typedef int32_t (*pxg_xfer_fn)(void* user, int32_t n_ops, const pxg_xfer* ops);
+int32_t pxg_comm_init_host(pxg_ctx* ctx, int32_t rank, int32_t nranks, pxg_xfer_fn fn, void* user, pxg_comm** out);
 /* Re-partition agg's state across the ranks by hash(group key): export nranks parts, exchange
  * the byte counts and the parts (grouped ncclSend/ncclRecv on the ctx stream), reset agg and
  * import what arrived.  Afterwards every group lives on exactly one rank; finalize locally.
+ * A rank whose export fails (its finalize checks, or parts past the send buffer) announces -1
+ * bytes to every peer; then no rank moves parts and every rank returns an error, so no peer is
+ * left waiting inside the collective.
  * Collective.  bytes_sent / bytes_recv (optional) receive this rank's traffic. */
 int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes_sent, int64_t* bytes_recv);
 /* Gather every rank's finalized result rows on `root` (the final rows to one

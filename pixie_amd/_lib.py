@@ -86,11 +86,21 @@ EXPORTED = [
     "pxg_pxrb_copy", "pxg_pxrb_destroy", "pxg_filter", "pxg_filter_split", "pxg_map", "pxg_agg_create",
     "pxg_agg_destroy", "pxg_agg_consume", "pxg_agg_finalize", "pxg_agg_result", "pxg_agg_result_skip", "pxg_agg_result_device", "pxg_agg_finalize_result", "pxg_agg_quantile_lanes", "pxg_result_free", "pxg_host_alloc", "pxg_host_free",
     "pxg_agg_reset", "pxg_agg_rows_selected", "pxg_agg_info", "pxg_agg_export_partial", "pxg_agg_import_partial", "pxg_agg_import_partials",
+    "pxg_agg_export_partial_dev",
     "pxg_join", "pxg_datagen_http_events", "pxg_table_append_http_events", "pxg_digest_chains", "pxg_digest_merge",
-    "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_destroy", "pxg_agg_alltoall", "pxg_agg_gather",
+    "pxg_comm_unique_id", "pxg_comm_init", "pxg_comm_init_host", "pxg_comm_destroy", "pxg_agg_alltoall", "pxg_agg_gather",
 ]
 
 _lib = None
+
+
+class Xfer(C.Structure):
+    """pxg_xfer (include/pxg.h): one point-to-point transfer of a host-transport batch."""
+    _fields_ = [("peer", C.c_int32), ("send", C.c_int32), ("buf", C.c_void_p), ("bytes", C.c_int64)]
+
+
+# pxg_xfer_fn: int32_t (*)(void* user, int32_t n_ops, const pxg_xfer* ops)
+XferFn = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(Xfer))
 
 
 class PxgError(RuntimeError):
@@ -157,6 +167,7 @@ def load() -> C.CDLL:
         "pxg_agg_export_partial": (i32, [vp, i32, vp, i64, p(i64), p(i64)]),
         "pxg_agg_import_partial": (i32, [vp, vp, i64]),
         "pxg_agg_import_partials": (i32, [vp, vp, i32, p(i64), p(i64)]),
+        "pxg_agg_export_partial_dev": (i32, [vp, i32, p(vp), p(i64), vp]),
         "pxg_join": (i32, [vp, vp, p(JoinSpec), p(vp), p(i64)]),
         "pxg_table_time_bound": (i32, [vp, i32, i64, i32, p(i64)]),
         "pxg_table_pxrb_image": (i32, [vp, p(i64), i64, i32, i32, p(vp), p(i64)]),
@@ -168,6 +179,7 @@ def load() -> C.CDLL:
         "pxg_digest_merge": (i32, [vp, vp, vp, i64, i32, vp]),
         "pxg_comm_unique_id": (i32, [vp, i32]),
         "pxg_comm_init": (i32, [vp, i32, i32, vp, i32, p(vp)]),
+        "pxg_comm_init_host": (i32, [vp, i32, i32, XferFn, vp, p(vp)]),
         "pxg_comm_destroy": (i32, [vp]),
         "pxg_agg_alltoall": (i32, [vp, vp, p(i64), p(i64)]),
         "pxg_agg_gather": (i32, [vp, vp, i32, p(i64)]),

@@ -162,6 +162,7 @@ struct Agg {
     const unsigned long long* e_slots = nullptr;
     const uint32_t* e_gslot = nullptr;
     uint64_t hc_key_words = 0;
+    DevBuf dsend, dcnt;  // pxg_agg_export_partial_dev: the device-laid-out parts, their sizes and headers
   } xc;
 
   // Finalize workspace, kept across finalize calls (grow-only; no per-step allocation).

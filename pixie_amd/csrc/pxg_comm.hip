@@ -23,9 +23,17 @@ namespace pxg {
 
 struct Comm {
   ncclComm_t nccl = nullptr;
+  // Host transport (pxg_comm_init_host): the caller's byte mover, used instead of RCCL.
+  pxg_xfer_fn host_fn = nullptr;
+  void* host_user = nullptr;
   int32_t rank = 0, nranks = 1;
   Ctx* ctx = nullptr;
   DevBuf send, recv, counts;  // grow-only exchange buffers
+  void* hstage = nullptr;     // host transport: grow-only pinned staging of one grouped exchange
+  size_t hstage_bytes = 0;
+  ~Comm() {
+    if (hstage) (void)hipHostFree(hstage);
+  }
 };
 
 #define PXG_NCCL(expr)                                                                                    \
@@ -34,23 +42,101 @@ struct Comm {
     if (r_ != ncclSuccess) return SetError(PXG_INTERNAL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
   } while (0)
 
-// An RCCL group that is closed on every exit path: an ncclSend / ncclRecv that fails between
-// ncclGroupStart and ncclGroupEnd must not leave the group open for later calls on the
-// communicator.
-struct NcclGroup {
+// One grouped exchange of point-to-point byte transfers between device buffers, the unit both
+// transports share.  RCCL: ncclGroupStart, an ncclSend / ncclRecv per transfer on the ctx
+// stream, ncclGroupEnd -- closed on every exit path, so a failing call between start and end
+// never leaves the group open for later calls on the communicator.  Host transport: the
+// transfers are collected; End() waits for the stream (the send buffers are written by earlier
+// kernels), copies the send buffers to pinned staging, hands the batch to the caller's byte mover,
+// and copies what arrived to the receive buffers on the stream (stream-ordered before any later
+// kernel).  A rank's transfers to itself are device-to-device copies matched in issue order.
+struct XferGroup {
+  Comm& C;
   bool open = false;
+  struct Op {
+    int32_t peer;
+    bool send;
+    void* dev;
+    size_t bytes;
+  };
+  std::vector<Op> ops;
+  explicit XferGroup(Comm& c) : C(c) {}
   int32_t Start() {
-    PXG_NCCL(ncclGroupStart());
-    open = true;
+    if (C.nccl) {
+      PXG_NCCL(ncclGroupStart());
+      open = true;
+    }
+    return PXG_OK;
+  }
+  int32_t Send(const void* dev, size_t bytes, int32_t peer) {
+    if (C.nccl) PXG_NCCL(ncclSend(dev, bytes, ncclUint8, peer, C.nccl, C.ctx->stream));
+    else if (bytes > 0) ops.push_back(Op{peer, true, const_cast<void*>(dev), bytes});
+    return PXG_OK;
+  }
+  int32_t Recv(void* dev, size_t bytes, int32_t peer) {
+    if (C.nccl) PXG_NCCL(ncclRecv(dev, bytes, ncclUint8, peer, C.nccl, C.ctx->stream));
+    else if (bytes > 0) ops.push_back(Op{peer, false, dev, bytes});
     return PXG_OK;
   }
   int32_t End() {
-    open = false;
-    PXG_NCCL(ncclGroupEnd());
-    return PXG_OK;
+    if (C.nccl) {
+      open = false;
+      PXG_NCCL(ncclGroupEnd());
+      return PXG_OK;
+    }
+    return RunHost();
   }
-  ~NcclGroup() {
+  ~XferGroup() {
     if (open) (void)ncclGroupEnd();
+  }
+
+ private:
+  int32_t RunHost() {
+    hipStream_t s = C.ctx->stream;
+    // Self transfers: the k-th send to this rank lands in the k-th receive from it.
+    std::vector<const Op*> self_s, self_r;
+    size_t stage = 0;
+    for (const Op& o : ops) {
+      if (o.peer < 0 || o.peer >= C.nranks) return SetError(PXG_INVALID_ARGUMENT, "transfer to rank %d of %d", o.peer, C.nranks);
+      if (o.peer == C.rank) (o.send ? self_s : self_r).push_back(&o);
+      else stage += (o.bytes + 63) & ~size_t(63);
+    }
+    if (self_s.size() != self_r.size()) return SetError(PXG_INTERNAL, "unmatched transfers of a rank to itself");
+    for (size_t i = 0; i < self_s.size(); ++i) {
+      if (self_s[i]->bytes != self_r[i]->bytes)
+        return SetError(PXG_INTERNAL, "self transfer of %zu bytes into a %zu-byte receive", self_s[i]->bytes, self_r[i]->bytes);
+      PXG_HIP(hipMemcpyAsync(self_r[i]->dev, self_s[i]->dev, self_s[i]->bytes, hipMemcpyDeviceToDevice, s));
+    }
+    if (stage == 0) return PXG_OK;
+    if (stage > C.hstage_bytes) {
+      const size_t want = std::max(stage, C.hstage_bytes * 2);
+      if (C.hstage) PXG_HIP(hipHostFree(C.hstage));
+      C.hstage = nullptr;
+      C.hstage_bytes = 0;
+      PXG_HIP(hipHostMalloc(&C.hstage, want, hipHostMallocDefault));
+      C.hstage_bytes = want;
+    }
+    std::vector<pxg_xfer> x;
+    x.reserve(ops.size());
+    uint8_t* h = static_cast<uint8_t*>(C.hstage);
+    size_t at = 0;
+    for (const Op& o : ops) {
+      if (o.peer == C.rank) continue;
+      x.push_back(pxg_xfer{o.peer, o.send ? 1 : 0, h + at, static_cast<int64_t>(o.bytes)});
+      if (o.send) PXG_HIP(hipMemcpyAsync(h + at, o.dev, o.bytes, hipMemcpyDeviceToHost, s));
+      at += (o.bytes + 63) & ~size_t(63);
+    }
+    PXG_HIP(hipStreamSynchronize(s));
+    const int32_t rc = C.host_fn(C.host_user, static_cast<int32_t>(x.size()), x.data());
+    if (rc != 0) return SetError(PXG_INTERNAL, "host transport failed (%d) on a batch of %zu transfers", rc, x.size());
+    at = 0;
+    for (const Op& o : ops) {
+      if (o.peer == C.rank) continue;
+      if (!o.send) PXG_HIP(hipMemcpyAsync(o.dev, h + at, o.bytes, hipMemcpyHostToDevice, s));
+      at += (o.bytes + 63) & ~size_t(63);
+    }
+    // The staging is reused by the next grouped exchange, which starts with a stream wait.
+    return PXG_OK;
   }
 };
 
@@ -86,6 +172,19 @@ extern "C" int32_t pxg_comm_init(pxg_ctx* ctx, int32_t rank, int32_t nranks, con
   return PXG_OK;
 }
 
+extern "C" int32_t pxg_comm_init_host(pxg_ctx* ctx, int32_t rank, int32_t nranks, pxg_xfer_fn fn, void* user, pxg_comm** out) {
+  if (!ctx || !fn || !out || nranks < 1 || rank < 0 || rank >= nranks) return SetError(PXG_INVALID_ARGUMENT, "bad pxg_comm_init_host arguments");
+  PXG_HIP(hipSetDevice(ctx->impl.device));
+  auto c = std::make_unique<pxg_comm>();
+  c->impl.ctx = &ctx->impl;
+  c->impl.rank = rank;
+  c->impl.nranks = nranks;
+  c->impl.host_fn = fn;
+  c->impl.host_user = user;
+  *out = c.release();
+  return PXG_OK;
+}
+
 extern "C" int32_t pxg_comm_destroy(pxg_comm* comm) {
   if (!comm) return PXG_OK;
   if (comm->impl.ctx) (void)hipStreamSynchronize(comm->impl.ctx->stream);
@@ -115,41 +214,55 @@ static int32_t AlltoallV2(pxg_agg* agg, Comm& C, int64_t* bytes_sent, int64_t* b
   uint8_t* pin8 = static_cast<uint8_t*>(ctx->pinned) + Ctx::kPinnedOps;
   const size_t back = static_cast<size_t>(n) * (16 + hb);
   if (back + 64 > Ctx::kPinnedBytes - Ctx::kPinnedOps) return SetError(PXG_UNIMPLEMENTED, "%d ranks", n);
-  PXG_RETURN_IF_ERROR(a.ExportPartialDev(n, &C.send, d_send_cnt, d_send_hdr));
+  // A failed export still takes part in the {bytes, header} exchange, announcing -1 bytes to every
+  // peer (the device layout does the same when the finalize checks fail or the parts would pass
+  // the send buffer): then no rank posts the part exchange and every rank returns an error, so no
+  // peer is left inside a collective this rank has dropped out of.
+  const int32_t xrc = a.ExportPartialDev(n, &C.send, d_send_cnt, d_send_hdr);
+  std::string xerr;
+  if (xrc != PXG_OK) {
+    xerr = LastErrorRef();
+    PXG_HIP(hipMemsetAsync(d_send_cnt, 0xFF, static_cast<size_t>(n) * 8, ctx->stream));
+    PXG_HIP(hipMemsetAsync(d_send_hdr, 0, static_cast<size_t>(n) * hb, ctx->stream));
+  }
   {
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
     for (int p = 0; p < n; ++p) {
-      PXG_NCCL(ncclSend(d_send_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
-      PXG_NCCL(ncclRecv(d_recv_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
-      PXG_NCCL(ncclSend(d_send_hdr + p * hb, hb, ncclUint8, p, C.nccl, ctx->stream));
-      PXG_NCCL(ncclRecv(d_recv_hdr + p * hb, hb, ncclUint8, p, C.nccl, ctx->stream));
+      PXG_RETURN_IF_ERROR(grp.Send(d_send_cnt + p, 8, p));
+      PXG_RETURN_IF_ERROR(grp.Recv(d_recv_cnt + p, 8, p));
+      PXG_RETURN_IF_ERROR(grp.Send(d_send_hdr + p * hb, hb, p));
+      PXG_RETURN_IF_ERROR(grp.Recv(d_recv_hdr + p * hb, hb, p));
     }
     PXG_RETURN_IF_ERROR(grp.End());
   }
   // The one wait before the parts move: own sizes, received sizes and headers, finalize checks.
   PXG_HIP(hipMemcpyAsync(pin8, d_send_cnt, back, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(pin8 + back, a.ws.meta.p, 24, hipMemcpyDeviceToHost, ctx->stream));
+  if (xrc == PXG_OK) PXG_HIP(hipMemcpyAsync(pin8 + back, a.ws.meta.p, 24, hipMemcpyDeviceToHost, ctx->stream));
   PXG_HIP(hipStreamSynchronize(ctx->stream));
-  PXG_RETURN_IF_ERROR(a.CheckExportFinalize(pin8 + back));
+  if (xrc != PXG_OK) return SetError(xrc, "%s", xerr.c_str());
+  const int32_t crc = a.CheckExportFinalize(pin8 + back);
   const int64_t* pin = reinterpret_cast<const int64_t*>(pin8);
   std::vector<int64_t> seg(pin, pin + n), rs(pin + n, pin + 2 * n);
   std::vector<uint8_t> rhdr(pin8 + 16 * n, pin8 + 16 * n + n * hb);
+  if (crc != PXG_OK) return crc;  // (the device layout announced -1 for this failure too)
   int64_t total = 0, rtotal = 0;
   for (int p = 0; p < n; ++p) {
-    if (seg[p] < 0 || rs[p] < 0) return SetError(PXG_INTERNAL, "part sizes %lld / %lld", static_cast<long long>(seg[p]), static_cast<long long>(rs[p]));
+    if (seg[p] < 0) return SetError(PXG_INTERNAL, "export parts would pass the %zu-byte send buffer; no parts moved", C.send.bytes);
     total += seg[p];
+  }
+  for (int p = 0; p < n; ++p) {
+    if (rs[p] < 0) return SetError(PXG_INTERNAL, "rank %d failed its export; no parts moved", p);
     rtotal += rs[p];
   }
-  if (static_cast<uint64_t>(total) > C.send.bytes) return SetError(PXG_INTERNAL, "export wrote %lld bytes past its bound", static_cast<long long>(total));
   PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(rtotal) + 64));
   {
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
     int64_t so = 0, ro = 0;
     for (int p = 0; p < n; ++p) {
-      if (seg[p] > 0) PXG_NCCL(ncclSend(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), ncclUint8, p, C.nccl, ctx->stream));
-      if (rs[p] > 0) PXG_NCCL(ncclRecv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), ncclUint8, p, C.nccl, ctx->stream));
+      if (seg[p] > 0) PXG_RETURN_IF_ERROR(grp.Send(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), p));
+      if (rs[p] > 0) PXG_RETURN_IF_ERROR(grp.Recv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), p));
       so += seg[p];
       ro += rs[p];
     }
@@ -217,14 +330,14 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   for (int p = 0; p < n; ++p) pin[p] = seg[p];
   PXG_HIP(hipMemcpyAsync(d_send_cnt, pin, static_cast<size_t>(n) * 8, hipMemcpyHostToDevice, ctx->stream));
   {
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
     for (int p = 0; p < n; ++p) {
-      PXG_NCCL(ncclSend(d_send_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
-      PXG_NCCL(ncclRecv(d_recv_cnt + p, 1, ncclInt64, p, C.nccl, ctx->stream));
+      PXG_RETURN_IF_ERROR(grp.Send(d_send_cnt + p, 8, p));
+      PXG_RETURN_IF_ERROR(grp.Recv(d_recv_cnt + p, 8, p));
       if (hb > 0) {
-        PXG_NCCL(ncclSend(C.send.as<uint8_t>() + offs[p], hb, ncclUint8, p, C.nccl, ctx->stream));
-        PXG_NCCL(ncclRecv(d_recv_hdr + p * hb, hb, ncclUint8, p, C.nccl, ctx->stream));
+        PXG_RETURN_IF_ERROR(grp.Send(C.send.as<uint8_t>() + offs[p], hb, p));
+        PXG_RETURN_IF_ERROR(grp.Recv(d_recv_hdr + p * hb, hb, p));
       }
     }
     PXG_RETURN_IF_ERROR(grp.End());
@@ -241,12 +354,12 @@ extern "C" int32_t pxg_agg_alltoall(pxg_agg* agg, pxg_comm* comm, int64_t* bytes
   // 3. The parts: all-to-all(v) as grouped point-to-point sends over xGMI.
   PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(rtotal) + 64));
   {
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
     int64_t so = 0, ro = 0;
     for (int p = 0; p < n; ++p) {
-      if (seg[p] > 0) PXG_NCCL(ncclSend(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), ncclUint8, p, C.nccl, ctx->stream));
-      if (rs[p] > 0) PXG_NCCL(ncclRecv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), ncclUint8, p, C.nccl, ctx->stream));
+      if (seg[p] > 0) PXG_RETURN_IF_ERROR(grp.Send(C.send.as<uint8_t>() + so, static_cast<size_t>(seg[p]), p));
+      if (rs[p] > 0) PXG_RETURN_IF_ERROR(grp.Recv(C.recv.as<uint8_t>() + ro, static_cast<size_t>(rs[p]), p));
       so += seg[p];
       ro += rs[p];
     }
@@ -347,17 +460,17 @@ extern "C" int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, in
   std::vector<int64_t> hdr(static_cast<size_t>(n) * kGatherHdr, 0);
   if (!me_root) {
     PXG_HIP(hipMemcpyAsync(d_hdr, pin, kGatherHdr * 8, hipMemcpyHostToDevice, ctx->stream));
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
-    PXG_NCCL(ncclSend(d_hdr, kGatherHdr, ncclInt64, root, C.nccl, ctx->stream));
+    PXG_RETURN_IF_ERROR(grp.Send(d_hdr, (kGatherHdr) * 8, root));
     PXG_RETURN_IF_ERROR(grp.End());
   } else {
     std::copy(pin, pin + kGatherHdr, hdr.begin() + static_cast<size_t>(root) * kGatherHdr);
     if (n > 1) {
-      NcclGroup grp;
+      XferGroup grp(C);
       PXG_RETURN_IF_ERROR(grp.Start());
       for (int r = 0; r < n; ++r)
-        if (r != root) PXG_NCCL(ncclRecv(d_hdr + static_cast<size_t>(1 + r) * kGatherHdr, kGatherHdr, ncclInt64, r, C.nccl, ctx->stream));
+        if (r != root) PXG_RETURN_IF_ERROR(grp.Recv(d_hdr + static_cast<size_t>(1 + r) * kGatherHdr, (kGatherHdr) * 8, r));
       PXG_RETURN_IF_ERROR(grp.End());
       PXG_HIP(hipMemcpyAsync(pin + kGatherHdr, d_hdr + kGatherHdr, static_cast<size_t>(n) * kGatherHdr * 8, hipMemcpyDeviceToHost, ctx->stream));
       PXG_HIP(hipStreamSynchronize(ctx->stream));
@@ -370,19 +483,19 @@ extern "C" int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, in
   if (!me_root) {
     const int64_t G = R.n_groups;
     if (G > 0) {
-      NcclGroup grp;
+      XferGroup grp(C);
       PXG_RETURN_IF_ERROR(grp.Start());
       for (int k = 0; k < a.n_keys; ++k) {
         if (a.key_types[k] == PXG_STRING) {
-          PXG_NCCL(ncclSend(R.key_offsets[k].p, static_cast<size_t>(G + 1), ncclInt32, root, C.nccl, ctx->stream));
-          if (R.key_data_len[k] > 0) PXG_NCCL(ncclSend(R.key_data[k].p, static_cast<size_t>(R.key_data_len[k]), ncclUint8, root, C.nccl, ctx->stream));
+          PXG_RETURN_IF_ERROR(grp.Send(R.key_offsets[k].p, (static_cast<size_t>(G + 1)) * 4, root));
+          if (R.key_data_len[k] > 0) PXG_RETURN_IF_ERROR(grp.Send(R.key_data[k].p, static_cast<size_t>(R.key_data_len[k]), root));
         } else {
-          PXG_NCCL(ncclSend(R.key_fixed[k].p, static_cast<size_t>(G * fixed_w(k)), ncclUint8, root, C.nccl, ctx->stream));
+          PXG_RETURN_IF_ERROR(grp.Send(R.key_fixed[k].p, static_cast<size_t>(G * fixed_w(k)), root));
         }
       }
       for (int u = 0; u < n_vcols; ++u) {
         const int64_t b = val_bytes(u, G);
-        if (b > 0) PXG_NCCL(ncclSend(vbuf[u]->p, static_cast<size_t>(b), ncclUint8, root, C.nccl, ctx->stream));
+        if (b > 0) PXG_RETURN_IF_ERROR(grp.Send(vbuf[u]->p, static_cast<size_t>(b), root));
       }
       PXG_RETURN_IF_ERROR(grp.End());
     }
@@ -433,7 +546,7 @@ extern "C" int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, in
   if (any_str) PXG_RETURN_IF_ERROR(C.recv.Ensure(static_cast<size_t>(a.n_keys) * tmp_words * 4 + static_cast<size_t>(4 * nr) * 8 + 128));
   int32_t* tmp = C.recv.as<int32_t>();
   if (Gt > G0) {
-    NcclGroup grp;
+    XferGroup grp(C);
     PXG_RETURN_IF_ERROR(grp.Start());
     for (int i = 1; i < nr; ++i) {
       const int64_t G = gcnt[i];
@@ -441,16 +554,16 @@ extern "C" int32_t pxg_agg_gather(pxg_agg* agg, pxg_comm* comm, int32_t root, in
       const int src = order[i];
       for (int k = 0; k < a.n_keys; ++k) {
         if (a.key_types[k] == PXG_STRING) {
-          PXG_NCCL(ncclRecv(tmp + static_cast<size_t>(k) * tmp_words + tbase[i], static_cast<size_t>(G + 1), ncclInt32, src, C.nccl, ctx->stream));
+          PXG_RETURN_IF_ERROR(grp.Recv(tmp + static_cast<size_t>(k) * tmp_words + tbase[i], (static_cast<size_t>(G + 1)) * 4, src));
           const int64_t len = hdr[static_cast<size_t>(src) * kGatherHdr + 1 + k];
-          if (len > 0) PXG_NCCL(ncclRecv(R.key_data[k].as<uint8_t>() + bbase[k][i], static_cast<size_t>(len), ncclUint8, src, C.nccl, ctx->stream));
+          if (len > 0) PXG_RETURN_IF_ERROR(grp.Recv(R.key_data[k].as<uint8_t>() + bbase[k][i], static_cast<size_t>(len), src));
         } else {
-          PXG_NCCL(ncclRecv(R.key_fixed[k].as<uint8_t>() + gbase[i] * fixed_w(k), static_cast<size_t>(G * fixed_w(k)), ncclUint8, src, C.nccl, ctx->stream));
+          PXG_RETURN_IF_ERROR(grp.Recv(R.key_fixed[k].as<uint8_t>() + gbase[i] * fixed_w(k), static_cast<size_t>(G * fixed_w(k)), src));
         }
       }
       for (int u = 0; u < n_vcols; ++u) {
         const int64_t b = val_bytes(u, G);
-        if (b > 0) PXG_NCCL(ncclRecv(vbuf[u]->as<uint8_t>() + val_bytes(u, gbase[i]), static_cast<size_t>(b), ncclUint8, src, C.nccl, ctx->stream));
+        if (b > 0) PXG_RETURN_IF_ERROR(grp.Recv(vbuf[u]->as<uint8_t>() + val_bytes(u, gbase[i]), static_cast<size_t>(b), src));
       }
     }
     PXG_RETURN_IF_ERROR(grp.End());

@@ -637,6 +637,7 @@ struct XDst {
   const uint64_t* poff;    // [n_parts] byte offset of each part
   const uint64_t* layout;  // [n_parts][6] koff, keys, states, gofs, items, -
   const uint64_t* nitems;  // [n_parts]
+  const int64_t* fail;     // device layout: seg[0] < 0 = the layout refused the export (nothing written)
 };
 
 // One wave per listed group (part order): key record, state record, items.
@@ -650,6 +651,7 @@ __global__ void XWriteGroupsKernel(const uint32_t* __restrict__ glist, uint64_t 
   const uint64_t j = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (j >= ng) return;
+  if (dst.fail && dst.fail[0] < 0) return;
   const uint32_t g = glist[j];
   const uint32_t p = gpart[g];
   const uint64_t local = j - gstarts[p];
@@ -1059,6 +1061,7 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
   D.poff = X.desc.as<const uint64_t>();
   D.layout = D.poff + n_parts;
   D.nitems = D.layout + 6 * n_parts;
+  D.fail = nullptr;
   const uint64_t G = X.G;
   if (G > 0) {
     const bool has_big = has_q && x_nbig > 0;
@@ -1079,13 +1082,22 @@ int32_t Agg::ExportPartialV2(int32_t n_parts, void* dst, int64_t dst_capacity, i
 // The layout ExportPartialV2 computes on the host, on the device: one thread walks the parts
 // (<= kPartBuckets) from the device bounds, writes the descriptor XWriteGroupsKernel reads, each
 // part's header (into the part and into hdr_out), and each part's aligned byte count.
+// The export finalize's deferred checks (Agg::CheckExportFinalize, from ws.meta) and the send
+// buffer's capacity are checked here first: on a failure every part's count becomes -1 and
+// nothing is written (XWriteGroupsKernel sees seg_out[0] < 0), so a rank announces its failure
+// to its peers in the {bytes, header} exchange instead of dropping out of the collective, and a
+// group count that differs from the host's sizing can never write past the buffer.
 struct XHdrConst {
   uint32_t n_keys, srec;
   uint64_t plan_sig;
   int32_t has_q;
+  int32_t check;          // the finalize's checks are pending (x_check_pending)
+  uint32_t check_groups;  // the host's group count (x_check_groups)
+  uint64_t cap;           // send buffer bytes
 };
-__global__ void XLayoutDevKernel(const uint64_t* __restrict__ bounds, int32_t n_parts, XHdrConst hc, uint8_t* __restrict__ base,
-                                 uint64_t* __restrict__ desc, int64_t* __restrict__ seg_out, uint8_t* __restrict__ hdr_out) {
+__global__ void XLayoutDevKernel(const uint64_t* __restrict__ bounds, int32_t n_parts, XHdrConst hc, const uint8_t* __restrict__ meta,
+                                 uint8_t* __restrict__ base, uint64_t* __restrict__ desc, int64_t* __restrict__ seg_out,
+                                 uint8_t* __restrict__ hdr_out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint64_t* g_start = bounds;
   const uint64_t* k_start = bounds + n_parts + 1;
@@ -1093,6 +1105,25 @@ __global__ void XLayoutDevKernel(const uint64_t* __restrict__ bounds, int32_t n_
   uint64_t* poff = desc;
   uint64_t* lay = desc + n_parts;
   uint64_t* nit = lay + 6 * n_parts;
+  bool ok = true;
+  if (hc.check) {
+    const uint32_t g_dev = *reinterpret_cast<const uint32_t*>(meta + 8);
+    const uint32_t err = *reinterpret_cast<const uint32_t*>(meta + 16);
+    ok = err == 0 && g_dev == hc.check_groups;
+  }
+  uint64_t total = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    const uint64_t nw = (r_start[p + 1] & 0xFFFFFFFFu) - (r_start[p] & 0xFFFFFFFFu);
+    total += Align8(XLayoutOf(g_start[p + 1] - g_start[p], nw, k_start[p + 1] - k_start[p], hc.srec, hc.has_q != 0).bytes);
+  }
+  if (!ok || total > hc.cap) {
+    for (int p = 0; p < n_parts; ++p) {
+      seg_out[p] = -1;
+      uint64_t* d1 = reinterpret_cast<uint64_t*>(hdr_out + 64 * static_cast<uint64_t>(p));
+      for (int w = 0; w < 8; ++w) d1[w] = 0;
+    }
+    return;
+  }
   uint64_t off = 0;
   for (int p = 0; p < n_parts; ++p) {
     const uint64_t ng = g_start[p + 1] - g_start[p];
@@ -1139,7 +1170,9 @@ int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, u
   ExportCache& X = xc;
   const bool has_q = x_qval >= 0;
   const uint32_t srec = static_cast<uint32_t>(hplan_x.state_rec);
-  PXG_RETURN_IF_ERROR(ExportGroupV2(n_parts));
+  // The grouping of a host-layout export of the same state is reused (pxg_agg_export_partial
+  // just ran for these parts); otherwise the export finalize runs here.
+  if (!(X.valid && X.v2 && X.n_parts == n_parts && X.version == state_version)) PXG_RETURN_IF_ERROR(ExportGroupV2(n_parts));
   const uint64_t G = X.G;
   // Host bound of the parts' total: headers, per-group offsets / states / item offsets, every
   // group's key record (<= the arena), items (raw values <= staged rows, <= 2 * kXCentCapH words
@@ -1153,14 +1186,18 @@ int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, u
   hc.srec = srec;
   hc.plan_sig = XPlanSig(*this);
   hc.has_q = has_q ? 1 : 0;
+  hc.check = x_check_pending ? 1 : 0;
+  hc.check_groups = x_check_groups;
+  hc.cap = send->bytes;
   PXG_RETURN_IF_ERROR(Launch(ctx, "export_layout", XLayoutDevKernel, dim3(1), dim3(64), 0,
-                             X.starts.as<const uint64_t>() + kPartBuckets + 1, n_parts, hc, send->as<uint8_t>(), X.desc.as<uint64_t>(),
-                             seg_dev, hdr_dev));
+                             X.starts.as<const uint64_t>() + kPartBuckets + 1, n_parts, hc, ws.meta.as<const uint8_t>(), send->as<uint8_t>(),
+                             X.desc.as<uint64_t>(), seg_dev, hdr_dev));
   XDst D;
   D.base = send->as<uint8_t>();
   D.poff = X.desc.as<const uint64_t>();
   D.layout = D.poff + n_parts;
   D.nitems = D.layout + 6 * n_parts;
+  D.fail = seg_dev;
   if (G > 0) {
     const bool has_big = has_q && x_nbig > 0;
     PXG_RETURN_IF_ERROR(Launch(ctx, "export_write_groups", XWriteGroupsKernel, dim3(GridFor(static_cast<int64_t>(G) * 64, 256, 1 << 30)),
@@ -1302,6 +1339,33 @@ extern "C" int32_t pxg_agg_export_partial(pxg_agg* agg, int32_t n_parts, void* d
   if (ExchangeV2(agg->impl)) return agg->impl.ExportPartialV2(n_parts, dst, dst_capacity, part_offsets, part_bytes);
   PXG_RETURN_IF_ERROR(agg->impl.SpillHc());  // v1 row parts are cut from the table state
   return agg->impl.ExportPartial(n_parts, dst, dst_capacity, part_offsets, part_bytes);
+}
+
+// The device-laid-out export that pxg_agg_alltoall sends (ExportPartialDev: sizes, headers and
+// part layout computed on the device), into an aggregation-owned device buffer; one wait brings
+// back the sizes, the headers and the export finalize's checks.
+extern "C" int32_t pxg_agg_export_partial_dev(pxg_agg* agg, int32_t n_parts, void** parts, int64_t* part_bytes, uint8_t* headers) {
+  if (!agg || !parts || !part_bytes) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
+  if (n_parts < 1 || n_parts > kMaxParts) return SetError(PXG_INVALID_ARGUMENT, "n_parts must be in [1, %d]", kMaxParts);
+  Agg& a = agg->impl;
+  if (!ExchangeV2(a)) return SetError(PXG_FAILED_PRECONDITION, "the device layout exports partial states (exchange v2) only");
+  Agg::ExportCache& X = a.xc;
+  const size_t hb = XHeaderBytes();
+  PXG_RETURN_IF_ERROR(X.dcnt.Ensure(static_cast<size_t>(n_parts) * (8 + hb) + 64));
+  int64_t* d_seg = X.dcnt.as<int64_t>();
+  uint8_t* d_hdr = reinterpret_cast<uint8_t*>(d_seg + n_parts);
+  PXG_RETURN_IF_ERROR(a.ExportPartialDev(n_parts, &X.dsend, d_seg, d_hdr));
+  std::vector<uint8_t> h(static_cast<size_t>(n_parts) * (8 + hb) + 24);
+  PXG_HIP(hipMemcpyAsync(h.data(), d_seg, static_cast<size_t>(n_parts) * (8 + hb), hipMemcpyDeviceToHost, a.ctx->stream));
+  PXG_HIP(hipMemcpyAsync(h.data() + static_cast<size_t>(n_parts) * (8 + hb), a.ws.meta.p, 24, hipMemcpyDeviceToHost, a.ctx->stream));
+  PXG_HIP(hipStreamSynchronize(a.ctx->stream));
+  PXG_RETURN_IF_ERROR(a.CheckExportFinalize(h.data() + static_cast<size_t>(n_parts) * (8 + hb)));
+  std::memcpy(part_bytes, h.data(), static_cast<size_t>(n_parts) * 8);
+  for (int p = 0; p < n_parts; ++p)
+    if (part_bytes[p] < 0) return SetError(PXG_INTERNAL, "device export refused its parts (send buffer of %zu bytes)", X.dsend.bytes);
+  if (headers) std::memcpy(headers, h.data() + static_cast<size_t>(n_parts) * 8, static_cast<size_t>(n_parts) * hb);
+  *parts = X.dsend.p;
+  return PXG_OK;
 }
 
 extern "C" int32_t pxg_agg_import_partial(pxg_agg* agg, const void* src, int64_t nbytes) {

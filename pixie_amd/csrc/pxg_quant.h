@@ -310,19 +310,26 @@ constexpr uint64_t kSelLargeN = uint64_t(1) << 21;
 // consume's tile completion order, which differs run to run; plain double sums differed in the
 // last bits).  The reference sums sequentially in double; both agree to its rounding.
 // Compiled with -ffp-contract=off (the transformations need unfused operations).
+// Determinism holds while a group's values span less than ~2^100 in magnitude (the low word
+// keeps ~53 more bits below the high one); beyond that, or under heavy cancellation, the rounded
+// result can still depend on the staging order.
+// Non-finite sums: once hi is +-inf or NaN (an inf / NaN value, or an overflow) the error word
+// is pinned to 0, so the result is the plain sequential sum's inf / NaN (the reference's), not
+// the NaN that inf - inf inside the error term would give.
 struct DD {
   double hi, lo;
 };
 __device__ __forceinline__ DD TwoSum(double a, double b) {
   const double s = a + b;
   const double bb = s - a;
-  return DD{s, (a - (s - bb)) + (b - bb)};
+  const double e = (a - (s - bb)) + (b - bb);
+  return DD{s, isfinite(s) ? e : 0.0};
 }
 __device__ __forceinline__ DD DDAdd(DD x, DD y) {
   const DD s = TwoSum(x.hi, y.hi);
   const double e = s.lo + (x.lo + y.lo);
   const double h = s.hi + e;
-  return DD{h, e - (h - s.hi)};
+  return DD{h, isfinite(h) ? e - (h - s.hi) : 0.0};
 }
 __device__ __forceinline__ DD DDAddD(DD x, double b) { return DDAdd(x, DD{b, 0.0}); }
 __device__ __forceinline__ DD WaveSumDD(DD v) {

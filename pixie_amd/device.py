@@ -321,6 +321,15 @@ class Agg:
         check(self.lib.pxg_agg_export_partial(self.h, n_parts, ptr, cap, offs, nb))
         return list(offs), list(nb)
 
+    def export_partial_dev(self, n_parts: int):
+        """The export pxg_agg_alltoall sends, laid out on the device (pxg_agg_export_partial_dev):
+        returns (device address of the parts, part byte counts, n_parts * 64 header bytes)."""
+        ptr = C.c_void_p()
+        nb = (C.c_int64 * n_parts)()
+        hdr = (C.c_uint8 * (64 * n_parts))()
+        check(self.lib.pxg_agg_export_partial_dev(self.h, n_parts, C.byref(ptr), nb, hdr))
+        return int(ptr.value or 0), list(nb), bytes(hdr)
+
     def import_partial(self, src) -> None:
         """Merge one exported part (a contiguous uint8 device tensor) into this agg."""
         check(self.lib.pxg_agg_import_partial(self.h, C.c_void_p(src.data_ptr()), src.numel()))
@@ -389,8 +398,11 @@ HTTP_EVENTS_SCHEMA = [("time_", TIME64NS), ("upid", UINT128), ("service", STRING
 
 
 class Comm:
-    """RCCL communicator of libpxg (pxg_comm_*): one rank per GPU, over the ctx's device."""
+    """Communicator of libpxg (pxg_comm_*) over the ctx's device: RCCL (one rank per GPU), or
+    with Comm.host() a caller-supplied byte mover (pxg_comm_init_host) that runs the same device
+    exchange code with the bytes staged through host memory."""
     ID_BYTES = 128
+    _transport = None
 
     @staticmethod
     def unique_id() -> bytes:
@@ -405,6 +417,36 @@ class Comm:
         check(self.lib.pxg_comm_init(ctx.h, rank, nranks, buf, Comm.ID_BYTES, C.byref(h)))
         self.h = h
         self.rank, self.nranks = rank, nranks
+
+    @classmethod
+    def host(cls, ctx: "Ctx", rank: int, nranks: int, transport) -> "Comm":
+        """A communicator whose bytes move through `transport(ops) -> None` (a list of
+        (peer, is_send, memoryview) transfers, matched per peer in order; e.g.
+        pixie_amd.dist.GlooTransport).  pxg_agg_alltoall / pxg_agg_gather keep their device
+        code; only the byte mover differs from the RCCL communicator."""
+        self = cls.__new__(cls)
+        self.lib = load()
+
+        def fn(_user, n, ops):
+            try:
+                batch = []
+                for i in range(n):
+                    o = ops[i]
+                    buf = (C.c_uint8 * o.bytes).from_address(o.buf)
+                    batch.append((int(o.peer), bool(o.send), memoryview(buf).cast("B")))
+                transport(batch)
+                return 0
+            except Exception:  # reported to libpxg as a failed transfer batch
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._transport = _lib.XferFn(fn)  # kept alive as long as the communicator
+        h = C.c_void_p()
+        check(self.lib.pxg_comm_init_host(ctx.h, rank, nranks, self._transport, None, C.byref(h)))
+        self.h = h
+        self.rank, self.nranks = rank, nranks
+        return self
 
     def close(self) -> None:
         if self.h:

@@ -71,3 +71,75 @@ def test_float_sum_and_mean_equal_the_exact_sum(ctx):
         assert means[g] == exact / len(sel), (k, means[g], exact / len(sel))
     a.close()
     t.close()
+
+
+def _same(a, b):
+    return (math.isnan(a) and math.isnan(b)) or a == b
+
+
+def test_float_sums_keep_inf_and_nan(ctx):
+    """an inf value (or an overflow) inside a double-double sum must give the
+    reference's sequential-sum inf / NaN, not the NaN of inf - inf in the error word.  Groups
+    hold +inf, -inf, both, an overflowing run of 1e308, a NaN, and plain values; two groups of
+    2.5M values (the selection path's 4096-bin sample) hold infinities too and their quantiles
+    stay within the rank bound of the restated reference digest."""
+    import oracle_client as oc
+    import parity
+    rng = np.random.default_rng(21)
+    groups = {}
+    groups[0] = np.append(rng.standard_normal(1000), np.inf)
+    groups[1] = np.append(rng.standard_normal(1000), -np.inf)
+    groups[2] = np.concatenate([rng.standard_normal(500), [np.inf, -np.inf]])
+    groups[3] = np.full(50, 1e308)
+    groups[4] = np.append(rng.standard_normal(300), np.nan)
+    groups[5] = rng.standard_normal(5000)
+    big = rng.lognormal(3.0, 1.0, 2_500_000)
+    groups[6] = big.copy()
+    groups[6][rng.choice(big.size, 4000, replace=False)] = np.inf
+    groups[6][rng.choice(big.size, 10, replace=False)] = -np.inf
+    groups[7] = rng.lognormal(2.0, 0.5, 2_500_000)
+    groups[7][rng.choice(groups[7].size, 3000, replace=False)] = np.inf
+    keys = np.concatenate([np.full(v.size, k, np.int64) for k, v in groups.items()])
+    vals = np.concatenate(list(groups.values()))
+    perm = rng.permutation(keys.size)
+    keys, vals = keys[perm], vals[perm]
+    plan = P.linear_plan([P.source_op("t", [2, 4], ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("sum", [P.col(1)], [4]), P.agg_expr("mean", [P.col(1)], [4], fid=1),
+                                         P.agg_expr("quantiles", [P.col(1)], [4], fid=2)]),
+                          P.sink_op("out")])
+    q = LinearQuery(plan, [2, 4])
+    t = Table(ctx, [2, 4])
+    t.append([Column(2, values=keys), Column(4, values=vals)])
+    a = q.make_agg(ctx)
+    a.consume(t)
+    a.finalize()
+    r = a.result()
+    ks = np.asarray(r[0].values)
+    sums, means = np.asarray(r[1].values), np.asarray(r[2].values)
+    qm = np.asarray(r[3].values).reshape(-1, 7)
+    with np.errstate(over="ignore", invalid="ignore"):
+        for g, k in enumerate(ks):
+            v = groups[int(k)]
+            ref = float(np.sum(v))  # every group here is order-insensitive in its non-finite class
+            if not math.isfinite(ref):
+                assert _same(sums[g], ref), (k, sums[g], ref)
+                assert _same(means[g], ref / v.size), (k, means[g], ref / v.size)
+            else:
+                assert sums[g] == math.fsum(v.tolist()), (k, sums[g])
+    tables = {"t": {"types": [2, 4], "batches": [[Column(2, values=keys), Column(4, values=vals)]], "names": ["k", "v"]}}
+    ref_cols = oc.execute_plan(plan, tables)["out"][0]["cols"]
+    ref_q = {int(k): row for k, row in zip(np.asarray(ref_cols[0].values), parity.quantile_matrix(ref_cols[3]))}
+    for g, k in enumerate(ks):
+        k = int(k)
+        if k not in (6, 7):
+            continue
+        s = np.sort(groups[k])
+        for j, qq in enumerate(QS_ALL):
+            fd = np.searchsorted(s, qm[g, j], side="right") / s.size
+            fr = np.searchsorted(s, ref_q[k][j], side="right") / s.size
+            assert abs(fd - fr) <= parity.rank_bound(qq, s.size), (k, qq, qm[g, j], ref_q[k][j])
+    a.close()
+    t.close()
+
+
+QS_ALL = [0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99]

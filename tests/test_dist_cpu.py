@@ -114,3 +114,69 @@ def test_exchange_partitions_every_group_to_one_owner(world):
 def test_segments_are_aligned_and_cover_parts():
     offs, nb = [0, 16, 40], [13, 20, 5]
     assert segments(offs, nb) == [16, 24, 8]
+
+
+def _transport_worker(rank, world, port, q):
+    """Two batches like pxg_agg_alltoall's: {8-byte count, 64-byte header} per peer, then parts
+    of per-peer sizes; every transfer to a peer matched in issue order (tags)."""
+    from pixie_amd.dist import GlooTransport
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = GlooTransport()
+        size = lambda s, d: 0 if (s + d) % 3 == 2 else 1 + 37 * s + 11 * d  # some pairs send nothing
+        bufs = []
+        ops = []
+        for p in range(world):
+            if p == rank:
+                continue  # libpxg never passes self transfers
+            cnt = bytearray(struct.pack("<q", size(rank, p)))
+            hdr = bytearray(bytes([rank * 16 + p]) * 64)
+            rc, rh = bytearray(8), bytearray(64)
+            bufs += [cnt, hdr, rc, rh]
+            ops += [(p, True, memoryview(cnt)), (p, False, memoryview(rc)), (p, True, memoryview(hdr)), (p, False, memoryview(rh))]
+        tr(ops)
+        got = {}
+        for i, p in enumerate(x for x in range(world) if x != rank):
+            rc, rh = bufs[4 * i + 2], bufs[4 * i + 3]
+            got[p] = struct.unpack("<q", bytes(rc))[0]
+            assert bytes(rh) == bytes([p * 16 + rank]) * 64
+        parts, ops = {}, []
+        for p in range(world):
+            if p == rank:
+                continue
+            n = size(rank, p)
+            if n:
+                out = bytearray((rank * 31 + p + i) & 0xFF for i in range(n))
+                parts[("s", p)] = out
+                ops.append((p, True, memoryview(out)))
+            if got[p]:
+                inb = bytearray(got[p])
+                parts[("r", p)] = inb
+                ops.append((p, False, memoryview(inb)))
+        tr(ops)
+        for p in range(world):
+            if p != rank and got[p]:
+                want = bytes((p * 31 + rank + i) & 0xFF for i in range(size(p, rank)))
+                assert bytes(parts[("r", p)]) == want, (rank, p)
+        q.put((rank, tr.batches))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_transport_matches_transfers_in_order(world):
+    """The host communicator's byte mover (pixie_amd.dist.GlooTransport, behind
+    pxg_comm_init_host) on gloo: per-peer transfers meet in issue order, zero-size pairs are
+    skipped symmetrically, every byte arrives."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert sorted(r[1] for r in res) == [2] * world
