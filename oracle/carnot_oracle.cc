@@ -7,7 +7,7 @@
 // the "CPU Carnot (restated)" baseline that bench.py times.
 
 #include "carnot_oracle.h"
-#include "../pixie_amd/host/json_double.h"
+#include "json_number.h"
 
 #include <algorithm>
 #include <array>
@@ -315,14 +315,15 @@ Registry::Registry() {
  * UDAs (math_ops.h:583-772, math_sketches.h:33-82, agg_node_test.cc:44-72 test UDAs).
  *********************************************************************************************/
 // QuantilesUDA::Finalize (math_sketches.h:40-54): rapidjson Document written by
-// rapidjson::Writer -- restated in pixie_amd/host/json_double.h (pinned by
-// tests/test_json_double.py against the reference's own known strings and rapidjson's rules).
+// rapidjson::Writer -- restated for the oracle in json_number.h, independently of the engine's
+// pixie_amd/host/json_double.h (tests/test_json_double.py pins both against the reference's own
+// known strings and rapidjson's rules, and compares them byte for byte).
 std::string QuantilesJson(TDigest* d) {
   static const double kQ[7] = {0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99};
   double q[7];
   for (int k = 0; k < 7; ++k) q[k] = d->quantile(kQ[k]);
   std::string s;
-  pxjson::AppendQuantilesJson(q, &s);
+  oracle_json::AppendQuantilesJson(q, &s);
   return s;
 }
 
@@ -1690,6 +1691,18 @@ extern "C" int32_t oracle_quantiles_json(const double* vals, int64_t n, char* bu
   std::string s = QuantilesJson(&d);
   std::snprintf(buf, static_cast<size_t>(buflen), "%s", s.c_str());
   return static_cast<int32_t>(s.size());
+}
+
+// n groups of 7 doubles -> each group's QuantilesUDA::Finalize JSON followed by a NUL, back to
+// back in buf (cap bytes); returns the bytes needed (nothing is written past cap).
+extern "C" int64_t oracle_quantiles_json_render(const double* q7, int64_t n, char* buf, int64_t cap) {
+  std::string all;
+  for (int64_t g = 0; g < n; ++g) {
+    oracle_json::AppendQuantilesJson(q7 + 7 * g, &all);
+    all.push_back('\0');
+  }
+  if (buf && cap > 0) std::memcpy(buf, all.data(), static_cast<size_t>(std::min<int64_t>(cap, static_cast<int64_t>(all.size()))));
+  return static_cast<int64_t>(all.size());
 }
 
 extern "C" double oracle_pluck_float64(const char* json, const char* key) {

@@ -87,8 +87,11 @@ void oracle_tdigest_batch_quantiles_mm(int32_t nparts, const int32_t* kind, cons
                                        const double* weights, const double* mins, const double* maxs, double* out7);
 void oracle_tdigest_merge_quantiles(const double* a, int64_t na, const double* b, int64_t nb,
                                     double* out7);
-// The JSON string QuantilesUDA::Finalize would produce (rapidjson Writer bytes, json_double.h).
+// The JSON string QuantilesUDA::Finalize would produce (rapidjson Writer bytes, json_number.h).
 int32_t oracle_quantiles_json(const double* vals, int64_t n, char* buf, int32_t buflen);
+// The oracle's own rendering (json_number.h) of n groups of 7 quantile values: each group's JSON
+// followed by a NUL, back to back; returns the bytes needed (writes at most cap).
+int64_t oracle_quantiles_json_render(const double* q7, int64_t n, char* buf, int64_t cap);
 // pluck_float64 (json_ops.h:131-153).
 double oracle_pluck_float64(const char* json, const char* key);
 

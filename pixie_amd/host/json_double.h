@@ -141,7 +141,31 @@ inline int CountDecimalDigit32(uint32_t n) {
 }
 
 inline void DigitGen(DiyFp W, DiyFp Mp, uint64_t delta, char* buffer, int* len, int* K) {
-  static const uint32_t kPow10[] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000, 100000000, 1000000000};
+  // 10^0 .. 10^19 (uint64): the fractional loop's rounding scales wp_w by 10^-kappa for up to 19
+  // fractional digits (rapidjson: `index < 20 ? kPow10[index] : 0`).  An earlier version of this
+  // header had 10 uint32 entries and `index < 9`, which skipped GrisuRound after the 9th fractional
+  // digit and left e.g. 2419999.9999999997 where rapidjson writes 2419999.9999999995; the oracle's
+  // separate restatement (oracle/json_number.h) exposed it.
+  static const uint64_t kPow10[] = {1ULL,
+                                    10ULL,
+                                    100ULL,
+                                    1000ULL,
+                                    10000ULL,
+                                    100000ULL,
+                                    1000000ULL,
+                                    10000000ULL,
+                                    100000000ULL,
+                                    1000000000ULL,
+                                    10000000000ULL,
+                                    100000000000ULL,
+                                    1000000000000ULL,
+                                    10000000000000ULL,
+                                    100000000000000ULL,
+                                    1000000000000000ULL,
+                                    10000000000000000ULL,
+                                    100000000000000000ULL,
+                                    1000000000000000000ULL,
+                                    10000000000000000000ULL};
   const DiyFp one{uint64_t(1) << -Mp.e, Mp.e};
   const uint64_t wp_w = Mp.f - W.f;
   uint32_t p1 = static_cast<uint32_t>(Mp.f >> -one.e);
@@ -149,7 +173,7 @@ inline void DigitGen(DiyFp W, DiyFp Mp, uint64_t delta, char* buffer, int* len, 
   int kappa = CountDecimalDigit32(p1);
   *len = 0;
   while (kappa > 0) {
-    const uint32_t div = kPow10[kappa - 1];
+    const uint32_t div = static_cast<uint32_t>(kPow10[kappa - 1]);
     const uint32_t d = p1 / div;
     p1 %= div;
     if (d || *len) buffer[(*len)++] = static_cast<char>('0' + d);
@@ -157,7 +181,7 @@ inline void DigitGen(DiyFp W, DiyFp Mp, uint64_t delta, char* buffer, int* len, 
     const uint64_t tmp = (static_cast<uint64_t>(p1) << -one.e) + p2;
     if (tmp <= delta) {
       *K += kappa;
-      GrisuRound(buffer, *len, delta, tmp, static_cast<uint64_t>(kPow10[kappa]) << -one.e, wp_w);
+      GrisuRound(buffer, *len, delta, tmp, kPow10[kappa] << -one.e, wp_w);
       return;
     }
   }
@@ -171,7 +195,7 @@ inline void DigitGen(DiyFp W, DiyFp Mp, uint64_t delta, char* buffer, int* len, 
     if (p2 < delta) {
       *K += kappa;
       const int index = -kappa;
-      GrisuRound(buffer, *len, delta, p2, one.f, wp_w * (index < 9 ? kPow10[index] : 0));
+      GrisuRound(buffer, *len, delta, p2, one.f, wp_w * (index < 20 ? kPow10[index] : 0));
       return;
     }
   }
