@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--no-engine-leg", action="store_true",
                     help="skip the engine query leg (profiling runs: keeps per-kernel averages to the timed steps)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (bin + join) leg")
+    ap.add_argument("--no-c3-full", action="store_true", help="skip the full-cardinality C3 leg (no filter, 10M groups)")
+    ap.add_argument("--no-c3-parity", action="store_true", help="skip the full-cardinality C3 leg's oracle parity (20M rows)")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 (carnot_csv, CSV parse included) leg")
     ap.add_argument("--c5-rows", type=int, default=20_000_000)
     ap.add_argument("--host-gen", action="store_true", help="generate on the host and upload (default: device generator)")
@@ -255,6 +257,7 @@ def main():
     # Per-kernel breakdown from one untimed, fully event-bracketed pass (the event records
     # themselves cost time, so the timed region brackets agg_consume only).
     kernel_ms = profiled_kernels(ctx, step)
+    step_launches = launches_of(ctx, step)
     ctx.reset_stats()
     ctx.set_profiling(True, only="agg_consume")
     torch.cuda.synchronize()
@@ -306,9 +309,11 @@ def main():
     filter_map = None
     if world == 1 and not args.no_engine_leg:
         filter_map = filter_map_leg(ctx, table, n, P)
-    c3 = None
+    c3 = c3_full = None
     if world == 1 and not args.no_engine_leg:
         c3 = c3_leg(args, ctx, table, n, P, plan_agg)
+        if not args.no_c3_full:
+            c3_full = c3_leg(args, ctx, table, n, P, plan_agg, full=True)
 
     c5 = None
     if world == 1 and not args.no_engine_leg and not args.no_c5:
@@ -366,6 +371,7 @@ def main():
                 "parallelism": "single GPU",
                 "algorithmic_bytes_per_row": alg_bytes / n,
                 "kernel_ms_per_step": kernel_ms,
+                "kernel_launches_per_step": step_launches,
                 "step_rate_gbs_algorithmic": alg_bytes / (ms_per_step / 1000.0) / 1e9,
             },
             "roofline": {
@@ -389,6 +395,7 @@ def main():
             "engine_query": engine_query,
             "filter_map": filter_map,
             "c3": c3,
+            "c3_full": c3_full,
             "c5": c5,
             "c1": c1,
             "n1": n1,
@@ -414,6 +421,17 @@ def profiled_kernels(ctx, step):
         if l:
             out[name] = round(ms, 4)
     return out
+
+
+def launches_of(ctx, step):
+    """Kernel launches of one step (every libpxg launch, counted with profiling on), without
+    the runtime's copy / fill operations."""
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    step()
+    ctx.sync()
+    ctx.set_profiling(False)
+    return ctx.kernel_stats("*")[0]
 
 
 def launch_ranks(args):
@@ -746,19 +764,22 @@ def filter_map_leg(ctx, table, n, P, reps=5):
                                        "definition (every referenced input column once + the output), as agg_consume does"}}
 
 
-def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
+def c3_leg(args, ctx, table, n, P, plan_agg, steps=3, full=False):
     """BASELINE config C3: the high-cardinality group-by, (pod, remote_addr) over the same
-    100M-row table (10M distinct pairs, ~7M groups after the filter): count, mean(latency),
-    sum(resp_body_size).  Parity for this shape is tests/test_scale_parity.py."""
-    alg = 24 * n + table.device_bytes(P.HE["pod"]) + table.device_bytes(P.HE["remote_addr"])
+    100M-row table (10M distinct pairs): count, mean(latency), sum(resp_body_size).  Default:
+    SURVEY §8d's query, behind Filter(resp_status >= 400) (~5M groups; parity for this shape is
+    tests/test_scale_parity.py).  full=True: no filter, every row, all 10M pairs as groups
+    (plans.c3_full_plan), with its own parity block against the oracle on a 20M-row prefix."""
+    plan = P.c3_full_plan() if full else P.c3_plan()
+    alg = (16 if full else 24) * n + table.device_bytes(P.HE["pod"]) + table.device_bytes(P.HE["remote_addr"])
     # The group-count hint comes from a first, untimed run without one, as the engine's
     # group-count statistics size the next run of the same plan (DESIGN.md §4.4).
-    probe = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=0)
+    probe = plan_agg(ctx, plan, "http_events", P.HTTP_TYPES, expected_groups=0)
     probe.reset()
     probe.consume(table)
     hint = probe.finalize()
     probe.close()
-    a = plan_agg(ctx, P.c3_plan(), "http_events", P.HTTP_TYPES, expected_groups=hint)
+    a = plan_agg(ctx, plan, "http_events", P.HTTP_TYPES, expected_groups=hint)
 
     def step():
         a.reset()
@@ -791,7 +812,10 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
     l, ms, _pre = consume_stats(ctx)
     avg = ms / steps
     achieved = alg / (avg / 1000.0) / 1e9
-    out = {"workload": "C3: Filter(resp_status>=400) -> Agg by (pod, remote_addr): count, mean(latency), sum(resp_body_size)",
+    wl = ("C3 full cardinality: Agg by (pod, remote_addr) over every row (no filter; 10M distinct pairs): count, mean(latency), "
+          "sum(resp_body_size)" if full else
+          "C3: Filter(resp_status>=400) -> Agg by (pod, remote_addr): count, mean(latency), sum(resp_body_size)")
+    out = {"workload": wl,
            "mode": "high-cardinality (partition records + LDS tables, pxg_hc.hip)" if mode.get("hc_mode") else "global table",
            "partition_bits": mode.get("hc_partition_bits"), "kernel_ms_per_step": kernel_ms,
            "rows": n, "steps": steps, "groups": g, "selected_rows": a.rows_selected(), "ms_per_step": el * 1000.0 / steps,
@@ -799,7 +823,44 @@ def c3_leg(args, ctx, table, n, P, plan_agg, steps=3):
            "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg}}
     a.close()
+    if full and not args.no_c3_parity:
+        out["parity"] = c3_full_parity(ctx, P, plan_agg, plan)
     return out
+
+
+def c3_full_parity(ctx, P, plan_agg, plan, n=20_000_000):
+    """The full-cardinality C3 plan on the table's first n rows (device table generated in HBM,
+    bit-identical to the host generator) against the oracle over the same rows: group keys and
+    counts and sums bit-exact, means 1e-6 (tests/parity.py bars)."""
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_client as oc
+        import parity
+        from pixie_amd.device import Table, datagen_http_events
+        t = Table(ctx, P.HTTP_TYPES)
+        t.append_http_events(SEED, 0, n, N_PAIR_KEYS)
+        a = plan_agg(ctx, plan, "http_events", P.HTTP_TYPES, expected_groups=n // 2)
+        a.reset()
+        a.consume(t)
+        a.finalize()
+        mode = a.info().get("hc_mode")
+        dev = a.result()
+        a.close()
+        t.close()
+        cols = datagen_http_events(SEED, 0, n, n_pair_keys=N_PAIR_KEYS, threads=16)
+        need = {P.HE[c] for c in ("pod", "remote_addr", "latency", "resp_body_size")}
+        ocols = [c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)]
+        tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [ocols], "names": P.HTTP_NAMES}}
+        t0 = time.time()
+        ref = oc.execute_plan(plan, tables)["output"][0]["cols"]
+        rep = parity.compare_agg(dev, ref, 2, ["count", "rel", "exact"])
+        rep.update(rows=n, oracle_s=round(time.time() - t0, 2), device_mode="high-cardinality" if mode else "global table",
+                   scope=f"the full-cardinality C3 plan over rows [0, {n}) of the same generator, device vs the oracle")
+        return rep
+    except Exception as e:  # the legs must never break the bench line
+        import traceback
+        traceback.print_exc()
+        return {"ok": False, "error": f"C3 full parity failed: {e}"}
 
 
 def c5_leg(args, engine, ctx, P, reps=5):
@@ -1002,6 +1063,11 @@ def n1_leg(args, ctx, P, Table, plan_agg):
         "kernel_ms_per_step": kernel_ms, "profiled_step_ms": round(prof_step_ms, 3),
         "finalize_ms_per_step": round(el * 1000.0 / args.n1_steps - avg, 3),
         "sort_fallback_groups": {"profiled_step": fallback_groups[0], "last_timed_step": fallback_groups[1]},
+        # the whole query (consume + finalize, HBM-resident inputs to finalized results) against
+        # the HBM roofline: algorithmic bytes / step time -- the north_star's >= 0.60 target
+        "roofline_step": {"achieved": alg / (el / args.n1_steps) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": alg / (el / args.n1_steps) / 1e9 / HBM_PEAK_GBS,
+                          "per": "whole step: reset + consume + finalize, timed over the steps"},
         "roofline": {"bound": "hbm", "kernel": "agg_consume", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, n),
                      "traffic_source": "committed file (replaced by the live PMC leg when it runs)", "algorithmic_bytes_per_launch": alg,

@@ -179,7 +179,7 @@ int32_t pxg_ctx_sync(pxg_ctx* ctx);
 void* pxg_ctx_stream(pxg_ctx* ctx);
 /* Kernel timing: when enabled every library kernel launch is bracketed by HIP events on the
  * ctx stream; pxg_ctx_kernel_stats returns launches and summed device milliseconds of the
- * named kernel since the last reset. */
+ * named kernel since the last reset ("*": every kernel launched meanwhile, summed). */
 int32_t pxg_ctx_set_profiling(pxg_ctx* ctx, int32_t enabled);
 int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* kernel_name, int64_t* launches,
                              double* total_ms);

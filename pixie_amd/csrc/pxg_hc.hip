@@ -504,16 +504,14 @@ int32_t Agg::FinalizeHc(HcExport* ex) {
   for (int k = 0; k < n_keys && !ex; ++k) {
     const int t = key_types[k];
     if (t == PXG_STRING) {
+      // (the payload is reserved after the partition pass, from its group count)
       dbase[k] = static_cast<uint64_t>(R.key_data_len[k]);
       PXG_RETURN_IF_ERROR(R.key_offsets[k].Reserve((cap_g + 1) * 4, static_cast<size_t>(g0) * 4, ctx->stream));
-      PXG_RETURN_IF_ERROR(R.key_data[k].Reserve(dbase[k] + n * 8 * kHcStrWords + 16, dbase[k], ctx->stream));
     } else {
       const size_t wd = t == PXG_UINT128 ? 16 : 8;
       PXG_RETURN_IF_ERROR(R.key_fixed[k].Reserve(cap_g * wd, static_cast<size_t>(g0) * wd, ctx->stream));
     }
   }
-  for (int k = 0; k < n_keys; ++k)
-    if (dbase[k] + n * 8 * kHcStrWords >= (uint64_t(1) << 31)) return SetError(PXG_UNIMPLEMENTED, "string key column over 2 GiB");
   HcOut out;
   std::memset(&out, 0, sizeof(out));
   if (ex) {
@@ -581,7 +579,15 @@ int32_t Agg::FinalizeHc(HcExport* ex) {
     ex->plan = hp;
     return PXG_OK;
   }
-  // String keys: lengths -> offsets (scan), then the bytes.
+  // String keys: lengths -> offsets (scan), then the bytes.  Payload bound: G groups of at most
+  // kHcStrWords words per key (int32 Arrow offsets: < 2 GiB per column; bounding by the G groups
+  // rather than the n records lets 100M records of 10M groups through).
+  for (int k = 0; k < n_keys; ++k) {
+    if (key_types[k] != PXG_STRING) continue;
+    const uint64_t need = dbase[k] + static_cast<uint64_t>(G) * 8 * kHcStrWords;
+    if (need >= (uint64_t(1) << 31)) return SetError(PXG_UNIMPLEMENTED, "string key column over 2 GiB");
+    PXG_RETURN_IF_ERROR(R.key_data[k].Reserve(need + 16, dbase[k], ctx->stream));
+  }
   bool any_str = false;
   HcKeyCopy kc;
   std::memset(&kc, 0, sizeof(kc));

@@ -402,6 +402,17 @@ extern "C" int32_t pxg_ctx_profile_only(pxg_ctx* ctx, const char* kernel_name) {
 extern "C" int32_t pxg_ctx_kernel_stats(pxg_ctx* ctx, const char* name, int64_t* launches, double* total_ms) {
   if (!ctx || !name) return SetError(PXG_INVALID_ARGUMENT, "bad arguments");
   PXG_RETURN_IF_ERROR(ctx->impl.ResolveTimings());
+  if (name[0] == '*' && name[1] == 0) {  // every kernel launched while profiling was on
+    int64_t l = 0;
+    double ms = 0;
+    for (const auto& kv : ctx->impl.stats) {
+      l += kv.second.launches;
+      ms += kv.second.total_ms;
+    }
+    if (launches) *launches = l;
+    if (total_ms) *total_ms = ms;
+    return PXG_OK;
+  }
   auto it = ctx->impl.stats.find(name);
   if (launches) *launches = it == ctx->impl.stats.end() ? 0 : it->second.launches;
   if (total_ms) *total_ms = it == ctx->impl.stats.end() ? 0 : it->second.total_ms;

@@ -286,6 +286,17 @@ def c3_plan(table: str = "http_events"):
     return linear_plan([src, flt, agg, sink_op("output")])
 
 
+def c3_full_plan(table: str = "http_events"):
+    """BASELINE configs[2] at its full cardinality: no filter, every row aggregated by
+    (pod, remote_addr) -- all 10M distinct pairs of the table -- count, mean(latency),
+    sum(resp_body_size)."""
+    src = source_op(table, HTTP_TYPES, HTTP_NAMES, [HE["pod"], HE["remote_addr"], HE["latency"], HE["resp_body_size"]])
+    agg = agg_op([0, 1], [agg_expr("count", [col(2)], [INT64]), agg_expr("mean", [col(2)], [INT64], fid=1),
+                          agg_expr("sum", [col(3)], [INT64], fid=2)],
+                 ["pod", "remote_addr"], ["count", "mean_latency", "sum_resp_body"])
+    return linear_plan([src, agg, sink_op("output")])
+
+
 # conn_stats subset and a pod metadata table for C5 (SURVEY.md §8d, "C5 (next)").
 CONN_STATS_SCHEMA = [("time_", TIME64NS), ("upid", UINT128), ("remote_addr", STRING), ("remote_port", INT64),
                      ("bytes_sent", INT64), ("bytes_recv", INT64)]

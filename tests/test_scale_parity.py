@@ -121,3 +121,25 @@ def test_sharded_c2_8_parts_10m_rows_matches_single_node(ctx):
     assert rep["v2_quantiles"]["groups_rank"] > 0
     for x in aggs + tabs:
         x.close()
+
+
+def test_c3_full_cardinality_matches_oracle_on_20m_rows(ctx):
+    """BASELINE configs[2] without the filter (plans.c3_full_plan): every row aggregated, ~8.6M
+    groups of the 10M pairs in 20M rows, through the partitioned high-cardinality path."""
+    n = 20_000_000
+    cols = datagen_http_events(SEED, 0, n, n_pair_keys=10_000_000, threads=16)
+    need = {P.HE[c] for c in ("pod", "remote_addr", "latency", "resp_body_size")}
+    ocols = [c if i in need else oc.AbsentColumn(c.type, len(c)) for i, c in enumerate(cols)]
+    ref = oc.execute_plan(P.c3_full_plan(), _tables(ocols))["output"][0]["cols"]
+    t = _device_table(ctx, 0, n)
+    q = LinearQuery(P.c3_full_plan(), P.HTTP_TYPES, expected_groups=n // 2)
+    a = q.make_agg(ctx)
+    a.consume(t)
+    assert a.info()["hc_mode"] == 1
+    a.finalize()
+    dev = a.result()
+    rep = parity.compare_agg(dev, ref, 2, ["count", "rel", "exact"])
+    assert rep["ok"], rep
+    assert rep["groups_ref"] > 5_000_000
+    a.close()
+    t.close()
