@@ -1706,11 +1706,17 @@ int32_t AggFinalizeTable(Agg* a) {
     clk.Mark("finalize: chains + small issued");
     PXG_RETURN_IF_ERROR(RunReductions());
     clk.Mark("finalize: reductions issued");
+    // The tiny digests follow the small ones on the side stream when no early big set runs (C2
+    // shape: the main stream then carries the reductions and the mid classes, the longest
+    // chain; round 6, tools/step_ab.py at 100M rows: step 2.210 -> 2.173 ms).  With an early set
+    // (1B rows) every placement measured the same (14.51-14.58 ms), so they stay on the main
+    // stream there, as do the mid classes (on either side stream: 14.56-14.59 ms).
+    const hipStream_t tiny_st = !early_on && guard.side ? ctx->side : ctx->stream;
     for (int u = 0; u < a->n_udas && !a->export_x; ++u) {
       if (a->uda_kind[u] != PXG_UDA_QUANTILES) continue;
-      PXG_RETURN_IF_ERROR(Launch(ctx, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
-                                 static_cast<const uint32_t*>(d_cls), gstart, cv.p[a->uda_val[u]], a->uda_arg_type[u],
-                                 R.uda_out[u].as<double>()));
+      PXG_RETURN_IF_ERROR(LaunchOn(ctx, tiny_st, "quant_tiny", QuantTinyKernel, dim3((ngroups + 3) / 4), dim3(256), 0, lists,
+                                   static_cast<const uint32_t*>(d_cls), gstart, cv.p[a->uda_val[u]], a->uda_arg_type[u],
+                                   R.uda_out[u].as<double>()));
     }
     uint32_t hm[6], hmid[kNumMidSub];
     clk.Mark("finalize: issue to meta");
