@@ -10,7 +10,7 @@ import os
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpxg.so")
+LIB_PATH = os.environ.get("PXG_LIB_PATH") or os.path.join(_HERE, "lib", "libpxg.so")  # (override: A/B builds in tools/)
 
 # px.types.DataType (src/shared/types/typespb/types.proto:26-34)
 BOOLEAN, INT64, UINT128, FLOAT64, STRING, TIME64NS = 1, 2, 3, 4, 5, 6

@@ -31,6 +31,7 @@
 namespace pxg {
 
 constexpr int kHcBlock = 256;
+constexpr uint64_t kHcMaxPartRecs = 4096;  // records per partition the first pass aims below (FinalizeHc)
 constexpr int kHcTable = 1024;  // LDS entries per partition (~1024 records, ~300-400 groups at C3)
 constexpr int kHcMaxAcc = 4;
 constexpr int kHcKeyWords = 1 + kMaxKeys * kHcStrWords;
@@ -225,7 +226,7 @@ __device__ __forceinline__ uint64_t HcWordsHash(const uint64_t* w) {
 // first LDS probe, and the representative compares of the batch are issued together after
 // every record has found its candidate slot.  KW: key words per record (hp.kwords), a template
 // so the batch's registers are sized exactly.
-constexpr int kHcR = 4;
+constexpr int kHcR = 4;  // (8 measured slower in round 6: C3 hc_agg 0.51 -> 0.88 ms, C3 full 2.79 -> 3.77 ms)
 template <int KW>
 __global__ void __launch_bounds__(kHcBlock) HcAggKernel(HcAggPlan hp, const uint64_t* __restrict__ rec,
                                                        const uint32_t* __restrict__ starts, uint32_t nparts, HcOut out,
@@ -545,6 +546,12 @@ int32_t Agg::FinalizeHc(HcExport* ex) {
   if (est == 0 || est > n) est = n;
   int pbits = 1;
   while (pbits < 28 && (est >> (pbits + kHcGroupsLog2)) > 0) ++pbits;
+  // ... and at most ~kHcMaxPartRecs records per partition: a workgroup's batches over a long
+  // partition are latency-bound (tools/hc_pbits_ab.py, C3 without the filter, 100M records of
+  // 6.4M groups: 14 bits by groups, 6100 records per partition -> 15 bits: hc_agg 3.78 -> 2.78 ms,
+  // step 16.3 -> 15.5 ms; 16 bits measured slower again, 16.1 ms).  The filtered C3 (12M records)
+  // keeps its 14 bits (13 / 15 / 16 bits: 3.46 / 3.36 / 3.84 ms against 3.11).
+  while (pbits < 28 && (n >> pbits) > kHcMaxPartRecs) ++pbits;
   const char* fe = std::getenv("PXG_HC_PBITS");  // tests: the first pass's partition count
   const int forced = fe ? std::atoi(fe) : 0;
   if (forced > 0 && forced <= 28) pbits = forced;
