@@ -241,7 +241,9 @@ __global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restric
 // 8-ballot match of the digit bits.  The tile is then reordered by digit in LDS and written
 // out in digit runs (consecutive threads -> consecutive addresses) instead of one scattered
 // store per item.  The first value stream is loaded up front so its latency overlaps the
-// ranking.
+// ranking.  (Round 6: loading stream v + 1 into the same registers right after stream v went to
+// LDS, ahead of stream v's run writes, made the 9-stream partition sort slower: C3 without the
+// filter, radix_scatter 7.0 -> 8.1 ms.)
 __global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
                                                                ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n, int shift,
                                                                const uint32_t* __restrict__ offs, uint32_t ntiles) {
