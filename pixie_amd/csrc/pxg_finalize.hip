@@ -1671,8 +1671,10 @@ int32_t AggFinalizeTable(Agg* a) {
     // event only, while the digests below keep the GPU busy.
     clk.Mark("finalize: classes issued");
     uint8_t* pin = static_cast<uint8_t*>(ctx->pinned);
-    PXG_HIP(hipMemcpyAsync(pin + 64, d_cls, 24, hipMemcpyDeviceToHost, ctx->stream));  // cls[4] @32, bigmeta[2] @48
-    PXG_HIP(hipMemcpyAsync(pin + 88, meta + 64, 4 * kNumMidSub, hipMemcpyDeviceToHost, ctx->stream));  // mid classes 4-6
+    {  // cls[4] @32, bigmeta[2] @48; mid classes 4-6
+      const SmallCopy rb[2] = {{d_cls, 64, 24}, {meta + 64, 88, 4 * kNumMidSub}};
+      PXG_RETURN_IF_ERROR(ReadbackSmall(ctx, ctx->stream, rb, 2));
+    }
     PXG_HIP(hipEventRecord(ctx->ev_meta, ctx->stream));
     // Kernels whose work lists are counted on the device launch right away with upper-bound
     // grids (blocks past the device count exit); the host reads the counts back only after
@@ -1825,14 +1827,19 @@ int32_t AggFinalizeTable(Agg* a) {
   std::vector<uint32_t> totals(kMaxKeys, 0);
   unsigned int err = 0;
   uint32_t* pin32 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pinned) + 128);
-  for (int k = 0; k < a->n_keys; ++k)
-    if (a->key_types[k] == PXG_STRING)
-      PXG_HIP(hipMemcpyAsync(pin32 + k, R.key_offsets[k].as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
   uint32_t g_dev = 0;
-  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 1, d_ngroups, 4, hipMemcpyDeviceToHost, ctx->stream));
-  PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 2, d_fallback, 4, hipMemcpyDeviceToHost, ctx->stream));
-  if (early_on) PXG_HIP(hipMemcpyAsync(pin32 + kMaxKeys + 3, ws.early.meta.p, 12, hipMemcpyDeviceToHost, ctx->stream));
+  {  // one launch for the string-key totals, the error / group count / fallback words, early meta
+    SmallCopy rb[kMaxSmallCopies];
+    int nrb = 0;
+    const uint32_t b = 128;  // pin32's byte offset in the pinned scratch
+    for (int k = 0; k < a->n_keys; ++k)
+      if (a->key_types[k] == PXG_STRING) rb[nrb++] = {R.key_offsets[k].as<uint32_t>() + ngroups, b + 4 * k, 4};
+    rb[nrb++] = {d_err, b + 4 * kMaxKeys, 4};
+    rb[nrb++] = {d_ngroups, b + 4 * (kMaxKeys + 1), 4};
+    rb[nrb++] = {d_fallback, b + 4 * (kMaxKeys + 2), 4};
+    if (early_on) rb[nrb++] = {ws.early.meta.p, b + 4 * (kMaxKeys + 3), 12};
+    PXG_RETURN_IF_ERROR(ReadbackSmall(ctx, ctx->stream, rb, nrb));
+  }
   clk.Mark("finalize: issue rest");
   PXG_HIP(hipStreamSynchronize(ctx->stream));
   clk.Mark("finalize: final wait");

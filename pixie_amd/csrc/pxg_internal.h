@@ -313,6 +313,18 @@ void ResultFree(void* p);
 // to kCopyKernelMaxBytes) by a copy kernel, otherwise hipMemcpyAsync.
 constexpr size_t kCopyKernelMaxBytes = size_t(8) << 20;
 int32_t CopyD2H(Ctx* ctx, hipStream_t stream, void* host, const void* dev, size_t n);
+// Several small device values (each <= 64 bytes, 4-byte aligned sizes and addresses) into the
+// ctx's pinned scratch at byte offsets dst_off, by one kernel launch: a hipMemcpyAsync per value
+// cost ~5 us of stream time each (round 6 C2 trace: 9 such copies per step).
+struct SmallCopy {
+  const void* src;
+  uint32_t dst_off;
+  uint32_t bytes;
+};
+constexpr int kMaxSmallCopies = 8;
+int32_t ReadbackSmall(Ctx* ctx, hipStream_t stream, const SmallCopy* items, int n);
+// Zero up to four device ranges (4-byte aligned, sizes multiples of 4) in one launch.
+int32_t ZeroRanges(Ctx* ctx, hipStream_t stream, void* const* ptrs, const size_t* bytes, int n);
 }
 
 struct pxg_ctx {

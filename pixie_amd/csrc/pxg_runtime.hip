@@ -752,6 +752,85 @@ int32_t CopyD2H(Ctx* ctx, hipStream_t stream, void* host, const void* dev, size_
   return PXG_OK;
 }
 
+struct SmallCopies {
+  const uint32_t* src[kMaxSmallCopies];
+  uint32_t dst_off[kMaxSmallCopies];
+  uint32_t words[kMaxSmallCopies];
+  int n;
+};
+// Thread t: item t / 16, word t % 16 (64 bytes per item at most).
+__global__ void __launch_bounds__(128) SmallReadbackKernel(SmallCopies c, uint8_t* __restrict__ host) {
+  const int i = threadIdx.x >> 4, w = threadIdx.x & 15;
+  if (i < c.n && static_cast<uint32_t>(w) < c.words[i]) reinterpret_cast<uint32_t*>(host + c.dst_off[i])[w] = c.src[i][w];
+}
+
+int32_t ReadbackSmall(Ctx* ctx, hipStream_t stream, const SmallCopy* items, int n) {
+  if (n <= 0) return PXG_OK;
+  if (n > kMaxSmallCopies) return SetError(PXG_INTERNAL, "%d small copies in one readback", n);
+  SmallCopies c;
+  std::memset(&c, 0, sizeof(c));
+  c.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (items[i].bytes > 64 || (items[i].bytes & 3) || (items[i].dst_off & 3) || (reinterpret_cast<uintptr_t>(items[i].src) & 3) ||
+        items[i].dst_off + items[i].bytes > Ctx::kPinnedBytes)
+      return SetError(PXG_INTERNAL, "small readback item %d: %u bytes at %u", i, items[i].bytes, items[i].dst_off);
+    c.src[i] = static_cast<const uint32_t*>(items[i].src);
+    c.dst_off[i] = items[i].dst_off;
+    c.words[i] = items[i].bytes / 4;
+  }
+  return LaunchOn(ctx, stream, "copy_to_host", SmallReadbackKernel, dim3(1), dim3(128), 0, c, static_cast<uint8_t*>(ctx->pinned));
+}
+
+struct ZeroSpec {
+  uint4* p[4];
+  uint64_t n16[4];  // 16-byte units
+  uint32_t* tail[4];
+  uint32_t tail_words[4];
+  int n;
+};
+__global__ void __launch_bounds__(256) ZeroRangesKernel(ZeroSpec z) {
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  for (int r = 0; r < z.n; ++r) {
+    for (uint64_t i = tid; i < z.n16[r]; i += stride) z.p[r][i] = zero;
+    if (tid < z.tail_words[r]) z.tail[r][tid] = 0;
+  }
+}
+
+int32_t ZeroRanges(Ctx* ctx, hipStream_t stream, void* const* ptrs, const size_t* bytes, int n) {
+  if (n <= 0) return PXG_OK;
+  if (n > 4) return SetError(PXG_INTERNAL, "%d zero ranges in one launch", n);
+  ZeroSpec z;
+  std::memset(&z, 0, sizeof(z));
+  z.n = n;
+  uint64_t most = 1;
+  for (int r = 0; r < n; ++r) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[r]);
+    if ((a & 3) || (bytes[r] & 3)) return SetError(PXG_INTERNAL, "zero range %d not 4-byte aligned", r);
+    // 16-byte body from the first 16-byte boundary; the 4-byte words before it and after it as tail.
+    const uintptr_t b16 = (a + 15) & ~uintptr_t(15);
+    const size_t head = std::min<size_t>(bytes[r], b16 - a);
+    const size_t body = ((bytes[r] - head) / 16) * 16;
+    z.p[r] = reinterpret_cast<uint4*>(b16);
+    z.n16[r] = body / 16;
+    // head and trailing words: at most 3 + 3 words, written as one tail list would need two
+    // ranges; instead a range with an unaligned head is zeroed word by word entirely.
+    if (head != 0) {
+      z.n16[r] = 0;
+      z.tail[r] = reinterpret_cast<uint32_t*>(a);
+      z.tail_words[r] = static_cast<uint32_t>(bytes[r] / 4);
+      if (bytes[r] / 4 > 256u * 1024u) return SetError(PXG_INTERNAL, "unaligned zero range of %zu bytes", bytes[r]);
+    } else {
+      z.tail[r] = reinterpret_cast<uint32_t*>(b16 + body);
+      z.tail_words[r] = static_cast<uint32_t>((bytes[r] - body) / 4);
+    }
+    most = std::max<uint64_t>(most, std::max<uint64_t>(z.n16[r], z.tail_words[r]));
+  }
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(2048, (most + 255) / 256));
+  return LaunchOn(ctx, stream, "zero_ranges", ZeroRangesKernel, dim3(std::max(1u, grid)), dim3(256), 0, z);
+}
+
 void ResultFree(void* p) {
   if (!p) return;
   {

@@ -1,6 +1,8 @@
 // Device-wide exclusive scan: reduce -> scan block sums (recursive) -> downsweep.
 #include "pxg_scan.h"
 
+#include <atomic>
+
 namespace pxg {
 
 template <typename T>
@@ -93,6 +95,87 @@ __global__ void __launch_bounds__(kScanBlock) ScanDownsweepKernel(const T* __res
   if (total && blockIdx.x == gridDim.x - 1 && t == kScanBlock - 1) *total = run;
 }
 
+// Single-pass exclusive scan of u32 values (decoupled look-back): one launch instead of the
+// reduce / spine / downsweep chain, whose ~5 us per launch dominated the small scans of a
+// finalize (dense ids, chunk counts, key lengths: 3 launches each).  Tile b publishes its sum
+// right after its block scan, then wave 0 walks back over the 64 preceding status words at a
+// time until it meets an inclusive prefix.  A status word is epoch(31) | inclusive(1) |
+// value(32); a word of another epoch reads as "not published yet".  Values are summed mod 2^32,
+// exactly as the multi-kernel scan does.  Tiles wait only on lower block ids, which are
+// dispatched first, so the spin always ends.  Status words are relaxed agent-scope atomics (the
+// value travels in the status word itself, so no other data needs ordering).
+constexpr uint64_t kLbInclBit = uint64_t(1) << 32;
+__global__ void __launch_bounds__(kScanBlock) ScanLookbackU32Kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int64_t n,
+                                                                    uint32_t* __restrict__ total, uint64_t* __restrict__ status,
+                                                                    uint64_t epoch_tag) {
+  constexpr int kPad = kScanItems + 1;
+  __shared__ uint32_t lds[kScanBlock / 64];
+  __shared__ uint32_t tile[kScanBlock * kPad];
+  __shared__ uint32_t s_excl;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  const int t = threadIdx.x, lane = t & 63;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * kScanBlock + t;
+    const int64_t i = base + j;
+    tile[j + j / kScanItems] = i < n ? in[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t vals[kScanItems];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    vals[k] = tile[t * kPad + k];
+    acc += vals[k];
+  }
+  uint32_t tot;
+  const uint32_t prefix = BlockExclusiveScan(acc, lds, &tot);
+  const uint32_t b = blockIdx.x;
+  if (t == 0) {
+    __hip_atomic_store(&status[b], epoch_tag | (b == 0 ? kLbInclBit : 0) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (b == 0) s_excl = 0;
+  }
+  if (b > 0 && t < 64) {
+    uint32_t excl = 0;
+    int64_t j = static_cast<int64_t>(b) - 1;
+    while (true) {
+      const int64_t idx = j - lane;
+      const uint64_t w = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (epoch_tag | kLbInclBit);
+      const bool ready = (w & ~((kLbInclBit << 1) - 1)) == epoch_tag;
+      const unsigned long long incl = __ballot(ready && (w & kLbInclBit));
+      const unsigned long long notready = __ballot(!ready);
+      const int fi = incl ? __ffsll(static_cast<long long>(incl)) - 1 : 64;
+      const unsigned long long need = fi == 64 ? ~0ULL : ((2ULL << fi) - 1);
+      if (notready & need) continue;  // a predecessor has not published: read the window again
+      uint32_t v = lane <= fi ? static_cast<uint32_t>(w) : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      excl += v;
+      if (fi < 64) break;
+      j -= 64;
+    }
+    if (lane == 0) {
+      __hip_atomic_store(&status[b], epoch_tag | kLbInclBit | static_cast<uint32_t>(excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = excl;
+    }
+  }
+  __syncthreads();
+  uint32_t run = prefix + s_excl;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    tile[t * kPad + k] = run;
+    run += vals[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int j = k * kScanBlock + t;
+    const int64_t i = base + j;
+    if (i < n) out[i] = tile[j + j / kScanItems];
+  }
+  if (total && b == gridDim.x - 1 && t == kScanBlock - 1) *total = run;
+}
+
 size_t ScanScratchBytes(int64_t n) {
   size_t bytes = 0;
   int64_t m = n;
@@ -126,13 +209,31 @@ static int32_t ScanImpl(Ctx* ctx, hipStream_t stream, const T* in, T* out, int64
 int32_t ScanExclusiveU64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, void* scratch) {
   return ScanImpl<uint64_t>(ctx, ctx->stream, in, out, n, total, static_cast<uint8_t*>(scratch));
 }
+// u32 scans of more than one tile take the single-pass look-back kernel (its status words live
+// in the caller's scratch: ScanScratchBytes(n) >= 8 bytes per tile).
+static int32_t ScanU32(Ctx* ctx, hipStream_t stream, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch) {
+  const int64_t nblocks = (n + kScanTile - 1) / kScanTile;
+  if (n <= 0 || nblocks == 1 || nblocks >= (int64_t(1) << 31) || EnvFlag("PXG_SCAN_3PASS"))
+    return ScanImpl<uint32_t>(ctx, stream, in, out, n, total, static_cast<uint8_t*>(scratch));
+  // The epoch is process-wide, not per context: a scratch buffer freed by one context and
+  // reallocated to another still holds the first one's status words (a per-context counter let a
+  // new context's first scans read them as published).  Fresh device memory is zeroed, and 0 is
+  // never an epoch.
+  static std::atomic<uint32_t> g_epoch{0};
+  uint32_t ep = (g_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0x7FFFFFFFu;
+  if (ep == 0) ep = (g_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0x7FFFFFFFu;
+  const uint64_t tag = static_cast<uint64_t>(ep) << 33;
+  return LaunchOn(ctx, stream, "scan_lookback", ScanLookbackU32Kernel, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock), 0, in, out,
+                  n, total, static_cast<uint64_t*>(scratch), tag);
+}
+
 int32_t ScanExclusiveU32(Ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch) {
-  return ScanImpl<uint32_t>(ctx, ctx->stream, in, out, n, total, static_cast<uint8_t*>(scratch));
+  return ScanU32(ctx, ctx->stream, in, out, n, total, scratch);
 }
 
 int32_t ScanExclusiveU32On(Ctx* ctx, hipStream_t stream, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total,
                            void* scratch) {
-  return ScanImpl<uint32_t>(ctx, stream, in, out, n, total, static_cast<uint8_t*>(scratch));
+  return ScanU32(ctx, stream, in, out, n, total, scratch);
 }
 
 }  // namespace pxg
