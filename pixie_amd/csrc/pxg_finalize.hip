@@ -211,7 +211,9 @@ __global__ void __launch_bounds__(256) ChunkReduceThreadKernel(const AggPlanDev*
 // One thread per group combines its chunk partials in order; a group of more than
 // kCombineWaveChunks chunks is combined by its whole wave instead (lane i takes chunks i, i + 64,
 // ..., then a fixed shuffle tree), so the largest groups (3400 chunks at 1B rows) are not one
-// thread's chain of dependent loads (0.41 ms at 1B rows).
+// thread's chain of dependent loads (0.41 ms at 1B rows).  (Round 6: one wave for every group
+// took group_combine 0.165 -> 0.078 ms at 1B rows, but the digests beside it slowed by more:
+// N1 step 14.60 vs 14.56 ms, C2 2.123 -> 2.140 ms.)
 constexpr uint32_t kCombineWaveChunks = 32;
 
 template <bool WAVE>

@@ -33,11 +33,22 @@ def main():
     keys = sorted({k for _, e in variants for k in e})
     res = {label: [] for label, _ in variants}
     groups = {}
+    kern_names = [k for k in os.environ.get("STEP_AB_KERNELS", "").split(",") if k]
+    kern = {}
     for r in range(rounds):
         for label, env in variants:
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)
+            if kern_names and r == 0:  # one event-bracketed step per variant, untimed
+                ctx.reset_stats()
+                ctx.set_profiling(True)
+                a.reset()
+                a.consume(t)
+                a.finalize()
+                ctx.sync()
+                ctx.set_profiling(False)
+                kern[label] = {k: round(ctx.kernel_stats(k)[1], 4) for k in kern_names}
             for i in range(3):
                 ctx.sync()
                 t0 = time.perf_counter()
@@ -50,7 +61,8 @@ def main():
             groups[label] = g
         print(f"round {r}: " + " ".join(f"{lb} {statistics.median(v):.3f}" for lb, v in res.items()), flush=True)
     for label, v in res.items():
-        print(f"{label}: median {statistics.median(v):.3f} ms min {min(v):.3f} ms over {len(v)} steps, groups {groups[label]}", flush=True)
+        print(f"{label}: median {statistics.median(v):.3f} ms min {min(v):.3f} ms over {len(v)} steps, groups {groups[label]}"
+              + (f", kernels {kern.get(label)}" if kern_names else ""), flush=True)
     a.close()
     t.close()
     ctx.close()
