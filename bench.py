@@ -77,6 +77,7 @@ def parse():
                     help="rehearsal only: every rank uses cuda:0 (a 1-GPU box; pair it with --backend gloo, since RCCL "
                          "refuses two ranks on one GPU)")
     ap.add_argument("--standin", action="store_true", help=argparse.SUPPRESS)  # tests only: N>1 protocol on CPU
+    ap.add_argument("--standin-hang-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests only: that rank never returns
     ap.add_argument("--pmc-file",default=os.path.join(REPO, "profiles", "pmc_agg_consume.json"),
                     help="committed PMC summary used for roofline.traffic only when the live PMC leg cannot run")
     ap.add_argument("--no-pmc", action="store_true",
@@ -626,6 +627,9 @@ def multi_main(args, rank, world, local_rank):
             sys.path.insert(0, os.path.join(REPO, "tests"))
             from bench_standin import StandinRank
             runner = StandinRank(args, rank, world, SEED, N_PAIR_KEYS)
+            if rank == args.standin_hang_rank:  # TEST ONLY: a rank stuck before the first collective
+                while True:
+                    time.sleep(1)
         else:
             runner = DeviceRank(args, rank, world, local_rank)
         n = runner.n

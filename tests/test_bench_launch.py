@@ -50,3 +50,17 @@ def test_bench_refuses_world_size_that_disagrees_with_gpus():
     assert r.returncode == 2
     assert "refusing" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_launcher_kills_ranks_after_rank_timeout():
+    """a rank stuck in a collective must not hang `bench.py --gpus N` forever; after
+    --rank-timeout the launcher kills every rank's process group and exits non-zero."""
+    import time
+    t0 = time.time()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--backend", "gloo", "--standin", "--steps", "1", "--warmup", "0",
+                        "--rows-per-gpu", "20000", "--standin-hang-rank", "1", "--rank-timeout", "20"],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "rank-timeout" in r.stderr
+    assert r.stdout.strip() == ""
+    assert time.time() - t0 < 200

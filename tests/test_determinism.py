@@ -143,3 +143,36 @@ def test_float_sums_keep_inf_and_nan(ctx):
 
 
 QS_ALL = [0.01, 0.10, 0.25, 0.50, 0.75, 0.90, 0.99]
+
+
+def test_float_sums_beyond_the_double_double_range_stay_within_the_bar(ctx):
+    """double-double keeps ~106 bits, so values spanning more than ~2^100 in
+    magnitude (here 1e-150 .. 1e150, with cancellation) may round differently from the exact sum
+    and from run to run.  Recorded behaviour: the sums and means stay within the 1e-6 relative
+    parity bar of the exactly rounded sum (math.fsum); bit-exactness is only claimed inside the
+    range (test_float_sum_and_mean_equal_the_exact_sum)."""
+    rng = np.random.default_rng(17)
+    n = 200_000
+    keys = rng.integers(0, 50, n)
+    vals = rng.standard_normal(n) * np.power(10.0, rng.integers(-150, 151, n).astype(np.float64))
+    plan = P.linear_plan([P.source_op("t", [2, 4], ["k", "v"], [0, 1]),
+                          P.agg_op([0], [P.agg_expr("sum", [P.col(1)], [4]), P.agg_expr("mean", [P.col(1)], [4], fid=1)]),
+                          P.sink_op("out")])
+    q = LinearQuery(plan, [2, 4])
+    t = Table(ctx, [2, 4])
+    t.append([Column(2, values=keys.astype(np.int64)), Column(4, values=vals)])
+    a = q.make_agg(ctx)
+    a.consume(t)
+    a.finalize()
+    r = a.result()
+    exact_hits = 0
+    for g, k in enumerate(np.asarray(r[0].values)):
+        sel = vals[keys == k]
+        exact = math.fsum(sel.tolist())
+        s, m = float(np.asarray(r[1].values)[g]), float(np.asarray(r[2].values)[g])
+        assert abs(s - exact) <= 1e-6 * abs(exact), (k, s, exact)
+        assert abs(m - exact / len(sel)) <= 1e-6 * abs(exact / len(sel)), (k, m)
+        exact_hits += s == exact
+    print(f"groups whose sum equals the exactly rounded sum: {exact_hits} of {len(r[0])}")
+    a.close()
+    t.close()
