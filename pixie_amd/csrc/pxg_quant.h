@@ -86,6 +86,11 @@ __device__ __forceinline__ void SortNetwork16(uint64_t (&r)[kMsIpt]) {
   }
 }
 
+// (Round 6: sorting each wave's runs of up to 1024 keys in registers first -- a bitonic network
+// with the lane-crossing steps as shuffles, replacing the first six merge rounds -- passed the
+// digest parity tests but measured no faster: C2 step 2.055 / 2.093 vs 2.047 / 2.111 ms, N1
+// 14.71 / 14.69 vs 14.50 / 14.63 ms, quant_mid 0.21 ms either way at C2.  The mid / small digests
+// are not bound by these merge rounds.)
 // Sorts a[0, P) (logical indices, PadIdx layout), P a power of two in [16, 16 * nthreads],
 // by the nthreads threads t = 0.. of a workgroup (kWave = false: block barriers) or of one wave
 // (kWave = true: wave-local LDS ordering only).
