@@ -1165,6 +1165,11 @@ __global__ void XLayoutDevKernel(const uint64_t* __restrict__ bounds, int32_t n_
 }
 
 int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, uint8_t* hdr_dev) {
+  // Tests only (tests/test_comm_gpu.py): PXG_TEST_EXPORT_FAIL=host fails this rank's export before
+  // anything is issued, =device makes the device layout refuse it (a forced group-count mismatch).
+  const char* inject = std::getenv("PXG_TEST_EXPORT_FAIL");
+  if (inject && std::strcmp(inject, "host") == 0) return SetError(PXG_INTERNAL, "export failure injected (PXG_TEST_EXPORT_FAIL=host)");
+  const bool inject_dev = inject && std::strcmp(inject, "device") == 0;
   if (merged) return SetError(PXG_FAILED_PRECONDITION, "an aggregation that merged imported states cannot be exported again");
   if (n_parts < 1 || n_parts > kPartBuckets) return SetError(PXG_INVALID_ARGUMENT, "%d parts", n_parts);
   ExportCache& X = xc;
@@ -1186,8 +1191,8 @@ int32_t Agg::ExportPartialDev(int32_t n_parts, DevBuf* send, int64_t* seg_dev, u
   hc.srec = srec;
   hc.plan_sig = XPlanSig(*this);
   hc.has_q = has_q ? 1 : 0;
-  hc.check = x_check_pending ? 1 : 0;
-  hc.check_groups = x_check_groups;
+  hc.check = x_check_pending || inject_dev ? 1 : 0;
+  hc.check_groups = x_check_groups + (inject_dev ? 1u : 0u);
   hc.cap = send->bytes;
   PXG_RETURN_IF_ERROR(Launch(ctx, "export_layout", XLayoutDevKernel, dim3(1), dim3(64), 0,
                              X.starts.as<const uint64_t>() + kPartBuckets + 1, n_parts, hc, ws.meta.as<const uint8_t>(), send->as<uint8_t>(),

@@ -308,3 +308,73 @@ def test_device_export_layout_matches_host_layout(ctx, plan_name):
 def _seg(offs, nb):
     from pixie_amd.dist import segments
     return segments(offs, nb)
+
+
+_FAIL_RANK = textwrap.dedent('''
+    import json, os, sys
+    sys.path.insert(0, {repo!r})
+    import torch
+    import torch.distributed as dist
+    from datetime import timedelta
+    from pixie_amd import plans as P
+    from pixie_amd._lib import PxgError
+    from pixie_amd.device import Ctx, Table
+    from pixie_amd.dist import exchange_partials, close_host_comms
+    from pixie_amd.pipeline import LinearQuery
+    rank, world, kind, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    ctx = Ctx(0)
+    t = Table(ctx, P.HTTP_TYPES)
+    t.append_http_events({seed}, rank * 200_000, 200_000, 10_000_000)
+    a = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536).make_agg(ctx)
+    a.consume(t)
+    if rank == world - 1:
+        os.environ["PXG_TEST_EXPORT_FAIL"] = kind
+    res = {{"rank": rank}}
+    try:
+        exchange_partials(a)
+        res["error"] = None
+    except PxgError as e:
+        res["error"] = str(e)
+    os.environ.pop("PXG_TEST_EXPORT_FAIL", None)
+    # the communicator is still usable afterwards: a clean exchange of the same state
+    a.reset()
+    a.consume(t)
+    sent, recv = exchange_partials(a)
+    res["after"] = [sent, recv]
+    json.dump(res, open(out, "w"))
+    dist.barrier()
+    close_host_comms()
+    dist.destroy_process_group()
+''')
+
+
+@pytest.mark.parametrize("kind", ["host", "device"])
+def test_failed_export_fails_every_rank_without_a_hang(tmp_path, kind):
+    """ADVICE r05 (medium): a rank whose export fails -- on the host before anything is issued,
+    or in the device layout (finalize checks / send-buffer bound) -- announces -1 bytes in the
+    {bytes, header} exchange; then no rank posts the part exchange and every rank returns an
+    error (the peers name the failed rank) instead of waiting.  The same communicator then runs
+    a clean exchange."""
+    world = 3
+    script = tmp_path / "fail_rank.py"
+    script.write_text(_FAIL_RANK.format(repo=REPO, seed=SEED))
+    env = dict(os.environ, **_ENV, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(31000 + (os.getpid() % 1000) + (5 if kind == "device" else 0)))
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), str(world), kind, str(tmp_path / f"f{r}.json")], env=env)
+             for r in range(world)]
+    import time
+    deadline = time.time() + 150
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=max(1.0, deadline - time.time())))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("a rank hung after an export failure")
+    assert codes == [0] * world
+    res = [json.load(open(tmp_path / f"f{r}.json")) for r in range(world)]
+    assert all(x["error"] for x in res), res
+    for x in res[:-1]:
+        assert f"rank {world - 1} failed its export" in x["error"], x
+    assert all(x["after"][0] > 0 and x["after"][1] > 0 for x in res)
