@@ -167,6 +167,10 @@ struct Ctx {
   // Finalize: t-digest boundary chains of every mid-class group size (a pure function of the
   // size; pxg_finalize.hip EnsureMidChains), built on first use.
   DevBuf mid_chains;
+  // Tile status words of the single-pass look-back scans (pxg_scan.hip), one array per stream
+  // (main, side, side 2), zeroed when allocated: a word left by another process in recycled
+  // device memory must never carry a live epoch.
+  DevBuf scan_status[3];
 
   hipEvent_t GetEvent();
   int32_t ResolveTimings();

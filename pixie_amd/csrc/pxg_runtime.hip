@@ -223,6 +223,9 @@ int32_t Table::AppendRows(const pxg_column_view* cols, int64_t n, hipMemcpyKind 
         PXG_RETURN_IF_ERROR(ReadDeviceI32(ctx, off + done + take, &o_last));
       }
       const int64_t bytes = static_cast<int64_t>(o_last) - o_first;
+      if (o_first < 0 || bytes < 0)
+        return SetError(PXG_INVALID_ARGUMENT, "column %d: string offsets %d (row %lld) .. %d (row %lld) are not monotone", k, o_first,
+                        static_cast<long long>(done), o_last, static_cast<long long>(done + take));
       if (cc.offsets.bytes < static_cast<size_t>(r1 + 1) * 4 + 16)
         PXG_RETURN_IF_ERROR(cc.offsets.ReserveExact(static_cast<size_t>(cap_rows + 1) * 4 + 16, static_cast<size_t>(r0 + 1) * 4, ctx->stream));
       const size_t need = static_cast<size_t>(cc.data_len + bytes) + 16;

@@ -209,22 +209,39 @@ static int32_t ScanImpl(Ctx* ctx, hipStream_t stream, const T* in, T* out, int64
 int32_t ScanExclusiveU64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, void* scratch) {
   return ScanImpl<uint64_t>(ctx, ctx->stream, in, out, n, total, static_cast<uint8_t*>(scratch));
 }
-// u32 scans of more than one tile take the single-pass look-back kernel (its status words live
-// in the caller's scratch: ScanScratchBytes(n) >= 8 bytes per tile).
+// u32 scans of more than one tile take the single-pass look-back kernel.  Its status words live
+// in the context's per-stream array (Ctx::scan_status), zeroed once when it is allocated, and
+// carry a process-wide epoch that every scan advances.  So a word the kernel reads is either
+// this scan's, an older scan's of this process (an older epoch: "not published"), or zero.
+// Status words in the caller's scratch were not safe: device memory freed by another process
+// (the GPU tests' rank processes) comes back with that process's words, whose epochs count from
+// 1 as ours do, and a tile that read one as its predecessor's prefix got a wrong offset
+// (a datagen append with non-monotone string offsets, 12 groups lost by a sharded C2 run).
+constexpr int64_t kLbMaxTiles = 65536;  // 256M elements; larger scans keep the three-kernel path
+static uint64_t* LbStatus(Ctx* ctx, hipStream_t stream) {
+  const int i = stream == ctx->stream ? 0 : stream == ctx->side ? 1 : stream == ctx->side2 ? 2 : -1;
+  if (i < 0) return nullptr;
+  DevBuf& b = ctx->scan_status[i];
+  if (!b.p) {
+    if (b.Alloc(static_cast<size_t>(kLbMaxTiles) * 8) != PXG_OK) return nullptr;
+    if (hipMemsetAsync(b.p, 0, b.bytes, stream) != hipSuccess) {  // ordered before every scan of this stream
+      b.Free();
+      return nullptr;
+    }
+  }
+  return b.as<uint64_t>();
+}
+
 static int32_t ScanU32(Ctx* ctx, hipStream_t stream, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch) {
   const int64_t nblocks = (n + kScanTile - 1) / kScanTile;
-  if (n <= 0 || nblocks == 1 || nblocks >= (int64_t(1) << 31) || EnvFlag("PXG_SCAN_3PASS"))
-    return ScanImpl<uint32_t>(ctx, stream, in, out, n, total, static_cast<uint8_t*>(scratch));
-  // The epoch is process-wide, not per context: a scratch buffer freed by one context and
-  // reallocated to another still holds the first one's status words (a per-context counter let a
-  // new context's first scans read them as published).  Fresh device memory is zeroed, and 0 is
-  // never an epoch.
+  uint64_t* status = n > 0 && nblocks > 1 && nblocks <= kLbMaxTiles && !EnvFlag("PXG_SCAN_3PASS") ? LbStatus(ctx, stream) : nullptr;
+  if (!status) return ScanImpl<uint32_t>(ctx, stream, in, out, n, total, static_cast<uint8_t*>(scratch));
   static std::atomic<uint32_t> g_epoch{0};
   uint32_t ep = (g_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0x7FFFFFFFu;
   if (ep == 0) ep = (g_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0x7FFFFFFFu;
   const uint64_t tag = static_cast<uint64_t>(ep) << 33;
   return LaunchOn(ctx, stream, "scan_lookback", ScanLookbackU32Kernel, dim3(static_cast<unsigned>(nblocks)), dim3(kScanBlock), 0, in, out,
-                  n, total, static_cast<uint64_t*>(scratch), tag);
+                  n, total, status, tag);
 }
 
 int32_t ScanExclusiveU32(Ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, void* scratch) {

@@ -136,17 +136,22 @@ _RANK = textwrap.dedent('''
     from pixie_amd.dist import exchange_partials, gather_device_results, close_host_comms
     from pixie_amd.pipeline import LinearQuery
     rank, world, n, mode, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
+    plan_name = sys.argv[6] if len(sys.argv) > 6 else "c2"
+    if plan_name == "c3":
+        os.environ["PXG_HC_MIN_GROUPS"] = "1"  # the high-cardinality path: partition groups exported as states
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world, timeout=timedelta(seconds=90))
     ctx = Ctx(0)
     t = Table(ctx, P.HTTP_TYPES)
-    t.append_http_events({seed}, rank * n, n, 10_000_000)
-    q = LinearQuery(P.c2_plan(with_pluck=False), P.HTTP_TYPES, expected_groups=65536)
+    t.append_http_events({seed}, rank * n, n, 300_000 if plan_name == "c3" else 10_000_000)
+    plan = P.c3_plan() if plan_name == "c3" else P.c2_plan(with_pluck=False)
+    q = LinearQuery(plan, P.HTTP_TYPES, expected_groups=100_000 if plan_name == "c3" else 65536)
     a = q.make_agg(ctx)
     reps = 2 if mode == "gloo" else 1
     for rep in range(reps):  # the bench's step twice: the host communicator and buffers are reused
         a.reset()
         a.consume(t)
         selected = a.rows_selected()
+        hc = a.info()["hc_mode"]  # the consume's mode (the exchange resets and imports)
         via = "host-comm"
         if mode == "rccl":
             obj = [Comm.unique_id() if rank == 0 else None]
@@ -174,19 +179,20 @@ _RANK = textwrap.dedent('''
                 arrs[f"{{f}}{{j}}"] = np.asarray(getattr(c, f))
     np.savez(out + ".npz", **arrs)
     json.dump({{"via": via, "sent": sent, "recv": recv, "ncols": len(cols), "owned": owned, "gathered": gathered,
-               "selected": selected}}, open(out, "w"))
+               "selected": selected, "hc": hc}}, open(out, "w"))
     dist.barrier()
     close_host_comms()
     dist.destroy_process_group()
 ''')
 
 
-def _run_ranks(tmp_path, mode, world, n):
+def _run_ranks(tmp_path, mode, world, n, plan_name="c2"):
     script = tmp_path / "rank.py"
     script.write_text(_RANK.format(repo=REPO, seed=SEED))
     env = dict(os.environ, **_ENV, MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(29500 + (os.getpid() % 1000) + (7 if mode == "rccl" else 0) + 13 * world))
-    procs = [subprocess.Popen([sys.executable, str(script), str(r), str(world), str(n), mode, str(tmp_path / f"r{r}.json")], env=env)
+               MASTER_PORT=str(29500 + (os.getpid() % 1000) + (7 if mode == "rccl" else 0) + 13 * world + (3 if plan_name == "c3" else 0)))
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), str(world), str(n), mode, str(tmp_path / f"r{r}.json"), plan_name],
+                              env=env)
              for r in range(world)]
     import time
     deadline = time.time() + 150
@@ -239,6 +245,22 @@ def test_host_comm_alltoall_and_gather_match_oracle(tmp_path, world):
     assert sum(x["sent"] for x in res) == sum(x["recv"] for x in res)
     for x in res:
         assert x["sent"] > 0 and x["recv"] > 0
+
+
+def test_host_comm_high_cardinality_matches_oracle(tmp_path):
+    """The C3 shape (high-cardinality mode: the partition pass's groups exported as states,
+    ExportHcGroups) through pxg_agg_alltoall + pxg_agg_gather at world 2 over the host
+    communicator, against the oracle over both shards: keys, counts and sums exact, means 1e-6."""
+    world, n = 2, 400_000
+    res = _run_ranks(tmp_path, "gloo", world, n, plan_name="c3")
+    assert all(x["via"] == "host-comm" and x["hc"] == 1 for x in res)
+    dev = _load_cols(tmp_path, 0, res[0]["ncols"])
+    cols = datagen_http_events(SEED, 0, world * n, n_pair_keys=300_000, threads=8)
+    tables = {"http_events": {"types": P.HTTP_TYPES, "batches": [cols], "names": P.HTTP_NAMES}}
+    ref = oc.execute_plan(P.c3_plan(), tables)["output"][0]["cols"]
+    rep = parity.compare_agg(dev, ref, 2, ["count", "rel", "exact"])
+    assert rep["ok"], rep
+    assert res[0]["gathered"] == sum(x["owned"] for x in res) == rep["groups_ref"]
 
 
 def test_two_processes_share_gpu0_rccl_or_skip(tmp_path):
