@@ -636,6 +636,9 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   const int nv = plan->n_vals;
   if (threadIdx.x == 0) s_ins = 0;
   const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
+  int64_t flo = 0, fhi = 0;
+  bool fneg = false;
+  const bool frange = !PAIRS && plan->has_filter && FilterRange(&plan->filter, plan->col_types[plan->filter.col], &flo, &fhi, &fneg);
   for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
   __syncthreads();
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
@@ -700,11 +703,29 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
         }
       } else {
         bool pass[kPer];
+        if (frange) {
+          // An integer range filter: the kPer loads (clamped rows) all issued before the first
+          // compare.  The generic loop below dispatches on the shape per row and waits for each
+          // load before the next.
+          const int64_t* fv = reinterpret_cast<const int64_t*>(ch.cols[plan->filter.col].values);
+          int64_t v[kPer];
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-          const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
-          pass[k] = r < row1;
-          if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
+          for (int k = 0; k < kPer; ++k) {
+            const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
+            v[k] = fv[r < row1 ? r : row1 - 1];
+          }
+#pragma unroll
+          for (int k = 0; k < kPer; ++k) {
+            const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
+            pass[k] = r < row1 && ((v[k] >= flo && v[k] <= fhi) != fneg);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < kPer; ++k) {
+            const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
+            pass[k] = r < row1;
+            if (pass[k] && plan->has_filter) pass[k] = EvalShape(&plan->filter, ch, r, plan->col_types) != 0;
+          }
         }
         unsigned long long m[kPer];
 #pragma unroll

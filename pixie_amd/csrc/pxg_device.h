@@ -259,6 +259,32 @@ __device__ __forceinline__ uint64_t ApplyShape(const DevProgram* __restrict__ p,
   return BinOp(p->binop, x, static_cast<uint64_t>(p->cimm));
 }
 
+// A `col op const` integer comparison (no conversion) on an 8-byte signed column as a range test:
+// BinOp(op, x, c) == (lo <= x <= hi) != neg.  Lets a filter loop issue all its loads before any
+// compare, with no per-row dispatch on the op.
+__device__ __forceinline__ bool FilterRange(const DevProgram* __restrict__ p, int col_type, int64_t* lo, int64_t* hi, bool* neg) {
+  if (p->shape != kShapeColOpConst || p->conv != 0 || (col_type != PXG_INT64 && col_type != PXG_TIME64NS)) return false;
+  const int64_t c = p->cimm;
+  *lo = INT64_MIN;
+  *hi = INT64_MAX;
+  *neg = false;
+  switch (p->binop) {
+    case PXG_OP_EQ_I: *lo = c; *hi = c; return true;
+    case PXG_OP_NE_I: *lo = c; *hi = c; *neg = true; return true;
+    case PXG_OP_GE_I: *lo = c; return true;
+    case PXG_OP_LE_I: *hi = c; return true;
+    case PXG_OP_GT_I:
+      if (c == INT64_MAX) *neg = true;  // empty: the full range negated
+      else *lo = c + 1;
+      return true;
+    case PXG_OP_LT_I:
+      if (c == INT64_MIN) *neg = true;
+      else *hi = c - 1;
+      return true;
+    default: return false;
+  }
+}
+
 // Whether rows of a fast shape's column can be read two at a time with 16-byte loads: an 8-byte
 // column whose values start 16-byte aligned (the pair loads then start at even rows).
 __device__ __forceinline__ bool PairLoadable(const DevProgram* __restrict__ p, const DevChunk& ch,
