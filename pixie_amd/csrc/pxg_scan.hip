@@ -39,12 +39,15 @@ template <typename T>
 __global__ void __launch_bounds__(kScanBlock) ScanReduceKernel(const T* __restrict__ in, int64_t n, T* __restrict__ sums) {
   __shared__ T lds[kScanBlock / 64];
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  T x[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {  // every load issued before the first use (clamped index)
+    const int64_t i = base + static_cast<int64_t>(k) * kScanBlock + threadIdx.x;
+    x[k] = in[i < n ? i : n - 1];
+  }
   T acc = 0;
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    int64_t i = base + static_cast<int64_t>(k) * kScanBlock + threadIdx.x;
-    if (i < n) acc += in[i];
-  }
+  for (int k = 0; k < kScanItems; ++k) acc += base + static_cast<int64_t>(k) * kScanBlock + threadIdx.x < n ? x[k] : T(0);
   T tot;
   (void)BlockExclusiveScan(acc, lds, &tot);
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
@@ -63,11 +66,20 @@ __global__ void __launch_bounds__(kScanBlock) ScanDownsweepKernel(const T* __res
   __shared__ T tile[kScanBlock * kPad];
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
   const int t = threadIdx.x;
+  {
+    // All loads in flight before the LDS writes: a guarded load per item compiled to a branch
+    // and a wait per item (16 serialised round trips per thread).
+    T x[kScanItems];
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    const int j = k * kScanBlock + t;
-    const int64_t i = base + j;
-    tile[j + j / kScanItems] = i < n ? in[i] : T(0);
+    for (int k = 0; k < kScanItems; ++k) {
+      const int64_t i = base + k * kScanBlock + t;
+      x[k] = in[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const int j = k * kScanBlock + t;
+      tile[j + j / kScanItems] = base + j < n ? x[k] : T(0);
+    }
   }
   __syncthreads();
   T vals[kScanItems];
@@ -114,11 +126,18 @@ __global__ void __launch_bounds__(kScanBlock) ScanLookbackU32Kernel(const uint32
   __shared__ uint32_t s_excl;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
   const int t = threadIdx.x, lane = t & 63;
+  {
+    uint32_t x[kScanItems];  // all loads in flight first (as in ScanDownsweepKernel)
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    const int j = k * kScanBlock + t;
-    const int64_t i = base + j;
-    tile[j + j / kScanItems] = i < n ? in[i] : 0u;
+    for (int k = 0; k < kScanItems; ++k) {
+      const int64_t i = base + k * kScanBlock + t;
+      x[k] = in[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const int j = k * kScanBlock + t;
+      tile[j + j / kScanItems] = base + j < n ? x[k] : 0u;
+    }
   }
   __syncthreads();
   uint32_t vals[kScanItems];
