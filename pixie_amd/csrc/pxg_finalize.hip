@@ -466,14 +466,23 @@ __global__ void __launch_bounds__(256) QuantSmallKernel(const uint32_t* __restri
   int P = 128;
   while (P < n) P <<= 1;
   uint64_t cv = 0, cneg = 0;
-  for (int i = lane; i < P; i += 64) {
-    uint64_t k = ~0ULL;
+  // The lane's loads (up to kSmallMax / 64) all issued before the first conversion: P / 64 is
+  // uniform, so the guards are scalar branches and no load waits for the one before it.
+  uint64_t raw[kSmallMax / 64];
+#pragma unroll
+  for (int k = 0; k < kSmallMax / 64; ++k)
+    if (k * 64 < P) raw[k] = vals[s + min(lane + 64 * k, n - 1)];
+#pragma unroll
+  for (int k = 0; k < kSmallMax / 64; ++k) {
+    if (k * 64 >= P) break;
+    const int i = lane + 64 * k;
+    uint64_t key = ~0ULL;
     if (i < n) {
-      k = QKey(vals[s + i], arg_type);
-      cv += (k >= kNegInfKey && k <= kPosInfKey) ? 1 : 0;
-      cneg += k < kNegInfKey ? 1 : 0;
+      key = QKey(raw[k], arg_type);
+      cv += (key >= kNegInfKey && key <= kPosInfKey) ? 1 : 0;
+      cneg += key < kNegInfKey ? 1 : 0;
     }
-    a[PadIdx(i)] = k;
+    a[PadIdx(i)] = key;
   }
   const int64_t W = static_cast<int64_t>(WaveSumU64(cv));
   const int64_t lead = static_cast<int64_t>(WaveSumU64(cneg));
@@ -544,7 +553,21 @@ __global__ void __launch_bounds__(kMaxN / kMsIpt) QuantMidKernel(const uint32_t*
   const uint32_t s = gstart[g], n = gstart[g + 1] - s;
   int P = 64;
   while (P < static_cast<int>(n)) P <<= 1;
-  for (int i = threadIdx.x; i < P; i += blockDim.x) keys[PadIdx(i)] = i < static_cast<int>(n) ? QKey(vals[s + i], arg_type) : ~0ULL;
+  {
+    // All kMsIpt loads of a thread in flight before the first conversion (clamped rows: n >= 1);
+    // a guarded load per loop step waited for each value before issuing the next.
+    uint64_t raw[kMsIpt];
+#pragma unroll
+    for (int k = 0; k < kMsIpt; ++k) {
+      const int i = threadIdx.x + k * (kMaxN / kMsIpt);
+      raw[k] = vals[s + min(i, static_cast<int>(n) - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < kMsIpt; ++k) {
+      const int i = threadIdx.x + k * (kMaxN / kMsIpt);
+      if (i < P) keys[PadIdx(i)] = i < static_cast<int>(n) ? QKey(raw[k], arg_type) : ~0ULL;
+    }
+  }
   __syncthreads();
   BlockMergeSortLds(keys, P);
   BlockDigest<true>([&](int64_t i) -> uint64_t { return keys[PadIdx(static_cast<int>(i))]; }, n, starts, kMidCentroids,

@@ -243,7 +243,10 @@ __global__ void __launch_bounds__(kRsScanBlock) RsScanKernel(uint32_t* __restric
 // store per item.  The first value stream is loaded up front so its latency overlaps the
 // ranking.  (Round 6: loading stream v + 1 into the same registers right after stream v went to
 // LDS, ahead of stream v's run writes, made the 9-stream partition sort slower: C3 without the
-// filter, radix_scatter 7.0 -> 8.1 ms.)
+// filter, radix_scatter 7.0 -> 8.1 ms.  The guarded per-item loads of streams 1.. compile to one
+// load and one wait per item; issuing a stream's 12 loads together (clamped rows) was slower
+// too: C3 without the filter 7.14 -> 8.58 ms, 1B rows' fused split 1.07 -> 1.16 ms,
+// profiles/r06_ab_loads.log.)
 __global__ void __launch_bounds__(kRadixBlock) RsScatterKernel(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
                                                                ConstValPtrs vin, ValPtrs vout, int nvals, uint64_t n, int shift,
                                                                const uint32_t* __restrict__ offs, uint32_t ntiles) {

@@ -1,11 +1,12 @@
+# Library A/B on the GPU box: ab_alt/libpxg_base.so (the committed build) against the working
+# build, alternating processes (tools/lib_ab.py), then the consume / finalize parity subset.
 set -o pipefail
 mkdir -p gpurun_out
-for i in 1 2 3; do
-  PXG_LIB_PATH=$PWD/ab_alt/libpxg_base.so timeout -k 10 120 python3 tools/lib_ab.py base 100000000 20 >> gpurun_out/prevals_ab.log 2>&1 || exit 1
-  timeout -k 10 120 python3 tools/lib_ab.py prevals 100000000 20 >> gpurun_out/prevals_ab.log 2>&1 || exit 1
+L=gpurun_out/lib_ab.log
+for spec in "100000000 20 c2" "1000000000 5 c2"; do
+  for i in 1 2 3; do
+    PXG_LIB_PATH=$PWD/ab_alt/libpxg_base.so timeout -k 10 200 python3 tools/lib_ab.py base $spec >> $L 2>&1 || exit 1
+    timeout -k 10 200 python3 tools/lib_ab.py new $spec >> $L 2>&1 || exit 1
+  done
 done
-for i in 1 2; do
-  PXG_LIB_PATH=$PWD/ab_alt/libpxg_base.so timeout -k 10 180 python3 tools/lib_ab.py base 1000000000 5 >> gpurun_out/prevals_ab.log 2>&1 || exit 1
-  timeout -k 10 180 python3 tools/lib_ab.py prevals 1000000000 5 >> gpurun_out/prevals_ab.log 2>&1 || exit 1
-done
-timeout -k 10 400 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_parity.py tests/test_row_records.py tests/test_n1_parity.py tests/test_hc_agg.py tests/test_consume_tiles.py -m gpu > gpurun_out/prevals_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_parity.py tests/test_n1_parity.py tests/test_big_select.py tests/test_determinism.py tests/test_fsplit.py -m gpu > gpurun_out/lib_ab_tests.log 2>&1
