@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
   const uint32_t n_lds_chunks = min(nchunks, static_cast<uint32_t>(kLdsChunks));
   int64_t flo = 0, fhi = 0;
   bool fneg = false;
-  const bool frange = !PAIRS && plan->has_filter && FilterRange(&plan->filter, plan->col_types[plan->filter.col], &flo, &fhi, &fneg);
+  const bool frange = !PAIRS && !HC && plan->has_filter && FilterRange(&plan->filter, plan->col_types[plan->filter.col], &flo, &fhi, &fneg);
   for (uint32_t c = threadIdx.x; c < n_lds_chunks; c += kConsumeBlock) s_kc[c] = KeyColsOf<NK, S>(plan, chunks[c]);
   __syncthreads();
   for (int64_t t = bid; t < ntiles; t += gridDim.x) {
@@ -708,16 +708,20 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
           // compare.  The generic loop below dispatches on the shape per row and waits for each
           // load before the next.
           const int64_t* fv = reinterpret_cast<const int64_t*>(ch.cols[plan->filter.col].values);
-          int64_t v[kPer];
+          constexpr int kFB = kPer / 2;
 #pragma unroll
-          for (int k = 0; k < kPer; ++k) {
-            const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
-            v[k] = fv[r < row1 ? r : row1 - 1];
-          }
+          for (int h = 0; h < kPer; h += kFB) {
+            int64_t v[kFB];
 #pragma unroll
-          for (int k = 0; k < kPer; ++k) {
-            const int64_t r = sb0 + k * kConsumeBlock + threadIdx.x;
-            pass[k] = r < row1 && ((v[k] >= flo && v[k] <= fhi) != fneg);
+            for (int k = 0; k < kFB; ++k) {
+              const int64_t r = sb0 + (h + k) * kConsumeBlock + threadIdx.x;
+              v[k] = fv[r < row1 ? r : row1 - 1];
+            }
+#pragma unroll
+            for (int k = 0; k < kFB; ++k) {
+              const int64_t r = sb0 + (h + k) * kConsumeBlock + threadIdx.x;
+              pass[h + k] = r < row1 && ((v[k] >= flo && v[k] <= fhi) != fneg);
+            }
           }
         } else {
 #pragma unroll
