@@ -40,7 +40,10 @@ __device__ __forceinline__ uint32_t DenseKey(uint32_t k, const uint32_t* __restr
 // tile, ~10M scattered writes per pass at 1B rows).  With a rank map (first pass) the dense keys are also written out, so the first scatter reads
 // them instead of gathering again.
 // A workgroup counts kHistTiles consecutive tiles: all their keys (and, in the first pass, their
-// rank gathers) are in flight at once, then each tile's counts are taken in turn.  Four tiles
+// rank gathers) are in flight at once, then each tile's counts are taken in turn.  (Until round 6
+// the gathers were guarded and compiled to one wait each; unconditional: 1B rows' fused-split
+// histogram 0.45-0.47 -> 0.41-0.42 ms, C2's first histogram 0.057-0.063 -> 0.046-0.048 ms,
+// profiles/r06_ab_rank_gathers.log.)  Four tiles
 // per workgroup at >= 16K tiles (1B rows: the rank-gathering pass 0.59 -> 0.51 ms); one below,
 // where four would leave too few workgroups (C2: 0.057 -> 0.085 ms).
 template <int kHistTiles>
@@ -66,12 +69,15 @@ __global__ void __launch_bounds__(kRadixBlock) RsHistKernel(const uint32_t* __re
       kk[j][k] = i < rem ? kp[i] : 0u;
     }
   if (rank) {
+    // The rank gathers unconditional (clamped slot), so all of them are in flight together: a
+    // guarded gather compiled to a branch and a wait per item.
 #pragma unroll
     for (int j = 0; j < kHistTiles; ++j)
 #pragma unroll
       for (int k = 0; k < kRadixItems; ++k) {
-        const uint32_t i = j * kRadixTile + k * kRadixBlock + threadIdx.x;
-        if (i < rem) kk[j][k] = DenseKey(kk[j][k], rank, cap, G);
+        const bool ok = kk[j][k] < cap;
+        const uint32_t g = rank[ok ? kk[j][k] : 0u];
+        kk[j][k] = ok ? g : G;
       }
     uint32_t* dp = dense_out + base;
 #pragma unroll
@@ -615,15 +621,22 @@ __global__ void __launch_bounds__(kFsBlock) FsHistKernel(const uint32_t* __restr
       const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
       kk[j][k] = i < rem ? kp[i] : 0u;
     }
+  // Every id gather issued before the first store (clamped slot, as in RsHistKernel): a guarded
+  // gather followed by its store compiled to a wait per item.
+#pragma unroll
+  for (int j = 0; j < kHistTiles; ++j)
+#pragma unroll
+    for (int k = 0; k < kFsItems; ++k) {
+      const bool ok = kk[j][k] < cap;
+      const uint32_t g = newid[ok ? kk[j][k] : 0u];
+      kk[j][k] = ok ? g : G;
+    }
 #pragma unroll
   for (int j = 0; j < kHistTiles; ++j)
 #pragma unroll
     for (int k = 0; k < kFsItems; ++k) {
       const uint32_t i = j * kFsTile + k * kFsBlock + threadIdx.x;
-      if (i < rem) {
-        kk[j][k] = kk[j][k] < cap ? newid[kk[j][k]] : G;
-        dense_out[base + i] = kk[j][k];
-      }
+      if (i < rem) dense_out[base + i] = kk[j][k];
     }
 #pragma unroll
   for (int j = 0; j < kHistTiles; ++j) {

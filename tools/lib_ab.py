@@ -49,7 +49,7 @@ def main():
     a.finalize()
     ctx.sync()
     ctx.set_profiling(False)
-    ks = {k: round(ctx.kernel_stats(k)[1], 3) for k in ("agg_consume", "radix_scatter", "quant_mid", "quant_small", "group_heads", "group_combine", "chunk_reduce")}
+    ks = {k: round(ctx.kernel_stats(k)[1], 3) for k in ("agg_consume", "radix_hist_rank", "radix_hist", "radix_scatter", "quant_mid", "group_heads")}
     print(f"{label} {plan_name} rows {rows}: step median {statistics.median(ms):.3f} min {min(ms):.3f} ms, groups {g}, kernels {ks}",
           flush=True)
     a.close()
