@@ -73,12 +73,44 @@ struct HcExport {
 };
 
 // starts[p] = first sorted record of partition p (p in [0, P]); partition = key >> shift.
-__global__ void HcPartStartsKernel(const uint32_t* __restrict__ skeys, uint64_t n, int shift, uint32_t P, uint32_t* __restrict__ starts) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > n) return;
-  const int64_t prev = i == 0 ? -1 : static_cast<int64_t>(skeys[i - 1] >> shift);
-  const int64_t cur = i == n ? static_cast<int64_t>(P) : static_cast<int64_t>(skeys[i] >> shift);
+// Record i writes the starts of the partitions in (part(i - 1), part(i)] (part(-1) = -1,
+// part(n) = P).  A wave takes 256 consecutive records per step (one 16-byte load per lane, the
+// previous lane's last key by a shuffle) over a resident grid, as GroupHeadsKernel does.
+__device__ __forceinline__ void HcPartFill(int64_t prev, int64_t cur, uint64_t i, uint32_t* __restrict__ starts) {
   for (int64_t p = prev + 1; p <= cur; ++p) starts[p] = static_cast<uint32_t>(i);
+}
+__global__ void __launch_bounds__(256) HcPartStartsKernel(const uint32_t* __restrict__ skeys, uint64_t n, int shift, uint32_t P,
+                                                          uint32_t* __restrict__ starts) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
+  const bool vec = (reinterpret_cast<uintptr_t>(skeys) & 15) == 0;
+  for (uint64_t w0 = ((static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6) * 256; w0 < n; w0 += nwaves * 256) {
+    const uint64_t b = w0 + 4 * static_cast<uint64_t>(lane);
+    uint32_t k[4];
+    if (vec && b + 4 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(skeys + b);
+      k[0] = v.x;
+      k[1] = v.y;
+      k[2] = v.z;
+      k[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k[j] = b + j < n ? skeys[b + j] : 0u;
+    }
+    int64_t p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = static_cast<int64_t>(k[j] >> shift);
+    int64_t prev = static_cast<int64_t>(__shfl_up(static_cast<int>(p[3]), 1, 64));
+    if (lane == 0) prev = w0 == 0 ? -1 : static_cast<int64_t>(skeys[w0 - 1] >> shift);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (b + j >= n) break;
+      HcPartFill(prev, p[j], b + j, starts);
+      prev = p[j];
+    }
+  }
+  // record n: the partitions after the last record's (all of them when n == 0)
+  if (blockIdx.x == 0 && threadIdx.x == 0) HcPartFill(n == 0 ? -1 : static_cast<int64_t>(skeys[n - 1] >> shift), static_cast<int64_t>(P), n, starts);
 }
 
 __device__ __forceinline__ unsigned long long HcAccInit(int op) {
@@ -565,8 +597,11 @@ int32_t Agg::FinalizeHc(HcExport* ex) {
     PXG_RETURN_IF_ERROR(RadixSortBits(ctx, hc_key.as<const uint32_t>(), shift, pbits, streams, hp.stride, n, w.hc_k, w.hc_v, w.rs, &sk,
                                       &srec));
     PXG_RETURN_IF_ERROR(w.hc_starts.Ensure((static_cast<size_t>(P) + 1) * 4));
-    PXG_RETURN_IF_ERROR(Launch(ctx, "hc_part_starts", HcPartStartsKernel, dim3(GridFor(static_cast<int64_t>(n) + 1, 256, 1 << 30)), dim3(256), 0,
-                               sk, n, shift, P, w.hc_starts.as<uint32_t>()));
+    {
+      const int64_t waves = (static_cast<int64_t>(n) + 255) / 256;
+      const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, static_cast<int64_t>(ctx->num_cus) * 8)));
+      PXG_RETURN_IF_ERROR(Launch(ctx, "hc_part_starts", HcPartStartsKernel, dim3(grid), dim3(256), 0, sk, n, shift, P, w.hc_starts.as<uint32_t>()));
+    }
     PXG_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
     const uint32_t grid = std::min<uint32_t>(P, 1u << 16);
     PXG_RETURN_IF_ERROR(Launch(ctx, "hc_agg", HcAggFor(hp.kwords), dim3(grid), dim3(kHcBlock), lds, hp, srec, w.hc_starts.as<const uint32_t>(), P,

@@ -3,10 +3,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 L=gpurun_out/lib_ab.log
-for spec in "1000000000 5 c2" "100000000 20 c2"; do
+for spec in "100000000 20 c3" "100000000 5 c3_full"; do
   for i in 1 2 3; do
     PXG_LIB_PATH=$PWD/ab_alt/libpxg_base.so timeout -k 10 200 python3 tools/lib_ab.py base $spec >> $L 2>&1 || exit 1
     timeout -k 10 200 python3 tools/lib_ab.py new $spec >> $L 2>&1 || exit 1
   done
 done
-timeout -k 10 500 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_parity.py tests/test_n1_parity.py tests/test_fsplit.py tests/test_split.py tests/test_big_select.py tests/test_gpu_parity.py tests/test_n1_parity.py tests/test_fsplit.py tests/test_split.py tests/test_big_select.py tests/test_determinism.py tests/test_scale_parity.py -m gpu > gpurun_out/lib_ab_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_hc_agg.py tests/test_scale_parity.py tests/test_comm_gpu.py tests/test_partial.py -m gpu > gpurun_out/lib_ab_tests.log 2>&1

@@ -49,7 +49,7 @@ def main():
     a.finalize()
     ctx.sync()
     ctx.set_profiling(False)
-    ks = {k: round(ctx.kernel_stats(k)[1], 3) for k in ("agg_consume", "radix_hist_rank", "radix_hist", "radix_scatter", "quant_mid", "group_heads")}
+    ks = {k: round(ctx.kernel_stats(k)[1], 3) for k in ("agg_consume", "radix_scatter", "hc_agg", "hc_part_starts", "hc_key_copy")}
     print(f"{label} {plan_name} rows {rows}: step median {statistics.median(ms):.3f} min {min(ms):.3f} ms, groups {g}, kernels {ks}",
           flush=True)
     a.close()
