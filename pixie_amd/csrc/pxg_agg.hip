@@ -789,6 +789,10 @@ __global__ void __launch_bounds__(kConsumeBlock) AggConsumeFastKernel(const AggP
               lens |= static_cast<uint64_t>(k.len[q]) << (16 * q);
               if (KeyT<S>(plan, q) == PXG_STRING) atomicMax(&s_mlen[q], k.len[q]);
             }
+            // Bytes 16-19 of a first STRING key also ride in the lengths word's spare half
+            // (<= 2 keys): when no staged first key is longer than 20 bytes, the partition pass
+            // drops that key's third word stream (MakeHcPlan, tail0).
+            if (NK <= 2 && KeyT<S>(plan, 0) == PXG_STRING) lens |= (k.w[0][2] & 0xFFFFFFFFULL) << 32;
             r[0] = lens;
 #pragma unroll
             for (int q = 0; q < NK; ++q) {

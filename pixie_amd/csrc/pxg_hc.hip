@@ -51,6 +51,7 @@ struct HcAggPlan {
   int64_t uda_init[kMaxUdas];
   int32_t acc_op[kHcMaxAcc], acc_word[kHcMaxAcc];
   int32_t acc_hi[kHcMaxAcc];  // kHcAddWide: LDS array of the high words (nacc + j), else -1
+  int32_t tail0;  // key 0's third word rides in the lengths word's high half (its stream is dropped)
 };
 
 struct HcOut {
@@ -446,6 +447,7 @@ __global__ void HcKeyCopyKernel(const uint64_t* __restrict__ kscr, uint64_t kcap
     uint64_t kw[kHcStrWords];
 #pragma unroll
     for (int j = 0; j < kHcStrWords; ++j) kw[j] = j < kc.kw[k] ? kscr[static_cast<uint64_t>(hp.koff[k] + j) * kcap + l] : 0;
+    if (k == 0 && hp.tail0) kw[2] = lens >> 32;  // (kc.kw[0] == 2)
     const uint32_t o = off[l] + kc.dbase[k];
     if (kc.dbase[k]) off[l] = o;
     CopyBytesOverlap(kc.data[k] + o, reinterpret_cast<const uint8_t*>(kw), len);
@@ -487,6 +489,11 @@ static HcAggPlan MakeHcPlan(const Agg& a, bool compact = false, int32_t* src = n
     hp.ktype[k] = a.key_types[k];
     int kw = a.hc_layout.kw[k];
     if (compact && a.key_types[k] == PXG_STRING) kw = std::min<int>(kw, static_cast<int>((a.hc_maxlen_h[k] + 7) / 8));
+    // (consume writes bytes 16-19 of key 0 into the lengths word when there are <= 2 keys)
+    if (compact && k == 0 && a.key_types[0] == PXG_STRING && a.n_keys <= 2 && kw == 3 && a.hc_maxlen_h[0] <= 20) {
+      kw = 2;
+      hp.tail0 = 1;
+    }
     hp.koff[k] = w;
     if (kwc) kwc[k] = kw;
     for (int j = 0; j < kw; ++j)
@@ -834,7 +841,7 @@ __global__ void __launch_bounds__(256) HcGroupArenaKernel(HcAggPlan hp, const ui
       const uint32_t len = static_cast<uint32_t>((lens >> (16 * k)) & 0xFFFF);
       ar[wo] = len;
       const int nw = static_cast<int>((len + 7) >> 3);
-      for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = kw[j * n];
+      for (int j = 0; j < nw; ++j) ar[wo + 1 + j] = (k == 0 && hp.tail0 && j == 2) ? (lens >> 32) : kw[j * n];
       wo += 1 + nw;
     } else if (t == PXG_UINT128) {
       ar[wo] = kw[0];
